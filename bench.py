@@ -1,0 +1,123 @@
+#!/usr/bin/env python
+"""Headline benchmark: whole-node samples/sec of T5-base summarization fine-tuning (BASELINE.json).
+
+One process per GPU (torchrun sets RANK/LOCAL_RANK/WORLD_SIZE/MASTER_*; N=1 runs standalone), data
+parallel over RCCL with the bucketed reducer, bf16 weights/activations with fp32 master weights and
+moments, full training step inside the timed region: encoder+decoder forward, fused CE loss,
+backward, gradient all-reduce, global-norm clip and AdamW update.  Synthetic SAMSum-shaped data
+(input 1024 / target 128 tokens, the ref/train-accelerator.py:114-133 shapes) and random-init
+weights with HF's initialisation (no network).  Weak scaling: fixed per-GPU micro-batch.
+
+    python bench.py --gpus N --steps K --warmup W
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+# Reference stack (HF transformers T5 + torch fused AdamW, bf16 autocast, SDPA) measured on one MI355X
+# with tools/hf_comparator.py at the same shapes: profiles/hf_comparator_t5base_mi355x.jsonl.
+# BASELINE.md publishes no number, so vs_baseline compares against this comparator scaled linearly
+# with N (an upper bound for the reference's own scaling).
+HF_COMPARATOR_SAMPLES_PER_S_1GPU = {16: 107.4, 32: 132.0}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--model", default="t5-base")
+    ap.add_argument("--batch-per-gpu", type=int, default=int(os.environ.get("DLLM_BENCH_BATCH", "32")))
+    ap.add_argument("--src-len", type=int, default=1024)
+    ap.add_argument("--tgt-len", type=int, default=128)
+    ap.add_argument("--bucket-mb", type=float, default=None)
+    ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--dropout", type=float, default=None, help="override model dropout (default: config 0.1)")
+    ap.add_argument("--seed", type=int, default=0)
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    from distributed_llms_example_amd.models import build_model, resolve_config
+    from distributed_llms_example_amd.ops.rng import manual_seed
+    from distributed_llms_example_amd.parallel.env import init_distributed
+    from distributed_llms_example_amd.parallel.reducer import DEFAULT_BUCKET_MB
+    from distributed_llms_example_amd.train.engine import TrainEngine
+
+    env = init_distributed()
+    n = env.world_size
+    if a.gpus != n and env.is_main_process:
+        print(f"[bench] note: --gpus {a.gpus} but WORLD_SIZE={n}; using {n}", file=sys.stderr)
+    torch.manual_seed(a.seed)
+    manual_seed(a.seed * 1000 + env.rank)
+    cfg = resolve_config(a.model)
+    if a.dropout is not None:
+        cfg = cfg.replace(dropout_rate=a.dropout, attention_dropout=a.dropout)
+    model = build_model(cfg)
+    eng = TrainEngine(model, env, lr=5e-5, weight_decay=0.01, max_grad_norm=1.0, dtype=torch.bfloat16,
+                      bucket_mb=a.bucket_mb or DEFAULT_BUCKET_MB, overlap=not a.no_overlap)
+    eng.train()
+    B, S, T, V = a.batch_per_gpu, a.src_len, a.tgt_len, cfg.vocab_size
+    g = torch.Generator(device="cpu").manual_seed(1000 + env.rank)
+    batches = []
+    for _ in range(2):
+        batches.append({
+            "input_ids": torch.randint(2, V, (B, S), generator=g).to(env.device),
+            "attention_mask": torch.ones(B, S, dtype=torch.long).to(env.device),
+            "labels": torch.randint(2, V, (B, T), generator=g).to(env.device),
+        })
+
+    def step(i):
+        eng.forward_backward(batches[i % len(batches)])
+        eng.step()
+
+    for i in range(a.warmup):
+        step(i)
+    env.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        step(i)
+    env.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], device=env.device, dtype=torch.float64)
+    if n > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = t.item()
+    ms = dt / a.steps * 1e3
+    value = B * n * a.steps / dt
+    base = HF_COMPARATOR_SAMPLES_PER_S_1GPU.get(B)
+    if env.is_main_process:
+        print(json.dumps({
+            "metric": "samples/sec (whole node) T5-base summarization fine-tune",
+            "value": round(value, 2), "unit": "samples/s", "n_gpus": n, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": round(value / (base * n), 3) if base else None,
+            "baseline_note": "HF transformers+torch stack measured on 1x MI355X at the same shapes x N "
+                             "(BASELINE.md publishes no number)",
+            "dtype": "bf16", "data": "synthetic (random token ids, random-init weights)",
+            "config": {"model": a.model, "global_batch": B * n, "per_gpu_batch": B, "seq_len": S,
+                       "target_len": T, "parallelism": f"dp{n}",
+                       "bucket_mb": eng.reducer.bucket_sizes_mb()[1] if eng.reducer and len(eng.reducer.buckets) > 1 else None,
+                       "tokens_per_s": round(value * (S + T), 1)},
+        }), flush=True)
+    if n > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,35 @@
+// Parameter block for the attention kernels (csrc/attn.hip), filled by the host binding.
+#pragma once
+#include <stdint.h>
+
+struct AttnParams {
+  const uint16_t* q;
+  const uint16_t* k;
+  const uint16_t* v;
+  const uint16_t* o;   // fwd output / bwd input
+  const uint16_t* dout;
+  uint16_t* o_out;
+  float* lse;          // [B, H, Sq]
+  const float* delta;  // [B, H, Sq] (bwd)
+  float* dq_acc;       // [B, Sq, H, D] fp32 (bwd)
+  uint16_t* dk;        // [B, Sk, H, D]
+  uint16_t* dv;
+  float* dlut;         // [H, Sq + Sk - 1] fp32 (bwd)
+  const uint8_t* kpm;  // [B, Sk] 1 = attend
+  const float* lut;    // [H, Sq + Sk - 1]
+  long q_sb, q_ss, q_sh;
+  long k_sb, k_ss, k_sh;
+  long v_sb, v_ss, v_sh;
+  long o_sb, o_ss, o_sh;
+  long do_sb, do_ss, do_sh;
+  long dk_sb, dk_ss, dk_sh;
+  long dv_sb, dv_ss, dv_sh;
+  int B, H, Sq, Sk;
+  float scale;
+  int causal;
+  int causal_off;  // Sk - Sq
+  float p_drop;
+  uint32_t seed;
+  uint32_t thr;
+  int n_tiles;  // fwd: q tiles; bwd: key blocks
+};

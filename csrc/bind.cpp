@@ -1,0 +1,364 @@
+// Python bindings for the gfx950 kernel library (one in-tree extension: distributed_llms_example_amd/_C).
+// Host-side validation lives here: every shape / dtype / stride / alignment a kernel assumes is checked
+// BEFORE launch (a kernel that faults can reset every GPU on the node), then the C-ABI launchers in
+// csrc/*.hip run on the current torch HIP stream.
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include <c10/hip/HIPStream.h>
+
+#include "attn_params.h"
+
+extern "C" {
+int dllm_norm_fwd(const void*, const void*, const void*, const void*, void*, void*, float*, float*, int, int, float,
+                  float, uint32_t, int, int, hipStream_t);
+int dllm_norm_bwd_grid(int);
+int dllm_norm_bwd(const void*, const void*, const void*, const void*, const float*, const float*, void*, void*,
+                  float*, float*, float*, float*, int, int, float, uint32_t, int, int, hipStream_t);
+int dllm_act_fwd(const void*, void*, long, int, int, int, float, uint32_t, int, hipStream_t);
+int dllm_act_bwd(const void*, const void*, void*, long, int, int, int, float, uint32_t, int, hipStream_t);
+int dllm_dropout(const void*, void*, long, float, uint32_t, int, hipStream_t);
+int dllm_ce_fwd(const void*, const int64_t*, const float*, float*, float*, long, int, float, long, int, hipStream_t);
+int dllm_ce_bwd(const float*, const void*, const int64_t*, const float*, const float*, void*, long, int, float, long,
+                int, hipStream_t);
+int dllm_sq_norm(const void*, long, float*, float*, int, hipStream_t);
+int dllm_adamw(void*, float*, const void*, float*, float*, const uint8_t*, const float*, long, float, float, float,
+               float, float, float, float, int, hipStream_t);
+int dllm_attn_fwd(AttnParams*, hipStream_t);
+int dllm_attn_bwd(AttnParams*, hipStream_t);
+int dllm_attn_dq_convert(const float*, void*, int, int, int, long, long, long, float, hipStream_t);
+int dllm_attn_params_size();
+}
+
+namespace {
+
+using at::Tensor;
+using c10::optional;
+
+hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check_rc(int rc, const char* what) {
+  TORCH_CHECK(rc == 0, "dllm kernel launch failed (", what, "): rc=", rc,
+              rc > 0 ? std::string(" ") + hipGetErrorString((hipError_t)rc) : std::string(""));
+}
+
+void check_gpu(const Tensor& t, const char* n) {
+  TORCH_CHECK(t.is_cuda(), n, " must be a GPU tensor");
+}
+
+bool is_bf16(const Tensor& t) {
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16 || t.scalar_type() == at::kFloat, "unsupported dtype ",
+              t.scalar_type());
+  return t.scalar_type() == at::kBFloat16;
+}
+
+void check_aligned(const Tensor& t, int bytes, const char* n) {
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % bytes == 0, n, " must be ", bytes, "-byte aligned");
+}
+
+const void* opt_ptr(const optional<Tensor>& t) { return t.has_value() && t->defined() ? t->data_ptr() : nullptr; }
+
+// ------------------------------------------------------------------------------------------- norms
+std::vector<Tensor> norm_fwd(const Tensor& x, const optional<Tensor>& resid, const Tensor& w,
+                             const optional<Tensor>& b, double eps, double p, int64_t seed, int64_t kind,
+                             bool want_s) {
+  check_gpu(x, "x");
+  TORCH_CHECK(x.dim() == 2 && x.is_contiguous(), "x must be contiguous [N, d]");
+  const int N = x.size(0), d = x.size(1);
+  TORCH_CHECK(d % 4 == 0 && d <= 2048, "norm: d must be a multiple of 4 and <= 2048, got ", d);
+  TORCH_CHECK(w.numel() == d && w.is_contiguous() && w.scalar_type() == x.scalar_type(), "norm weight mismatch");
+  if (resid.has_value() && resid->defined())
+    TORCH_CHECK(resid->sizes() == x.sizes() && resid->is_contiguous() && resid->scalar_type() == x.scalar_type(),
+                "resid mismatch");
+  if (b.has_value() && b->defined())
+    TORCH_CHECK(b->numel() == d && b->is_contiguous() && b->scalar_type() == x.scalar_type(), "norm bias mismatch");
+  const bool need_s = want_s && ((resid.has_value() && resid->defined()) || p > 0.0);
+  auto out = at::empty_like(x);
+  Tensor s = need_s ? at::empty_like(x) : Tensor();
+  auto f32 = x.options().dtype(at::kFloat);
+  auto rstd = at::empty({N}, f32);
+  auto mean = kind == 1 ? at::empty({N}, f32) : Tensor();
+  if (N > 0)
+    check_rc(dllm_norm_fwd(x.data_ptr(), opt_ptr(resid), w.data_ptr(), opt_ptr(b), out.data_ptr(),
+                           need_s ? s.data_ptr() : nullptr, kind == 1 ? mean.data_ptr<float>() : nullptr,
+                           rstd.data_ptr<float>(), N, d, (float)eps, (float)p, (uint32_t)seed, (int)kind, is_bf16(x),
+                           stream()),
+             "norm_fwd");
+  return {out, s, mean, rstd};
+}
+
+std::vector<Tensor> norm_bwd(const optional<Tensor>& dout_o, const optional<Tensor>& ds, const Tensor& s,
+                             const Tensor& w, const optional<Tensor>& b, const optional<Tensor>& mean,
+                             const Tensor& rstd, double p, int64_t seed, int64_t kind, bool want_stream) {
+  check_gpu(s, "s");
+  TORCH_CHECK(s.dim() == 2 && s.is_contiguous(), "s must be contiguous [N, d]");
+  const int N = s.size(0), d = s.size(1);
+  Tensor dout = dout_o.has_value() && dout_o->defined() ? dout_o->contiguous() : at::zeros_like(s);
+  TORCH_CHECK(dout.sizes() == s.sizes() && dout.scalar_type() == s.scalar_type(), "dout mismatch");
+  Tensor dse;
+  if (ds.has_value() && ds->defined()) {
+    dse = ds->contiguous();
+    TORCH_CHECK(dse.sizes() == s.sizes() && dse.scalar_type() == s.scalar_type(), "ds mismatch");
+  }
+  TORCH_CHECK(rstd.numel() == N, "rstd mismatch");
+  if (kind == 1) TORCH_CHECK(mean.has_value() && mean->numel() == N, "mean required for LayerNorm");
+  auto dx = at::empty_like(s);
+  Tensor dstream = want_stream ? at::empty_like(s) : Tensor();
+  const int G = dllm_norm_bwd_grid(N > 0 ? N : 1);
+  auto f32 = s.options().dtype(at::kFloat);
+  auto dw_part = at::empty({G, d}, f32);
+  auto dw = at::zeros({d}, f32);
+  const bool has_b = b.has_value() && b->defined();
+  Tensor db_part = has_b ? at::empty({G, d}, f32) : Tensor();
+  Tensor db = has_b ? at::zeros({d}, f32) : Tensor();
+  if (N > 0)
+    check_rc(dllm_norm_bwd(dout.data_ptr(), dse.defined() ? dse.data_ptr() : nullptr, s.data_ptr(), w.data_ptr(),
+                           kind == 1 ? mean->data_ptr<float>() : nullptr, rstd.data_ptr<float>(), dx.data_ptr(),
+                           want_stream ? dstream.data_ptr() : nullptr, dw_part.data_ptr<float>(),
+                           has_b ? db_part.data_ptr<float>() : nullptr, dw.data_ptr<float>(),
+                           has_b ? db.data_ptr<float>() : nullptr, N, d, (float)p, (uint32_t)seed, (int)kind,
+                           is_bf16(s), stream()),
+             "norm_bwd");
+  return {dx, dstream, dw, db};
+}
+
+// ------------------------------------------------------------------------------------------- activations
+Tensor act_fwd(const Tensor& x, int64_t act, bool gated, double p, int64_t seed) {
+  check_gpu(x, "x");
+  TORCH_CHECK(x.dim() == 2 && x.is_contiguous(), "act: x must be contiguous [N, F]");
+  const long N = x.size(0);
+  const int F = gated ? x.size(1) / 2 : x.size(1);
+  TORCH_CHECK(F % 4 == 0 && (!gated || x.size(1) == 2 * F), "act: F must be a multiple of 4");
+  auto y = at::empty({N, F}, x.options());
+  if (N > 0) check_rc(dllm_act_fwd(x.data_ptr(), y.data_ptr(), N, F, (int)act, gated, (float)p, (uint32_t)seed,
+                                   is_bf16(x), stream()), "act_fwd");
+  return y;
+}
+
+Tensor act_bwd(const Tensor& dy_, const Tensor& x, int64_t act, bool gated, double p, int64_t seed) {
+  check_gpu(x, "x");
+  Tensor dy = dy_.contiguous();
+  const long N = x.size(0);
+  const int F = gated ? x.size(1) / 2 : x.size(1);
+  TORCH_CHECK(dy.dim() == 2 && dy.size(0) == N && dy.size(1) == F && dy.scalar_type() == x.scalar_type(),
+              "act_bwd: dy shape mismatch");
+  auto dx = at::empty_like(x);
+  if (N > 0) check_rc(dllm_act_bwd(dy.data_ptr(), x.data_ptr(), dx.data_ptr(), N, F, (int)act, gated, (float)p,
+                                   (uint32_t)seed, is_bf16(x), stream()), "act_bwd");
+  return dx;
+}
+
+Tensor dropout_fwd(const Tensor& x, double p, int64_t seed) {
+  check_gpu(x, "x");
+  TORCH_CHECK(x.is_contiguous() && x.numel() % 4 == 0, "dropout: contiguous, numel % 4 == 0");
+  auto y = at::empty_like(x);
+  if (x.numel() > 0)
+    check_rc(dllm_dropout(x.data_ptr(), y.data_ptr(), x.numel(), (float)p, (uint32_t)seed, is_bf16(x), stream()),
+             "dropout");
+  return y;
+}
+
+// ------------------------------------------------------------------------------------------- cross entropy
+std::vector<Tensor> ce_fwd(const Tensor& logits, const Tensor& labels, const optional<Tensor>& bias, double eps,
+                           int64_t ignore) {
+  check_gpu(logits, "logits");
+  TORCH_CHECK(logits.dim() == 2 && logits.is_contiguous(), "ce: logits must be contiguous [N, V]");
+  TORCH_CHECK(labels.scalar_type() == at::kLong && labels.numel() == logits.size(0) && labels.is_contiguous(),
+              "ce: labels must be int64 [N]");
+  const long N = logits.size(0);
+  const int V = logits.size(1);
+  Tensor bf;
+  if (bias.has_value() && bias->defined()) {
+    bf = bias->to(at::kFloat).contiguous();
+    TORCH_CHECK(bf.numel() == V, "ce: bias must have V entries");
+  }
+  auto f32 = logits.options().dtype(at::kFloat);
+  auto loss = at::empty({N}, f32), lse = at::empty({N}, f32);
+  if (N > 0)
+    check_rc(dllm_ce_fwd(logits.data_ptr(), labels.data_ptr<int64_t>(), bf.defined() ? bf.data_ptr<float>() : nullptr,
+                         loss.data_ptr<float>(), lse.data_ptr<float>(), N, V, (float)eps, ignore, is_bf16(logits),
+                         stream()),
+             "ce_fwd");
+  return {loss, lse};
+}
+
+Tensor ce_bwd(const Tensor& scale, Tensor logits, const Tensor& labels, const Tensor& lse,
+              const optional<Tensor>& bias, double eps, int64_t ignore, bool inplace) {
+  check_gpu(logits, "logits");
+  TORCH_CHECK(scale.scalar_type() == at::kFloat && scale.numel() >= 1 && scale.is_cuda(), "ce: scale");
+  const long N = logits.size(0);
+  const int V = logits.size(1);
+  Tensor bf;
+  if (bias.has_value() && bias->defined()) bf = bias->to(at::kFloat).contiguous();
+  Tensor out = inplace ? logits : at::empty_like(logits);
+  if (N > 0)
+    check_rc(dllm_ce_bwd(scale.data_ptr<float>(), logits.data_ptr(), labels.data_ptr<int64_t>(),
+                         lse.data_ptr<float>(), bf.defined() ? bf.data_ptr<float>() : nullptr, out.data_ptr(), N, V,
+                         (float)eps, ignore, is_bf16(logits), stream()),
+             "ce_bwd");
+  return out;
+}
+
+// ------------------------------------------------------------------------------------------- optimizer
+Tensor sq_norm(const Tensor& g) {
+  check_gpu(g, "g");
+  TORCH_CHECK(g.is_contiguous() && g.numel() % 4 == 0, "sq_norm: contiguous, numel % 4 == 0");
+  check_aligned(g, 16, "g");
+  auto f32 = g.options().dtype(at::kFloat);
+  auto part = at::empty({1024}, f32);
+  auto out = at::empty({}, f32);
+  check_rc(dllm_sq_norm(g.data_ptr(), g.numel(), part.data_ptr<float>(), out.data_ptr<float>(), is_bf16(g),
+                        stream()),
+           "sq_norm");
+  return out;
+}
+
+void adamw_step(Tensor param, const optional<Tensor>& master, const Tensor& grad, Tensor m, Tensor v,
+                const optional<Tensor>& wd_mask, const Tensor& coef, double lr, double b1, double b2, double eps,
+                double wd, double bc1, double bc2) {
+  check_gpu(param, "param");
+  const long n = param.numel();
+  TORCH_CHECK(n % 4 == 0 && param.is_contiguous() && grad.numel() == n && m.numel() == n && v.numel() == n,
+              "adamw: flat buffers must match, numel % 4 == 0");
+  TORCH_CHECK(grad.scalar_type() == param.scalar_type(), "adamw: grad dtype must equal param dtype");
+  TORCH_CHECK(m.scalar_type() == at::kFloat && v.scalar_type() == at::kFloat, "adamw: moments fp32");
+  if (master.has_value() && master->defined())
+    TORCH_CHECK(master->numel() == n && master->scalar_type() == at::kFloat, "adamw: master fp32 [n]");
+  if (wd_mask.has_value() && wd_mask->defined())
+    TORCH_CHECK(wd_mask->numel() == n && wd_mask->scalar_type() == at::kByte, "adamw: wd_mask u8 [n]");
+  TORCH_CHECK(coef.scalar_type() == at::kFloat && coef.is_cuda(), "adamw: coef fp32 device scalar");
+  for (auto* t : {&param, &m, &v}) check_aligned(*t, 16, "adamw buffer");
+  check_rc(dllm_adamw(param.data_ptr(),
+                      master.has_value() && master->defined() ? master->data_ptr<float>() : nullptr, grad.data_ptr(),
+                      m.data_ptr<float>(), v.data_ptr<float>(),
+                      wd_mask.has_value() && wd_mask->defined() ? wd_mask->data_ptr<uint8_t>() : nullptr,
+                      coef.data_ptr<float>(), n, (float)lr, (float)b1, (float)b2, (float)eps, (float)wd, (float)bc1,
+                      (float)bc2, is_bf16(param), stream()),
+           "adamw");
+}
+
+// ------------------------------------------------------------------------------------------- attention
+void check_bshd(const Tensor& t, const char* n, int64_t B, int64_t S, int64_t H) {
+  check_gpu(t, n);
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, n, ": attention kernels take bf16");
+  TORCH_CHECK(t.dim() == 4 && t.size(0) == B && t.size(1) == S && t.size(2) == H && t.size(3) == 64, n,
+              ": expected [B, S, H, 64], got ", t.sizes());
+  TORCH_CHECK(t.stride(3) == 1, n, ": head dim must be contiguous");
+  TORCH_CHECK(t.stride(0) % 8 == 0 && t.stride(1) % 8 == 0 && t.stride(2) % 8 == 0, n,
+              ": strides must be multiples of 8 elements (16-B vector loads)");
+  check_aligned(t, 16, n);
+}
+
+void fill_qkv(AttnParams& P, const Tensor& q, const Tensor& k, const Tensor& v, const optional<Tensor>& kpm,
+              const optional<Tensor>& lut, double scale, bool causal, double p, int64_t seed) {
+  const int64_t B = q.size(0), Sq = q.size(1), H = q.size(2), Sk = k.size(1);
+  check_bshd(q, "q", B, Sq, H);
+  check_bshd(k, "k", B, Sk, H);
+  check_bshd(v, "v", B, Sk, H);
+  TORCH_CHECK(Sq > 0 && Sk > 0, "empty attention");
+  TORCH_CHECK(Sk <= 16384 && Sq <= 16384, "attention: sequence length > 16384 unsupported");
+  TORCH_CHECK(B * H * Sq * Sk < (int64_t)1 << 40, "attention too large");
+  P.q = reinterpret_cast<const uint16_t*>(q.data_ptr());
+  P.k = reinterpret_cast<const uint16_t*>(k.data_ptr());
+  P.v = reinterpret_cast<const uint16_t*>(v.data_ptr());
+  P.q_sb = q.stride(0); P.q_ss = q.stride(1); P.q_sh = q.stride(2);
+  P.k_sb = k.stride(0); P.k_ss = k.stride(1); P.k_sh = k.stride(2);
+  P.v_sb = v.stride(0); P.v_ss = v.stride(1); P.v_sh = v.stride(2);
+  P.B = B; P.H = H; P.Sq = Sq; P.Sk = Sk;
+  P.scale = (float)scale;
+  P.causal = causal ? 1 : 0;
+  P.causal_off = Sk - Sq;
+  P.p_drop = (float)p;
+  P.seed = (uint32_t)seed;
+  P.kpm = nullptr;
+  P.lut = nullptr;
+  if (kpm.has_value() && kpm->defined()) {
+    TORCH_CHECK(kpm->scalar_type() == at::kByte && kpm->is_contiguous() && kpm->dim() == 2 && kpm->size(0) == B &&
+                    kpm->size(1) == Sk && kpm->is_cuda(),
+                "key_padding_mask must be uint8 [B, Sk] contiguous on GPU");
+    P.kpm = kpm->data_ptr<uint8_t>();
+  }
+  if (lut.has_value() && lut->defined()) {
+    TORCH_CHECK(lut->scalar_type() == at::kFloat && lut->is_contiguous() && lut->dim() == 2 && lut->size(0) == H &&
+                    lut->size(1) == Sq + Sk - 1 && lut->is_cuda(),
+                "bias_lut must be fp32 [H, Sq + Sk - 1] contiguous on GPU");
+    P.lut = lut->data_ptr<float>();
+  }
+}
+
+std::vector<Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, const optional<Tensor>& kpm,
+                             const optional<Tensor>& lut, double scale, bool causal, double p, int64_t seed) {
+  AttnParams P{};
+  fill_qkv(P, q, k, v, kpm, lut, scale, causal, p, seed);
+  auto o = at::empty({P.B, P.Sq, P.H, 64}, q.options());
+  auto lse = at::empty({P.B, P.H, P.Sq}, q.options().dtype(at::kFloat));
+  P.o_out = reinterpret_cast<uint16_t*>(o.data_ptr());
+  P.o_sb = o.stride(0); P.o_ss = o.stride(1); P.o_sh = o.stride(2);
+  P.lse = lse.data_ptr<float>();
+  check_rc(dllm_attn_fwd(&P, stream()), "attn_fwd");
+  return {o, lse};
+}
+
+std::vector<Tensor> attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o,
+                             const Tensor& lse, const optional<Tensor>& kpm, const optional<Tensor>& lut,
+                             double scale, bool causal, double p, int64_t seed, bool need_dlut,
+                             const optional<Tensor>& dq_out, const optional<Tensor>& dk_out,
+                             const optional<Tensor>& dv_out) {
+  AttnParams P{};
+  fill_qkv(P, q, k, v, kpm, lut, scale, causal, p, seed);
+  check_bshd(o, "o", P.B, P.Sq, P.H);
+  check_bshd(dout, "dout", P.B, P.Sq, P.H);
+  TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.numel() == (int64_t)P.B * P.H * P.Sq && lse.is_contiguous(),
+              "lse mismatch");
+  auto f32 = q.options().dtype(at::kFloat);
+  auto dq_acc = at::zeros({P.B, P.Sq, P.H, 64}, f32);
+  // outputs may be caller-provided strided views (e.g. slices of one packed d(qkv) buffer)
+  auto pick = [&](const optional<Tensor>& t, int64_t S, const char* n) {
+    if (t.has_value() && t->defined()) {
+      check_bshd(*t, n, P.B, S, P.H);
+      return *t;
+    }
+    return at::empty({P.B, S, P.H, 64}, q.options());
+  };
+  Tensor dq = pick(dq_out, P.Sq, "dq_out");
+  Tensor dk = pick(dk_out, P.Sk, "dk_out");
+  Tensor dv = pick(dv_out, P.Sk, "dv_out");
+  auto delta = at::empty({P.B, P.H, P.Sq}, f32);
+  Tensor dlut;
+  if (P.lut != nullptr) dlut = at::zeros({P.H, P.Sq + P.Sk - 1}, f32);
+  P.o = reinterpret_cast<const uint16_t*>(o.data_ptr());
+  P.o_sb = o.stride(0); P.o_ss = o.stride(1); P.o_sh = o.stride(2);
+  P.dout = reinterpret_cast<const uint16_t*>(dout.data_ptr());
+  P.do_sb = dout.stride(0); P.do_ss = dout.stride(1); P.do_sh = dout.stride(2);
+  P.lse = lse.data_ptr<float>();
+  P.delta = delta.data_ptr<float>();
+  P.dq_acc = dq_acc.data_ptr<float>();
+  P.dk = reinterpret_cast<uint16_t*>(dk.data_ptr());
+  P.dk_sb = dk.stride(0); P.dk_ss = dk.stride(1); P.dk_sh = dk.stride(2);
+  P.dv = reinterpret_cast<uint16_t*>(dv.data_ptr());
+  P.dv_sb = dv.stride(0); P.dv_ss = dv.stride(1); P.dv_sh = dv.stride(2);
+  P.dlut = dlut.defined() ? dlut.data_ptr<float>() : nullptr;
+  check_rc(dllm_attn_bwd(&P, stream()), "attn_bwd");
+  check_rc(dllm_attn_dq_convert(dq_acc.data_ptr<float>(), dq.data_ptr(), P.B, P.Sq, P.H, dq.stride(0), dq.stride(1),
+                                dq.stride(2), (float)scale, stream()),
+           "attn_dq_convert");
+  return {dq, dk, dv, need_dlut ? dlut : Tensor()};
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "gfx950 (MI355X) kernel library for distributed_llms_example_amd";
+  m.def("norm_fwd", &norm_fwd);
+  m.def("norm_bwd", &norm_bwd);
+  m.def("act_fwd", &act_fwd);
+  m.def("act_bwd", &act_bwd);
+  m.def("dropout_fwd", &dropout_fwd);
+  m.def("ce_fwd", &ce_fwd);
+  m.def("ce_bwd", &ce_bwd);
+  m.def("sq_norm", &sq_norm);
+  m.def("adamw_step", &adamw_step);
+  m.def("attn_fwd", &attn_fwd);
+  m.def("attn_bwd", &attn_bwd);
+  m.def("attn_params_size", []() { return dllm_attn_params_size(); });
+  m.attr("arch") = "gfx950";
+}

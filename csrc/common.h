@@ -1,0 +1,116 @@
+// Shared device helpers for the gfx950 (MI355X / CDNA4) kernel library.
+// Wave64 everywhere: lane = threadIdx.x & 63, reductions over 64 lanes.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define DLLM_HOST_DEVICE __host__ __device__ __forceinline__
+#define DLLM_DEVICE __device__ __forceinline__
+
+typedef uint16_t bf16_raw;
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(8))) short bf16x8;   // MFMA A/B fragment (8 x bf16)
+typedef __attribute__((ext_vector_type(4))) short bf16x4;
+typedef __attribute__((ext_vector_type(4))) uint16_t u16x4;
+typedef __attribute__((ext_vector_type(8))) uint16_t u16x8;
+
+namespace dllm {
+
+constexpr int kWave = 64;
+
+DLLM_DEVICE float bf2f(uint16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+
+// Round-to-nearest-even f32 -> bf16.  A plain cast to __bf16 lowers to v_cvt_pk_bf16_f32 on gfx950
+// (keeps NaN a NaN: MI355X_MICROARCH.md "Correctness boundaries").
+DLLM_DEVICE uint16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(uint16_t, b);
+}
+
+DLLM_DEVICE uint32_t pack_bf16x2(float lo, float hi) {
+  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+}
+
+// ---- generic element access for bf16 (uint16 storage) / fp32 --------------------------------
+template <typename T> struct Elem;
+template <> struct Elem<float> {
+  static DLLM_DEVICE float load(const float* p) { return *p; }
+  static DLLM_DEVICE void store(float* p, float v) { *p = v; }
+  static DLLM_DEVICE f32x4 load4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+  static DLLM_DEVICE void store4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
+  static DLLM_DEVICE float round(float v) { return v; }
+};
+template <> struct Elem<uint16_t> {
+  static DLLM_DEVICE float load(const uint16_t* p) { return bf2f(*p); }
+  static DLLM_DEVICE void store(uint16_t* p, float v) { *p = f2bf(v); }
+  static DLLM_DEVICE f32x4 load4(const uint16_t* p) {
+    u16x4 r = *reinterpret_cast<const u16x4*>(p);
+    return f32x4{bf2f(r.x), bf2f(r.y), bf2f(r.z), bf2f(r.w)};
+  }
+  static DLLM_DEVICE void store4(uint16_t* p, f32x4 v) {
+    u16x4 r = {f2bf(v.x), f2bf(v.y), f2bf(v.z), f2bf(v.w)};
+    *reinterpret_cast<u16x4*>(p) = r;
+  }
+  static DLLM_DEVICE float round(float v) { return bf2f(f2bf(v)); }
+};
+
+// ---- counter-based dropout hash (mirrors ops/rng.py mix32) ------------------------------------
+DLLM_HOST_DEVICE uint32_t mix32(uint32_t seed, uint32_t idx) {
+  uint32_t x = (idx * 0x9E3779B1u) ^ seed;
+  x ^= x >> 16;
+  x *= 0x85EBCA6Bu;
+  x ^= x >> 13;
+  x *= 0xC2B2AE35u;
+  x ^= x >> 16;
+  return x;
+}
+
+inline uint32_t drop_threshold(float p) {
+  double t = (double)p * 4294967296.0;
+  return t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
+}
+
+// ---- wave64 reductions -------------------------------------------------------------------------
+DLLM_DEVICE float wave_sum(float v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+  return v;
+}
+DLLM_DEVICE float wave_max(float v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v = fmaxf(v, __shfl_xor(v, m, 64));
+  return v;
+}
+
+// Block-wide sum for blockDim.x == NT (multiple of 64). `red` must hold NT/64 floats.
+template <int NT>
+DLLM_DEVICE float block_sum(float v, float* red) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  v = wave_sum(v);
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  float r = 0.f;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) r += red[i];
+  return r;
+}
+template <int NT>
+DLLM_DEVICE float block_max(float v, float* red) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  v = wave_max(v);
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  float r = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) r = fmaxf(r, red[i]);
+  return r;
+}
+
+}  // namespace dllm
+
+#define DLLM_CHECK_LAUNCH() \
+  do { hipError_t e__ = hipGetLastError(); if (e__ != hipSuccess) return (int)e__; } while (0)

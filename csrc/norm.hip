@@ -1,0 +1,247 @@
+// Fused (residual + dropout +) RMSNorm / LayerNorm, forward and backward, for gfx950.
+//
+// One wave64 owns one row; the row stays in registers (up to MAXV*256 columns, 4 elements / lane /
+// chunk, 8-byte bf16 vector loads) so the residual stream is read once and written once.
+// fwd:  s = (resid) + dropout(x)          [stored if resid or dropout]
+//       out = norm(s) * w (+ b)            [RMS: T5 (fp32 variance, weight only); LN: BART]
+// bwd:  ds = norm_bwd(dout) + ds_extra     [ds_extra = gradient of the stream from later layers]
+//       dx = dropout_bwd(ds);  dstream = ds (optional);  dw/db via per-block column partials.
+// The dropout keep-decision is mix32(seed, row*d + col) >= threshold (common.h / ops/rng.py).
+#include "common.h"
+
+using namespace dllm;
+
+namespace {
+
+template <typename T, int KIND, int MAXV>
+__global__ __launch_bounds__(256) void norm_fwd_kernel(const T* __restrict__ x, const T* __restrict__ resid,
+                                                       const T* __restrict__ w, const T* __restrict__ b,
+                                                       T* __restrict__ out, T* __restrict__ s_out,
+                                                       float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                       int N, int d, float eps, float p, uint32_t seed,
+                                                       uint32_t thr) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= N) return;
+  const size_t base = (size_t)row * d;
+  const bool drop = p > 0.f;
+  const float dscale = drop ? 1.f / (1.f - p) : 1.f;
+  f32x4 v[MAXV];
+  float sum = 0.f;
+#pragma unroll
+  for (int c = 0; c < MAXV; ++c) {
+    const int col = (c * 64 + lane) * 4;
+    v[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (col < d) {
+      f32x4 xv = Elem<T>::load4(x + base + col);
+      if (drop) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const bool keep = mix32(seed, (uint32_t)(base + col + k)) >= thr;
+          xv[k] = keep ? xv[k] * dscale : 0.f;
+        }
+      }
+      if (resid != nullptr) {
+        f32x4 rv = Elem<T>::load4(resid + base + col);
+        xv += rv;
+      }
+      if (s_out != nullptr) {
+        Elem<T>::store4(s_out + base + col, xv);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) xv[k] = Elem<T>::round(xv[k]);
+      }
+      v[c] = xv;
+      sum += xv.x + xv.y + xv.z + xv.w;
+    }
+  }
+  float mean = 0.f;
+  if (KIND == 1) mean = wave_sum(sum) / (float)d;
+  float sq = 0.f;
+#pragma unroll
+  for (int c = 0; c < MAXV; ++c) {
+    const int col = (c * 64 + lane) * 4;
+    if (col < d) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float t = v[c][k] - mean;
+        sq += t * t;
+      }
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(sq) / (float)d + eps);
+#pragma unroll
+  for (int c = 0; c < MAXV; ++c) {
+    const int col = (c * 64 + lane) * 4;
+    if (col < d) {
+      f32x4 wv = Elem<T>::load4(w + col);
+      f32x4 o = (v[c] - mean) * rstd * wv;
+      if (KIND == 1 && b != nullptr) o += Elem<T>::load4(b + col);
+      Elem<T>::store4(out + base + col, o);
+    }
+  }
+  if (lane == 0) {
+    rstd_out[row] = rstd;
+    if (KIND == 1) mean_out[row] = mean;
+  }
+}
+
+template <typename T, int KIND, int MAXV>
+__global__ __launch_bounds__(256) void norm_bwd_kernel(const T* __restrict__ dout, const T* __restrict__ ds_extra,
+                                                       const T* __restrict__ s, const T* __restrict__ w,
+                                                       const float* __restrict__ mean_in,
+                                                       const float* __restrict__ rstd_in, T* __restrict__ dx,
+                                                       T* __restrict__ dstream, float* __restrict__ dw_part,
+                                                       float* __restrict__ db_part, int N, int d, float p,
+                                                       uint32_t seed, uint32_t thr) {
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [4][d]
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const bool drop = p > 0.f;
+  const float dscale = drop ? 1.f / (1.f - p) : 1.f;
+  f32x4 adw[MAXV], adb[MAXV];
+#pragma unroll
+  for (int c = 0; c < MAXV; ++c) adw[c] = adb[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int row = blockIdx.x * 4 + wv; row < N; row += gridDim.x * 4) {
+    const size_t base = (size_t)row * d;
+    const float rstd = rstd_in[row];
+    const float mean = KIND == 1 ? mean_in[row] : 0.f;
+    f32x4 xh[MAXV], g[MAXV];
+    float s1 = 0.f, s2 = 0.f;  // sum(g), sum(g*xhat)
+#pragma unroll
+    for (int c = 0; c < MAXV; ++c) {
+      const int col = (c * 64 + lane) * 4;
+      xh[c] = g[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (col < d) {
+        xh[c] = (Elem<T>::load4(s + base + col) - mean) * rstd;
+        f32x4 dy = Elem<T>::load4(dout + base + col);
+        g[c] = dy * Elem<T>::load4(w + col);
+        adw[c] += dy * xh[c];
+        adb[c] += dy;
+        s1 += g[c].x + g[c].y + g[c].z + g[c].w;
+        f32x4 gx = g[c] * xh[c];
+        s2 += gx.x + gx.y + gx.z + gx.w;
+      }
+    }
+    s2 = wave_sum(s2) / (float)d;
+    if (KIND == 1) s1 = wave_sum(s1) / (float)d;
+    else s1 = 0.f;
+#pragma unroll
+    for (int c = 0; c < MAXV; ++c) {
+      const int col = (c * 64 + lane) * 4;
+      if (col < d) {
+        f32x4 dsv = (g[c] - s1 - xh[c] * s2) * rstd;
+        if (ds_extra != nullptr) dsv += Elem<T>::load4(ds_extra + base + col);
+        if (dstream != nullptr) Elem<T>::store4(dstream + base + col, dsv);
+        if (drop) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const bool keep = mix32(seed, (uint32_t)(base + col + k)) >= thr;
+            dsv[k] = keep ? dsv[k] * dscale : 0.f;
+          }
+        }
+        Elem<T>::store4(dx + base + col, dsv);
+      }
+    }
+  }
+  // block-reduce the column partials of the 4 waves, one pass for dw, one for db
+  for (int pass = 0; pass < (db_part != nullptr ? 2 : 1); ++pass) {
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < MAXV; ++c) {
+      const int col = (c * 64 + lane) * 4;
+      if (col < d) *reinterpret_cast<f32x4*>(red + wv * d + col) = pass == 0 ? adw[c] : adb[c];
+    }
+    __syncthreads();
+    float* dst = (pass == 0 ? dw_part : db_part) + (size_t)blockIdx.x * d;
+    for (int col = threadIdx.x; col < d; col += 256) dst[col] = red[col] + red[d + col] + red[2 * d + col] + red[3 * d + col];
+  }
+}
+
+__global__ __launch_bounds__(256) void col_sum_kernel(const float* __restrict__ part, float* __restrict__ out, int G,
+                                                      int d) {
+  const int col = blockIdx.x * 256 + threadIdx.x;
+  if (col >= d) return;
+  float acc = 0.f;
+  for (int g = 0; g < G; ++g) acc += part[(size_t)g * d + col];
+  out[col] = acc;
+}
+
+template <typename T, int KIND>
+int launch_fwd(const void* x, const void* resid, const void* w, const void* b, void* out, void* s_out, float* mean,
+               float* rstd, int N, int d, float eps, float p, uint32_t seed, hipStream_t st) {
+  const int chunks = (d + 255) / 256;
+  dim3 grid((N + 3) / 4), block(256);
+  const uint32_t thr = drop_threshold(p);
+#define L(MV)                                                                                                     \
+  hipLaunchKernelGGL((norm_fwd_kernel<T, KIND, MV>), grid, block, 0, st, (const T*)x, (const T*)resid,           \
+                     (const T*)w, (const T*)b, (T*)out, (T*)s_out, mean, rstd, N, d, eps, p, seed, thr)
+  if (chunks <= 1) L(1);
+  else if (chunks <= 2) L(2);
+  else if (chunks <= 4) L(4);
+  else if (chunks <= 8) L(8);
+  else return -1;
+#undef L
+  DLLM_CHECK_LAUNCH();
+  return 0;
+}
+
+template <typename T, int KIND>
+int launch_bwd(const void* dout, const void* ds_extra, const void* s, const void* w, const float* mean,
+               const float* rstd, void* dx, void* dstream, float* dw_part, float* db_part, float* dw, float* db,
+               int N, int d, float p, uint32_t seed, int G, hipStream_t st) {
+  const int chunks = (d + 255) / 256;
+  dim3 grid(G), block(256);
+  const size_t lds = (size_t)4 * d * sizeof(float);
+  const uint32_t thr = drop_threshold(p);
+#define L(MV)                                                                                                     \
+  hipLaunchKernelGGL((norm_bwd_kernel<T, KIND, MV>), grid, block, lds, st, (const T*)dout, (const T*)ds_extra,   \
+                     (const T*)s, (const T*)w, mean, rstd, (T*)dx, (T*)dstream, dw_part, db_part, N, d, p, seed,  \
+                     thr)
+  if (chunks <= 1) L(1);
+  else if (chunks <= 2) L(2);
+  else if (chunks <= 4) L(4);
+  else if (chunks <= 8) L(8);
+  else return -1;
+#undef L
+  DLLM_CHECK_LAUNCH();
+  hipLaunchKernelGGL(col_sum_kernel, dim3((d + 255) / 256), dim3(256), 0, st, dw_part, dw, G, d);
+  if (db_part != nullptr) hipLaunchKernelGGL(col_sum_kernel, dim3((d + 255) / 256), dim3(256), 0, st, db_part, db, G, d);
+  DLLM_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // namespace
+
+extern "C" int dllm_norm_fwd(const void* x, const void* resid, const void* w, const void* b, void* out, void* s_out,
+                             float* mean, float* rstd, int N, int d, float eps, float p, uint32_t seed, int kind,
+                             int is_bf16, hipStream_t st) {
+  if (d % 4 != 0) return -2;
+  if (is_bf16) {
+    return kind ? launch_fwd<uint16_t, 1>(x, resid, w, b, out, s_out, mean, rstd, N, d, eps, p, seed, st)
+                : launch_fwd<uint16_t, 0>(x, resid, w, b, out, s_out, mean, rstd, N, d, eps, p, seed, st);
+  }
+  return kind ? launch_fwd<float, 1>(x, resid, w, b, out, s_out, mean, rstd, N, d, eps, p, seed, st)
+              : launch_fwd<float, 0>(x, resid, w, b, out, s_out, mean, rstd, N, d, eps, p, seed, st);
+}
+
+// Number of partial rows the caller must allocate for dw_part/db_part.
+extern "C" int dllm_norm_bwd_grid(int N) {
+  int g = (N + 3) / 4;
+  return g < 512 ? g : 512;
+}
+
+extern "C" int dllm_norm_bwd(const void* dout, const void* ds_extra, const void* s, const void* w, const float* mean,
+                             const float* rstd, void* dx, void* dstream, float* dw_part, float* db_part, float* dw,
+                             float* db, int N, int d, float p, uint32_t seed, int kind, int is_bf16, hipStream_t st) {
+  if (d % 4 != 0) return -2;
+  const int G = dllm_norm_bwd_grid(N);
+  if (is_bf16) {
+    return kind ? launch_bwd<uint16_t, 1>(dout, ds_extra, s, w, mean, rstd, dx, dstream, dw_part, db_part, dw, db, N,
+                                          d, p, seed, G, st)
+                : launch_bwd<uint16_t, 0>(dout, ds_extra, s, w, mean, rstd, dx, dstream, dw_part, db_part, dw, db, N,
+                                          d, p, seed, G, st);
+  }
+  return kind ? launch_bwd<float, 1>(dout, ds_extra, s, w, mean, rstd, dx, dstream, dw_part, db_part, dw, db, N, d, p,
+                                     seed, G, st)
+              : launch_bwd<float, 0>(dout, ds_extra, s, w, mean, rstd, dx, dstream, dw_part, db_part, dw, db, N, d, p,
+                                     seed, G, st);
+}

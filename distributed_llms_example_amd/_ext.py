@@ -1,0 +1,52 @@
+"""Loader for the in-tree native extension ``_C`` (HIP kernels + C++ runtime, built for gfx950).
+
+Policy (round-end driver records which .so files the GPU tests load): on a GPU tensor every op
+dispatches to the HIP kernel library; if the extension is missing on a GPU box the op raises
+instead of silently falling back to eager PyTorch.  ``DLLM_REFERENCE_OPS=1`` forces the pure-torch
+reference implementations (used as numerics oracles in tests and on CPU).
+"""
+from __future__ import annotations
+
+import importlib
+import os
+
+import torch
+
+_C = None
+_err: Exception | None = None
+
+
+def _load():
+    global _C, _err
+    if _C is not None or _err is not None:
+        return _C
+    try:
+        _C = importlib.import_module("distributed_llms_example_amd._C")
+    except Exception as e:  # pragma: no cover - depends on build state
+        _err = e
+    return _C
+
+
+def native():
+    """The extension module, or None if it is not built."""
+    return _load()
+
+
+def load_error():
+    _load()
+    return _err
+
+
+def force_reference() -> bool:
+    return os.environ.get("DLLM_REFERENCE_OPS", "0") == "1"
+
+
+def use_native(t: torch.Tensor) -> bool:
+    """True when ``t`` lives on the GPU and the HIP path must run."""
+    if not t.is_cuda or force_reference():
+        return False
+    if _load() is None:
+        raise RuntimeError(
+            "distributed_llms_example_amd._C (HIP kernels for gfx950) is not built/loadable: "
+            f"{_err!r}. Build it with `python setup.py build_ext --inplace` (or __graft_entry__.build()).")
+    return True

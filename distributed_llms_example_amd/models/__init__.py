@@ -1,0 +1,8 @@
+"""Encoder-decoder model families (T5 / FLAN-T5 / BART) on the fused-op library."""
+from .bart import BartForConditionalGeneration
+from .config import PRESETS, Seq2SeqConfig, resolve_config
+from .hf_io import build_model, from_hf_state_dict, from_pretrained, save_pretrained, to_hf_state_dict
+from .t5 import T5ForConditionalGeneration
+
+__all__ = ["PRESETS", "Seq2SeqConfig", "resolve_config", "build_model", "from_pretrained", "save_pretrained",
+           "to_hf_state_dict", "from_hf_state_dict", "T5ForConditionalGeneration", "BartForConditionalGeneration"]

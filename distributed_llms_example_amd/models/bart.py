@@ -1,0 +1,221 @@
+"""BART (bart-large-cnn, the reference's default checkpoint: ref/valohai.yaml:10,36,65).
+
+Follows transformers' BartForConditionalGeneration (modeling_bart.py:835-958): learned positions
+with offset 2 (:74-98), ``layernorm_embedding`` + dropout after the embeddings (:507-549),
+post-LN encoder/decoder layers (:280-308, :343-390), exact-erf GELU, attention scale d**-0.5
+(:169), tied LM head + ``final_logits_bias`` (:939-940).  MI355X restructuring as in models/t5.py:
+fused QKV / cross-KV projections (one GEMM each), ``LN(residual + dropout(x))`` as one kernel,
+flash attention with key-padding / causal masks, fused CE with the logits bias inside the kernel.
+LayerDrop (encoder/decoder_layerdrop, 0.0 in every public BART config) is not implemented.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..ops import activations, attention as attn_ops, norms
+from ..ops.cross_entropy import cross_entropy
+from ..ops.rng import default_rng
+from .config import Seq2SeqConfig
+from .output import Seq2SeqLMOutput
+
+
+class BartAttention(nn.Module):
+    def __init__(self, cfg: Seq2SeqConfig, cross: bool):
+        super().__init__()
+        d = cfg.d_model
+        self.cross = cross
+        self.n_heads = cfg.num_heads
+        self.head_dim = d // cfg.num_heads
+        self.scaling = self.head_dim ** -0.5
+        if cross:
+            self.q_proj = nn.Linear(d, d)
+            self.kv_proj = nn.Linear(d, 2 * d)
+        else:
+            self.qkv_proj = nn.Linear(d, 3 * d)
+        self.out_proj = nn.Linear(d, d)
+
+    def project_kv(self, kv_in):
+        B, S, _ = kv_in.shape
+        return self.kv_proj(kv_in).view(B, S, 2, self.n_heads, self.head_dim)
+
+    def forward(self, x, kv_in=None, mask=None, causal=False, p=0.0, cache=None, kv=None):
+        B, S, _ = x.shape
+        H, D = self.n_heads, self.head_dim
+        seed = default_rng().next_seed() if p > 0 else 0
+        kw = dict(scale=self.scaling, causal=causal, key_padding_mask=mask, dropout_p=p, seed=seed)
+        if self.cross:
+            q = self.q_proj(x).view(B, S, H, D)
+            o = attn_ops.attention_q_kv(q, kv if kv is not None else self.project_kv(kv_in), **kw)
+        else:
+            qkv = self.qkv_proj(x).view(B, S, 3, H, D)
+            if cache is not None:
+                k, v = cache.append(qkv[:, :, 1], qkv[:, :, 2])
+                o = attn_ops.attention(qkv[:, :, 0], k, v, **kw)
+            else:
+                o = attn_ops.attention_qkv(qkv, **kw)
+        return self.out_proj(o.reshape(B, S, H * D))
+
+
+class BartLayer(nn.Module):
+    def __init__(self, cfg, is_decoder):
+        super().__init__()
+        d = cfg.d_model
+        self.is_decoder = is_decoder
+        self.self_attn = BartAttention(cfg, cross=False)
+        self.self_attn_layer_norm = nn.LayerNorm(d)
+        if is_decoder:
+            self.encoder_attn = BartAttention(cfg, cross=True)
+            self.encoder_attn_layer_norm = nn.LayerNorm(d)
+        self.fc1 = nn.Linear(d, cfg.d_ff)
+        self.fc2 = nn.Linear(cfg.d_ff, d)
+        self.final_layer_norm = nn.LayerNorm(d)
+        self.cfg = cfg
+
+    def forward(self, h, mask=None, enc_out=None, enc_mask=None, cache=None, cross_kv=None):
+        cfg = self.cfg
+        tr = self.training
+        p = cfg.dropout_rate if tr else 0.0
+        pa = cfg.attention_dropout if tr else 0.0
+        pact = cfg.activation_dropout if tr else 0.0
+        eps = cfg.layer_norm_epsilon
+        rng = default_rng()
+        a = self.self_attn(h, mask=None if self.is_decoder else mask, causal=self.is_decoder, p=pa, cache=cache)
+        h = norms.add_dropout_layer_norm(h, a, self.self_attn_layer_norm.weight, self.self_attn_layer_norm.bias, eps,
+                                         p, rng.next_seed() if p > 0 else 0)
+        if self.is_decoder:
+            c = self.encoder_attn(h, kv_in=enc_out, mask=enc_mask, p=pa, kv=cross_kv)
+            h = norms.add_dropout_layer_norm(h, c, self.encoder_attn_layer_norm.weight,
+                                             self.encoder_attn_layer_norm.bias, eps, p,
+                                             rng.next_seed() if p > 0 else 0)
+        f = activations.act_dropout(self.fc1(h), cfg.act, pact, rng.next_seed() if pact > 0 else 0)
+        f = self.fc2(f)
+        return norms.add_dropout_layer_norm(h, f, self.final_layer_norm.weight, self.final_layer_norm.bias, eps, p,
+                                            rng.next_seed() if p > 0 else 0)
+
+
+class BartLearnedPositionalEmbedding(nn.Embedding):
+    offset = 2
+
+    def __init__(self, n, d):
+        super().__init__(n + self.offset, d)
+
+
+class BartStack(nn.Module):
+    def __init__(self, cfg, is_decoder, embed_tokens):
+        super().__init__()
+        self.cfg = cfg
+        self.is_decoder = is_decoder
+        self._embed = [embed_tokens]
+        self.embed_positions = BartLearnedPositionalEmbedding(cfg.max_position_embeddings, cfg.d_model)
+        n = cfg.num_decoder_layers if is_decoder else cfg.num_layers
+        self.layers = nn.ModuleList([BartLayer(cfg, is_decoder) for _ in range(n)])
+        self.layernorm_embedding = nn.LayerNorm(cfg.d_model)
+        self.embed_scale = math.sqrt(cfg.d_model) if cfg.scale_embedding else 1.0
+
+    def forward(self, input_ids, attention_mask=None, enc_out=None, enc_mask=None, caches=None, q_offset=0,
+                cross_kv=None):
+        cfg = self.cfg
+        p = cfg.dropout_rate if self.training else 0.0
+        B, S = input_ids.shape
+        x = F.embedding(input_ids, self._embed[0].weight, padding_idx=cfg.pad_token_id)
+        if self.embed_scale != 1.0:
+            x = x * self.embed_scale
+        pos = torch.arange(q_offset, q_offset + S, device=input_ids.device) + BartLearnedPositionalEmbedding.offset
+        x = x + F.embedding(pos, self.embed_positions.weight).unsqueeze(0)
+        h = norms.layer_norm(x, self.layernorm_embedding.weight, self.layernorm_embedding.bias, cfg.layer_norm_epsilon)
+        h = activations.dropout(h, p, default_rng().next_seed() if p > 0 else 0)
+        for i, layer in enumerate(self.layers):
+            h = layer(h, mask=attention_mask, enc_out=enc_out, enc_mask=enc_mask,
+                      cache=caches[i] if caches is not None else None,
+                      cross_kv=cross_kv[i] if cross_kv is not None else None)
+        return h
+
+
+class BartModel(nn.Module):
+    def __init__(self, cfg):
+        super().__init__()
+        self.shared = nn.Embedding(cfg.vocab_size, cfg.d_model, padding_idx=cfg.pad_token_id)
+        self.encoder = BartStack(cfg, False, self.shared)
+        self.decoder = BartStack(cfg, True, self.shared)
+
+
+class BartForConditionalGeneration(nn.Module):
+    model_type = "bart"
+
+    def __init__(self, cfg: Seq2SeqConfig):
+        super().__init__()
+        self.config = cfg
+        self.model = BartModel(cfg)
+        self.register_buffer("final_logits_bias", torch.zeros(1, cfg.vocab_size))
+        self.reset_parameters()
+
+    @torch.no_grad()
+    def reset_parameters(self):
+        """PreTrainedModel._init_weights with init_std (Linear/Embedding ~ N(0, std), bias 0,
+        padding row 0, LayerNorm 1/0) + final_logits_bias = 0 (modeling_bart.py:431-434)."""
+        std = self.config.init_std
+        for m in self.modules():
+            if isinstance(m, nn.Linear):
+                m.weight.normal_(0.0, std)
+                if m.bias is not None:
+                    m.bias.zero_()
+            elif isinstance(m, nn.Embedding):
+                m.weight.normal_(0.0, std)
+                if m.padding_idx is not None:
+                    m.weight[m.padding_idx].zero_()
+            elif isinstance(m, nn.LayerNorm):
+                m.weight.fill_(1.0)
+                m.bias.zero_()
+        self.final_logits_bias.zero_()
+
+    def shift_right(self, labels):
+        """shift_tokens_right (modeling_bart.py:58-71)"""
+        out = labels.new_zeros(labels.shape)
+        out[:, 1:] = labels[:, :-1]
+        out[:, 0] = self.config.decoder_start_token_id
+        out.masked_fill_(out == -100, self.config.pad_token_id)
+        return out
+
+    prepare_decoder_input_ids_from_labels = shift_right
+
+    def encode(self, input_ids, attention_mask=None):
+        return self.model.encoder(input_ids, attention_mask=attention_mask)
+
+    def decode(self, decoder_input_ids, enc_out, enc_mask=None, caches=None, q_offset=0, cross_kv=None):
+        return self.model.decoder(decoder_input_ids, enc_out=enc_out, enc_mask=enc_mask, caches=caches,
+                                  q_offset=q_offset, cross_kv=cross_kv)
+
+    def output_embedding(self):
+        return self.model.shared.weight
+
+    def logits_bias(self):
+        return self.final_logits_bias.view(-1)
+
+    def lm_logits(self, hidden):
+        return F.linear(hidden, self.output_embedding()) + self.final_logits_bias.to(hidden.dtype)
+
+    def cross_attention_modules(self):
+        return [layer.encoder_attn for layer in self.model.decoder.layers]
+
+    def forward(self, input_ids=None, attention_mask=None, decoder_input_ids=None, labels=None,
+                label_smoothing: float = 0.0, return_logits: bool = False, encoder_outputs=None):
+        enc = encoder_outputs if encoder_outputs is not None else self.encode(input_ids, attention_mask)
+        if decoder_input_ids is None:
+            decoder_input_ids = self.shift_right(labels)
+        dec = self.decode(decoder_input_ids, enc, attention_mask)
+        loss = None
+        if labels is not None and not return_logits:
+            raw = F.linear(dec, self.output_embedding())
+            V = raw.shape[-1]
+            loss = cross_entropy(raw.view(-1, V), labels.reshape(-1), bias=self.logits_bias(),
+                                 label_smoothing=label_smoothing, inplace_grad=True)
+            return Seq2SeqLMOutput(loss=loss, logits=None, encoder_last_hidden_state=enc)
+        logits = self.lm_logits(dec)
+        if labels is not None:
+            V = logits.shape[-1]
+            loss = cross_entropy(logits.view(-1, V), labels.reshape(-1), label_smoothing=label_smoothing)
+        return Seq2SeqLMOutput(loss=loss, logits=logits, encoder_last_hidden_state=enc)

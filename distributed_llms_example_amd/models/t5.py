@@ -1,0 +1,263 @@
+"""T5 / FLAN-T5 encoder-decoder, written for the fused-op library.
+
+Behaviour follows transformers' T5ForConditionalGeneration (modeling_t5.py:939-1066, the model the
+reference fine-tunes through ``AutoModelForSeq2SeqLM``), restructured for MI355X:
+
+* module paths mirror HF (``encoder.block.{i}.layer.{j}.SelfAttention``...) so checkpoints map 1:1,
+  but q/k/v (and cross-attention k/v, and gated wi_0/wi_1) are ONE weight each → one GEMM, viewed
+  as ``[B, S, 3, H, D]`` by the attention kernel without transposes (models/hf_io.py splits them);
+* every residual update ``h + dropout(sublayer)`` is fused with the NEXT sub-layer's RMSNorm
+  (ops/norms.py), so the residual stream is read/written once per sub-layer;
+* the relative-position bias is a per-head LUT (ops/attention.py) — layer 0 owns the bucket table
+  and every layer reuses it (modeling_t5.py:739-740), as in HF;
+* LM head + cross-entropy: logits in bf16, CE fused (ops/cross_entropy.py), the
+  ``d_model**-0.5`` tied-embedding scale (modeling_t5.py:1044-1045) applied to the decoder output.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..ops import activations, attention as attn_ops, norms
+from ..ops.cross_entropy import cross_entropy
+from ..ops.rng import default_rng
+from .config import Seq2SeqConfig
+from .output import Seq2SeqLMOutput
+
+
+class T5LayerNorm(nn.Module):
+    def __init__(self, d, eps):
+        super().__init__()
+        self.weight = nn.Parameter(torch.ones(d))
+        self.variance_epsilon = eps
+
+
+class T5Attention(nn.Module):
+    def __init__(self, cfg: Seq2SeqConfig, cross: bool, has_relative_attention_bias: bool, is_decoder: bool):
+        super().__init__()
+        self.cfg = cfg
+        self.cross = cross
+        self.is_decoder = is_decoder
+        self.n_heads = cfg.num_heads
+        self.d_kv = cfg.d_kv
+        inner = cfg.inner_dim
+        if cross:
+            self.q = nn.Linear(cfg.d_model, inner, bias=False)
+            self.kv = nn.Linear(cfg.d_model, 2 * inner, bias=False)
+        else:
+            self.qkv = nn.Linear(cfg.d_model, 3 * inner, bias=False)
+        self.o = nn.Linear(inner, cfg.d_model, bias=False)
+        self.has_relative_attention_bias = has_relative_attention_bias
+        if has_relative_attention_bias:
+            self.relative_attention_bias = nn.Embedding(cfg.relative_attention_num_buckets, cfg.num_heads)
+
+    def bias_lut(self, q_len, k_len, q_offset=0):
+        return attn_ops.relative_bias_lut(self.relative_attention_bias.weight, q_len, k_len,
+                                          bidirectional=not self.is_decoder,
+                                          num_buckets=self.cfg.relative_attention_num_buckets,
+                                          max_distance=self.cfg.relative_attention_max_distance, q_offset=q_offset)
+
+    def project_kv(self, kv_in):
+        B, S, _ = kv_in.shape
+        return self.kv(kv_in).view(B, S, 2, self.n_heads, self.d_kv)
+
+    def forward(self, x, kv_in=None, mask=None, lut=None, causal=False, p=0.0, cache=None, kv=None):
+        B, S, _ = x.shape
+        H, D = self.n_heads, self.d_kv
+        seed = default_rng().next_seed() if p > 0 else 0
+        kw = dict(scale=1.0, causal=causal, key_padding_mask=mask, bias_lut=lut, dropout_p=p, seed=seed)
+        if self.cross:
+            q = self.q(x).view(B, S, H, D)
+            o = attn_ops.attention_q_kv(q, kv if kv is not None else self.project_kv(kv_in), **kw)
+        else:
+            qkv = self.qkv(x).view(B, S, 3, H, D)
+            if cache is not None:
+                k, v = cache.append(qkv[:, :, 1], qkv[:, :, 2])
+                o = attn_ops.attention(qkv[:, :, 0], k, v, **kw)
+            else:
+                o = attn_ops.attention_qkv(qkv, **kw)
+        return self.o(o.reshape(B, S, H * D))
+
+
+class T5DenseActDense(nn.Module):
+    def __init__(self, cfg):
+        super().__init__()
+        self.wi = nn.Linear(cfg.d_model, cfg.d_ff * (2 if cfg.is_gated else 1), bias=False)
+        self.wo = nn.Linear(cfg.d_ff, cfg.d_model, bias=False)
+        self.act = cfg.act
+        self.gated = cfg.is_gated
+
+    def forward(self, x, p):
+        h = self.wi(x)
+        seed = default_rng().next_seed() if p > 0 else 0
+        h = activations.act_dropout(h, self.act, p, seed, gated=self.gated)
+        return self.wo(h)
+
+
+class T5LayerSelfAttention(nn.Module):
+    def __init__(self, cfg, has_bias, is_decoder):
+        super().__init__()
+        self.SelfAttention = T5Attention(cfg, cross=False, has_relative_attention_bias=has_bias, is_decoder=is_decoder)
+        self.layer_norm = T5LayerNorm(cfg.d_model, cfg.layer_norm_epsilon)
+
+
+class T5LayerCrossAttention(nn.Module):
+    def __init__(self, cfg):
+        super().__init__()
+        self.EncDecAttention = T5Attention(cfg, cross=True, has_relative_attention_bias=False, is_decoder=True)
+        self.layer_norm = T5LayerNorm(cfg.d_model, cfg.layer_norm_epsilon)
+
+
+class T5LayerFF(nn.Module):
+    def __init__(self, cfg):
+        super().__init__()
+        self.DenseReluDense = T5DenseActDense(cfg)
+        self.layer_norm = T5LayerNorm(cfg.d_model, cfg.layer_norm_epsilon)
+
+
+class T5Block(nn.Module):
+    def __init__(self, cfg, has_bias, is_decoder):
+        super().__init__()
+        self.layer = nn.ModuleList([T5LayerSelfAttention(cfg, has_bias, is_decoder)])
+        if is_decoder:
+            self.layer.append(T5LayerCrossAttention(cfg))
+        self.layer.append(T5LayerFF(cfg))
+
+    def norms(self):
+        return [lyr.layer_norm for lyr in self.layer]
+
+
+class T5Stack(nn.Module):
+    def __init__(self, cfg: Seq2SeqConfig, is_decoder: bool, embed_tokens: nn.Embedding):
+        super().__init__()
+        self.cfg = cfg
+        self.is_decoder = is_decoder
+        self._embed = [embed_tokens]  # shared; not registered twice
+        n = cfg.num_decoder_layers if is_decoder else cfg.num_layers
+        self.block = nn.ModuleList([T5Block(cfg, has_bias=(i == 0), is_decoder=is_decoder) for i in range(n)])
+        self.final_layer_norm = T5LayerNorm(cfg.d_model, cfg.layer_norm_epsilon)
+
+    def forward(self, input_ids, attention_mask=None, enc_out=None, enc_mask=None, caches=None, q_offset=0,
+                cross_kv=None):
+        cfg = self.cfg
+        p = cfg.dropout_rate if self.training else 0.0
+        pa = cfg.attention_dropout if self.training else 0.0
+        eps = cfg.layer_norm_epsilon
+        rng = default_rng()
+        x = F.embedding(input_ids, self._embed[0].weight)
+        B, S = input_ids.shape
+        k_len = S + q_offset
+        lut = self.block[0].layer[0].SelfAttention.bias_lut(S, k_len, q_offset=q_offset)
+        blocks = list(self.block)
+        # h = dropout(embeddings); normed = block0 self-attn norm(h)
+        normed, h = norms.dropout_rms_norm(x, blocks[0].layer[0].layer_norm.weight, eps, p,
+                                           rng.next_seed() if p > 0 else 0)
+        for i, blk in enumerate(blocks):
+            subs = list(blk.layer)
+            next_norms = [lyr.layer_norm.weight for lyr in subs[1:]]
+            next_norms.append(blocks[i + 1].layer[0].layer_norm.weight if i + 1 < len(blocks)
+                              else self.final_layer_norm.weight)
+            cache = caches[i] if caches is not None else None
+            a = subs[0].SelfAttention(normed, mask=attention_mask if not self.is_decoder else None, lut=lut,
+                                      causal=self.is_decoder, p=pa, cache=cache)
+            normed, h = norms.add_dropout_rms_norm(h, a, next_norms[0], eps, p, rng.next_seed() if p > 0 else 0)
+            j = 1
+            if self.is_decoder:
+                ckv = cross_kv[i] if cross_kv is not None else None
+                c = subs[1].EncDecAttention(normed, kv_in=enc_out, mask=enc_mask, lut=None, causal=False, p=pa, kv=ckv)
+                normed, h = norms.add_dropout_rms_norm(h, c, next_norms[1], eps, p, rng.next_seed() if p > 0 else 0)
+                j = 2
+            f = subs[j].DenseReluDense(normed, p)
+            normed, h = norms.add_dropout_rms_norm(h, f, next_norms[j], eps, p, rng.next_seed() if p > 0 else 0)
+        # `normed` is now final_layer_norm(h); HF applies dropout after it (modeling_t5.py:744-745)
+        return activations.dropout(normed, p, rng.next_seed() if p > 0 else 0)
+
+
+class T5ForConditionalGeneration(nn.Module):
+    model_type = "t5"
+
+    def __init__(self, cfg: Seq2SeqConfig):
+        super().__init__()
+        self.config = cfg
+        self.shared = nn.Embedding(cfg.vocab_size, cfg.d_model)
+        self.encoder = T5Stack(cfg, False, self.shared)
+        self.decoder = T5Stack(cfg, True, self.shared)
+        if not cfg.tie_word_embeddings:
+            self.lm_head = nn.Linear(cfg.d_model, cfg.vocab_size, bias=False)
+        self.reset_parameters()
+
+    # ---------------------------------------------------------------------------------- init
+    @torch.no_grad()
+    def reset_parameters(self):
+        """HF T5PreTrainedModel._init_weights (modeling_t5.py:563-616)."""
+        cfg = self.config
+        fac = cfg.initializer_factor
+        d, dkv, H, dff = cfg.d_model, cfg.d_kv, cfg.num_heads, cfg.d_ff
+        self.shared.weight.normal_(0.0, fac * 1.0)
+        if not cfg.tie_word_embeddings:
+            self.lm_head.weight.normal_(0.0, fac * 1.0)
+        for m in self.modules():
+            if isinstance(m, T5LayerNorm):
+                m.weight.fill_(fac)
+            elif isinstance(m, T5DenseActDense):
+                m.wi.weight.normal_(0.0, fac * d ** -0.5)
+                m.wo.weight.normal_(0.0, fac * dff ** -0.5)
+            elif isinstance(m, T5Attention):
+                inner = H * dkv
+                if m.cross:
+                    m.q.weight.normal_(0.0, fac * (d * dkv) ** -0.5)
+                    m.kv.weight.normal_(0.0, fac * d ** -0.5)
+                else:
+                    m.qkv.weight[:inner].normal_(0.0, fac * (d * dkv) ** -0.5)
+                    m.qkv.weight[inner:].normal_(0.0, fac * d ** -0.5)
+                m.o.weight.normal_(0.0, fac * (H * dkv) ** -0.5)
+                if m.has_relative_attention_bias:
+                    m.relative_attention_bias.weight.normal_(0.0, fac * d ** -0.5)
+
+    # ---------------------------------------------------------------------------------- API
+    def shift_right(self, labels):
+        """modeling_t5.py:618-637"""
+        out = labels.new_zeros(labels.shape)
+        out[..., 1:] = labels[..., :-1]
+        out[..., 0] = self.config.decoder_start_token_id
+        out.masked_fill_(out == -100, self.config.pad_token_id)
+        return out
+
+    prepare_decoder_input_ids_from_labels = shift_right
+
+    def encode(self, input_ids, attention_mask=None):
+        return self.encoder(input_ids, attention_mask=attention_mask)
+
+    def decode(self, decoder_input_ids, enc_out, enc_mask=None, caches=None, q_offset=0, cross_kv=None):
+        return self.decoder(decoder_input_ids, enc_out=enc_out, enc_mask=enc_mask, caches=caches, q_offset=q_offset,
+                            cross_kv=cross_kv)
+
+    def output_embedding(self):
+        return self.shared.weight if self.config.tie_word_embeddings else self.lm_head.weight
+
+    def lm_logits(self, hidden):
+        if self.config.scale_decoder_outputs:
+            hidden = hidden * (self.config.d_model ** -0.5)
+        return F.linear(hidden, self.output_embedding())
+
+    def logits_bias(self):
+        return None
+
+    def cross_attention_modules(self):
+        return [blk.layer[1].EncDecAttention for blk in self.decoder.block]
+
+    def forward(self, input_ids=None, attention_mask=None, decoder_input_ids=None, labels=None,
+                label_smoothing: float = 0.0, return_logits: bool = False, encoder_outputs=None):
+        enc = encoder_outputs if encoder_outputs is not None else self.encode(input_ids, attention_mask)
+        if decoder_input_ids is None:
+            decoder_input_ids = self.shift_right(labels)
+        dec = self.decode(decoder_input_ids, enc, attention_mask)
+        logits = self.lm_logits(dec)
+        loss = None
+        if labels is not None:
+            V = logits.shape[-1]
+            loss = cross_entropy(logits.view(-1, V), labels.reshape(-1), label_smoothing=label_smoothing,
+                                 inplace_grad=not return_logits)
+        return Seq2SeqLMOutput(loss=loss, logits=logits if (return_logits or labels is None) else None,
+                               encoder_last_hidden_state=enc)

@@ -1,0 +1,177 @@
+"""Fused multi-head attention for encoder-decoder models (flash-style, HIP/MFMA on gfx950).
+
+One op covers every attention variant the reference's models run (SURVEY.md §2.3 "SDPA attention"):
+
+* T5 self-attention: no 1/sqrt(d) scale (transformers modeling_t5.py:196-197) and an additive
+  relative-position bias built from a (num_buckets, H) table (modeling_t5.py:217-279).  HF
+  materialises the bias as a float ``[1, H, Sq, Sk]`` mask, which also knocks SDPA off its flash path
+  (integrations/sdpa_attention.py:39-76).  Here the bias is a per-head LUT indexed by the relative
+  distance ``j - i`` (``[H, Sq + Sk - 1]``, O(S) memory) that the kernel reads from LDS; its
+  backward returns the gradient of that LUT (diagonal sums of dS), which autograd scatters back
+  into the bucket table.
+* T5 / BART decoder: causal (+ bias); cross-attention: key-padding mask only.
+* BART: scale ``d**-0.5`` (modeling_bart.py:169), key-padding mask.
+* Attention-probability dropout (T5 applies ``dropout_rate`` to the probabilities,
+  modeling_t5.py:360) with the counter-based mask of ops/rng.py, regenerated in backward.
+
+Layout: q ``[B, Sq, H, D]``, k/v ``[B, Sk, H, D]`` — the natural output of the fused QKV GEMM
+viewed without any transpose copy (only the last dim must be contiguous).  Output ``[B, Sq, H, D]``.
+
+Kernels: csrc/attn_fwd.hip, csrc/attn_bwd.hip.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from .. import _ext
+from .rng import mix32, threshold
+
+# --------------------------------------------------------------------------- T5 relative bias
+
+
+def relative_position_bucket(relative_position: torch.Tensor, bidirectional: bool = True, num_buckets: int = 32,
+                             max_distance: int = 128) -> torch.Tensor:
+    """Bit-exact re-statement of T5Attention._relative_position_bucket (modeling_t5.py:217-262)."""
+    relative_buckets = 0
+    if bidirectional:
+        num_buckets //= 2
+        relative_buckets += (relative_position > 0).to(torch.long) * num_buckets
+        relative_position = torch.abs(relative_position)
+    else:
+        relative_position = -torch.min(relative_position, torch.zeros_like(relative_position))
+    max_exact = num_buckets // 2
+    is_small = relative_position < max_exact
+    rp_large = max_exact + (torch.log(relative_position.float() / max_exact) / math.log(max_distance / max_exact)
+                            * (num_buckets - max_exact)).to(torch.long)
+    rp_large = torch.min(rp_large, torch.full_like(rp_large, num_buckets - 1))
+    relative_buckets += torch.where(is_small, relative_position, rp_large)
+    return relative_buckets
+
+
+_bucket_cache: dict = {}
+
+
+def relative_bias_lut(table: torch.Tensor, q_len: int, k_len: int, bidirectional: bool, num_buckets: int,
+                      max_distance: int, q_offset: int = 0) -> torch.Tensor:
+    """Per-head bias indexed by relative distance: ``lut[h, (j - i) + (q_len - 1)]`` for local query
+    row ``i`` (absolute position ``i + q_offset``) and key ``j``.  Differentiable w.r.t. ``table``
+    (shape ``[num_buckets, H]``).  Returns fp32 ``[H, q_len + k_len - 1]``."""
+    key = (q_len, k_len, bidirectional, num_buckets, max_distance, q_offset, table.device)
+    idx = _bucket_cache.get(key)
+    if idx is None:
+        rel = torch.arange(-(q_len - 1), k_len, device=table.device, dtype=torch.long) - q_offset
+        idx = relative_position_bucket(rel, bidirectional, num_buckets, max_distance)
+        if len(_bucket_cache) > 256:
+            _bucket_cache.clear()
+        _bucket_cache[key] = idx
+    return table.float().index_select(0, idx).t().contiguous()
+
+
+# --------------------------------------------------------------------------- reference
+
+
+def _reference(q, k, v, scale, causal, kpm, lut, p, seed):
+    B, Sq, H, D = q.shape
+    Sk = k.shape[1]
+    qf = q.float().permute(0, 2, 1, 3)
+    kf = k.float().permute(0, 2, 1, 3)
+    vf = v.float().permute(0, 2, 1, 3)
+    s = torch.matmul(qf, kf.transpose(-1, -2)) * scale
+    if lut is not None:
+        rel = torch.arange(Sk, device=q.device)[None, :] - torch.arange(Sq, device=q.device)[:, None] + (Sq - 1)
+        s = s + lut.float()[:, rel].unsqueeze(0)
+    neg = torch.finfo(torch.float32).min
+    if kpm is not None:
+        s = s.masked_fill(~kpm.bool()[:, None, None, :], neg)
+    if causal:
+        off = Sk - Sq
+        cm = torch.arange(Sk, device=q.device)[None, :] > (torch.arange(Sq, device=q.device)[:, None] + off)
+        s = s.masked_fill(cm, neg)
+    pr = torch.softmax(s, dim=-1)
+    if p > 0.0:
+        idx = torch.arange(B * H * Sq * Sk, device=q.device, dtype=torch.int64).view(B, H, Sq, Sk)
+        keep = mix32(seed, idx) >= threshold(p)
+        pr = pr * keep.to(pr.dtype) * (1.0 / (1.0 - p))
+    o = torch.matmul(pr, vf)
+    return o.permute(0, 2, 1, 3).to(q.dtype)
+
+
+# --------------------------------------------------------------------------- native
+
+
+def _split(mode, a, b, c):
+    if mode == "qkv":  # a = [B,S,3,H,D]
+        return a[:, :, 0], a[:, :, 1], a[:, :, 2]
+    if mode == "q_kv":  # a = q, b = [B,Sk,2,H,D]
+        return a, b[:, :, 0], b[:, :, 1]
+    return a, b, c
+
+
+class _AttnFn(torch.autograd.Function):
+    """Inputs are packed the way the projections produce them (``qkv`` = one [B,S,3,H,D] tensor for
+    self-attention, ``q`` + ``kv`` [B,Sk,2,H,D] for cross-attention) so backward writes ONE packed
+    gradient buffer through strided views instead of three zero-padded slice gradients."""
+
+    @staticmethod
+    def forward(ctx, mode, a, b, c, lut, kpm, scale, causal, p, seed):
+        C = _ext.native()
+        q, k, v = _split(mode, a, b, c)
+        o, lse = C.attn_fwd(q, k, v, kpm, lut, float(scale), bool(causal), float(p), int(seed))
+        ctx.save_for_backward(a, b, c, o, lse, lut, kpm)
+        ctx.cfg = (mode, scale, causal, p, seed, lut is not None and lut.requires_grad)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        C = _ext.native()
+        a, b, c, o, lse, lut, kpm = ctx.saved_tensors
+        mode, scale, causal, p, seed, need_dlut = ctx.cfg
+        q, k, v = _split(mode, a, b, c)
+        da = db = dc = None
+        if mode == "qkv":
+            da = torch.empty_like(a)
+            dq, dk, dv = da[:, :, 0], da[:, :, 1], da[:, :, 2]
+        elif mode == "q_kv":
+            da = torch.empty_like(a)
+            db = torch.empty_like(b)
+            dq, dk, dv = da, db[:, :, 0], db[:, :, 1]
+        else:
+            dq = dk = dv = None
+        rq, rk, rv, dlut = C.attn_bwd(do.contiguous(), q, k, v, o, lse, kpm, lut, float(scale), bool(causal),
+                                      float(p), int(seed), bool(need_dlut), dq, dk, dv)
+        if mode == "sep":
+            da, db, dc = rq, rk, rv
+        return None, da, db, dc, (dlut if need_dlut else None), None, None, None, None, None
+
+
+def _prep_kpm(kpm):
+    if kpm is not None and kpm.dtype != torch.uint8:
+        kpm = kpm.to(torch.uint8)
+    return kpm.contiguous() if kpm is not None else None
+
+
+def attention(q, k, v, *, scale: float = 1.0, causal: bool = False, key_padding_mask=None, bias_lut=None,
+              dropout_p: float = 0.0, seed: int = 0):
+    """Multi-head attention.  q ``[B,Sq,H,D]``, k/v ``[B,Sk,H,D]``; ``key_padding_mask`` bool
+    ``[B,Sk]`` (True = attend); ``bias_lut`` from :func:`relative_bias_lut`."""
+    if _ext.use_native(q):
+        return _AttnFn.apply("sep", q, k, v, bias_lut, _prep_kpm(key_padding_mask), scale, causal, dropout_p, seed)
+    return _reference(q, k, v, scale, causal, key_padding_mask, bias_lut, dropout_p, seed)
+
+
+def attention_qkv(qkv, **kw):
+    """Self-attention on the fused projection output ``qkv`` = [B, S, 3, H, D]."""
+    if _ext.use_native(qkv):
+        return _AttnFn.apply("qkv", qkv, None, None, kw.get("bias_lut"), _prep_kpm(kw.get("key_padding_mask")),
+                             kw.get("scale", 1.0), kw.get("causal", False), kw.get("dropout_p", 0.0), kw.get("seed", 0))
+    return attention(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], **kw)
+
+
+def attention_q_kv(q, kv, **kw):
+    """Cross-attention with q = [B, Sq, H, D] and the fused key/value projection kv = [B, Sk, 2, H, D]."""
+    if _ext.use_native(q):
+        return _AttnFn.apply("q_kv", q, kv, None, kw.get("bias_lut"), _prep_kpm(kw.get("key_padding_mask")),
+                             kw.get("scale", 1.0), kw.get("causal", False), kw.get("dropout_p", 0.0), kw.get("seed", 0))
+    return attention(q, kv[:, :, 0], kv[:, :, 1], **kw)

@@ -1,0 +1,133 @@
+"""Fused (residual + dropout +) RMSNorm / LayerNorm.
+
+T5 is pre-norm with a weight-only RMSNorm in fp32 (transformers modeling_t5.py:50-72, residual +
+dropout at :137-141, :400): the residual stream update ``h = h + dropout(sublayer)`` and the next
+sub-layer's norm are one kernel here, returning both the new stream ``s`` and ``norm(s)``.
+BART is post-norm with a biased LayerNorm (modeling_bart.py:280-308):
+``LN(residual + dropout(sublayer))`` is one kernel.  Backward regenerates the dropout mask from
+the counter-based seed (ops/rng.py), so no mask is stored.
+
+Kernels: csrc/norm.hip (``norm_fwd`` / ``norm_bwd``).  On CPU (or with DLLM_REFERENCE_OPS=1)
+the functions below run the plain-torch reference, which is also the test oracle.
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import _ext
+from .rng import keep_mask
+
+RMS, LAYER = 0, 1
+
+
+def _reference(x, resid, weight, bias, eps, p, seed, kind):
+    xf = x.float()
+    if p > 0.0:
+        xf = xf * keep_mask(seed, p, x.shape, x.device).to(xf.dtype) * (1.0 / (1.0 - p))
+    s = xf + resid.float() if resid is not None else xf
+    s = s.to(x.dtype)
+    sf = s.float()
+    if kind == RMS:
+        rstd = torch.rsqrt(sf.pow(2).mean(-1, keepdim=True) + eps)
+        out = sf * rstd * weight.float()
+    else:
+        mean = sf.mean(-1, keepdim=True)
+        var = (sf - mean).pow(2).mean(-1, keepdim=True)
+        out = (sf - mean) * torch.rsqrt(var + eps) * weight.float()
+        if bias is not None:
+            out = out + bias.float()
+    return out.to(x.dtype), s
+
+
+class _NormFn(torch.autograd.Function):
+    """out = norm(s) with s = (resid +) dropout(x); returns (out, s)."""
+
+    @staticmethod
+    def forward(ctx, x, resid, weight, bias, eps, p, seed, kind):
+        C = _ext.native()
+        shape = x.shape
+        d = shape[-1]
+        x2 = x.reshape(-1, d)
+        r2 = resid.reshape(-1, d) if resid is not None else None
+        out, s, mean, rstd = C.norm_fwd(x2, r2, weight, bias, float(eps), float(p), int(seed), int(kind), True)
+        ctx.save_for_backward(s, weight, bias, mean, rstd)
+        ctx.cfg = (p, seed, kind, resid is not None, shape)
+        ctx.set_materialize_grads(False)
+        return out.view(shape), s.view(shape)
+
+    @staticmethod
+    def backward(ctx, dout, ds):
+        C = _ext.native()
+        s, weight, bias, mean, rstd = ctx.saved_tensors
+        p, seed, kind, has_resid, shape = ctx.cfg
+        d = shape[-1]
+        dout2 = dout.reshape(-1, d) if dout is not None else None
+        ds2 = ds.reshape(-1, d) if ds is not None else None
+        want_stream = has_resid and p > 0.0
+        dx, dstream, dw, db = C.norm_bwd(dout2, ds2, s, weight, bias, mean, rstd, float(p), int(seed), int(kind),
+                                         want_stream)
+        dx = dx.view(shape)
+        # d(resid) == d(s) (pre-dropout gradient); identical to dx when p == 0
+        dres = None
+        if has_resid:
+            dres = dstream.view(shape) if want_stream else dx
+        return (dx, dres, dw.to(weight.dtype), db.to(bias.dtype) if db is not None else None,
+                None, None, None, None)
+
+
+class _NormOnlyFn(torch.autograd.Function):
+    """out = norm(x) (no residual, no dropout)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, eps, kind):
+        C = _ext.native()
+        shape = x.shape
+        x2 = x.reshape(-1, shape[-1])
+        out, _, mean, rstd = C.norm_fwd(x2, None, weight, bias, float(eps), 0.0, 0, int(kind), False)
+        ctx.save_for_backward(x2, weight, bias, mean, rstd)
+        ctx.cfg = (kind, shape)
+        return out.view(shape)
+
+    @staticmethod
+    def backward(ctx, dout):
+        C = _ext.native()
+        x2, weight, bias, mean, rstd = ctx.saved_tensors
+        kind, shape = ctx.cfg
+        dx, _, dw, db = C.norm_bwd(dout.reshape(-1, shape[-1]), None, x2, weight, bias, mean, rstd, 0.0, 0, int(kind),
+                                   False)
+        return dx.view(shape), dw.to(weight.dtype), db.to(bias.dtype) if db is not None else None, None, None
+
+
+def _norm(x, resid, weight, bias, eps, p, seed, kind):
+    if _ext.use_native(x):
+        if resid is None and p == 0.0:
+            return _NormOnlyFn.apply(x, weight, bias, eps, kind), x
+        return _NormFn.apply(x, resid, weight, bias, eps, p, seed, kind)
+    return _reference(x, resid, weight, bias, eps, p, seed, kind)
+
+
+def rms_norm(x, weight, eps=1e-6):
+    return _norm(x, None, weight, None, eps, 0.0, 0, RMS)[0]
+
+
+def layer_norm(x, weight, bias, eps=1e-5):
+    return _norm(x, None, weight, bias, eps, 0.0, 0, LAYER)[0]
+
+
+def dropout_rms_norm(x, weight, eps, p, seed):
+    """(rms(s)*w, s) with s = dropout(x): T5 embedding dropout fused with block 0's first norm."""
+    return _norm(x, None, weight, None, eps, p, seed, RMS)
+
+
+def add_dropout_rms_norm(resid, x, weight, eps, p, seed):
+    """(rms(s)*w, s) with s = resid + dropout(x): T5 residual update fused with the next norm."""
+    return _norm(x, resid, weight, None, eps, p, seed, RMS)
+
+
+def add_dropout_layer_norm(resid, x, weight, bias, eps, p, seed):
+    """LN(resid + dropout(x)): BART post-norm residual block."""
+    return _norm(x, resid, weight, bias, eps, p, seed, LAYER)[0]
+
+
+def dropout_layer_norm(x, weight, bias, eps, p, seed):
+    return _norm(x, None, weight, bias, eps, p, seed, LAYER)[0]

@@ -1,0 +1,82 @@
+"""Counter-based dropout RNG shared by the HIP kernels and the torch reference path.
+
+Every dropout site gets a 32-bit ``seed`` from :class:`DropoutRNG`; element ``i`` of the tensor is
+kept iff ``mix32(seed, i) >= threshold(p)``.  Because the decision is a pure function of
+(seed, index), backward kernels regenerate the mask instead of storing it (no mask tensors in HBM),
+and the reference implementation below reproduces the kernels' masks bit-for-bit so numerics tests
+can run with p > 0.  Mirrors csrc/common.h ``dllm_mix32``.
+"""
+from __future__ import annotations
+
+import torch
+
+_C1 = 0x9E3779B1
+_M1 = 0x85EBCA6B
+_M2 = 0xC2B2AE35
+_MASK = 0xFFFFFFFF
+
+
+def mix32(seed: int, idx: torch.Tensor) -> torch.Tensor:
+    """murmur3-fmix32 of (idx * golden) ^ seed, computed in int64 with 32-bit wraparound."""
+    x = ((idx.to(torch.int64) * _C1) & _MASK) ^ (seed & _MASK)
+    x = x ^ (x >> 16)
+    x = (x * _M1) & _MASK
+    x = x ^ (x >> 13)
+    x = (x * _M2) & _MASK
+    x = x ^ (x >> 16)
+    return x
+
+
+def threshold(p: float) -> int:
+    return min(int(p * 4294967296.0), 0xFFFFFFFF)
+
+
+def keep_mask(seed: int, p: float, shape, device, numel_offset: int = 0) -> torch.Tensor:
+    """Boolean keep-mask of ``shape`` (row-major element indices starting at ``numel_offset``)."""
+    n = 1
+    for s in shape:
+        n *= s
+    idx = torch.arange(numel_offset, numel_offset + n, device=device, dtype=torch.int64)
+    return (mix32(seed, idx) >= threshold(p)).view(shape)
+
+
+def mix_host(seed: int, idx: int) -> int:
+    x = ((idx * _C1) & _MASK) ^ (seed & _MASK)
+    x ^= x >> 16
+    x = (x * _M1) & _MASK
+    x ^= x >> 13
+    x = (x * _M2) & _MASK
+    x ^= x >> 16
+    return x
+
+
+class DropoutRNG:
+    """Per-process seed stream.  ``next_seed()`` is called once per dropout site per forward; the
+    seed is saved for the backward.  ``state_dict`` makes resumed runs reproduce the stream."""
+
+    def __init__(self, seed: int = 42):
+        self.base = seed & _MASK
+        self.counter = 0
+
+    def next_seed(self) -> int:
+        self.counter += 1
+        return mix_host(self.base, self.counter)
+
+    def state_dict(self):
+        return {"base": self.base, "counter": self.counter}
+
+    def load_state_dict(self, d):
+        self.base = int(d["base"])
+        self.counter = int(d["counter"])
+
+
+_global = DropoutRNG(42)
+
+
+def default_rng() -> DropoutRNG:
+    return _global
+
+
+def manual_seed(seed: int) -> None:
+    _global.base = seed & _MASK
+    _global.counter = 0

@@ -1,0 +1,104 @@
+"""Flat parameter / gradient storage.
+
+Every trainable parameter becomes a view into ONE contiguous parameter buffer and its ``.grad`` a
+view into ONE contiguous gradient buffer, laid out in reverse registration order (≈ the order in
+which backward produces gradients).  This is the memory layout the whole runtime is built on:
+
+* the gradient reducer (parallel/reducer.py) all-reduces contiguous slices of the gradient buffer
+  in place — "gradient as bucket view", the layout torch DDP's C++ Reducer builds per bucket
+  (torch/nn/parallel/distributed.py:828-834, reducer.cpp) — with no flatten/unflatten copies;
+* the fused AdamW (ops/optim.py) runs ONE kernel over the whole buffer instead of a multi-tensor
+  launch group, and the clip-grad norm is one reduction (transformers trainer.py:2535-2539 →
+  torch clip_grad.py:93-96 does foreach norms over ~500 tensors);
+* train-task's per-tensor ``all_reduce`` loop (ref/train-task.py:65-69) becomes one coalesced
+  all-reduce over the same bytes.
+
+Segments are padded to 64 elements so every parameter starts 128-byte aligned for the vector
+loads in csrc/adamw.hip.  Tied parameters (T5 ``shared`` == ``lm_head``) appear once.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+import torch.nn as nn
+
+ALIGN = 64
+
+
+@dataclass
+class Segment:
+    name: str
+    offset: int
+    numel: int
+    shape: tuple
+
+
+class FlatParams:
+    def __init__(self, module: nn.Module, grad_dtype: torch.dtype | None = None, reverse: bool = True):
+        seen = set()
+        named = []
+        for n, p in module.named_parameters():
+            if not p.requires_grad or id(p) in seen:
+                continue
+            seen.add(id(p))
+            named.append((n, p))
+        if reverse:
+            named = named[::-1]
+        if not named:
+            raise ValueError("module has no trainable parameters")
+        dtypes = {p.dtype for _, p in named}
+        devices = {p.device for _, p in named}
+        if len(dtypes) != 1 or len(devices) != 1:
+            raise ValueError(f"FlatParams needs one dtype/device, got {dtypes} {devices}")
+        self.dtype = dtypes.pop()
+        self.device = devices.pop()
+        self.grad_dtype = grad_dtype or self.dtype
+        self.segments: list[Segment] = []
+        self.params: list[nn.Parameter] = []
+        off = 0
+        for n, p in named:
+            self.segments.append(Segment(n, off, p.numel(), tuple(p.shape)))
+            self.params.append(p)
+            off += (p.numel() + ALIGN - 1) // ALIGN * ALIGN
+        self.numel = off
+        self.param_buf = torch.zeros(off, dtype=self.dtype, device=self.device)
+        self.grad_buf = torch.zeros(off, dtype=self.grad_dtype, device=self.device)
+        with torch.no_grad():
+            for seg, p in zip(self.segments, self.params):
+                view = self.param_buf[seg.offset:seg.offset + seg.numel].view(seg.shape)
+                view.copy_(p.data)
+                p.data = view
+        self.attach_grads()
+
+    # -------------------------------------------------------------------------------------------
+    def grad_view(self, i: int) -> torch.Tensor:
+        seg = self.segments[i]
+        return self.grad_buf[seg.offset:seg.offset + seg.numel].view(seg.shape)
+
+    def attach_grads(self) -> None:
+        """(Re)bind every ``p.grad`` to its slice of the flat gradient buffer."""
+        for i, p in enumerate(self.params):
+            p.grad = self.grad_view(i)
+
+    def zero_grad(self) -> None:
+        self.grad_buf.zero_()
+        # something (e.g. user code) may have replaced a .grad: re-bind cheaply
+        for i, p in enumerate(self.params):
+            g = p.grad
+            if g is None or g.data_ptr() != self.grad_buf.data_ptr() + self.segments[i].offset * self.grad_buf.element_size():
+                p.grad = self.grad_view(i)
+
+    def decay_mask(self, no_decay_pred) -> torch.Tensor | None:
+        """uint8 mask over the flat buffer: 1 where weight decay applies; None if uniform."""
+        flags = [0 if no_decay_pred(s.name) else 1 for s in self.segments]
+        if all(flags) or not any(flags):
+            return None
+        m = torch.zeros(self.numel, dtype=torch.uint8, device=self.device)
+        for s, f in zip(self.segments, flags):
+            if f:
+                m[s.offset:s.offset + s.numel] = 1
+        return m
+
+    def state_layout(self) -> list[dict]:
+        return [{"name": s.name, "offset": s.offset, "numel": s.numel, "shape": list(s.shape)} for s in self.segments]

@@ -1,0 +1,77 @@
+"""The training step every loop shares: model → flat params → gradient reducer → fused AdamW.
+
+Both the Trainer-style loop (train/trainer.py, ref/train-torchrun.py) and the Accelerate-style
+facade (train/accelerator.py, ref/train-accelerator.py / train-task.py) — and bench.py — dispatch to
+this one engine and therefore to the same kernel library and the same RCCL reducer (BASELINE.json
+north star: "both loops dispatch to the same kernel library").
+"""
+from __future__ import annotations
+
+import contextlib
+
+import torch
+
+from ..ops.optim import FusedAdamW
+from ..parallel.env import DistEnv
+from ..parallel.flat import FlatParams
+from ..parallel.reducer import DEFAULT_BUCKET_MB, GradReducer
+
+# transformers Trainer.get_decay_parameter_names: no decay for biases and norm weights (trainer.py:1305-1315)
+def default_no_decay(name: str) -> bool:
+    n = name.lower()
+    return n.endswith(".bias") or "layer_norm" in n or "layernorm" in n or "norm.weight" in n
+
+
+class TrainEngine:
+    def __init__(self, model: torch.nn.Module, env: DistEnv, *, lr: float = 5e-5, weight_decay: float = 0.0,
+                 betas=(0.9, 0.999), eps: float = 1e-8, max_grad_norm: float | None = 1.0,
+                 dtype: torch.dtype = torch.bfloat16, bucket_mb: float = DEFAULT_BUCKET_MB, overlap: bool = True,
+                 no_decay=default_no_decay, label_smoothing: float = 0.0):
+        self.env = env
+        self.model = model.to(device=env.device, dtype=dtype)
+        self.dtype = dtype
+        self.flat = FlatParams(self.model)
+        self.reducer = GradReducer(self.flat, bucket_mb=bucket_mb, overlap=overlap) if env.world_size > 1 else None
+        if self.reducer is not None:
+            self.reducer.broadcast_params(self.model)
+        self.optimizer = FusedAdamW(self.flat, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay,
+                                    no_decay=no_decay)
+        self.max_grad_norm = max_grad_norm
+        self.label_smoothing = label_smoothing
+
+    def no_sync(self):
+        return self.reducer.no_sync() if self.reducer is not None else contextlib.nullcontext()
+
+    def forward(self, batch: dict):
+        return self.model(input_ids=batch["input_ids"], attention_mask=batch.get("attention_mask"),
+                          decoder_input_ids=batch.get("decoder_input_ids"), labels=batch["labels"],
+                          label_smoothing=self.label_smoothing)
+
+    def backward(self, loss: torch.Tensor, scale: float = 1.0, sync: bool = True):
+        ctx = contextlib.nullcontext() if sync else self.no_sync()
+        with ctx:
+            (loss * scale if scale != 1.0 else loss).backward()
+        if sync and self.reducer is not None:
+            self.reducer.post_backward()
+
+    def forward_backward(self, batch: dict, grad_accum: int = 1, sync: bool = True) -> torch.Tensor:
+        ctx = contextlib.nullcontext() if sync else self.no_sync()
+        with ctx:
+            out = self.forward(batch)
+            loss = out.loss
+            (loss / grad_accum if grad_accum > 1 else loss).backward()
+        if sync and self.reducer is not None:
+            self.reducer.post_backward()
+        return loss.detach()
+
+    def step(self, lr: float | None = None):
+        """Clip + AdamW + zero_grad.  Returns the pre-clip grad norm as a device tensor (or None)."""
+        if lr is not None:
+            self.optimizer.param_groups[0]["lr"] = lr
+        norm = self.optimizer.step(self.max_grad_norm)
+        self.optimizer.zero_grad()
+        return norm
+
+    def train(self, mode: bool = True):
+        self.model.train(mode)
+        return self

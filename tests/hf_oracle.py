@@ -1,0 +1,28 @@
+"""Build the transformers model that matches one of our configs and copy our weights into it."""
+import torch
+
+from distributed_llms_example_amd.models import to_hf_state_dict
+
+
+def hf_model_for(model):
+    import transformers
+    cfg = model.config
+    d = cfg.to_hf_dict()
+    d.pop("architectures", None)
+    d.pop("torch_dtype", None)
+    mt = d.pop("model_type")
+    if mt == "t5":
+        hcfg = transformers.T5Config(**d)
+        hf = transformers.T5ForConditionalGeneration(hcfg)
+    else:
+        hcfg = transformers.BartConfig(**d)
+        hf = transformers.BartForConditionalGeneration(hcfg)
+    hcfg._attn_implementation = "eager"
+    sd = to_hf_state_dict(model)
+    missing, unexpected = hf.load_state_dict(sd, strict=False)
+    allowed = {"encoder.embed_tokens.weight", "decoder.embed_tokens.weight", "lm_head.weight",
+               "model.encoder.embed_tokens.weight", "model.decoder.embed_tokens.weight"}
+    bad = [m for m in missing if m not in allowed]
+    assert not bad, bad
+    assert not unexpected, unexpected
+    return hf.to(dtype=next(model.parameters()).dtype)

@@ -1,0 +1,230 @@
+"""HIP kernel numerics vs plain-PyTorch fp32 references (SURVEY.md §4 level 1).
+
+Every test runs the native (gfx950) op on bf16 inputs and the reference implementation of the SAME
+op in fp32 on the same (bf16-rounded) values; dropout uses the shared counter-based mask so p > 0
+is compared exactly, not statistically.  Also asserts the native extension is the code that ran.
+"""
+import math
+
+import pytest
+import torch
+
+from distributed_llms_example_amd import _ext
+from distributed_llms_example_amd.ops import activations, attention as A, cross_entropy as CE, norms
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _close(a, b, rtol, atol, msg=""):
+    a = a.float()
+    b = b.float()
+    err = (a - b).abs()
+    lim = atol + rtol * b.abs()
+    bad = (err > lim).float().mean().item()
+    assert bad < 1e-3, f"{msg}: {bad*100:.3f}% elements out of tol; max err {err.max().item():.4g}"
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+def test_native_extension_loaded():
+    assert _ext.native() is not None, _ext.load_error()
+    assert _ext.native().arch == "gfx950"
+    x = torch.randn(8, 64, device=DEV, dtype=torch.bfloat16)
+    assert _ext.use_native(x)
+
+
+@pytest.mark.parametrize("kind", [norms.RMS, norms.LAYER])
+@pytest.mark.parametrize("d", [64, 512, 768, 1024, 2048])
+@pytest.mark.parametrize("resid,p", [(False, 0.0), (True, 0.0), (True, 0.1), (False, 0.1)])
+def test_norm(kind, d, resid, p):
+    torch.manual_seed(d)
+    N = 301
+    x = torch.randn(N, d, device=DEV, dtype=torch.bfloat16)
+    r = torch.randn(N, d, device=DEV, dtype=torch.bfloat16) if resid else None
+    w = (1 + 0.1 * torch.randn(d, device=DEV)).to(torch.bfloat16)
+    b = (0.1 * torch.randn(d, device=DEV)).to(torch.bfloat16) if kind == norms.LAYER else None
+    seed = 1234
+    eps = 1e-6
+    xs = [t.clone().requires_grad_(True) if t is not None else None for t in (x, r, w, b)]
+    out, s = norms._norm(xs[0], xs[1], xs[2], xs[3], eps, p, seed, kind)
+    xr = [t.detach().float().clone().requires_grad_(True) if t is not None else None for t in (x, r, w, b)]
+    ref_out, ref_s = norms._reference(xr[0], xr[1], xr[2], xr[3], eps, p, seed, kind)
+    _close(out, ref_out, 2e-2, 2e-2, "out")
+    _close(s, ref_s, 1e-2, 1e-2, "s")
+    g1 = torch.randn_like(out)
+    g2 = torch.randn_like(out) if (resid or p > 0) else None
+    loss = (out.float() * g1.float()).sum() + ((s.float() * g2.float()).sum() if g2 is not None else 0)
+    loss.backward()
+    ref_loss = (ref_out * g1.float()).sum() + ((ref_s * g2.float()).sum() if g2 is not None else 0)
+    ref_loss.backward()
+    assert _rel(xs[0].grad, xr[0].grad) < 2e-2
+    if resid:
+        assert _rel(xs[1].grad, xr[1].grad) < 2e-2
+    assert _rel(xs[2].grad, xr[2].grad) < 2e-2
+    if b is not None:
+        assert _rel(xs[3].grad, xr[3].grad) < 2e-2
+
+
+@pytest.mark.parametrize("act,gated", [("relu", False), ("gelu", False), ("gelu_new", True), ("gelu_new", False),
+                                       ("silu", True)])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_act(act, gated, p):
+    torch.manual_seed(0)
+    N, F = 257, 384
+    x = torch.randn(N, 2 * F if gated else F, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    y = activations.act_dropout(x, act, p, 77, gated=gated)
+    xr = x.detach().float().requires_grad_(True)
+    yr = activations._reference(xr, act, gated, p, 77)
+    _close(y, yr, 2e-2, 2e-2, "act fwd")
+    g = torch.randn_like(y)
+    (y.float() * g.float()).sum().backward()
+    (yr * g.float()).sum().backward()
+    assert _rel(x.grad, xr.grad) < 2e-2
+
+
+def test_dropout_standalone():
+    x = torch.randn(64, 96, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    y = activations.dropout(x, 0.25, 99)
+    from distributed_llms_example_amd.ops.rng import keep_mask
+    ref = x.detach().float() * keep_mask(99, 0.25, x.shape, x.device).float() / 0.75
+    _close(y, ref, 1e-2, 1e-2)
+    y.sum().backward()
+    _close(x.grad, keep_mask(99, 0.25, x.shape, x.device).float() / 0.75, 1e-2, 1e-2)
+
+
+@pytest.mark.parametrize("V", [32128, 50264, 50265, 1000])
+@pytest.mark.parametrize("smooth,bias", [(0.0, False), (0.1, False), (0.0, True)])
+def test_cross_entropy(V, smooth, bias):
+    torch.manual_seed(V)
+    N = 300
+    logits = (3 * torch.randn(N, V, device=DEV)).to(torch.bfloat16).requires_grad_(True)
+    labels = torch.randint(0, V, (N,), device=DEV)
+    labels[::7] = -100
+    bvec = (0.5 * torch.randn(V, device=DEV)) if bias else None
+    loss = CE.cross_entropy(logits, labels, bias=bvec, label_smoothing=smooth, inplace_grad=False)
+    lr = logits.detach().float().requires_grad_(True)
+    ref = CE._reference(lr, labels, bvec, smooth, -100)
+    assert abs(loss.item() - ref.item()) < 2e-3 * max(1.0, abs(ref.item()))
+    loss.backward()
+    ref.backward()
+    assert _rel(logits.grad, lr.grad) < 2e-2
+
+
+def test_cross_entropy_inplace_grad():
+    V, N = 32128, 64
+    logits = torch.randn(N, V, device=DEV, dtype=torch.bfloat16)
+    labels = torch.randint(0, V, (N,), device=DEV)
+    lref = logits.float().clone().requires_grad_(True)
+    leaf = torch.zeros(N, V, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    x = leaf + logits  # non-leaf produced by an op, like the LM-head GEMM output
+    loss = CE.cross_entropy(x, labels, inplace_grad=True)
+    loss.backward()
+    ref = torch.nn.functional.cross_entropy(lref, labels)
+    ref.backward()
+    assert _rel(leaf.grad, lref.grad) < 2e-2
+
+
+def test_adamw_matches_reference():
+    from distributed_llms_example_amd.ops.optim import FusedAdamW
+    from distributed_llms_example_amd.parallel.flat import FlatParams
+    torch.manual_seed(0)
+    m1 = torch.nn.Sequential(torch.nn.Linear(64, 128), torch.nn.LayerNorm(128), torch.nn.Linear(128, 32)).to(DEV)
+    m2 = torch.nn.Sequential(torch.nn.Linear(64, 128), torch.nn.LayerNorm(128), torch.nn.Linear(128, 32)).to(DEV)
+    m1 = m1.to(torch.bfloat16)
+    m2.load_state_dict({k: v.float() for k, v in m1.state_dict().items()})
+    f1 = FlatParams(m1)
+    opt = FusedAdamW(f1, lr=1e-2, weight_decay=0.01, no_decay=lambda n: "bias" in n or n.startswith("1."))
+    ref_groups = [
+        {"params": [p for n, p in m2.named_parameters() if not ("bias" in n or n.startswith("1."))], "weight_decay": 0.01},
+        {"params": [p for n, p in m2.named_parameters() if ("bias" in n or n.startswith("1."))], "weight_decay": 0.0}]
+    ref = torch.optim.AdamW(ref_groups, lr=1e-2)
+    for step in range(5):
+        x = torch.randn(16, 64, device=DEV)
+        loss1 = m1(x.to(torch.bfloat16)).float().pow(2).mean()
+        opt.zero_grad()
+        loss1.backward()
+        # use identical gradients on both sides
+        for (n1, p1), (n2, p2) in zip(m1.named_parameters(), m2.named_parameters()):
+            p2.grad = p1.grad.float().clone()
+        norm = opt.step(max_grad_norm=1.0)
+        tn = torch.nn.utils.clip_grad_norm_(m2.parameters(), 1.0)
+        assert abs(norm.item() - tn.item()) < 1e-2 * tn.item() + 1e-4
+        ref.step()
+        for p1, p2 in zip(m1.parameters(), m2.parameters()):
+            assert _rel(p1, p2) < 1e-2
+    # master weights track fp32 reference exactly (up to fp32 rounding)
+    for seg, p2 in zip(f1.segments, [p for n, p in reversed(list(m2.named_parameters()))]):
+        mw = opt.master[seg.offset:seg.offset + seg.numel].view(seg.shape)
+        assert _rel(mw, p2) < 1e-4
+
+
+ATTN_CASES = [
+    # B, H, Sq, Sk, bias, kpm, causal, p, scale
+    (2, 4, 128, 128, False, False, False, 0.0, 0.125),
+    (2, 3, 200, 200, True, True, False, 0.0, 1.0),
+    (1, 2, 77, 300, False, True, False, 0.0, 0.125),   # cross-attention shape
+    (2, 2, 130, 130, True, False, True, 0.0, 1.0),     # T5 decoder (causal + unidirectional bias)
+    (2, 2, 96, 96, False, False, True, 0.1, 0.125),    # dropout on probabilities
+    (1, 2, 257, 257, True, True, False, 0.1, 1.0),
+    (1, 2, 1, 33, True, False, True, 0.0, 1.0),        # single-token decode step with cache
+    (2, 12, 1024, 1024, True, True, False, 0.1, 1.0),  # t5-base encoder shape
+]
+
+
+@pytest.mark.parametrize("B,H,Sq,Sk,bias,kpm,causal,p,scale", ATTN_CASES)
+def test_attention(B, H, Sq, Sk, bias, kpm, causal, p, scale):
+    torch.manual_seed(Sq * 7 + Sk)
+    D = 64
+    q = torch.randn(B, Sq, H, D, device=DEV).to(torch.bfloat16)
+    k = torch.randn(B, Sk, H, D, device=DEV).to(torch.bfloat16)
+    v = torch.randn(B, Sk, H, D, device=DEV).to(torch.bfloat16)
+    table = torch.randn(32, H, device=DEV) * 0.5 if bias else None
+    mask = None
+    if kpm:
+        mask = torch.ones(B, Sk, dtype=torch.bool, device=DEV)
+        mask[0, Sk - Sk // 5:] = False
+    seed = 4242
+    qs, ks, vs = (t.clone().requires_grad_(True) for t in (q, k, v))
+    tab1 = table.clone().requires_grad_(True) if bias else None
+    lut = A.relative_bias_lut(tab1, Sq, Sk, not causal, 32, 128, q_offset=Sk - Sq) if bias else None
+    o = A.attention(qs, ks, vs, scale=scale, causal=causal, key_padding_mask=mask, bias_lut=lut, dropout_p=p, seed=seed)
+    qr, kr, vr = (t.detach().float().requires_grad_(True) for t in (q, k, v))
+    tab2 = table.clone().requires_grad_(True) if bias else None
+    lut2 = A.relative_bias_lut(tab2, Sq, Sk, not causal, 32, 128, q_offset=Sk - Sq) if bias else None
+    ref = A._reference(qr, kr, vr, scale, causal, mask, lut2, p, seed)
+    assert _rel(o, ref) < 2e-2, _rel(o, ref)
+    g = torch.randn_like(o)
+    (o.float() * g.float()).sum().backward()
+    (ref * g.float()).sum().backward()
+    # a single query row (decode step) makes dq one 64-vector dominated by bf16 rounding of dS
+    tol = 6e-2 if Sq < 4 else 3e-2
+    for name, a_, b_ in (("dq", qs.grad, qr.grad), ("dk", ks.grad, kr.grad), ("dv", vs.grad, vr.grad)):
+        assert _rel(a_, b_) < tol, (name, _rel(a_, b_))
+    if bias:
+        assert _rel(tab1.grad, tab2.grad) < 3e-2, _rel(tab1.grad, tab2.grad)
+
+
+def test_attention_packed_qkv_grad():
+    B, S, H, D = 2, 150, 4, 64
+    qkv = torch.randn(B, S, 3, H, D, device=DEV).to(torch.bfloat16).requires_grad_(True)
+    o = A.attention_qkv(qkv, scale=0.125, causal=True)
+    r = qkv.detach().float().requires_grad_(True)
+    ref = A._reference(r[:, :, 0], r[:, :, 1], r[:, :, 2], 0.125, True, None, None, 0.0, 0)
+    assert _rel(o, ref) < 2e-2
+    g = torch.randn_like(o)
+    (o.float() * g.float()).sum().backward()
+    (ref * g.float()).sum().backward()
+    assert _rel(qkv.grad, r.grad) < 3e-2
+    kvin = torch.randn(B, 70, 2, H, D, device=DEV).to(torch.bfloat16).requires_grad_(True)
+    q = torch.randn(B, S, H, D, device=DEV).to(torch.bfloat16).requires_grad_(True)
+    o2 = A.attention_q_kv(q, kvin, scale=0.125)
+    kr = kvin.detach().float().requires_grad_(True)
+    qr = q.detach().float().requires_grad_(True)
+    ref2 = A._reference(qr, kr[:, :, 0], kr[:, :, 1], 0.125, False, None, None, 0.0, 0)
+    assert _rel(o2, ref2) < 2e-2
+    (o2.float().sum()).backward()
+    ref2.sum().backward()
+    assert _rel(kvin.grad, kr.grad) < 3e-2 and _rel(q.grad, qr.grad) < 3e-2

@@ -1,0 +1,109 @@
+"""Build the in-tree native extension ``distributed_llms_example_amd/_C*.so`` for gfx950.
+
+No hipify, no CUDA compatibility layer: every ``csrc/*.hip`` file is plain HIP compiled by
+``hipcc --offload-arch=gfx950`` into an object with C-ABI launchers; ``csrc/bind.cpp`` (torch +
+pybind11 glue, host-only) is compiled by the host C++ compiler with torch's headers; both are linked
+into one shared object next to the Python package so it travels with the repo snapshot.
+Incremental: an object is rebuilt only when its source or a header is newer.
+
+    python tools/build_native.py [--force] [-j N]
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import glob
+import os
+import subprocess
+import sys
+import sysconfig
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "csrc")
+BUILD = os.path.join(ROOT, "build", "native")
+PKG = os.path.join(ROOT, "distributed_llms_example_amd")
+ARCH = os.environ.get("DLLM_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+CXX = os.environ.get("CXX", "g++")
+
+
+def _torch_paths():
+    import torch
+    from torch.utils import cpp_extension as ce
+    inc = ce.include_paths(device_type="cuda")
+    lib = os.path.join(os.path.dirname(torch.__file__), "lib")
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    return inc, lib, abi
+
+
+def so_path() -> str:
+    return os.path.join(PKG, "_C" + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def _newer(src_list, out) -> bool:
+    if not os.path.exists(out):
+        return True
+    t = os.path.getmtime(out)
+    return any(os.path.getmtime(s) > t for s in src_list)
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"command failed ({r.returncode}): {' '.join(cmd)}\n{r.stdout}")
+    return r.stdout
+
+
+def build(force: bool = False, jobs: int = 8, verbose: bool = True) -> str:
+    os.makedirs(BUILD, exist_ok=True)
+    headers = glob.glob(os.path.join(CSRC, "*.h"))
+    hip_srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+    inc, lib, abi = _torch_paths()
+    py_inc = sysconfig.get_paths()["include"]
+    jobs_list = []
+    objs = []
+    for src in hip_srcs:
+        obj = os.path.join(BUILD, os.path.basename(src) + ".o")
+        objs.append(obj)
+        if force or _newer([src] + headers, obj):
+            jobs_list.append([HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-ffp-contract=fast",
+                              "-munsafe-fp-atomics", "-I", CSRC, "-c", src, "-o", obj])
+    bind_src = os.path.join(CSRC, "bind.cpp")
+    bind_obj = os.path.join(BUILD, "bind.cpp.o")
+    objs.append(bind_obj)
+    if force or _newer([bind_src] + headers, bind_obj):
+        cmd = [CXX, "-O2", "-fPIC", "-std=c++17", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DUSE_ROCM=1",
+               "-D__HIP_PLATFORM_AMD__=1", "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H",
+               "-Wno-deprecated-declarations", "-I", CSRC, "-I", py_inc]
+        for i in inc:
+            cmd += ["-I", i]
+        cmd += ["-c", bind_src, "-o", bind_obj]
+        jobs_list.append(cmd)
+    if jobs_list:
+        with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+            futs = [ex.submit(_run, c) for c in jobs_list]
+            for f in futs:
+                f.result()
+    out = so_path()
+    if force or jobs_list or _newer(objs, out):
+        link = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out] + objs + [
+            f"-L{lib}", "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python", "-lc10_hip", "-ltorch_hip",
+            "-L/opt/rocm/lib", "-lamdhip64", f"-Wl,-rpath,{lib}", "-Wl,-rpath,/opt/rocm/lib"]
+        _run(link)
+        if verbose:
+            print(f"[build_native] linked {os.path.relpath(out, ROOT)} ({len(hip_srcs)} HIP sources, arch {ARCH})")
+    elif verbose:
+        print(f"[build_native] up to date: {os.path.relpath(out, ROOT)}")
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-j", type=int, default=8)
+    a = ap.parse_args()
+    build(force=a.force, jobs=a.j)
+
+
+if __name__ == "__main__":
+    sys.exit(main())
