@@ -54,10 +54,7 @@ __global__ __launch_bounds__(256) void act_fwd_kernel(const T* __restrict__ x, T
 #pragma unroll
       for (int k = 0; k < 4; ++k) r[k] = act_f<ACT>(a[k]);
     }
-    if (p > 0.f) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) r[k] = (mix32(seed, (uint32_t)(oidx + k)) >= thr) ? r[k] * dscale : 0.f;
-    }
+    if (p > 0.f) dropout4(r, seed, thr, (uint32_t)oidx, dscale);
     Elem<T>::store4(y + oidx, r);
   }
 }
@@ -73,10 +70,7 @@ __global__ __launch_bounds__(256) void act_bwd_kernel(const T* __restrict__ dy, 
     const int col = (int)(i - row * F4) * 4;
     const long oidx = row * F + col;
     f32x4 g = Elem<T>::load4(dy + oidx);
-    if (p > 0.f) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) g[k] = (mix32(seed, (uint32_t)(oidx + k)) >= thr) ? g[k] * dscale : 0.f;
-    }
+    if (p > 0.f) dropout4(g, seed, thr, (uint32_t)oidx, dscale);
     if (GATED) {
       f32x4 a = Elem<T>::load4(x + row * 2 * F + col);
       f32x4 b = Elem<T>::load4(x + row * 2 * F + F + col);
@@ -103,8 +97,7 @@ __global__ __launch_bounds__(256) void dropout_kernel(const T* __restrict__ x, T
   const float dscale = 1.f / (1.f - p);
   for (long i = blockIdx.x * 256L + threadIdx.x; i < total4; i += (long)gridDim.x * 256) {
     f32x4 v = Elem<T>::load4(x + i * 4);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) v[k] = (mix32(seed, (uint32_t)(i * 4 + k)) >= thr) ? v[k] * dscale : 0.f;
+    dropout4(v, seed, thr, (uint32_t)(i * 4), dscale);
     Elem<T>::store4(y + i * 4, v);
   }
 }

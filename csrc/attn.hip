@@ -15,13 +15,15 @@
 //   (V^T, 8-B pad, conflict-free ds_read_b64).  Grid is 1-D with an XCD-aware bijective remap so the
 //   q-tiles of one (b, h) land on one XCD and share K/V through its L2.
 //
-// Backward (one workgroup = 4 waves = 128 keys; loop over 32-row query tiles):
-//   "key on the lane": S = Q K^T and dPd = dO V^T come out with the key on the MFMA column, so the
-//   P / dS accumulators are directly the B operands of dV^T += dO^T Pd and dK^T += Q^T dS (K and V of
-//   the wave's 32 keys stay in registers).  dS crosses LDS once (per wave) for dQ = dS K; the four
-//   waves' dQ partials are summed in LDS and added to an fp32 dQ buffer with 256-B-contiguous atomics.
-//   The relative-bias gradient is the sum of dS along diagonals: LDS float atomics into a window of
-//   the LUT, then one global atomic per entry per workgroup.
+// Backward = two atomic-free kernels (recompute P from the forward's LSE in both):
+//   dQ kernel (query blocks, query on the lane, like the forward): dS^T = P^T (dP^T - delta) stays in
+//   registers and feeds dQ^T += K^T dS^T as the B operand; it also computes delta = rowsum(dO * O).
+//   dK/dV kernel (key blocks of 128, key on the lane): S = Q K^T and dPd = dO V^T come out with the key
+//   on the MFMA column, so P and dS are directly the B operands of dV^T += dO^T Pd and dK^T += Q^T dS
+//   (K and V of the wave's 32 keys stay in registers).  The extra recompute (2 of 7 GEMMs) buys no
+//   fp32 dQ atomics, no dS round trip through LDS and no cross-wave reduction.  The relative-bias
+//   gradient is the sum of dS along diagonals: LDS float atomics into a window of the LUT, then one
+//   global atomic per entry per workgroup.
 #include "common.h"
 #include "attn_params.h"
 
@@ -111,7 +113,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnParams P) {
   }
   const int ntiles = kend > 0 ? (kend + FWD_BN - 1) / FWD_BN : 0;
   const float dscale = DROP ? 1.f / (1.f - P.p_drop) : 1.f;
-  const long drop_row = ((long)(b * P.H + h) * P.Sq + qrow) * P.Sk;
+  const long drop_row = ((long)(b * P.H + h) * P.Sq + qrow) * ((P.Sk + 1) & ~1);  // Sk rounded to even
 
   for (int kt = 0; kt < ntiles; ++kt) {
     const int kbase = kt * FWD_BN;
@@ -173,16 +175,25 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnParams P) {
     float lsum = 0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      float p0 = exp2f((s0[i] - m_use) * LOG2E);
-      float p1 = exp2f((s1[i] - m_use) * LOG2E);
+      const float p0 = exp2f((s0[i] - m_use) * LOG2E);
+      const float p1 = exp2f((s1[i] - m_use) * LOG2E);
       lsum += p0 + p1;
-      if (DROP) {
-        const int kl0 = crow(i, hh), kl1 = 32 + crow(i, hh);
-        p0 = (mix32(P.seed, (uint32_t)(drop_row + kbase + kl0)) >= P.thr) ? p0 * dscale : 0.f;
-        p1 = (mix32(P.seed, (uint32_t)(drop_row + kbase + kl1)) >= P.thr) ? p1 * dscale : 0.f;
-      }
       s0[i] = p0;
       s1[i] = p1;
+    }
+    if (DROP) {
+      // registers (i, i+1), i even, hold keys (2m, 2m+1): one hash per pair
+#pragma unroll
+      for (int i = 0; i < 16; i += 2) {
+        const uint32_t e0 = (uint32_t)(drop_row + kbase + crow(i, hh));
+        bool a0, a1, c0, c1;
+        keep_two(P.seed, P.thr, e0, a0, a1);
+        keep_two(P.seed, P.thr, e0 + 32u, c0, c1);
+        s0[i] = a0 ? s0[i] * dscale : 0.f;
+        s0[i + 1] = a1 ? s0[i + 1] * dscale : 0.f;
+        s1[i] = c0 ? s1[i] * dscale : 0.f;
+        s1[i + 1] = c1 ? s1[i + 1] * dscale : 0.f;
+      }
     }
     l_run = l_run * alpha + lsum;
     m_run = m_new;
@@ -236,39 +247,196 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnParams P) {
 }
 
 // ================================================================================== backward
-// delta[b,h,q] = sum_d dO * O
-__global__ __launch_bounds__(256) void attn_bwd_delta_kernel(AttnParams P) {
-  const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  const long nrows = (long)P.B * P.H * P.Sq;
-  if (wid >= nrows) return;
-  const int q = wid % P.Sq;
-  const int bh = wid / P.Sq;
+constexpr int BWD_BK = 128;    // dK/dV kernel: keys per workgroup (4 waves x 32)
+constexpr int BWD_BQ = 32;     // dK/dV kernel: query rows per tile
+constexpr int QS_STRIDE = 72;  // [32 q][64 d] bf16 rows (144 B)
+constexpr int QT_STRIDE = 36;  // [64 d][32 q] bf16 rows (72 B: 8-B reads conflict-free)
+
+// ---- dQ kernel.  One workgroup = 128 query rows (4 waves x 32, query on the lane); loop over 64-key tiles.
+// S^T = K Q^T and dP^T = V dO^T (swapped, like the forward), dS^T = P^T (dP^T - delta) in registers, and
+// dQ^T += K^T dS^T takes the dS^T accumulators directly as B operands.  Also computes and stores
+// delta = rowsum(dO * O) (one dot per lane pair) for the dK/dV kernel.  No atomics.
+template <bool HAS_BIAS, bool HAS_KPM, bool CAUSAL, bool DROP>
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnParams P) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint16_t* Ks = reinterpret_cast<uint16_t*>(smem);             // [64][KS_STRIDE]
+  uint16_t* Vs = Ks + FWD_BN * KS_STRIDE;                        // [64][KS_STRIDE]
+  uint16_t* Kt = Vs + FWD_BN * KS_STRIDE;                        // [64 d][VT_STRIDE]
+  float* kmask = reinterpret_cast<float*>(Kt + D * VT_STRIDE);   // [64]
+  float* lut_s = kmask + FWD_BN;                                 // [Sk + FWD_BM + FWD_BN]
+
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 31, hh = lane >> 5;
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int qt = logical % P.n_tiles;
+  const int bh = logical / P.n_tiles;
   const int h = bh % P.H, b = bh / P.H;
-  const float a = bf2f(P.dout[b * P.do_sb + (long)q * P.do_ss + h * P.do_sh + lane]);
-  const float c = bf2f(P.o[b * P.o_sb + (long)q * P.o_ss + h * P.o_sh + lane]);
-  const float s = wave_sum(a * c);
-  if (lane == 0) const_cast<float*>(P.delta)[wid] = s;
+  const int q0 = qt * FWD_BM;
+  const int qrow = q0 + w * 32 + r;
+  const bool qvalid = qrow < P.Sq;
+  const int lut_base = P.Sq - 1 - (q0 + FWD_BM - 1);
+  if (HAS_BIAS) {
+    const int L = P.Sq + P.Sk - 1;
+    const float* lrow = P.lut + (long)h * L;
+    for (int i = tid; i < P.Sk + FWD_BM + FWD_BN; i += 256) {
+      const int gi = lut_base + i;
+      lut_s[i] = (gi >= 0 && gi < L) ? lrow[gi] : 0.f;
+    }
+  }
+  bf16x8v qf[4], dof[4];
+  float dpart = 0.f;
+  {
+    const uint16_t* qp = P.q + b * P.q_sb + (long)qrow * P.q_ss + h * P.q_sh;
+    const uint16_t* dp = P.dout + b * P.do_sb + (long)qrow * P.do_ss + h * P.do_sh;
+    const uint16_t* op = P.o + b * P.o_sb + (long)qrow * P.o_ss + h * P.o_sh;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      u16x8 a = {0, 0, 0, 0, 0, 0, 0, 0}, c = a, o8 = a;
+      if (qvalid) {
+        a = *reinterpret_cast<const u16x8*>(qp + 16 * s + 8 * hh);
+        c = *reinterpret_cast<const u16x8*>(dp + 16 * s + 8 * hh);
+        o8 = *reinterpret_cast<const u16x8*>(op + 16 * s + 8 * hh);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dpart += bf2f(c[j]) * bf2f(o8[j]);
+      qf[s] = as_frag(a);
+      dof[s] = as_frag(c);
+    }
+  }
+  const float delta = dpart + __shfl_xor(dpart, 32, 64);
+  const long row_off = (long)(b * P.H + h) * P.Sq + qrow;
+  if (qvalid && hh == 0) P.delta[row_off] = delta;
+  const float lse_q = qvalid ? P.lse[row_off] : INFINITY;
+
+  f32x16 dq0 = {}, dq1 = {};
+  int kend = P.Sk;
+  if (CAUSAL) {
+    const int lim = q0 + FWD_BM - 1 + P.causal_off + 1;
+    kend = lim < kend ? lim : kend;
+  }
+  const int ntiles = kend > 0 ? (kend + FWD_BN - 1) / FWD_BN : 0;
+  const float dscale = DROP ? 1.f / (1.f - P.p_drop) : 1.f;
+  const long drop_row = row_off * ((P.Sk + 1) & ~1);
+
+  for (int kt = 0; kt < ntiles; ++kt) {
+    const int kbase = kt * FWD_BN;
+    __syncthreads();
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+      const int key = (tid >> 3) + 32 * pass, ch = tid & 7;
+      const int kk = kbase + key;
+      u16x8 kv = {0, 0, 0, 0, 0, 0, 0, 0}, vv = kv;
+      if (kk < P.Sk) {
+        kv = *reinterpret_cast<const u16x8*>(P.k + b * P.k_sb + (long)kk * P.k_ss + h * P.k_sh + ch * 8);
+        vv = *reinterpret_cast<const u16x8*>(P.v + b * P.v_sb + (long)kk * P.v_ss + h * P.v_sh + ch * 8);
+      }
+      *reinterpret_cast<u16x8*>(Ks + key * KS_STRIDE + ch * 8) = kv;
+      *reinterpret_cast<u16x8*>(Vs + key * KS_STRIDE + ch * 8) = vv;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) Kt[(ch * 8 + e) * VT_STRIDE + key] = kv[e];
+    }
+    if (tid < FWD_BN) {
+      const int kk = kbase + tid;
+      bool ok = kk < P.Sk;
+      if (HAS_KPM && ok) ok = P.kpm[(long)b * P.Sk + kk] != 0;
+      kmask[tid] = ok ? 0.f : -INFINITY;
+    }
+    __syncthreads();
+
+    f32x16 s0 = {}, s1 = {}, p0 = {}, p1 = {};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      bf16x8v a0 = as_frag(*reinterpret_cast<const u16x8*>(Ks + r * KS_STRIDE + 16 * s + 8 * hh));
+      bf16x8v a1 = as_frag(*reinterpret_cast<const u16x8*>(Ks + (32 + r) * KS_STRIDE + 16 * s + 8 * hh));
+      bf16x8v v0 = as_frag(*reinterpret_cast<const u16x8*>(Vs + r * KS_STRIDE + 16 * s + 8 * hh));
+      bf16x8v v1 = as_frag(*reinterpret_cast<const u16x8*>(Vs + (32 + r) * KS_STRIDE + 16 * s + 8 * hh));
+      s0 = mfma32(a0, qf[s], s0);
+      s1 = mfma32(a1, qf[s], s1);
+      p0 = mfma32(v0, dof[s], p0);
+      p1 = mfma32(v1, dof[s], p1);
+    }
+    // dS^T = P^T * (dP^T * keep - delta), P^T = exp(S^T * scale + bias - lse)
+#pragma unroll
+    for (int i = 0; i < 16; i += 2) {
+      float kf0[2] = {1.f, 1.f}, kf1[2] = {1.f, 1.f};
+      if (DROP) {
+        const uint32_t e0 = (uint32_t)(drop_row + kbase + crow(i, hh));
+        bool a0, a1, c0, c1;
+        keep_two(P.seed, P.thr, e0, a0, a1);
+        keep_two(P.seed, P.thr, e0 + 32u, c0, c1);
+        kf0[0] = a0 ? dscale : 0.f;
+        kf0[1] = a1 ? dscale : 0.f;
+        kf1[0] = c0 ? dscale : 0.f;
+        kf1[1] = c1 ? dscale : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int ii = i + u;
+        const int kl0 = crow(ii, hh), kl1 = 32 + kl0;
+        float v0 = s0[ii] * P.scale + kmask[kl0];
+        float v1 = s1[ii] * P.scale + kmask[kl1];
+        if (HAS_BIAS) {
+          v0 += lut_s[kbase + kl0 - qrow + P.Sq - 1 - lut_base];
+          v1 += lut_s[kbase + kl1 - qrow + P.Sq - 1 - lut_base];
+        }
+        if (CAUSAL) {
+          if (kbase + kl0 > qrow + P.causal_off) v0 = -INFINITY;
+          if (kbase + kl1 > qrow + P.causal_off) v1 = -INFINITY;
+        }
+        const float pr0 = exp2f((v0 - lse_q) * LOG2E);
+        const float pr1 = exp2f((v1 - lse_q) * LOG2E);
+        s0[ii] = pr0 * (p0[ii] * kf0[u] - delta);
+        s1[ii] = pr1 * (p1[ii] * kf1[u] - delta);
+      }
+    }
+    // dQ^T += K^T dS^T
+    const bf16x8v da0 = pack8(s0, 0), da1 = pack8(s0, 8), db0 = pack8(s1, 0), db1 = pack8(s1, 8);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const uint16_t* krow = Kt + (32 * t + r) * VT_STRIDE;
+      f32x16 acc = t == 0 ? dq0 : dq1;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+        for (int sp = 0; sp < 2; ++sp) {
+          const int kb0 = kb * 32 + 16 * sp + 4 * hh;
+          u16x4 lo = *reinterpret_cast<const u16x4*>(krow + kb0);
+          u16x4 hi = *reinterpret_cast<const u16x4*>(krow + kb0 + 8);
+          u16x8 av = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+          const bf16x8v bf = kb == 0 ? (sp == 0 ? da0 : da1) : (sp == 0 ? db0 : db1);
+          acc = mfma32(as_frag(av), bf, acc);
+        }
+      }
+      if (t == 0) dq0 = acc; else dq1 = acc;
+    }
+  }
+  if (qvalid) {
+    uint16_t* dqp = P.dq + b * P.dq_sb + (long)qrow * P.dq_ss + h * P.dq_sh;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const f32x16& acc = t == 0 ? dq0 : dq1;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        u16x4 pk = {f2bf(acc[4 * g] * P.scale), f2bf(acc[4 * g + 1] * P.scale), f2bf(acc[4 * g + 2] * P.scale),
+                    f2bf(acc[4 * g + 3] * P.scale)};
+        *reinterpret_cast<u16x4*>(dqp + 32 * t + 8 * g + 4 * hh) = pk;
+      }
+    }
+  }
 }
 
-constexpr int BWD_BK = 128;  // keys per workgroup (4 waves x 32)
-constexpr int BWD_BQ = 32;   // query rows per tile
-constexpr int QS_STRIDE = 72;  // [32 q][64 d] rows, bf16
-constexpr int QT_STRIDE = 36;  // [64 d][32 q] rows, bf16 (72 B)
-constexpr int KT_STRIDE = 40;  // [64 d][32 keys] rows per wave, bf16 (80 B)
-constexpr int DS_STRIDE = 40;  // [32 q][32 keys] rows per wave, bf16
-
+// ---- dK/dV kernel.  One workgroup = 128 keys (4 waves x 32, key on the lane); loop over 32-row query tiles.
+// S = Q K^T and dPd = dO V^T come out with the key on the MFMA column, so P and dS are directly the B
+// operands of dV^T += dO^T Pd and dK^T += Q^T dS (K and V of the wave's keys stay in registers).  The
+// relative-bias gradient (sum of dS along diagonals) goes through LDS float atomics, then one global
+// atomic per LUT entry per workgroup.  Needs delta from the dQ kernel.
 template <bool HAS_BIAS, bool HAS_KPM, bool CAUSAL, bool DROP>
-__global__ __launch_bounds__(256) void attn_bwd_kernel(AttnParams P) {
+__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint16_t* Qs = reinterpret_cast<uint16_t*>(smem);        // [32][72]
   uint16_t* dOs = Qs + BWD_BQ * QS_STRIDE;                   // [32][72]
   uint16_t* Qt = dOs + BWD_BQ * QS_STRIDE;                   // [64][36]
   uint16_t* dOt = Qt + D * QT_STRIDE;                        // [64][36]
-  uint16_t* Kt = dOt + D * QT_STRIDE;                        // [4 waves][64][40]
-  uint16_t* dSs = Kt + 4 * D * KT_STRIDE;                    // [4 waves][32][40]
-  float* dQs = reinterpret_cast<float*>(dSs + 4 * BWD_BQ * DS_STRIDE);  // [4][32][64]
-  float* lse_s = dQs + 4 * BWD_BQ * D;                       // [32]
+  float* lse_s = reinterpret_cast<float*>(dOt + D * QT_STRIDE);  // [32]
   float* del_s = lse_s + BWD_BQ;                             // [32]
   float* kmask = del_s + BWD_BQ;                             // [128]
   float* lut_s = kmask + BWD_BK;                             // [Sq + 128]
@@ -281,7 +449,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(AttnParams P) {
   const int h = bh % P.H, b = bh / P.H;
   const int k0 = kblk * BWD_BK;
   const int kw0 = k0 + w * 32;
-  const int key = kw0 + r;  // this lane's key column
+  const int key = kw0 + r;
   const bool kvalid = key < P.Sk;
   const int L = P.Sq + P.Sk - 1;
   const int win = P.Sq + BWD_BK;
@@ -300,23 +468,19 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(AttnParams P) {
     if (HAS_KPM && ok) ok = P.kpm[(long)b * P.Sk + kk] != 0;
     kmask[tid] = ok ? 0.f : -INFINITY;
   }
-  // K, V fragments of this wave's 32 keys (B operands of S = Q K^T and dPd = dO V^T), K^T image for dQ
   bf16x8v kf[4], vf[4];
   {
     const uint16_t* kp = P.k + b * P.k_sb + (long)key * P.k_ss + h * P.k_sh;
     const uint16_t* vp = P.v + b * P.v_sb + (long)key * P.v_ss + h * P.v_sh;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      u16x8 a = {0, 0, 0, 0, 0, 0, 0, 0}, c = {0, 0, 0, 0, 0, 0, 0, 0};
+      u16x8 a = {0, 0, 0, 0, 0, 0, 0, 0}, c = a;
       if (kvalid) {
         a = *reinterpret_cast<const u16x8*>(kp + 16 * s + 8 * hh);
         c = *reinterpret_cast<const u16x8*>(vp + 16 * s + 8 * hh);
       }
       kf[s] = as_frag(a);
       vf[s] = as_frag(c);
-      uint16_t* ktw = Kt + w * D * KT_STRIDE;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) ktw[(16 * s + 8 * hh + e) * KT_STRIDE + r] = a[e];
     }
   }
 
@@ -328,18 +492,18 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(AttnParams P) {
     qt_begin = qmin > 0 ? qmin / BWD_BQ : 0;
   }
   const int nqt = (P.Sq + BWD_BQ - 1) / BWD_BQ;
-  const float* lse_row = P.lse + (long)(b * P.H + h) * P.Sq;
-  const float* del_row = P.delta + (long)(b * P.H + h) * P.Sq;
-  const long drop_base = (long)(b * P.H + h) * P.Sq;
+  const long bh_rows = (long)(b * P.H + h) * P.Sq;
+  const float* lse_row = P.lse + bh_rows;
+  const float* del_row = P.delta + bh_rows;
+  const long sk2 = (P.Sk + 1) & ~1;
 
   for (int qt = qt_begin; qt < nqt; ++qt) {
     const int q0 = qt * BWD_BQ;
     __syncthreads();
-    // ---- stage Q, dO (row-major and transposed), lse, delta
     {
-      const int qq = tid >> 3, ch = tid & 7;  // 32 rows x 8 chunks
+      const int qq = tid >> 3, ch = tid & 7;
       const int qg = q0 + qq;
-      u16x8 a = {0, 0, 0, 0, 0, 0, 0, 0}, c = {0, 0, 0, 0, 0, 0, 0, 0};
+      u16x8 a = {0, 0, 0, 0, 0, 0, 0, 0}, c = a;
       if (qg < P.Sq) {
         a = *reinterpret_cast<const u16x8*>(P.q + b * P.q_sb + (long)qg * P.q_ss + h * P.q_sh + ch * 8);
         c = *reinterpret_cast<const u16x8*>(P.dout + b * P.do_sb + (long)qg * P.do_ss + h * P.do_sh + ch * 8);
@@ -359,7 +523,6 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(AttnParams P) {
     }
     __syncthreads();
 
-    // ---- S = Q K^T, dPd = dO V^T   (C layout: row q = crow(i,hh), column key = r)
     f32x16 sacc = {}, dpacc = {};
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
@@ -368,7 +531,6 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(AttnParams P) {
       sacc = mfma32(qa, kf[s], sacc);
       dpacc = mfma32(da, vf[s], dpacc);
     }
-    // ---- P, Pd, dS
     f32x16 pd, ds;
     const float km = kmask[w * 32 + r];
 #pragma unroll
@@ -384,19 +546,30 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(AttnParams P) {
       if (CAUSAL && key > qg + P.causal_off) sv = -INFINITY;
       const float pr = exp2f((sv - lse_s[ql]) * LOG2E);  // lse = +inf for q >= Sq -> 0
       float keepf = 1.f;
-      if (DROP) keepf = (mix32(P.seed, (uint32_t)((drop_base + qg) * P.Sk + key)) >= P.thr) ? dscale : 0.f;
+      if (DROP) keepf = keep_one(P.seed, P.thr, (uint32_t)((bh_rows + qg) * sk2 + key)) ? dscale : 0.f;
       pd[i] = pr * keepf;
-      const float dp = dpacc[i] * keepf;
-      ds[i] = pr * (dp - del_s[ql]);
+      ds[i] = pr * (dpacc[i] * keepf - del_s[ql]);
     }
     if (HAS_BIAS) {
+      // Diagonal sums of this wave's 32x32 dS tile without per-element atomics: rotate register i
+      // (tile row rho = crow(i, hh)) left by rho lanes so lane r receives element (rho, (r + rho) & 31),
+      // whose diagonal (col - row) is r (no wrap) or r - 32 (wrapped).  Masked / out-of-range
+      // elements are exactly 0 (P = 0), so no guards are needed.
+      float pos = 0.f, neg = 0.f;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const int qg = q0 + crow(i, hh);
-        if (qg < P.Sq && kvalid) atomicAdd(&dlut_s[key - qg + P.Sq - 1 - k0], ds[i]);
+        const int rho = crow(i, hh);
+        const float v = __shfl(ds[i], ((r + rho) & 31) + 32 * hh, 64);
+        if (r + rho < 32) pos += v; else neg += v;
+      }
+      pos += __shfl_xor(pos, 32, 64);
+      neg += __shfl_xor(neg, 32, 64);
+      if (hh == 0) {
+        const int li = w * 32 + r - q0 + P.Sq - 1;  // LUT index (window-local) of diagonal r
+        atomicAdd(&dlut_s[li], pos);
+        if (li >= 32) atomicAdd(&dlut_s[li - 32], neg);
       }
     }
-    // ---- dV^T += dO^T Pd ; dK^T += Q^T dS   (A from transposed LDS images, B = accumulators)
     const bf16x8v pf0 = pack8(pd, 0), pf1 = pack8(pd, 8), sf0 = pack8(ds, 0), sf1 = pack8(ds, 8);
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
@@ -418,42 +591,8 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(AttnParams P) {
       }
       if (t == 0) { dv0 = av; dk0 = ak; } else { dv1 = av; dk1 = ak; }
     }
-    // ---- dQ partial = dS K  (dS through this wave's LDS tile, K^T image as B)
-    uint16_t* dsw = dSs + w * BWD_BQ * DS_STRIDE;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) dsw[crow(i, hh) * DS_STRIDE + r] = f2bf(ds[i]);
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes visible to its reads
-    __builtin_amdgcn_wave_barrier();
-    f32x16 q0acc = {}, q1acc = {};
-    const uint16_t* ktw = Kt + w * D * KT_STRIDE;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      bf16x8v a = as_frag(*reinterpret_cast<const u16x8*>(dsw + r * DS_STRIDE + 16 * s + 8 * hh));
-      bf16x8v b0 = as_frag(*reinterpret_cast<const u16x8*>(ktw + r * KT_STRIDE + 16 * s + 8 * hh));
-      bf16x8v b1 = as_frag(*reinterpret_cast<const u16x8*>(ktw + (32 + r) * KT_STRIDE + 16 * s + 8 * hh));
-      q0acc = mfma32(a, b0, q0acc);
-      q1acc = mfma32(a, b1, q1acc);
-    }
-    // dQ partial C layout: row q = crow(i,hh), column d = 32t + r
-    float* dqw = dQs + w * BWD_BQ * D;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      dqw[crow(i, hh) * D + r] = q0acc[i];
-      dqw[crow(i, hh) * D + 32 + r] = q1acc[i];
-    }
-    __syncthreads();
-    // sum the 4 wave partials; fp32 atomics, 256 contiguous bytes per wave-instruction
-#pragma unroll
-    for (int it = 0; it < (BWD_BQ * D) / 256; ++it) {
-      const int e = it * 256 + tid;
-      const int ql = e >> 6, dd = e & 63;
-      const int qg = q0 + ql;
-      const float v = dQs[e] + dQs[BWD_BQ * D + e] + dQs[2 * BWD_BQ * D + e] + dQs[3 * BWD_BQ * D + e];
-      if (qg < P.Sq) atomicAdd(P.dq_acc + (((long)b * P.Sq + qg) * P.H + h) * D + dd, v);
-    }
   }
 
-  // ---- store dK (scaled), dV:  C layout row d = 32t + crow(i,hh), column key = r
   if (kvalid) {
     uint16_t* dkp = P.dk + b * P.dk_sb + (long)key * P.dk_ss + h * P.dk_sh;
     uint16_t* dvp = P.dv + b * P.dv_sb + (long)key * P.dv_ss + h * P.dv_sh;
@@ -482,23 +621,6 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(AttnParams P) {
   }
 }
 
-// dq (bf16, strided [B,Sq,H,D]) = scale * dq_acc (fp32 contiguous [B,Sq,H,D])
-__global__ __launch_bounds__(256) void attn_dq_convert_kernel(const float* __restrict__ acc, uint16_t* __restrict__ dq,
-                                                              long n4, int Sq, int H, long sb, long ss, long sh,
-                                                              float scale) {
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
-    const int dc = (int)(i % (D / 4));
-    long t = i / (D / 4);
-    const int h = (int)(t % H);
-    t /= H;
-    const int q = (int)(t % Sq);
-    const long b = t / Sq;
-    f32x4 v = *reinterpret_cast<const f32x4*>(acc + i * 4) * scale;
-    u16x4 o = {f2bf(v.x), f2bf(v.y), f2bf(v.z), f2bf(v.w)};
-    *reinterpret_cast<u16x4*>(dq + b * sb + (long)q * ss + h * sh + dc * 4) = o;
-  }
-}
-
 #define DISPATCH4(FN, hb, hk, ca, dr, ...)                                              \
   do {                                                                                  \
     if (hb) {                                                                           \
@@ -519,8 +641,12 @@ void launch_fwd_t(const AttnParams& p, int nblk, size_t lds, hipStream_t st) {
   hipLaunchKernelGGL((attn_fwd_kernel<HB, HK, CA, DR>), dim3(nblk), dim3(256), lds, st, p);
 }
 template <bool HB, bool HK, bool CA, bool DR>
-void launch_bwd_t(const AttnParams& p, int nblk, size_t lds, hipStream_t st) {
-  hipLaunchKernelGGL((attn_bwd_kernel<HB, HK, CA, DR>), dim3(nblk), dim3(256), lds, st, p);
+void launch_bwd_dq_t(const AttnParams& p, int nblk, size_t lds, hipStream_t st) {
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<HB, HK, CA, DR>), dim3(nblk), dim3(256), lds, st, p);
+}
+template <bool HB, bool HK, bool CA, bool DR>
+void launch_bwd_dkdv_t(const AttnParams& p, int nblk, size_t lds, hipStream_t st) {
+  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<HB, HK, CA, DR>), dim3(nblk), dim3(256), lds, st, p);
 }
 
 }  // namespace
@@ -542,28 +668,23 @@ extern "C" int dllm_attn_fwd(AttnParams* pp, hipStream_t st) {
 extern "C" int dllm_attn_bwd(AttnParams* pp, hipStream_t st) {
   AttnParams p = *pp;
   p.thr = drop_threshold(p.p_drop);
-  // delta
-  const long rows = (long)p.B * p.H * p.Sq;
-  hipLaunchKernelGGL(attn_bwd_delta_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, p);
-  p.n_tiles = (p.Sk + BWD_BK - 1) / BWD_BK;
-  const long nblk = (long)p.n_tiles * p.H * p.B;
-  size_t lds = (size_t)2 * BWD_BQ * QS_STRIDE * 2 + (size_t)2 * D * QT_STRIDE * 2 + (size_t)4 * D * KT_STRIDE * 2 +
-               (size_t)4 * BWD_BQ * DS_STRIDE * 2 + (size_t)4 * BWD_BQ * D * 4 + 2 * BWD_BQ * 4 + BWD_BK * 4;
-  if (p.lut) lds += (size_t)2 * (p.Sq + BWD_BK) * 4;
-  if (lds > 160 * 1024) return -4;
-  DISPATCH4(launch_bwd_t, p.lut != nullptr, p.kpm != nullptr, p.causal != 0, p.p_drop > 0.f, p, (int)nblk, lds, st);
+  // 1) dQ (+ delta): query blocks, same geometry as the forward
+  p.n_tiles = (p.Sq + FWD_BM - 1) / FWD_BM;
+  long nblk = (long)p.n_tiles * p.H * p.B;
+  size_t lds = (size_t)2 * FWD_BN * KS_STRIDE * 2 + (size_t)D * VT_STRIDE * 2 + FWD_BN * 4;
+  if (p.lut) lds += (size_t)(p.Sk + FWD_BM + FWD_BN) * 4;
+  if (nblk <= 0 || nblk > 0x7fffffff || lds > 160 * 1024) return -4;
+  DISPATCH4(launch_bwd_dq_t, p.lut != nullptr, p.kpm != nullptr, p.causal != 0, p.p_drop > 0.f, p, (int)nblk, lds,
+            st);
   DLLM_CHECK_LAUNCH();
-  return 0;
-}
-
-extern "C" int dllm_attn_dq_convert(const float* acc, void* dq, int B, int Sq, int H, long sb, long ss, long sh,
-                                    float scale, hipStream_t st) {
-  const long n4 = (long)B * Sq * H * (D / 4);
-  long g = (n4 + 255) / 256;
-  if (g > 8192) g = 8192;
-  if (g < 1) g = 1;
-  hipLaunchKernelGGL(attn_dq_convert_kernel, dim3((int)g), dim3(256), 0, st, acc, (uint16_t*)dq, n4, Sq, H, sb, ss,
-                     sh, scale);
+  // 2) dK, dV (+ bias-LUT gradient): key blocks
+  p.n_tiles = (p.Sk + BWD_BK - 1) / BWD_BK;
+  nblk = (long)p.n_tiles * p.H * p.B;
+  lds = (size_t)2 * BWD_BQ * QS_STRIDE * 2 + (size_t)2 * D * QT_STRIDE * 2 + 2 * BWD_BQ * 4 + BWD_BK * 4;
+  if (p.lut) lds += (size_t)2 * (p.Sq + BWD_BK) * 4;
+  if (nblk <= 0 || nblk > 0x7fffffff || lds > 160 * 1024) return -4;
+  DISPATCH4(launch_bwd_dkdv_t, p.lut != nullptr, p.kpm != nullptr, p.causal != 0, p.p_drop > 0.f, p, (int)nblk, lds,
+            st);
   DLLM_CHECK_LAUNCH();
   return 0;
 }

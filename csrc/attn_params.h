@@ -10,8 +10,8 @@ struct AttnParams {
   const uint16_t* dout;
   uint16_t* o_out;
   float* lse;          // [B, H, Sq]
-  const float* delta;  // [B, H, Sq] (bwd)
-  float* dq_acc;       // [B, Sq, H, D] fp32 (bwd)
+  float* delta;        // [B, H, Sq] (bwd, written by the dQ kernel)
+  uint16_t* dq;        // [B, Sq, H, D] strided (bwd)
   uint16_t* dk;        // [B, Sk, H, D]
   uint16_t* dv;
   float* dlut;         // [H, Sq + Sk - 1] fp32 (bwd)
@@ -22,6 +22,7 @@ struct AttnParams {
   long v_sb, v_ss, v_sh;
   long o_sb, o_ss, o_sh;
   long do_sb, do_ss, do_sh;
+  long dq_sb, dq_ss, dq_sh;
   long dk_sb, dk_ss, dk_sh;
   long dv_sb, dv_ss, dv_sh;
   int B, H, Sq, Sk;

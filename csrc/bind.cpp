@@ -25,7 +25,6 @@ int dllm_adamw(void*, float*, const void*, float*, float*, const uint8_t*, const
                float, float, float, float, int, hipStream_t);
 int dllm_attn_fwd(AttnParams*, hipStream_t);
 int dllm_attn_bwd(AttnParams*, hipStream_t);
-int dllm_attn_dq_convert(const float*, void*, int, int, int, long, long, long, float, hipStream_t);
 int dllm_attn_params_size();
 }
 
@@ -310,7 +309,6 @@ std::vector<Tensor> attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& 
   TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.numel() == (int64_t)P.B * P.H * P.Sq && lse.is_contiguous(),
               "lse mismatch");
   auto f32 = q.options().dtype(at::kFloat);
-  auto dq_acc = at::zeros({P.B, P.Sq, P.H, 64}, f32);
   // outputs may be caller-provided strided views (e.g. slices of one packed d(qkv) buffer)
   auto pick = [&](const optional<Tensor>& t, int64_t S, const char* n) {
     if (t.has_value() && t->defined()) {
@@ -331,16 +329,14 @@ std::vector<Tensor> attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& 
   P.do_sb = dout.stride(0); P.do_ss = dout.stride(1); P.do_sh = dout.stride(2);
   P.lse = lse.data_ptr<float>();
   P.delta = delta.data_ptr<float>();
-  P.dq_acc = dq_acc.data_ptr<float>();
+  P.dq = reinterpret_cast<uint16_t*>(dq.data_ptr());
+  P.dq_sb = dq.stride(0); P.dq_ss = dq.stride(1); P.dq_sh = dq.stride(2);
   P.dk = reinterpret_cast<uint16_t*>(dk.data_ptr());
   P.dk_sb = dk.stride(0); P.dk_ss = dk.stride(1); P.dk_sh = dk.stride(2);
   P.dv = reinterpret_cast<uint16_t*>(dv.data_ptr());
   P.dv_sb = dv.stride(0); P.dv_ss = dv.stride(1); P.dv_sh = dv.stride(2);
   P.dlut = dlut.defined() ? dlut.data_ptr<float>() : nullptr;
   check_rc(dllm_attn_bwd(&P, stream()), "attn_bwd");
-  check_rc(dllm_attn_dq_convert(dq_acc.data_ptr<float>(), dq.data_ptr(), P.B, P.Sq, P.H, dq.stride(0), dq.stride(1),
-                                dq.stride(2), (float)scale, stream()),
-           "attn_dq_convert");
   return {dq, dk, dv, need_dlut ? dlut : Tensor()};
 }
 

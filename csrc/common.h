@@ -67,9 +67,33 @@ DLLM_HOST_DEVICE uint32_t mix32(uint32_t seed, uint32_t idx) {
   return x;
 }
 
+// 16-bit threshold: element e is kept iff half (e & 1) of mix32(seed, e >> 1) >= thr16.
 inline uint32_t drop_threshold(float p) {
-  double t = (double)p * 4294967296.0;
-  return t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
+  double t = (double)p * 65536.0;
+  return t >= 65535.0 ? 0xFFFFu : (uint32_t)t;
+}
+
+DLLM_DEVICE bool keep_one(uint32_t seed, uint32_t thr16, uint32_t e) {
+  const uint32_t h = mix32(seed, e >> 1);
+  return ((e & 1u) ? (h >> 16) : (h & 0xFFFFu)) >= thr16;
+}
+
+// e_even must be even: decisions for elements e_even and e_even + 1 from one hash
+DLLM_DEVICE void keep_two(uint32_t seed, uint32_t thr16, uint32_t e_even, bool& k0, bool& k1) {
+  const uint32_t h = mix32(seed, e_even >> 1);
+  k0 = (h & 0xFFFFu) >= thr16;
+  k1 = (h >> 16) >= thr16;
+}
+
+// v[k] (elements e4 .. e4+3, e4 even) -> dropped or scaled
+DLLM_DEVICE void dropout4(f32x4& v, uint32_t seed, uint32_t thr16, uint32_t e4, float scale) {
+  bool k0, k1, k2, k3;
+  keep_two(seed, thr16, e4, k0, k1);
+  keep_two(seed, thr16, e4 + 2u, k2, k3);
+  v.x = k0 ? v.x * scale : 0.f;
+  v.y = k1 ? v.y * scale : 0.f;
+  v.z = k2 ? v.z * scale : 0.f;
+  v.w = k3 ? v.w * scale : 0.f;
 }
 
 // ---- wave64 reductions -------------------------------------------------------------------------

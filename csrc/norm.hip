@@ -6,7 +6,7 @@
 //       out = norm(s) * w (+ b)            [RMS: T5 (fp32 variance, weight only); LN: BART]
 // bwd:  ds = norm_bwd(dout) + ds_extra     [ds_extra = gradient of the stream from later layers]
 //       dx = dropout_bwd(ds);  dstream = ds (optional);  dw/db via per-block column partials.
-// The dropout keep-decision is mix32(seed, row*d + col) >= threshold (common.h / ops/rng.py).
+// Dropout keep-decision for element row*d + col: common.h dropout4 / ops/rng.py keep_mask.
 #include "common.h"
 
 using namespace dllm;
@@ -34,13 +34,7 @@ __global__ __launch_bounds__(256) void norm_fwd_kernel(const T* __restrict__ x, 
     v[c] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (col < d) {
       f32x4 xv = Elem<T>::load4(x + base + col);
-      if (drop) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const bool keep = mix32(seed, (uint32_t)(base + col + k)) >= thr;
-          xv[k] = keep ? xv[k] * dscale : 0.f;
-        }
-      }
+      if (drop) dropout4(xv, seed, thr, (uint32_t)(base + col), dscale);
       if (resid != nullptr) {
         f32x4 rv = Elem<T>::load4(resid + base + col);
         xv += rv;
@@ -131,13 +125,7 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(const T* __restrict__ dou
         f32x4 dsv = (g[c] - s1 - xh[c] * s2) * rstd;
         if (ds_extra != nullptr) dsv += Elem<T>::load4(ds_extra + base + col);
         if (dstream != nullptr) Elem<T>::store4(dstream + base + col, dsv);
-        if (drop) {
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const bool keep = mix32(seed, (uint32_t)(base + col + k)) >= thr;
-            dsv[k] = keep ? dsv[k] * dscale : 0.f;
-          }
-        }
+        if (drop) dropout4(dsv, seed, thr, (uint32_t)(base + col), dscale);
         Elem<T>::store4(dx + base + col, dsv);
       }
     }
@@ -156,13 +144,23 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(const T* __restrict__ dou
   }
 }
 
+// out[col] += sum over a chunk of partial rows; grid (ceil(d/64), row-chunks), 4 waves split the chunk,
+// lane = column (256-B coalesced rows), LDS combine, one fp32 atomic per column per block (out pre-zeroed).
+constexpr int kColChunks = 16;
 __global__ __launch_bounds__(256) void col_sum_kernel(const float* __restrict__ part, float* __restrict__ out, int G,
                                                       int d) {
-  const int col = blockIdx.x * 256 + threadIdx.x;
-  if (col >= d) return;
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + lane;
+  const int per = (G + gridDim.y - 1) / gridDim.y;
+  const int g0 = blockIdx.y * per;
+  const int g1 = g0 + per < G ? g0 + per : G;
   float acc = 0.f;
-  for (int g = 0; g < G; ++g) acc += part[(size_t)g * d + col];
-  out[col] = acc;
+  if (col < d)
+    for (int g = g0 + w; g < g1; g += 4) acc += part[(size_t)g * d + col];
+  red[w][lane] = acc;
+  __syncthreads();
+  if (w == 0 && col < d) atomicAdd(out + col, red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane]);
 }
 
 template <typename T, int KIND>
@@ -203,8 +201,9 @@ int launch_bwd(const void* dout, const void* ds_extra, const void* s, const void
   else return -1;
 #undef L
   DLLM_CHECK_LAUNCH();
-  hipLaunchKernelGGL(col_sum_kernel, dim3((d + 255) / 256), dim3(256), 0, st, dw_part, dw, G, d);
-  if (db_part != nullptr) hipLaunchKernelGGL(col_sum_kernel, dim3((d + 255) / 256), dim3(256), 0, st, db_part, db, G, d);
+  const dim3 cg((d + 63) / 64, kColChunks);
+  hipLaunchKernelGGL(col_sum_kernel, cg, dim3(256), 0, st, dw_part, dw, G, d);
+  if (db_part != nullptr) hipLaunchKernelGGL(col_sum_kernel, cg, dim3(256), 0, st, db_part, db, G, d);
   DLLM_CHECK_LAUNCH();
   return 0;
 }

@@ -17,7 +17,7 @@ One op covers every attention variant the reference's models run (SURVEY.md §2.
 Layout: q ``[B, Sq, H, D]``, k/v ``[B, Sk, H, D]`` — the natural output of the fused QKV GEMM
 viewed without any transpose copy (only the last dim must be contiguous).  Output ``[B, Sq, H, D]``.
 
-Kernels: csrc/attn_fwd.hip, csrc/attn_bwd.hip.
+Kernels: csrc/attn.hip (forward; backward = dQ kernel + dK/dV kernel, no atomics except the bias LUT).
 """
 from __future__ import annotations
 
@@ -26,7 +26,7 @@ import math
 import torch
 
 from .. import _ext
-from .rng import mix32, threshold
+from .rng import attention_keep_mask
 
 # --------------------------------------------------------------------------- T5 relative bias
 
@@ -91,8 +91,7 @@ def _reference(q, k, v, scale, causal, kpm, lut, p, seed):
         s = s.masked_fill(cm, neg)
     pr = torch.softmax(s, dim=-1)
     if p > 0.0:
-        idx = torch.arange(B * H * Sq * Sk, device=q.device, dtype=torch.int64).view(B, H, Sq, Sk)
-        keep = mix32(seed, idx) >= threshold(p)
+        keep = attention_keep_mask(seed, p, B, H, Sq, Sk, q.device)
         pr = pr * keep.to(pr.dtype) * (1.0 / (1.0 - p))
     o = torch.matmul(pr, vf)
     return o.permute(0, 2, 1, 3).to(q.dtype)

@@ -1,7 +1,9 @@
 """Counter-based dropout RNG shared by the HIP kernels and the torch reference path.
 
 Every dropout site gets a 32-bit ``seed`` from :class:`DropoutRNG`; element ``i`` of the tensor is
-kept iff ``mix32(seed, i) >= threshold(p)``.  Because the decision is a pure function of
+kept iff the 16-bit half ``i & 1`` of ``mix32(seed, i >> 1)`` is ``>= threshold16(p)`` — one hash
+serves two adjacent elements (half the VALU cost inside the attention / norm kernels; p is quantised
+to 1/65536).  Because the decision is a pure function of
 (seed, index), backward kernels regenerate the mask instead of storing it (no mask tensors in HBM),
 and the reference implementation below reproduces the kernels' masks bit-for-bit so numerics tests
 can run with p > 0.  Mirrors csrc/common.h ``dllm_mix32``.
@@ -27,8 +29,15 @@ def mix32(seed: int, idx: torch.Tensor) -> torch.Tensor:
     return x
 
 
-def threshold(p: float) -> int:
-    return min(int(p * 4294967296.0), 0xFFFFFFFF)
+def threshold16(p: float) -> int:
+    return min(int(p * 65536.0), 0xFFFF)
+
+
+def keep_from_index(seed: int, p: float, idx: torch.Tensor) -> torch.Tensor:
+    """Keep decision for element indices ``idx`` (any shape, int64)."""
+    h = mix32(seed, idx >> 1)
+    half = torch.where((idx & 1) == 1, h >> 16, h & 0xFFFF)
+    return half >= threshold16(p)
 
 
 def keep_mask(seed: int, p: float, shape, device, numel_offset: int = 0) -> torch.Tensor:
@@ -37,7 +46,17 @@ def keep_mask(seed: int, p: float, shape, device, numel_offset: int = 0) -> torc
     for s in shape:
         n *= s
     idx = torch.arange(numel_offset, numel_offset + n, device=device, dtype=torch.int64)
-    return (mix32(seed, idx) >= threshold(p)).view(shape)
+    return keep_from_index(seed, p, idx).view(shape)
+
+
+def attention_keep_mask(seed: int, p: float, B: int, H: int, Sq: int, Sk: int, device) -> torch.Tensor:
+    """Attention-probability mask [B, H, Sq, Sk]: element (b, h, i, j) uses index
+    ``((b*H + h)*Sq + i) * Sk2 + j`` with ``Sk2 = Sk`` rounded up to even, so keys (2m, 2m+1) of a
+    row share one hash in the kernels."""
+    sk2 = (Sk + 1) & ~1
+    rows = torch.arange(B * H * Sq, device=device, dtype=torch.int64).view(B, H, Sq, 1)
+    idx = rows * sk2 + torch.arange(Sk, device=device, dtype=torch.int64).view(1, 1, 1, Sk)
+    return keep_from_index(seed, p, idx)
 
 
 def mix_host(seed: int, idx: int) -> int:

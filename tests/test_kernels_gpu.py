@@ -204,7 +204,7 @@ def test_attention(B, H, Sq, Sk, bias, kpm, causal, p, scale):
     for name, a_, b_ in (("dq", qs.grad, qr.grad), ("dk", ks.grad, kr.grad), ("dv", vs.grad, vr.grad)):
         assert _rel(a_, b_) < tol, (name, _rel(a_, b_))
     if bias:
-        assert _rel(tab1.grad, tab2.grad) < 3e-2, _rel(tab1.grad, tab2.grad)
+        assert _rel(tab1.grad, tab2.grad) < tol, _rel(tab1.grad, tab2.grad)
 
 
 def test_attention_packed_qkv_grad():

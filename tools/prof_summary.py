@@ -1,0 +1,35 @@
+"""Summarise a rocprofv3 --stats kernel CSV: per-step time by kernel (and grouped families)."""
+import csv
+import re
+import sys
+from collections import defaultdict
+
+
+def family(name):
+    if name.startswith("Cijk") or name.startswith("Custom_Cijk"):
+        return "GEMM (hipBLASLt)"
+    m = re.search(r"(attn_\w+|norm_\w+|act_\w+|ce_\w+|adamw\w*|col_sum\w*|sq_norm\w*|dropout\w*|sum_partials)", name)
+    if m:
+        return m.group(1)
+    m = re.search(r"at::native::(\w+)", name)
+    return "torch:" + (m.group(1) if m else name[:40])
+
+
+def main(path, steps):
+    rows = list(csv.DictReader(open(path)))
+    tot = sum(float(r["TotalDurationNs"]) for r in rows)
+    fam = defaultdict(float)
+    for r in rows:
+        fam[family(r["Name"])] += float(r["TotalDurationNs"])
+    print(f"total GPU kernel time {tot/1e6:.1f} ms over {steps} steps = {tot/steps/1e6:.2f} ms/step")
+    print("--- by family (ms/step, %)")
+    for k, v in sorted(fam.items(), key=lambda kv: -kv[1]):
+        print(f"{v/steps/1e6:9.2f}  {100*v/tot:5.1f}%  {k}")
+    print("--- top kernels")
+    for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:25]:
+        print(f"{float(r['TotalDurationNs'])/steps/1e6:9.2f} ms/step  calls/step {int(r['Calls'])/steps:6.1f}  "
+              f"avg {float(r['AverageNs'])/1e3:8.1f} us  {r['Name'][:100]}")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], float(sys.argv[2]) if len(sys.argv) > 2 else 1.0)
