@@ -1,0 +1,88 @@
+"""Shared command-line surface of the three entry points.
+
+The six flags of the reference are kept verbatim (ref/train-torchrun.py:183-188,
+ref/train-accelerator.py:320-325, ref/train-task.py:411-416); everything else is optional and
+defaults to reference semantics.  Data comes from the Valohai ``dataset``
+input (``train.json``/``val.json``), or ``--data-dir``, or ``--synthetic N`` (offline runs).
+"""
+from __future__ import annotations
+
+import argparse
+import os
+
+from .data.dataset import convert_examples_to_features, load_samsum, synthetic_samsum_records
+from .data.tokenization import load_tokenizer
+from .models.config import resolve_config
+from .platform import valohai
+
+
+def base_parser(description: str, defaults: dict | None = None) -> argparse.ArgumentParser:
+    d = {"batch_size": 1, "num_epochs": 1, "warmup_steps": 500, "evaluation_steps": 500}
+    d.update(defaults or {})
+    ap = argparse.ArgumentParser(description=description)
+    ap.add_argument("--model-ckpt", type=str, default="facebook/bart-large-cnn", help="Pretrained model checkpoint")
+    ap.add_argument("--output-dir", type=str, default="bart-large-cnn", help="Output directory for the trained model")
+    ap.add_argument("--batch-size", type=int, default=d["batch_size"], help="Batch size")
+    ap.add_argument("--num-epochs", type=int, default=d["num_epochs"], help="Number of training epochs")
+    ap.add_argument("--warmup-steps", type=int, default=d["warmup_steps"], help="Warmup steps")
+    ap.add_argument("--evaluation-steps", type=int, default=d["evaluation_steps"], help="Evaluation steps")
+    g = ap.add_argument_group("MI355X framework options (defaults reproduce the reference)")
+    g.add_argument("--data-dir", type=str, default=None, help="directory with train.json/val.json")
+    g.add_argument("--synthetic", type=int, default=0, help="use N synthetic SAMSum-schema records")
+    g.add_argument("--max-source-length", type=int, default=1024)
+    g.add_argument("--max-target-length", type=int, default=128)
+    g.add_argument("--ignore-pad-labels", action="store_true", help="mask pad tokens out of the loss")
+    g.add_argument("--precision", choices=["bf16", "fp32"], default=None, help="default: bf16 on GPU, fp32 on CPU")
+    g.add_argument("--grad-accum", type=int, default=None)
+    g.add_argument("--learning-rate", type=float, default=5e-5)
+    g.add_argument("--max-steps", type=int, default=-1)
+    g.add_argument("--bucket-mb", type=float, default=None, help="gradient all-reduce bucket size (MiB)")
+    g.add_argument("--no-overlap", action="store_true", help="all-reduce after backward instead of overlapping")
+    g.add_argument("--eval-batch-size", type=int, default=None)
+    g.add_argument("--max-eval-samples", type=int, default=None)
+    g.add_argument("--gen-max-length", type=int, default=128)
+    g.add_argument("--num-beams", type=int, default=2)
+    g.add_argument("--resume-from", type=str, default=None, help="checkpoint dir, or 'latest'")
+    g.add_argument("--seed", type=int, default=42)
+    g.add_argument("--model-overrides", type=str, default=None,
+                   help="comma list key=value applied to the model config (e.g. num_layers=2)")
+    return ap
+
+
+def apply_overrides(cfg, spec: str | None):
+    if not spec:
+        return cfg
+    kv = {}
+    for item in spec.split(","):
+        k, v = item.split("=")
+        cur = getattr(cfg, k)
+        kv[k] = type(cur)(v) if not isinstance(cur, bool) else v.lower() in ("1", "true", "yes")
+    if "num_layers" in kv and "num_decoder_layers" not in kv:
+        kv["num_decoder_layers"] = kv["num_layers"]
+    return cfg.replace(**kv)
+
+
+def load_records(args):
+    if args.synthetic:
+        n = args.synthetic
+        return {"train": synthetic_samsum_records(n, args.seed), "validation": synthetic_samsum_records(max(4, n // 4),
+                                                                                                    args.seed + 1)}
+    data_dir = args.data_dir or os.path.dirname(valohai.inputs("dataset").path())
+    return load_samsum(data_dir)
+
+
+def build_data(args, cfg):
+    """(tokenizer, train_features, eval_features, eval_records) following convert_examples_to_features."""
+    recs = load_records(args)
+    tok = load_tokenizer(args.model_ckpt, cfg, texts=[r["dialogue"] for r in recs["train"]] +
+                         [r["summary"] for r in recs["train"]])
+    tr = convert_examples_to_features(recs["train"], tok, args.max_source_length, args.max_target_length,
+                                      ignore_pad_labels=args.ignore_pad_labels)
+    ev_recs = recs["validation"][: args.max_eval_samples] if args.max_eval_samples else recs["validation"]
+    ev = convert_examples_to_features(ev_recs, tok, args.max_source_length, args.max_target_length,
+                                      ignore_pad_labels=args.ignore_pad_labels)
+    return tok, tr, ev
+
+
+def model_config(args):
+    return apply_overrides(resolve_config(args.model_ckpt), args.model_overrides)

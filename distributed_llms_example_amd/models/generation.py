@@ -1,0 +1,209 @@
+"""Autoregressive generation for the seq2seq models: greedy and beam search with a KV cache.
+
+The reference evaluates with ``unwrap_model(model).generate(input_ids, attention_mask=...,
+max_length=128, num_beams=2)`` (ref/train-accelerator.py:239-249, ref/train-task.py:310-313), i.e.
+transformers' GenerationMixin beam search (generation/utils.py:3208): encode once, expand to
+``batch × num_beams``, per step fp32 ``log_softmax`` + logits processors, top-``2·num_beams``
+candidates over ``num_beams × V``, finished hypotheses scored ``sum_logprobs / len**length_penalty``,
+``early_stopping`` rules, cache reordering.  Processors implemented: ``min_length``,
+``no_repeat_ngram_size``, ``forced_bos_token_id``, ``forced_eos_token_id`` (bart-large-cnn's
+generation_config uses all of them).
+
+MI355X specifics: the decoder self-attention cache is preallocated ``[B, max_len, H, D]`` (no
+per-step concatenation; the attention kernel reads the strided prefix view), cross-attention K/V are
+projected once per generate call, and every decode step runs the same fused kernels as training
+(attention with the bias LUT offset by the cache length).
+"""
+from __future__ import annotations
+
+import torch
+
+from ..ops.attention import relative_bias_lut  # noqa: F401  (documented dependency)
+
+
+class KVCache:
+    """Preallocated self-attention K/V for one decoder layer."""
+
+    def __init__(self, batch: int, max_len: int, heads: int, dim: int, dtype, device):
+        self.k = torch.empty(batch, max_len, heads, dim, dtype=dtype, device=device)
+        self.v = torch.empty(batch, max_len, heads, dim, dtype=dtype, device=device)
+        self.len = 0
+
+    def append(self, k, v):
+        s = k.shape[1]
+        self.k[:, self.len:self.len + s] = k
+        self.v[:, self.len:self.len + s] = v
+        self.len += s
+        return self.k[:, :self.len], self.v[:, :self.len]
+
+    def reorder(self, idx):
+        self.k = self.k.index_select(0, idx)
+        self.v = self.v.index_select(0, idx)
+
+
+def _head_geom(model):
+    cfg = model.config
+    if cfg.model_type == "t5":
+        return cfg.num_heads, cfg.d_kv
+    return cfg.num_heads, cfg.d_model // cfg.num_heads
+
+
+def _apply_processors(logp, seqs, cur_len, cfg, min_length, no_repeat_ngram_size, forced_bos, forced_eos,
+                      max_length, eos):
+    V = logp.shape[-1]
+    if min_length is not None and cur_len < min_length and eos is not None:
+        logp[:, eos] = -float("inf")
+    if forced_bos is not None and cur_len == 1:
+        logp[:] = -float("inf")
+        logp[:, forced_bos] = 0.0
+    if forced_eos is not None and cur_len == max_length - 1:
+        logp[:] = -float("inf")
+        logp[:, forced_eos] = 0.0
+    n = no_repeat_ngram_size or 0
+    if n > 0 and cur_len + 1 >= n:
+        rows = seqs.tolist()
+        for b, row in enumerate(rows):
+            prefix = tuple(row[cur_len - n + 1:cur_len]) if n > 1 else ()
+            banned = set()
+            for i in range(cur_len - n + 1):
+                if tuple(row[i:i + n - 1]) == prefix:
+                    banned.add(row[i + n - 1])
+            if banned:
+                logp[b, [t for t in banned if t < V]] = -float("inf")
+    return logp
+
+
+@torch.no_grad()
+def generate(model, input_ids, attention_mask=None, max_length: int | None = None, num_beams: int | None = None,
+             min_length: int | None = None, length_penalty: float | None = None, no_repeat_ngram_size=None,
+             early_stopping=None, forced_bos_token_id=None, forced_eos_token_id=None, max_new_tokens=None,
+             **_unused):
+    cfg = model.config
+    gen = dict(cfg.generation)
+    max_length = max_length if max_length is not None else gen.get("max_length", 20)
+    if max_new_tokens is not None:
+        max_length = max_new_tokens + 1
+    num_beams = num_beams if num_beams is not None else gen.get("num_beams", 1)
+    min_length = min_length if min_length is not None else gen.get("min_length", 0)
+    length_penalty = length_penalty if length_penalty is not None else gen.get("length_penalty", 1.0)
+    no_repeat_ngram_size = no_repeat_ngram_size if no_repeat_ngram_size is not None else \
+        gen.get("no_repeat_ngram_size", 0)
+    early_stopping = early_stopping if early_stopping is not None else gen.get("early_stopping", False)
+    forced_bos = forced_bos_token_id if forced_bos_token_id is not None else cfg.forced_bos_token_id
+    forced_eos = forced_eos_token_id if forced_eos_token_id is not None else cfg.forced_eos_token_id
+    eos, pad, start = cfg.eos_token_id, cfg.pad_token_id, cfg.decoder_start_token_id
+    was_training = model.training
+    model.eval()
+    try:
+        B = input_ids.shape[0]
+        dev = input_ids.device
+        enc = model.encode(input_ids, attention_mask)
+        nb = max(1, num_beams)
+        if nb > 1:
+            enc = enc.repeat_interleave(nb, 0)
+            attention_mask = attention_mask.repeat_interleave(nb, 0) if attention_mask is not None else None
+        N = B * nb
+        H, D = _head_geom(model)
+        dtype = next(model.parameters()).dtype
+        caches = [KVCache(N, max_length, H, D, dtype, dev) for _ in range(cfg.num_decoder_layers)]
+        cross = [m.project_kv(enc) for m in model.cross_attention_modules()]
+        seqs = torch.full((N, max_length), pad, dtype=torch.long, device=dev)
+        seqs[:, 0] = start
+        cur = 1
+        if nb == 1:
+            done = torch.zeros(B, dtype=torch.bool, device=dev)
+            while cur < max_length:
+                h = model.decode(seqs[:, cur - 1:cur], enc, attention_mask, caches=caches, q_offset=cur - 1,
+                                 cross_kv=cross)
+                logp = torch.log_softmax(model.lm_logits(h[:, -1]).float(), dim=-1)
+                logp = _apply_processors(logp, seqs[:, :cur], cur, cfg, min_length, no_repeat_ngram_size, forced_bos,
+                                         forced_eos, max_length, eos)
+                nxt = logp.argmax(-1)
+                nxt = torch.where(done, torch.full_like(nxt, pad), nxt)
+                seqs[:, cur] = nxt
+                done |= nxt == eos
+                cur += 1
+                if bool(done.all()):
+                    break
+            return seqs[:, :cur]
+        # ---------------------------------------------------------------- beam search
+        beam_scores = torch.zeros(B, nb, device=dev)
+        beam_scores[:, 1:] = -1e9
+        beam_scores = beam_scores.view(-1)
+        finished = [[] for _ in range(B)]  # (score, tokens)
+        batch_done = [False] * B
+        V = cfg.vocab_size
+        while cur < max_length:
+            h = model.decode(seqs[:, cur - 1:cur], enc, attention_mask, caches=caches, q_offset=cur - 1,
+                             cross_kv=cross)
+            logp = torch.log_softmax(model.lm_logits(h[:, -1]).float(), dim=-1)
+            logp = _apply_processors(logp, seqs[:, :cur], cur, cfg, min_length, no_repeat_ngram_size, forced_bos,
+                                     forced_eos, max_length, eos)
+            V = logp.shape[-1]
+            cand = (beam_scores[:, None] + logp).view(B, nb * V)
+            top_s, top_i = cand.topk(2 * nb, dim=1)
+            top_s, top_i = top_s.tolist(), top_i.tolist()
+            new_scores = torch.empty(B, nb, device=dev)
+            new_beam = torch.empty(B, nb, dtype=torch.long)
+            new_tok = torch.empty(B, nb, dtype=torch.long)
+            for b in range(B):
+                if batch_done[b]:
+                    new_scores[b] = -1e9
+                    new_beam[b] = b * nb
+                    new_tok[b] = pad
+                    continue
+                k = 0
+                for rank, (s, idx) in enumerate(zip(top_s[b], top_i[b])):
+                    beam, tok = divmod(idx, V)
+                    src = b * nb + beam
+                    if eos is not None and tok == eos:
+                        if rank >= nb:
+                            continue
+                        hyp = seqs[src, :cur].tolist() + [tok]
+                        gen_len = len(hyp) - 1
+                        finished[b].append((s / (max(gen_len, 1) ** length_penalty), hyp))
+                        finished[b].sort(key=lambda x: -x[0])
+                        del finished[b][nb:]
+                    else:
+                        new_scores[b, k] = s
+                        new_beam[b, k] = src
+                        new_tok[b, k] = tok
+                        k += 1
+                    if k == nb:
+                        break
+                # stopping rule (BeamHypotheses.is_done)
+                if len(finished[b]) == nb:
+                    if early_stopping is True:
+                        batch_done[b] = True
+                    else:
+                        best_running = float(new_scores[b].max())
+                        gl = cur if early_stopping is False else max_length - 1
+                        if finished[b][-1][0] >= best_running / (max(gl, 1) ** length_penalty):
+                            batch_done[b] = True
+            beam_idx = new_beam.view(-1).to(dev)
+            seqs = seqs.index_select(0, beam_idx)
+            seqs[:, cur] = new_tok.view(-1).to(dev)
+            for c in caches:
+                c.reorder(beam_idx)
+            beam_scores = new_scores.view(-1)
+            cur += 1
+            if all(batch_done):
+                break
+        # finalize: add running beams
+        scores = beam_scores.view(B, nb).tolist()
+        for b in range(B):
+            if batch_done[b]:
+                continue
+            for j in range(nb):
+                hyp = seqs[b * nb + j, :cur].tolist()
+                gen_len = len(hyp) - 1
+                finished[b].append((scores[b][j] / (max(gen_len, 1) ** length_penalty), hyp))
+            finished[b].sort(key=lambda x: -x[0])
+        best = [finished[b][0][1] for b in range(B)]
+        L = max(len(x) for x in best)
+        out = torch.full((B, L), pad, dtype=torch.long, device=dev)
+        for b, x in enumerate(best):
+            out[b, : len(x)] = torch.tensor(x, device=dev)
+        return out
+    finally:
+        model.train(was_training)

@@ -247,6 +247,10 @@ class T5ForConditionalGeneration(nn.Module):
     def cross_attention_modules(self):
         return [blk.layer[1].EncDecAttention for blk in self.decoder.block]
 
+    def generate(self, input_ids, attention_mask=None, **kw):
+        from .generation import generate
+        return generate(self, input_ids, attention_mask=attention_mask, **kw)
+
     def forward(self, input_ids=None, attention_mask=None, decoder_input_ids=None, labels=None,
                 label_smoothing: float = 0.0, return_logits: bool = False, encoder_outputs=None):
         enc = encoder_outputs if encoder_outputs is not None else self.encode(input_ids, attention_mask)

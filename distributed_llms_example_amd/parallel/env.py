@@ -78,6 +78,8 @@ def init_distributed(init_method: str | None = None, rank: int | None = None, wo
         dev_index = local_rank % max(ndev, 1)
         torch.cuda.set_device(dev_index)
         device = torch.device("cuda", dev_index)
+        from ..utils import tunableop
+        tunableop.enable(dev_index)
     else:
         device = torch.device("cpu")
     be = backend or _pick_backend(use_gpu)

@@ -46,7 +46,7 @@ class GradReducer:
         esz = flat.grad_buf.element_size()
         self.buckets: list[tuple[int, int]] = []
         self.seg_bucket: list[int] = []
-        limit = first_bucket_mb * 2**20
+        limit = min(first_bucket_mb, bucket_mb) * 2**20
         start = flat.segments[0].offset
         cur_bytes = 0
         counts = []

@@ -54,6 +54,7 @@ class LRScheduler:
                 "last_step": self.last_step}
 
     def load_state_dict(self, d):
-        self.name, self.warmup, self.total = d["name"], d["warmup"], d["total"]
+        # like torch LambdaLR: restore the step counter and base lr; the schedule shape (warmup, total)
+        # comes from the resuming run's arguments
         self.base_lr, self.last_step = d["base_lr"], d["last_step"]
         self._apply()

@@ -1,0 +1,263 @@
+"""Trainer-style loop (the HF Trainer path of ref/train-torchrun.py) on the native runtime.
+
+Semantics kept from transformers' Trainer as the reference configures it:
+``TrainingArguments`` names and defaults (lr 5e-5, betas (0.9, 0.999), eps 1e-8, max_grad_norm 1.0,
+linear schedule with ``warmup_steps``, seed 42, weight decay excluded for biases / norm weights),
+gradient accumulation with ``no_sync`` on all but the last micro-batch, clip → AdamW → scheduler →
+zero_grad on the sync step, ``logging_steps`` JSON logs through callbacks (``loss`` = mean over the
+logged micro-batches — the true mean, not the GA-summed value 5.15 prints, Appendix A Q12;
+``grad_norm``, ``learning_rate``, ``epoch``), eval every ``eval_steps`` (eval loss; the reference's
+eval set is passed untokenised and crashes, Q3 — here it is tokenised), checkpoints every
+``save_steps`` and at the last step, final ``train_runtime`` / ``train_samples_per_second`` /
+``train_steps_per_second`` / ``train_loss`` (trainer_utils.py:531-558).  Accepts both
+``evaluation_strategy`` and ``eval_strategy`` and both ``tokenizer`` and ``processing_class`` (Q2).
+
+The step itself is train/engine.py's: flat params, bucketed RCCL reducer, fused kernels, fused AdamW.
+"""
+from __future__ import annotations
+
+import dataclasses
+import math
+import os
+import time
+from dataclasses import dataclass, field
+
+import torch
+
+from ..ops.rng import manual_seed
+from ..parallel import collectives
+from ..parallel.env import init_distributed
+from ..parallel.reducer import DEFAULT_BUCKET_MB
+from ..parallel.sampler import ShardedBatchSampler
+from ..utils.logging import get_logger
+from .callbacks import CallbackHandler, DefaultFlowCallback, TrainerControl, TrainerState
+from .checkpoint import latest_checkpoint, load_checkpoint, save_checkpoint
+from .engine import TrainEngine, default_no_decay
+from .schedule import LRScheduler
+
+logger = get_logger(__name__)
+
+
+@dataclass
+class TrainingArguments:
+    output_dir: str = "output"
+    num_train_epochs: float = 1.0
+    max_steps: int = -1
+    per_device_train_batch_size: int = 8
+    per_device_eval_batch_size: int = 8
+    gradient_accumulation_steps: int = 1
+    learning_rate: float = 5e-5
+    weight_decay: float = 0.0
+    adam_beta1: float = 0.9
+    adam_beta2: float = 0.999
+    adam_epsilon: float = 1e-8
+    max_grad_norm: float = 1.0
+    lr_scheduler_type: str = "linear"
+    warmup_steps: int = 0
+    warmup_ratio: float = 0.0
+    logging_steps: int = 500
+    eval_strategy: str = "no"
+    evaluation_strategy: str | None = None
+    eval_steps: int | None = None
+    save_strategy: str = "steps"
+    save_steps: float = 500
+    save_total_limit: int | None = None
+    seed: int = 42
+    label_smoothing_factor: float = 0.0
+    bf16: bool | None = None
+    dataloader_num_workers: int = 0
+    dataloader_drop_last: bool = False
+    ddp_find_unused_parameters: bool | None = None
+    ddp_bucket_cap_mb: float | None = None
+    ddp_timeout: int = 1800
+    overlap_comm: bool = True
+    resume_from_checkpoint: str | None = None
+    report_to: list = field(default_factory=list)
+
+    def __post_init__(self):
+        if self.evaluation_strategy is not None:
+            self.eval_strategy = self.evaluation_strategy
+        if self.eval_strategy == "steps" and not self.eval_steps:
+            self.eval_steps = self.logging_steps
+
+    def to_dict(self):
+        return dataclasses.asdict(self)
+
+
+@dataclass
+class TrainOutput:
+    global_step: int
+    training_loss: float
+    metrics: dict
+
+
+class Trainer:
+    def __init__(self, model, args: TrainingArguments, train_dataset=None, eval_dataset=None, data_collator=None,
+                 callbacks=None, tokenizer=None, processing_class=None, compute_metrics=None, env=None):
+        self.args = args
+        self.env = env or init_distributed(timeout_s=args.ddp_timeout)
+        self.tokenizer = processing_class if processing_class is not None else tokenizer
+        torch.manual_seed(args.seed)
+        manual_seed(args.seed + 7919 * self.env.rank)
+        bf16 = args.bf16 if args.bf16 is not None else self.env.device.type == "cuda"
+        self.dtype = torch.bfloat16 if bf16 else torch.float32
+        self.engine = TrainEngine(model, self.env, lr=args.learning_rate, weight_decay=args.weight_decay,
+                                  betas=(args.adam_beta1, args.adam_beta2), eps=args.adam_epsilon,
+                                  max_grad_norm=args.max_grad_norm, dtype=self.dtype,
+                                  bucket_mb=args.ddp_bucket_cap_mb or DEFAULT_BUCKET_MB, overlap=args.overlap_comm,
+                                  no_decay=default_no_decay, label_smoothing=args.label_smoothing_factor)
+        self.model = self.engine.model
+        self.train_dataset = train_dataset
+        self.eval_dataset = eval_dataset
+        self.data_collator = data_collator
+        self.compute_metrics = compute_metrics
+        self.handler = CallbackHandler([DefaultFlowCallback] + list(callbacks or []))
+        self.state = TrainerState(is_world_process_zero=self.env.is_main_process)
+        self.control = TrainerControl()
+        self.scheduler = None
+
+    # ------------------------------------------------------------------ data
+    def _loader(self, dataset, batch_size, shuffle, epoch=0):
+        sampler = ShardedBatchSampler(len(dataset), batch_size, self.env.world_size, self.env.rank, shuffle=shuffle,
+                                      seed=self.args.seed, drop_last=self.args.dataloader_drop_last)
+        sampler.set_epoch(epoch)
+        return torch.utils.data.DataLoader(dataset, batch_sampler=sampler, collate_fn=self.data_collator,
+                                           num_workers=self.args.dataloader_num_workers,
+                                           pin_memory=self.env.device.type == "cuda"), sampler
+
+    def _to_device(self, batch):
+        nb = self.env.device.type == "cuda"
+        return {k: v.to(self.env.device, non_blocking=nb) for k, v in batch.items() if torch.is_tensor(v)}
+
+    # ------------------------------------------------------------------ main loop
+    def train(self, resume_from_checkpoint: str | bool | None = None):
+        args, eng, env = self.args, self.engine, self.env
+        _, probe = self._loader(self.train_dataset, args.per_device_train_batch_size, True)
+        steps_per_epoch = max(1, len(probe) // args.gradient_accumulation_steps)
+        if args.max_steps > 0:
+            max_steps = args.max_steps
+            epochs = math.ceil(max_steps / steps_per_epoch)
+        else:
+            epochs = math.ceil(args.num_train_epochs)
+            max_steps = math.ceil(args.num_train_epochs * steps_per_epoch)
+        warmup = args.warmup_steps or int(math.ceil(args.warmup_ratio * max_steps))
+        self.scheduler = LRScheduler(eng.optimizer, args.lr_scheduler_type, warmup, max_steps)
+        self.state.max_steps = max_steps
+        self.state.num_train_epochs = epochs
+        start_epoch, skip = 0, 0
+        resume = resume_from_checkpoint if resume_from_checkpoint is not None else args.resume_from_checkpoint
+        if resume:
+            path = latest_checkpoint(args.output_dir) if resume is True else resume
+            if path:
+                info = load_checkpoint(path, self.model, eng.optimizer, self.scheduler, rank=env.rank)
+                ts = info.get("trainer_state", {})
+                self.state.global_step = ts.get("global_step", 0)
+                self.state.log_history = ts.get("log_history", [])
+                start_epoch = self.state.global_step // steps_per_epoch
+                skip = (self.state.global_step % steps_per_epoch) * args.gradient_accumulation_steps
+                logger.info(f"resumed from {path} at step {self.state.global_step}")
+        n_examples = len(self.train_dataset)
+        self.handler.fire("on_train_begin", args, self.state, self.control)
+        eng.train()
+        t_start = time.perf_counter()
+        tr_loss_sum = torch.zeros((), device=env.device)
+        tr_loss_n = 0
+        total_loss_sum, total_loss_n = 0.0, 0
+        last_norm = None
+        ga = args.gradient_accumulation_steps
+        for epoch in range(start_epoch, epochs):
+            loader, sampler = self._loader(self.train_dataset, args.per_device_train_batch_size, True, epoch)
+            self.handler.fire("on_epoch_begin", args, self.state, self.control)
+            micro = 0
+            for i, batch in enumerate(loader):
+                if epoch == start_epoch and i < skip:
+                    continue
+                micro += 1
+                sync = micro % ga == 0
+                loss = eng.forward_backward(self._to_device(batch), grad_accum=ga, sync=sync)
+                tr_loss_sum += loss.float()
+                tr_loss_n += 1
+                if not sync:
+                    continue
+                last_norm = eng.step(self.scheduler.get_last_lr()[0])
+                self.scheduler.step()
+                self.state.global_step += 1
+                self.state.epoch = epoch + micro / max(1, len(loader))
+                self.control = self.handler.fire("on_step_end", args, self.state, self.control)
+                if self.control.should_log:
+                    mean = collectives.mean_across_processes({"loss": float(tr_loss_sum) / max(1, tr_loss_n)},
+                                                             env.device)["loss"]
+                    total_loss_sum += mean * tr_loss_n
+                    total_loss_n += tr_loss_n
+                    tr_loss_sum.zero_()
+                    tr_loss_n = 0
+                    self.log({"loss": round(mean, 4), "grad_norm": float(last_norm) if last_norm is not None else None,
+                              "learning_rate": self.scheduler.get_last_lr()[0], "epoch": round(self.state.epoch, 4)})
+                if self.control.should_evaluate and self.eval_dataset is not None:
+                    self.evaluate()
+                    eng.train()
+                if self.control.should_save:
+                    self._save_checkpoint()
+                self.control.reset_step()
+                if self.state.global_step >= max_steps:
+                    break
+            self.control = self.handler.fire("on_epoch_end", args, self.state, self.control)
+            if self.state.global_step >= max_steps:
+                break
+        if tr_loss_n:
+            mean = collectives.mean_across_processes({"loss": float(tr_loss_sum) / tr_loss_n}, env.device)["loss"]
+            total_loss_sum += mean * tr_loss_n
+            total_loss_n += tr_loss_n
+        if env.device.type == "cuda":
+            torch.cuda.synchronize()
+        runtime = time.perf_counter() - t_start
+        train_loss = total_loss_sum / max(1, total_loss_n)
+        n_samples = n_examples * args.num_train_epochs if args.max_steps <= 0 else \
+            max_steps * args.per_device_train_batch_size * ga * env.world_size
+        metrics = {"train_runtime": round(runtime, 4), "train_samples_per_second": round(n_samples / runtime, 3),
+                   "train_steps_per_second": round(self.state.global_step / runtime, 3),
+                   "train_loss": train_loss, "epoch": round(self.state.epoch, 4)}
+        self.log(metrics)
+        self.handler.fire("on_train_end", args, self.state, self.control)
+        return TrainOutput(self.state.global_step, train_loss, metrics)
+
+    def log(self, logs: dict):
+        logs = {k: v for k, v in logs.items() if v is not None}
+        self.state.log_history.append({**logs, "step": self.state.global_step})
+        self.handler.fire("on_log", self.args, self.state, self.control, logs=logs)
+
+    @torch.no_grad()
+    def evaluate(self, eval_dataset=None):
+        ds = eval_dataset if eval_dataset is not None else self.eval_dataset
+        self.engine.train(False)
+        loader, _ = self._loader(ds, self.args.per_device_eval_batch_size, False)
+        tot = torch.zeros((), device=self.env.device, dtype=torch.float64)
+        n = 0
+        for batch in loader:
+            out = self.engine.forward(self._to_device(batch))
+            tot += out.loss.double()
+            n += 1
+        m = collectives.mean_across_processes({"eval_loss": float(tot) / max(1, n)}, self.env.device)
+        metrics = {"eval_loss": m["eval_loss"], "epoch": round(self.state.epoch, 4)}
+        self.log(metrics)
+        self.handler.fire("on_evaluate", self.args, self.state, self.control, metrics=metrics)
+        return metrics
+
+    def _save_checkpoint(self):
+        path = os.path.join(self.args.output_dir, f"checkpoint-{self.state.global_step}")
+        save_checkpoint(path, self.model, self.engine.optimizer, self.scheduler, self.state, rank=self.env.rank,
+                        device=self.env.device)
+        if self.env.is_main_process and self.tokenizer is not None and hasattr(self.tokenizer, "save_pretrained"):
+            self.tokenizer.save_pretrained(path)
+        self.handler.fire("on_save", self.args, self.state, self.control)
+        if self.args.save_total_limit and self.env.is_main_process:
+            import shutil
+            cks = sorted((d for d in os.listdir(self.args.output_dir) if d.startswith("checkpoint-")),
+                         key=lambda d: int(d.split("-")[1]))
+            for d in cks[: max(0, len(cks) - self.args.save_total_limit)]:
+                shutil.rmtree(os.path.join(self.args.output_dir, d), ignore_errors=True)
+
+    def save_model(self, output_dir=None):
+        from ..platform.valohai import save_valohai_metadata
+        return save_valohai_metadata(self.model, output_dir or self.args.output_dir, self.env.is_main_process,
+                                     self.tokenizer)

@@ -1,0 +1,91 @@
+"""Tracing / throughput instrumentation.
+
+* ``range(name)``: roctx push/pop ranges (``/opt/rocm/lib/libroctx64.so`` via ctypes) around
+  forward / backward / optimizer / comm so ``rocprofv3 --marker-trace`` timelines are annotated; a
+  no-op when the library is absent or ``DLLM_ROCTX=0``.
+* ``StepTimer``: wall-clock per step synchronised on the device, samples/s, tokens/s and model FLOP
+  utilisation (6 × params × tokens + attention terms, against the MI355X dense bf16 peak).
+"""
+from __future__ import annotations
+
+import contextlib
+import ctypes
+import os
+import time
+
+import torch
+
+_roctx = None
+_roctx_tried = False
+MI355X_BF16_DENSE_PEAK = 2.5e15
+
+
+def _lib():
+    global _roctx, _roctx_tried
+    if not _roctx_tried:
+        _roctx_tried = True
+        if os.environ.get("DLLM_ROCTX", "1") != "0":
+            for p in ("/opt/rocm/lib/libroctx64.so", "libroctx64.so"):
+                try:
+                    _roctx = ctypes.CDLL(p)
+                    _roctx.roctxRangePushA.argtypes = [ctypes.c_char_p]
+                    break
+                except OSError:
+                    continue
+    return _roctx
+
+
+@contextlib.contextmanager
+def range(name: str):  # noqa: A001 - mirrors the roctx API name
+    lib = _lib()
+    if lib is not None:
+        lib.roctxRangePushA(name.encode())
+    try:
+        yield
+    finally:
+        if lib is not None:
+            lib.roctxRangePop()
+
+
+def seq2seq_train_flops(cfg, batch: int, src: int, tgt: int) -> float:
+    """Training FLOPs (fwd + bwd = 3 × fwd) of one step: dense GEMMs + attention + LM head."""
+    d, f, H, dk = cfg.d_model, cfg.d_ff, cfg.num_heads, cfg.d_kv
+    inner = H * dk
+    ff_mult = 3 if cfg.is_gated else 2
+    enc = cfg.num_layers * (2 * src * d * inner * 4 + 2 * src * d * f * ff_mult + 4 * src * src * inner)
+    dec = cfg.num_decoder_layers * (2 * tgt * d * inner * 4 + 2 * tgt * d * inner * 2 + 2 * src * d * inner * 2
+                                    + 2 * tgt * d * f * ff_mult + 4 * tgt * tgt * inner + 4 * tgt * src * inner)
+    head = 2 * tgt * d * cfg.vocab_size
+    return 3.0 * batch * (enc + dec + head)
+
+
+class StepTimer:
+    def __init__(self, device=None):
+        self.device = device
+        self.t0 = None
+        self.times = []
+
+    def _sync(self):
+        if self.device is not None and getattr(self.device, "type", "cpu") == "cuda":
+            torch.cuda.synchronize(self.device)
+
+    def start(self):
+        self._sync()
+        self.t0 = time.perf_counter()
+
+    def stop(self):
+        self._sync()
+        dt = time.perf_counter() - self.t0
+        self.times.append(dt)
+        return dt
+
+    def summary(self, samples_per_step: int, tokens_per_step: int, flops_per_step: float | None = None,
+                n_gpus: int = 1) -> dict:
+        if not self.times:
+            return {}
+        avg = sum(self.times) / len(self.times)
+        out = {"step_time_s": avg, "samples_per_second": samples_per_step / avg,
+               "tokens_per_second": tokens_per_step / avg}
+        if flops_per_step:
+            out["mfu"] = flops_per_step / avg / (MI355X_BF16_DENSE_PEAK * n_gpus)
+        return out

@@ -1,0 +1,170 @@
+"""Distributed runtime on CPU/gloo (SURVEY.md §4 level 4): reducer math, overlap vs coalesced,
+GA/no_sync, parameter broadcast, sharded sampler, collectives."""
+import functools
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from distributed_llms_example_amd.parallel.sampler import DataPartitioner, ShardedBatchSampler
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, fn, q):
+    os.environ["DLLM_FORCE_CPU"] = "1"
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    def by_value(x):  # tensors through a Queue travel as shared-memory fds that die with the child
+        if torch.is_tensor(x):
+            return x.detach().cpu().numpy().copy()
+        if isinstance(x, (tuple, list)):
+            return type(x)(by_value(v) for v in x)
+        return x
+
+    try:
+        q.put((rank, by_value(fn(rank, world))))
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put((rank, "ERR " + traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+def run_ranks(fn, world=2):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, fn, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    out = dict(q.get(timeout=240) for _ in ps)
+    for p in ps:
+        p.join(60)
+    for r, v in out.items():
+        assert not (isinstance(v, str) and v.startswith("ERR")), v
+    return out
+
+
+def _grad_case(rank, world, overlap=True, ga=1, bucket_mb=0.05):
+    from distributed_llms_example_amd.models import build_model
+    from distributed_llms_example_amd.parallel.env import DistEnv
+    from distributed_llms_example_amd.train.engine import TrainEngine
+    torch.manual_seed(0)
+    model = build_model("t5-tiny")
+    env = DistEnv(rank=rank, world_size=world, backend="gloo", device=torch.device("cpu"))
+    torch.manual_seed(123 + rank)  # different init on rank 1 -> must be overwritten by the broadcast
+    if rank == 1:
+        with torch.no_grad():
+            for p in model.parameters():
+                p.add_(1.0)
+    eng = TrainEngine(model, env, lr=1e-3, dtype=torch.float32, bucket_mb=bucket_mb, overlap=overlap)
+    eng.train(False)  # no dropout: deterministic comparison
+    g = torch.Generator().manual_seed(7)
+    ids = torch.randint(3, 500, (4 * world, 10), generator=g)
+    lab = torch.randint(3, 500, (4 * world, 5), generator=g)
+    sl = slice(rank * 4, rank * 4 + 4)
+    mb = 4 // ga
+    for i in range(ga):
+        s = slice(rank * 4 + i * mb, rank * 4 + (i + 1) * mb)
+        eng.forward_backward({"input_ids": ids[s], "attention_mask": torch.ones_like(ids[s]), "labels": lab[s]},
+                             grad_accum=ga, sync=(i == ga - 1))
+    return eng.flat.grad_buf.clone(), eng.flat.param_buf.clone(), len(eng.reducer.buckets)
+
+
+def _reference_grad(world):
+    from distributed_llms_example_amd.models import build_model
+    from distributed_llms_example_amd.parallel.flat import FlatParams
+    torch.manual_seed(0)
+    model = build_model("t5-tiny").eval()
+    flat = FlatParams(model)
+    g = torch.Generator().manual_seed(7)
+    ids = torch.randint(3, 500, (4 * world, 10), generator=g)
+    lab = torch.randint(3, 500, (4 * world, 5), generator=g)
+    # mean over ranks of per-rank mean losses == DDP semantics
+    loss = sum(model(input_ids=ids[r * 4:(r + 1) * 4], attention_mask=torch.ones(4, 10, dtype=torch.long),
+                     labels=lab[r * 4:(r + 1) * 4]).loss for r in range(world)) / world
+    loss.backward()
+    return flat.grad_buf.clone()
+
+
+@pytest.mark.parametrize("overlap", [True, False])
+def test_reducer_matches_single_process(overlap):
+    out = run_ranks(functools.partial(_grad_case, overlap=overlap))
+    ref = _reference_grad(2)
+    g0, p0, nb = (torch.as_tensor(x) if not isinstance(x, int) else x for x in out[0])
+    g1, p1, _ = (torch.as_tensor(x) if not isinstance(x, int) else x for x in out[1])
+    assert nb > 2  # several buckets exercised
+    torch.testing.assert_close(g0, g1)
+    torch.testing.assert_close(p0, p1)  # broadcast made rank 1 identical
+    torch.testing.assert_close(g0, ref, atol=1e-5, rtol=1e-4)
+
+
+def test_grad_accumulation_no_sync():
+    out = run_ranks(functools.partial(_grad_case, overlap=True, ga=2))
+    ref = _reference_grad(2)
+    a, b = torch.as_tensor(out[0][0]), torch.as_tensor(out[1][0])
+    torch.testing.assert_close(a, b)
+    torch.testing.assert_close(a, ref, atol=1e-5, rtol=1e-4)
+
+
+def _collectives(rank, world):
+    from distributed_llms_example_amd.parallel import collectives as C
+    t = torch.full((2, 3 + rank), float(rank))
+    padded = C.pad_across_processes(t, dim=1, pad_index=-1)
+    g = C.gather(padded)
+    m = C.mean_across_processes({"a": rank * 2.0, "epoch": 3}, torch.device("cpu"))
+    return g, m
+
+
+def test_collectives():
+    out = run_ranks(_collectives)
+    g, m = out[0]
+    g = torch.as_tensor(g)
+    assert g.shape == (4, 4)
+    assert (g[:2, 3] == -1).all() and (g[2:, :] == 1).all()
+    assert m == {"a": 1.0, "epoch": 3}
+
+
+def test_sharded_sampler_even_batches():
+    n, bs, R = 818, 1, 4
+    seen = []
+    lens = set()
+    for r in range(R):
+        s = ShardedBatchSampler(n, bs, R, r, shuffle=False)
+        b = list(s)
+        lens.add(len(b))
+        assert len(b) == len(s)
+        seen += [i for x in b for i in x]
+    assert lens == {205}  # 820 = 818 + 2 wrapped samples
+    assert len(seen) == 820 and set(seen) == set(range(n))
+
+
+def test_sharded_sampler_shuffle_synced():
+    a = list(ShardedBatchSampler(100, 8, 2, 0, shuffle=True, seed=3))
+    b = list(ShardedBatchSampler(100, 8, 2, 1, shuffle=True, seed=3))
+    flat = [i for x in a + b for i in x]
+    assert set(flat) == set(range(100))
+    s = ShardedBatchSampler(100, 8, 2, 0, shuffle=True, seed=3)
+    s.set_epoch(1)
+    assert list(s) != a
+
+
+def test_data_partitioner_matches_reference_semantics():
+    import random
+    data = list(range(37))
+    parts = DataPartitioner(data, [0.25] * 4, seed=1234)
+    rng = random.Random()
+    rng.seed(1234)
+    idx = list(range(37))
+    rng.shuffle(idx)
+    assert [parts.use(0)[i] for i in range(len(parts.use(0)))] == idx[:9]
+    assert sum(len(parts.use(r)) for r in range(4)) == 36

@@ -1,0 +1,102 @@
+"""End-to-end CLI smoke tests of the three entry points on CPU (SURVEY.md §4 level 5; BASELINE.json
+config #1 "t5-small summarization fine-tune on CPU, world_size=1" with a tiny random-init T5)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _env(tmp):
+    e = dict(os.environ)
+    e.update({"VH_ROOT": str(tmp), "DLLM_FORCE_CPU": "1", "OMP_NUM_THREADS": "2", "PYTHONPATH": ROOT})
+    return e
+
+
+def _json_lines(out):
+    res = []
+    for line in out.splitlines():
+        line = line.strip()
+        if line.startswith("{"):
+            try:
+                res.append(json.loads(line))
+            except json.JSONDecodeError:
+                pass
+    return res
+
+
+COMMON = ["--synthetic", "32", "--max-source-length", "40", "--max-target-length", "10", "--gen-max-length", "8"]
+
+
+def test_train_torchrun_single_process(tmp_path):
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "train-torchrun.py"), "--model-ckpt", "t5-tiny",
+                        "--output-dir", "out", "--batch-size", "4", "--grad-accum", "2", "--evaluation-steps", "2",
+                        "--warmup-steps", "1", *COMMON], env=_env(tmp_path), capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    logs = _json_lines(r.stdout)
+    assert any("eval_loss" in x for x in logs)
+    final = [x for x in logs if "train_samples_per_second" in x]
+    assert final and final[-1]["train_loss"] > 0
+    out = tmp_path / "outputs" / "out"
+    for f in ("config.json", "model.safetensors", "generation_config.json", "model.safetensors.metadata.json"):
+        assert (out / f).exists(), f
+    md = json.load(open(out / "model.safetensors.metadata.json"))
+    assert md["valohai.dataset-versions"][0]["uri"].startswith("dataset://llm-models/")
+    assert not any(p.name.endswith(".metadata.json.metadata.json") for p in out.iterdir())
+
+
+@pytest.mark.slow
+def test_train_accelerator_two_ranks(tmp_path):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "train-accelerator.py"), "--model-ckpt",
+           "bart-tiny", "--output-dir", "acc", "--batch-size", "2", *COMMON]
+    r = subprocess.run(cmd, env=_env(tmp_path), capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    logs = _json_lines(r.stdout)
+    assert any("rougeLsum" in x for x in logs)
+    assert (tmp_path / "outputs" / "acc" / "model.safetensors").exists()
+
+
+@pytest.mark.slow
+def test_train_task_spawn_two_local_ranks(tmp_path):
+    cmd = [sys.executable, os.path.join(ROOT, "train-task.py"), "--model-ckpt", "t5-tiny", "--output-dir", "task",
+           "--batch-size", "2", "--local-procs", "2", "--master-port", str(_port()), *COMMON]
+    r = subprocess.run(cmd, env=_env(tmp_path), capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    logs = _json_lines(r.stdout)
+    agg = [x for x in logs if "rouge1" in x]
+    assert agg and agg[-1]["epoch"] == 0
+    assert (tmp_path / "outputs" / "task" / "model.safetensors").exists()
+
+
+def test_train_task_valohai_distributed_contract(tmp_path):
+    """The Valohai distributed shim: master ip / world / rank from /valohai/config/distributed.json."""
+    cfgdir = tmp_path / "config"
+    cfgdir.mkdir()
+    json.dump({"required_count": 4, "me": {"rank": 2, "primary_local_ip": "10.0.0.3"},
+               "master": {"primary_local_ip": "10.0.0.1"}}, open(cfgdir / "distributed.json", "w"))
+    os.environ["VH_ROOT"] = str(tmp_path)
+    try:
+        from distributed_llms_example_amd.platform import valohai
+        assert valohai.distributed.required_count == 4
+        assert valohai.distributed.me().rank == 2
+        assert valohai.distributed.master().primary_local_ip == "10.0.0.1"
+        (tmp_path / "inputs" / "dataset").mkdir(parents=True)
+        (tmp_path / "inputs" / "dataset" / "train.json").write_text("[]")
+        assert valohai.inputs("dataset").path().endswith("train.json")
+        assert valohai.outputs().path("model-dir").startswith(str(tmp_path / "outputs"))
+    finally:
+        os.environ.pop("VH_ROOT", None)

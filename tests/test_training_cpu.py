@@ -1,0 +1,141 @@
+"""Training-loop semantics on CPU (SURVEY.md §4 level 3): schedule, optimizer, clip, checkpoint
+round-trip through transformers, resume, collator, ROUGE, dropout RNG."""
+import json
+import math
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from distributed_llms_example_amd.data.collator import DataCollatorForSeq2Seq
+from distributed_llms_example_amd.models import build_model, from_pretrained, save_pretrained
+from distributed_llms_example_amd.ops import rng
+from distributed_llms_example_amd.ops.optim import FusedAdamW
+from distributed_llms_example_amd.parallel.flat import FlatParams
+from distributed_llms_example_amd.train import rouge
+from distributed_llms_example_amd.train.schedule import LRScheduler, lr_lambda
+
+
+def test_linear_schedule_matches_transformers():
+    from transformers import get_linear_schedule_with_warmup
+    p = torch.nn.Parameter(torch.zeros(1))
+    opt = torch.optim.SGD([p], lr=5e-5)
+    ref = get_linear_schedule_with_warmup(opt, 7, 40)
+    fake = FusedAdamW.__new__(FusedAdamW)
+    fake.param_groups = [{"lr": 5e-5, "initial_lr": 5e-5}]
+    ours = LRScheduler(fake, "linear", 7, 40)
+    for _ in range(45):
+        assert abs(ours.get_last_lr()[0] - ref.get_last_lr()[0]) < 1e-12
+        opt.step()
+        ref.step()
+        ours.step()
+    assert lr_lambda("cosine", 5, 0, 10) == pytest.approx(0.5)
+
+
+def test_fused_adamw_reference_matches_torch_with_clip():
+    torch.manual_seed(0)
+    m1 = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.LayerNorm(16), torch.nn.Linear(16, 4))
+    m2 = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.LayerNorm(16), torch.nn.Linear(16, 4))
+    m2.load_state_dict(m1.state_dict())
+    flat = FlatParams(m1)
+    nd = lambda n: n.endswith("bias") or n.startswith("1.")  # noqa: E731
+    opt = FusedAdamW(flat, lr=1e-2, weight_decay=0.1, no_decay=nd)
+    ref = torch.optim.AdamW([{"params": [p for n, p in m2.named_parameters() if not nd(n)], "weight_decay": 0.1},
+                             {"params": [p for n, p in m2.named_parameters() if nd(n)], "weight_decay": 0.0}], lr=1e-2)
+    for _ in range(6):
+        x = torch.randn(5, 8)
+        opt.zero_grad()
+        ref.zero_grad()
+        (m1(x).pow(2).sum() * 10).backward()
+        (m2(x).pow(2).sum() * 10).backward()
+        n1 = opt.step(max_grad_norm=1.0)
+        n2 = torch.nn.utils.clip_grad_norm_(m2.parameters(), 1.0)
+        ref.step()
+        assert float(n1) == pytest.approx(float(n2), rel=1e-5)
+        for a, b in zip(m1.parameters(), m2.parameters()):
+            torch.testing.assert_close(a, b, atol=1e-6, rtol=1e-5)
+
+
+def test_checkpoint_loads_in_transformers(tmp_path):
+    import transformers
+    for name in ("t5-tiny", "bart-tiny"):
+        m = build_model(name).eval()
+        d = tmp_path / name
+        save_pretrained(m, str(d))
+        hf = transformers.AutoModelForSeq2SeqLM.from_pretrained(str(d)).eval()
+        ids = torch.randint(3, 500, (2, 11))
+        lab = torch.randint(3, 500, (2, 6))
+        a = m(input_ids=ids, labels=lab).loss
+        b = hf(input_ids=ids, labels=lab).loss
+        assert float(a) == pytest.approx(float(b), rel=1e-5, abs=1e-5)
+        m2 = from_pretrained(str(d)).eval()
+        assert float(m2(input_ids=ids, labels=lab).loss) == pytest.approx(float(a), rel=1e-6)
+        meta = json.load(open(d / "config.json"))
+        assert meta["model_type"] == m.config.model_type
+
+
+def test_trainer_resume_is_exact(tmp_path):
+    """Train 6 steps straight vs 3 + resume-from-checkpoint + 3: identical weights."""
+    from distributed_llms_example_amd.data.dataset import SyntheticSeq2Seq
+    from distributed_llms_example_amd.parallel.env import init_distributed
+    from distributed_llms_example_amd.train.trainer import Trainer, TrainingArguments
+    env = init_distributed(cpu=True)
+    ds = SyntheticSeq2Seq(24, 12, 6, 500, seed=1)
+    coll = DataCollatorForSeq2Seq(0, 0)
+
+    def make(out, max_steps, save_steps):
+        torch.manual_seed(0)
+        m = build_model("t5-tiny")
+        args = TrainingArguments(output_dir=str(out), max_steps=max_steps, per_device_train_batch_size=4,
+                                 learning_rate=1e-3, warmup_steps=2, logging_steps=100, save_steps=save_steps,
+                                 bf16=False, seed=3)
+        return Trainer(m, args, train_dataset=ds, data_collator=coll, env=env)
+
+    t1 = make(tmp_path / "a", 6, 1000)
+    t1.train()
+    t2 = make(tmp_path / "b", 3, 3)
+    t2.train()
+    t3 = make(tmp_path / "b", 6, 1000)
+    t3.train(resume_from_checkpoint=str(tmp_path / "b" / "checkpoint-3"))
+    assert t3.state.global_step == 6
+    torch.testing.assert_close(t1.engine.flat.param_buf, t3.engine.flat.param_buf, atol=1e-6, rtol=1e-5)
+
+
+def test_collator_shift_right_and_padding():
+    c = DataCollatorForSeq2Seq(pad_token_id=1, decoder_start_token_id=2, pad_to_multiple_of=8)
+    feats = [{"input_ids": [5, 6, 7], "attention_mask": [1, 1, 1], "labels": [9, 10]},
+             {"input_ids": [5], "attention_mask": [1], "labels": [11, 12, 13]}]
+    b = c(feats)
+    assert b["input_ids"].shape == (2, 8) and b["input_ids"][1, 1] == 1
+    assert b["labels"].tolist()[0][:3] == [9, 10, -100]
+    assert b["decoder_input_ids"].tolist()[0][:3] == [2, 9, 10]
+    assert b["decoder_input_ids"].tolist()[0][3] == 1  # -100 -> pad
+
+
+def test_rouge_known_values():
+    s = rouge.score("the cat sat on the mat", "the cat sat on the mat")
+    assert all(v == pytest.approx(1.0) for v in s.values())
+    s = rouge.score("the cat was found under the bed", "the cat was under the bed")
+    # unigram: P = 6/7, R = 6/6 -> F = 12/13; bigram: overlaps the cat, cat was, under the, the bed = 4 -> P 4/6 R 4/5
+    assert s["rouge1"] == pytest.approx(12 / 13)
+    assert s["rouge2"] == pytest.approx(2 * (4 / 6) * (4 / 5) / (4 / 6 + 4 / 5))
+    assert s["rougeL"] == pytest.approx(12 / 13)
+    st = rouge.PorterStemmer()
+    assert [st.stem(w) for w in ("caresses", "ponies", "running", "relational", "happiness")] == \
+        ["caress", "poni", "run", "relat", "happi"]
+    m = rouge.load("rouge")
+    m.add_batch(["a b c", "x y"], ["a b c", "z"])
+    r = m.compute()
+    assert r["rouge1"] == pytest.approx(0.5)
+
+
+def test_dropout_rng_statistics_and_reproducibility():
+    k1 = rng.keep_mask(1234, 0.1, (1000, 100), "cpu")
+    k2 = rng.keep_mask(1234, 0.1, (1000, 100), "cpu")
+    assert torch.equal(k1, k2)
+    assert abs(1 - k1.float().mean().item() - 0.1) < 0.003
+    k3 = rng.keep_mask(1235, 0.1, (1000, 100), "cpu")
+    assert (k1 != k3).float().mean() > 0.1
+    a = rng.attention_keep_mask(5, 0.25, 2, 3, 7, 9, "cpu")
+    assert a.shape == (2, 3, 7, 9) and abs(1 - a.float().mean().item() - 0.25) < 0.08
