@@ -1,46 +1,55 @@
 // Flash attention forward + backward for encoder-decoder models on gfx950 (MI355X / CDNA4).
 //
-// Head dim D = 64 (T5 d_kv, BART 1024/16, flan-t5-xl 2048/32).  bf16 in/out, fp32 accumulate, MFMA
+// Head dim D = 64 (T5 d_kv, BART 1024/16, flan-t5-xl 2048/32).  bf16 in/out, fp32 accumulate,
 // v_mfma_f32_32x32x16_bf16 (wave64).  Supports: softmax scale (BART d^-0.5, T5 1.0), T5 relative
 // position bias as a per-head LUT over (j - i) staged in LDS, key-padding mask, causal mask
 // (bottom-right aligned: key j visible to query i iff j <= i + Sk - Sq), attention-probability
-// dropout with the counter-based mask of common.h (regenerated in backward, never stored).
+// dropout regenerated from a counter-based hash (never stored).
 //
-// Forward (one workgroup = 4 waves = 128 query rows of one (b, h); KV tiles of 64 keys):
-//   "swapped" QK^T: each wave computes S^T = K Q^T so one lane owns one query column and holds 16 of
-//   its 32 scores per 32-key subtile in registers -> row max / row sum are in-lane + one xor-32 shuffle.
-//   The S^T accumulator is converted to bf16 and fed straight back as the B operand of O^T = V^T P^T
-//   (no LDS round trip for P; cdna_hip_programming.md §3 "accumulator tile as the next MFMA's operand").
-//   K is staged row-major in LDS with a 16-B row pad (conflict-free ds_read_b128), V transposed
-//   (V^T, 8-B pad, conflict-free ds_read_b64).  Grid is 1-D with an XCD-aware bijective remap so the
-//   q-tiles of one (b, h) land on one XCD and share K/V through its L2.
+// LDS tiles are [rows][64] bf16 with 128-B rows and no padding; 16-B chunk c of row r is stored at
+// chunk c ^ swz(r), swz(r) = ((r>>1)&1)<<2 | ((r>>2)&3).  With that one image both access kinds the
+// kernels need are bank-conflict free: row reads (ds_read_b128, MFMA operands whose k-dim is the head
+// dim) and hardware-transposed reads (ds_read_b64_tr_b16, operands whose k-dim is the sequence) — so
+// no tile is ever written transposed element by element.
 //
-// Backward = two atomic-free kernels (recompute P from the forward's LSE in both):
-//   dQ kernel (query blocks, query on the lane, like the forward): dS^T = P^T (dP^T - delta) stays in
-//   registers and feeds dQ^T += K^T dS^T as the B operand; it also computes delta = rowsum(dO * O).
-//   dK/dV kernel (key blocks of 128, key on the lane): S = Q K^T and dPd = dO V^T come out with the key
-//   on the MFMA column, so P and dS are directly the B operands of dV^T += dO^T Pd and dK^T += Q^T dS
-//   (K and V of the wave's 32 keys stay in registers).  The extra recompute (2 of 7 GEMMs) buys no
-//   fp32 dQ atomics, no dS round trip through LDS and no cross-wave reduction.  The relative-bias
-//   gradient is the sum of dS along diagonals: LDS float atomics into a window of the LUT, then one
-//   global atomic per entry per workgroup.
+// Scores are computed in log2 units: s2 = (q.k) * scale * log2(e) + bias * log2(e) (the LUT is
+// pre-scaled when staged), softmax via exp2; the LSE handed from forward to backward is in log2 units.
+// Online softmax defers the O/l rescale until the running max grows by more than 8 (P <= 2^8 in bf16).
+//
+// Forward (workgroup = 4 waves = 128 query rows of one (b, h); K/V tiles of 64 keys, double-buffered,
+// next tile's global loads in flight during compute, one barrier per tile):
+//   swapped QK^T: each wave computes S^T = K Q^T so a lane owns one query row; row max / sum are in-lane
+//   + one xor-32 shuffle; the P^T accumulator registers, converted to bf16, are directly the B operand
+//   of O^T = V^T P^T (cdna_hip_programming.md §3, accumulator as the next MFMA's operand); V^T comes
+//   from transposed LDS reads.  1-D grid with a bijective XCD remap: q-tiles of one (b, h) share an XCD.
+// Backward = two atomic-free kernels (P recomputed from LSE in both):
+//   dQ kernel (query blocks, query on the lane): dS^T = P^T (dP^T - delta) feeds dQ^T += K^T dS^T as the
+//   B operand (K^T by transposed reads); also computes delta = rowsum(dO * O).
+//   dK/dV kernel (key blocks of 128, key on the lane): P and dS accumulators are the B operands of
+//   dV^T += dO^T Pd and dK^T += Q^T dS (dO^T, Q^T by transposed reads); bias-LUT gradient = diagonal sums
+//   of dS via a register shear + 2 LDS atomics per lane per tile.
 #include "common.h"
 #include "attn_params.h"
 
 using namespace dllm;
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8v;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
 
 namespace {
 
 constexpr int D = 64;
-constexpr int FWD_BM = 128;  // 4 waves x 32 query rows
-constexpr int FWD_BN = 64;   // keys per KV tile
-constexpr int KS_STRIDE = 72;  // bf16 elements per K row in LDS (64 + 8 pad = 144 B)
-constexpr int VT_STRIDE = 68;  // bf16 elements per V^T row (64 keys + 4 pad = 136 B)
+constexpr int TILE64 = 64 * D;  // elements of a 64-row tile (8 KB)
+constexpr int TILE32 = 32 * D;  // elements of a 32-row tile (4 KB)
+constexpr int FWD_BM = 128;     // query rows per forward / dQ workgroup (4 waves x 32)
+constexpr int FWD_BN = 64;      // keys per K/V tile
+constexpr int BWD_BK = 128;     // keys per dK/dV workgroup (4 waves x 32)
+constexpr int BWD_BQ = 32;      // query rows per dK/dV tile
 constexpr float LOG2E = 1.4426950408889634f;
-
-// AttnParams: csrc/attn_params.h (shared with the host binding)
+constexpr float LN2 = 0.6931471805599453f;
+constexpr float RESCALE_THR = 8.f;
+constexpr uint32_t HG = 0x9E3779B1u;
+constexpr uint32_t HC = 0x85EBCA6Bu;
 
 DLLM_DEVICE bf16x8v as_frag(u16x8 v) { return __builtin_bit_cast(bf16x8v, v); }
 
@@ -64,14 +73,47 @@ DLLM_DEVICE int xcd_remap(int bid, int nblk) {
 // row of the C/D accumulator held in register `reg` by lane-half `hh` (32x32x16 layout)
 DLLM_DEVICE int crow(int reg, int hh) { return (reg & 3) + 8 * (reg >> 2) + 4 * hh; }
 
+// ---- swizzled [rows][64] bf16 tiles
+DLLM_DEVICE int swz(int r) { return (((r >> 1) & 1) << 2) | ((r >> 2) & 3); }
+DLLM_DEVICE int toff(int r, int c) { return (r << 6) + ((c ^ swz(r)) << 3); }
+DLLM_DEVICE u16x8 ld_row(const uint16_t* T, int r, int c) { return *reinterpret_cast<const u16x8*>(T + toff(r, c)); }
+DLLM_DEVICE void st_row(uint16_t* T, int r, int c, u16x8 v) { *reinterpret_cast<u16x8*>(T + toff(r, c)) = v; }
+
+// Transposed read (ds_read_b64_tr_b16): the calling lane's 16-lane group reads rows r0..r0+3 (r0 % 4 == 0) x
+// columns c0..c0+15 (c0 % 16 == 0); group lane i receives column c0 + i of the 4 rows (row q in element q).
+// Lane 4q+p supplies the address of row q, columns 4p..4p+3.  EXEC must be full (no divergence here).
+DLLM_DEVICE u16x4 ld_tr(const uint16_t* T, int r0, int c0, int i) {
+  const int r = r0 + (i >> 2);
+  const int col = c0 + 4 * (i & 3);
+  const int off = (r << 6) + (((col >> 3) ^ swz(r)) << 3) + (col & 4);
+  s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(T + off));
+  return __builtin_bit_cast(u16x4, v);
+}
+
+// A operand (32x32x16, k = sequence, permuted k order of an accumulator-fed B) for head-dim rows
+// [32t, 32t+32) and sequence rows kb0.. (lo: kb0+0..3, hi: kb0+8..11) of a swizzled tile.
+DLLM_DEVICE bf16x8v ld_tr_operand(const uint16_t* T, int kb0, int t, int r) {
+  const int c0 = 32 * t + 16 * ((r >> 4) & 1);
+  const u16x4 lo = ld_tr(T, kb0, c0, r & 15);
+  const u16x4 hi = ld_tr(T, kb0 + 8, c0, r & 15);
+  const u16x8 v = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+  return as_frag(v);
+}
+
+// attention dropout: x = (rowhash ^ (key>>1)*HG) * HC; x ^= x >> 16; key keeps iff half (key & 1) >= thr16
+DLLM_DEVICE uint32_t pair_hash(uint32_t rh, uint32_t kpg) {
+  uint32_t x = (rh ^ kpg) * HC;
+  return x ^ (x >> 16);
+}
+
 // ================================================================================== forward
 template <bool HAS_BIAS, bool HAS_KPM, bool CAUSAL, bool DROP>
-__global__ __launch_bounds__(256) void attn_fwd_kernel(AttnParams P) {
+__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  uint16_t* Ks = reinterpret_cast<uint16_t*>(smem);                 // [64][KS_STRIDE]
-  uint16_t* Vt = Ks + FWD_BN * KS_STRIDE;                             // [64 d][VT_STRIDE]
-  float* kmask = reinterpret_cast<float*>(Vt + D * VT_STRIDE);        // [64]
-  float* lut_s = kmask + FWD_BN;                                      // [Sk + FWD_BM + FWD_BN]
+  uint16_t* KV = reinterpret_cast<uint16_t*>(smem);            // [2 buffers][K tile | V tile]
+  float* kmask = reinterpret_cast<float*>(KV + 4 * TILE64);     // [2][64]
+  int* anym = reinterpret_cast<int*>(kmask + 2 * FWD_BN);       // [4]
+  float* lut_s = reinterpret_cast<float*>(anym + 4);            // [Sk + FWD_BM + FWD_BN], log2-scaled
 
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 31, hh = lane >> 5;
   const int logical = xcd_remap(blockIdx.x, gridDim.x);
@@ -79,20 +121,20 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnParams P) {
   const int bh = logical / P.n_tiles;
   const int h = bh % P.H, b = bh / P.H;
   const int q0 = qt * FWD_BM;
-  const int qrow = q0 + w * 32 + r;
+  const int qw0 = q0 + w * 32;
+  const int qrow = qw0 + r;
   const bool qvalid = qrow < P.Sq;
+  const float sl2 = P.scale * LOG2E;
 
-  // LUT window: idx = key - q + Sq - 1, key in [0,Sk), q in [q0, q0+127]
-  const int lut_base = P.Sq - 1 - (q0 + FWD_BM - 1);
+  const int lut_base = P.Sq - 1 - (q0 + FWD_BM - 1);  // lut_s[i] = LUT[lut_base + i]
   if (HAS_BIAS) {
     const int L = P.Sq + P.Sk - 1;
     const float* lrow = P.lut + (long)h * L;
     for (int i = tid; i < P.Sk + FWD_BM + FWD_BN; i += 256) {
       const int gi = lut_base + i;
-      lut_s[i] = (gi >= 0 && gi < L) ? lrow[gi] : 0.f;
+      lut_s[i] = (gi >= 0 && gi < L) ? lrow[gi] * LOG2E : 0.f;
     }
   }
-
   bf16x8v qf[4];
   {
     const uint16_t* qp = P.q + b * P.q_sb + (long)qrow * P.q_ss + h * P.q_sh;
@@ -103,64 +145,88 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnParams P) {
       qf[s] = as_frag(t);
     }
   }
+  const long row_g = (long)(b * P.H + h) * P.Sq + qrow;
+  const uint32_t rh = DROP ? mix32(P.seed, (uint32_t)row_g) : 0u;
+  const float dscale = DROP ? 1.f / (1.f - P.p_drop) : 1.f;
 
-  f32x16 o0 = {}, o1 = {};
-  float m_run = -INFINITY, l_run = 0.f;
   int kend = P.Sk;
   if (CAUSAL) {
-    const int lim = q0 + FWD_BM - 1 + P.causal_off + 1;
+    const int lim = q0 + FWD_BM + P.causal_off;  // keys <= last row + off
     kend = lim < kend ? lim : kend;
   }
   const int ntiles = kend > 0 ? (kend + FWD_BN - 1) / FWD_BN : 0;
-  const float dscale = DROP ? 1.f / (1.f - P.p_drop) : 1.f;
-  const long drop_row = ((long)(b * P.H + h) * P.Sq + qrow) * ((P.Sk + 1) & ~1);  // Sk rounded to even
 
-  for (int kt = 0; kt < ntiles; ++kt) {
-    const int kbase = kt * FWD_BN;
-    __syncthreads();
-    // ---- stage K (row-major) and V^T into LDS
+  // ---- staging: thread t moves 16-B chunk (t & 7) of keys (t >> 3) and (t >> 3) + 32
+  const int skey = tid >> 3, sch = tid & 7;
+  u16x8 kr[2], vr[2];
+  auto load_tile = [&](int kt) {
 #pragma unroll
     for (int pass = 0; pass < 2; ++pass) {
-      const int key = (tid >> 3) + 32 * pass, ch = tid & 7;
-      const int kk = kbase + key;
-      u16x8 kv = {0, 0, 0, 0, 0, 0, 0, 0}, vv = {0, 0, 0, 0, 0, 0, 0, 0};
+      const int kk = kt * FWD_BN + skey + 32 * pass;
+      u16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+      kr[pass] = z;
+      vr[pass] = z;
       if (kk < P.Sk) {
-        kv = *reinterpret_cast<const u16x8*>(P.k + b * P.k_sb + (long)kk * P.k_ss + h * P.k_sh + ch * 8);
-        vv = *reinterpret_cast<const u16x8*>(P.v + b * P.v_sb + (long)kk * P.v_ss + h * P.v_sh + ch * 8);
+        kr[pass] = *reinterpret_cast<const u16x8*>(P.k + b * P.k_sb + (long)kk * P.k_ss + h * P.k_sh + sch * 8);
+        vr[pass] = *reinterpret_cast<const u16x8*>(P.v + b * P.v_sb + (long)kk * P.v_ss + h * P.v_sh + sch * 8);
       }
-      *reinterpret_cast<u16x8*>(Ks + key * KS_STRIDE + ch * 8) = kv;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) Vt[(ch * 8 + e) * VT_STRIDE + key] = vv[e];
     }
-    if (tid < FWD_BN) {
-      const int kk = kbase + tid;
+  };
+  auto store_tile = [&](int buf, int kt) {
+    uint16_t* Kb = KV + buf * 2 * TILE64;
+    uint16_t* Vb = Kb + TILE64;
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+      st_row(Kb, skey + 32 * pass, sch, kr[pass]);
+      st_row(Vb, skey + 32 * pass, sch, vr[pass]);
+    }
+    if (tid < FWD_BN) {  // wave 0
+      const int kk = kt * FWD_BN + tid;
       bool ok = kk < P.Sk;
       if (HAS_KPM && ok) ok = P.kpm[(long)b * P.Sk + kk] != 0;
-      kmask[tid] = ok ? 0.f : -INFINITY;
+      kmask[buf * FWD_BN + tid] = ok ? 0.f : -INFINITY;
+      const unsigned long long m = __ballot(!ok);
+      if (tid == 0) anym[buf] = m != 0ull;
     }
-    __syncthreads();
+  };
 
-    // ---- S^T = K Q^T for two 32-key subtiles
+  f32x16 o0 = {}, o1 = {};
+  float m_run = -INFINITY, l_run = 0.f;
+  if (ntiles > 0) {
+    load_tile(0);
+    store_tile(0, 0);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < ntiles; ++kt) {
+    const int cur = kt & 1;
+    const int kbase = kt * FWD_BN;
+    if (kt + 1 < ntiles) load_tile(kt + 1);
+    const uint16_t* Kb = KV + cur * 2 * TILE64;
+    const uint16_t* Vb = Kb + TILE64;
+
     f32x16 s0 = {}, s1 = {};
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      bf16x8v a0 = as_frag(*reinterpret_cast<const u16x8*>(Ks + r * KS_STRIDE + 16 * s + 8 * hh));
-      bf16x8v a1 = as_frag(*reinterpret_cast<const u16x8*>(Ks + (32 + r) * KS_STRIDE + 16 * s + 8 * hh));
-      s0 = mfma32(a0, qf[s], s0);
-      s1 = mfma32(a1, qf[s], s1);
+      s0 = mfma32(as_frag(ld_row(Kb, r, 2 * s + hh)), qf[s], s0);
+      s1 = mfma32(as_frag(ld_row(Kb, 32 + r, 2 * s + hh)), qf[s], s1);
     }
-    // ---- scale, bias, masks; running max
+    const bool tile_masked = anym[cur] != 0;
+    const bool tile_causal = CAUSAL && (kbase + FWD_BN - 1 > qw0 + P.causal_off);
     float mloc = -INFINITY;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const int kl0 = crow(i, hh), kl1 = 32 + crow(i, hh);
-      float v0 = s0[i] * P.scale + kmask[kl0];
-      float v1 = s1[i] * P.scale + kmask[kl1];
+      const int kl0 = crow(i, hh), kl1 = 32 + kl0;
+      float v0 = s0[i] * sl2, v1 = s1[i] * sl2;
       if (HAS_BIAS) {
-        v0 += lut_s[kbase + kl0 - qrow + P.Sq - 1 - lut_base];
-        v1 += lut_s[kbase + kl1 - qrow + P.Sq - 1 - lut_base];
+        const float* lb = lut_s + (kbase - qrow + P.Sq - 1 - lut_base);
+        v0 += lb[kl0];
+        v1 += lb[kl1];
       }
-      if (CAUSAL) {
+      if (tile_masked) {
+        v0 += kmask[cur * FWD_BN + kl0];
+        v1 += kmask[cur * FWD_BN + kl1];
+      }
+      if (tile_causal) {
         if (kbase + kl0 > qrow + P.causal_off) v0 = -INFINITY;
         if (kbase + kl1 > qrow + P.causal_off) v1 = -INFINITY;
       }
@@ -169,71 +235,67 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnParams P) {
       mloc = fmaxf(mloc, fmaxf(v0, v1));
     }
     mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
-    const float m_new = fmaxf(m_run, mloc);
-    const float m_use = m_new == -INFINITY ? 0.f : m_new;
-    const float alpha = exp2f((m_run - m_use) * LOG2E);
+    // deferred rescale (T13): keep the running max unless the tile max exceeds it by > 8 (log2 units)
+    const bool grow = mloc > m_run + RESCALE_THR;
+    float alpha = 1.f;
+    if (grow) {
+      alpha = exp2f(m_run - mloc);
+      m_run = mloc;
+    }
+    const float m_use = m_run == -INFINITY ? 0.f : m_run;
     float lsum = 0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const float p0 = exp2f((s0[i] - m_use) * LOG2E);
-      const float p1 = exp2f((s1[i] - m_use) * LOG2E);
-      lsum += p0 + p1;
-      s0[i] = p0;
-      s1[i] = p1;
-    }
-    if (DROP) {
-      // registers (i, i+1), i even, hold keys (2m, 2m+1): one hash per pair
-#pragma unroll
-      for (int i = 0; i < 16; i += 2) {
-        const uint32_t e0 = (uint32_t)(drop_row + kbase + crow(i, hh));
-        bool a0, a1, c0, c1;
-        keep_two(P.seed, P.thr, e0, a0, a1);
-        keep_two(P.seed, P.thr, e0 + 32u, c0, c1);
-        s0[i] = a0 ? s0[i] * dscale : 0.f;
-        s0[i + 1] = a1 ? s0[i + 1] * dscale : 0.f;
-        s1[i] = c0 ? s1[i] * dscale : 0.f;
-        s1[i + 1] = c1 ? s1[i + 1] * dscale : 0.f;
-      }
+      s0[i] = exp2f(s0[i] - m_use);
+      s1[i] = exp2f(s1[i] - m_use);
+      lsum += s0[i] + s1[i];
     }
     l_run = l_run * alpha + lsum;
-    m_run = m_new;
+    if (__any(grow)) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      o0[i] *= alpha;
-      o1[i] *= alpha;
+      for (int i = 0; i < 16; ++i) {
+        o0[i] *= alpha;
+        o1[i] *= alpha;
+      }
     }
-    // ---- O^T += V^T P^T  (P^T accumulator registers reused as the B operand)
+    if (DROP) {
+      const uint32_t tbase = (uint32_t)(kbase >> 1) * HG + (uint32_t)(2 * hh) * HG;
+#pragma unroll
+      for (int i = 0; i < 16; i += 2) {
+        const uint32_t kpg = tbase + (uint32_t)(((i & 3) >> 1) + 4 * (i >> 2)) * HG;
+        const uint32_t x0 = pair_hash(rh, kpg);
+        const uint32_t x1 = pair_hash(rh, kpg + 16u * HG);  // keys + 32
+        s0[i] = (x0 & 0xFFFFu) >= P.thr ? s0[i] * dscale : 0.f;
+        s0[i + 1] = (x0 >> 16) >= P.thr ? s0[i + 1] * dscale : 0.f;
+        s1[i] = (x1 & 0xFFFFu) >= P.thr ? s1[i] * dscale : 0.f;
+        s1[i + 1] = (x1 >> 16) >= P.thr ? s1[i + 1] * dscale : 0.f;
+      }
+    }
+    // O^T += V^T P^T
     const bf16x8v pa0 = pack8(s0, 0), pa1 = pack8(s0, 8), pb0 = pack8(s1, 0), pb1 = pack8(s1, 8);
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const uint16_t* vrow = Vt + (32 * t + r) * VT_STRIDE;
-      f32x16 acc = t == 0 ? o0 : o1;
+    for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb) {
-#pragma unroll
-        for (int sp = 0; sp < 2; ++sp) {
-          const int kb0 = kb * 32 + 16 * sp + 4 * hh;
-          u16x4 lo = *reinterpret_cast<const u16x4*>(vrow + kb0);
-          u16x4 hi = *reinterpret_cast<const u16x4*>(vrow + kb0 + 8);
-          u16x8 av = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-          const bf16x8v pf = kb == 0 ? (sp == 0 ? pa0 : pa1) : (sp == 0 ? pb0 : pb1);
-          acc = mfma32(as_frag(av), pf, acc);
-        }
+      for (int sp = 0; sp < 2; ++sp) {
+        const int kb0 = kb * 32 + 16 * sp + 4 * hh;
+        const bf16x8v pf = kb == 0 ? (sp == 0 ? pa0 : pa1) : (sp == 0 ? pb0 : pb1);
+        o0 = mfma32(ld_tr_operand(Vb, kb0, 0, r), pf, o0);
+        o1 = mfma32(ld_tr_operand(Vb, kb0, 1, r), pf, o1);
       }
-      if (t == 0) o0 = acc; else o1 = acc;
     }
+    if (kt + 1 < ntiles) store_tile(cur ^ 1, kt + 1);
+    __syncthreads();
   }
 
-  // ---- epilogue
   const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
   const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
   if (qvalid) {
     uint16_t* op = P.o_out + b * P.o_sb + (long)qrow * P.o_ss + h * P.o_sh;
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
+      const f32x16& acc = t == 0 ? o0 : o1;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const f32x16& acc = t == 0 ? o0 : o1;
         u16x4 pk = {f2bf(acc[4 * g] * inv), f2bf(acc[4 * g + 1] * inv), f2bf(acc[4 * g + 2] * inv),
                     f2bf(acc[4 * g + 3] * inv)};
         *reinterpret_cast<u16x4*>(op + 32 * t + 8 * g + 4 * hh) = pk;
@@ -241,29 +303,19 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnParams P) {
     }
     if (hh == 0) {
       const float m_use = m_run == -INFINITY ? 0.f : m_run;
-      P.lse[(long)(b * P.H + h) * P.Sq + qrow] = l_tot > 0.f ? m_use + logf(l_tot) : INFINITY;
+      P.lse[row_g] = l_tot > 0.f ? m_use + log2f(l_tot) : INFINITY;  // log2 units
     }
   }
 }
 
-// ================================================================================== backward
-constexpr int BWD_BK = 128;    // dK/dV kernel: keys per workgroup (4 waves x 32)
-constexpr int BWD_BQ = 32;     // dK/dV kernel: query rows per tile
-constexpr int QS_STRIDE = 72;  // [32 q][64 d] bf16 rows (144 B)
-constexpr int QT_STRIDE = 36;  // [64 d][32 q] bf16 rows (72 B: 8-B reads conflict-free)
-
-// ---- dQ kernel.  One workgroup = 128 query rows (4 waves x 32, query on the lane); loop over 64-key tiles.
-// S^T = K Q^T and dP^T = V dO^T (swapped, like the forward), dS^T = P^T (dP^T - delta) in registers, and
-// dQ^T += K^T dS^T takes the dS^T accumulators directly as B operands.  Also computes and stores
-// delta = rowsum(dO * O) (one dot per lane pair) for the dK/dV kernel.  No atomics.
+// ================================================================================== backward: dQ
 template <bool HAS_BIAS, bool HAS_KPM, bool CAUSAL, bool DROP>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  uint16_t* Ks = reinterpret_cast<uint16_t*>(smem);             // [64][KS_STRIDE]
-  uint16_t* Vs = Ks + FWD_BN * KS_STRIDE;                        // [64][KS_STRIDE]
-  uint16_t* Kt = Vs + FWD_BN * KS_STRIDE;                        // [64 d][VT_STRIDE]
-  float* kmask = reinterpret_cast<float*>(Kt + D * VT_STRIDE);   // [64]
-  float* lut_s = kmask + FWD_BN;                                 // [Sk + FWD_BM + FWD_BN]
+  uint16_t* KV = reinterpret_cast<uint16_t*>(smem);            // [2][K | V]
+  float* kmask = reinterpret_cast<float*>(KV + 4 * TILE64);     // [2][64]
+  int* anym = reinterpret_cast<int*>(kmask + 2 * FWD_BN);       // [4]
+  float* lut_s = reinterpret_cast<float*>(anym + 4);            // [Sk + FWD_BM + FWD_BN]
 
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 31, hh = lane >> 5;
   const int logical = xcd_remap(blockIdx.x, gridDim.x);
@@ -271,15 +323,17 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnParams P) {
   const int bh = logical / P.n_tiles;
   const int h = bh % P.H, b = bh / P.H;
   const int q0 = qt * FWD_BM;
-  const int qrow = q0 + w * 32 + r;
+  const int qw0 = q0 + w * 32;
+  const int qrow = qw0 + r;
   const bool qvalid = qrow < P.Sq;
+  const float sl2 = P.scale * LOG2E;
   const int lut_base = P.Sq - 1 - (q0 + FWD_BM - 1);
   if (HAS_BIAS) {
     const int L = P.Sq + P.Sk - 1;
     const float* lrow = P.lut + (long)h * L;
     for (int i = tid; i < P.Sk + FWD_BM + FWD_BN; i += 256) {
       const int gi = lut_base + i;
-      lut_s[i] = (gi >= 0 && gi < L) ? lrow[gi] : 0.f;
+      lut_s[i] = (gi >= 0 && gi < L) ? lrow[gi] * LOG2E : 0.f;
     }
   }
   bf16x8v qf[4], dof[4];
@@ -303,111 +357,123 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnParams P) {
     }
   }
   const float delta = dpart + __shfl_xor(dpart, 32, 64);
-  const long row_off = (long)(b * P.H + h) * P.Sq + qrow;
-  if (qvalid && hh == 0) P.delta[row_off] = delta;
-  const float lse_q = qvalid ? P.lse[row_off] : INFINITY;
+  const long row_g = (long)(b * P.H + h) * P.Sq + qrow;
+  if (qvalid && hh == 0) P.delta[row_g] = delta;
+  const float lse2 = qvalid ? P.lse[row_g] : INFINITY;
+  const uint32_t rh = DROP ? mix32(P.seed, (uint32_t)row_g) : 0u;
+  const float dscale = DROP ? 1.f / (1.f - P.p_drop) : 1.f;
 
-  f32x16 dq0 = {}, dq1 = {};
   int kend = P.Sk;
   if (CAUSAL) {
-    const int lim = q0 + FWD_BM - 1 + P.causal_off + 1;
+    const int lim = q0 + FWD_BM + P.causal_off;
     kend = lim < kend ? lim : kend;
   }
   const int ntiles = kend > 0 ? (kend + FWD_BN - 1) / FWD_BN : 0;
-  const float dscale = DROP ? 1.f / (1.f - P.p_drop) : 1.f;
-  const long drop_row = row_off * ((P.Sk + 1) & ~1);
-
-  for (int kt = 0; kt < ntiles; ++kt) {
-    const int kbase = kt * FWD_BN;
-    __syncthreads();
+  const int skey = tid >> 3, sch = tid & 7;
+  u16x8 kr[2], vr[2];
+  auto load_tile = [&](int kt) {
 #pragma unroll
     for (int pass = 0; pass < 2; ++pass) {
-      const int key = (tid >> 3) + 32 * pass, ch = tid & 7;
-      const int kk = kbase + key;
-      u16x8 kv = {0, 0, 0, 0, 0, 0, 0, 0}, vv = kv;
+      const int kk = kt * FWD_BN + skey + 32 * pass;
+      u16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+      kr[pass] = z;
+      vr[pass] = z;
       if (kk < P.Sk) {
-        kv = *reinterpret_cast<const u16x8*>(P.k + b * P.k_sb + (long)kk * P.k_ss + h * P.k_sh + ch * 8);
-        vv = *reinterpret_cast<const u16x8*>(P.v + b * P.v_sb + (long)kk * P.v_ss + h * P.v_sh + ch * 8);
+        kr[pass] = *reinterpret_cast<const u16x8*>(P.k + b * P.k_sb + (long)kk * P.k_ss + h * P.k_sh + sch * 8);
+        vr[pass] = *reinterpret_cast<const u16x8*>(P.v + b * P.v_sb + (long)kk * P.v_ss + h * P.v_sh + sch * 8);
       }
-      *reinterpret_cast<u16x8*>(Ks + key * KS_STRIDE + ch * 8) = kv;
-      *reinterpret_cast<u16x8*>(Vs + key * KS_STRIDE + ch * 8) = vv;
+    }
+  };
+  auto store_tile = [&](int buf, int kt) {
+    uint16_t* Kb = KV + buf * 2 * TILE64;
+    uint16_t* Vb = Kb + TILE64;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) Kt[(ch * 8 + e) * VT_STRIDE + key] = kv[e];
+    for (int pass = 0; pass < 2; ++pass) {
+      st_row(Kb, skey + 32 * pass, sch, kr[pass]);
+      st_row(Vb, skey + 32 * pass, sch, vr[pass]);
     }
     if (tid < FWD_BN) {
-      const int kk = kbase + tid;
+      const int kk = kt * FWD_BN + tid;
       bool ok = kk < P.Sk;
       if (HAS_KPM && ok) ok = P.kpm[(long)b * P.Sk + kk] != 0;
-      kmask[tid] = ok ? 0.f : -INFINITY;
+      kmask[buf * FWD_BN + tid] = ok ? 0.f : -INFINITY;
+      const unsigned long long m = __ballot(!ok);
+      if (tid == 0) anym[buf] = m != 0ull;
     }
-    __syncthreads();
+  };
 
+  f32x16 dq0 = {}, dq1 = {};
+  if (ntiles > 0) {
+    load_tile(0);
+    store_tile(0, 0);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < ntiles; ++kt) {
+    const int cur = kt & 1;
+    const int kbase = kt * FWD_BN;
+    if (kt + 1 < ntiles) load_tile(kt + 1);
+    const uint16_t* Kb = KV + cur * 2 * TILE64;
+    const uint16_t* Vb = Kb + TILE64;
     f32x16 s0 = {}, s1 = {}, p0 = {}, p1 = {};
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      bf16x8v a0 = as_frag(*reinterpret_cast<const u16x8*>(Ks + r * KS_STRIDE + 16 * s + 8 * hh));
-      bf16x8v a1 = as_frag(*reinterpret_cast<const u16x8*>(Ks + (32 + r) * KS_STRIDE + 16 * s + 8 * hh));
-      bf16x8v v0 = as_frag(*reinterpret_cast<const u16x8*>(Vs + r * KS_STRIDE + 16 * s + 8 * hh));
-      bf16x8v v1 = as_frag(*reinterpret_cast<const u16x8*>(Vs + (32 + r) * KS_STRIDE + 16 * s + 8 * hh));
-      s0 = mfma32(a0, qf[s], s0);
-      s1 = mfma32(a1, qf[s], s1);
-      p0 = mfma32(v0, dof[s], p0);
-      p1 = mfma32(v1, dof[s], p1);
+      s0 = mfma32(as_frag(ld_row(Kb, r, 2 * s + hh)), qf[s], s0);
+      s1 = mfma32(as_frag(ld_row(Kb, 32 + r, 2 * s + hh)), qf[s], s1);
+      p0 = mfma32(as_frag(ld_row(Vb, r, 2 * s + hh)), dof[s], p0);
+      p1 = mfma32(as_frag(ld_row(Vb, 32 + r, 2 * s + hh)), dof[s], p1);
     }
-    // dS^T = P^T * (dP^T * keep - delta), P^T = exp(S^T * scale + bias - lse)
+    const bool tile_masked = anym[cur] != 0;
+    const bool tile_causal = CAUSAL && (kbase + FWD_BN - 1 > qw0 + P.causal_off);
+    const uint32_t tbase = (uint32_t)(kbase >> 1) * HG + (uint32_t)(2 * hh) * HG;
 #pragma unroll
     for (int i = 0; i < 16; i += 2) {
-      float kf0[2] = {1.f, 1.f}, kf1[2] = {1.f, 1.f};
+      float k0a = 1.f, k0b = 1.f, k1a = 1.f, k1b = 1.f;
       if (DROP) {
-        const uint32_t e0 = (uint32_t)(drop_row + kbase + crow(i, hh));
-        bool a0, a1, c0, c1;
-        keep_two(P.seed, P.thr, e0, a0, a1);
-        keep_two(P.seed, P.thr, e0 + 32u, c0, c1);
-        kf0[0] = a0 ? dscale : 0.f;
-        kf0[1] = a1 ? dscale : 0.f;
-        kf1[0] = c0 ? dscale : 0.f;
-        kf1[1] = c1 ? dscale : 0.f;
+        const uint32_t kpg = tbase + (uint32_t)(((i & 3) >> 1) + 4 * (i >> 2)) * HG;
+        const uint32_t x0 = pair_hash(rh, kpg);
+        const uint32_t x1 = pair_hash(rh, kpg + 16u * HG);
+        k0a = (x0 & 0xFFFFu) >= P.thr ? dscale : 0.f;
+        k0b = (x0 >> 16) >= P.thr ? dscale : 0.f;
+        k1a = (x1 & 0xFFFFu) >= P.thr ? dscale : 0.f;
+        k1b = (x1 >> 16) >= P.thr ? dscale : 0.f;
       }
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const int ii = i + u;
         const int kl0 = crow(ii, hh), kl1 = 32 + kl0;
-        float v0 = s0[ii] * P.scale + kmask[kl0];
-        float v1 = s1[ii] * P.scale + kmask[kl1];
+        float v0 = s0[ii] * sl2, v1 = s1[ii] * sl2;
         if (HAS_BIAS) {
-          v0 += lut_s[kbase + kl0 - qrow + P.Sq - 1 - lut_base];
-          v1 += lut_s[kbase + kl1 - qrow + P.Sq - 1 - lut_base];
+          const float* lb = lut_s + (kbase - qrow + P.Sq - 1 - lut_base);
+          v0 += lb[kl0];
+          v1 += lb[kl1];
         }
-        if (CAUSAL) {
+        if (tile_masked) {
+          v0 += kmask[cur * FWD_BN + kl0];
+          v1 += kmask[cur * FWD_BN + kl1];
+        }
+        if (tile_causal) {
           if (kbase + kl0 > qrow + P.causal_off) v0 = -INFINITY;
           if (kbase + kl1 > qrow + P.causal_off) v1 = -INFINITY;
         }
-        const float pr0 = exp2f((v0 - lse_q) * LOG2E);
-        const float pr1 = exp2f((v1 - lse_q) * LOG2E);
-        s0[ii] = pr0 * (p0[ii] * kf0[u] - delta);
-        s1[ii] = pr1 * (p1[ii] * kf1[u] - delta);
+        const float pr0 = exp2f(v0 - lse2), pr1 = exp2f(v1 - lse2);
+        s0[ii] = pr0 * (p0[ii] * (u == 0 ? k0a : k0b) - delta);
+        s1[ii] = pr1 * (p1[ii] * (u == 0 ? k1a : k1b) - delta);
       }
     }
     // dQ^T += K^T dS^T
     const bf16x8v da0 = pack8(s0, 0), da1 = pack8(s0, 8), db0 = pack8(s1, 0), db1 = pack8(s1, 8);
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const uint16_t* krow = Kt + (32 * t + r) * VT_STRIDE;
-      f32x16 acc = t == 0 ? dq0 : dq1;
+    for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb) {
-#pragma unroll
-        for (int sp = 0; sp < 2; ++sp) {
-          const int kb0 = kb * 32 + 16 * sp + 4 * hh;
-          u16x4 lo = *reinterpret_cast<const u16x4*>(krow + kb0);
-          u16x4 hi = *reinterpret_cast<const u16x4*>(krow + kb0 + 8);
-          u16x8 av = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-          const bf16x8v bf = kb == 0 ? (sp == 0 ? da0 : da1) : (sp == 0 ? db0 : db1);
-          acc = mfma32(as_frag(av), bf, acc);
-        }
+      for (int sp = 0; sp < 2; ++sp) {
+        const int kb0 = kb * 32 + 16 * sp + 4 * hh;
+        const bf16x8v bf = kb == 0 ? (sp == 0 ? da0 : da1) : (sp == 0 ? db0 : db1);
+        dq0 = mfma32(ld_tr_operand(Kb, kb0, 0, r), bf, dq0);
+        dq1 = mfma32(ld_tr_operand(Kb, kb0, 1, r), bf, dq1);
       }
-      if (t == 0) dq0 = acc; else dq1 = acc;
     }
+    if (kt + 1 < ntiles) store_tile(cur ^ 1, kt + 1);
+    __syncthreads();
   }
   if (qvalid) {
     uint16_t* dqp = P.dq + b * P.dq_sb + (long)qrow * P.dq_ss + h * P.dq_sh;
@@ -424,23 +490,15 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnParams P) {
   }
 }
 
-// ---- dK/dV kernel.  One workgroup = 128 keys (4 waves x 32, key on the lane); loop over 32-row query tiles.
-// S = Q K^T and dPd = dO V^T come out with the key on the MFMA column, so P and dS are directly the B
-// operands of dV^T += dO^T Pd and dK^T += Q^T dS (K and V of the wave's keys stay in registers).  The
-// relative-bias gradient (sum of dS along diagonals) goes through LDS float atomics, then one global
-// atomic per LUT entry per workgroup.  Needs delta from the dQ kernel.
+// ================================================================================== backward: dK, dV
 template <bool HAS_BIAS, bool HAS_KPM, bool CAUSAL, bool DROP>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  uint16_t* Qs = reinterpret_cast<uint16_t*>(smem);        // [32][72]
-  uint16_t* dOs = Qs + BWD_BQ * QS_STRIDE;                   // [32][72]
-  uint16_t* Qt = dOs + BWD_BQ * QS_STRIDE;                   // [64][36]
-  uint16_t* dOt = Qt + D * QT_STRIDE;                        // [64][36]
-  float* lse_s = reinterpret_cast<float*>(dOt + D * QT_STRIDE);  // [32]
-  float* del_s = lse_s + BWD_BQ;                             // [32]
-  float* kmask = del_s + BWD_BQ;                             // [128]
-  float* lut_s = kmask + BWD_BK;                             // [Sq + 128]
-  float* dlut_s = lut_s + (HAS_BIAS ? P.Sq + BWD_BK : 0);    // [Sq + 128]
+  uint16_t* QD = reinterpret_cast<uint16_t*>(smem);             // [2 buffers][Q tile | dO tile] (32 rows)
+  float* rowv = reinterpret_cast<float*>(QD + 4 * TILE32);       // [2][3][32]: lse2, delta, rowhash
+  float* kmask = rowv + 2 * 3 * BWD_BQ;                          // [128]
+  float* lut_s = kmask + BWD_BK;                                 // [Sq + 128] (log2-scaled)
+  float* dlut_s = lut_s + (HAS_BIAS ? P.Sq + BWD_BK : 0);        // [Sq + 128]
 
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 31, hh = lane >> 5;
   const int logical = xcd_remap(blockIdx.x, gridDim.x);
@@ -453,12 +511,13 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnParams P) {
   const bool kvalid = key < P.Sk;
   const int L = P.Sq + P.Sk - 1;
   const int win = P.Sq + BWD_BK;
+  const float sl2 = P.scale * LOG2E;
 
   if (HAS_BIAS) {
     const float* lrow = P.lut + (long)h * L;
     for (int i = tid; i < win; i += 256) {
       const int gi = k0 + i;
-      lut_s[i] = gi < L ? lrow[gi] : 0.f;
+      lut_s[i] = gi < L ? lrow[gi] * LOG2E : 0.f;
       dlut_s[i] = 0.f;
     }
   }
@@ -483,8 +542,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnParams P) {
       vf[s] = as_frag(c);
     }
   }
-
-  f32x16 dv0 = {}, dv1 = {}, dk0 = {}, dk1 = {};
+  const uint32_t kpg = (uint32_t)(key >> 1) * HG;
+  const bool khi = key & 1;
   const float dscale = DROP ? 1.f / (1.f - P.p_drop) : 1.f;
   int qt_begin = 0;
   if (CAUSAL) {
@@ -495,66 +554,85 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnParams P) {
   const long bh_rows = (long)(b * P.H + h) * P.Sq;
   const float* lse_row = P.lse + bh_rows;
   const float* del_row = P.delta + bh_rows;
-  const long sk2 = (P.Sk + 1) & ~1;
 
-  for (int qt = qt_begin; qt < nqt; ++qt) {
-    const int q0 = qt * BWD_BQ;
-    __syncthreads();
-    {
-      const int qq = tid >> 3, ch = tid & 7;
-      const int qg = q0 + qq;
-      u16x8 a = {0, 0, 0, 0, 0, 0, 0, 0}, c = a;
-      if (qg < P.Sq) {
-        a = *reinterpret_cast<const u16x8*>(P.q + b * P.q_sb + (long)qg * P.q_ss + h * P.q_sh + ch * 8);
-        c = *reinterpret_cast<const u16x8*>(P.dout + b * P.do_sb + (long)qg * P.do_ss + h * P.do_sh + ch * 8);
-      }
-      *reinterpret_cast<u16x8*>(Qs + qq * QS_STRIDE + ch * 8) = a;
-      *reinterpret_cast<u16x8*>(dOs + qq * QS_STRIDE + ch * 8) = c;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        Qt[(ch * 8 + e) * QT_STRIDE + qq] = a[e];
-        dOt[(ch * 8 + e) * QT_STRIDE + qq] = c[e];
-      }
-      if (tid < BWD_BQ) {
-        const int qg2 = q0 + tid;
-        lse_s[tid] = qg2 < P.Sq ? lse_row[qg2] : INFINITY;
-        del_s[tid] = qg2 < P.Sq ? del_row[qg2] : 0.f;
-      }
+  const int srow = tid >> 3, sch = tid & 7;  // 32 rows x 8 chunks
+  u16x8 qr, dr;
+  float lr = 0.f, dl = 0.f;
+  uint32_t rhr = 0;
+  auto load_tile = [&](int qt) {
+    const int qg = qt * BWD_BQ + srow;
+    u16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+    qr = z;
+    dr = z;
+    if (qg < P.Sq) {
+      qr = *reinterpret_cast<const u16x8*>(P.q + b * P.q_sb + (long)qg * P.q_ss + h * P.q_sh + sch * 8);
+      dr = *reinterpret_cast<const u16x8*>(P.dout + b * P.do_sb + (long)qg * P.do_ss + h * P.do_sh + sch * 8);
     }
-    __syncthreads();
+    if (tid < BWD_BQ) {
+      const int q2 = qt * BWD_BQ + tid;
+      lr = q2 < P.Sq ? lse_row[q2] : INFINITY;
+      dl = q2 < P.Sq ? del_row[q2] : 0.f;
+      rhr = DROP ? mix32(P.seed, (uint32_t)(bh_rows + q2)) : 0u;
+    }
+  };
+  auto store_tile = [&](int buf) {
+    uint16_t* Qb = QD + buf * 2 * TILE32;
+    st_row(Qb, srow, sch, qr);
+    st_row(Qb + TILE32, srow, sch, dr);
+    if (tid < BWD_BQ) {
+      float* rv = rowv + buf * 3 * BWD_BQ;
+      rv[tid] = lr;
+      rv[BWD_BQ + tid] = dl;
+      rv[2 * BWD_BQ + tid] = __uint_as_float(rhr);
+    }
+  };
+
+  f32x16 dv0 = {}, dv1 = {}, dk0 = {}, dk1 = {};
+  if (qt_begin < nqt) {
+    load_tile(qt_begin);
+    store_tile(0);
+  }
+  __syncthreads();
+  const float km = kmask[w * 32 + r];  // 0 or -inf for this lane's key column
+  for (int qt = qt_begin; qt < nqt; ++qt) {
+    const int cur = (qt - qt_begin) & 1;
+    const int q0 = qt * BWD_BQ;
+    if (qt + 1 < nqt) load_tile(qt + 1);
+    const uint16_t* Qb = QD + cur * 2 * TILE32;
+    const uint16_t* dOb = Qb + TILE32;
+    const float* rv = rowv + cur * 3 * BWD_BQ;
 
     f32x16 sacc = {}, dpacc = {};
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      bf16x8v qa = as_frag(*reinterpret_cast<const u16x8*>(Qs + r * QS_STRIDE + 16 * s + 8 * hh));
-      bf16x8v da = as_frag(*reinterpret_cast<const u16x8*>(dOs + r * QS_STRIDE + 16 * s + 8 * hh));
-      sacc = mfma32(qa, kf[s], sacc);
-      dpacc = mfma32(da, vf[s], dpacc);
+      sacc = mfma32(as_frag(ld_row(Qb, r, 2 * s + hh)), kf[s], sacc);
+      dpacc = mfma32(as_frag(ld_row(dOb, r, 2 * s + hh)), vf[s], dpacc);
     }
+    const bool tile_causal = CAUSAL && (kw0 + 31 > q0 + P.causal_off);
     f32x16 pd, ds;
-    const float km = kmask[w * 32 + r];
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int ql = crow(i, hh);
       const int qg = q0 + ql;
-      float sv = sacc[i] * P.scale + km;
+      float sv = sacc[i] * sl2 + km;
       if (HAS_BIAS) {
         int li = key - qg + P.Sq - 1 - k0;
         li = li < 0 ? 0 : li;
         sv += lut_s[li];
       }
-      if (CAUSAL && key > qg + P.causal_off) sv = -INFINITY;
-      const float pr = exp2f((sv - lse_s[ql]) * LOG2E);  // lse = +inf for q >= Sq -> 0
+      if (tile_causal && key > qg + P.causal_off) sv = -INFINITY;
+      const float pr = exp2f(sv - rv[ql]);  // lse = +inf for q >= Sq -> 0
       float keepf = 1.f;
-      if (DROP) keepf = keep_one(P.seed, P.thr, (uint32_t)((bh_rows + qg) * sk2 + key)) ? dscale : 0.f;
+      if (DROP) {
+        const uint32_t x = pair_hash(__float_as_uint(rv[2 * BWD_BQ + ql]), kpg);
+        keepf = ((khi ? (x >> 16) : (x & 0xFFFFu)) >= P.thr) ? dscale : 0.f;
+      }
       pd[i] = pr * keepf;
-      ds[i] = pr * (dpacc[i] * keepf - del_s[ql]);
+      ds[i] = pr * (dpacc[i] * keepf - rv[BWD_BQ + ql]);
     }
     if (HAS_BIAS) {
-      // Diagonal sums of this wave's 32x32 dS tile without per-element atomics: rotate register i
-      // (tile row rho = crow(i, hh)) left by rho lanes so lane r receives element (rho, (r + rho) & 31),
-      // whose diagonal (col - row) is r (no wrap) or r - 32 (wrapped).  Masked / out-of-range
-      // elements are exactly 0 (P = 0), so no guards are needed.
+      // diagonal sums of the wave's 32x32 dS tile: rotate register i (row rho = crow(i, hh)) left by rho
+      // lanes so lane r receives element (rho, (r + rho) & 31) whose diagonal (col - row) is r or r - 32
       float pos = 0.f, neg = 0.f;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
@@ -565,32 +643,23 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnParams P) {
       pos += __shfl_xor(pos, 32, 64);
       neg += __shfl_xor(neg, 32, 64);
       if (hh == 0) {
-        const int li = w * 32 + r - q0 + P.Sq - 1;  // LUT index (window-local) of diagonal r
+        const int li = w * 32 + r - q0 + P.Sq - 1;
         atomicAdd(&dlut_s[li], pos);
         if (li >= 32) atomicAdd(&dlut_s[li - 32], neg);
       }
     }
     const bf16x8v pf0 = pack8(pd, 0), pf1 = pack8(pd, 8), sf0 = pack8(ds, 0), sf1 = pack8(ds, 8);
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const uint16_t* drow = dOt + (32 * t + r) * QT_STRIDE;
-      const uint16_t* qrw = Qt + (32 * t + r) * QT_STRIDE;
-      f32x16 av = t == 0 ? dv0 : dv1;
-      f32x16 ak = t == 0 ? dk0 : dk1;
-#pragma unroll
-      for (int sp = 0; sp < 2; ++sp) {
-        const int c0 = 16 * sp + 4 * hh;
-        u16x4 lo = *reinterpret_cast<const u16x4*>(drow + c0);
-        u16x4 hi = *reinterpret_cast<const u16x4*>(drow + c0 + 8);
-        u16x8 a8 = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-        av = mfma32(as_frag(a8), sp == 0 ? pf0 : pf1, av);
-        u16x4 lo2 = *reinterpret_cast<const u16x4*>(qrw + c0);
-        u16x4 hi2 = *reinterpret_cast<const u16x4*>(qrw + c0 + 8);
-        u16x8 b8 = {lo2.x, lo2.y, lo2.z, lo2.w, hi2.x, hi2.y, hi2.z, hi2.w};
-        ak = mfma32(as_frag(b8), sp == 0 ? sf0 : sf1, ak);
-      }
-      if (t == 0) { dv0 = av; dk0 = ak; } else { dv1 = av; dk1 = ak; }
+    for (int sp = 0; sp < 2; ++sp) {
+      const int c0 = 16 * sp + 4 * hh;
+      const bf16x8v pfv = sp == 0 ? pf0 : pf1, sfv = sp == 0 ? sf0 : sf1;
+      dv0 = mfma32(ld_tr_operand(dOb, c0, 0, r), pfv, dv0);
+      dv1 = mfma32(ld_tr_operand(dOb, c0, 1, r), pfv, dv1);
+      dk0 = mfma32(ld_tr_operand(Qb, c0, 0, r), sfv, dk0);
+      dk1 = mfma32(ld_tr_operand(Qb, c0, 1, r), sfv, dk1);
     }
+    if (qt + 1 < nqt) store_tile(cur ^ 1);
+    __syncthreads();
   }
 
   if (kvalid) {
@@ -649,6 +718,12 @@ void launch_bwd_dkdv_t(const AttnParams& p, int nblk, size_t lds, hipStream_t st
   hipLaunchKernelGGL((attn_bwd_dkdv_kernel<HB, HK, CA, DR>), dim3(nblk), dim3(256), lds, st, p);
 }
 
+size_t fwd_lds(const AttnParams& p) {
+  size_t lds = (size_t)4 * TILE64 * 2 + 2 * FWD_BN * 4 + 16;
+  if (p.lut) lds += (size_t)(p.Sk + FWD_BM + FWD_BN) * 4;
+  return lds;
+}
+
 }  // namespace
 
 extern "C" int dllm_attn_fwd(AttnParams* pp, hipStream_t st) {
@@ -656,10 +731,8 @@ extern "C" int dllm_attn_fwd(AttnParams* pp, hipStream_t st) {
   p.thr = drop_threshold(p.p_drop);
   p.n_tiles = (p.Sq + FWD_BM - 1) / FWD_BM;
   const long nblk = (long)p.n_tiles * p.H * p.B;
-  if (nblk <= 0 || nblk > 0x7fffffff) return -3;
-  size_t lds = (size_t)FWD_BN * KS_STRIDE * 2 + (size_t)D * VT_STRIDE * 2 + FWD_BN * 4;
-  if (p.lut) lds += (size_t)(p.Sk + FWD_BM + FWD_BN) * 4;
-  if (lds > 160 * 1024) return -4;
+  const size_t lds = fwd_lds(p);
+  if (nblk <= 0 || nblk > 0x7fffffff || lds > 160 * 1024) return -4;
   DISPATCH4(launch_fwd_t, p.lut != nullptr, p.kpm != nullptr, p.causal != 0, p.p_drop > 0.f, p, (int)nblk, lds, st);
   DLLM_CHECK_LAUNCH();
   return 0;
@@ -668,11 +741,10 @@ extern "C" int dllm_attn_fwd(AttnParams* pp, hipStream_t st) {
 extern "C" int dllm_attn_bwd(AttnParams* pp, hipStream_t st) {
   AttnParams p = *pp;
   p.thr = drop_threshold(p.p_drop);
-  // 1) dQ (+ delta): query blocks, same geometry as the forward
+  // 1) dQ (+ delta): query blocks, forward geometry
   p.n_tiles = (p.Sq + FWD_BM - 1) / FWD_BM;
   long nblk = (long)p.n_tiles * p.H * p.B;
-  size_t lds = (size_t)2 * FWD_BN * KS_STRIDE * 2 + (size_t)D * VT_STRIDE * 2 + FWD_BN * 4;
-  if (p.lut) lds += (size_t)(p.Sk + FWD_BM + FWD_BN) * 4;
+  size_t lds = fwd_lds(p);
   if (nblk <= 0 || nblk > 0x7fffffff || lds > 160 * 1024) return -4;
   DISPATCH4(launch_bwd_dq_t, p.lut != nullptr, p.kpm != nullptr, p.causal != 0, p.p_drop > 0.f, p, (int)nblk, lds,
             st);
@@ -680,7 +752,7 @@ extern "C" int dllm_attn_bwd(AttnParams* pp, hipStream_t st) {
   // 2) dK, dV (+ bias-LUT gradient): key blocks
   p.n_tiles = (p.Sk + BWD_BK - 1) / BWD_BK;
   nblk = (long)p.n_tiles * p.H * p.B;
-  lds = (size_t)2 * BWD_BQ * QS_STRIDE * 2 + (size_t)2 * D * QT_STRIDE * 2 + 2 * BWD_BQ * 4 + BWD_BK * 4;
+  lds = (size_t)4 * TILE32 * 2 + (size_t)2 * 3 * BWD_BQ * 4 + BWD_BK * 4;
   if (p.lut) lds += (size_t)2 * (p.Sq + BWD_BK) * 4;
   if (nblk <= 0 || nblk > 0x7fffffff || lds > 160 * 1024) return -4;
   DISPATCH4(launch_bwd_dkdv_t, p.lut != nullptr, p.kpm != nullptr, p.causal != 0, p.p_drop > 0.f, p, (int)nblk, lds,

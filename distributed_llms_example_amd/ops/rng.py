@@ -49,14 +49,25 @@ def keep_mask(seed: int, p: float, shape, device, numel_offset: int = 0) -> torc
     return keep_from_index(seed, p, idx).view(shape)
 
 
+_G = 0x9E3779B1
+_C = 0x85EBCA6B
+
+
 def attention_keep_mask(seed: int, p: float, B: int, H: int, Sq: int, Sk: int, device) -> torch.Tensor:
-    """Attention-probability mask [B, H, Sq, Sk]: element (b, h, i, j) uses index
-    ``((b*H + h)*Sq + i) * Sk2 + j`` with ``Sk2 = Sk`` rounded up to even, so keys (2m, 2m+1) of a
-    row share one hash in the kernels."""
-    sk2 = (Sk + 1) & ~1
-    rows = torch.arange(B * H * Sq, device=device, dtype=torch.int64).view(B, H, Sq, 1)
-    idx = rows * sk2 + torch.arange(Sk, device=device, dtype=torch.int64).view(1, 1, 1, Sk)
-    return keep_from_index(seed, p, idx)
+    """Attention-probability mask [B, H, Sq, Sk] (mirrors csrc/attn.hip ``attn_keep``).
+
+    Per query row ``r = (b*H + h)*Sq + i``: ``rh = mix32(seed, r)`` (computed once per row in the
+    kernels); per key pair ``kp = j >> 1``: ``x = (rh ^ kp*G) * C; x ^= x >> 16``; key ``j`` keeps iff
+    the 16-bit half ``j & 1`` of ``x`` is ``>= threshold16(p)``.  One multiply per two keys inside the
+    attention kernels instead of a full hash per element."""
+    rows = torch.arange(B * H * Sq, device=device, dtype=torch.int64)
+    rh = mix32(seed, rows).view(B, H, Sq, 1)
+    j = torch.arange(Sk, device=device, dtype=torch.int64).view(1, 1, 1, Sk)
+    x = rh ^ (((j >> 1) * _G) & _MASK)
+    x = (x * _C) & _MASK
+    x = x ^ (x >> 16)
+    half = torch.where((j & 1) == 1, x >> 16, x & 0xFFFF)
+    return half >= threshold16(p)
 
 
 def mix_host(seed: int, idx: int) -> int:
