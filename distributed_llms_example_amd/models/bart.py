@@ -18,6 +18,7 @@ import torch.nn.functional as F
 
 from ..ops import activations, attention as attn_ops, norms
 from ..ops.cross_entropy import cross_entropy
+from ..ops.linear import Linear, stacked_linear
 from ..ops.rng import default_rng
 from .config import Seq2SeqConfig
 from .output import Seq2SeqLMOutput
@@ -32,11 +33,11 @@ class BartAttention(nn.Module):
         self.head_dim = d // cfg.num_heads
         self.scaling = self.head_dim ** -0.5
         if cross:
-            self.q_proj = nn.Linear(d, d)
-            self.kv_proj = nn.Linear(d, 2 * d)
+            self.q_proj = Linear(d, d)
+            self.kv_proj = Linear(d, 2 * d)
         else:
-            self.qkv_proj = nn.Linear(d, 3 * d)
-        self.out_proj = nn.Linear(d, d)
+            self.qkv_proj = Linear(d, 3 * d)
+        self.out_proj = Linear(d, d)
 
     def project_kv(self, kv_in):
         B, S, _ = kv_in.shape
@@ -70,8 +71,8 @@ class BartLayer(nn.Module):
         if is_decoder:
             self.encoder_attn = BartAttention(cfg, cross=True)
             self.encoder_attn_layer_norm = nn.LayerNorm(d)
-        self.fc1 = nn.Linear(d, cfg.d_ff)
-        self.fc2 = nn.Linear(cfg.d_ff, d)
+        self.fc1 = Linear(d, cfg.d_ff)
+        self.fc2 = Linear(cfg.d_ff, d)
         self.final_layer_norm = nn.LayerNorm(d)
         self.cfg = cfg
 
@@ -116,6 +117,15 @@ class BartStack(nn.Module):
         self.layernorm_embedding = nn.LayerNorm(cfg.d_model)
         self.embed_scale = math.sqrt(cfg.d_model) if cfg.scale_embedding else 1.0
 
+    def cross_kv_linears(self):
+        return [layer.encoder_attn.kv_proj for layer in self.layers]
+
+    def project_cross_kv(self, enc_out):
+        """All decoder layers' cross-attention K/V in ONE GEMM (ops/linear.py stacked_linear)."""
+        B, S, _ = enc_out.shape
+        H = self.cfg.num_heads
+        return stacked_linear(enc_out, self.cross_kv_linears(), (B, S, 2, H, self.cfg.d_model // H))
+
     def forward(self, input_ids, attention_mask=None, enc_out=None, enc_mask=None, caches=None, q_offset=0,
                 cross_kv=None):
         cfg = self.cfg
@@ -128,6 +138,8 @@ class BartStack(nn.Module):
         x = x + F.embedding(pos, self.embed_positions.weight).unsqueeze(0)
         h = norms.layer_norm(x, self.layernorm_embedding.weight, self.layernorm_embedding.bias, cfg.layer_norm_epsilon)
         h = activations.dropout(h, p, default_rng().next_seed() if p > 0 else 0)
+        if self.is_decoder and cross_kv is None and enc_out is not None:
+            cross_kv = self.project_cross_kv(enc_out)
         for i, layer in enumerate(self.layers):
             h = layer(h, mask=attention_mask, enc_out=enc_out, enc_mask=enc_mask,
                       cache=caches[i] if caches is not None else None,
@@ -200,6 +212,13 @@ class BartForConditionalGeneration(nn.Module):
 
     def cross_attention_modules(self):
         return [layer.encoder_attn for layer in self.model.decoder.layers]
+
+    def project_cross_kv(self, enc_out):
+        return self.model.decoder.project_cross_kv(enc_out)
+
+    def _dllm_param_groups(self):
+        lin = self.model.decoder.cross_kv_linears()
+        return [[m.weight for m in lin], [m.bias for m in lin]]
 
     def generate(self, input_ids, attention_mask=None, **kw):
         from .generation import generate

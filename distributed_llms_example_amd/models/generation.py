@@ -106,7 +106,7 @@ def generate(model, input_ids, attention_mask=None, max_length: int | None = Non
         H, D = _head_geom(model)
         dtype = next(model.parameters()).dtype
         caches = [KVCache(N, max_length, H, D, dtype, dev) for _ in range(cfg.num_decoder_layers)]
-        cross = [m.project_kv(enc) for m in model.cross_attention_modules()]
+        cross = model.project_cross_kv(enc)
         seqs = torch.full((N, max_length), pad, dtype=torch.long, device=dev)
         seqs[:, 0] = start
         cur = 1

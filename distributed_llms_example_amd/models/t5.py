@@ -21,6 +21,7 @@ import torch.nn.functional as F
 
 from ..ops import activations, attention as attn_ops, norms
 from ..ops.cross_entropy import cross_entropy
+from ..ops.linear import Linear, stacked_linear
 from ..ops.rng import default_rng
 from .config import Seq2SeqConfig
 from .output import Seq2SeqLMOutput
@@ -43,11 +44,11 @@ class T5Attention(nn.Module):
         self.d_kv = cfg.d_kv
         inner = cfg.inner_dim
         if cross:
-            self.q = nn.Linear(cfg.d_model, inner, bias=False)
-            self.kv = nn.Linear(cfg.d_model, 2 * inner, bias=False)
+            self.q = Linear(cfg.d_model, inner, bias=False)
+            self.kv = Linear(cfg.d_model, 2 * inner, bias=False)
         else:
-            self.qkv = nn.Linear(cfg.d_model, 3 * inner, bias=False)
-        self.o = nn.Linear(inner, cfg.d_model, bias=False)
+            self.qkv = Linear(cfg.d_model, 3 * inner, bias=False)
+        self.o = Linear(inner, cfg.d_model, bias=False)
         self.has_relative_attention_bias = has_relative_attention_bias
         if has_relative_attention_bias:
             self.relative_attention_bias = nn.Embedding(cfg.relative_attention_num_buckets, cfg.num_heads)
@@ -83,8 +84,8 @@ class T5Attention(nn.Module):
 class T5DenseActDense(nn.Module):
     def __init__(self, cfg):
         super().__init__()
-        self.wi = nn.Linear(cfg.d_model, cfg.d_ff * (2 if cfg.is_gated else 1), bias=False)
-        self.wo = nn.Linear(cfg.d_ff, cfg.d_model, bias=False)
+        self.wi = Linear(cfg.d_model, cfg.d_ff * (2 if cfg.is_gated else 1), bias=False)
+        self.wo = Linear(cfg.d_ff, cfg.d_model, bias=False)
         self.act = cfg.act
         self.gated = cfg.is_gated
 
@@ -138,6 +139,14 @@ class T5Stack(nn.Module):
         self.block = nn.ModuleList([T5Block(cfg, has_bias=(i == 0), is_decoder=is_decoder) for i in range(n)])
         self.final_layer_norm = T5LayerNorm(cfg.d_model, cfg.layer_norm_epsilon)
 
+    def cross_kv_linears(self):
+        return [blk.layer[1].EncDecAttention.kv for blk in self.block]
+
+    def project_cross_kv(self, enc_out):
+        """All decoder layers' cross-attention K/V in ONE GEMM (ops/linear.py stacked_linear)."""
+        B, S, _ = enc_out.shape
+        return stacked_linear(enc_out, self.cross_kv_linears(), (B, S, 2, self.cfg.num_heads, self.cfg.d_kv))
+
     def forward(self, input_ids, attention_mask=None, enc_out=None, enc_mask=None, caches=None, q_offset=0,
                 cross_kv=None):
         cfg = self.cfg
@@ -153,6 +162,8 @@ class T5Stack(nn.Module):
         # h = dropout(embeddings); normed = block0 self-attn norm(h)
         normed, h = norms.dropout_rms_norm(x, blocks[0].layer[0].layer_norm.weight, eps, p,
                                            rng.next_seed() if p > 0 else 0)
+        if self.is_decoder and cross_kv is None and enc_out is not None:
+            cross_kv = self.project_cross_kv(enc_out)
         for i, blk in enumerate(blocks):
             subs = list(blk.layer)
             next_norms = [lyr.layer_norm.weight for lyr in subs[1:]]
@@ -184,7 +195,7 @@ class T5ForConditionalGeneration(nn.Module):
         self.encoder = T5Stack(cfg, False, self.shared)
         self.decoder = T5Stack(cfg, True, self.shared)
         if not cfg.tie_word_embeddings:
-            self.lm_head = nn.Linear(cfg.d_model, cfg.vocab_size, bias=False)
+            self.lm_head = Linear(cfg.d_model, cfg.vocab_size, bias=False)
         self.reset_parameters()
 
     # ---------------------------------------------------------------------------------- init
@@ -246,6 +257,12 @@ class T5ForConditionalGeneration(nn.Module):
 
     def cross_attention_modules(self):
         return [blk.layer[1].EncDecAttention for blk in self.decoder.block]
+
+    def project_cross_kv(self, enc_out):
+        return self.decoder.project_cross_kv(enc_out)
+
+    def _dllm_param_groups(self):
+        return [[m.weight for m in self.decoder.cross_kv_linears()]]
 
     def generate(self, input_ids, attention_mask=None, **kw):
         from .generation import generate

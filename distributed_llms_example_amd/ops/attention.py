@@ -120,6 +120,9 @@ class _AttnFn(torch.autograd.Function):
         o, lse = C.attn_fwd(q, k, v, kpm, lut, float(scale), bool(causal), float(p), int(seed))
         ctx.save_for_backward(a, b, c, o, lse, lut, kpm)
         ctx.cfg = (mode, scale, causal, p, seed, lut is not None and lut.requires_grad)
+        # ops/linear.py stacked_linear: the packed kv is a slice of a multi-layer projection and its
+        # gradient has a home in the stacked gradient buffer — write dK/dV there directly
+        ctx.grad_into = getattr(b, "_dllm_grad_into", None) if mode == "q_kv" else None
         return o
 
     @staticmethod
@@ -134,7 +137,9 @@ class _AttnFn(torch.autograd.Function):
             dq, dk, dv = da[:, :, 0], da[:, :, 1], da[:, :, 2]
         elif mode == "q_kv":
             da = torch.empty_like(a)
-            db = torch.empty_like(b)
+            gi = ctx.grad_into
+            db = gi if gi is not None and gi.shape == b.shape else torch.empty_like(b)
+            ctx.grad_into = None
             dq, dk, dv = da, db[:, :, 0], db[:, :, 1]
         else:
             dq = dk = dv = None

@@ -1,0 +1,157 @@
+"""Linear layer whose weight gradient is accumulated by the GEMM itself into the flat gradient buffer.
+
+With parameters living in FlatParams (parallel/flat.py) every ``p.grad`` is a view of one gradient
+buffer.  Through plain autograd the weight-gradient GEMM writes a fresh ``[out, in]`` tensor and
+AccumulateGrad then adds it into that view — an extra read+write of every weight gradient and one
+elementwise kernel per parameter per micro-batch (≈200 launches per T5-base step).  Here the backward
+issues ``grad.addmm_(dyᵀ, x)`` (β = 1): hipBLASLt accumulates straight into the flat buffer in its
+epilogue, and the post-accumulate hooks the gradient reducer relies on (parallel/reducer.py) are fired
+by hand because AccumulateGrad never runs for the weight.
+
+The fused path is taken only when the weight is marked by FlatParams (``_dllm_fused_wgrad``) and its
+``.grad`` is a live tensor; anything else (plain modules, ``zero_grad(set_to_none=True)``) falls back to
+ordinary autograd with identical results.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+def _fire(p: torch.Tensor) -> None:
+    for h in getattr(p, "_dllm_post_hooks", ()):
+        h(p)
+
+
+class _LinearAccumFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, params):
+        # weight/bias arrive detached (no autograd edge → no AccumulateGrad node, no double hook);
+        # ``params`` carries the Parameters themselves, whose .grad views are accumulated into below
+        ctx.save_for_backward(x)
+        ctx.weight, ctx.bias = params
+        return F.linear(x, weight, bias)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        w, bias = ctx.weight, ctx.bias
+        dx = torch.matmul(dy, w) if ctx.needs_input_grad[0] else None
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        x2 = x.reshape(-1, x.shape[-1])
+        with torch.no_grad():
+            w.grad.addmm_(dy2.t(), x2)
+            if bias is not None:
+                bias.grad.add_(dy2.sum(0))
+        _fire(w)
+        if bias is not None:
+            _fire(bias)
+        return dx, None, None, None
+
+
+def _fusable(p: torch.Tensor | None) -> bool:
+    return p is None or (getattr(p, "_dllm_fused_wgrad", False) and p.grad is not None and p.requires_grad)
+
+
+class Linear(nn.Linear):
+    """Drop-in ``nn.Linear`` (same parameters / state-dict keys / init) with GEMM-fused grad accumulation."""
+
+    def forward(self, x):
+        if torch.is_grad_enabled() and _fusable(self.weight) and _fusable(self.bias):
+            b = self.bias
+            return _LinearAccumFn.apply(x, self.weight.detach(), None if b is None else b.detach(), (self.weight, b))
+        return F.linear(x, self.weight, self.bias)
+
+
+# ------------------------------------------------------------------------------------------------
+# One GEMM for several projections of the same input (the decoder's per-layer cross-attention K/V)
+
+
+def _adjacent(ts):
+    """[t0; t1; ...] as ONE view when the tensors sit back-to-back in memory (same trailing shape),
+    else None.  FlatParams lays out grouped parameters this way (``_dllm_param_groups``)."""
+    t0 = ts[0]
+    if t0 is None or not t0.is_contiguous():
+        return None
+    tail = tuple(t0.shape[1:])
+    rows = 0
+    for t in ts:
+        if (t is None or not t.is_contiguous() or tuple(t.shape[1:]) != tail or t.dtype != t0.dtype
+                or t.data_ptr() != t0.data_ptr() + rows * (t0.numel() // t0.shape[0]) * t0.element_size()):
+            return None
+        rows += t.shape[0]
+    return t0.as_strided((rows,) + tail, t0.stride())
+
+
+class _StackedFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, W, b, ws, bs, shape):
+        y = F.linear(x, W, b)
+        n = ws[0].shape[0]
+        gbuf = torch.empty_like(y)
+        outs = []
+        for l in range(len(ws)):
+            o = y[..., l * n:(l + 1) * n].view(shape)
+            o._dllm_grad_into = gbuf[..., l * n:(l + 1) * n].view(shape)  # consumers may write dY_l here
+            outs.append(o)
+        ctx.save_for_backward(x)
+        ctx.W, ctx.gbuf, ctx.params, ctx.n = W, gbuf, (ws, bs), n
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        (x,) = ctx.saved_tensors
+        gbuf, W, n = ctx.gbuf, ctx.W, ctx.n
+        ws, bs = ctx.params
+        for l, g in enumerate(grads):
+            part = gbuf[..., l * n:(l + 1) * n]
+            if g is None:
+                part.zero_()
+                continue
+            mine = part.view(g.shape)
+            if not (g.data_ptr() == mine.data_ptr() and g.stride() == mine.stride()):
+                mine.copy_(g)  # consumer produced its own buffer
+        G2 = gbuf.view(-1, gbuf.shape[-1])
+        x2 = x.reshape(-1, x.shape[-1])
+        dx = torch.matmul(G2, W).view(x.shape) if ctx.needs_input_grad[0] else None
+        with torch.no_grad():
+            gw = _adjacent([w.grad for w in ws])
+            if gw is not None:
+                gw.addmm_(G2.t(), x2)
+            else:
+                dW = G2.t() @ x2
+                for l, w in enumerate(ws):
+                    w.grad.add_(dW[l * n:(l + 1) * n])
+            if bs[0] is not None:
+                db = G2.sum(0)
+                for l, bb in enumerate(bs):
+                    bb.grad.add_(db[l * n:(l + 1) * n])
+        ctx.gbuf = None
+        for p in list(ws) + [bb for bb in bs if bb is not None]:
+            _fire(p)
+        return dx, None, None, None, None, None
+
+
+def stacked_linear(x, mods, shape):
+    """``[mods[l](x).view(shape) for l]`` computed by ONE GEMM against the row-stacked weights.
+
+    With the weights laid out back-to-back by FlatParams the stacked weight is a view (no copy), the
+    backward is one dgrad GEMM with K = Σ n_l (instead of L GEMMs plus L-1 adds of dX) and one wgrad
+    GEMM accumulated into the flat gradient buffer; consumers that know how (ops/attention.py) write
+    their input gradient straight into the stacked gradient buffer through ``_dllm_grad_into``."""
+    ws = [m.weight for m in mods]
+    bs = [m.bias for m in mods]
+    has_b = bs[0] is not None
+    W = _adjacent(ws)
+    B_ = _adjacent(bs) if has_b else None
+    if (torch.is_grad_enabled() and W is not None and (B_ is not None or not has_b)
+            and all(_fusable(w) for w in ws) and all(_fusable(b) for b in bs)):
+        return list(_StackedFn.apply(x, W.detach(), None if B_ is None else B_.detach(), tuple(ws), tuple(bs), shape))
+    if W is None or torch.is_grad_enabled():  # an adjacent view would route all grads to ws[0]
+        W = torch.cat(ws)
+    if has_b and (B_ is None or torch.is_grad_enabled()):
+        B_ = torch.cat(bs)
+    y = F.linear(x, W, B_)
+    n = ws[0].shape[0]
+    return [y[..., l * n:(l + 1) * n].view(shape) for l in range(len(mods))]

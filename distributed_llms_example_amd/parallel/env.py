@@ -54,7 +54,9 @@ _ENV: DistEnv | None = None
 
 
 def _pick_backend(use_gpu: bool) -> str:
-    return "nccl" if use_gpu else "gloo"
+    # DLLM_DIST_BACKEND=gloo lets several ranks share one GPU (RCCL refuses duplicate devices): used to
+    # rehearse the multi-process GPU path on a 1-GPU box.
+    return os.environ.get("DLLM_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
 
 
 def init_distributed(init_method: str | None = None, rank: int | None = None, world_size: int | None = None,

@@ -18,6 +18,7 @@ loads in csrc/adamw.hip.  Tied parameters (T5 ``shared`` == ``lm_head``) appear 
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 
 import torch
@@ -45,6 +46,20 @@ class FlatParams:
             named.append((n, p))
         if reverse:
             named = named[::-1]
+        # parameters a fused op consumes as ONE stacked tensor (ops/linear.py stacked_linear, e.g. the
+        # decoder's per-layer cross-attention K/V weights) are placed back-to-back, in group order,
+        # where the group's first member would have gone
+        groups = module._dllm_param_groups() if hasattr(module, "_dllm_param_groups") else []
+        for grp in groups:
+            ids = [id(p) for p in grp]
+            pos = {id(p): i for i, (_, p) in enumerate(named)}
+            if not all(i in pos for i in ids):
+                continue
+            first = min(pos[i] for i in ids)
+            members = {id(p): (n, p) for n, p in named if id(p) in ids}
+            rest = [(n, p) for n, p in named if id(p) not in members]
+            at = sum(1 for n, p in named[:first] if id(p) not in members)
+            named = rest[:at] + [members[i] for i in ids] + rest[at:]
         if not named:
             raise ValueError("module has no trainable parameters")
         dtypes = {p.dtype for _, p in named}
@@ -69,6 +84,8 @@ class FlatParams:
                 view = self.param_buf[seg.offset:seg.offset + seg.numel].view(seg.shape)
                 view.copy_(p.data)
                 p.data = view
+                # ops/linear.py may accumulate this parameter's weight gradient inside the GEMM
+                p._dllm_fused_wgrad = os.environ.get("DLLM_FUSED_WGRAD", "1") != "0"
         self.attach_grads()
 
     # -------------------------------------------------------------------------------------------

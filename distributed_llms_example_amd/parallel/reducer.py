@@ -70,9 +70,14 @@ class GradReducer:
         self._works = []
         self._callback_queued = False
         self._hooks = []
+        self._manual = []
         if self.world > 1 and overlap:
             for i, p in enumerate(flat.params):
-                self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
+                h = self._make_hook(i)
+                self._hooks.append(p.register_post_accumulate_grad_hook(h))
+                # fired by ops/linear.py when the GEMM accumulated the gradient (AccumulateGrad skipped)
+                p._dllm_post_hooks = getattr(p, "_dllm_post_hooks", []) + [h]
+                self._manual.append(p)
 
     # --------------------------------------------------------------------------------- hooks
     def _make_hook(self, seg_index: int):
@@ -165,3 +170,6 @@ class GradReducer:
         for h in self._hooks:
             h.remove()
         self._hooks.clear()
+        for p in self._manual:
+            p._dllm_post_hooks = []
+        self._manual.clear()

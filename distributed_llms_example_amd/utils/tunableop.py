@@ -23,7 +23,8 @@ def enable(device_index: int = 0, arch: str = "gfx950") -> str | None:
     src = os.path.join(ROOT, "configs", "tunableop", f"{arch}.csv")
     if not os.path.exists(src):
         return None
-    d = tempfile.mkdtemp(prefix="dllm_tunableop_")
+    d = os.environ.get("DLLM_TUNABLEOP_DIR") or tempfile.mkdtemp(prefix="dllm_tunableop_")
+    os.makedirs(d, exist_ok=True)
     # every rank gets its own copy of the shared table (TunableOp may append to it)
     dst = os.path.join(d, f"tunableop_results{device_index}.csv")
     with open(src) as f, open(dst, "w") as g:
