@@ -7,13 +7,14 @@
 #include <c10/hip/HIPStream.h>
 
 #include "attn_params.h"
+#include "gemm_params.h"
 
 extern "C" {
 int dllm_norm_fwd(const void*, const void*, const void*, const void*, void*, void*, float*, float*, int, int, float,
                   float, uint32_t, int, int, hipStream_t);
 int dllm_norm_bwd_grid(int);
 int dllm_norm_bwd(const void*, const void*, const void*, const void*, const float*, const float*, void*, void*,
-                  float*, float*, float*, float*, int, int, float, uint32_t, int, int, hipStream_t);
+                  float*, float*, float*, float*, void*, void*, int, int, float, uint32_t, int, int, hipStream_t);
 int dllm_act_fwd(const void*, void*, long, int, int, int, float, uint32_t, int, hipStream_t);
 int dllm_act_bwd(const void*, const void*, void*, long, int, int, int, float, uint32_t, int, hipStream_t);
 int dllm_dropout(const void*, void*, long, float, uint32_t, int, hipStream_t);
@@ -26,6 +27,7 @@ int dllm_adamw(void*, float*, const void*, float*, float*, const uint8_t*, const
 int dllm_attn_fwd(AttnParams*, hipStream_t);
 int dllm_attn_bwd(AttnParams*, hipStream_t);
 int dllm_attn_params_size();
+int dllm_gemm_wgrad(const GemmWgradParams*, int, hipStream_t);
 }
 
 namespace {
@@ -87,7 +89,8 @@ std::vector<Tensor> norm_fwd(const Tensor& x, const optional<Tensor>& resid, con
 
 std::vector<Tensor> norm_bwd(const optional<Tensor>& dout_o, const optional<Tensor>& ds, const Tensor& s,
                              const Tensor& w, const optional<Tensor>& b, const optional<Tensor>& mean,
-                             const Tensor& rstd, double p, int64_t seed, int64_t kind, bool want_stream) {
+                             const Tensor& rstd, double p, int64_t seed, int64_t kind, bool want_stream,
+                             const optional<Tensor>& dw_acc, const optional<Tensor>& db_acc) {
   check_gpu(s, "s");
   TORCH_CHECK(s.dim() == 2 && s.is_contiguous(), "s must be contiguous [N, d]");
   const int N = s.size(0), d = s.size(1);
@@ -105,16 +108,26 @@ std::vector<Tensor> norm_bwd(const optional<Tensor>& dout_o, const optional<Tens
   const int G = dllm_norm_bwd_grid(N > 0 ? N : 1);
   auto f32 = s.options().dtype(at::kFloat);
   auto dw_part = at::empty({G, d}, f32);
-  auto dw = at::zeros({d}, f32);
   const bool has_b = b.has_value() && b->defined();
+  // dw_acc / db_acc: accumulate the parameter gradients in place (param dtype, contiguous, d elements)
+  const bool acc = dw_acc.has_value() && dw_acc->defined();
+  if (acc) {
+    TORCH_CHECK(dw_acc->numel() == d && dw_acc->is_contiguous() && dw_acc->scalar_type() == s.scalar_type(),
+                "dw_acc mismatch");
+    TORCH_CHECK(!has_b || (db_acc.has_value() && db_acc->defined() && db_acc->numel() == d &&
+                           db_acc->is_contiguous() && db_acc->scalar_type() == s.scalar_type()),
+                "db_acc mismatch");
+  }
+  Tensor dw = acc ? Tensor() : at::zeros({d}, f32);
   Tensor db_part = has_b ? at::empty({G, d}, f32) : Tensor();
-  Tensor db = has_b ? at::zeros({d}, f32) : Tensor();
+  Tensor db = (has_b && !acc) ? at::zeros({d}, f32) : Tensor();
   if (N > 0)
     check_rc(dllm_norm_bwd(dout.data_ptr(), dse.defined() ? dse.data_ptr() : nullptr, s.data_ptr(), w.data_ptr(),
                            kind == 1 ? mean->data_ptr<float>() : nullptr, rstd.data_ptr<float>(), dx.data_ptr(),
                            want_stream ? dstream.data_ptr() : nullptr, dw_part.data_ptr<float>(),
-                           has_b ? db_part.data_ptr<float>() : nullptr, dw.data_ptr<float>(),
-                           has_b ? db.data_ptr<float>() : nullptr, N, d, (float)p, (uint32_t)seed, (int)kind,
+                           has_b ? db_part.data_ptr<float>() : nullptr, acc ? nullptr : dw.data_ptr<float>(),
+                           (has_b && !acc) ? db.data_ptr<float>() : nullptr, acc ? dw_acc->data_ptr() : nullptr,
+                           (acc && has_b) ? db_acc->data_ptr() : nullptr, N, d, (float)p, (uint32_t)seed, (int)kind,
                            is_bf16(s), stream()),
              "norm_bwd");
   return {dx, dstream, dw, db};
@@ -342,10 +355,60 @@ std::vector<Tensor> attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& 
 
 }  // namespace
 
+// ------------------------------------------------------------------------------------------- GEMM
+// c[M][N] (+)= a^T b with a = [K][M], b = [K][N] (token-major), bf16; returns the split count used.
+bool gemm_wgrad_supported(const Tensor& a, const Tensor& b, const Tensor& c) {
+  auto ok2 = [](const Tensor& t) {
+    return t.is_cuda() && t.dim() == 2 && t.scalar_type() == at::kBFloat16 && t.stride(1) == 1 && t.stride(0) % 8 == 0 &&
+           reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0;
+  };
+  if (!ok2(a) || !ok2(b) || !ok2(c)) return false;
+  const int64_t K = a.size(0), M = a.size(1), N = b.size(1);
+  return b.size(0) == K && c.size(0) == M && c.size(1) == N && K % 64 == 0 && K > 0 && M % 256 == 0 && N % 256 == 0 &&
+         K < (1LL << 31) && M * N < (1LL << 31);
+}
+
+int64_t gemm_wgrad(const Tensor& a, const Tensor& b, Tensor& c, bool beta, int64_t variant, int64_t splits_req) {
+  TORCH_CHECK(gemm_wgrad_supported(a, b, c),
+              "gemm_wgrad: need bf16 GPU [K,M] x [K,N] -> [M,N], unit inner stride, 16-B aligned rows, K % 64 == 0, "
+              "M and N multiples of 256");
+  TORCH_CHECK(a.device() == b.device() && a.device() == c.device(), "gemm_wgrad: device mismatch");
+  const int K = a.size(0), M = a.size(1), N = b.size(1);
+  GemmWgradParams P{};
+  P.A = reinterpret_cast<const uint16_t*>(a.data_ptr());
+  P.B = reinterpret_cast<const uint16_t*>(b.data_ptr());
+  P.C = reinterpret_cast<uint16_t*>(c.data_ptr());
+  P.lda = a.stride(0);
+  P.ldb = b.stride(0);
+  P.ldc = c.stride(0);
+  P.M = M;
+  P.N = N;
+  P.K = K;
+  P.tn = N / 256;
+  P.ntiles = (M / 256) * (N / 256);
+  P.beta = beta ? 1 : 0;
+  // fill the 256 CUs once: split K until tiles x splits ~ 256, at least 4 k-stages of 64 per split
+  int splits = splits_req > 0 ? (int)splits_req : std::max(1, 256 / P.ntiles);
+  splits = std::max(1, std::min(splits, K / 256));
+  int kchunk = ((K + splits - 1) / splits + 63) / 64 * 64;
+  splits = (K + kchunk - 1) / kchunk;
+  P.kchunk = kchunk;
+  P.splits = splits;
+  Tensor ws;
+  if (splits > 1) {
+    ws = at::empty({(int64_t)splits * M * N}, a.options().dtype(at::kFloat));
+    P.ws = ws.data_ptr<float>();
+  }
+  check_rc(dllm_gemm_wgrad(&P, (int)variant, stream()), "gemm_wgrad");
+  return splits;
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gfx950 (MI355X) kernel library for distributed_llms_example_amd";
   m.def("norm_fwd", &norm_fwd);
-  m.def("norm_bwd", &norm_bwd);
+  m.def("norm_bwd", &norm_bwd, py::arg("dout"), py::arg("ds"), py::arg("s"), py::arg("w"), py::arg("b"),
+        py::arg("mean"), py::arg("rstd"), py::arg("p"), py::arg("seed"), py::arg("kind"), py::arg("want_stream"),
+        py::arg("dw_acc") = py::none(), py::arg("db_acc") = py::none());
   m.def("act_fwd", &act_fwd);
   m.def("act_bwd", &act_bwd);
   m.def("dropout_fwd", &dropout_fwd);
@@ -356,5 +419,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);
   m.def("attn_params_size", []() { return dllm_attn_params_size(); });
+  m.def("gemm_wgrad", &gemm_wgrad, "c (+)= a^T b (token-major bf16 operands)", py::arg("a"), py::arg("b"), py::arg("c"),
+        py::arg("beta") = true, py::arg("variant") = 0, py::arg("splits") = 0);
+  m.def("gemm_wgrad_supported", &gemm_wgrad_supported);
   m.attr("arch") = "gfx950";
 }

@@ -1,0 +1,255 @@
+// Weight-gradient GEMM for gfx950 (MI355X / CDNA4):  C[M][N] (+)= A^T B,  A = [K][M], B = [K][N].
+//
+// In a linear layer's backward dW[out][in] = dY^T X with dY = [tokens][out] and X = [tokens][in]: both
+// operands are token-major, so the reduction dim (tokens, K = 10^4..10^5) is the SLOW index of both — the
+// layout library GEMMs handle worst (hipBLASLt reaches 450-900 TF/s on these shapes vs ~1.3-1.5 PF/s for
+// the forward projections, profiles/r1_t5base_b64_prof10_summary.txt).  This kernel is built for it:
+//
+// * 256x256 output tile per 512-thread workgroup (8 waves as 2(M) x 4(N), 128x64 per wave = 4x2
+//   v_mfma_f32_32x32x16_bf16 accumulators), BK = 64 k-rows per stage;
+// * operand tiles go global -> LDS by LDS-DMA (global_load_lds_dwordx4, no VGPR staging) into [BK][256]
+//   images with 512-B rows; the MFMA fragments (k = 8 consecutive rows of one column per lane) come out
+//   with hardware-transposed reads (ds_read_b64_tr_b16), so neither operand is ever transposed in memory.
+//   16-B chunk c of row r lives at chunk c ^ 4(r&3): the DMA's lane-linear image is fed from pre-swizzled
+//   source addresses, and every transposed read (4 rows x 64 B per half-wave) hits 64 distinct banks;
+// * NBUF-deep LDS ring, one barrier per k-stage, counted vmcnt so the next stages' DMA stays in flight;
+// * output is small (out x in) while K is huge, so K is split over workgroups to fill all 256 CUs:
+//   each split writes an fp32 slab, a bandwidth-bound pass sums the slabs and accumulates into the bf16
+//   gradient (beta = 1: the flat gradient buffer of parallel/flat.py, no AccumulateGrad kernel).
+//   Split ids are the slow index of the XCD-remapped block id so one XCD works one K range (L2 reuse).
+#include "common.h"
+
+using namespace dllm;
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8v;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+
+#include "gemm_params.h"
+
+namespace {
+
+constexpr int BM = 256, BN = 256, NT = 512;
+
+DLLM_DEVICE int xcd_remap(int bid, int nblk) {
+  const int q = nblk / 8, r = nblk % 8, x = bid % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+}
+
+DLLM_DEVICE int crow(int reg, int hh) { return (reg & 3) + 8 * (reg >> 2) + 4 * hh; }
+
+DLLM_DEVICE int gsw(int r) { return (r & 3) << 2; }
+
+// element offset of (row r, col) in a swizzled [rows][256] bf16 image
+DLLM_DEVICE int loff(int r, int col) { return (r << 8) + (((col >> 3) ^ gsw(r)) << 3) + (col & 7); }
+
+// ds_read_b64_tr_b16: the calling lane's 16-lane group reads rows r0..r0+3 x columns c0..c0+15; group
+// lane i receives column c0 + i (row q in element q).  Lane 4q+p supplies the address of row q, cols 4p..
+DLLM_DEVICE u16x4 ld_tr(const uint16_t* T, int r0, int c0, int i) {
+  const int r = r0 + (i >> 2);
+  const int col = c0 + 4 * (i & 3);
+  s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(T + loff(r, col)));
+  return __builtin_bit_cast(u16x4, v);
+}
+
+// 32x32x16 operand for columns [cb, cb+32) and k rows [kk, kk+16): lane l holds column cb + (l & 31),
+// k = kk + 8 (l >> 5) + j — the same fragment shape for A (column = m) and B (column = n).
+DLLM_DEVICE bf16x8v frag(const uint16_t* T, int kk, int cb, int lane) {
+  const int g = lane >> 4;
+  const int r0 = kk + 8 * (g >> 1);
+  const int c0 = cb + 16 * (g & 1);
+  const u16x4 lo = ld_tr(T, r0, c0, lane & 15);
+  const u16x4 hi = ld_tr(T, r0 + 4, c0, lane & 15);
+  const u16x8 v = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+  return __builtin_bit_cast(bf16x8v, v);
+}
+
+// LDS-DMA of 16 B per lane: lane i's bytes land at LDS byte address `lds_byte` + 16 i (wave-uniform base in
+// M0).  Inline asm, not the builtin: hipcc treats the builtin as an LDS store and waits vmcnt(0) before the
+// next ds_read of ANY buffer, which would drain the ring every stage; the asm load is invisible to its
+// bookkeeping and is retired by the explicit counted waits in the k-loop (cdna_hip_programming.md §6).
+DLLM_DEVICE void glds16(const uint16_t* g, uint32_t lds_byte) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(g), "s"(lds_byte)
+               : "memory");
+}
+
+DLLM_DEVICE uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
+template <int N_>
+DLLM_DEVICE void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_) : "memory");
+}
+
+template <int BK, int NBUF>
+__global__ __launch_bounds__(NT, 1) void gemm_wgrad_kernel(GemmWgradParams P) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint16_t* lds = reinterpret_cast<uint16_t*>(smem);  // [NBUF][A tile | B tile], each [BK][256]
+  constexpr int TILE = BK * 256;
+  constexpr int PW = BK / 16;  // DMA instructions per wave per operand per stage (1 KB = 2 rows each)
+  constexpr int LPS = 2 * PW;  // per wave per stage (A + B)
+  static_assert(NBUF >= 2 && NBUF <= 4, "ring depth");
+
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, hh = lane >> 5;
+  const int wm = w >> 2, wn = w & 3;
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int s = logical / P.ntiles, t = logical % P.ntiles;
+  const int m0 = (t / P.tn) * BM, n0 = (t % P.tn) * BN;
+  const int kbeg = s * P.kchunk;
+  const int nk = min(P.kchunk, P.K - kbeg) / BK;
+
+  // this lane's DMA source: row 2*rp + hh of the stage, chunk (lane & 31) of the swizzled image
+  const uint16_t* Ag = P.A + m0 + (long)kbeg * P.lda;
+  const uint16_t* Bg = P.B + n0 + (long)kbeg * P.ldb;
+  int srow[PW], scol[PW];
+#pragma unroll
+  for (int i = 0; i < PW; ++i) {
+    const int r = 2 * (w * PW + i) + hh;
+    srow[i] = r;
+    scol[i] = ((lane & 31) ^ gsw(r)) << 3;
+  }
+  const uint32_t lds0 = lds_addr(lds);
+  auto issue = [&](int buf, int kt) {
+    const long k0 = (long)kt * BK;
+    const uint32_t Al = lds0 + (uint32_t)(buf * 2 * TILE) * 2u;
+    const uint32_t Bl = Al + TILE * 2u;
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+      const uint32_t rp = __builtin_amdgcn_readfirstlane(w * PW + i);
+      glds16(Ag + (k0 + srow[i]) * P.lda + scol[i], __builtin_amdgcn_readfirstlane(Al + rp * 1024u));
+      glds16(Bg + (k0 + srow[i]) * P.ldb + scol[i], __builtin_amdgcn_readfirstlane(Bl + rp * 1024u));
+    }
+  };
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+#pragma unroll
+  for (int p = 0; p < NBUF - 1; ++p)
+    if (p < nk) issue(p, p);
+
+  for (int it = 0; it < nk; ++it) {
+    // stage `it` must have landed; stages it+1 .. it+NBUF-2 (if issued) may stay in flight
+    const int ahead = min(NBUF - 2, nk - 1 - it);
+    if (NBUF >= 4 && ahead >= 2) wait_vm<(NBUF >= 4 ? 2 * LPS : 0)>();
+    else if (NBUF >= 3 && ahead >= 1) wait_vm<(NBUF >= 3 ? LPS : 0)>();
+    else wait_vm<0>();
+    // every wave's reads of the buffer about to be refilled are complete before anyone passes
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (it + NBUF - 1 < nk) issue((it + NBUF - 1) % NBUF, it + NBUF - 1);
+    const uint16_t* As = lds + (it % NBUF) * 2 * TILE;
+    const uint16_t* Bs = As + TILE;
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 16) {
+      bf16x8v a[4], b[2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = frag(As, kk, wm * 128 + 32 * i, lane);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) b[j] = frag(Bs, kk, wn * 64 + 32 * j, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+  }
+
+  // epilogue: lane owns column n0 + wn*64 + 32j + (lane & 31) of rows m0 + wm*128 + 32i + crow(reg)
+  const int ncol = n0 + wn * 64 + (lane & 31);
+  if (P.splits == 1) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+          const int m = m0 + wm * 128 + 32 * i + crow(reg, hh);
+          uint16_t* cp = P.C + (long)m * P.ldc + ncol + 32 * j;
+          float v = acc[i][j][reg];
+          if (P.beta) v += bf2f(*cp);
+          *cp = f2bf(v);
+        }
+  } else {
+    float* W = P.ws + (long)s * P.M * P.N;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+          const int m = m0 + wm * 128 + 32 * i + crow(reg, hh);
+          W[(long)m * P.N + ncol + 32 * j] = acc[i][j][reg];
+        }
+  }
+}
+
+// C[m][n] = bf16(sum_s ws[s][m][n] (+ C[m][n])), 8 columns per thread (N % 8 == 0)
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws, uint16_t* __restrict__ C,
+                                                            long ldc, int M, int N, int splits, int beta) {
+  const long n8 = (long)M * N / 8;
+  const long slab = (long)M * N;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+    const long e = i * 8;
+    const int m = (int)(e / N), n = (int)(e % N);
+    f32x4 a = *reinterpret_cast<const f32x4*>(ws + e);
+    f32x4 b = *reinterpret_cast<const f32x4*>(ws + e + 4);
+    for (int s = 1; s < splits; ++s) {
+      a += *reinterpret_cast<const f32x4*>(ws + s * slab + e);
+      b += *reinterpret_cast<const f32x4*>(ws + s * slab + e + 4);
+    }
+    uint16_t* cp = C + (long)m * ldc + n;
+    if (beta) {
+      const u16x8 c = *reinterpret_cast<const u16x8*>(cp);
+      a.x += bf2f(c[0]); a.y += bf2f(c[1]); a.z += bf2f(c[2]); a.w += bf2f(c[3]);
+      b.x += bf2f(c[4]); b.y += bf2f(c[5]); b.z += bf2f(c[6]); b.w += bf2f(c[7]);
+    }
+    const u16x8 o = {f2bf(a.x), f2bf(a.y), f2bf(a.z), f2bf(a.w), f2bf(b.x), f2bf(b.y), f2bf(b.z), f2bf(b.w)};
+    *reinterpret_cast<u16x8*>(cp) = o;
+  }
+}
+
+template <int BK, int NBUF>
+int launch_wgrad(const GemmWgradParams& p, hipStream_t st) {
+  const size_t lds = (size_t)NBUF * 2 * BK * 256 * 2;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm_wgrad_kernel<BK, NBUF>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+    attr = true;
+  }
+  const int nblk = p.ntiles * p.splits;
+  hipLaunchKernelGGL((gemm_wgrad_kernel<BK, NBUF>), dim3(nblk), dim3(NT), lds, st, p);
+  DLLM_CHECK_LAUNCH();
+  if (p.splits > 1) {
+    const long n8 = (long)p.M * p.N / 8;
+    const int blocks = (int)std::min<long>((n8 + 255) / 256, 2048);
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, p.ws, p.C, p.ldc, p.M, p.N, p.splits,
+                       p.beta);
+    DLLM_CHECK_LAUNCH();
+  }
+  return 0;
+}
+
+}  // namespace
+
+extern "C" int dllm_gemm_wgrad_bk() { return 64; }
+
+// variant: 0 = BK64 x 2 stages (128 KB LDS), 1 = BK32 x 4 stages (128 KB), 2 = BK32 x 3 stages (96 KB)
+extern "C" int dllm_gemm_wgrad(const GemmWgradParams* pp, int variant, hipStream_t st) {
+  const GemmWgradParams& p = *pp;
+  if (p.M % BM || p.N % BN || p.K <= 0 || p.splits < 1 || p.ntiles != (p.M / BM) * (p.N / BN)) return -4;
+  switch (variant) {
+    case 1: return launch_wgrad<32, 4>(p, st);
+    case 2: return launch_wgrad<32, 3>(p, st);
+    default: return launch_wgrad<64, 2>(p, st);
+  }
+}

@@ -163,6 +163,23 @@ __global__ __launch_bounds__(256) void col_sum_kernel(const float* __restrict__ 
   if (w == 0 && col < d) atomicAdd(out + col, red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane]);
 }
 
+// out[col] (+)= sum over ALL partial rows, stored in the parameter dtype: accumulates a norm weight/bias
+// gradient straight into its slice of the flat gradient buffer (no zero-fill, atomics, cast, or add kernel)
+template <typename T>
+__global__ __launch_bounds__(256) void col_sum_acc_kernel(const float* __restrict__ part, T* __restrict__ out, int G,
+                                                          int d) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + lane;
+  float acc = 0.f;
+  if (col < d)
+    for (int g = w; g < G; g += 4) acc += part[(size_t)g * d + col];
+  red[w][lane] = acc;
+  __syncthreads();
+  if (w == 0 && col < d)
+    Elem<T>::store(out + col, Elem<T>::load(out + col) + red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane]);
+}
+
 template <typename T, int KIND>
 int launch_fwd(const void* x, const void* resid, const void* w, const void* b, void* out, void* s_out, float* mean,
                float* rstd, int N, int d, float eps, float p, uint32_t seed, hipStream_t st) {
@@ -185,7 +202,7 @@ int launch_fwd(const void* x, const void* resid, const void* w, const void* b, v
 template <typename T, int KIND>
 int launch_bwd(const void* dout, const void* ds_extra, const void* s, const void* w, const float* mean,
                const float* rstd, void* dx, void* dstream, float* dw_part, float* db_part, float* dw, float* db,
-               int N, int d, float p, uint32_t seed, int G, hipStream_t st) {
+               void* dw_acc, void* db_acc, int N, int d, float p, uint32_t seed, int G, hipStream_t st) {
   const int chunks = (d + 255) / 256;
   dim3 grid(G), block(256);
   const size_t lds = (size_t)4 * d * sizeof(float);
@@ -201,9 +218,15 @@ int launch_bwd(const void* dout, const void* ds_extra, const void* s, const void
   else return -1;
 #undef L
   DLLM_CHECK_LAUNCH();
-  const dim3 cg((d + 63) / 64, kColChunks);
-  hipLaunchKernelGGL(col_sum_kernel, cg, dim3(256), 0, st, dw_part, dw, G, d);
-  if (db_part != nullptr) hipLaunchKernelGGL(col_sum_kernel, cg, dim3(256), 0, st, db_part, db, G, d);
+  if (dw_acc != nullptr) {
+    hipLaunchKernelGGL(col_sum_acc_kernel<T>, dim3((d + 63) / 64), dim3(256), 0, st, dw_part, (T*)dw_acc, G, d);
+    if (db_part != nullptr)
+      hipLaunchKernelGGL(col_sum_acc_kernel<T>, dim3((d + 63) / 64), dim3(256), 0, st, db_part, (T*)db_acc, G, d);
+  } else {
+    const dim3 cg((d + 63) / 64, kColChunks);
+    hipLaunchKernelGGL(col_sum_kernel, cg, dim3(256), 0, st, dw_part, dw, G, d);
+    if (db_part != nullptr) hipLaunchKernelGGL(col_sum_kernel, cg, dim3(256), 0, st, db_part, db, G, d);
+  }
   DLLM_CHECK_LAUNCH();
   return 0;
 }
@@ -230,17 +253,18 @@ extern "C" int dllm_norm_bwd_grid(int N) {
 
 extern "C" int dllm_norm_bwd(const void* dout, const void* ds_extra, const void* s, const void* w, const float* mean,
                              const float* rstd, void* dx, void* dstream, float* dw_part, float* db_part, float* dw,
-                             float* db, int N, int d, float p, uint32_t seed, int kind, int is_bf16, hipStream_t st) {
+                             float* db, void* dw_acc, void* db_acc, int N, int d, float p, uint32_t seed, int kind,
+                             int is_bf16, hipStream_t st) {
   if (d % 4 != 0) return -2;
   const int G = dllm_norm_bwd_grid(N);
   if (is_bf16) {
-    return kind ? launch_bwd<uint16_t, 1>(dout, ds_extra, s, w, mean, rstd, dx, dstream, dw_part, db_part, dw, db, N,
+    return kind ? launch_bwd<uint16_t, 1>(dout, ds_extra, s, w, mean, rstd, dx, dstream, dw_part, db_part, dw, db, dw_acc, db_acc, N,
                                           d, p, seed, G, st)
-                : launch_bwd<uint16_t, 0>(dout, ds_extra, s, w, mean, rstd, dx, dstream, dw_part, db_part, dw, db, N,
+                : launch_bwd<uint16_t, 0>(dout, ds_extra, s, w, mean, rstd, dx, dstream, dw_part, db_part, dw, db, dw_acc, db_acc, N,
                                           d, p, seed, G, st);
   }
-  return kind ? launch_bwd<float, 1>(dout, ds_extra, s, w, mean, rstd, dx, dstream, dw_part, db_part, dw, db, N, d, p,
+  return kind ? launch_bwd<float, 1>(dout, ds_extra, s, w, mean, rstd, dx, dstream, dw_part, db_part, dw, db, dw_acc, db_acc, N, d, p,
                                      seed, G, st)
-              : launch_bwd<float, 0>(dout, ds_extra, s, w, mean, rstd, dx, dstream, dw_part, db_part, dw, db, N, d, p,
+              : launch_bwd<float, 0>(dout, ds_extra, s, w, mean, rstd, dx, dstream, dw_part, db_part, dw, db, dw_acc, db_acc, N, d, p,
                                      seed, G, st);
 }

@@ -1,0 +1,33 @@
+"""Weight-gradient GEMM ``dW (+)= dYᵀ X`` on the hand-written gfx950 kernel (csrc/gemm.hip).
+
+Both operands are token-major ([tokens, features]), the reduction runs over tokens (10⁴-10⁵), and the
+result is accumulated straight into the bf16 flat gradient buffer.  Shapes the kernel does not cover
+(feature dims not multiples of 256, token counts not multiples of 64, CPU tensors) go to
+``torch.addmm`` (hipBLASLt / CPU BLAS).  ``DLLM_NATIVE_WGRAD=0`` forces the library path (A/B runs).
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+from .. import _ext
+
+_VARIANT = int(os.environ.get("DLLM_WGRAD_VARIANT", "0"))
+
+
+def _native_ok(dy2: torch.Tensor, x2: torch.Tensor, out: torch.Tensor) -> bool:
+    if os.environ.get("DLLM_NATIVE_WGRAD", "1") == "0" or not _ext.use_native(dy2):
+        return False
+    return bool(_ext.native().gemm_wgrad_supported(dy2, x2, out))
+
+
+@torch.no_grad()
+def wgrad_accumulate(out: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, beta: bool = True) -> torch.Tensor:
+    """``out (+)= dy2ᵀ @ x2`` with dy2 = [T, M], x2 = [T, N], out = [M, N]."""
+    if _native_ok(dy2, x2, out):
+        _ext.native().gemm_wgrad(dy2, x2, out, beta, _VARIANT, 0)
+        return out
+    if beta:
+        return out.addmm_(dy2.t(), x2)
+    return torch.mm(dy2.t(), x2, out=out)

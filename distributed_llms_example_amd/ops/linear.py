@@ -18,6 +18,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from .gemm import wgrad_accumulate
+
 
 def _fire(p: torch.Tensor) -> None:
     for h in getattr(p, "_dllm_post_hooks", ()):
@@ -41,7 +43,7 @@ class _LinearAccumFn(torch.autograd.Function):
         dy2 = dy.reshape(-1, dy.shape[-1])
         x2 = x.reshape(-1, x.shape[-1])
         with torch.no_grad():
-            w.grad.addmm_(dy2.t(), x2)
+            wgrad_accumulate(w.grad, dy2, x2)
             if bias is not None:
                 bias.grad.add_(dy2.sum(0))
         _fire(w)
@@ -118,7 +120,7 @@ class _StackedFn(torch.autograd.Function):
         with torch.no_grad():
             gw = _adjacent([w.grad for w in ws])
             if gw is not None:
-                gw.addmm_(G2.t(), x2)
+                wgrad_accumulate(gw, G2, x2)
             else:
                 dW = G2.t() @ x2
                 for l, w in enumerate(ws):

@@ -15,6 +15,7 @@ from __future__ import annotations
 import torch
 
 from .. import _ext
+from .linear import _fire, _fusable
 from .rng import keep_mask
 
 RMS, LAYER = 0, 1
@@ -43,8 +44,9 @@ class _NormFn(torch.autograd.Function):
     """out = norm(s) with s = (resid +) dropout(x); returns (out, s)."""
 
     @staticmethod
-    def forward(ctx, x, resid, weight, bias, eps, p, seed, kind):
+    def forward(ctx, x, resid, weight, bias, eps, p, seed, kind, params=None):
         C = _ext.native()
+        ctx.params = params
         shape = x.shape
         d = shape[-1]
         x2 = x.reshape(-1, d)
@@ -65,22 +67,22 @@ class _NormFn(torch.autograd.Function):
         ds2 = ds.reshape(-1, d) if ds is not None else None
         want_stream = has_resid and p > 0.0
         dx, dstream, dw, db = C.norm_bwd(dout2, ds2, s, weight, bias, mean, rstd, float(p), int(seed), int(kind),
-                                         want_stream)
+                                         want_stream, *_acc_targets(ctx.params))
         dx = dx.view(shape)
         # d(resid) == d(s) (pre-dropout gradient); identical to dx when p == 0
         dres = None
         if has_resid:
             dres = dstream.view(shape) if want_stream else dx
-        return (dx, dres, dw.to(weight.dtype), db.to(bias.dtype) if db is not None else None,
-                None, None, None, None)
+        return (dx, dres) + _param_grads(ctx.params, weight, bias, dw, db) + (None, None, None, None, None)
 
 
 class _NormOnlyFn(torch.autograd.Function):
     """out = norm(x) (no residual, no dropout)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, eps, kind):
+    def forward(ctx, x, weight, bias, eps, kind, params=None):
         C = _ext.native()
+        ctx.params = params
         shape = x.shape
         x2 = x.reshape(-1, shape[-1])
         out, _, mean, rstd = C.norm_fwd(x2, None, weight, bias, float(eps), 0.0, 0, int(kind), False)
@@ -94,15 +96,37 @@ class _NormOnlyFn(torch.autograd.Function):
         x2, weight, bias, mean, rstd = ctx.saved_tensors
         kind, shape = ctx.cfg
         dx, _, dw, db = C.norm_bwd(dout.reshape(-1, shape[-1]), None, x2, weight, bias, mean, rstd, 0.0, 0, int(kind),
-                                   False)
-        return dx.view(shape), dw.to(weight.dtype), db.to(bias.dtype) if db is not None else None, None, None
+                                   False, *_acc_targets(ctx.params))
+        return (dx.view(shape),) + _param_grads(ctx.params, weight, bias, dw, db) + (None, None, None)
+
+
+def _acc_targets(params):
+    """Flat-buffer gradient views the kernel accumulates into (ops/linear.py: GEMM-fused accumulation)."""
+    if params is None:
+        return None, None
+    w, b = params
+    return w.grad, (b.grad if b is not None else None)
+
+
+def _param_grads(params, weight, bias, dw, db):
+    if params is not None:  # accumulated in place by the kernel; AccumulateGrad never runs for them
+        for q in params:
+            if q is not None:
+                _fire(q)
+        return None, None
+    return dw.to(weight.dtype), (db.to(bias.dtype) if db is not None else None)
 
 
 def _norm(x, resid, weight, bias, eps, p, seed, kind):
     if _ext.use_native(x):
+        params = None
+        if torch.is_grad_enabled() and _fusable(weight) and _fusable(bias):
+            params = (weight, bias)
+            weight = weight.detach()
+            bias = bias.detach() if bias is not None else None
         if resid is None and p == 0.0:
-            return _NormOnlyFn.apply(x, weight, bias, eps, kind), x
-        return _NormFn.apply(x, resid, weight, bias, eps, p, seed, kind)
+            return _NormOnlyFn.apply(x, weight, bias, eps, kind, params), x
+        return _NormFn.apply(x, resid, weight, bias, eps, p, seed, kind, params)
     return _reference(x, resid, weight, bias, eps, p, seed, kind)
 
 

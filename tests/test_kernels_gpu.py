@@ -228,3 +228,52 @@ def test_attention_packed_qkv_grad():
     (o2.float().sum()).backward()
     ref2.sum().backward()
     assert _rel(kvin.grad, kr.grad) < 3e-2 and _rel(q.grad, qr.grad) < 3e-2
+
+
+# ------------------------------------------------------------------------------------ wgrad GEMM
+@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("K,M,N,beta,lda_pad", [
+    (4096, 768, 768, True, 0),      # t5-base o-proj shape class (many splits)
+    (8192, 768, 3072, False, 0),    # wi wgrad, decoder token count
+    (2048, 256, 512, True, 64),     # strided A (a column slice of a wider activation)
+    (960, 512, 256, True, 0),       # K not a multiple of the split chunk: short last split
+    (256, 1024, 2304, False, 0),    # tiles >= CUs / few k-stages: splits == 1, direct bf16 epilogue
+])
+def test_gemm_wgrad(variant, K, M, N, beta, lda_pad):
+    torch.manual_seed(0)
+    a_full = torch.randn(K, M + lda_pad, device=DEV, dtype=torch.bfloat16)
+    a = a_full[:, lda_pad:] if lda_pad else a_full
+    b = torch.randn(K, N, device=DEV, dtype=torch.bfloat16)
+    c0 = torch.randn(M, N, device=DEV, dtype=torch.bfloat16)
+    c = c0.clone()
+    C = _ext.native()
+    assert C.gemm_wgrad_supported(a, b, c)
+    C.gemm_wgrad(a, b, c, beta, variant, 0)
+    ref = a.float().t() @ b.float() + (c0.float() if beta else 0)
+    assert _rel(c, ref) < 5e-3, _rel(c, ref)
+    _close(c, ref, rtol=2e-2, atol=2e-2 * ref.abs().mean().item(), msg="wgrad")
+
+
+def test_gemm_wgrad_explicit_splits_match():
+    torch.manual_seed(1)
+    a = torch.randn(4096, 512, device=DEV, dtype=torch.bfloat16)
+    b = torch.randn(4096, 768, device=DEV, dtype=torch.bfloat16)
+    outs = []
+    for s in (1, 3, 16):
+        c = torch.zeros(512, 768, device=DEV, dtype=torch.bfloat16)
+        _ext.native().gemm_wgrad(a, b, c, False, 0, s)
+        outs.append(c.float())
+    ref = a.float().t() @ b.float()
+    for o in outs:
+        assert _rel(o, ref) < 5e-3
+
+
+def test_linear_wgrad_path_uses_native_gemm():
+    from distributed_llms_example_amd.ops.gemm import _native_ok, wgrad_accumulate
+    dy = torch.randn(1024, 768, device=DEV, dtype=torch.bfloat16)
+    x = torch.randn(1024, 256, device=DEV, dtype=torch.bfloat16)
+    g = torch.zeros(768, 256, device=DEV, dtype=torch.bfloat16)
+    assert _native_ok(dy, x, g)
+    wgrad_accumulate(g, dy, x)
+    wgrad_accumulate(g, dy, x)
+    assert _rel(g, 2 * (dy.float().t() @ x.float())) < 5e-3
