@@ -30,6 +30,7 @@
 //   of dS via a register shear + 2 LDS atomics per lane per tile.
 #include "common.h"
 #include "attn_params.h"
+#include <stdlib.h>
 
 using namespace dllm;
 
@@ -107,8 +108,8 @@ DLLM_DEVICE uint32_t pair_hash(uint32_t rh, uint32_t kpg) {
 }
 
 // ================================================================================== forward
-template <bool HAS_BIAS, bool HAS_KPM, bool CAUSAL, bool DROP>
-__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
+template <bool HAS_BIAS, bool HAS_KPM, bool CAUSAL, bool DROP, int OCC = 2>
+__global__ __launch_bounds__(256, OCC) void attn_fwd_kernel(AttnParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint16_t* KV = reinterpret_cast<uint16_t*>(smem);            // [2 buffers][K tile | V tile]
   float* kmask = reinterpret_cast<float*>(KV + 4 * TILE64);     // [2][64]
@@ -309,8 +310,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
 }
 
 // ================================================================================== backward: dQ
-template <bool HAS_BIAS, bool HAS_KPM, bool CAUSAL, bool DROP>
-__global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnParams P) {
+template <bool HAS_BIAS, bool HAS_KPM, bool CAUSAL, bool DROP, int OCC = 2>
+__global__ __launch_bounds__(256, OCC) void attn_bwd_dq_kernel(AttnParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint16_t* KV = reinterpret_cast<uint16_t*>(smem);            // [2][K | V]
   float* kmask = reinterpret_cast<float*>(KV + 4 * TILE64);     // [2][64]
@@ -705,13 +706,27 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnParams P) {
     }                                                                                   \
   } while (0)
 
+// occupancy experiment knob (DLLM_ATTN_OCC=3: 3 workgroups per CU for the forward and dQ kernels)
+int attn_occ() {
+  static int occ = [] {
+    const char* e = getenv("DLLM_ATTN_OCC");
+    return e && atoi(e) == 3 ? 3 : 2;
+  }();
+  return occ;
+}
 template <bool HB, bool HK, bool CA, bool DR>
 void launch_fwd_t(const AttnParams& p, int nblk, size_t lds, hipStream_t st) {
-  hipLaunchKernelGGL((attn_fwd_kernel<HB, HK, CA, DR>), dim3(nblk), dim3(256), lds, st, p);
+  if (attn_occ() == 3)
+    hipLaunchKernelGGL((attn_fwd_kernel<HB, HK, CA, DR, 3>), dim3(nblk), dim3(256), lds, st, p);
+  else
+    hipLaunchKernelGGL((attn_fwd_kernel<HB, HK, CA, DR, 2>), dim3(nblk), dim3(256), lds, st, p);
 }
 template <bool HB, bool HK, bool CA, bool DR>
 void launch_bwd_dq_t(const AttnParams& p, int nblk, size_t lds, hipStream_t st) {
-  hipLaunchKernelGGL((attn_bwd_dq_kernel<HB, HK, CA, DR>), dim3(nblk), dim3(256), lds, st, p);
+  if (attn_occ() == 3)
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<HB, HK, CA, DR, 3>), dim3(nblk), dim3(256), lds, st, p);
+  else
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<HB, HK, CA, DR, 2>), dim3(nblk), dim3(256), lds, st, p);
 }
 template <bool HB, bool HK, bool CA, bool DR>
 void launch_bwd_dkdv_t(const AttnParams& p, int nblk, size_t lds, hipStream_t st) {

@@ -403,6 +403,10 @@ int64_t gemm_wgrad(const Tensor& a, const Tensor& b, Tensor& c, bool beta, int64
   return splits;
 }
 
+namespace dllm {
+void bind_reducer(pybind11::module& m);  // csrc/reducer.cpp
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gfx950 (MI355X) kernel library for distributed_llms_example_amd";
   m.def("norm_fwd", &norm_fwd);
@@ -422,5 +426,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_wgrad", &gemm_wgrad, "c (+)= a^T b (token-major bf16 operands)", py::arg("a"), py::arg("b"), py::arg("c"),
         py::arg("beta") = true, py::arg("variant") = 0, py::arg("splits") = 0);
   m.def("gemm_wgrad_supported", &gemm_wgrad_supported);
+  dllm::bind_reducer(m);
   m.attr("arch") = "gfx950";
 }

@@ -166,18 +166,29 @@ __global__ __launch_bounds__(256) void col_sum_kernel(const float* __restrict__ 
 // out[col] (+)= sum over ALL partial rows, stored in the parameter dtype: accumulates a norm weight/bias
 // gradient straight into its slice of the flat gradient buffer (no zero-fill, atomics, cast, or add kernel)
 template <typename T>
-__global__ __launch_bounds__(256) void col_sum_acc_kernel(const float* __restrict__ part, T* __restrict__ out, int G,
-                                                          int d) {
-  __shared__ float red[4][64];
+__global__ __launch_bounds__(1024) void col_sum_acc_kernel(const float* __restrict__ part, T* __restrict__ out, int G,
+                                                           int d) {
+  // 16 waves x 64 columns; each wave sums rows w, w+16, ... with 8 independent loads in flight
+  __shared__ float red[16][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int col = blockIdx.x * 64 + lane;
-  float acc = 0.f;
-  if (col < d)
-    for (int g = w; g < G; g += 4) acc += part[(size_t)g * d + col];
-  red[w][lane] = acc;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (col < d) {
+    int g = w;
+    for (; g + 16 * 7 < G; g += 16 * 8) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc[u] += part[(size_t)(g + 16 * u) * d + col];
+    }
+    for (; g < G; g += 16) acc[0] += part[(size_t)g * d + col];
+  }
+  red[w][lane] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
   __syncthreads();
-  if (w == 0 && col < d)
-    Elem<T>::store(out + col, Elem<T>::load(out + col) + red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane]);
+  if (w == 0 && col < d) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s += red[i][lane];
+    Elem<T>::store(out + col, Elem<T>::load(out + col) + s);
+  }
 }
 
 template <typename T, int KIND>
@@ -219,9 +230,9 @@ int launch_bwd(const void* dout, const void* ds_extra, const void* s, const void
 #undef L
   DLLM_CHECK_LAUNCH();
   if (dw_acc != nullptr) {
-    hipLaunchKernelGGL(col_sum_acc_kernel<T>, dim3((d + 63) / 64), dim3(256), 0, st, dw_part, (T*)dw_acc, G, d);
+    hipLaunchKernelGGL(col_sum_acc_kernel<T>, dim3((d + 63) / 64), dim3(1024), 0, st, dw_part, (T*)dw_acc, G, d);
     if (db_part != nullptr)
-      hipLaunchKernelGGL(col_sum_acc_kernel<T>, dim3((d + 63) / 64), dim3(256), 0, st, db_part, (T*)db_acc, G, d);
+      hipLaunchKernelGGL(col_sum_acc_kernel<T>, dim3((d + 63) / 64), dim3(1024), 0, st, db_part, (T*)db_acc, G, d);
   } else {
     const dim3 cg((d + 63) / 64, kColChunks);
     hipLaunchKernelGGL(col_sum_kernel, cg, dim3(256), 0, st, dw_part, dw, G, d);

@@ -1,0 +1,160 @@
+// Native bucketed data-parallel gradient reducer (the MI355X counterpart of torch DDP's C++ Reducer,
+// torch/csrc/distributed/c10d/reducer.cpp, which the reference reaches through HF Trainer / Accelerate).
+//
+// Works on the flat gradient buffer of parallel/flat.py: bucket b is the contiguous slice
+// [bounds[2b], bounds[2b+1]) of ONE buffer ("gradient as bucket view"), so a bucket's all-reduce runs in
+// place with no flatten/unflatten copies.  Readiness is tracked per flat segment:
+//   * post hooks on each parameter's AccumulateGrad node (registered here, in C++, like DDP) fire when
+//     autograd has accumulated that parameter's gradient;
+//   * parameters whose gradient is accumulated INSIDE a GEMM/norm kernel (ops/linear.py, ops/norms.py —
+//     AccumulateGrad never runs for them) call mark_ready() from Python.
+// A bucket is launched the moment its last segment is ready, strictly in bucket order on every rank (RCCL
+// requires the same collective order everywhere), as an async all_reduce on the process group
+// (ProcessGroupNCCL = RCCL over xGMI on ROCm: the collective runs on RCCL's own stream while backward
+// keeps computing).  The first hook of a backward queues finalize() on the autograd engine; finalize
+// launches leftovers (unused parameters) and makes the compute stream wait on the RCCL work — no host
+// synchronisation on the GPU path.  Averaging uses ReduceOp::AVG (RCCL) or SUM + one scale (gloo).
+#include <torch/extension.h>
+#include <torch/csrc/autograd/engine.h>
+#include <torch/csrc/autograd/functions/accumulate_grad.h>
+#include <torch/csrc/autograd/utils/lambda_post_hook.h>
+#include <torch/csrc/distributed/c10d/ProcessGroup.hpp>
+
+#include <mutex>
+
+namespace dllm {
+
+class NativeReducer {
+ public:
+  NativeReducer(at::Tensor grad_buf, std::vector<int64_t> bounds, std::vector<int64_t> seg_bucket,
+                c10::intrusive_ptr<c10d::ProcessGroup> pg, bool average, bool use_avg_op)
+      : grad_buf_(std::move(grad_buf)),
+        bounds_(std::move(bounds)),
+        seg_bucket_(std::move(seg_bucket)),
+        pg_(std::move(pg)),
+        average_(average),
+        use_avg_op_(use_avg_op) {
+    TORCH_CHECK(bounds_.size() % 2 == 0 && !bounds_.empty(), "bounds must be [start0, end0, start1, end1, ...]");
+    TORCH_CHECK(grad_buf_.dim() == 1 && grad_buf_.is_contiguous(), "grad_buf must be a contiguous 1-D buffer");
+    const int64_t nb = (int64_t)bounds_.size() / 2;
+    counts_.assign(nb, 0);
+    for (int64_t b : seg_bucket_) {
+      TORCH_CHECK(b >= 0 && b < nb, "segment bucket index out of range");
+      counts_[b] += 1;
+    }
+    reset_state();
+  }
+
+  // Register C++ post hooks on the AccumulateGrad node of every parameter (index = flat segment index).
+  void attach_hooks(const std::vector<at::Tensor>& params) {
+    TORCH_CHECK(params.size() == seg_bucket_.size(), "one parameter per flat segment expected");
+    for (size_t i = 0; i < params.size(); ++i) {
+      auto acc = torch::autograd::impl::grad_accumulator(params[i]);
+      TORCH_CHECK(acc, "parameter ", i, " has no grad accumulator (requires_grad=False?)");
+      const int64_t seg = (int64_t)i;
+      acc->add_post_hook(std::make_unique<torch::autograd::utils::LambdaPostHook>(
+          [this, seg](const torch::autograd::variable_list& outputs, const torch::autograd::variable_list&) {
+            this->mark_ready(seg);
+            return outputs;
+          }));
+      grad_accs_.push_back(std::move(acc));
+    }
+  }
+
+  void mark_ready(int64_t seg) {
+    std::lock_guard<std::mutex> g(mu_);
+    if (!enabled_) return;
+    TORCH_CHECK(seg >= 0 && seg < (int64_t)seg_bucket_.size(), "segment index out of range");
+    if (!callback_queued_) {
+      callback_queued_ = true;
+      torch::autograd::Engine::get_default_engine().queue_callback([this] { this->finalize(); });
+    }
+    const int64_t b = seg_bucket_[seg];
+    if (--pending_[b] == 0) {
+      ready_[b] = true;
+      launch_ready_locked();
+    }
+  }
+
+  // End of backward (queued on the engine): launch leftovers in order, order the compute stream after them.
+  void finalize() {
+    std::lock_guard<std::mutex> g(mu_);
+    const int64_t nb = num_buckets();
+    while (next_ < nb) launch_locked(next_++);
+    for (auto& w : works_) w->wait();
+    works_.clear();
+    if (average_ && !use_avg_op_) grad_buf_.div_(pg_->getSize());
+    reset_state();
+  }
+
+  // train-task path: one coalesced all-reduce of the whole buffer, no hooks involved
+  void sync_all() {
+    std::vector<at::Tensor> ts{grad_buf_};
+    c10d::AllreduceOptions opts;
+    opts.reduceOp = use_avg_op_ && average_ ? c10d::ReduceOp::AVG : c10d::ReduceOp::SUM;
+    pg_->allreduce(ts, opts)->wait();
+    if (average_ && !use_avg_op_) grad_buf_.div_(pg_->getSize());
+  }
+
+  void set_enabled(bool e) {
+    std::lock_guard<std::mutex> g(mu_);
+    enabled_ = e;
+  }
+  bool enabled() const { return enabled_; }
+  int64_t num_buckets() const { return (int64_t)bounds_.size() / 2; }
+  int64_t launched() const { return next_; }
+  void detach() { grad_accs_.clear(); }
+
+ private:
+  void reset_state() {
+    pending_ = counts_;
+    ready_.assign(counts_.size(), false);
+    next_ = 0;
+    callback_queued_ = false;
+  }
+
+  void launch_locked(int64_t b) {
+    const int64_t s = bounds_[2 * b], e = bounds_[2 * b + 1];
+    std::vector<at::Tensor> ts{grad_buf_.narrow(0, s, e - s)};
+    c10d::AllreduceOptions opts;
+    opts.reduceOp = use_avg_op_ && average_ ? c10d::ReduceOp::AVG : c10d::ReduceOp::SUM;
+    works_.push_back(pg_->allreduce(ts, opts));
+  }
+
+  void launch_ready_locked() {
+    const int64_t nb = num_buckets();
+    while (next_ < nb && ready_[next_]) launch_locked(next_++);
+  }
+
+  at::Tensor grad_buf_;
+  std::vector<int64_t> bounds_, seg_bucket_, counts_, pending_;
+  std::vector<bool> ready_;
+  c10::intrusive_ptr<c10d::ProcessGroup> pg_;
+  bool average_, use_avg_op_;
+  bool enabled_ = true;
+  bool callback_queued_ = false;
+  int64_t next_ = 0;
+  std::vector<c10::intrusive_ptr<c10d::Work>> works_;
+  std::vector<std::shared_ptr<torch::autograd::Node>> grad_accs_;
+  std::mutex mu_;
+};
+
+void bind_reducer(pybind11::module& m) {
+  namespace py = pybind11;
+  py::class_<NativeReducer, std::shared_ptr<NativeReducer>>(m, "NativeReducer")
+      .def(py::init<at::Tensor, std::vector<int64_t>, std::vector<int64_t>, c10::intrusive_ptr<c10d::ProcessGroup>,
+                    bool, bool>(),
+           py::arg("grad_buf"), py::arg("bounds"), py::arg("seg_bucket"), py::arg("process_group"),
+           py::arg("average") = true, py::arg("use_avg_op") = true)
+      .def("attach_hooks", &NativeReducer::attach_hooks)
+      .def("mark_ready", &NativeReducer::mark_ready)
+      .def("finalize", &NativeReducer::finalize, py::call_guard<py::gil_scoped_release>())
+      .def("sync_all", &NativeReducer::sync_all, py::call_guard<py::gil_scoped_release>())
+      .def("set_enabled", &NativeReducer::set_enabled)
+      .def("enabled", &NativeReducer::enabled)
+      .def("num_buckets", &NativeReducer::num_buckets)
+      .def("launched", &NativeReducer::launched)
+      .def("detach", &NativeReducer::detach);
+}
+
+}  // namespace dllm

@@ -17,16 +17,22 @@ Replaces torch DDP's C++ Reducer that the reference reaches through HF Trainer /
 * ``no_sync()`` for gradient accumulation (HF Trainer trainer.py:1750-1757);
 * ``overlap=False`` → one coalesced all-reduce after backward (train-task semantics, same math).
 
-The C++ implementation of the same bucket/launch policy (csrc/reducer.cpp, ``native=True``) drives
-the c10d ProcessGroup from native code; this Python class is the orchestration both share.
+Two engines implement the same bucket/launch policy: the native one (csrc/reducer.cpp,
+``NativeReducer``: C++ post hooks on the AccumulateGrad nodes, bucket state machine and c10d
+``ProcessGroup::allreduce`` launches in C++ — the counterpart of DDP's C++ Reducer) is used whenever the
+extension is built (``DLLM_NATIVE_REDUCER=0`` selects the Python engine below, kept as the readable
+reference and for A/B tests).  Bucket layout is computed here once and handed to either engine.
 """
 from __future__ import annotations
 
 import contextlib
 
+import os
+
 import torch
 import torch.distributed as dist
 
+from .. import _ext
 from .flat import FlatParams
 
 DEFAULT_BUCKET_MB = 128.0
@@ -35,7 +41,8 @@ FIRST_BUCKET_MB = 1.0
 
 class GradReducer:
     def __init__(self, flat: FlatParams, group=None, bucket_mb: float = DEFAULT_BUCKET_MB,
-                 first_bucket_mb: float = FIRST_BUCKET_MB, overlap: bool = True, average: bool = True):
+                 first_bucket_mb: float = FIRST_BUCKET_MB, overlap: bool = True, average: bool = True,
+                 native: bool | None = None):
         self.flat = flat
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -71,7 +78,21 @@ class GradReducer:
         self._callback_queued = False
         self._hooks = []
         self._manual = []
-        if self.world > 1 and overlap:
+        self.native = None
+        if native is None:
+            native = os.environ.get("DLLM_NATIVE_REDUCER", "1") != "0" and _ext.native() is not None
+        if native and self.world > 1:
+            pg = group if group is not None else dist.distributed_c10d._get_default_group()
+            bounds = [x for se in self.buckets for x in se]
+            self.native = _ext.native().NativeReducer(flat.grad_buf, bounds, self.seg_bucket, pg, average,
+                                                      self.backend == "nccl")
+            if overlap:
+                self.native.attach_hooks(list(flat.params))
+                for i, p in enumerate(flat.params):
+                    p._dllm_post_hooks = getattr(p, "_dllm_post_hooks", []) + [
+                        (lambda _q, i=i, nat=self.native: nat.mark_ready(i))]
+                    self._manual.append(p)
+        elif self.world > 1 and overlap:
             for i, p in enumerate(flat.params):
                 h = self._make_hook(i)
                 self._hooks.append(p.register_post_accumulate_grad_hook(h))
@@ -130,14 +151,21 @@ class GradReducer:
     def no_sync(self):
         prev = self.enabled
         self.enabled = False
+        if self.native is not None:
+            self.native.set_enabled(False)
         try:
             yield
         finally:
             self.enabled = prev
+            if self.native is not None:
+                self.native.set_enabled(prev)
 
     def sync_now(self):
         """Non-overlapped path (train-task semantics): one coalesced all-reduce of all gradients."""
         if self.world <= 1:
+            return
+        if self.native is not None:
+            self.native.sync_all()
             return
         g = self.flat.grad_buf
         if self.average and self.backend == "nccl":
@@ -173,3 +201,5 @@ class GradReducer:
         for p in self._manual:
             p._dllm_post_hooks = []
         self._manual.clear()
+        if self.native is not None:
+            self.native.detach()

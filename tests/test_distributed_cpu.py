@@ -54,7 +54,7 @@ def run_ranks(fn, world=2):
     return out
 
 
-def _grad_case(rank, world, overlap=True, ga=1, bucket_mb=0.05):
+def _grad_case(rank, world, overlap=True, ga=1, bucket_mb=0.05, native=None):
     from distributed_llms_example_amd.models import build_model
     from distributed_llms_example_amd.parallel.env import DistEnv
     from distributed_llms_example_amd.train.engine import TrainEngine
@@ -66,7 +66,11 @@ def _grad_case(rank, world, overlap=True, ga=1, bucket_mb=0.05):
         with torch.no_grad():
             for p in model.parameters():
                 p.add_(1.0)
+    if native is not None:
+        os.environ["DLLM_NATIVE_REDUCER"] = "1" if native else "0"
     eng = TrainEngine(model, env, lr=1e-3, dtype=torch.float32, bucket_mb=bucket_mb, overlap=overlap)
+    if native:
+        assert eng.reducer.native is not None
     eng.train(False)  # no dropout: deterministic comparison
     g = torch.Generator().manual_seed(7)
     ids = torch.randint(3, 500, (4 * world, 10), generator=g)
@@ -96,9 +100,16 @@ def _reference_grad(world):
     return flat.grad_buf.clone()
 
 
+def _native_available():
+    from distributed_llms_example_amd import _ext
+    return _ext.native() is not None
+
+
+@pytest.mark.parametrize("native", [False, pytest.param(True, marks=pytest.mark.skipif(
+    not _native_available(), reason="native extension not built"))])
 @pytest.mark.parametrize("overlap", [True, False])
-def test_reducer_matches_single_process(overlap):
-    out = run_ranks(functools.partial(_grad_case, overlap=overlap))
+def test_reducer_matches_single_process(overlap, native):
+    out = run_ranks(functools.partial(_grad_case, overlap=overlap, native=native))
     ref = _reference_grad(2)
     g0, p0, nb = (torch.as_tensor(x) if not isinstance(x, int) else x for x in out[0])
     g1, p1, _ = (torch.as_tensor(x) if not isinstance(x, int) else x for x in out[1])
@@ -108,8 +119,10 @@ def test_reducer_matches_single_process(overlap):
     torch.testing.assert_close(g0, ref, atol=1e-5, rtol=1e-4)
 
 
-def test_grad_accumulation_no_sync():
-    out = run_ranks(functools.partial(_grad_case, overlap=True, ga=2))
+@pytest.mark.parametrize("native", [False, pytest.param(True, marks=pytest.mark.skipif(
+    not _native_available(), reason="native extension not built"))])
+def test_grad_accumulation_no_sync(native):
+    out = run_ranks(functools.partial(_grad_case, overlap=True, ga=2, native=native))
     ref = _reference_grad(2)
     a, b = torch.as_tensor(out[0][0]), torch.as_tensor(out[1][0])
     torch.testing.assert_close(a, b)

@@ -68,17 +68,19 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = True) -> str:
         if force or _newer([src] + headers, obj):
             jobs_list.append([HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-ffp-contract=fast",
                               "-munsafe-fp-atomics", "-I", CSRC, "-c", src, "-o", obj])
-    bind_src = os.path.join(CSRC, "bind.cpp")
-    bind_obj = os.path.join(BUILD, "bind.cpp.o")
-    objs.append(bind_obj)
-    if force or _newer([bind_src] + headers, bind_obj):
-        cmd = [CXX, "-O2", "-fPIC", "-std=c++17", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DUSE_ROCM=1",
-               "-D__HIP_PLATFORM_AMD__=1", "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H",
-               "-Wno-deprecated-declarations", "-I", CSRC, "-I", py_inc]
-        for i in inc:
-            cmd += ["-I", i]
-        cmd += ["-c", bind_src, "-o", bind_obj]
-        jobs_list.append(cmd)
+    # host C++ (torch + pybind11 glue, native runtime pieces): every csrc/*.cpp
+    for cpp_src in sorted(glob.glob(os.path.join(CSRC, "*.cpp"))):
+        cpp_obj = os.path.join(BUILD, os.path.basename(cpp_src) + ".o")
+        objs.append(cpp_obj)
+        if force or _newer([cpp_src] + headers, cpp_obj):
+            cmd = [CXX, "-O2", "-fPIC", "-std=c++17", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DUSE_ROCM=1",
+                   "-D__HIP_PLATFORM_AMD__=1", "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H",
+                   "-DUSE_C10D_GLOO", "-DUSE_C10D_NCCL", "-DUSE_DISTRIBUTED",
+                   "-Wno-deprecated-declarations", "-I", CSRC, "-I", py_inc]
+            for i in inc:
+                cmd += ["-I", i]
+            cmd += ["-c", cpp_src, "-o", cpp_obj]
+            jobs_list.append(cmd)
     if jobs_list:
         with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
             futs = [ex.submit(_run, c) for c in jobs_list]
