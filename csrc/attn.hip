@@ -54,6 +54,10 @@ constexpr uint32_t HC = 0x85EBCA6Bu;
 
 DLLM_DEVICE bf16x8v as_frag(u16x8 v) { return __builtin_bit_cast(bf16x8v, v); }
 
+// v_exp_f32 directly: libm exp2f wraps it in a denormal-range fix-up (compare, select, add, ldexp) that costs
+// 5 extra VALU ops per score; softmax probabilities below 2^-126 are irrelevant (flushed to 0).
+DLLM_DEVICE float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 DLLM_DEVICE bf16x8v pack8(const f32x16& a, int base) {
   u16x8 r;
 #pragma unroll
@@ -211,25 +215,34 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_kernel(AttnParams P) {
       s0 = mfma32(as_frag(ld_row(Kb, r, 2 * s + hh)), qf[s], s0);
       s1 = mfma32(as_frag(ld_row(Kb, 32 + r, 2 * s + hh)), qf[s], s1);
     }
-    const bool tile_masked = anym[cur] != 0;
+    // key mask (padding / past Sk) as 8 vector LDS reads, added branch-free: a per-score `if` here made the
+    // compiler emit 16 branches each ending in s_waitcnt lgkmcnt(0)
+    f32x4 km0[4], km1[4];
+    if (HAS_KPM || anym[cur] != 0) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        km0[g] = *reinterpret_cast<const f32x4*>(kmask + cur * FWD_BN + 8 * g + 4 * hh);
+        km1[g] = *reinterpret_cast<const f32x4*>(kmask + cur * FWD_BN + 32 + 8 * g + 4 * hh);
+      }
+    } else {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) km0[g] = km1[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
     const bool tile_causal = CAUSAL && (kbase + FWD_BN - 1 > qw0 + P.causal_off);
+    const int climit = qrow + P.causal_off - kbase;  // key offsets above this are masked (causal)
+    const float* lb = lut_s + (kbase - qrow + P.Sq - 1 - lut_base);
     float mloc = -INFINITY;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int kl0 = crow(i, hh), kl1 = 32 + kl0;
-      float v0 = s0[i] * sl2, v1 = s1[i] * sl2;
+      float v0 = s0[i] * sl2 + km0[i >> 2][i & 3], v1 = s1[i] * sl2 + km1[i >> 2][i & 3];
       if (HAS_BIAS) {
-        const float* lb = lut_s + (kbase - qrow + P.Sq - 1 - lut_base);
         v0 += lb[kl0];
         v1 += lb[kl1];
       }
-      if (tile_masked) {
-        v0 += kmask[cur * FWD_BN + kl0];
-        v1 += kmask[cur * FWD_BN + kl1];
-      }
-      if (tile_causal) {
-        if (kbase + kl0 > qrow + P.causal_off) v0 = -INFINITY;
-        if (kbase + kl1 > qrow + P.causal_off) v1 = -INFINITY;
+      if (CAUSAL) {
+        v0 = (tile_causal && kl0 > climit) ? -INFINITY : v0;
+        v1 = (tile_causal && kl1 > climit) ? -INFINITY : v1;
       }
       s0[i] = v0;
       s1[i] = v1;
@@ -240,15 +253,15 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_kernel(AttnParams P) {
     const bool grow = mloc > m_run + RESCALE_THR;
     float alpha = 1.f;
     if (grow) {
-      alpha = exp2f(m_run - mloc);
+      alpha = fast_exp2(m_run - mloc);
       m_run = mloc;
     }
     const float m_use = m_run == -INFINITY ? 0.f : m_run;
     float lsum = 0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      s0[i] = exp2f(s0[i] - m_use);
-      s1[i] = exp2f(s1[i] - m_use);
+      s0[i] = fast_exp2(s0[i] - m_use);
+      s1[i] = fast_exp2(s1[i] - m_use);
       lsum += s0[i] + s1[i];
     }
     l_run = l_run * alpha + lsum;
@@ -423,8 +436,20 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dq_kernel(AttnParams P) {
       p0 = mfma32(as_frag(ld_row(Vb, r, 2 * s + hh)), dof[s], p0);
       p1 = mfma32(as_frag(ld_row(Vb, 32 + r, 2 * s + hh)), dof[s], p1);
     }
-    const bool tile_masked = anym[cur] != 0;
+    f32x4 km0[4], km1[4];
+    if (HAS_KPM || anym[cur] != 0) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        km0[g] = *reinterpret_cast<const f32x4*>(kmask + cur * FWD_BN + 8 * g + 4 * hh);
+        km1[g] = *reinterpret_cast<const f32x4*>(kmask + cur * FWD_BN + 32 + 8 * g + 4 * hh);
+      }
+    } else {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) km0[g] = km1[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
     const bool tile_causal = CAUSAL && (kbase + FWD_BN - 1 > qw0 + P.causal_off);
+    const int climit = qrow + P.causal_off - kbase;
+    const float* lb = lut_s + (kbase - qrow + P.Sq - 1 - lut_base);
     const uint32_t tbase = (uint32_t)(kbase >> 1) * HG + (uint32_t)(2 * hh) * HG;
 #pragma unroll
     for (int i = 0; i < 16; i += 2) {
@@ -442,21 +467,16 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dq_kernel(AttnParams P) {
       for (int u = 0; u < 2; ++u) {
         const int ii = i + u;
         const int kl0 = crow(ii, hh), kl1 = 32 + kl0;
-        float v0 = s0[ii] * sl2, v1 = s1[ii] * sl2;
+        float v0 = s0[ii] * sl2 + km0[ii >> 2][ii & 3], v1 = s1[ii] * sl2 + km1[ii >> 2][ii & 3];
         if (HAS_BIAS) {
-          const float* lb = lut_s + (kbase - qrow + P.Sq - 1 - lut_base);
           v0 += lb[kl0];
           v1 += lb[kl1];
         }
-        if (tile_masked) {
-          v0 += kmask[cur * FWD_BN + kl0];
-          v1 += kmask[cur * FWD_BN + kl1];
+        if (CAUSAL) {
+          v0 = (tile_causal && kl0 > climit) ? -INFINITY : v0;
+          v1 = (tile_causal && kl1 > climit) ? -INFINITY : v1;
         }
-        if (tile_causal) {
-          if (kbase + kl0 > qrow + P.causal_off) v0 = -INFINITY;
-          if (kbase + kl1 > qrow + P.causal_off) v1 = -INFINITY;
-        }
-        const float pr0 = exp2f(v0 - lse2), pr1 = exp2f(v1 - lse2);
+        const float pr0 = fast_exp2(v0 - lse2), pr1 = fast_exp2(v1 - lse2);
         s0[ii] = pr0 * (p0[ii] * (u == 0 ? k0a : k0b) - delta);
         s1[ii] = pr1 * (p1[ii] * (u == 0 ? k1a : k1b) - delta);
       }
@@ -498,8 +518,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnParams P) {
   uint16_t* QD = reinterpret_cast<uint16_t*>(smem);             // [2 buffers][Q tile | dO tile] (32 rows)
   float* rowv = reinterpret_cast<float*>(QD + 4 * TILE32);       // [2][3][32]: lse2, delta, rowhash
   float* kmask = rowv + 2 * 3 * BWD_BQ;                          // [128]
-  float* lut_s = kmask + BWD_BK;                                 // [Sq + 128] (log2-scaled)
-  float* dlut_s = lut_s + (HAS_BIAS ? P.Sq + BWD_BK : 0);        // [Sq + 128]
+  float* lut_r = kmask + BWD_BK;                                 // [Sq + 128 + 32] reversed, log2-scaled
+  float* dlut_s = lut_r + (HAS_BIAS ? P.Sq + BWD_BK + BWD_BQ : 0);  // [Sq + 128]
 
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 31, hh = lane >> 5;
   const int logical = xcd_remap(blockIdx.x, gridDim.x);
@@ -515,12 +535,14 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnParams P) {
   const float sl2 = P.scale * LOG2E;
 
   if (HAS_BIAS) {
+    // lut_r[t] = LUT[k0 + win - 1 - t] (0 outside): a score's LUT index li = key - q + Sq - 1 - k0 (>= -32 for
+    // the padded rows of a partial last q-tile) lives at t = win - 1 - li = lane base + (row offset in tile)
     const float* lrow = P.lut + (long)h * L;
-    for (int i = tid; i < win; i += 256) {
-      const int gi = k0 + i;
-      lut_s[i] = gi < L ? lrow[gi] * LOG2E : 0.f;
-      dlut_s[i] = 0.f;
+    for (int t = tid; t < win + BWD_BQ; t += 256) {
+      const int i = win - 1 - t, gi = k0 + i;
+      lut_r[t] = (i >= 0 && gi < L) ? lrow[gi] * LOG2E : 0.f;
     }
+    for (int i = tid; i < win; i += 256) dlut_s[i] = 0.f;
   }
   if (tid < BWD_BK) {
     const int kk = k0 + tid;
@@ -544,7 +566,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnParams P) {
     }
   }
   const uint32_t kpg = (uint32_t)(key >> 1) * HG;
-  const bool khi = key & 1;
+  const uint32_t hshift = (key & 1) ? 0u : 16u;
+  const uint32_t thr_hi = P.thr << 16;
   const float dscale = DROP ? 1.f / (1.f - P.p_drop) : 1.f;
   int qt_begin = 0;
   if (CAUSAL) {
@@ -610,23 +633,22 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnParams P) {
       dpacc = mfma32(as_frag(ld_row(dOb, r, 2 * s + hh)), vf[s], dpacc);
     }
     const bool tile_causal = CAUSAL && (kw0 + 31 > q0 + P.causal_off);
+    // row i of the tile sits at t = lbase + crow(i, 0): immediate ds_read offsets, no per-score index math
+    const float* lrow_t = lut_r + (win - 1 - (key - q0 - 4 * hh + P.Sq - 1 - k0));
     f32x16 pd, ds;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int ql = crow(i, hh);
       const int qg = q0 + ql;
       float sv = sacc[i] * sl2 + km;
-      if (HAS_BIAS) {
-        int li = key - qg + P.Sq - 1 - k0;
-        li = li < 0 ? 0 : li;
-        sv += lut_s[li];
-      }
+      if (HAS_BIAS) sv += lrow_t[crow(i, 0)];
       if (tile_causal && key > qg + P.causal_off) sv = -INFINITY;
-      const float pr = exp2f(sv - rv[ql]);  // lse = +inf for q >= Sq -> 0
+      const float pr = fast_exp2(sv - rv[ql]);  // lse = +inf for q >= Sq -> 0
       float keepf = 1.f;
       if (DROP) {
-        const uint32_t x = pair_hash(__float_as_uint(rv[2 * BWD_BQ + ql]), kpg);
-        keepf = ((khi ? (x >> 16) : (x & 0xFFFFu)) >= P.thr) ? dscale : 0.f;
+        // half (key & 1) of x >= thr  <=>  (x << 16*(1 - (key & 1))) >= thr << 16
+        const uint32_t x = pair_hash(__float_as_uint(rv[2 * BWD_BQ + ql]), kpg) << hshift;
+        keepf = x >= thr_hi ? dscale : 0.f;
       }
       pd[i] = pr * keepf;
       ds[i] = pr * (dpacc[i] * keepf - rv[BWD_BQ + ql]);
@@ -768,7 +790,7 @@ extern "C" int dllm_attn_bwd(AttnParams* pp, hipStream_t st) {
   p.n_tiles = (p.Sk + BWD_BK - 1) / BWD_BK;
   nblk = (long)p.n_tiles * p.H * p.B;
   lds = (size_t)4 * TILE32 * 2 + (size_t)2 * 3 * BWD_BQ * 4 + BWD_BK * 4;
-  if (p.lut) lds += (size_t)2 * (p.Sq + BWD_BK) * 4;
+  if (p.lut) lds += (size_t)(2 * (p.Sq + BWD_BK) + BWD_BQ) * 4;
   if (nblk <= 0 || nblk > 0x7fffffff || lds > 160 * 1024) return -4;
   DISPATCH4(launch_bwd_dkdv_t, p.lut != nullptr, p.kpm != nullptr, p.causal != 0, p.p_drop > 0.f, p, (int)nblk, lds,
             st);

@@ -1,0 +1,10 @@
+#!/bin/bash
+set -o pipefail
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 600 python -m pytest tests/ -q -m gpu -x > gpurun_out/gputests14.log 2>&1 || { echo GT_FAIL; grep -E "Error|assert|FAILED|passed|failed" gpurun_out/gputests14.log | tail -20; exit 1; }
+tail -1 gpurun_out/gputests14.log
+timeout -k 10 300 python tools/attn_bench.py > gpurun_out/attn14.jsonl 2>&1 || { echo AB_FAIL; tail -5 gpurun_out/attn14.jsonl; exit 1; }
+grep '^{' gpurun_out/attn14.jsonl | cut -c1-250
+timeout -k 10 300 python bench.py > gpurun_out/bench14.log 2>&1 || { echo BENCH_FAIL; tail -20 gpurun_out/bench14.log; exit 1; }
+tail -1 gpurun_out/bench14.log | cut -c1-220
