@@ -112,13 +112,13 @@ DLLM_DEVICE uint32_t pair_hash(uint32_t rh, uint32_t kpg) {
 }
 
 // ================================================================================== forward
-template <bool HAS_BIAS, bool HAS_KPM, bool CAUSAL, bool DROP, int OCC = 2>
-__global__ __launch_bounds__(256, OCC) void attn_fwd_kernel(AttnParams P) {
+template <bool HAS_BIAS, bool HAS_KPM, bool CAUSAL, bool DROP, bool PIPE>
+__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  uint16_t* KV = reinterpret_cast<uint16_t*>(smem);            // [2 buffers][K tile | V tile]
-  float* kmask = reinterpret_cast<float*>(KV + 4 * TILE64);     // [2][64]
-  int* anym = reinterpret_cast<int*>(kmask + 2 * FWD_BN);       // [4]
-  float* lut_s = reinterpret_cast<float*>(anym + 4);            // [Sk + FWD_BM + FWD_BN], log2-scaled
+  uint16_t* KV = reinterpret_cast<uint16_t*>(smem);            // [3 buffers][K tile | V tile]
+  float* kmask = reinterpret_cast<float*>(KV + 6 * TILE64);     // [ntiles * 64]: 0 or -inf per key
+  int* tflag = reinterpret_cast<int*>(kmask + P.n_ktiles * FWD_BN);  // [ntiles]: tile has a masked key
+  float* lut_s = reinterpret_cast<float*>(tflag + P.n_ktiles);   // [Sk + FWD_BM + FWD_BN], log2-scaled
 
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 31, hh = lane >> 5;
   const int logical = xcd_remap(blockIdx.x, gridDim.x);
@@ -161,81 +161,58 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_kernel(AttnParams P) {
   }
   const int ntiles = kend > 0 ? (kend + FWD_BN - 1) / FWD_BN : 0;
 
-  // ---- staging: thread t moves 16-B chunk (t & 7) of keys (t >> 3) and (t >> 3) + 32
-  const int skey = tid >> 3, sch = tid & 7;
-  u16x8 kr[2], vr[2];
-  auto load_tile = [&](int kt) {
+  // ---- staging by LDS-DMA: wave w moves rows 16w .. 16w+15 of the K and V tiles (2 x 1 KB per operand);
+  // lane L of DMA j lands at row 8j + L/8, physical chunk L%8 and fetches logical chunk (L%8) ^ swz(row).
+  // Keys past Sk re-read row Sk-1 (finite values; masked to -inf / P = 0).  No staging VGPRs, no ds_write.
+  const uint32_t kv_lds = lds_addr(KV);
+  auto issue_tile = [&](int buf, int kt) {
 #pragma unroll
-    for (int pass = 0; pass < 2; ++pass) {
-      const int kk = kt * FWD_BN + skey + 32 * pass;
-      u16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
-      kr[pass] = z;
-      vr[pass] = z;
-      if (kk < P.Sk) {
-        kr[pass] = *reinterpret_cast<const u16x8*>(P.k + b * P.k_sb + (long)kk * P.k_ss + h * P.k_sh + sch * 8);
-        vr[pass] = *reinterpret_cast<const u16x8*>(P.v + b * P.v_sb + (long)kk * P.v_ss + h * P.v_sh + sch * 8);
-      }
+    for (int i = 0; i < 2; ++i) {
+      const int j = 2 * w + i;
+      const int row = 8 * j + (lane >> 3);
+      int kk = kt * FWD_BN + row;
+      kk = kk < P.Sk ? kk : P.Sk - 1;
+      const int c = (lane & 7) ^ swz(row);
+      const uint32_t dst = kv_lds + (uint32_t)(buf * 2 * TILE64 * 2 + j * 1024);
+      glds16(P.k + b * P.k_sb + (long)kk * P.k_ss + h * P.k_sh + c * 8, __builtin_amdgcn_readfirstlane(dst));
+      glds16(P.v + b * P.v_sb + (long)kk * P.v_ss + h * P.v_sh + c * 8,
+             __builtin_amdgcn_readfirstlane(dst + TILE64 * 2));
     }
   };
-  auto store_tile = [&](int buf, int kt) {
-    uint16_t* Kb = KV + buf * 2 * TILE64;
-    uint16_t* Vb = Kb + TILE64;
-#pragma unroll
-    for (int pass = 0; pass < 2; ++pass) {
-      st_row(Kb, skey + 32 * pass, sch, kr[pass]);
-      st_row(Vb, skey + 32 * pass, sch, vr[pass]);
-    }
-    if (tid < FWD_BN) {  // wave 0
-      const int kk = kt * FWD_BN + tid;
-      bool ok = kk < P.Sk;
-      if (HAS_KPM && ok) ok = P.kpm[(long)b * P.Sk + kk] != 0;
-      kmask[buf * FWD_BN + tid] = ok ? 0.f : -INFINITY;
-      const unsigned long long m = __ballot(!ok);
-      if (tid == 0) anym[buf] = m != 0ull;
-    }
-  };
+  for (int t = w; t < ntiles; t += 4) {  // wave-per-tile: per-key mask + "tile has a masked key" flag
+    const int j = t * FWD_BN + lane;
+    bool ok = j < P.Sk;
+    if (HAS_KPM && ok) ok = P.kpm[(long)b * P.Sk + j] != 0;
+    kmask[j] = ok ? 0.f : -INFINITY;
+    const unsigned long long m = __ballot(!ok);
+    if (lane == 0) tflag[t] = m != 0ull;
+  }
 
   f32x16 o0 = {}, o1 = {};
   float m_run = -INFINITY, l_run = 0.f;
-  if (ntiles > 0) {
-    load_tile(0);
-    store_tile(0, 0);
-  }
-  __syncthreads();
-  for (int kt = 0; kt < ntiles; ++kt) {
-    const int cur = kt & 1;
-    const int kbase = kt * FWD_BN;
-    if (kt + 1 < ntiles) load_tile(kt + 1);
-    const uint16_t* Kb = KV + cur * 2 * TILE64;
-    const uint16_t* Vb = Kb + TILE64;
 
-    f32x16 s0 = {}, s1 = {};
+  // S^T = K Q^T for the tile in LDS buffer `buf` (8 MFMAs, two independent accumulation chains)
+  auto scores = [&](int buf, f32x16& s0, f32x16& s1) {
+    const uint16_t* Kb = KV + buf * 2 * TILE64;
+    s0 = f32x16{};
+    s1 = f32x16{};
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       s0 = mfma32(as_frag(ld_row(Kb, r, 2 * s + hh)), qf[s], s0);
       s1 = mfma32(as_frag(ld_row(Kb, 32 + r, 2 * s + hh)), qf[s], s1);
     }
-    // key mask (padding / past Sk) as 8 vector LDS reads, added branch-free: a per-score `if` here made the
-    // compiler emit 16 branches each ending in s_waitcnt lgkmcnt(0)
-    f32x4 km0[4], km1[4];
-    if (HAS_KPM || anym[cur] != 0) {
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        km0[g] = *reinterpret_cast<const f32x4*>(kmask + cur * FWD_BN + 8 * g + 4 * hh);
-        km1[g] = *reinterpret_cast<const f32x4*>(kmask + cur * FWD_BN + 32 + 8 * g + 4 * hh);
-      }
-    } else {
-#pragma unroll
-      for (int g = 0; g < 4; ++g) km0[g] = km1[g] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
+  };
+  // online softmax of tile kt's scores (in s0/s1) and O^T += V^T P^T with V from buffer `buf`
+  auto softmax_pv = [&](int kt, int buf, f32x16& s0, f32x16& s1) {
+    const int kbase = kt * FWD_BN;
+    const uint16_t* Vb = KV + buf * 2 * TILE64 + TILE64;
     const bool tile_causal = CAUSAL && (kbase + FWD_BN - 1 > qw0 + P.causal_off);
     const int climit = qrow + P.causal_off - kbase;  // key offsets above this are masked (causal)
     const float* lb = lut_s + (kbase - qrow + P.Sq - 1 - lut_base);
-    float mloc = -INFINITY;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int kl0 = crow(i, hh), kl1 = 32 + kl0;
-      float v0 = s0[i] * sl2 + km0[i >> 2][i & 3], v1 = s1[i] * sl2 + km1[i >> 2][i & 3];
+      float v0 = s0[i] * sl2, v1 = s1[i] * sl2;
       if (HAS_BIAS) {
         v0 += lb[kl0];
         v1 += lb[kl1];
@@ -246,8 +223,24 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_kernel(AttnParams P) {
       }
       s0[i] = v0;
       s1[i] = v1;
-      mloc = fmaxf(mloc, fmaxf(v0, v1));
     }
+    // key mask (padding / past Sk): one uniform branch per tile around 8 vector LDS reads; a per-score `if`
+    // made the compiler emit 16 branches each ending in s_waitcnt lgkmcnt(0)
+    if ((HAS_KPM || kbase + FWD_BN > P.Sk) && tflag[kt] != 0) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 m0 = *reinterpret_cast<const f32x4*>(kmask + kbase + 8 * g + 4 * hh);
+        const f32x4 m1 = *reinterpret_cast<const f32x4*>(kmask + kbase + 32 + 8 * g + 4 * hh);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          s0[4 * g + e] += m0[e];
+          s1[4 * g + e] += m1[e];
+        }
+      }
+    }
+    float mloc = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) mloc = fmaxf(mloc, fmaxf(s0[i], s1[i]));
     mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
     // deferred rescale (T13): keep the running max unless the tile max exceeds it by > 8 (log2 units)
     const bool grow = mloc > m_run + RESCALE_THR;
@@ -297,8 +290,43 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_kernel(AttnParams P) {
         o1 = mfma32(ld_tr_operand(Vb, kb0, 1, r), pf, o1);
       }
     }
-    if (kt + 1 < ntiles) store_tile(cur ^ 1, kt + 1);
-    __syncthreads();
+  };
+
+  // Software pipeline over a 3-buffer K/V ring: while the VALU runs tile kt's softmax, the matrix core already
+  // computes tile kt+1's scores (issued first, independent registers); tile kt+2's DMA goes into the buffer
+  // tile kt-1 vacated and has a whole tile of compute to land.  One barrier per tile.
+  f32x16 sa0, sa1, sb0, sb1;
+  if (ntiles > 0) issue_tile(0, 0);
+  if (ntiles > 1) issue_tile(1, 1);
+  wait_vm<0>();
+  __syncthreads();
+  if (PIPE) {
+    if (ntiles > 0) scores(0, sa0, sa1);
+    for (int kt = 0; kt < ntiles; kt += 2) {
+      wait_vm<0>();     // this wave's DMA of tile kt+1 landed ...
+      __syncthreads();  // ... and everyone's; every wave is done with tile kt-1's buffer
+      if (kt + 1 < ntiles) scores((kt + 1) % 3, sb0, sb1);
+      softmax_pv(kt, kt % 3, sa0, sa1);
+      if (kt + 2 < ntiles) issue_tile((kt + 2) % 3, kt + 2);
+      if (kt + 1 >= ntiles) break;
+      wait_vm<0>();
+      __syncthreads();
+      if (kt + 2 < ntiles) scores((kt + 2) % 3, sa0, sa1);
+      softmax_pv(kt + 1, (kt + 1) % 3, sb0, sb1);
+      if (kt + 3 < ntiles) issue_tile((kt + 3) % 3, kt + 3);
+    }
+  } else {
+    for (int kt = 0; kt < ntiles; ++kt) {
+      if (kt > 0) {
+        // tile kt landed (this wave's 4 DMAs of tile kt+1, issued one tile later, may stay in flight)
+        if (kt + 1 < ntiles) wait_vm<4>();
+        else wait_vm<0>();
+        __syncthreads();
+      }
+      scores(kt % 3, sa0, sa1);
+      softmax_pv(kt, kt % 3, sa0, sa1);
+      if (kt + 2 < ntiles) issue_tile((kt + 2) % 3, kt + 2);
+    }
   }
 
   const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
@@ -736,12 +764,20 @@ int attn_occ() {
   }();
   return occ;
 }
+// DLLM_ATTN_FWD_PIPE=1: software-pipelined forward (next tile's QK^T issued before this tile's softmax)
+bool fwd_pipe() {
+  static bool v = [] {
+    const char* e = getenv("DLLM_ATTN_FWD_PIPE");
+    return e && atoi(e) == 1;
+  }();
+  return v;
+}
 template <bool HB, bool HK, bool CA, bool DR>
 void launch_fwd_t(const AttnParams& p, int nblk, size_t lds, hipStream_t st) {
-  if (attn_occ() == 3)
-    hipLaunchKernelGGL((attn_fwd_kernel<HB, HK, CA, DR, 3>), dim3(nblk), dim3(256), lds, st, p);
+  if (fwd_pipe())
+    hipLaunchKernelGGL((attn_fwd_kernel<HB, HK, CA, DR, true>), dim3(nblk), dim3(256), lds, st, p);
   else
-    hipLaunchKernelGGL((attn_fwd_kernel<HB, HK, CA, DR, 2>), dim3(nblk), dim3(256), lds, st, p);
+    hipLaunchKernelGGL((attn_fwd_kernel<HB, HK, CA, DR, false>), dim3(nblk), dim3(256), lds, st, p);
 }
 template <bool HB, bool HK, bool CA, bool DR>
 void launch_bwd_dq_t(const AttnParams& p, int nblk, size_t lds, hipStream_t st) {
@@ -755,8 +791,8 @@ void launch_bwd_dkdv_t(const AttnParams& p, int nblk, size_t lds, hipStream_t st
   hipLaunchKernelGGL((attn_bwd_dkdv_kernel<HB, HK, CA, DR>), dim3(nblk), dim3(256), lds, st, p);
 }
 
-size_t fwd_lds(const AttnParams& p) {
-  size_t lds = (size_t)4 * TILE64 * 2 + 2 * FWD_BN * 4 + 16;
+size_t fwd_lds(const AttnParams& p, int nbuf = 2) {
+  size_t lds = (size_t)2 * nbuf * TILE64 * 2 + nbuf * FWD_BN * 4 + 16;
   if (p.lut) lds += (size_t)(p.Sk + FWD_BM + FWD_BN) * 4;
   return lds;
 }
@@ -768,7 +804,10 @@ extern "C" int dllm_attn_fwd(AttnParams* pp, hipStream_t st) {
   p.thr = drop_threshold(p.p_drop);
   p.n_tiles = (p.Sq + FWD_BM - 1) / FWD_BM;
   const long nblk = (long)p.n_tiles * p.H * p.B;
-  const size_t lds = fwd_lds(p);
+  p.n_ktiles = (p.Sk + FWD_BN - 1) / FWD_BN;
+  // 3 K/V buffers + per-key mask + bias LUT window
+  size_t lds = (size_t)6 * TILE64 * 2 + (size_t)p.n_ktiles * (FWD_BN + 1) * 4;
+  if (p.lut) lds += (size_t)(p.Sk + FWD_BM + FWD_BN) * 4;
   if (nblk <= 0 || nblk > 0x7fffffff || lds > 160 * 1024) return -4;
   DISPATCH4(launch_fwd_t, p.lut != nullptr, p.kpm != nullptr, p.causal != 0, p.p_drop > 0.f, p, (int)nblk, lds, st);
   DLLM_CHECK_LAUNCH();

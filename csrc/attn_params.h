@@ -33,4 +33,5 @@ struct AttnParams {
   uint32_t seed;
   uint32_t thr;
   int n_tiles;  // fwd: q tiles; bwd: key blocks
+  int n_ktiles;  // fwd: 64-key tiles (key-mask array length / 64)
 };

@@ -134,6 +134,28 @@ DLLM_DEVICE float block_max(float v, float* red) {
   return r;
 }
 
+// ---- LDS-DMA (global_load_lds_dwordx4) ---------------------------------------------------------
+// LDS-DMA of 16 B per lane: lane i's bytes land at LDS byte address `lds_byte` + 16 i (wave-uniform base in
+// M0).  Inline asm, not the builtin: hipcc treats the builtin as an LDS store and waits vmcnt(0) before the
+// next ds_read of ANY buffer, which would drain the ring every stage; the asm load is invisible to its
+// bookkeeping and is retired by the explicit counted waits in the k-loop (cdna_hip_programming.md §6).
+DLLM_DEVICE void glds16(const uint16_t* g, uint32_t lds_byte) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(g), "s"(lds_byte)
+               : "memory");
+}
+
+DLLM_DEVICE uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
+template <int N_>
+DLLM_DEVICE void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_) : "memory");
+}
+
 }  // namespace dllm
 
 #define DLLM_CHECK_LAUNCH() \

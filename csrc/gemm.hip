@@ -63,27 +63,6 @@ DLLM_DEVICE bf16x8v frag(const uint16_t* T, int kk, int cb, int lane) {
   return __builtin_bit_cast(bf16x8v, v);
 }
 
-// LDS-DMA of 16 B per lane: lane i's bytes land at LDS byte address `lds_byte` + 16 i (wave-uniform base in
-// M0).  Inline asm, not the builtin: hipcc treats the builtin as an LDS store and waits vmcnt(0) before the
-// next ds_read of ANY buffer, which would drain the ring every stage; the asm load is invisible to its
-// bookkeeping and is retired by the explicit counted waits in the k-loop (cdna_hip_programming.md §6).
-DLLM_DEVICE void glds16(const uint16_t* g, uint32_t lds_byte) {
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(g), "s"(lds_byte)
-               : "memory");
-}
-
-DLLM_DEVICE uint32_t lds_addr(const void* p) {
-  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
-}
-
-template <int N_>
-DLLM_DEVICE void wait_vm() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_) : "memory");
-}
-
 template <int BK, int NBUF>
 __global__ __launch_bounds__(NT, 1) void gemm_wgrad_kernel(GemmWgradParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
