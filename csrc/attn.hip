@@ -351,8 +351,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
 }
 
 // ================================================================================== backward: dQ
-template <bool HAS_BIAS, bool HAS_KPM, bool CAUSAL, bool DROP, int OCC = 2>
-__global__ __launch_bounds__(256, OCC) void attn_bwd_dq_kernel(AttnParams P) {
+template <bool HAS_BIAS, bool HAS_KPM, bool CAUSAL, bool DROP>
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint16_t* KV = reinterpret_cast<uint16_t*>(smem);            // [2][K | V]
   float* kmask = reinterpret_cast<float*>(KV + 4 * TILE64);     // [2][64]
@@ -756,14 +756,6 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnParams P) {
     }                                                                                   \
   } while (0)
 
-// occupancy experiment knob (DLLM_ATTN_OCC=3: 3 workgroups per CU for the forward and dQ kernels)
-int attn_occ() {
-  static int occ = [] {
-    const char* e = getenv("DLLM_ATTN_OCC");
-    return e && atoi(e) == 3 ? 3 : 2;
-  }();
-  return occ;
-}
 // DLLM_ATTN_FWD_PIPE=1: software-pipelined forward (next tile's QK^T issued before this tile's softmax)
 bool fwd_pipe() {
   static bool v = [] {
@@ -781,10 +773,7 @@ void launch_fwd_t(const AttnParams& p, int nblk, size_t lds, hipStream_t st) {
 }
 template <bool HB, bool HK, bool CA, bool DR>
 void launch_bwd_dq_t(const AttnParams& p, int nblk, size_t lds, hipStream_t st) {
-  if (attn_occ() == 3)
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<HB, HK, CA, DR, 3>), dim3(nblk), dim3(256), lds, st, p);
-  else
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<HB, HK, CA, DR, 2>), dim3(nblk), dim3(256), lds, st, p);
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<HB, HK, CA, DR>), dim3(nblk), dim3(256), lds, st, p);
 }
 template <bool HB, bool HK, bool CA, bool DR>
 void launch_bwd_dkdv_t(const AttnParams& p, int nblk, size_t lds, hipStream_t st) {

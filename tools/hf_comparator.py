@@ -9,9 +9,13 @@ Usage: python tools/hf_comparator.py --model t5-base --batch 16 --src 1024 --tgt
 """
 import argparse
 import json
+import os
+import sys
 import time
 
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def t5_config(name):
@@ -35,12 +39,20 @@ def main():
     ap.add_argument("--prec", default="bf16-amp", choices=["fp32", "bf16-amp", "bf16"])
     ap.add_argument("--attn", default="sdpa")
     a = ap.parse_args()
-    from transformers import T5ForConditionalGeneration
+    import transformers
+    from distributed_llms_example_amd.models.config import resolve_config
     torch.manual_seed(0)
-    cfg = t5_config(a.model)
+    ours = resolve_config(a.model)  # same architecture presets as bench.py (config.json-compatible dict)
+    d = ours.to_hf_dict()
+    if ours.model_type == "t5":
+        cfg = transformers.T5Config(**{k: v for k, v in d.items() if k not in ("architectures", "model_type")})
+        cls = transformers.T5ForConditionalGeneration
+    else:
+        cfg = transformers.BartConfig(**{k: v for k, v in d.items() if k not in ("architectures", "model_type")})
+        cls = transformers.BartForConditionalGeneration
     cfg._attn_implementation = a.attn
     dev = "cuda" if torch.cuda.is_available() else "cpu"
-    model = T5ForConditionalGeneration(cfg).to(dev)
+    model = cls(cfg).to(dev)
     if a.prec == "bf16":
         model = model.to(torch.bfloat16)
     model.train()
