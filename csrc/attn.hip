@@ -266,17 +266,24 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
       }
     }
     if (DROP) {
+      // keep decisions -> P (the 1/(1-p) scale is applied once to O at the end) and one bit word per lane and
+      // tile for the backward kernels (bit i <-> s0[i], bit 16+i <-> s1[i]): they never re-hash
       const uint32_t tbase = (uint32_t)(kbase >> 1) * HG + (uint32_t)(2 * hh) * HG;
+      uint32_t word = 0;
 #pragma unroll
       for (int i = 0; i < 16; i += 2) {
         const uint32_t kpg = tbase + (uint32_t)(((i & 3) >> 1) + 4 * (i >> 2)) * HG;
         const uint32_t x0 = pair_hash(rh, kpg);
         const uint32_t x1 = pair_hash(rh, kpg + 16u * HG);  // keys + 32
-        s0[i] = (x0 & 0xFFFFu) >= P.thr ? s0[i] * dscale : 0.f;
-        s0[i + 1] = (x0 >> 16) >= P.thr ? s0[i + 1] * dscale : 0.f;
-        s1[i] = (x1 & 0xFFFFu) >= P.thr ? s1[i] * dscale : 0.f;
-        s1[i + 1] = (x1 >> 16) >= P.thr ? s1[i + 1] * dscale : 0.f;
+        const bool k0a = (x0 & 0xFFFFu) >= P.thr, k0b = (x0 >> 16) >= P.thr;
+        const bool k1a = (x1 & 0xFFFFu) >= P.thr, k1b = (x1 >> 16) >= P.thr;
+        s0[i] = k0a ? s0[i] : 0.f;
+        s0[i + 1] = k0b ? s0[i + 1] : 0.f;
+        s1[i] = k1a ? s1[i] : 0.f;
+        s1[i + 1] = k1b ? s1[i + 1] : 0.f;
+        word |= (k0a ? 1u << i : 0u) | (k0b ? 2u << i : 0u) | (k1a ? 0x10000u << i : 0u) | (k1b ? 0x20000u << i : 0u);
       }
+      P.dmask[((long)bh * P.n_ktiles * 2 + 2 * kt + hh) * P.sq_pad + qrow] = word;
     }
     // O^T += V^T P^T
     const bf16x8v pa0 = pack8(s0, 0), pa1 = pack8(s0, 8), pb0 = pack8(s1, 0), pb1 = pack8(s1, 8);
@@ -330,7 +337,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
   }
 
   const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
-  const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+  const float inv = l_tot > 0.f ? dscale / l_tot : 0.f;  // dropout's 1/(1-p) folded in
   if (qvalid) {
     uint16_t* op = P.o_out + b * P.o_sb + (long)qrow * P.o_ss + h * P.o_sh;
 #pragma unroll
@@ -355,9 +362,9 @@ template <bool HAS_BIAS, bool HAS_KPM, bool CAUSAL, bool DROP>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint16_t* KV = reinterpret_cast<uint16_t*>(smem);            // [2][K | V]
-  float* kmask = reinterpret_cast<float*>(KV + 4 * TILE64);     // [2][64]
-  int* anym = reinterpret_cast<int*>(kmask + 2 * FWD_BN);       // [4]
-  float* lut_s = reinterpret_cast<float*>(anym + 4);            // [Sk + FWD_BM + FWD_BN]
+  float* kmask = reinterpret_cast<float*>(KV + 4 * TILE64);     // [ntiles * 64]: 0 or -inf per key
+  int* tflag = reinterpret_cast<int*>(kmask + P.n_ktiles * FWD_BN);  // [ntiles]: tile has a masked key
+  float* lut_s = reinterpret_cast<float*>(tflag + P.n_ktiles);   // [Sk + FWD_BM + FWD_BN]
 
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 31, hh = lane >> 5;
   const int logical = xcd_remap(blockIdx.x, gridDim.x);
@@ -402,7 +409,6 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnParams P) {
   const long row_g = (long)(b * P.H + h) * P.Sq + qrow;
   if (qvalid && hh == 0) P.delta[row_g] = delta;
   const float lse2 = qvalid ? P.lse[row_g] : INFINITY;
-  const uint32_t rh = DROP ? mix32(P.seed, (uint32_t)row_g) : 0u;
   const float dscale = DROP ? 1.f / (1.f - P.p_drop) : 1.f;
 
   int kend = P.Sk;
@@ -411,49 +417,48 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnParams P) {
     kend = lim < kend ? lim : kend;
   }
   const int ntiles = kend > 0 ? (kend + FWD_BN - 1) / FWD_BN : 0;
-  const int skey = tid >> 3, sch = tid & 7;
-  u16x8 kr[2], vr[2];
-  auto load_tile = [&](int kt) {
+  // K/V tiles by LDS-DMA into 2 buffers (see the forward kernel); per-key mask + tile flags up front
+  const uint32_t kv_lds = lds_addr(KV);
+  auto issue_tile = [&](int buf, int kt) {
 #pragma unroll
-    for (int pass = 0; pass < 2; ++pass) {
-      const int kk = kt * FWD_BN + skey + 32 * pass;
-      u16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
-      kr[pass] = z;
-      vr[pass] = z;
-      if (kk < P.Sk) {
-        kr[pass] = *reinterpret_cast<const u16x8*>(P.k + b * P.k_sb + (long)kk * P.k_ss + h * P.k_sh + sch * 8);
-        vr[pass] = *reinterpret_cast<const u16x8*>(P.v + b * P.v_sb + (long)kk * P.v_ss + h * P.v_sh + sch * 8);
-      }
+    for (int i = 0; i < 2; ++i) {
+      const int j = 2 * w + i;
+      const int row = 8 * j + (lane >> 3);
+      int kk = kt * FWD_BN + row;
+      kk = kk < P.Sk ? kk : P.Sk - 1;
+      const int c = (lane & 7) ^ swz(row);
+      const uint32_t dst = kv_lds + (uint32_t)(buf * 2 * TILE64 * 2 + j * 1024);
+      glds16(P.k + b * P.k_sb + (long)kk * P.k_ss + h * P.k_sh + c * 8, __builtin_amdgcn_readfirstlane(dst));
+      glds16(P.v + b * P.v_sb + (long)kk * P.v_ss + h * P.v_sh + c * 8,
+             __builtin_amdgcn_readfirstlane(dst + TILE64 * 2));
     }
   };
-  auto store_tile = [&](int buf, int kt) {
-    uint16_t* Kb = KV + buf * 2 * TILE64;
-    uint16_t* Vb = Kb + TILE64;
-#pragma unroll
-    for (int pass = 0; pass < 2; ++pass) {
-      st_row(Kb, skey + 32 * pass, sch, kr[pass]);
-      st_row(Vb, skey + 32 * pass, sch, vr[pass]);
-    }
-    if (tid < FWD_BN) {
-      const int kk = kt * FWD_BN + tid;
-      bool ok = kk < P.Sk;
-      if (HAS_KPM && ok) ok = P.kpm[(long)b * P.Sk + kk] != 0;
-      kmask[buf * FWD_BN + tid] = ok ? 0.f : -INFINITY;
-      const unsigned long long m = __ballot(!ok);
-      if (tid == 0) anym[buf] = m != 0ull;
-    }
-  };
+  for (int t = w; t < ntiles; t += 4) {
+    const int j = t * FWD_BN + lane;
+    bool ok = j < P.Sk;
+    if (HAS_KPM && ok) ok = P.kpm[(long)b * P.Sk + j] != 0;
+    kmask[j] = ok ? 0.f : -INFINITY;
+    const unsigned long long m = __ballot(!ok);
+    if (lane == 0) tflag[t] = m != 0ull;
+  }
+  // dropout decisions: the bit words the forward stored (bit i <-> s0[i], bit 16+i <-> s1[i])
+  const uint32_t* mrow = DROP ? P.dmask + ((long)bh * P.n_ktiles * 2 + hh) * P.sq_pad + qrow : nullptr;
+  const uint32_t dsbits = __float_as_uint(dscale);
+  uint32_t mword = 0, mnext = 0;
+  if (DROP && ntiles > 0) mnext = mrow[0];
 
   f32x16 dq0 = {}, dq1 = {};
-  if (ntiles > 0) {
-    load_tile(0);
-    store_tile(0, 0);
-  }
-  __syncthreads();
+  if (ntiles > 0) issue_tile(0, 0);
   for (int kt = 0; kt < ntiles; ++kt) {
     const int cur = kt & 1;
     const int kbase = kt * FWD_BN;
-    if (kt + 1 < ntiles) load_tile(kt + 1);
+    wait_vm<0>();
+    __syncthreads();  // tile kt visible; every wave is done with tile kt-1 (buffer cur ^ 1)
+    if (kt + 1 < ntiles) issue_tile(cur ^ 1, kt + 1);
+    if (DROP) {
+      mword = mnext;
+      if (kt + 1 < ntiles) mnext = mrow[(long)(kt + 1) * 2 * P.sq_pad];
+    }
     const uint16_t* Kb = KV + cur * 2 * TILE64;
     const uint16_t* Vb = Kb + TILE64;
     f32x16 s0 = {}, s1 = {}, p0 = {}, p1 = {};
@@ -464,50 +469,46 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnParams P) {
       p0 = mfma32(as_frag(ld_row(Vb, r, 2 * s + hh)), dof[s], p0);
       p1 = mfma32(as_frag(ld_row(Vb, 32 + r, 2 * s + hh)), dof[s], p1);
     }
-    f32x4 km0[4], km1[4];
-    if (HAS_KPM || anym[cur] != 0) {
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        km0[g] = *reinterpret_cast<const f32x4*>(kmask + cur * FWD_BN + 8 * g + 4 * hh);
-        km1[g] = *reinterpret_cast<const f32x4*>(kmask + cur * FWD_BN + 32 + 8 * g + 4 * hh);
-      }
-    } else {
-#pragma unroll
-      for (int g = 0; g < 4; ++g) km0[g] = km1[g] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
     const bool tile_causal = CAUSAL && (kbase + FWD_BN - 1 > qw0 + P.causal_off);
     const int climit = qrow + P.causal_off - kbase;
     const float* lb = lut_s + (kbase - qrow + P.Sq - 1 - lut_base);
-    const uint32_t tbase = (uint32_t)(kbase >> 1) * HG + (uint32_t)(2 * hh) * HG;
 #pragma unroll
-    for (int i = 0; i < 16; i += 2) {
-      float k0a = 1.f, k0b = 1.f, k1a = 1.f, k1b = 1.f;
-      if (DROP) {
-        const uint32_t kpg = tbase + (uint32_t)(((i & 3) >> 1) + 4 * (i >> 2)) * HG;
-        const uint32_t x0 = pair_hash(rh, kpg);
-        const uint32_t x1 = pair_hash(rh, kpg + 16u * HG);
-        k0a = (x0 & 0xFFFFu) >= P.thr ? dscale : 0.f;
-        k0b = (x0 >> 16) >= P.thr ? dscale : 0.f;
-        k1a = (x1 & 0xFFFFu) >= P.thr ? dscale : 0.f;
-        k1b = (x1 >> 16) >= P.thr ? dscale : 0.f;
+    for (int i = 0; i < 16; ++i) {
+      const int kl0 = crow(i, hh), kl1 = 32 + kl0;
+      float v0 = s0[i] * sl2, v1 = s1[i] * sl2;
+      if (HAS_BIAS) {
+        v0 += lb[kl0];
+        v1 += lb[kl1];
       }
+      if (CAUSAL) {
+        v0 = (tile_causal && kl0 > climit) ? -INFINITY : v0;
+        v1 = (tile_causal && kl1 > climit) ? -INFINITY : v1;
+      }
+      s0[i] = v0;
+      s1[i] = v1;
+    }
+    if ((HAS_KPM || kbase + FWD_BN > P.Sk) && tflag[kt] != 0) {
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int ii = i + u;
-        const int kl0 = crow(ii, hh), kl1 = 32 + kl0;
-        float v0 = s0[ii] * sl2 + km0[ii >> 2][ii & 3], v1 = s1[ii] * sl2 + km1[ii >> 2][ii & 3];
-        if (HAS_BIAS) {
-          v0 += lb[kl0];
-          v1 += lb[kl1];
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 m0 = *reinterpret_cast<const f32x4*>(kmask + kbase + 8 * g + 4 * hh);
+        const f32x4 m1 = *reinterpret_cast<const f32x4*>(kmask + kbase + 32 + 8 * g + 4 * hh);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          s0[4 * g + e] += m0[e];
+          s1[4 * g + e] += m1[e];
         }
-        if (CAUSAL) {
-          v0 = (tile_causal && kl0 > climit) ? -INFINITY : v0;
-          v1 = (tile_causal && kl1 > climit) ? -INFINITY : v1;
-        }
-        const float pr0 = fast_exp2(v0 - lse2), pr1 = fast_exp2(v1 - lse2);
-        s0[ii] = pr0 * (p0[ii] * (u == 0 ? k0a : k0b) - delta);
-        s1[ii] = pr1 * (p1[ii] * (u == 0 ? k1a : k1b) - delta);
       }
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float pr0 = fast_exp2(s0[i] - lse2), pr1 = fast_exp2(s1[i] - lse2);
+      float k0 = 1.f, k1 = 1.f;
+      if (DROP) {  // sign-extended bit -> all-ones mask -> dscale or 0.0f
+        k0 = __uint_as_float((uint32_t)__builtin_amdgcn_sbfe((int)mword, i, 1) & dsbits);
+        k1 = __uint_as_float((uint32_t)__builtin_amdgcn_sbfe((int)mword, 16 + i, 1) & dsbits);
+      }
+      s0[i] = pr0 * (p0[i] * k0 - delta);
+      s1[i] = pr1 * (p1[i] * k1 - delta);
     }
     // dQ^T += K^T dS^T
     const bf16x8v da0 = pack8(s0, 0), da1 = pack8(s0, 8), db0 = pack8(s1, 0), db1 = pack8(s1, 8);
@@ -521,8 +522,6 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnParams P) {
         dq1 = mfma32(ld_tr_operand(Kb, kb0, 1, r), bf, dq1);
       }
     }
-    if (kt + 1 < ntiles) store_tile(cur ^ 1, kt + 1);
-    __syncthreads();
   }
   if (qvalid) {
     uint16_t* dqp = P.dq + b * P.dq_sb + (long)qrow * P.dq_ss + h * P.dq_sh;
@@ -546,7 +545,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnParams P) {
   uint16_t* QD = reinterpret_cast<uint16_t*>(smem);             // [2 buffers][Q tile | dO tile] (32 rows)
   float* rowv = reinterpret_cast<float*>(QD + 4 * TILE32);       // [2][3][32]: lse2, delta, rowhash
   float* kmask = rowv + 2 * 3 * BWD_BQ;                          // [128]
-  float* lut_r = kmask + BWD_BK;                                 // [Sq + 128 + 32] reversed, log2-scaled
+  uint32_t* mwd = reinterpret_cast<uint32_t*>(kmask + BWD_BK);   // [2][4][32] dropout bit words (see fwd)
+  float* lut_r = reinterpret_cast<float*>(mwd + 2 * 4 * BWD_BQ); // [Sq + 128 + 32] reversed, log2-scaled
   float* dlut_s = lut_r + (HAS_BIAS ? P.Sq + BWD_BK + BWD_BQ : 0);  // [Sq + 128]
 
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 31, hh = lane >> 5;
@@ -593,10 +593,12 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnParams P) {
       vf[s] = as_frag(c);
     }
   }
-  const uint32_t kpg = (uint32_t)(key >> 1) * HG;
-  const uint32_t hshift = (key & 1) ? 0u : 16u;
-  const uint32_t thr_hi = P.thr << 16;
+  // this lane's dropout bit: the forward's lane (hh_f) and register (bit) that held (q, key)
+  const int kl = key - k0, kc = kl & 31;
+  const int mcol = (kl >> 6) * 2 + ((kc >> 2) & 1);
+  const int mbit = (kc & 3) + 4 * (kc >> 3) + 16 * ((kl >> 5) & 1);
   const float dscale = DROP ? 1.f / (1.f - P.p_drop) : 1.f;
+  const uint32_t dsbits = __float_as_uint(dscale);
   int qt_begin = 0;
   if (CAUSAL) {
     const int qmin = k0 - P.causal_off;  // first query that can see key k0
@@ -610,7 +612,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnParams P) {
   const int srow = tid >> 3, sch = tid & 7;  // 32 rows x 8 chunks
   u16x8 qr, dr;
   float lr = 0.f, dl = 0.f;
-  uint32_t rhr = 0;
+  uint32_t mwr = 0;
   auto load_tile = [&](int qt) {
     const int qg = qt * BWD_BQ + srow;
     u16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -624,7 +626,12 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnParams P) {
       const int q2 = qt * BWD_BQ + tid;
       lr = q2 < P.Sq ? lse_row[q2] : INFINITY;
       dl = q2 < P.Sq ? del_row[q2] : 0.f;
-      rhr = DROP ? mix32(P.seed, (uint32_t)(bh_rows + q2)) : 0u;
+    }
+    if (DROP && tid < 4 * BWD_BQ) {  // words of the 2 forward key tiles x 2 lane halves this key block spans
+      const int col = tid >> 5, q2 = qt * BWD_BQ + (tid & 31);
+      const int ktf = (k0 >> 6) + (col >> 1);
+      mwr = (q2 < P.Sq && ktf < P.n_ktiles)
+                ? P.dmask[(((long)bh * P.n_ktiles + ktf) * 2 + (col & 1)) * P.sq_pad + q2] : 0u;
     }
   };
   auto store_tile = [&](int buf) {
@@ -635,8 +642,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnParams P) {
       float* rv = rowv + buf * 3 * BWD_BQ;
       rv[tid] = lr;
       rv[BWD_BQ + tid] = dl;
-      rv[2 * BWD_BQ + tid] = __uint_as_float(rhr);
     }
+    if (DROP && tid < 4 * BWD_BQ) mwd[buf * 4 * BWD_BQ + tid] = mwr;
   };
 
   f32x16 dv0 = {}, dv1 = {}, dk0 = {}, dk1 = {};
@@ -663,6 +670,17 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnParams P) {
     const bool tile_causal = CAUSAL && (kw0 + 31 > q0 + P.causal_off);
     // row i of the tile sits at t = lbase + crow(i, 0): immediate ds_read offsets, no per-score index math
     const float* lrow_t = lut_r + (win - 1 - (key - q0 - 4 * hh + P.Sq - 1 - k0));
+    uint32_t mw[16];
+    if (DROP) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const u32x4 v = *reinterpret_cast<const u32x4*>(mwd + cur * 4 * BWD_BQ + mcol * BWD_BQ + 8 * g + 4 * hh);
+        mw[4 * g] = v.x;
+        mw[4 * g + 1] = v.y;
+        mw[4 * g + 2] = v.z;
+        mw[4 * g + 3] = v.w;
+      }
+    }
     f32x16 pd, ds;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -673,11 +691,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnParams P) {
       if (tile_causal && key > qg + P.causal_off) sv = -INFINITY;
       const float pr = fast_exp2(sv - rv[ql]);  // lse = +inf for q >= Sq -> 0
       float keepf = 1.f;
-      if (DROP) {
-        // half (key & 1) of x >= thr  <=>  (x << 16*(1 - (key & 1))) >= thr << 16
-        const uint32_t x = pair_hash(__float_as_uint(rv[2 * BWD_BQ + ql]), kpg) << hshift;
-        keepf = x >= thr_hi ? dscale : 0.f;
-      }
+      if (DROP) keepf = __uint_as_float((uint32_t)__builtin_amdgcn_sbfe((int)mw[i], mbit, 1) & dsbits);
       pd[i] = pr * keepf;
       ds[i] = pr * (dpacc[i] * keepf - rv[BWD_BQ + ql]);
     }
@@ -780,11 +794,6 @@ void launch_bwd_dkdv_t(const AttnParams& p, int nblk, size_t lds, hipStream_t st
   hipLaunchKernelGGL((attn_bwd_dkdv_kernel<HB, HK, CA, DR>), dim3(nblk), dim3(256), lds, st, p);
 }
 
-size_t fwd_lds(const AttnParams& p, int nbuf = 2) {
-  size_t lds = (size_t)2 * nbuf * TILE64 * 2 + nbuf * FWD_BN * 4 + 16;
-  if (p.lut) lds += (size_t)(p.Sk + FWD_BM + FWD_BN) * 4;
-  return lds;
-}
 
 }  // namespace
 
@@ -794,6 +803,8 @@ extern "C" int dllm_attn_fwd(AttnParams* pp, hipStream_t st) {
   p.n_tiles = (p.Sq + FWD_BM - 1) / FWD_BM;
   const long nblk = (long)p.n_tiles * p.H * p.B;
   p.n_ktiles = (p.Sk + FWD_BN - 1) / FWD_BN;
+  p.sq_pad = p.n_tiles * FWD_BM;
+  if (p.p_drop > 0.f && p.dmask == nullptr) return -5;  // the caller allocates the dropout bit planes
   // 3 K/V buffers + per-key mask + bias LUT window
   size_t lds = (size_t)6 * TILE64 * 2 + (size_t)p.n_ktiles * (FWD_BN + 1) * 4;
   if (p.lut) lds += (size_t)(p.Sk + FWD_BM + FWD_BN) * 4;
@@ -808,8 +819,13 @@ extern "C" int dllm_attn_bwd(AttnParams* pp, hipStream_t st) {
   p.thr = drop_threshold(p.p_drop);
   // 1) dQ (+ delta): query blocks, forward geometry
   p.n_tiles = (p.Sq + FWD_BM - 1) / FWD_BM;
+  p.n_ktiles = (p.Sk + FWD_BN - 1) / FWD_BN;
+  p.sq_pad = p.n_tiles * FWD_BM;
+  if (p.p_drop > 0.f && p.dmask == nullptr) return -5;
   long nblk = (long)p.n_tiles * p.H * p.B;
-  size_t lds = fwd_lds(p);
+  // 2 K/V buffers + per-key mask + tile flags + bias LUT window
+  size_t lds = (size_t)4 * TILE64 * 2 + (size_t)p.n_ktiles * (FWD_BN + 1) * 4;
+  if (p.lut) lds += (size_t)(p.Sk + FWD_BM + FWD_BN) * 4;
   if (nblk <= 0 || nblk > 0x7fffffff || lds > 160 * 1024) return -4;
   DISPATCH4(launch_bwd_dq_t, p.lut != nullptr, p.kpm != nullptr, p.causal != 0, p.p_drop > 0.f, p, (int)nblk, lds,
             st);
@@ -817,7 +833,7 @@ extern "C" int dllm_attn_bwd(AttnParams* pp, hipStream_t st) {
   // 2) dK, dV (+ bias-LUT gradient): key blocks
   p.n_tiles = (p.Sk + BWD_BK - 1) / BWD_BK;
   nblk = (long)p.n_tiles * p.H * p.B;
-  lds = (size_t)4 * TILE32 * 2 + (size_t)2 * 3 * BWD_BQ * 4 + BWD_BK * 4;
+  lds = (size_t)4 * TILE32 * 2 + (size_t)2 * 3 * BWD_BQ * 4 + BWD_BK * 4 + (size_t)2 * 4 * BWD_BQ * 4;
   if (p.lut) lds += (size_t)(2 * (p.Sq + BWD_BK) + BWD_BQ) * 4;
   if (nblk <= 0 || nblk > 0x7fffffff || lds > 160 * 1024) return -4;
   DISPATCH4(launch_bwd_dkdv_t, p.lut != nullptr, p.kpm != nullptr, p.causal != 0, p.p_drop > 0.f, p, (int)nblk, lds,

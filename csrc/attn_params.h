@@ -33,5 +33,7 @@ struct AttnParams {
   uint32_t seed;
   uint32_t thr;
   int n_tiles;  // fwd: q tiles; bwd: key blocks
-  int n_ktiles;  // fwd: 64-key tiles (key-mask array length / 64)
+  int n_ktiles;  // 64-key tiles (key-mask array length / 64)
+  int sq_pad;    // rows of the dropout bit-mask planes (query tiles x 128)
+  uint32_t* dmask;  // [B*H][n_ktiles][2][sq_pad] dropout keep bits written by fwd, read by bwd
 };

@@ -28,6 +28,8 @@ int dllm_attn_fwd(AttnParams*, hipStream_t);
 int dllm_attn_bwd(AttnParams*, hipStream_t);
 int dllm_attn_params_size();
 int dllm_gemm_wgrad(const GemmWgradParams*, int, hipStream_t);
+int dllm_colsum_rows();
+int dllm_colsum_acc(const void*, long, long, int, float*, void*, int, hipStream_t);
 }
 
 namespace {
@@ -297,6 +299,11 @@ void fill_qkv(AttnParams& P, const Tensor& q, const Tensor& k, const Tensor& v, 
   }
 }
 
+int64_t dmask_numel(const AttnParams& P) {
+  const int64_t sq_pad = (P.Sq + 127) / 128 * 128, nkt = (P.Sk + 63) / 64;
+  return (int64_t)P.B * P.H * nkt * 2 * sq_pad;
+}
+
 std::vector<Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, const optional<Tensor>& kpm,
                              const optional<Tensor>& lut, double scale, bool causal, double p, int64_t seed) {
   AttnParams P{};
@@ -306,17 +313,29 @@ std::vector<Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, 
   P.o_out = reinterpret_cast<uint16_t*>(o.data_ptr());
   P.o_sb = o.stride(0); P.o_ss = o.stride(1); P.o_sh = o.stride(2);
   P.lse = lse.data_ptr<float>();
+  // dropout keep bits: [B*H][ceil(Sk/64)][2][ceil(Sq/128)*128] uint32, written here, read by attn_bwd
+  Tensor dmask;
+  if (p > 0.0) {
+    dmask = at::empty({dmask_numel(P)}, q.options().dtype(at::kInt));
+    P.dmask = reinterpret_cast<uint32_t*>(dmask.data_ptr());
+  }
   check_rc(dllm_attn_fwd(&P, stream()), "attn_fwd");
-  return {o, lse};
+  return {o, lse, dmask};
 }
 
 std::vector<Tensor> attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o,
                              const Tensor& lse, const optional<Tensor>& kpm, const optional<Tensor>& lut,
                              double scale, bool causal, double p, int64_t seed, bool need_dlut,
                              const optional<Tensor>& dq_out, const optional<Tensor>& dk_out,
-                             const optional<Tensor>& dv_out) {
+                             const optional<Tensor>& dv_out, const optional<Tensor>& dmask) {
   AttnParams P{};
   fill_qkv(P, q, k, v, kpm, lut, scale, causal, p, seed);
+  if (p > 0.0) {
+    TORCH_CHECK(dmask.has_value() && dmask->defined() && dmask->scalar_type() == at::kInt && dmask->is_contiguous() &&
+                    dmask->numel() == dmask_numel(P) && dmask->is_cuda(),
+                "attn_bwd: dropout needs the bit planes attn_fwd returned");
+    P.dmask = reinterpret_cast<uint32_t*>(dmask->data_ptr());
+  }
   check_bshd(o, "o", P.B, P.Sq, P.H);
   check_bshd(dout, "dout", P.B, P.Sq, P.H);
   TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.numel() == (int64_t)P.B * P.H * P.Sq && lse.is_contiguous(),
@@ -403,6 +422,25 @@ int64_t gemm_wgrad(const Tensor& a, const Tensor& b, Tensor& c, bool beta, int64
   return splits;
 }
 
+// out (+)= column sums of x ([T, N] bf16, unit inner stride): bias gradients accumulated in place
+void colsum_acc(const Tensor& x, Tensor& out) {
+  check_gpu(x, "x");
+  TORCH_CHECK(x.dim() == 2 && x.scalar_type() == at::kBFloat16 && x.stride(1) == 1 && x.stride(0) % 2 == 0 &&
+                  reinterpret_cast<uintptr_t>(x.data_ptr()) % 4 == 0,
+              "colsum_acc: x must be bf16 [T, N] with unit inner stride and 4-B aligned rows");
+  const int64_t T = x.size(0), N = x.size(1);
+  TORCH_CHECK(N % 2 == 0 && N < (1LL << 31), "colsum_acc: N must be even");
+  TORCH_CHECK(out.is_cuda() && out.is_contiguous() && out.numel() == N &&
+                  (out.scalar_type() == at::kBFloat16 || out.scalar_type() == at::kFloat),
+              "colsum_acc: out must be a contiguous bf16/fp32 [N] GPU tensor");
+  if (T == 0) return;
+  const int R = (int)std::min<int64_t>(T, dllm_colsum_rows());
+  auto part = at::empty({(int64_t)R * N}, x.options().dtype(at::kFloat));
+  check_rc(dllm_colsum_acc(x.data_ptr(), x.stride(0), T, (int)N, part.data_ptr<float>(), out.data_ptr(),
+                           out.scalar_type() == at::kBFloat16, stream()),
+           "colsum_acc");
+}
+
 namespace dllm {
 void bind_reducer(pybind11::module& m);  // csrc/reducer.cpp
 }
@@ -421,11 +459,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sq_norm", &sq_norm);
   m.def("adamw_step", &adamw_step);
   m.def("attn_fwd", &attn_fwd);
-  m.def("attn_bwd", &attn_bwd);
+  m.def("attn_bwd", &attn_bwd, py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"),
+        py::arg("lse"), py::arg("kpm"), py::arg("lut"), py::arg("scale"), py::arg("causal"), py::arg("p"),
+        py::arg("seed"), py::arg("need_dlut"), py::arg("dq_out") = py::none(), py::arg("dk_out") = py::none(),
+        py::arg("dv_out") = py::none(), py::arg("dmask") = py::none());
   m.def("attn_params_size", []() { return dllm_attn_params_size(); });
   m.def("gemm_wgrad", &gemm_wgrad, "c (+)= a^T b (token-major bf16 operands)", py::arg("a"), py::arg("b"), py::arg("c"),
         py::arg("beta") = true, py::arg("variant") = 0, py::arg("splits") = 0);
   m.def("gemm_wgrad_supported", &gemm_wgrad_supported);
+  m.def("colsum_acc", &colsum_acc, "out += x.sum(0) for a token-major bf16 x (bias gradients)");
   dllm::bind_reducer(m);
   m.attr("arch") = "gfx950";
 }

@@ -15,6 +15,7 @@ typedef __attribute__((ext_vector_type(8))) short bf16x8;   // MFMA A/B fragment
 typedef __attribute__((ext_vector_type(4))) short bf16x4;
 typedef __attribute__((ext_vector_type(4))) uint16_t u16x4;
 typedef __attribute__((ext_vector_type(8))) uint16_t u16x8;
+typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
 
 namespace dllm {
 

@@ -117,8 +117,8 @@ class _AttnFn(torch.autograd.Function):
     def forward(ctx, mode, a, b, c, lut, kpm, scale, causal, p, seed):
         C = _ext.native()
         q, k, v = _split(mode, a, b, c)
-        o, lse = C.attn_fwd(q, k, v, kpm, lut, float(scale), bool(causal), float(p), int(seed))
-        ctx.save_for_backward(a, b, c, o, lse, lut, kpm)
+        o, lse, dmask = C.attn_fwd(q, k, v, kpm, lut, float(scale), bool(causal), float(p), int(seed))
+        ctx.save_for_backward(a, b, c, o, lse, lut, kpm, dmask)
         ctx.cfg = (mode, scale, causal, p, seed, lut is not None and lut.requires_grad)
         # ops/linear.py stacked_linear: the packed kv is a slice of a multi-layer projection and its
         # gradient has a home in the stacked gradient buffer — write dK/dV there directly
@@ -128,7 +128,7 @@ class _AttnFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, do):
         C = _ext.native()
-        a, b, c, o, lse, lut, kpm = ctx.saved_tensors
+        a, b, c, o, lse, lut, kpm, dmask = ctx.saved_tensors
         mode, scale, causal, p, seed, need_dlut = ctx.cfg
         q, k, v = _split(mode, a, b, c)
         da = db = dc = None
@@ -144,7 +144,7 @@ class _AttnFn(torch.autograd.Function):
         else:
             dq = dk = dv = None
         rq, rk, rv, dlut = C.attn_bwd(do.contiguous(), q, k, v, o, lse, kpm, lut, float(scale), bool(causal),
-                                      float(p), int(seed), bool(need_dlut), dq, dk, dv)
+                                      float(p), int(seed), bool(need_dlut), dq, dk, dv, dmask)
         if mode == "sep":
             da, db, dc = rq, rk, rv
         return None, da, db, dc, (dlut if need_dlut else None), None, None, None, None, None

@@ -31,3 +31,13 @@ def wgrad_accumulate(out: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, bet
     if beta:
         return out.addmm_(dy2.t(), x2)
     return torch.mm(dy2.t(), x2, out=out)
+
+
+@torch.no_grad()
+def bias_grad_accumulate(out: torch.Tensor, dy2: torch.Tensor) -> torch.Tensor:
+    """``out += dy2.sum(0)`` (bias gradient of a linear layer, accumulated in place)."""
+    if _ext.use_native(dy2) and dy2.dtype == torch.bfloat16 and dy2.stride(-1) == 1 and dy2.shape[-1] % 2 == 0 \
+            and dy2.stride(0) % 2 == 0 and out.is_contiguous():
+        _ext.native().colsum_acc(dy2, out)
+        return out
+    return out.add_(dy2.sum(0).to(out.dtype))

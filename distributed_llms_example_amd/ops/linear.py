@@ -18,7 +18,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .gemm import wgrad_accumulate
+from .gemm import bias_grad_accumulate, wgrad_accumulate
 
 
 def _fire(p: torch.Tensor) -> None:
@@ -45,7 +45,7 @@ class _LinearAccumFn(torch.autograd.Function):
         with torch.no_grad():
             wgrad_accumulate(w.grad, dy2, x2)
             if bias is not None:
-                bias.grad.add_(dy2.sum(0))
+                bias_grad_accumulate(bias.grad, dy2)
         _fire(w)
         if bias is not None:
             _fire(bias)
@@ -126,9 +126,13 @@ class _StackedFn(torch.autograd.Function):
                 for l, w in enumerate(ws):
                     w.grad.add_(dW[l * n:(l + 1) * n])
             if bs[0] is not None:
-                db = G2.sum(0)
-                for l, bb in enumerate(bs):
-                    bb.grad.add_(db[l * n:(l + 1) * n])
+                gb = _adjacent([bb.grad for bb in bs])
+                if gb is not None:
+                    bias_grad_accumulate(gb, G2)
+                else:
+                    db = G2.sum(0)
+                    for l, bb in enumerate(bs):
+                        bb.grad.add_(db[l * n:(l + 1) * n])
         ctx.gbuf = None
         for p in list(ws) + [bb for bb in bs if bb is not None]:
             _fire(p)

@@ -277,3 +277,15 @@ def test_linear_wgrad_path_uses_native_gemm():
     wgrad_accumulate(g, dy, x)
     wgrad_accumulate(g, dy, x)
     assert _rel(g, 2 * (dy.float().t() @ x.float())) < 5e-3
+
+
+@pytest.mark.parametrize("T,N,dt", [(32768, 1024, torch.bfloat16), (1000, 4096, torch.bfloat16), (37, 770, torch.float32)])
+def test_colsum_acc_bias_grad(T, N, dt):
+    torch.manual_seed(0)
+    x_full = torch.randn(T, N + 6, device=DEV, dtype=torch.bfloat16)
+    x = x_full[:, 2:N + 2]  # strided rows
+    out0 = torch.randn(N, device=DEV, dtype=dt)
+    out = out0.clone()
+    _ext.native().colsum_acc(x, out)
+    ref = out0.float() + x.float().sum(0)
+    _close(out, ref, rtol=1e-2, atol=1e-2 * (T ** 0.5) / 10 + 1e-2, msg="colsum")
