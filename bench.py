@@ -48,6 +48,7 @@ def parse():
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--dropout", type=float, default=None, help="override model dropout (default: config 0.1)")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--grad-ckpt", action="store_true", help="activation checkpointing per block")
     return ap.parse_args()
 
 
@@ -68,6 +69,8 @@ def main():
     cfg = resolve_config(a.model)
     if a.dropout is not None:
         cfg = cfg.replace(dropout_rate=a.dropout, attention_dropout=a.dropout)
+    if a.grad_ckpt:
+        cfg = cfg.replace(gradient_checkpointing=True)
     model = build_model(cfg)
     eng = TrainEngine(model, env, lr=5e-5, weight_decay=0.01, max_grad_norm=1.0, dtype=torch.bfloat16,
                       bucket_mb=a.bucket_mb or DEFAULT_BUCKET_MB, overlap=not a.no_overlap)
@@ -119,7 +122,7 @@ def main():
                              f"{base_batch}) x N (BASELINE.md publishes no number)",
             "dtype": "bf16", "data": "synthetic (random token ids, random-init weights)",
             "config": {"model": a.model, "global_batch": B * n, "per_gpu_batch": B, "seq_len": S,
-                       "target_len": T, "parallelism": f"dp{n}",
+                       "target_len": T, "parallelism": f"dp{n}", "grad_ckpt": bool(a.grad_ckpt),
                        "bucket_mb": eng.reducer.bucket_sizes_mb()[1] if eng.reducer and len(eng.reducer.buckets) > 1 else None,
                        "tokens_per_s": round(value * (S + T), 1)},
         }), flush=True)

@@ -43,7 +43,11 @@ def base_parser(description: str, defaults: dict | None = None) -> argparse.Argu
     g.add_argument("--gen-max-length", type=int, default=128)
     g.add_argument("--num-beams", type=int, default=2)
     g.add_argument("--resume-from", type=str, default=None, help="checkpoint dir, or 'latest'")
+    g.add_argument("--save-steps", type=int, default=None,
+                   help="full training checkpoint every N optimizer steps (reference: final only)")
     g.add_argument("--seed", type=int, default=42)
+    g.add_argument("--gradient-checkpointing", action="store_true",
+                   help="recompute each transformer block in backward (long sequences / large models)")
     g.add_argument("--model-overrides", type=str, default=None,
                    help="comma list key=value applied to the model config (e.g. num_layers=2)")
     return ap
@@ -85,4 +89,7 @@ def build_data(args, cfg):
 
 
 def model_config(args):
-    return apply_overrides(resolve_config(args.model_ckpt), args.model_overrides)
+    cfg = apply_overrides(resolve_config(args.model_ckpt), args.model_overrides)
+    if getattr(args, "gradient_checkpointing", False):
+        cfg = cfg.replace(gradient_checkpointing=True)
+    return cfg

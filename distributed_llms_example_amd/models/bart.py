@@ -20,6 +20,7 @@ from ..ops import activations, attention as attn_ops, norms
 from ..ops.cross_entropy import cross_entropy
 from ..ops.linear import Linear, stacked_linear
 from ..ops.rng import default_rng
+from .blocks import run_block
 from .config import Seq2SeqConfig
 from .output import Seq2SeqLMOutput
 
@@ -141,9 +142,13 @@ class BartStack(nn.Module):
         if self.is_decoder and cross_kv is None and enc_out is not None:
             cross_kv = self.project_cross_kv(enc_out)
         for i, layer in enumerate(self.layers):
-            h = layer(h, mask=attention_mask, enc_out=enc_out, enc_mask=enc_mask,
-                      cache=caches[i] if caches is not None else None,
-                      cross_kv=cross_kv[i] if cross_kv is not None else None)
+            cache = caches[i] if caches is not None else None
+            ckv = cross_kv[i] if cross_kv is not None else None
+
+            def run(h, layer=layer, cache=cache, ckv=ckv):
+                return layer(h, mask=attention_mask, enc_out=enc_out, enc_mask=enc_mask, cache=cache, cross_kv=ckv)
+
+            h = run_block(run, h, checkpoint=cfg.gradient_checkpointing and self.training and caches is None)
         return h
 
 
@@ -223,6 +228,14 @@ class BartForConditionalGeneration(nn.Module):
     def generate(self, input_ids, attention_mask=None, **kw):
         from .generation import generate
         return generate(self, input_ids, attention_mask=attention_mask, **kw)
+
+    def gradient_checkpointing_enable(self, enable: bool = True):
+        """HF-style switch: recompute every layer in backward."""
+        self.config.gradient_checkpointing = bool(enable)
+        for st in (self.model.encoder, self.model.decoder):
+            st.cfg = self.config
+            for layer in st.layers:
+                layer.cfg = self.config
 
     def forward(self, input_ids=None, attention_mask=None, decoder_input_ids=None, labels=None,
                 label_smoothing: float = 0.0, return_logits: bool = False, encoder_outputs=None):

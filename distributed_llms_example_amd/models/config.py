@@ -39,6 +39,8 @@ class Seq2SeqConfig:
     initializer_factor: float = 1.0  # T5
     init_std: float = 0.02  # BART
     tie_word_embeddings: bool = True
+    # recompute each transformer block in backward (O(layers) less activation memory; long sequences)
+    gradient_checkpointing: bool = False
     scale_decoder_outputs: bool = True  # T5: scale by d_model**-0.5 before lm_head when tied
     # BART specifics
     max_position_embeddings: int = 1024

@@ -23,6 +23,7 @@ from ..ops import activations, attention as attn_ops, norms
 from ..ops.cross_entropy import cross_entropy
 from ..ops.linear import Linear, stacked_linear
 from ..ops.rng import default_rng
+from .blocks import run_block
 from .config import Seq2SeqConfig
 from .output import Seq2SeqLMOutput
 
@@ -165,24 +166,35 @@ class T5Stack(nn.Module):
         if self.is_decoder and cross_kv is None and enc_out is not None:
             cross_kv = self.project_cross_kv(enc_out)
         for i, blk in enumerate(blocks):
-            subs = list(blk.layer)
-            next_norms = [lyr.layer_norm.weight for lyr in subs[1:]]
-            next_norms.append(blocks[i + 1].layer[0].layer_norm.weight if i + 1 < len(blocks)
-                              else self.final_layer_norm.weight)
+            nxt = blocks[i + 1].layer[0].layer_norm.weight if i + 1 < len(blocks) else self.final_layer_norm.weight
+            ckv = cross_kv[i] if cross_kv is not None else None
             cache = caches[i] if caches is not None else None
-            a = subs[0].SelfAttention(normed, mask=attention_mask if not self.is_decoder else None, lut=lut,
-                                      causal=self.is_decoder, p=pa, cache=cache)
-            normed, h = norms.add_dropout_rms_norm(h, a, next_norms[0], eps, p, rng.next_seed() if p > 0 else 0)
-            j = 1
-            if self.is_decoder:
-                ckv = cross_kv[i] if cross_kv is not None else None
-                c = subs[1].EncDecAttention(normed, kv_in=enc_out, mask=enc_mask, lut=None, causal=False, p=pa, kv=ckv)
-                normed, h = norms.add_dropout_rms_norm(h, c, next_norms[1], eps, p, rng.next_seed() if p > 0 else 0)
-                j = 2
-            f = subs[j].DenseReluDense(normed, p)
-            normed, h = norms.add_dropout_rms_norm(h, f, next_norms[j], eps, p, rng.next_seed() if p > 0 else 0)
+
+            def run(normed, h, blk=blk, nxt=nxt, ckv=ckv, cache=cache):
+                return self._block(blk, nxt, normed, h, attention_mask, lut, enc_out, enc_mask, ckv, cache, p, pa, eps)
+
+            normed, h = run_block(run, normed, h, checkpoint=cfg.gradient_checkpointing and self.training and
+                                  caches is None)
         # `normed` is now final_layer_norm(h); HF applies dropout after it (modeling_t5.py:744-745)
         return activations.dropout(normed, p, rng.next_seed() if p > 0 else 0)
+
+
+    def _block(self, blk, next_norm, normed, h, attention_mask, lut, enc_out, enc_mask, ckv, cache, p, pa, eps):
+        """One T5 block on (norm(h), h) -> (next norm(h'), h'): self-attention, [cross-attention], FFN, each
+        residual update fused with the following RMSNorm."""
+        rng = default_rng()
+        subs = list(blk.layer)
+        norms_w = [lyr.layer_norm.weight for lyr in subs[1:]] + [next_norm]
+        a = subs[0].SelfAttention(normed, mask=attention_mask if not self.is_decoder else None, lut=lut,
+                                  causal=self.is_decoder, p=pa, cache=cache)
+        normed, h = norms.add_dropout_rms_norm(h, a, norms_w[0], eps, p, rng.next_seed() if p > 0 else 0)
+        j = 1
+        if self.is_decoder:
+            c = subs[1].EncDecAttention(normed, kv_in=enc_out, mask=enc_mask, lut=None, causal=False, p=pa, kv=ckv)
+            normed, h = norms.add_dropout_rms_norm(h, c, norms_w[1], eps, p, rng.next_seed() if p > 0 else 0)
+            j = 2
+        f = subs[j].DenseReluDense(normed, p)
+        return norms.add_dropout_rms_norm(h, f, norms_w[j], eps, p, rng.next_seed() if p > 0 else 0)
 
 
 class T5ForConditionalGeneration(nn.Module):
@@ -267,6 +279,12 @@ class T5ForConditionalGeneration(nn.Module):
     def generate(self, input_ids, attention_mask=None, **kw):
         from .generation import generate
         return generate(self, input_ids, attention_mask=attention_mask, **kw)
+
+    def gradient_checkpointing_enable(self, enable: bool = True):
+        """HF-style switch: recompute every block in backward (activation memory O(1) in depth)."""
+        self.config.gradient_checkpointing = bool(enable)
+        for st in (self.encoder, self.decoder):
+            st.cfg = self.config
 
     def forward(self, input_ids=None, attention_mask=None, decoder_input_ids=None, labels=None,
                 label_smoothing: float = 0.0, return_logits: bool = False, encoder_outputs=None):

@@ -101,10 +101,28 @@ class DropoutRNG:
 
 
 _global = DropoutRNG(42)
+_scoped: list[DropoutRNG] = []
 
 
 def default_rng() -> DropoutRNG:
-    return _global
+    return _scoped[-1] if _scoped else _global
+
+
+class rng_scope:
+    """Run a region with its own seed stream derived from ``seed``.  Every transformer block draws one seed
+    from the outer stream and runs under ``rng_scope(seed)``, so activation checkpointing can recompute a
+    block in backward with bit-identical dropout masks (the outer stream is not replayed)."""
+
+    def __init__(self, seed: int):
+        self.rng = DropoutRNG(seed)
+
+    def __enter__(self):
+        _scoped.append(self.rng)
+        return self.rng
+
+    def __exit__(self, *exc):
+        _scoped.pop()
+        return False
 
 
 def manual_seed(seed: int) -> None:

@@ -31,6 +31,7 @@ from ..parallel.reducer import DEFAULT_BUCKET_MB
 from ..parallel.sampler import ShardedBatchSampler
 from ..utils.logging import get_logger
 from .callbacks import CallbackHandler, DefaultFlowCallback, TrainerControl, TrainerState
+from ..utils import faults
 from .checkpoint import latest_checkpoint, load_checkpoint, save_checkpoint
 from .engine import TrainEngine, default_no_decay
 from .schedule import LRScheduler
@@ -72,6 +73,7 @@ class TrainingArguments:
     ddp_timeout: int = 1800
     overlap_comm: bool = True
     resume_from_checkpoint: str | None = None
+    nan_guard: bool = True  # raise when the (logged, already synchronised) mean loss is NaN/Inf
     report_to: list = field(default_factory=list)
 
     def __post_init__(self):
@@ -191,6 +193,8 @@ class Trainer:
                     total_loss_n += tr_loss_n
                     tr_loss_sum.zero_()
                     tr_loss_n = 0
+                    if args.nan_guard and not math.isfinite(mean):  # NaN/Inf guard on loss
+                        raise FloatingPointError(f"non-finite training loss {mean} at step {self.state.global_step}")
                     self.log({"loss": round(mean, 4), "grad_norm": float(last_norm) if last_norm is not None else None,
                               "learning_rate": self.scheduler.get_last_lr()[0], "epoch": round(self.state.epoch, 4)})
                 if self.control.should_evaluate and self.eval_dataset is not None:
@@ -198,6 +202,7 @@ class Trainer:
                     eng.train()
                 if self.control.should_save:
                     self._save_checkpoint()
+                faults.maybe_inject(self.state.global_step, env.rank)
                 self.control.reset_step()
                 if self.state.global_step >= max_steps:
                     break

@@ -7,6 +7,7 @@ import subprocess
 import sys
 
 import pytest
+import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -100,3 +101,28 @@ def test_train_task_valohai_distributed_contract(tmp_path):
         assert valohai.outputs().path("model-dir").startswith(str(tmp_path / "outputs"))
     finally:
         os.environ.pop("VH_ROOT", None)
+
+
+def test_fault_injection_then_resume_matches_uninterrupted(tmp_path):
+    """a worker killed mid-run (DLLM_FAULT_INJECT) restarts from its last checkpoint with
+    --resume-from latest and ends bit-identical to a run that was never interrupted."""
+    from safetensors.torch import load_file
+    base = [sys.executable, os.path.join(ROOT, "train-torchrun.py"), "--model-ckpt", "t5-tiny", "--batch-size", "4",
+            "--grad-accum", "1", "--evaluation-steps", "1000", "--warmup-steps", "1", "--max-steps", "6",
+            "--save-steps", "2", *COMMON]
+    env = _env(tmp_path)
+    r = subprocess.run(base + ["--output-dir", "ref"], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    env_f = dict(env, DLLM_FAULT_INJECT="step=5")
+    r = subprocess.run(base + ["--output-dir", "ft"], env=env_f, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 43, (r.returncode, r.stderr[-3000:])
+    assert "injected fault after step 5" in r.stderr
+    r = subprocess.run(base + ["--output-dir", "ft", "--resume-from", "latest"], env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = tmp_path / "outputs"
+    a = load_file(str(out / "ref" / "model.safetensors"))
+    b = load_file(str(out / "ft" / "model.safetensors"))
+    assert a.keys() == b.keys()
+    for k in a:
+        torch.testing.assert_close(a[k], b[k], rtol=0, atol=0, msg=k)

@@ -26,6 +26,7 @@ from torch.utils.data import DataLoader  # noqa: E402
 from distributed_llms_example_amd.cli import base_parser, build_data, model_config  # noqa: E402
 from distributed_llms_example_amd.data.collator import DataCollatorForSeq2Seq  # noqa: E402
 from distributed_llms_example_amd.models import build_model, from_pretrained  # noqa: E402
+from distributed_llms_example_amd.utils import faults  # noqa: E402
 from distributed_llms_example_amd.ops.rng import manual_seed  # noqa: E402
 from distributed_llms_example_amd.platform import valohai  # noqa: E402
 from distributed_llms_example_amd.train import rouge  # noqa: E402
@@ -51,6 +52,8 @@ class ModelTrainer:
         self.cfg = model_config(args)
         self.model = from_pretrained(args.model_ckpt) if os.path.isdir(args.model_ckpt or "") else \
             build_model(self.cfg)
+        if self.cfg.gradient_checkpointing:
+            self.model.gradient_checkpointing_enable()
 
     def dump(self, logs):
         if self.accelerator.is_main_process:
@@ -88,6 +91,7 @@ class ModelTrainer:
                 lr_scheduler.step()
                 optimizer.zero_grad()
                 completed += 1
+                faults.maybe_inject(completed, acc.process_index)
                 if completed % 300 == 0:
                     self.dump({"loss": loss.item(), "step": completed})
                 if completed >= max_train_steps:

@@ -56,6 +56,7 @@ def run(env, args):
     from distributed_llms_example_amd.parallel import collectives
     from distributed_llms_example_amd.parallel.sampler import DataPartitioner, ShardedBatchSampler
     from distributed_llms_example_amd.train import rouge
+    from distributed_llms_example_amd.utils import faults
     from distributed_llms_example_amd.train.engine import TrainEngine
     from distributed_llms_example_amd.train.schedule import LRScheduler
     from distributed_llms_example_amd.utils.gpu_report import gpu_report
@@ -74,6 +75,8 @@ def run(env, args):
         print(f"Train dataset size: {len(train_ds)}")
         print(f"Test dataset size: {len(eval_ds)}")
     model = from_pretrained(args.model_ckpt) if os.path.isdir(args.model_ckpt or "") else build_model(cfg)
+    if cfg.gradient_checkpointing:
+        model.gradient_checkpointing_enable()
     dtype = torch.bfloat16 if (args.precision or ("bf16" if env.device.type == "cuda" else "fp32")) == "bf16" \
         else torch.float32
     eng = TrainEngine(model, env, lr=args.learning_rate, weight_decay=0.0, max_grad_norm=None, dtype=dtype,
@@ -103,6 +106,7 @@ def run(env, args):
             eng.step(sched.get_last_lr()[0])
             sched.step()
             completed += 1
+            faults.maybe_inject(completed, env.rank)
             if completed % 100 == 0:
                 dump_metrics({"loss": float(loss), "step": completed}, env.is_main_process)
             if completed >= max_steps:

@@ -14,6 +14,8 @@ The final model is written in HF format with Valohai metadata sidecars (rank 0 o
 import os
 import sys
 
+import torch
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 os.environ.setdefault("TRANSFORMERS_NO_ADVISORY_WARNINGS", "true")
@@ -46,12 +48,15 @@ def run(args):
     if env.is_main_process:
         print(f"Train dataset size: {len(train_ds)}")
         print(f"Test dataset size: {len(eval_ds)}")
+    torch.manual_seed(args.seed)  # random-init runs (no pretrained weights offline) start identically
     model = from_pretrained(args.model_ckpt) if os.path.isdir(args.model_ckpt or "") else build_model(cfg)
+    if cfg.gradient_checkpointing:
+        model.gradient_checkpointing_enable()
     targs = TrainingArguments(
         output_dir=output_dir, num_train_epochs=args.num_epochs, warmup_steps=args.warmup_steps,
         per_device_train_batch_size=args.batch_size, per_device_eval_batch_size=args.eval_batch_size or args.batch_size,
         weight_decay=0.01, logging_steps=10, evaluation_strategy="steps", eval_steps=args.evaluation_steps,
-        save_steps=1e6, gradient_accumulation_steps=args.grad_accum or 16, ddp_find_unused_parameters=False,
+        save_steps=args.save_steps or 1e6, gradient_accumulation_steps=args.grad_accum or 16, ddp_find_unused_parameters=False,
         learning_rate=args.learning_rate, max_steps=args.max_steps, seed=args.seed,
         bf16=None if args.precision is None else args.precision == "bf16",
         ddp_bucket_cap_mb=args.bucket_mb, overlap_comm=not args.no_overlap)
