@@ -185,7 +185,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
     if (HAS_KPM && ok) ok = P.kpm[(long)b * P.Sk + j] != 0;
     kmask[j] = ok ? 0.f : -INFINITY;
     const unsigned long long m = __ballot(!ok);
-    if (lane == 0) tflag[t] = m != 0ull;
+    if (lane == 0) tflag[t] = m == 0ull ? 0 : (~m == 0ull ? 2 : 1);  // 2: every key masked -> tile skipped
   }
 
   f32x16 o0 = {}, o1 = {};
@@ -330,8 +330,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
         else wait_vm<0>();
         __syncthreads();
       }
-      scores(kt % 3, sa0, sa1);
-      softmax_pv(kt, kt % 3, sa0, sa1);
+      if (!HAS_KPM || tflag[kt] != 2) {  // a fully padded key tile contributes exactly nothing
+        scores(kt % 3, sa0, sa1);
+        softmax_pv(kt, kt % 3, sa0, sa1);
+      }
       if (kt + 2 < ntiles) issue_tile((kt + 2) % 3, kt + 2);
     }
   }
@@ -439,7 +441,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnParams P) {
     if (HAS_KPM && ok) ok = P.kpm[(long)b * P.Sk + j] != 0;
     kmask[j] = ok ? 0.f : -INFINITY;
     const unsigned long long m = __ballot(!ok);
-    if (lane == 0) tflag[t] = m != 0ull;
+    if (lane == 0) tflag[t] = m == 0ull ? 0 : (~m == 0ull ? 2 : 1);  // 2: every key masked -> tile skipped
   }
   // dropout decisions: the bit words the forward stored (bit i <-> s0[i], bit 16+i <-> s1[i])
   const uint32_t* mrow = DROP ? P.dmask + ((long)bh * P.n_ktiles * 2 + hh) * P.sq_pad + qrow : nullptr;
@@ -459,6 +461,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnParams P) {
       mword = mnext;
       if (kt + 1 < ntiles) mnext = mrow[(long)(kt + 1) * 2 * P.sq_pad];
     }
+    if (HAS_KPM && tflag[kt] == 2) continue;  // fully padded key tile: P = 0, no dQ contribution
     const uint16_t* Kb = KV + cur * 2 * TILE64;
     const uint16_t* Vb = Kb + TILE64;
     f32x16 s0 = {}, s1 = {}, p0 = {}, p1 = {};
@@ -572,12 +575,15 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnParams P) {
     }
     for (int i = tid; i < win; i += 256) dlut_s[i] = 0.f;
   }
+  bool key_ok = false;
   if (tid < BWD_BK) {
     const int kk = k0 + tid;
-    bool ok = kk < P.Sk;
-    if (HAS_KPM && ok) ok = P.kpm[(long)b * P.Sk + kk] != 0;
-    kmask[tid] = ok ? 0.f : -INFINITY;
+    key_ok = kk < P.Sk;
+    if (HAS_KPM && key_ok) key_ok = P.kpm[(long)b * P.Sk + kk] != 0;
+    kmask[tid] = key_ok ? 0.f : -INFINITY;
   }
+  // a key block that is entirely padding gets dK = dV = 0 without visiting any query tile
+  const bool block_live = !HAS_KPM || __syncthreads_or(key_ok ? 1 : 0);
   bf16x8v kf[4], vf[4];
   {
     const uint16_t* kp = P.k + b * P.k_sb + (long)key * P.k_ss + h * P.k_sh;
@@ -604,7 +610,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnParams P) {
     const int qmin = k0 - P.causal_off;  // first query that can see key k0
     qt_begin = qmin > 0 ? qmin / BWD_BQ : 0;
   }
-  const int nqt = (P.Sq + BWD_BQ - 1) / BWD_BQ;
+  const int nqt = block_live ? (P.Sq + BWD_BQ - 1) / BWD_BQ : qt_begin;
   const long bh_rows = (long)(b * P.H + h) * P.Sq;
   const float* lse_row = P.lse + bh_rows;
   const float* del_row = P.delta + bh_rows;

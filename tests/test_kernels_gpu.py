@@ -171,6 +171,8 @@ ATTN_CASES = [
     (1, 2, 257, 257, True, True, False, 0.1, 1.0),
     (1, 2, 1, 33, True, False, True, 0.0, 1.0),        # single-token decode step with cache
     (2, 12, 1024, 1024, True, True, False, 0.1, 1.0),  # t5-base encoder shape
+    (2, 3, 300, 600, True, "heavy", False, 0.1, 1.0),  # short dialogue padded to max length: skipped key tiles
+    (2, 2, 64, 600, False, "heavy", False, 0.1, 0.125),  # same for cross-attention
 ]
 
 
@@ -186,6 +188,8 @@ def test_attention(B, H, Sq, Sk, bias, kpm, causal, p, scale):
     if kpm:
         mask = torch.ones(B, Sk, dtype=torch.bool, device=DEV)
         mask[0, Sk - Sk // 5:] = False
+        if kpm == "heavy":  # batch 0: only the first 70 keys are real (whole 64-key tiles / 128-key blocks padded)
+            mask[0, 70:] = False
     seed = 4242
     qs, ks, vs = (t.clone().requires_grad_(True) for t in (q, k, v))
     tab1 = table.clone().requires_grad_(True) if bias else None
