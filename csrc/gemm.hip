@@ -63,7 +63,7 @@ DLLM_DEVICE bf16x8v frag(const uint16_t* T, int kk, int cb, int lane) {
   return __builtin_bit_cast(bf16x8v, v);
 }
 
-template <int BK, int NBUF>
+template <int BK, int NBUF, bool PRIO>
 __global__ __launch_bounds__(NT, 1) void gemm_wgrad_kernel(GemmWgradParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint16_t* lds = reinterpret_cast<uint16_t*>(smem);  // [NBUF][A tile | B tile], each [BK][256]
@@ -135,10 +135,12 @@ __global__ __launch_bounds__(NT, 1) void gemm_wgrad_kernel(GemmWgradParams P) {
       for (int i = 0; i < 4; ++i) a[i] = frag(As, kk, wm * 128 + 32 * i, lane);
 #pragma unroll
       for (int j = 0; j < 2; ++j) b[j] = frag(Bs, kk, wn * 64 + 32 * j, lane);
+      if (PRIO) __builtin_amdgcn_s_setprio(1);  // MFMA-issuing wave first (the other wave is reading LDS)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+      if (PRIO) __builtin_amdgcn_s_setprio(0);
     }
   }
 
@@ -196,17 +198,17 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   }
 }
 
-template <int BK, int NBUF>
+template <int BK, int NBUF, bool PRIO = false>
 int launch_wgrad(const GemmWgradParams& p, hipStream_t st) {
   const size_t lds = (size_t)NBUF * 2 * BK * 256 * 2;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_wgrad_kernel<BK, NBUF>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)gemm_wgrad_kernel<BK, NBUF, PRIO>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds);
     attr = true;
   }
   const int nblk = p.ntiles * p.splits;
-  hipLaunchKernelGGL((gemm_wgrad_kernel<BK, NBUF>), dim3(nblk), dim3(NT), lds, st, p);
+  hipLaunchKernelGGL((gemm_wgrad_kernel<BK, NBUF, PRIO>), dim3(nblk), dim3(NT), lds, st, p);
   DLLM_CHECK_LAUNCH();
   if (p.splits > 1) {
     const long n8 = (long)p.M * p.N / 8;
@@ -222,13 +224,16 @@ int launch_wgrad(const GemmWgradParams& p, hipStream_t st) {
 
 extern "C" int dllm_gemm_wgrad_bk() { return 64; }
 
-// variant: 0 = BK64 x 2 stages (128 KB LDS), 1 = BK32 x 4 stages (128 KB), 2 = BK32 x 3 stages (96 KB)
+// variant: 0 = BK64 x 2 stages (128 KB LDS), 1 = BK32 x 4 stages (128 KB), 2 = BK32 x 3 stages (96 KB),
+// 3 / 4 = variants 0 / 1 with s_setprio raised around the MFMA block
 extern "C" int dllm_gemm_wgrad(const GemmWgradParams* pp, int variant, hipStream_t st) {
   const GemmWgradParams& p = *pp;
   if (p.M % BM || p.N % BN || p.K <= 0 || p.splits < 1 || p.ntiles != (p.M / BM) * (p.N / BN)) return -4;
   switch (variant) {
     case 1: return launch_wgrad<32, 4>(p, st);
     case 2: return launch_wgrad<32, 3>(p, st);
+    case 3: return launch_wgrad<64, 2, true>(p, st);
+    case 4: return launch_wgrad<32, 4, true>(p, st);
     default: return launch_wgrad<64, 2>(p, st);
   }
 }

@@ -139,3 +139,17 @@ def test_dropout_rng_statistics_and_reproducibility():
     assert (k1 != k3).float().mean() > 0.1
     a = rng.attention_keep_mask(5, 0.25, 2, 3, 7, 9, "cpu")
     assert a.shape == (2, 3, 7, 9) and abs(1 - a.float().mean().item() - 0.25) < 0.08
+
+
+def test_calculate_metric_on_test_ds_cpu():
+    from distributed_llms_example_amd.data.tokenization import WordTokenizer
+    from distributed_llms_example_amd.train.evaluation import calculate_metric_on_test_ds, generate_batch_sized_chunks
+    assert [list(c) for c in generate_batch_sized_chunks(list(range(7)), 3)] == [[0, 1, 2], [3, 4, 5], [6]]
+    ds = {"article": ["the cat sat on the mat", "a dog ran in the park", "birds fly south"],
+          "highlights": ["cat on mat", "dog in park", "birds fly"]}
+    tok = WordTokenizer.build(ds["article"] + ds["highlights"], 500)
+    torch.manual_seed(0)
+    m = build_model("t5-tiny")
+    scores = calculate_metric_on_test_ds(m, tok, ds, batch_size=2, max_source_length=16, num_beams=2, max_length=6)
+    assert set(scores) >= {"rouge1", "rouge2", "rougeL", "rougeLsum"}
+    assert all(0.0 <= v <= 1.0 for v in scores.values())

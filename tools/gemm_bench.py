@@ -28,21 +28,26 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--variants", default="0,1,2")
+    ap.add_argument("--shapes", default=None, help="K:M:N,... (default: the T5/BART training set)")
+    ap.add_argument("--no-torch", action="store_true")
     a = ap.parse_args()
     tunableop.enable(0)
     C = _ext.native()
     shapes = [(65536, 768, 768), (65536, 2304, 768), (65536, 3072, 768), (65536, 768, 3072),
               (65536, 18432, 768), (8192, 768, 768), (8192, 2304, 768), (8192, 3072, 768), (8192, 768, 3072),
               (32768, 1024, 1024), (32768, 4096, 1024), (32768, 1024, 4096)]
+    if a.shapes:
+        shapes = [tuple(int(x) for x in sh.split(":")) for sh in a.shapes.split(",")]
     for K, M, N in shapes:
         dy = torch.randn(K, M, device="cuda", dtype=torch.bfloat16)
         x = torch.randn(K, N, device="cuda", dtype=torch.bfloat16)
         g = torch.zeros(M, N, device="cuda", dtype=torch.bfloat16)
         fl = 2.0 * K * M * N
         rec = {"K": K, "M": M, "N": N}
-        t = timeit(lambda: g.addmm_(dy.t(), x), a.iters)
-        rec["torch_us"] = round(t * 1e6, 1)
-        rec["torch_tflops"] = round(fl / t / 1e12, 1)
+        if not a.no_torch:
+            t = timeit(lambda: g.addmm_(dy.t(), x), a.iters)
+            rec["torch_us"] = round(t * 1e6, 1)
+            rec["torch_tflops"] = round(fl / t / 1e12, 1)
         ref = dy.float().t() @ x.float()
         for v in map(int, a.variants.split(",")):
             g.zero_()

@@ -8,7 +8,8 @@ from collections import defaultdict
 def family(name):
     if name.startswith("Cijk") or name.startswith("Custom_Cijk"):
         return "GEMM (hipBLASLt)"
-    m = re.search(r"(attn_\w+|norm_\w+|act_\w+|ce_\w+|adamw\w*|col_sum\w*|sq_norm\w*|dropout\w*|sum_partials)", name)
+    m = re.search(r"\b(attn_\w+|norm_\w+|act_\w+|ce_\w+|adamw\w*|col_sum\w*|colsum\w*|sq_norm\w*|dropout\w*|"
+                  r"sum_partials|gemm_wgrad\w*|splitk_reduce\w*)", name)
     if m:
         return m.group(1)
     m = re.search(r"at::native::(\w+)", name)
