@@ -111,12 +111,46 @@ DLLM_DEVICE uint32_t pair_hash(uint32_t rh, uint32_t kpg) {
   return x ^ (x >> 16);
 }
 
+// Dropout keep bits of one (row, 64-key tile, lane half): bit i <-> key kbase + crow(i, hh) (the forward's
+// s0[i]), bit 16 + i <-> key kbase + 32 + crow(i, hh) (s1[i]); one hash per adjacent key pair (ops/rng.py).
+DLLM_DEVICE uint32_t dropout_word(uint32_t rh, int kbase, int hh, uint32_t thr) {
+  const uint32_t tbase = (uint32_t)(kbase >> 1) * HG + (uint32_t)(2 * hh) * HG;
+  uint32_t word = 0;
+#pragma unroll
+  for (int i = 0; i < 16; i += 2) {
+    const uint32_t kpg = tbase + (uint32_t)(((i & 3) >> 1) + 4 * (i >> 2)) * HG;
+    const uint32_t x0 = pair_hash(rh, kpg);
+    const uint32_t x1 = pair_hash(rh, kpg + 16u * HG);  // keys + 32
+    word |= ((x0 & 0xFFFFu) >= thr ? 1u << i : 0u) | ((x0 >> 16) >= thr ? 2u << i : 0u) |
+            ((x1 & 0xFFFFu) >= thr ? 0x10000u << i : 0u) | ((x1 >> 16) >= thr ? 0x20000u << i : 0u);
+  }
+  return word;
+}
+
+// ================================================================================== dropout bit planes
+// All keep decisions of one attention call, [B*H][n_ktiles][2][sq_pad] words, one thread per word (q fastest:
+// coalesced stores).  Pure VALU + streaming stores: generating the mask here instead of inside the flash
+// forward keeps the hash off the forward's critical path (it was ~1/3 of the forward's time at p = 0.1).
+__global__ __launch_bounds__(256) void attn_dropout_mask_kernel(AttnParams P, long nwords) {
+  for (long w = (long)blockIdx.x * blockDim.x + threadIdx.x; w < nwords; w += (long)gridDim.x * blockDim.x) {
+    const int q = (int)(w % P.sq_pad);
+    const long r = w / P.sq_pad;
+    const int hh = (int)(r & 1);
+    const long t2 = r >> 1;
+    const int kt = (int)(t2 % P.n_ktiles);
+    const long bh = t2 / P.n_ktiles;
+    const uint32_t rh = mix32(P.seed, (uint32_t)(bh * P.Sq + q));
+    P.dmask[w] = dropout_word(rh, kt * FWD_BN, hh, P.thr);
+  }
+}
+
 // ================================================================================== forward
-template <bool HAS_BIAS, bool HAS_KPM, bool CAUSAL, bool DROP, bool PIPE>
+template <bool HAS_BIAS, bool HAS_KPM, bool CAUSAL, bool DROP>
 __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint16_t* KV = reinterpret_cast<uint16_t*>(smem);            // [3 buffers][K tile | V tile]
-  float* kmask = reinterpret_cast<float*>(KV + 6 * TILE64);     // [ntiles * 64]: 0 or -inf per key
+  uint32_t* mwl = reinterpret_cast<uint32_t*>(KV + 6 * TILE64); // [3][4 waves][2 halves][32 rows] keep bits
+  float* kmask = reinterpret_cast<float*>(mwl + 3 * 256);       // [ntiles * 64]: 0 or -inf per key
   int* tflag = reinterpret_cast<int*>(kmask + P.n_ktiles * FWD_BN);  // [ntiles]: tile has a masked key
   float* lut_s = reinterpret_cast<float*>(tflag + P.n_ktiles);   // [Sk + FWD_BM + FWD_BN], log2-scaled
 
@@ -151,7 +185,6 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
     }
   }
   const long row_g = (long)(b * P.H + h) * P.Sq + qrow;
-  const uint32_t rh = DROP ? mix32(P.seed, (uint32_t)row_g) : 0u;
   const float dscale = DROP ? 1.f / (1.f - P.p_drop) : 1.f;
 
   int kend = P.Sk;
@@ -165,6 +198,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
   // lane L of DMA j lands at row 8j + L/8, physical chunk L%8 and fetches logical chunk (L%8) ^ swz(row).
   // Keys past Sk re-read row Sk-1 (finite values; masked to -inf / P = 0).  No staging VGPRs, no ds_write.
   const uint32_t kv_lds = lds_addr(KV);
+  const uint32_t mw_lds = lds_addr(mwl);
   auto issue_tile = [&](int buf, int kt) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -178,6 +212,9 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
       glds16(P.v + b * P.v_sb + (long)kk * P.v_ss + h * P.v_sh + c * 8,
              __builtin_amdgcn_readfirstlane(dst + TILE64 * 2));
     }
+    if (DROP)  // this wave's 32 rows x 2 lane halves of keep bits: lane L -> half L/32, row qw0 + L%32
+      glds4(P.dmask + ((long)bh * P.n_ktiles * 2 + 2 * kt + hh) * P.sq_pad + qrow,
+            __builtin_amdgcn_readfirstlane(mw_lds + (uint32_t)((buf * 256 + w * 64) * 4)));
   };
   for (int t = w; t < ntiles; t += 4) {  // wave-per-tile: per-key mask + "tile has a masked key" flag
     const int j = t * FWD_BN + lane;
@@ -203,7 +240,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
     }
   };
   // online softmax of tile kt's scores (in s0/s1) and O^T += V^T P^T with V from buffer `buf`
-  auto softmax_pv = [&](int kt, int buf, f32x16& s0, f32x16& s1) {
+  auto softmax_pv = [&](int kt, int buf, f32x16& s0, f32x16& s1, uint32_t mword) {
     const int kbase = kt * FWD_BN;
     const uint16_t* Vb = KV + buf * 2 * TILE64 + TILE64;
     const bool tile_causal = CAUSAL && (kbase + FWD_BN - 1 > qw0 + P.causal_off);
@@ -266,24 +303,12 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
       }
     }
     if (DROP) {
-      // keep decisions -> P (the 1/(1-p) scale is applied once to O at the end) and one bit word per lane and
-      // tile for the backward kernels (bit i <-> s0[i], bit 16+i <-> s1[i]): they never re-hash
-      const uint32_t tbase = (uint32_t)(kbase >> 1) * HG + (uint32_t)(2 * hh) * HG;
-      uint32_t word = 0;
+      // keep bits from the precomputed planes (attn_dropout_mask_kernel); the 1/(1-p) scale is applied to O
 #pragma unroll
-      for (int i = 0; i < 16; i += 2) {
-        const uint32_t kpg = tbase + (uint32_t)(((i & 3) >> 1) + 4 * (i >> 2)) * HG;
-        const uint32_t x0 = pair_hash(rh, kpg);
-        const uint32_t x1 = pair_hash(rh, kpg + 16u * HG);  // keys + 32
-        const bool k0a = (x0 & 0xFFFFu) >= P.thr, k0b = (x0 >> 16) >= P.thr;
-        const bool k1a = (x1 & 0xFFFFu) >= P.thr, k1b = (x1 >> 16) >= P.thr;
-        s0[i] = k0a ? s0[i] : 0.f;
-        s0[i + 1] = k0b ? s0[i + 1] : 0.f;
-        s1[i] = k1a ? s1[i] : 0.f;
-        s1[i + 1] = k1b ? s1[i + 1] : 0.f;
-        word |= (k0a ? 1u << i : 0u) | (k0b ? 2u << i : 0u) | (k1a ? 0x10000u << i : 0u) | (k1b ? 0x20000u << i : 0u);
+      for (int i = 0; i < 16; ++i) {
+        s0[i] = __uint_as_float(__float_as_uint(s0[i]) & (uint32_t)__builtin_amdgcn_sbfe((int)mword, i, 1));
+        s1[i] = __uint_as_float(__float_as_uint(s1[i]) & (uint32_t)__builtin_amdgcn_sbfe((int)mword, 16 + i, 1));
       }
-      P.dmask[((long)bh * P.n_ktiles * 2 + 2 * kt + hh) * P.sq_pad + qrow] = word;
     }
     // O^T += V^T P^T
     const bf16x8v pa0 = pack8(s0, 0), pa1 = pack8(s0, 8), pb0 = pack8(s1, 0), pb1 = pack8(s1, 8);
@@ -299,43 +324,27 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
     }
   };
 
-  // Software pipeline over a 3-buffer K/V ring: while the VALU runs tile kt's softmax, the matrix core already
-  // computes tile kt+1's scores (issued first, independent registers); tile kt+2's DMA goes into the buffer
-  // tile kt-1 vacated and has a whole tile of compute to land.  One barrier per tile.
-  f32x16 sa0, sa1, sb0, sb1;
+  // 3-buffer K/V ring: tile kt+2's DMA goes into the buffer tile kt-1 vacated and has a whole tile of compute to
+  // land; one barrier per tile.  With dropout each wave also DMAs its 64 keep-bit words of the tile (4 B/lane).
+  f32x16 sa0, sa1;
+  constexpr int DPT = DROP ? 5 : 4;  // DMAs per wave per tile
   if (ntiles > 0) issue_tile(0, 0);
   if (ntiles > 1) issue_tile(1, 1);
   wait_vm<0>();
   __syncthreads();
-  if (PIPE) {
-    if (ntiles > 0) scores(0, sa0, sa1);
-    for (int kt = 0; kt < ntiles; kt += 2) {
-      wait_vm<0>();     // this wave's DMA of tile kt+1 landed ...
-      __syncthreads();  // ... and everyone's; every wave is done with tile kt-1's buffer
-      if (kt + 1 < ntiles) scores((kt + 1) % 3, sb0, sb1);
-      softmax_pv(kt, kt % 3, sa0, sa1);
-      if (kt + 2 < ntiles) issue_tile((kt + 2) % 3, kt + 2);
-      if (kt + 1 >= ntiles) break;
-      wait_vm<0>();
+  for (int kt = 0; kt < ntiles; ++kt) {
+    if (kt > 0) {
+      // tile kt landed (this wave's DMAs of tile kt+1, issued one tile later, may stay in flight)
+      if (kt + 1 < ntiles) wait_vm<DPT>();
+      else wait_vm<0>();
       __syncthreads();
-      if (kt + 2 < ntiles) scores((kt + 2) % 3, sa0, sa1);
-      softmax_pv(kt + 1, (kt + 1) % 3, sb0, sb1);
-      if (kt + 3 < ntiles) issue_tile((kt + 3) % 3, kt + 3);
     }
-  } else {
-    for (int kt = 0; kt < ntiles; ++kt) {
-      if (kt > 0) {
-        // tile kt landed (this wave's 4 DMAs of tile kt+1, issued one tile later, may stay in flight)
-        if (kt + 1 < ntiles) wait_vm<4>();
-        else wait_vm<0>();
-        __syncthreads();
-      }
-      if (!HAS_KPM || tflag[kt] != 2) {  // a fully padded key tile contributes exactly nothing
-        scores(kt % 3, sa0, sa1);
-        softmax_pv(kt, kt % 3, sa0, sa1);
-      }
-      if (kt + 2 < ntiles) issue_tile((kt + 2) % 3, kt + 2);
+    if (!HAS_KPM || tflag[kt] != 2) {  // a fully padded key tile contributes exactly nothing
+      scores(kt % 3, sa0, sa1);
+      const uint32_t mword = DROP ? mwl[(kt % 3) * 256 + w * 64 + hh * 32 + r] : 0u;
+      softmax_pv(kt, kt % 3, sa0, sa1, mword);
     }
+    if (kt + 2 < ntiles) issue_tile((kt + 2) % 3, kt + 2);
   }
 
   const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
@@ -776,20 +785,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnParams P) {
     }                                                                                   \
   } while (0)
 
-// DLLM_ATTN_FWD_PIPE=1: software-pipelined forward (next tile's QK^T issued before this tile's softmax)
-bool fwd_pipe() {
-  static bool v = [] {
-    const char* e = getenv("DLLM_ATTN_FWD_PIPE");
-    return e && atoi(e) == 1;
-  }();
-  return v;
-}
 template <bool HB, bool HK, bool CA, bool DR>
 void launch_fwd_t(const AttnParams& p, int nblk, size_t lds, hipStream_t st) {
-  if (fwd_pipe())
-    hipLaunchKernelGGL((attn_fwd_kernel<HB, HK, CA, DR, true>), dim3(nblk), dim3(256), lds, st, p);
-  else
-    hipLaunchKernelGGL((attn_fwd_kernel<HB, HK, CA, DR, false>), dim3(nblk), dim3(256), lds, st, p);
+  hipLaunchKernelGGL((attn_fwd_kernel<HB, HK, CA, DR>), dim3(nblk), dim3(256), lds, st, p);
 }
 template <bool HB, bool HK, bool CA, bool DR>
 void launch_bwd_dq_t(const AttnParams& p, int nblk, size_t lds, hipStream_t st) {
@@ -812,9 +810,15 @@ extern "C" int dllm_attn_fwd(AttnParams* pp, hipStream_t st) {
   p.sq_pad = p.n_tiles * FWD_BM;
   if (p.p_drop > 0.f && p.dmask == nullptr) return -5;  // the caller allocates the dropout bit planes
   // 3 K/V buffers + per-key mask + bias LUT window
-  size_t lds = (size_t)6 * TILE64 * 2 + (size_t)p.n_ktiles * (FWD_BN + 1) * 4;
+  size_t lds = (size_t)6 * TILE64 * 2 + 3 * 256 * 4 + (size_t)p.n_ktiles * (FWD_BN + 1) * 4;
   if (p.lut) lds += (size_t)(p.Sk + FWD_BM + FWD_BN) * 4;
   if (nblk <= 0 || nblk > 0x7fffffff || lds > 160 * 1024) return -4;
+  if (p.p_drop > 0.f) {  // keep-bit planes for this call (read by the forward and both backward kernels)
+    const long nwords = (long)p.B * p.H * p.n_ktiles * 2 * p.sq_pad;
+    const int blocks = (int)std::min<long>((nwords + 255) / 256, 65536);
+    hipLaunchKernelGGL(attn_dropout_mask_kernel, dim3(blocks), dim3(256), 0, st, p, nwords);
+    DLLM_CHECK_LAUNCH();
+  }
   DISPATCH4(launch_fwd_t, p.lut != nullptr, p.kpm != nullptr, p.causal != 0, p.p_drop > 0.f, p, (int)nblk, lds, st);
   DLLM_CHECK_LAUNCH();
   return 0;

@@ -148,6 +148,15 @@ DLLM_DEVICE void glds16(const uint16_t* g, uint32_t lds_byte) {
                : "memory");
 }
 
+// 4 B per lane variant (lane i -> lds_byte + 4 i)
+DLLM_DEVICE void glds4(const void* g, uint32_t lds_byte) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(g), "s"(lds_byte)
+               : "memory");
+}
+
 DLLM_DEVICE uint32_t lds_addr(const void* p) {
   return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
 }

@@ -63,17 +63,20 @@ DLLM_DEVICE bf16x8v frag(const uint16_t* T, int kk, int cb, int lane) {
   return __builtin_bit_cast(bf16x8v, v);
 }
 
-template <int BK, int NBUF, bool PRIO>
-__global__ __launch_bounds__(NT, 1) void gemm_wgrad_kernel(GemmWgradParams P) {
+// NI = 32x32 MFMA tiles per wave along N: NI = 2 -> 8 waves of 128x64 (2 waves per SIMD), NI = 4 -> 4 waves of
+// 128x128 (one wave per SIMD, 256 fp32 accumulators in AGPRs, next k-step's fragments prefetched in VGPRs)
+template <int BK, int NBUF, bool PRIO, int NI>
+__global__ __launch_bounds__((256 / (32 * NI)) * 2 * 64, 1) void gemm_wgrad_kernel(GemmWgradParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint16_t* lds = reinterpret_cast<uint16_t*>(smem);  // [NBUF][A tile | B tile], each [BK][256]
+  constexpr int WAVES_N = 256 / (32 * NI), NW = 2 * WAVES_N;
   constexpr int TILE = BK * 256;
-  constexpr int PW = BK / 16;  // DMA instructions per wave per operand per stage (1 KB = 2 rows each)
-  constexpr int LPS = 2 * PW;  // per wave per stage (A + B)
-  static_assert(NBUF >= 2 && NBUF <= 4, "ring depth");
+  constexpr int PW = (BK / 2) / NW;  // DMA instructions per wave per operand per stage (1 KB = 2 rows each)
+  constexpr int LPS = 2 * PW;        // per wave per stage (A + B)
+  static_assert(NBUF >= 2 && NBUF <= 4 && PW >= 1, "ring depth / DMA split");
 
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, hh = lane >> 5;
-  const int wm = w >> 2, wn = w & 3;
+  const int wm = w / WAVES_N, wn = w % WAVES_N;
   const int logical = xcd_remap(blockIdx.x, gridDim.x);
   const int s = logical / P.ntiles, t = logical % P.ntiles;
   const int m0 = (t / P.tn) * BM, n0 = (t % P.tn) * BN;
@@ -103,11 +106,11 @@ __global__ __launch_bounds__(NT, 1) void gemm_wgrad_kernel(GemmWgradParams P) {
     }
   };
 
-  f32x16 acc[4][2];
+  f32x16 acc[4][NI];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < NI; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
@@ -128,29 +131,37 @@ __global__ __launch_bounds__(NT, 1) void gemm_wgrad_kernel(GemmWgradParams P) {
     if (it + NBUF - 1 < nk) issue((it + NBUF - 1) % NBUF, it + NBUF - 1);
     const uint16_t* As = lds + (it % NBUF) * 2 * TILE;
     const uint16_t* Bs = As + TILE;
+    bf16x8v a[2][4], b[2][NI];
 #pragma unroll
-    for (int kk = 0; kk < BK; kk += 16) {
-      bf16x8v a[4], b[2];
+    for (int i = 0; i < 4; ++i) a[0][i] = frag(As, 0, wm * 128 + 32 * i, lane);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) a[i] = frag(As, kk, wm * 128 + 32 * i, lane);
+    for (int j = 0; j < NI; ++j) b[0][j] = frag(Bs, 0, wn * 32 * NI + 32 * j, lane);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) b[j] = frag(Bs, kk, wn * 64 + 32 * j, lane);
-      if (PRIO) __builtin_amdgcn_s_setprio(1);  // MFMA-issuing wave first (the other wave is reading LDS)
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      const int cur = ks & 1;
+      if (ks + 1 < BK / 16) {  // next k-step's fragments in flight while this step's MFMAs run
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[cur ^ 1][i] = frag(As, 16 * (ks + 1), wm * 128 + 32 * i, lane);
+#pragma unroll
+        for (int j = 0; j < NI; ++j) b[cur ^ 1][j] = frag(Bs, 16 * (ks + 1), wn * 32 * NI + 32 * j, lane);
+      }
+      if (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[cur][i], b[cur][j], acc[i][j], 0, 0, 0);
       if (PRIO) __builtin_amdgcn_s_setprio(0);
     }
   }
 
-  // epilogue: lane owns column n0 + wn*64 + 32j + (lane & 31) of rows m0 + wm*128 + 32i + crow(reg)
-  const int ncol = n0 + wn * 64 + (lane & 31);
+  // epilogue: lane owns column n0 + wn*32*NI + 32j + (lane & 31) of rows m0 + wm*128 + 32i + crow(reg)
+  const int ncol = n0 + wn * 32 * NI + (lane & 31);
   if (P.splits == 1) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < NI; ++j)
 #pragma unroll
         for (int reg = 0; reg < 16; ++reg) {
           const int m = m0 + wm * 128 + 32 * i + crow(reg, hh);
@@ -164,7 +175,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_wgrad_kernel(GemmWgradParams P) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < NI; ++j)
 #pragma unroll
         for (int reg = 0; reg < 16; ++reg) {
           const int m = m0 + wm * 128 + 32 * i + crow(reg, hh);
@@ -198,17 +209,18 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   }
 }
 
-template <int BK, int NBUF, bool PRIO = false>
+template <int BK, int NBUF, bool PRIO = false, int NI = 2>
 int launch_wgrad(const GemmWgradParams& p, hipStream_t st) {
+  constexpr int threads = (256 / (32 * NI)) * 2 * 64;
   const size_t lds = (size_t)NBUF * 2 * BK * 256 * 2;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_wgrad_kernel<BK, NBUF, PRIO>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)gemm_wgrad_kernel<BK, NBUF, PRIO, NI>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds);
     attr = true;
   }
   const int nblk = p.ntiles * p.splits;
-  hipLaunchKernelGGL((gemm_wgrad_kernel<BK, NBUF, PRIO>), dim3(nblk), dim3(NT), lds, st, p);
+  hipLaunchKernelGGL((gemm_wgrad_kernel<BK, NBUF, PRIO, NI>), dim3(nblk), dim3(threads), lds, st, p);
   DLLM_CHECK_LAUNCH();
   if (p.splits > 1) {
     const long n8 = (long)p.M * p.N / 8;
@@ -225,15 +237,20 @@ int launch_wgrad(const GemmWgradParams& p, hipStream_t st) {
 extern "C" int dllm_gemm_wgrad_bk() { return 64; }
 
 // variant: 0 = BK64 x 2 stages (128 KB LDS), 1 = BK32 x 4 stages (128 KB), 2 = BK32 x 3 stages (96 KB),
-// 3 / 4 = variants 0 / 1 with s_setprio raised around the MFMA block
+// 3 / 4 = variants 0 / 1 with s_setprio raised around the MFMA block,
+// 5 / 6 = variants 0 / 1 with 4 waves of 128x128 (one wave per SIMD, accumulators in AGPRs)
 extern "C" int dllm_gemm_wgrad(const GemmWgradParams* pp, int variant, hipStream_t st) {
   const GemmWgradParams& p = *pp;
   if (p.M % BM || p.N % BN || p.K <= 0 || p.splits < 1 || p.ntiles != (p.M / BM) * (p.N / BN)) return -4;
+  if (variant < 0)  // auto: deep BK=32 ring + prioritised MFMA issue on long K (measured best at K >= 32k)
+    variant = p.K >= 32768 ? 4 : 0;
   switch (variant) {
     case 1: return launch_wgrad<32, 4>(p, st);
     case 2: return launch_wgrad<32, 3>(p, st);
     case 3: return launch_wgrad<64, 2, true>(p, st);
     case 4: return launch_wgrad<32, 4, true>(p, st);
+    case 5: return launch_wgrad<64, 2, false, 4>(p, st);
+    case 6: return launch_wgrad<32, 4, false, 4>(p, st);
     default: return launch_wgrad<64, 2>(p, st);
   }
 }

@@ -13,7 +13,7 @@ import torch
 
 from .. import _ext
 
-_VARIANT = int(os.environ.get("DLLM_WGRAD_VARIANT", "0"))
+_VARIANT = int(os.environ.get("DLLM_WGRAD_VARIANT", "-1"))  # -1: pick by K (csrc/gemm.hip)
 
 
 def _native_ok(dy2: torch.Tensor, x2: torch.Tensor, out: torch.Tensor) -> bool:

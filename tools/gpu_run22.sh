@@ -1,0 +1,14 @@
+#!/bin/bash
+set -o pipefail
+export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 600 python -m pytest tests/ -q -m gpu -x > gpurun_out/gputests22.log 2>&1 || { echo GT_FAIL; grep -E "Error|error|assert|FAILED|passed|failed" gpurun_out/gputests22.log | tail -20; exit 1; }
+tail -1 gpurun_out/gputests22.log
+timeout -k 10 300 python tools/attn_bench.py > gpurun_out/attn22.jsonl 2>&1 || { echo AB_FAIL; tail -5 gpurun_out/attn22.jsonl; exit 1; }
+grep '^{' gpurun_out/attn22.jsonl | cut -c1-200
+timeout -k 10 300 python bench.py > gpurun_out/bench22.log 2>&1 || { echo BENCH_FAIL; tail -20 gpurun_out/bench22.log; exit 1; }
+tail -1 gpurun_out/bench22.log | cut -c1-220
+cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof22 -o run --output-format csv -- python3 $R/bench.py --steps 5 --warmup 2 > $R/gpurun_out/prof22.log 2>&1 || { echo PROF_FAIL; tail -20 $R/gpurun_out/prof22.log; exit 1; }
+rm -f $R/gpurun_out/prof22/run_kernel_trace.csv
+python3 $R/tools/prof_summary.py $R/gpurun_out/prof22/run_kernel_stats.csv 7 > $R/gpurun_out/prof22_summary.txt; head -45 $R/gpurun_out/prof22_summary.txt
