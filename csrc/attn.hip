@@ -129,8 +129,8 @@ DLLM_DEVICE uint32_t dropout_word(uint32_t rh, int kbase, int hh, uint32_t thr) 
 
 // ================================================================================== dropout bit planes
 // All keep decisions of one attention call, [B*H][n_ktiles][2][sq_pad] words, one thread per word (q fastest:
-// coalesced stores).  Pure VALU + streaming stores: generating the mask here instead of inside the flash
-// forward keeps the hash off the forward's critical path (it was ~1/3 of the forward's time at p = 0.1).
+// coalesced stores).  Pure VALU + streaming stores, for generating the planes ahead of the forward on a side
+// stream (ops/attention.py prefetch_dropout_mask) where they overlap the projection GEMM.
 __global__ __launch_bounds__(256) void attn_dropout_mask_kernel(AttnParams P, long nwords) {
   for (long w = (long)blockIdx.x * blockDim.x + threadIdx.x; w < nwords; w += (long)gridDim.x * blockDim.x) {
     const int q = (int)(w % P.sq_pad);
@@ -145,11 +145,13 @@ __global__ __launch_bounds__(256) void attn_dropout_mask_kernel(AttnParams P, lo
 }
 
 // ================================================================================== forward
-template <bool HAS_BIAS, bool HAS_KPM, bool CAUSAL, bool DROP>
+// DROP_IN: dropout keep bits are read from precomputed planes (attn_dropout_mask_kernel on a side stream);
+// otherwise the forward hashes them itself (hidden in its MFMA/LDS latency) and stores the planes for backward.
+template <bool HAS_BIAS, bool HAS_KPM, bool CAUSAL, bool DROP, bool DROP_IN>
 __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint16_t* KV = reinterpret_cast<uint16_t*>(smem);            // [3 buffers][K tile | V tile]
-  uint32_t* mwl = reinterpret_cast<uint32_t*>(KV + 6 * TILE64); // [3][4 waves][2 halves][32 rows] keep bits
+  uint32_t* mwl = reinterpret_cast<uint32_t*>(KV + 6 * TILE64); // [3][4 waves][2 halves][32 rows] keep bits (DROP_IN)
   float* kmask = reinterpret_cast<float*>(mwl + 3 * 256);       // [ntiles * 64]: 0 or -inf per key
   int* tflag = reinterpret_cast<int*>(kmask + P.n_ktiles * FWD_BN);  // [ntiles]: tile has a masked key
   float* lut_s = reinterpret_cast<float*>(tflag + P.n_ktiles);   // [Sk + FWD_BM + FWD_BN], log2-scaled
@@ -185,6 +187,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
     }
   }
   const long row_g = (long)(b * P.H + h) * P.Sq + qrow;
+  const uint32_t rh = DROP ? mix32(P.seed, (uint32_t)row_g) : 0u;
   const float dscale = DROP ? 1.f / (1.f - P.p_drop) : 1.f;
 
   int kend = P.Sk;
@@ -212,7 +215,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
       glds16(P.v + b * P.v_sb + (long)kk * P.v_ss + h * P.v_sh + c * 8,
              __builtin_amdgcn_readfirstlane(dst + TILE64 * 2));
     }
-    if (DROP)  // this wave's 32 rows x 2 lane halves of keep bits: lane L -> half L/32, row qw0 + L%32
+    if (DROP && DROP_IN)  // this wave's 32 rows x 2 lane halves of keep bits: lane L -> half L/32, row qw0 + L%32
       glds4(P.dmask + ((long)bh * P.n_ktiles * 2 + 2 * kt + hh) * P.sq_pad + qrow,
             __builtin_amdgcn_readfirstlane(mw_lds + (uint32_t)((buf * 256 + w * 64) * 4)));
   };
@@ -240,7 +243,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
     }
   };
   // online softmax of tile kt's scores (in s0/s1) and O^T += V^T P^T with V from buffer `buf`
-  auto softmax_pv = [&](int kt, int buf, f32x16& s0, f32x16& s1, uint32_t mword) {
+  auto softmax_pv = [&](int kt, int buf, f32x16& s0, f32x16& s1) {
+    const uint32_t mword = (DROP && DROP_IN) ? mwl[buf * 256 + w * 64 + hh * 32 + r] : 0u;
     const int kbase = kt * FWD_BN;
     const uint16_t* Vb = KV + buf * 2 * TILE64 + TILE64;
     const bool tile_causal = CAUSAL && (kbase + FWD_BN - 1 > qw0 + P.causal_off);
@@ -302,13 +306,31 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
         o1[i] *= alpha;
       }
     }
-    if (DROP) {
-      // keep bits from the precomputed planes (attn_dropout_mask_kernel); the 1/(1-p) scale is applied to O
+    if (DROP && DROP_IN) {  // precomputed keep bits; the 1/(1-p) scale is applied once to O at the end
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         s0[i] = __uint_as_float(__float_as_uint(s0[i]) & (uint32_t)__builtin_amdgcn_sbfe((int)mword, i, 1));
         s1[i] = __uint_as_float(__float_as_uint(s1[i]) & (uint32_t)__builtin_amdgcn_sbfe((int)mword, 16 + i, 1));
       }
+    } else if (DROP) {
+      // keep decisions -> P (the 1/(1-p) scale is applied once to O at the end) and one bit word per lane and
+      // tile for the backward kernels (bit i <-> s0[i], bit 16+i <-> s1[i]): they never re-hash
+      const uint32_t tbase = (uint32_t)(kbase >> 1) * HG + (uint32_t)(2 * hh) * HG;
+      uint32_t word = 0;
+#pragma unroll
+      for (int i = 0; i < 16; i += 2) {
+        const uint32_t kpg = tbase + (uint32_t)(((i & 3) >> 1) + 4 * (i >> 2)) * HG;
+        const uint32_t x0 = pair_hash(rh, kpg);
+        const uint32_t x1 = pair_hash(rh, kpg + 16u * HG);  // keys + 32
+        const bool k0a = (x0 & 0xFFFFu) >= P.thr, k0b = (x0 >> 16) >= P.thr;
+        const bool k1a = (x1 & 0xFFFFu) >= P.thr, k1b = (x1 >> 16) >= P.thr;
+        s0[i] = k0a ? s0[i] : 0.f;
+        s0[i + 1] = k0b ? s0[i + 1] : 0.f;
+        s1[i] = k1a ? s1[i] : 0.f;
+        s1[i + 1] = k1b ? s1[i + 1] : 0.f;
+        word |= (k0a ? 1u << i : 0u) | (k0b ? 2u << i : 0u) | (k1a ? 0x10000u << i : 0u) | (k1b ? 0x20000u << i : 0u);
+      }
+      P.dmask[((long)bh * P.n_ktiles * 2 + 2 * kt + hh) * P.sq_pad + qrow] = word;
     }
     // O^T += V^T P^T
     const bf16x8v pa0 = pack8(s0, 0), pa1 = pack8(s0, 8), pb0 = pack8(s1, 0), pb1 = pack8(s1, 8);
@@ -325,24 +347,22 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
   };
 
   // 3-buffer K/V ring: tile kt+2's DMA goes into the buffer tile kt-1 vacated and has a whole tile of compute to
-  // land; one barrier per tile.  With dropout each wave also DMAs its 64 keep-bit words of the tile (4 B/lane).
+  // land; one barrier per tile.
   f32x16 sa0, sa1;
-  constexpr int DPT = DROP ? 5 : 4;  // DMAs per wave per tile
   if (ntiles > 0) issue_tile(0, 0);
   if (ntiles > 1) issue_tile(1, 1);
   wait_vm<0>();
   __syncthreads();
   for (int kt = 0; kt < ntiles; ++kt) {
     if (kt > 0) {
-      // tile kt landed (this wave's DMAs of tile kt+1, issued one tile later, may stay in flight)
-      if (kt + 1 < ntiles) wait_vm<DPT>();
+      // tile kt landed (this wave's 4 DMAs of tile kt+1, issued one tile later, may stay in flight)
+      if (kt + 1 < ntiles) wait_vm<((DROP && DROP_IN) ? 5 : 4)>();
       else wait_vm<0>();
       __syncthreads();
     }
     if (!HAS_KPM || tflag[kt] != 2) {  // a fully padded key tile contributes exactly nothing
       scores(kt % 3, sa0, sa1);
-      const uint32_t mword = DROP ? mwl[(kt % 3) * 256 + w * 64 + hh * 32 + r] : 0u;
-      softmax_pv(kt, kt % 3, sa0, sa1, mword);
+      softmax_pv(kt, kt % 3, sa0, sa1);
     }
     if (kt + 2 < ntiles) issue_tile((kt + 2) % 3, kt + 2);
   }
@@ -787,7 +807,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnParams P) {
 
 template <bool HB, bool HK, bool CA, bool DR>
 void launch_fwd_t(const AttnParams& p, int nblk, size_t lds, hipStream_t st) {
-  hipLaunchKernelGGL((attn_fwd_kernel<HB, HK, CA, DR>), dim3(nblk), dim3(256), lds, st, p);
+  if (DR && p.dmask_ready)
+    hipLaunchKernelGGL((attn_fwd_kernel<HB, HK, CA, DR, true>), dim3(nblk), dim3(256), lds, st, p);
+  else
+    hipLaunchKernelGGL((attn_fwd_kernel<HB, HK, CA, DR, false>), dim3(nblk), dim3(256), lds, st, p);
 }
 template <bool HB, bool HK, bool CA, bool DR>
 void launch_bwd_dq_t(const AttnParams& p, int nblk, size_t lds, hipStream_t st) {
@@ -813,12 +836,6 @@ extern "C" int dllm_attn_fwd(AttnParams* pp, hipStream_t st) {
   size_t lds = (size_t)6 * TILE64 * 2 + 3 * 256 * 4 + (size_t)p.n_ktiles * (FWD_BN + 1) * 4;
   if (p.lut) lds += (size_t)(p.Sk + FWD_BM + FWD_BN) * 4;
   if (nblk <= 0 || nblk > 0x7fffffff || lds > 160 * 1024) return -4;
-  if (p.p_drop > 0.f) {  // keep-bit planes for this call (read by the forward and both backward kernels)
-    const long nwords = (long)p.B * p.H * p.n_ktiles * 2 * p.sq_pad;
-    const int blocks = (int)std::min<long>((nwords + 255) / 256, 65536);
-    hipLaunchKernelGGL(attn_dropout_mask_kernel, dim3(blocks), dim3(256), 0, st, p, nwords);
-    DLLM_CHECK_LAUNCH();
-  }
   DISPATCH4(launch_fwd_t, p.lut != nullptr, p.kpm != nullptr, p.causal != 0, p.p_drop > 0.f, p, (int)nblk, lds, st);
   DLLM_CHECK_LAUNCH();
   return 0;
@@ -848,6 +865,20 @@ extern "C" int dllm_attn_bwd(AttnParams* pp, hipStream_t st) {
   if (nblk <= 0 || nblk > 0x7fffffff || lds > 160 * 1024) return -4;
   DISPATCH4(launch_bwd_dkdv_t, p.lut != nullptr, p.kpm != nullptr, p.causal != 0, p.p_drop > 0.f, p, (int)nblk, lds,
             st);
+  DLLM_CHECK_LAUNCH();
+  return 0;
+}
+
+// keep-bit planes only (same layout/decisions the forward would produce); p.dmask preallocated by the caller
+extern "C" int dllm_attn_dropout_mask(AttnParams* pp, hipStream_t st) {
+  AttnParams p = *pp;
+  if (p.p_drop <= 0.f || p.dmask == nullptr) return -5;
+  p.thr = drop_threshold(p.p_drop);
+  p.n_ktiles = (p.Sk + FWD_BN - 1) / FWD_BN;
+  p.sq_pad = (p.Sq + FWD_BM - 1) / FWD_BM * FWD_BM;
+  const long nwords = (long)p.B * p.H * p.n_ktiles * 2 * p.sq_pad;
+  const int blocks = (int)std::min<long>((nwords + 255) / 256, 65536);
+  hipLaunchKernelGGL(attn_dropout_mask_kernel, dim3(blocks), dim3(256), 0, st, p, nwords);
   DLLM_CHECK_LAUNCH();
   return 0;
 }

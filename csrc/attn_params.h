@@ -36,4 +36,5 @@ struct AttnParams {
   int n_ktiles;  // 64-key tiles (key-mask array length / 64)
   int sq_pad;    // rows of the dropout bit-mask planes (query tiles x 128)
   uint32_t* dmask;  // [B*H][n_ktiles][2][sq_pad] dropout keep bits written by fwd, read by bwd
+  int dmask_ready;  // fwd: planes already generated (attn_dropout_mask) -> read instead of hash
 };

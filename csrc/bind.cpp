@@ -27,6 +27,7 @@ int dllm_adamw(void*, float*, const void*, float*, float*, const uint8_t*, const
 int dllm_attn_fwd(AttnParams*, hipStream_t);
 int dllm_attn_bwd(AttnParams*, hipStream_t);
 int dllm_attn_params_size();
+int dllm_attn_dropout_mask(AttnParams*, hipStream_t);
 int dllm_gemm_wgrad(const GemmWgradParams*, int, hipStream_t);
 int dllm_colsum_rows();
 int dllm_colsum_acc(const void*, long, long, int, float*, void*, int, hipStream_t);
@@ -305,7 +306,8 @@ int64_t dmask_numel(const AttnParams& P) {
 }
 
 std::vector<Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, const optional<Tensor>& kpm,
-                             const optional<Tensor>& lut, double scale, bool causal, double p, int64_t seed) {
+                             const optional<Tensor>& lut, double scale, bool causal, double p, int64_t seed,
+                             const optional<Tensor>& dmask_in) {
   AttnParams P{};
   fill_qkv(P, q, k, v, kpm, lut, scale, causal, p, seed);
   auto o = at::empty({P.B, P.Sq, P.H, 64}, q.options());
@@ -316,11 +318,32 @@ std::vector<Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, 
   // dropout keep bits: [B*H][ceil(Sk/64)][2][ceil(Sq/128)*128] uint32, written here, read by attn_bwd
   Tensor dmask;
   if (p > 0.0) {
-    dmask = at::empty({dmask_numel(P)}, q.options().dtype(at::kInt));
+    if (dmask_in.has_value() && dmask_in->defined()) {  // planes from attn_dropout_mask (same seed and shapes)
+      TORCH_CHECK(dmask_in->scalar_type() == at::kInt && dmask_in->is_contiguous() && dmask_in->is_cuda() &&
+                      dmask_in->numel() == dmask_numel(P),
+                  "attn_fwd: dmask_in must come from attn_dropout_mask for the same shapes");
+      dmask = *dmask_in;
+      P.dmask_ready = 1;
+    } else {
+      dmask = at::empty({dmask_numel(P)}, q.options().dtype(at::kInt));
+    }
     P.dmask = reinterpret_cast<uint32_t*>(dmask.data_ptr());
   }
   check_rc(dllm_attn_fwd(&P, stream()), "attn_fwd");
   return {o, lse, dmask};
+}
+
+// dropout keep-bit planes of an attention call (generated ahead, e.g. on a side stream)
+Tensor attn_dropout_mask(int64_t B, int64_t H, int64_t Sq, int64_t Sk, double p, int64_t seed, const Tensor& like) {
+  TORCH_CHECK(p > 0.0 && B > 0 && H > 0 && Sq > 0 && Sk > 0 && like.is_cuda(), "attn_dropout_mask: bad arguments");
+  AttnParams P{};
+  P.B = B; P.H = H; P.Sq = Sq; P.Sk = Sk;
+  P.p_drop = (float)p;
+  P.seed = (uint32_t)seed;
+  auto dmask = at::empty({dmask_numel(P)}, like.options().dtype(at::kInt));
+  P.dmask = reinterpret_cast<uint32_t*>(dmask.data_ptr());
+  check_rc(dllm_attn_dropout_mask(&P, stream()), "attn_dropout_mask");
+  return dmask;
 }
 
 std::vector<Tensor> attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o,
@@ -458,7 +481,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ce_bwd", &ce_bwd);
   m.def("sq_norm", &sq_norm);
   m.def("adamw_step", &adamw_step);
-  m.def("attn_fwd", &attn_fwd);
+  m.def("attn_fwd", &attn_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("kpm"), py::arg("lut"),
+        py::arg("scale"), py::arg("causal"), py::arg("p"), py::arg("seed"), py::arg("dmask_in") = py::none());
+  m.def("attn_dropout_mask", &attn_dropout_mask);
   m.def("attn_bwd", &attn_bwd, py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"),
         py::arg("lse"), py::arg("kpm"), py::arg("lut"), py::arg("scale"), py::arg("causal"), py::arg("p"),
         py::arg("seed"), py::arg("need_dlut"), py::arg("dq_out") = py::none(), py::arg("dk_out") = py::none(),

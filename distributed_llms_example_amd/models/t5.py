@@ -73,12 +73,13 @@ class T5Attention(nn.Module):
             q = self.q(x).view(B, S, H, D)
             o = attn_ops.attention_q_kv(q, kv if kv is not None else self.project_kv(kv_in), **kw)
         else:
+            pre = attn_ops.prefetch_dropout_mask(x, B, H, S, S, p, seed) if cache is None else None
             qkv = self.qkv(x).view(B, S, 3, H, D)
             if cache is not None:
                 k, v = cache.append(qkv[:, :, 1], qkv[:, :, 2])
                 o = attn_ops.attention(qkv[:, :, 0], k, v, **kw)
             else:
-                o = attn_ops.attention_qkv(qkv, **kw)
+                o = attn_ops.attention_qkv(qkv, pre=pre, **kw)
         return self.o(o.reshape(B, S, H * D))
 
 

@@ -23,6 +23,8 @@ from __future__ import annotations
 
 import math
 
+import os
+
 import torch
 
 from .. import _ext
@@ -114,10 +116,16 @@ class _AttnFn(torch.autograd.Function):
     gradient buffer through strided views instead of three zero-padded slice gradients."""
 
     @staticmethod
-    def forward(ctx, mode, a, b, c, lut, kpm, scale, causal, p, seed):
+    def forward(ctx, mode, a, b, c, lut, kpm, scale, causal, p, seed, pre=None):
         C = _ext.native()
         q, k, v = _split(mode, a, b, c)
-        o, lse, dmask = C.attn_fwd(q, k, v, kpm, lut, float(scale), bool(causal), float(p), int(seed))
+        dmask_in = None
+        if pre is not None:  # keep-bit planes generated ahead on the side stream (prefetch_dropout_mask)
+            dmask_in, ev = pre
+            cur = torch.cuda.current_stream(q.device)
+            cur.wait_event(ev)
+            dmask_in.record_stream(cur)
+        o, lse, dmask = C.attn_fwd(q, k, v, kpm, lut, float(scale), bool(causal), float(p), int(seed), dmask_in)
         ctx.save_for_backward(a, b, c, o, lse, lut, kpm, dmask)
         ctx.cfg = (mode, scale, causal, p, seed, lut is not None and lut.requires_grad)
         # ops/linear.py stacked_linear: the packed kv is a slice of a multi-layer projection and its
@@ -147,7 +155,7 @@ class _AttnFn(torch.autograd.Function):
                                       float(p), int(seed), bool(need_dlut), dq, dk, dv, dmask)
         if mode == "sep":
             da, db, dc = rq, rk, rv
-        return None, da, db, dc, (dlut if need_dlut else None), None, None, None, None, None
+        return None, da, db, dc, (dlut if need_dlut else None), None, None, None, None, None, None
 
 
 def _prep_kpm(kpm):
@@ -165,12 +173,33 @@ def attention(q, k, v, *, scale: float = 1.0, causal: bool = False, key_padding_
     return _reference(q, k, v, scale, causal, key_padding_mask, bias_lut, dropout_p, seed)
 
 
-def attention_qkv(qkv, **kw):
+def attention_qkv(qkv, pre=None, **kw):
     """Self-attention on the fused projection output ``qkv`` = [B, S, 3, H, D]."""
     if _ext.use_native(qkv):
         return _AttnFn.apply("qkv", qkv, None, None, kw.get("bias_lut"), _prep_kpm(kw.get("key_padding_mask")),
-                             kw.get("scale", 1.0), kw.get("causal", False), kw.get("dropout_p", 0.0), kw.get("seed", 0))
+                             kw.get("scale", 1.0), kw.get("causal", False), kw.get("dropout_p", 0.0), kw.get("seed", 0),
+                             pre)
     return attention(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], **kw)
+
+
+_SIDE: dict = {}
+
+
+def prefetch_dropout_mask(like: torch.Tensor, B: int, H: int, Sq: int, Sk: int, p: float, seed: int):
+    """``DLLM_ATTN_MASK_STREAM=1``: generate the attention-dropout keep bits for an upcoming call on a side HIP
+    stream, so the VALU-only mask kernel overlaps the (MFMA-bound) projection GEMM issued meanwhile on the
+    compute stream.  Returns a handle for ``attention_qkv(pre=...)`` or None (mask hashed inside the forward)."""
+    if p <= 0.0 or os.environ.get("DLLM_ATTN_MASK_STREAM", "0") != "1" or not _ext.use_native(like):
+        return None
+    dev = like.device
+    side = _SIDE.get(dev)
+    if side is None:
+        side = _SIDE[dev] = torch.cuda.Stream(dev)
+    with torch.cuda.stream(side):
+        m = _ext.native().attn_dropout_mask(B, H, Sq, Sk, float(p), int(seed), like)
+        ev = torch.cuda.Event()
+        ev.record(side)
+    return m, ev
 
 
 def attention_q_kv(q, kv, **kw):

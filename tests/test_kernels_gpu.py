@@ -293,3 +293,22 @@ def test_colsum_acc_bias_grad(T, N, dt):
     _ext.native().colsum_acc(x, out)
     ref = out0.float() + x.float().sum(0)
     _close(out, ref, rtol=1e-2, atol=1e-2 * (T ** 0.5) / 10 + 1e-2, msg="colsum")
+
+
+def test_attention_prefetched_dropout_planes_match(monkeypatch):
+    """Keep bits generated ahead on the side stream == bits hashed inside the forward (same seed)."""
+    B, S, H, D, p, seed = 2, 200, 3, 64, 0.1, 99
+    torch.manual_seed(0)
+    qkv = torch.randn(B, S, 3, H, D, device=DEV).to(torch.bfloat16)
+    g = torch.randn(B, S, H, D, device=DEV).to(torch.bfloat16)
+    outs = []
+    for use_pre in (False, True):
+        monkeypatch.setenv("DLLM_ATTN_MASK_STREAM", "1" if use_pre else "0")
+        x = qkv.clone().requires_grad_(True)
+        pre = A.prefetch_dropout_mask(x, B, H, S, S, p, seed)
+        assert (pre is not None) == use_pre
+        o = A.attention_qkv(x, pre=pre, scale=0.125, dropout_p=p, seed=seed)
+        o.backward(g)
+        outs.append((o.detach(), x.grad))
+    torch.testing.assert_close(outs[0][0], outs[1][0], rtol=0, atol=0)
+    torch.testing.assert_close(outs[0][1], outs[1][1], rtol=0, atol=0)
