@@ -29,6 +29,7 @@ int dllm_attn_bwd(AttnParams*, hipStream_t);
 int dllm_attn_params_size();
 int dllm_attn_dropout_mask(AttnParams*, hipStream_t);
 int dllm_gemm_wgrad(const GemmWgradParams*, int, hipStream_t);
+int dllm_gemm_fused(const GemmFusedParams*, int, int, hipStream_t);
 int dllm_colsum_rows();
 int dllm_colsum_acc(const void*, long, long, int, float*, void*, int, hipStream_t);
 }
@@ -445,6 +446,93 @@ int64_t gemm_wgrad(const Tensor& a, const Tensor& b, Tensor& c, bool beta, int64
   return splits;
 }
 
+// c[M][N] = epi(a[M][K] . b) with b = [N][K] (nn.Linear weight, b_kmajor = false) or [K][N] (b_kmajor = true).
+// epi (csrc/gemm_fused.hip): 0 none, 1 relu, 2 gelu-erf, 3 d-relu, 4 d-gelu-erf, 5 gelu-tanh, 6 d-gelu-tanh.
+// Forward activations apply dropout(p, seed) on the output element index m * N + n (ops/rng.py); the GELU
+// forwards also write the pre-activation to aux_out; the backward epilogues read aux (saved activation for
+// d-relu, pre-activation for d-gelu) and apply the matching dropout backward.
+int64_t gemm_fused_variant(int64_t K) {
+  // 16x16x32 MFMA, BK = 64, 2 stages: fastest of the four on every T5 / BART FFN shape measured
+  // (profiles/r1_gemm_fused_bench.jsonl: 8-25 % over the 32x32x16 variants, 5-24 % over hipBLASLt + act kernel)
+  return K % 64 == 0 ? 3 : 1;
+}
+
+bool gemm_fused_supported(const Tensor& a, const Tensor& b, bool b_kmajor) {
+  auto ok2 = [](const Tensor& t) {
+    return t.is_cuda() && t.dim() == 2 && t.scalar_type() == at::kBFloat16 && t.stride(1) == 1 && t.stride(0) % 8 == 0 &&
+           reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0;
+  };
+  if (!ok2(a) || !ok2(b)) return false;
+  const int64_t M = a.size(0), K = a.size(1);
+  const int64_t N = b_kmajor ? b.size(1) : b.size(0);
+  const int64_t Kb = b_kmajor ? b.size(0) : b.size(1);
+  return Kb == K && M % 256 == 0 && N % 256 == 0 && K % 64 == 0 && K > 0 && M > 0 && M * N < (1LL << 32) &&
+         K < (1LL << 31);
+}
+
+Tensor gemm_fused(const Tensor& a, const Tensor& b, bool b_kmajor, int64_t epi, const optional<Tensor>& bias,
+                  const optional<Tensor>& aux, const optional<Tensor>& aux_out, double p, int64_t seed,
+                  int64_t variant) {
+  TORCH_CHECK(gemm_fused_supported(a, b, b_kmajor),
+              "gemm_fused: need bf16 GPU a [M,K], b [N,K] (or [K,N] k-major), unit inner stride, 16-B aligned rows, "
+              "M and N multiples of 256, K % 64 == 0, M*N < 2^32");
+  TORCH_CHECK(a.device() == b.device(), "gemm_fused: device mismatch");
+  TORCH_CHECK(epi >= 0 && epi <= 6, "gemm_fused: bad epilogue ", epi);
+  TORCH_CHECK(p >= 0.0 && p < 1.0, "gemm_fused: dropout p must be in [0, 1)");
+  const int64_t M = a.size(0), K = a.size(1), N = b_kmajor ? b.size(1) : b.size(0);
+  auto out = at::empty({M, N}, a.options());
+  GemmFusedParams P{};
+  P.A = reinterpret_cast<const uint16_t*>(a.data_ptr());
+  P.B = reinterpret_cast<const uint16_t*>(b.data_ptr());
+  P.C = reinterpret_cast<uint16_t*>(out.data_ptr());
+  P.lda = a.stride(0);
+  P.ldb = b.stride(0);
+  P.ldc = out.stride(0);
+  P.M = (int)M;
+  P.N = (int)N;
+  P.K = (int)K;
+  P.tm = (int)(M / 256);
+  P.tn = (int)(N / 256);
+  P.epi = (int)epi;
+  if (bias.has_value() && bias->defined()) {
+    TORCH_CHECK(bias->is_cuda() && bias->scalar_type() == at::kBFloat16 && bias->is_contiguous() && bias->numel() == N &&
+                    reinterpret_cast<uintptr_t>(bias->data_ptr()) % 8 == 0,
+                "gemm_fused: bias must be a contiguous 8-B aligned bf16 [N] GPU tensor");
+    TORCH_CHECK(epi <= 2 || epi == 5, "gemm_fused: bias only on forward epilogues");
+    P.bias = reinterpret_cast<const uint16_t*>(bias->data_ptr());
+  }
+  const bool needs_aux = epi == 3 || epi == 4 || epi == 6;
+  const bool needs_aux_out = epi == 2 || epi == 5;
+  auto check_mn = [&](const Tensor& t, const char* n) {
+    TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.dim() == 2 && t.size(0) == M && t.size(1) == N &&
+                    t.stride(1) == 1 && t.stride(0) % 4 == 0 && reinterpret_cast<uintptr_t>(t.data_ptr()) % 8 == 0,
+                "gemm_fused: ", n, " must be a bf16 [M, N] GPU tensor with unit inner stride, 8-B aligned rows");
+  };
+  if (needs_aux) {
+    TORCH_CHECK(aux.has_value() && aux->defined(), "gemm_fused: epilogue ", epi, " needs aux");
+    check_mn(*aux, "aux");
+    P.aux = reinterpret_cast<const uint16_t*>(aux->data_ptr());
+    P.ldaux = aux->stride(0);
+  }
+  if (needs_aux_out) {
+    TORCH_CHECK(aux_out.has_value() && aux_out->defined(), "gemm_fused: epilogue ", epi, " needs aux_out");
+    check_mn(*aux_out, "aux_out");
+    P.aux_out = reinterpret_cast<uint16_t*>(aux_out->data_ptr());
+    P.ldaux = aux_out->stride(0);
+  }
+  P.p = (float)p;
+  P.scale = p > 0.0 ? (float)(1.0 / (1.0 - p)) : 1.f;
+  P.seed = (uint32_t)seed;
+  {  // 16-bit keep threshold, identical to common.h drop_threshold
+    const double t = p * 65536.0;
+    P.thr = t >= 65535.0 ? 0xFFFFu : (uint32_t)t;
+  }
+  const int v = variant >= 0 ? (int)variant : (int)gemm_fused_variant(K);
+  TORCH_CHECK(v >= 0 && v <= 3, "gemm_fused: bad variant ", v);
+  check_rc(dllm_gemm_fused(&P, b_kmajor ? 1 : 0, v, stream()), "gemm_fused");
+  return out;
+}
+
 // out (+)= column sums of x ([T, N] bf16, unit inner stride): bias gradients accumulated in place
 void colsum_acc(const Tensor& x, Tensor& out) {
   check_gpu(x, "x");
@@ -492,6 +580,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_wgrad", &gemm_wgrad, "c (+)= a^T b (token-major bf16 operands)", py::arg("a"), py::arg("b"), py::arg("c"),
         py::arg("beta") = true, py::arg("variant") = 0, py::arg("splits") = 0);
   m.def("gemm_wgrad_supported", &gemm_wgrad_supported);
+  m.def("gemm_fused", &gemm_fused, "epi(a . b) with a fused bias / activation / dropout (or their backward) epilogue",
+        py::arg("a"), py::arg("b"), py::arg("b_kmajor"), py::arg("epi"), py::arg("bias") = py::none(),
+        py::arg("aux") = py::none(), py::arg("aux_out") = py::none(), py::arg("p") = 0.0, py::arg("seed") = 0,
+        py::arg("variant") = -1);
+  m.def("gemm_fused_supported", &gemm_fused_supported);
   m.def("colsum_acc", &colsum_acc, "out += x.sum(0) for a token-major bf16 x (bias gradients)");
   dllm::bind_reducer(m);
   m.attr("arch") = "gfx950";

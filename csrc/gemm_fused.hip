@@ -1,0 +1,365 @@
+// Projection GEMMs with fused epilogues for gfx950 (MI355X / CDNA4):
+//
+//   NT (forward):  C[M][N] = epi( A[M][K] · B[N][K]^T )   A = activations [tokens][in], B = nn.Linear weight [out][in]
+//   NN (dgrad):    C[M][N] = epi( A[M][K] · B[K][N] )     A = output grad [tokens][out], B = weight [out][in]
+//
+// Why a hand-written kernel when hipBLASLt runs these shapes well: the epilogue.  The T5 / BART FFN is
+// `wo(dropout(act(wi x)))`; through the library every FFN costs two extra full passes over the
+// [tokens, d_ff] activation (activation+dropout forward, activation+dropout backward, ~0.8-1.2 GB of HBM
+// traffic each at t5-base b=64) and keeps BOTH the pre-activation and the activation alive for backward.
+// Here the wi GEMM applies bias + activation + dropout before its store (the keep decision is the shared
+// counter hash of ops/rng.py on the output element index), and the wo dgrad GEMM applies the activation /
+// dropout backward to its accumulators before its store: for ReLU the mask is `H != 0` read back from the
+// saved activation itself (ReLU and dropout both produce exact zeros), so the pre-activation is never
+// stored at all.  GELU keeps its pre-activation (written by the forward epilogue as a second output).
+//
+// Structure (same machinery as csrc/gemm.hip, the weight-gradient kernel):
+// * 256x256 output tile per 512-thread workgroup, 8 waves as 2(M) x 4(N), 128x64 per wave = 4x2
+//   v_mfma_f32_32x32x16_bf16 accumulators; operands staged global -> LDS by LDS-DMA
+//   (global_load_lds_dwordx4, lane-linear, pre-swizzled source addresses), NBUF-deep ring, one barrier
+//   per k-stage, counted vmcnt keeps the next stages in flight;
+// * K-contiguous operands live in [256][BK] images (BK*2-byte rows); 16-B chunk c of row r sits at
+//   chunk c ^ ((r / RPB) & (CPR-1)) (RPB = rows per 256-B bank row): the 16 rows one ds_read_b128 phase
+//   touches land on 16 distinct bank slots.  N-contiguous B (dgrad) uses the k-major [BK][256] image with
+//   hardware-transposed reads (ds_read_b64_tr_b16) exactly as the wgrad kernel;
+// * the MFMA operand roles are swapped (C^T = B A^T per 32x32 sub-tile) so a lane's accumulators are 4
+//   CONSECUTIVE output columns of one row: the epilogue does its math on f32x4 and stores 8 B per lane,
+//   and dropout pairs (2 decisions per hash) fall inside one lane;
+// * bijective XCD remap of the 1-D grid, tiles of one 256-row block of A consecutive (L2 reuse of A).
+#include "common.h"
+
+using namespace dllm;
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8v;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+
+#include "gemm_params.h"
+
+namespace {
+
+constexpr int BM = 256, BN = 256, NT = 512;
+
+enum Epi { EPI_NONE = 0, EPI_RELU = 1, EPI_GELU = 2, EPI_DRELU = 3, EPI_DGELU = 4, EPI_GELU_TANH = 5,
+           EPI_DGELU_TANH = 6 };
+
+DLLM_DEVICE int xcd_remap(int bid, int nblk) {
+  const int q = nblk / 8, r = nblk % 8, x = bid % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+}
+
+// ---- k-major [BK][256] image (512-B rows), transposed reads (as csrc/gemm.hip).  Bit 3 of the k-row also enters
+// the swizzle: the two 16-lane groups of one 16x16x32 fragment read (k-rows kk..kk+3 and kk+8..kk+11 of the same 16
+// columns, one ds_read_b64_tr_b16) then land on distinct banks; the 32x32x16 reads stay conflict-free.
+DLLM_DEVICE int gsw(int r) { return ((r & 3) << 2) ^ (((r >> 3) & 1) << 1); }
+DLLM_DEVICE int loff_km(int r, int col) { return (r << 8) + (((col >> 3) ^ gsw(r)) << 3) + (col & 7); }
+
+DLLM_DEVICE u16x4 ld_tr(const uint16_t* T, int r0, int c0, int i) {
+  const int r = r0 + (i >> 2);
+  const int col = c0 + 4 * (i & 3);
+  s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(T + loff_km(r, col)));
+  return __builtin_bit_cast(u16x4, v);
+}
+
+DLLM_DEVICE bf16x8v frag_km(const uint16_t* T, int kk, int cb, int lane) {
+  const int g = lane >> 4;
+  const int r0 = kk + 8 * (g >> 1);
+  const int c0 = cb + 16 * (g & 1);
+  const u16x4 lo = ld_tr(T, r0, c0, lane & 15);
+  const u16x4 hi = ld_tr(T, r0 + 4, c0, lane & 15);
+  const u16x8 v = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+  return __builtin_bit_cast(bf16x8v, v);
+}
+
+// 16x16x32 operand from the k-major image: lane l holds column cb + (l & 15), k = kk + 8 (l >> 4) + 0..7
+DLLM_DEVICE bf16x8v frag_km16(const uint16_t* T, int kk, int cb, int lane) {
+  const int r0 = kk + 8 * (lane >> 4);
+  const u16x4 lo = ld_tr(T, r0, cb, lane & 15);
+  const u16x4 hi = ld_tr(T, r0 + 4, cb, lane & 15);
+  const u16x8 v = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+  return __builtin_bit_cast(bf16x8v, v);
+}
+
+// ---- row-major [256][BK] image (k contiguous)
+template <int BK>
+struct RowImg {
+  static constexpr int CPR = BK / 8;          // 16-B chunks per row
+  static constexpr int RPB = 256 / (BK * 2);  // rows per 256-B bank row
+  static constexpr int RPI = 1024 / (BK * 2); // rows per 1-KB DMA wave-instruction
+  static DLLM_DEVICE int swz(int r) { return (r / RPB) & (CPR - 1); }
+  // 32x32x16 operand: lane l holds row cb + (l & 31), k = kk + 8 (l >> 5) + 0..7
+  static DLLM_DEVICE bf16x8v frag(const uint16_t* T, int kk, int cb, int lane) {
+    const int r = cb + (lane & 31);
+    const int c = (kk >> 3) + (lane >> 5);
+    const u16x8 v = *reinterpret_cast<const u16x8*>(T + r * BK + ((c ^ swz(r)) << 3));
+    return __builtin_bit_cast(bf16x8v, v);
+  }
+  // 16x16x32 operand: lane l holds row cb + (l & 15), k = kk + 8 (l >> 4) + 0..7 (conflict-free at BK = 64)
+  static DLLM_DEVICE bf16x8v frag16(const uint16_t* T, int kk, int cb, int lane) {
+    const int r = cb + (lane & 15);
+    const int c = (kk >> 3) + (lane >> 4);
+    const u16x8 v = *reinterpret_cast<const u16x8*>(T + r * BK + ((c ^ swz(r)) << 3));
+    return __builtin_bit_cast(bf16x8v, v);
+  }
+};
+
+constexpr float kInvSqrt2 = 0.7071067811865476f;
+constexpr float kInvSqrt2Pi = 0.3989422804014327f;
+constexpr float kSqrt2OverPi = 0.7978845608028654f;
+
+DLLM_DEVICE float gelu_f(float x) { return 0.5f * x * (1.f + erff(x * kInvSqrt2)); }
+DLLM_DEVICE float gelu_df(float x) {
+  return 0.5f * (1.f + erff(x * kInvSqrt2)) + x * kInvSqrt2Pi * __expf(-0.5f * x * x);
+}
+DLLM_DEVICE float gelu_tanh_f(float x) {
+  return 0.5f * x * (1.f + tanhf(kSqrt2OverPi * (x + 0.044715f * x * x * x)));
+}
+DLLM_DEVICE float gelu_tanh_df(float x) {
+  const float t = tanhf(kSqrt2OverPi * (x + 0.044715f * x * x * x));
+  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * kSqrt2OverPi * (1.f + 3.f * 0.044715f * x * x);
+}
+
+DLLM_DEVICE void store4(uint16_t* p, f32x4 v) {
+  const u16x4 o = {f2bf(v.x), f2bf(v.y), f2bf(v.z), f2bf(v.w)};
+  *reinterpret_cast<u16x4*>(p) = o;
+}
+
+DLLM_DEVICE f32x4 load4(const uint16_t* p) {
+  const u16x4 r = *reinterpret_cast<const u16x4*>(p);
+  return f32x4{bf2f(r.x), bf2f(r.y), bf2f(r.z), bf2f(r.w)};
+}
+
+// v = accumulators for C[m][n .. n+3] (n % 4 == 0)
+template <int EPI>
+DLLM_DEVICE void epilogue4(const GemmFusedParams& P, int m, int n, f32x4 v) {
+  if (P.bias) v += load4(P.bias + n);
+  const bool drop = P.p > 0.f;
+  const uint32_t e = (uint32_t)m * (uint32_t)P.N + (uint32_t)n;  // output element index (< 2^32, host-checked)
+  if (EPI == EPI_RELU || EPI == EPI_GELU || EPI == EPI_GELU_TANH) {
+    if (EPI != EPI_RELU) store4(P.aux_out + (long)m * P.ldaux + n, v);  // pre-activation for the backward
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      v[k] = EPI == EPI_RELU ? fmaxf(v[k], 0.f) : (EPI == EPI_GELU ? gelu_f(v[k]) : gelu_tanh_f(v[k]));
+    if (drop) dropout4(v, P.seed, P.thr, e, P.scale);
+  } else if (EPI == EPI_DRELU) {
+    // H = dropout(relu(u)) was stored by the forward: dH/du = (H != 0) * scale
+    const u16x4 h = *reinterpret_cast<const u16x4*>(P.aux + (long)m * P.ldaux + n);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = (h[k] & 0x7fff) ? v[k] * P.scale : 0.f;
+  } else if (EPI == EPI_DGELU || EPI == EPI_DGELU_TANH) {
+    if (drop) dropout4(v, P.seed, P.thr, e, P.scale);
+    const f32x4 u = load4(P.aux + (long)m * P.ldaux + n);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] *= EPI == EPI_DGELU ? gelu_df(u[k]) : gelu_tanh_df(u[k]);
+  }
+  store4(P.C + (long)m * P.ldc + n, v);
+}
+
+// MF = 32: v_mfma_f32_32x32x16_bf16, 4x2 accumulator tiles of 32x32 per wave;
+// MF = 16: v_mfma_f32_16x16x32_bf16, 8x4 tiles of 16x16 (same cycles per FLOP; on random data the chip holds a
+// higher clock on this shape, MI355X_MICROARCH.md "DVFS give-back" item 7) — both built, the faster picked by
+// measurement (tools/gemm_fused_bench.py).
+template <int BK, int NBUF, bool BKM, int EPI, int MF>
+__global__ __launch_bounds__(NT, 1) void gemm_fused_kernel(GemmFusedParams P) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint16_t* lds = reinterpret_cast<uint16_t*>(smem);  // [NBUF][A image | B image], BK*256 elements each
+  using RI = RowImg<BK>;
+  constexpr int TILE = BK * 256;
+  constexpr int PW = BK / 16;  // 1-KB DMA instructions per wave per operand per stage
+  constexpr int LPS = 2 * PW;
+  static_assert(NBUF >= 2 && NBUF <= 4, "ring depth");
+
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, hh = lane >> 5;
+  const int wm = w >> 2, wn = w & 3;
+  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (t / P.tn) * BM, n0 = (t % P.tn) * BN;
+  const int nk = P.K / BK;
+
+  // DMA sources.  Row image: instruction q covers rows q*RPI .. +RPI, lane -> (row l / CPR, pos l % CPR).
+  const uint16_t* Ag = P.A + (long)m0 * P.lda;
+  const uint16_t* Bg = BKM ? P.B + n0 : P.B + (long)n0 * P.ldb;
+  long aoff[PW], boff[PW];
+#pragma unroll
+  for (int i = 0; i < PW; ++i) {
+    const int q = w * PW + i;
+    const int r = q * RI::RPI + lane / RI::CPR;
+    const int c = (lane % RI::CPR) ^ RI::swz(r);
+    aoff[i] = (long)r * P.lda + c * 8;
+    if (BKM) {  // k-major image: instruction q covers k-rows 2q, 2q+1; lane -> (row 2q + l/32, chunk l%32)
+      const int kr = 2 * q + hh;
+      boff[i] = (long)kr * P.ldb + (((lane & 31) ^ gsw(kr)) << 3);
+    } else {
+      boff[i] = (long)r * P.ldb + c * 8;
+    }
+  }
+  const uint32_t lds0 = lds_addr(lds);
+  auto issue = [&](int buf, int kt) {
+    const long k0 = (long)kt * BK;
+    const uint32_t Al = lds0 + (uint32_t)(buf * 2 * TILE) * 2u;
+    const uint32_t Bl = Al + TILE * 2u;
+    const uint16_t* Bk = BKM ? Bg + k0 * P.ldb : Bg + k0;
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+      const uint32_t q = __builtin_amdgcn_readfirstlane(w * PW + i);
+      glds16(Ag + k0 + aoff[i], __builtin_amdgcn_readfirstlane(Al + q * 1024u));
+      glds16(Bk + boff[i], __builtin_amdgcn_readfirstlane(Bl + q * 1024u));
+    }
+  };
+
+#pragma unroll
+  for (int p = 0; p < NBUF - 1; ++p)
+    if (p < nk) issue(p, p);
+
+  // stage `it` must have landed (stages it+1 .. it+NBUF-2 may stay in flight); every wave is done reading the
+  // buffer about to be refilled; then the refill of that buffer is issued
+  auto stage_sync = [&](int it) {
+    const int ahead = min(NBUF - 2, nk - 1 - it);
+    if (NBUF >= 4 && ahead >= 2) wait_vm<(NBUF >= 4 ? 2 * LPS : 0)>();
+    else if (NBUF >= 3 && ahead >= 1) wait_vm<(NBUF >= 3 ? LPS : 0)>();
+    else wait_vm<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (it + NBUF - 1 < nk) issue((it + NBUF - 1) % NBUF, it + NBUF - 1);
+  };
+
+  if constexpr (MF == 32) {
+    f32x16 acc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    auto bfrag = [&](const uint16_t* Bs, int kk, int j) {
+      const int cb = wn * 64 + 32 * j;
+      return BKM ? frag_km(Bs, kk, cb, lane) : RI::frag(Bs, kk, cb, lane);
+    };
+
+    for (int it = 0; it < nk; ++it) {
+      stage_sync(it);
+      const uint16_t* As = lds + (it % NBUF) * 2 * TILE;
+      const uint16_t* Bs = As + TILE;
+      bf16x8v a[2][4], b[2][2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[0][i] = RI::frag(As, 0, wm * 128 + 32 * i, lane);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) b[0][j] = bfrag(Bs, 0, j);
+#pragma unroll
+      for (int ks = 0; ks < BK / 16; ++ks) {
+        const int cur = ks & 1;
+        if (ks + 1 < BK / 16) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) a[cur ^ 1][i] = RI::frag(As, 16 * (ks + 1), wm * 128 + 32 * i, lane);
+#pragma unroll
+          for (int j = 0; j < 2; ++j) b[cur ^ 1][j] = bfrag(Bs, 16 * (ks + 1), j);
+        }
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)  // swapped roles: D = B_sub A_sub^T -> lane holds row m, 4 consecutive n
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[cur][j], a[cur][i], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+      }
+    }
+
+    // epilogue: acc[i][j][4g + 0..3] = C[m0 + wm*128 + 32i + (lane & 31)][n0 + wn*64 + 32j + 8g + 4hh + 0..3]
+    const int mrow = m0 + wm * 128 + (lane & 31);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 v = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
+          epilogue4<EPI>(P, mrow + 32 * i, n0 + wn * 64 + 32 * j + 8 * g + 4 * hh, v);
+        }
+  } else {
+    static_assert(MF == 16 && BK == 64, "16x16x32 fragments are bank-conflict free on the BK = 64 images only");
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    for (int it = 0; it < nk; ++it) {
+      stage_sync(it);
+      const uint16_t* As = lds + (it % NBUF) * 2 * TILE;
+      const uint16_t* Bs = As + TILE;
+#pragma unroll
+      for (int ks = 0; ks < BK / 32; ++ks) {
+        bf16x8v a[8], b[4];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) a[i] = RI::frag16(As, 32 * ks, wm * 128 + 16 * i, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          b[j] = BKM ? frag_km16(Bs, 32 * ks, wn * 64 + 16 * j, lane) : RI::frag16(Bs, 32 * ks, wn * 64 + 16 * j, lane);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)  // swapped roles: lane holds row m = lane & 15, 4 consecutive n
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+      }
+    }
+
+    // epilogue: acc[i][j][0..3] = C[m0 + wm*128 + 16i + (lane & 15)][n0 + wn*64 + 16j + 4 (lane >> 4) + 0..3]
+    const int mrow = m0 + wm * 128 + (lane & 15);
+    const int ncol = n0 + wn * 64 + 4 * (lane >> 4);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) epilogue4<EPI>(P, mrow + 16 * i, ncol + 16 * j, acc[i][j]);
+  }
+}
+
+template <int BK, int NBUF, bool BKM, int EPI, int MF>
+int launch(const GemmFusedParams& p, hipStream_t st) {
+  const size_t lds = (size_t)NBUF * 2 * BK * 256 * 2;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm_fused_kernel<BK, NBUF, BKM, EPI, MF>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = true;
+  }
+  hipLaunchKernelGGL((gemm_fused_kernel<BK, NBUF, BKM, EPI, MF>), dim3(p.tm * p.tn), dim3(NT), lds, st, p);
+  DLLM_CHECK_LAUNCH();
+  return 0;
+}
+
+template <bool BKM, int EPI>
+int launch_v(const GemmFusedParams& p, int variant, hipStream_t st) {
+  switch (variant) {
+    case 1: return launch<32, 4, BKM, EPI, 32>(p, st);
+    case 2: return launch<32, 3, BKM, EPI, 32>(p, st);
+    case 3: return launch<64, 2, BKM, EPI, 16>(p, st);
+    default: return launch<64, 2, BKM, EPI, 32>(p, st);
+  }
+}
+
+template <bool BKM>
+int dispatch_epi(const GemmFusedParams& p, int variant, hipStream_t st) {
+  switch (p.epi) {
+    case EPI_NONE: return launch_v<BKM, EPI_NONE>(p, variant, st);
+    case EPI_RELU: return launch_v<BKM, EPI_RELU>(p, variant, st);
+    case EPI_GELU: return launch_v<BKM, EPI_GELU>(p, variant, st);
+    case EPI_GELU_TANH: return launch_v<BKM, EPI_GELU_TANH>(p, variant, st);
+    case EPI_DRELU: return launch_v<BKM, EPI_DRELU>(p, variant, st);
+    case EPI_DGELU: return launch_v<BKM, EPI_DGELU>(p, variant, st);
+    case EPI_DGELU_TANH: return launch_v<BKM, EPI_DGELU_TANH>(p, variant, st);
+    default: return -5;
+  }
+}
+
+}  // namespace
+
+// variant: 0 = BK64 x 2 stages, 1 = BK32 x 4 stages, 2 = BK32 x 3 stages (all 128 / 96 KB LDS, 32x32x16 MFMA),
+// 3 = BK64 x 2 stages with 16x16x32 MFMA
+extern "C" int dllm_gemm_fused(const GemmFusedParams* pp, int b_kmajor, int variant, hipStream_t st) {
+  const GemmFusedParams& p = *pp;
+  const int bk = (variant == 0 || variant == 3) ? 64 : 32;
+  if (p.M % BM || p.N % BN || p.K <= 0 || p.K % bk || p.tm * BM != p.M || p.tn * BN != p.N) return -4;
+  return b_kmajor ? dispatch_epi<true>(p, variant, st) : dispatch_epi<false>(p, variant, st);
+}

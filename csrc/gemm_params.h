@@ -15,3 +15,20 @@ struct GemmWgradParams {
   int splits;
   int beta;  // 1: C += A^T B, 0: C = A^T B
 };
+
+// csrc/gemm_fused.hip: C[M][N] = epi(A[M][K] . B), B = [N][K] (b_kmajor = 0) or [K][N] (b_kmajor = 1)
+struct GemmFusedParams {
+  const uint16_t* A;
+  const uint16_t* B;
+  uint16_t* C;
+  const uint16_t* bias;  // [N] or null (added before the activation)
+  const uint16_t* aux;   // backward epilogues: saved activation (ReLU) / pre-activation (GELU), [M][ldaux]
+  uint16_t* aux_out;     // GELU forward: pre-activation output, [M][ldaux]
+  long lda, ldb, ldc, ldaux;
+  int M, N, K;
+  int tm, tn;  // M / 256, N / 256
+  int epi;     // 0 none, 1 relu, 2 gelu(erf), 3 d-relu, 4 d-gelu(erf), 5 gelu(tanh), 6 d-gelu(tanh)
+  float p;     // dropout probability on the activation output (forward element index m * N + n)
+  float scale; // 1 / (1 - p), or 1
+  uint32_t seed, thr;
+};

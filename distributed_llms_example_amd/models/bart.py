@@ -17,6 +17,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops import activations, attention as attn_ops, norms
+from ..ops.ffn import ffn
 from ..ops.cross_entropy import cross_entropy
 from ..ops.linear import Linear, stacked_linear
 from ..ops.rng import default_rng
@@ -93,8 +94,7 @@ class BartLayer(nn.Module):
             h = norms.add_dropout_layer_norm(h, c, self.encoder_attn_layer_norm.weight,
                                              self.encoder_attn_layer_norm.bias, eps, p,
                                              rng.next_seed() if p > 0 else 0)
-        f = activations.act_dropout(self.fc1(h), cfg.act, pact, rng.next_seed() if pact > 0 else 0)
-        f = self.fc2(f)
+        f = ffn(h, self.fc1, self.fc2, cfg.act, pact, rng.next_seed() if pact > 0 else 0)
         return norms.add_dropout_layer_norm(h, f, self.final_layer_norm.weight, self.final_layer_norm.bias, eps, p,
                                             rng.next_seed() if p > 0 else 0)
 

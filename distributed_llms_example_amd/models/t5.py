@@ -20,6 +20,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops import activations, attention as attn_ops, norms
+from ..ops.ffn import ffn
 from ..ops.cross_entropy import cross_entropy
 from ..ops.linear import Linear, stacked_linear
 from ..ops.rng import default_rng
@@ -92,9 +93,10 @@ class T5DenseActDense(nn.Module):
         self.gated = cfg.is_gated
 
     def forward(self, x, p):
-        h = self.wi(x)
         seed = default_rng().next_seed() if p > 0 else 0
-        h = activations.act_dropout(h, self.act, p, seed, gated=self.gated)
+        if not self.gated:  # activation + dropout in the GEMM epilogues where possible (ops/ffn.py)
+            return ffn(x, self.wi, self.wo, self.act, p, seed)
+        h = activations.act_dropout(self.wi(x), self.act, p, seed, gated=True)
         return self.wo(h)
 
 

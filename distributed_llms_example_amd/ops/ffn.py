@@ -1,0 +1,117 @@
+"""Feed-forward block ``lin_out(dropout(act(lin_in(x))))`` with the activation and dropout inside GEMM epilogues.
+
+Reference semantics: T5 ``T5DenseActDense`` (transformers modeling_t5.py:83-94: wi -> relu -> dropout -> wo)
+and BART's ``fc1 -> activation_fn -> dropout(activation_dropout) -> fc2`` (modeling_bart.py:297-301).
+
+Through the library path (hipBLASLt + csrc/act.hip) every FFN makes two extra full passes over the
+``[tokens, d_ff]`` activation — the activation+dropout kernel forward and its backward — and keeps both
+the pre-activation (for the activation backward) and the activation (for the ``lin_out`` weight gradient)
+alive until backward.  Here (csrc/gemm_fused.hip):
+
+* forward:  ``H = dropout(act(X Wiᵀ + bi))`` is ONE GEMM whose epilogue applies bias, activation and the
+  counter-based dropout mask (ops/rng.py, same element index as csrc/act.hip, so both paths draw identical
+  masks); GELU also writes its pre-activation ``U`` as a second output; ReLU stores nothing else;
+* backward: ``dU = act'(U) · dropout'(dY Wo)`` is ONE GEMM (``dY [M, d] x Wo [d, F]``, k-major B) whose
+  epilogue applies the dropout and activation backward.  For ReLU the derivative mask is ``H != 0``
+  read back from the saved activation itself (ReLU and dropout both produce exact zeros), so the
+  pre-activation is never stored: one ``[tokens, d_ff]`` tensor less per layer;
+* weight gradients are accumulated straight into the flat gradient buffer (ops/gemm.py), and the
+  reducer's post hooks are fired by hand exactly as ops/linear.py does.
+
+Taken only when both linears carry FlatParams-managed gradients (``_dllm_fused_wgrad``), the input is
+bf16 on the GPU and the shapes suit the kernel (tokens and d_ff multiples of 256, d_model of 64); anything
+else (gated FLAN-T5 FFNs, CPU, odd token counts) runs the unfused modules with identical semantics.
+``DLLM_FUSED_FFN=0`` forces the unfused path (A/B runs); ``DLLM_GEMM_FUSED_VARIANT=n`` forces a kernel
+variant (csrc/gemm_fused.hip).
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.nn.functional as F
+
+from .. import _ext
+from .activations import act_dropout
+from .gemm import bias_grad_accumulate, wgrad_accumulate
+from .linear import _fire, _fusable
+
+# activation -> (forward epilogue, backward epilogue) of csrc/gemm_fused.hip
+EPILOGUES = {"relu": (1, 3), "gelu": (2, 4), "gelu_new": (5, 6), "gelu_fast": (5, 6)}
+_VARIANT = int(os.environ.get("DLLM_GEMM_FUSED_VARIANT", "-1"))  # -1: picked by K in csrc/bind.cpp
+fused_calls = 0  # number of FFN forwards that took the fused path (tests assert the kernel really ran)
+
+
+def _enabled() -> bool:
+    return os.environ.get("DLLM_FUSED_FFN", "1") != "0"
+
+
+class _FusedFFNFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, wi, bi, wo, bo, act, p, seed, params):
+        C = _ext.native()
+        shape = x.shape
+        x2 = x.reshape(-1, shape[-1])
+        efwd, _ = EPILOGUES[act]
+        u = None
+        if efwd != 1:  # GELU: the backward needs the pre-activation
+            u = torch.empty(x2.shape[0], wi.shape[0], device=x.device, dtype=x.dtype)
+        h = C.gemm_fused(x2, wi, False, efwd, bi, None, u, float(p), int(seed), _VARIANT)
+        y = F.linear(h, wo, bo)
+        ctx.save_for_backward(x2, h, u)
+        ctx.params = params
+        ctx.cfg = (act, float(p), int(seed), shape)
+        return y.view(*shape[:-1], wo.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, h, u = ctx.saved_tensors
+        Wi, Bi, Wo, Bo = ctx.params
+        act, p, seed, shape = ctx.cfg
+        C = _ext.native()
+        _, ebwd = EPILOGUES[act]
+        wo = Wo.detach()
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        if not C.gemm_fused_supported(dy2, wo, True):
+            dy2 = dy2.contiguous()
+        du = C.gemm_fused(dy2, wo, True, ebwd, None, h if ebwd == 3 else u, None, p, seed, _VARIANT)
+        with torch.no_grad():
+            wgrad_accumulate(Wo.grad, dy2, h)
+            if Bo is not None:
+                bias_grad_accumulate(Bo.grad, dy2)
+        _fire(Wo)
+        if Bo is not None:
+            _fire(Bo)
+        dx = torch.matmul(du, Wi.detach()) if ctx.needs_input_grad[0] else None
+        with torch.no_grad():
+            wgrad_accumulate(Wi.grad, du, x2)
+            if Bi is not None:
+                bias_grad_accumulate(Bi.grad, du)
+        _fire(Wi)
+        if Bi is not None:
+            _fire(Bi)
+        return (None if dx is None else dx.view(shape)), None, None, None, None, None, None, None, None
+
+
+def _fusable_shapes(x2: torch.Tensor, wi: torch.Tensor, wo: torch.Tensor) -> bool:
+    C = _ext.native()
+    M, d = x2.shape
+    Fd = wi.shape[0]
+    return (tuple(wo.shape) == (d, Fd) and M % 256 == 0 and Fd % 256 == 0 and d % 64 == 0 and M * Fd < 2**32
+            and C.gemm_fused_supported(x2, wi, False) and C.gemm_fused_supported(x2, wo, True))
+
+
+def ffn(x: torch.Tensor, lin_in, lin_out, act: str, p: float = 0.0, seed: int = 0) -> torch.Tensor:
+    """``lin_out(act_dropout(lin_in(x), act, p, seed))`` (non-gated), fused where possible."""
+    global fused_calls
+    if (act in EPILOGUES and _enabled() and x.dtype == torch.bfloat16 and _ext.use_native(x)
+            and torch.is_grad_enabled()
+            and all(_fusable(t) for t in (lin_in.weight, lin_in.bias, lin_out.weight, lin_out.bias))):
+        x2 = x.reshape(-1, x.shape[-1])
+        if _fusable_shapes(x2, lin_in.weight, lin_out.weight):
+            fused_calls += 1
+            bi, bo = lin_in.bias, lin_out.bias
+            return _FusedFFNFn.apply(x, lin_in.weight.detach(), None if bi is None else bi.detach(),
+                                     lin_out.weight.detach(), None if bo is None else bo.detach(), act, p, seed,
+                                     (lin_in.weight, bi, lin_out.weight, bo))
+    return lin_out(act_dropout(lin_in(x), act, p, seed))

@@ -312,3 +312,65 @@ def test_attention_prefetched_dropout_planes_match(monkeypatch):
         outs.append((o.detach(), x.grad))
     torch.testing.assert_close(outs[0][0], outs[1][0], rtol=0, atol=0)
     torch.testing.assert_close(outs[0][1], outs[1][1], rtol=0, atol=0)
+
+
+# ------------------------------------------------------------------------ fused-epilogue GEMM (csrc/gemm_fused.hip)
+_EPI_FWD = {None: 0, "relu": 1, "gelu": 2, "gelu_new": 5}
+_EPI_BWD = {"relu": 3, "gelu": 4, "gelu_new": 6}
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("act,p,bias", [(None, 0.0, False), ("relu", 0.1, False), ("gelu", 0.0, True),
+                                        ("gelu_new", 0.1, True)])
+def test_gemm_fused_forward(variant, act, p, bias):
+    """H = dropout(act(X Wᵀ + b)) with the epilogue in the GEMM (nn.Linear weight layout) vs fp32 torch."""
+    from distributed_llms_example_amd.ops.rng import keep_mask
+    torch.manual_seed(0)
+    M, K, N = 512, 768, 1280
+    C = _ext.native()
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) * K ** -0.5).to(torch.bfloat16)
+    b = (0.5 * torch.randn(N, device=DEV)).to(torch.bfloat16) if bias else None
+    epi = _EPI_FWD[act]
+    aux = torch.empty(M, N, device=DEV, dtype=torch.bfloat16) if epi in (2, 5) else None
+    assert C.gemm_fused_supported(x, w, False)
+    h = C.gemm_fused(x, w, False, epi, b, None, aux, p, 77, variant)
+    u = x.float() @ w.float().t() + (b.float() if bias else 0.0)
+    ref = u if act is None else activations._act_ref(u, act)
+    if p > 0:
+        ref = ref * keep_mask(77, p, ref.shape, ref.device).float() / (1.0 - p)
+    assert _rel(h, ref) < 1e-2, _rel(h, ref)
+    _close(h, ref, 2e-2, 2e-2, "fused fwd")
+    if aux is not None:
+        assert _rel(aux, u) < 1e-2
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("act,p", [("relu", 0.1), ("relu", 0.0), ("gelu", 0.1), ("gelu_new", 0.0)])
+def test_gemm_fused_backward(variant, act, p):
+    """dU = act'(U) * dropout'(dY Wo) with Wo k-major ([d, F]) vs fp32 autograd of the same composite."""
+    from distributed_llms_example_amd.ops.rng import keep_mask
+    torch.manual_seed(1)
+    M, d, F_ = 768, 512, 1024
+    C = _ext.native()
+    dy = torch.randn(M, d, device=DEV).to(torch.bfloat16)
+    wo = (torch.randn(d, F_, device=DEV) * d ** -0.5).to(torch.bfloat16)
+    u = torch.randn(M, F_, device=DEV).to(torch.bfloat16)
+    keep = (keep_mask(9, p, (M, F_), u.device).float() / (1.0 - p)) if p > 0 else torch.ones(M, F_, device=DEV)
+    h = (activations._act_ref(u.float(), act) * keep).to(torch.bfloat16)
+    aux = h if act == "relu" else u  # ReLU derives its mask from the saved activation itself
+    assert C.gemm_fused_supported(dy, wo, True)
+    du = C.gemm_fused(dy, wo, True, _EPI_BWD[act], None, aux, None, p, 9, variant)
+    uf = u.float().requires_grad_(True)
+    (activations._act_ref(uf, act) * keep).backward(dy.float() @ wo.float())
+    assert _rel(du, uf.grad) < 1e-2, _rel(du, uf.grad)
+    _close(du, uf.grad, 2e-2, 2e-2, "fused bwd")
+
+
+def test_gemm_fused_rejects_unsupported_shapes():
+    C = _ext.native()
+    x = torch.randn(300, 768, device=DEV).to(torch.bfloat16)  # tokens not a multiple of 256
+    w = torch.randn(1024, 768, device=DEV).to(torch.bfloat16)
+    assert not C.gemm_fused_supported(x, w, False)
+    with pytest.raises(RuntimeError):
+        C.gemm_fused(x, w, False, 1, None, None, None, 0.0, 0, -1)

@@ -83,3 +83,35 @@ def test_engine_steps_reduce_loss_on_gpu():
         eng.step()
     assert losses[-1] < losses[0] - 0.3, losses
     assert _ext.native() is not None
+
+
+@pytest.mark.parametrize("name", ["t5-base", "bart-base"])
+def test_fused_ffn_matches_unfused_in_engine(name, monkeypatch):
+    """TrainEngine (FlatParams: the FFN runs as GEMMs with activation/dropout epilogues, ops/ffn.py) vs the same
+    step with DLLM_FUSED_FFN=0 (hipBLASLt + activation kernels): same loss, same flat gradient."""
+    from distributed_llms_example_amd.ops import ffn as ffn_mod
+    from distributed_llms_example_amd.ops.rng import manual_seed
+    from distributed_llms_example_amd.parallel.env import init_distributed
+    from distributed_llms_example_amd.train.engine import TrainEngine
+    env = init_distributed()
+    cfg = _cfg(name)
+    torch.manual_seed(0)
+    sd = build_model(cfg).state_dict()
+    b = _batch(cfg, B=4, S=256, T=64)  # 1024 / 256 tokens: the fused kernel's shapes
+    res = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("DLLM_FUSED_FFN", flag)
+        m = build_model(cfg)
+        m.load_state_dict(sd)
+        eng = TrainEngine(m, env, lr=1e-4, dtype=torch.bfloat16)
+        eng.train()
+        before = ffn_mod.fused_calls
+        manual_seed(5)
+        loss = eng.forward_backward(b)
+        used = ffn_mod.fused_calls - before
+        res.append((float(loss), eng.flat.grad_buf.float().clone(), used))
+    (l0, g0, n0), (l1, g1, n1) = res
+    assert n0 == 0 and n1 == cfg.num_layers + cfg.num_decoder_layers, (n0, n1)
+    assert abs(l0 - l1) < 1e-2 * abs(l0), (l0, l1)
+    cos = torch.nn.functional.cosine_similarity(g0, g1, dim=0).item()
+    assert cos > 0.999, cos

@@ -16,8 +16,19 @@ def family(name):
     return "torch:" + (m.group(1) if m else name[:40])
 
 
+def _rows_from_db(path):
+    """rocprofv3 >= 7 writes a rocpd SQLite database; aggregate its ``kernels`` view like --stats does."""
+    import sqlite3
+    agg = defaultdict(lambda: [0, 0.0])
+    for name, dur in sqlite3.connect(path).execute("select name, duration from kernels"):
+        a = agg[name]
+        a[0] += 1
+        a[1] += float(dur)
+    return [{"Name": k, "Calls": n, "TotalDurationNs": t, "AverageNs": t / n} for k, (n, t) in agg.items()]
+
+
 def main(path, steps):
-    rows = list(csv.DictReader(open(path)))
+    rows = _rows_from_db(path) if path.endswith(".db") else list(csv.DictReader(open(path)))
     tot = sum(float(r["TotalDurationNs"]) for r in rows)
     fam = defaultdict(float)
     for r in rows:
