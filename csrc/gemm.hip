@@ -37,7 +37,9 @@ DLLM_DEVICE int xcd_remap(int bid, int nblk) {
 
 DLLM_DEVICE int crow(int reg, int hh) { return (reg & 3) + 8 * (reg >> 2) + 4 * hh; }
 
-DLLM_DEVICE int gsw(int r) { return (r & 3) << 2; }
+// bit 3 of the k-row also enters the swizzle so the two 16-lane groups of a 16x16x32 fragment read (k-rows
+// kk..kk+3 and kk+8..kk+11 of the same 16 columns, one ds_read_b64_tr_b16) land on distinct banks
+DLLM_DEVICE int gsw(int r) { return ((r & 3) << 2) ^ (((r >> 3) & 1) << 1); }
 
 // element offset of (row r, col) in a swizzled [rows][256] bf16 image
 DLLM_DEVICE int loff(int r, int col) { return (r << 8) + (((col >> 3) ^ gsw(r)) << 3) + (col & 7); }
@@ -63,9 +65,21 @@ DLLM_DEVICE bf16x8v frag(const uint16_t* T, int kk, int cb, int lane) {
   return __builtin_bit_cast(bf16x8v, v);
 }
 
+// 16x16x32 operand for columns [cb, cb+16) and k rows [kk, kk+32): lane l holds column cb + (l & 15),
+// k = kk + 8 (l >> 4) + j
+DLLM_DEVICE bf16x8v frag16(const uint16_t* T, int kk, int cb, int lane) {
+  const int r0 = kk + 8 * (lane >> 4);
+  const u16x4 lo = ld_tr(T, r0, cb, lane & 15);
+  const u16x4 hi = ld_tr(T, r0 + 4, cb, lane & 15);
+  const u16x8 v = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+  return __builtin_bit_cast(bf16x8v, v);
+}
+
 // NI = 32x32 MFMA tiles per wave along N: NI = 2 -> 8 waves of 128x64 (2 waves per SIMD), NI = 4 -> 4 waves of
 // 128x128 (one wave per SIMD, 256 fp32 accumulators in AGPRs, next k-step's fragments prefetched in VGPRs)
-template <int BK, int NBUF, bool PRIO, int NI>
+// MF = 16: v_mfma_f32_16x16x32_bf16 with the NI = 2 geometry (8 waves of 128x64, 8x4 tiles of 16x16 per wave):
+// same cycles per FLOP as 32x32x16, higher sustained clock on random data (MI355X_MICROARCH.md "DVFS give-back" 7)
+template <int BK, int NBUF, bool PRIO, int NI, int MF = 32>
 __global__ __launch_bounds__((256 / (32 * NI)) * 2 * 64, 1) void gemm_wgrad_kernel(GemmWgradParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint16_t* lds = reinterpret_cast<uint16_t*>(smem);  // [NBUF][A tile | B tile], each [BK][256]
@@ -106,19 +120,11 @@ __global__ __launch_bounds__((256 / (32 * NI)) * 2 * 64, 1) void gemm_wgrad_kern
     }
   };
 
-  f32x16 acc[4][NI];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < NI; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
 #pragma unroll
   for (int p = 0; p < NBUF - 1; ++p)
     if (p < nk) issue(p, p);
 
-  for (int it = 0; it < nk; ++it) {
+  auto stage_sync = [&](int it) {
     // stage `it` must have landed; stages it+1 .. it+NBUF-2 (if issued) may stay in flight
     const int ahead = min(NBUF - 2, nk - 1 - it);
     if (NBUF >= 4 && ahead >= 2) wait_vm<(NBUF >= 4 ? 2 * LPS : 0)>();
@@ -129,6 +135,72 @@ __global__ __launch_bounds__((256 / (32 * NI)) * 2 * 64, 1) void gemm_wgrad_kern
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (it + NBUF - 1 < nk) issue((it + NBUF - 1) % NBUF, it + NBUF - 1);
+  };
+
+  if constexpr (MF == 16) {
+    static_assert(NI == 2, "16x16x32 path uses the 8-wave 128x64 geometry");
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int it = 0; it < nk; ++it) {
+      stage_sync(it);
+      const uint16_t* As = lds + (it % NBUF) * 2 * TILE;
+      const uint16_t* Bs = As + TILE;
+#pragma unroll
+      for (int ks = 0; ks < BK / 32; ++ks) {
+        bf16x8v a[8], b[4];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) a[i] = frag16(As, 32 * ks, wm * 128 + 16 * i, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b[j] = frag16(Bs, 32 * ks, wn * 64 + 16 * j, lane);
+        if (PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)  // swapped roles: lane holds row m = lane & 15, 4 consecutive columns n
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
+        if (PRIO) __builtin_amdgcn_s_setprio(0);
+      }
+    }
+    // acc[i][j][0..3] = C[m0 + wm*128 + 16i + (lane & 15)][n0 + wn*64 + 16j + 4 (lane >> 4) + 0..3]
+    const int mrow = m0 + wm * 128 + (lane & 15);
+    const int ncol4 = n0 + wn * 64 + 4 * (lane >> 4);
+    if (P.splits == 1) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          uint16_t* cp = P.C + (long)(mrow + 16 * i) * P.ldc + ncol4 + 16 * j;
+          f32x4 v = acc[i][j];
+          if (P.beta) {
+            const u16x4 c = *reinterpret_cast<const u16x4*>(cp);
+            v += f32x4{bf2f(c.x), bf2f(c.y), bf2f(c.z), bf2f(c.w)};
+          }
+          const u16x4 o = {f2bf(v.x), f2bf(v.y), f2bf(v.z), f2bf(v.w)};
+          *reinterpret_cast<u16x4*>(cp) = o;
+        }
+    } else {
+      float* W = P.ws + (long)s * P.M * P.N;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          *reinterpret_cast<f32x4*>(W + (long)(mrow + 16 * i) * P.N + ncol4 + 16 * j) = acc[i][j];
+    }
+    return;
+  } else {
+  f32x16 acc[4][NI];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  for (int it = 0; it < nk; ++it) {
+    stage_sync(it);
     const uint16_t* As = lds + (it % NBUF) * 2 * TILE;
     const uint16_t* Bs = As + TILE;
     bf16x8v a[2][4], b[2][NI];
@@ -182,6 +254,7 @@ __global__ __launch_bounds__((256 / (32 * NI)) * 2 * 64, 1) void gemm_wgrad_kern
           W[(long)m * P.N + ncol + 32 * j] = acc[i][j][reg];
         }
   }
+  }  // MF == 32
 }
 
 // C[m][n] = bf16(sum_s ws[s][m][n] (+ C[m][n])), 8 columns per thread (N % 8 == 0)
@@ -209,18 +282,18 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   }
 }
 
-template <int BK, int NBUF, bool PRIO = false, int NI = 2>
+template <int BK, int NBUF, bool PRIO = false, int NI = 2, int MF = 32>
 int launch_wgrad(const GemmWgradParams& p, hipStream_t st) {
   constexpr int threads = (256 / (32 * NI)) * 2 * 64;
   const size_t lds = (size_t)NBUF * 2 * BK * 256 * 2;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_wgrad_kernel<BK, NBUF, PRIO, NI>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
+    (void)hipFuncSetAttribute((const void*)gemm_wgrad_kernel<BK, NBUF, PRIO, NI, MF>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
   const int nblk = p.ntiles * p.splits;
-  hipLaunchKernelGGL((gemm_wgrad_kernel<BK, NBUF, PRIO, NI>), dim3(nblk), dim3(threads), lds, st, p);
+  hipLaunchKernelGGL((gemm_wgrad_kernel<BK, NBUF, PRIO, NI, MF>), dim3(nblk), dim3(threads), lds, st, p);
   DLLM_CHECK_LAUNCH();
   if (p.splits > 1) {
     const long n8 = (long)p.M * p.N / 8;
@@ -242,8 +315,8 @@ extern "C" int dllm_gemm_wgrad_bk() { return 64; }
 extern "C" int dllm_gemm_wgrad(const GemmWgradParams* pp, int variant, hipStream_t st) {
   const GemmWgradParams& p = *pp;
   if (p.M % BM || p.N % BN || p.K <= 0 || p.splits < 1 || p.ntiles != (p.M / BM) * (p.N / BN)) return -4;
-  if (variant < 0)  // auto: deep BK=32 ring + prioritised MFMA issue on long K (measured best at K >= 32k)
-    variant = p.K >= 32768 ? 4 : 0;
+  if (variant < 0)  // auto: 16x16x32 MFMA, BK=64 x 2, prioritised MFMA issue — fastest on every T5 / BART wgrad
+    variant = 9;     // shape measured (profiles/r1_gemm_wgrad_bench_v3.jsonl: +3-11 % over the 32x32x16 variants)
   switch (variant) {
     case 1: return launch_wgrad<32, 4>(p, st);
     case 2: return launch_wgrad<32, 3>(p, st);
@@ -251,6 +324,9 @@ extern "C" int dllm_gemm_wgrad(const GemmWgradParams* pp, int variant, hipStream
     case 4: return launch_wgrad<32, 4, true>(p, st);
     case 5: return launch_wgrad<64, 2, false, 4>(p, st);
     case 6: return launch_wgrad<32, 4, false, 4>(p, st);
+    case 7: return launch_wgrad<64, 2, false, 2, 16>(p, st);
+    case 8: return launch_wgrad<32, 4, true, 2, 16>(p, st);
+    case 9: return launch_wgrad<64, 2, true, 2, 16>(p, st);
     default: return launch_wgrad<64, 2>(p, st);
   }
 }

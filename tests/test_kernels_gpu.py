@@ -235,7 +235,7 @@ def test_attention_packed_qkv_grad():
 
 
 # ------------------------------------------------------------------------------------ wgrad GEMM
-@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("variant", [0, 1, 2, 4, 7, 8, 9])
 @pytest.mark.parametrize("K,M,N,beta,lda_pad", [
     (4096, 768, 768, True, 0),      # t5-base o-proj shape class (many splits)
     (8192, 768, 3072, False, 0),    # wi wgrad, decoder token count
