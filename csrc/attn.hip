@@ -28,9 +28,14 @@
 //   dK/dV kernel (key blocks of 128, key on the lane): P and dS accumulators are the B operands of
 //   dV^T += dO^T Pd and dK^T += Q^T dS (dO^T, Q^T by transposed reads); bias-LUT gradient = diagonal sums
 //   of dS via a register shear + 2 LDS atomics per lane per tile.
+// Saturated T5 bias tiles (backward only, AttnParams::sat_lo / sat_hi): a wave tile whose relative distances all
+// lie beyond the last exact bucket (|j - i| >= 91 for bidirectional T5) sees one constant bias — it adds a scalar
+// instead of reading the LUT, and dK/dV credits its whole dS sum to the range's end entry instead of shearing
+// diagonals (the LUT gradient is consumed per bucket).  dK/dV -12..20 %.
 #include "common.h"
 #include "attn_params.h"
 #include <stdlib.h>
+#include <type_traits>
 
 using namespace dllm;
 
@@ -250,6 +255,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
     const bool tile_causal = CAUSAL && (kbase + FWD_BN - 1 > qw0 + P.causal_off);
     const int climit = qrow + P.causal_off - kbase;  // key offsets above this are masked (causal)
     const float* lb = lut_s + (kbase - qrow + P.Sq - 1 - lut_base);
+    // (no saturated-tile fast path here, unlike the backward kernels: with dropout hashing in this loop the
+    // scalar-bias body measured 12 % SLOWER than the LUT body, profiles/r1_attn_bench_v7_sat.jsonl)
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int kl0 = crow(i, hh), kl1 = 32 + kl0;
@@ -408,6 +415,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnParams P) {
   const bool qvalid = qrow < P.Sq;
   const float sl2 = P.scale * LOG2E;
   const int lut_base = P.Sq - 1 - (q0 + FWD_BM - 1);
+  float c_lo = 0.f, c_hi = 0.f;
   if (HAS_BIAS) {
     const int L = P.Sq + P.Sk - 1;
     const float* lrow = P.lut + (long)h * L;
@@ -415,6 +423,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnParams P) {
       const int gi = lut_base + i;
       lut_s[i] = (gi >= 0 && gi < L) ? lrow[gi] * LOG2E : 0.f;
     }
+    c_lo = lrow[0] * LOG2E;
+    c_hi = lrow[L - 1] * LOG2E;
   }
   bf16x8v qf[4], dof[4];
   float dpart = 0.f;
@@ -504,21 +514,31 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnParams P) {
     const bool tile_causal = CAUSAL && (kbase + FWD_BN - 1 > qw0 + P.causal_off);
     const int climit = qrow + P.causal_off - kbase;
     const float* lb = lut_s + (kbase - qrow + P.Sq - 1 - lut_base);
+    const int sat = !HAS_BIAS ? 0
+                    : (kbase + FWD_BN - 1 - qw0 + P.Sq - 1 <= P.sat_lo ? 1
+                       : (kbase - qw0 - 31 + P.Sq - 1 >= P.sat_hi ? 2 : 0));
+    auto bias_scale = [&](auto use_lut, float cbias) {  // as in the forward: saturated tiles add a scalar
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int kl0 = crow(i, hh), kl1 = 32 + kl0;
-      float v0 = s0[i] * sl2, v1 = s1[i] * sl2;
-      if (HAS_BIAS) {
-        v0 += lb[kl0];
-        v1 += lb[kl1];
+      for (int i = 0; i < 16; ++i) {
+        const int kl0 = crow(i, hh), kl1 = 32 + kl0;
+        float v0, v1;
+        if constexpr (decltype(use_lut)::value) {
+          v0 = s0[i] * sl2 + lb[kl0];
+          v1 = s1[i] * sl2 + lb[kl1];
+        } else {
+          v0 = s0[i] * sl2 + cbias;
+          v1 = s1[i] * sl2 + cbias;
+        }
+        if (CAUSAL) {
+          v0 = (tile_causal && kl0 > climit) ? -INFINITY : v0;
+          v1 = (tile_causal && kl1 > climit) ? -INFINITY : v1;
+        }
+        s0[i] = v0;
+        s1[i] = v1;
       }
-      if (CAUSAL) {
-        v0 = (tile_causal && kl0 > climit) ? -INFINITY : v0;
-        v1 = (tile_causal && kl1 > climit) ? -INFINITY : v1;
-      }
-      s0[i] = v0;
-      s1[i] = v1;
-    }
+    };
+    if (HAS_BIAS && sat == 0) bias_scale(std::true_type{}, 0.f);
+    else bias_scale(std::false_type{}, sat == 1 ? c_lo : (sat == 2 ? c_hi : 0.f));
     if ((HAS_KPM || kbase + FWD_BN > P.Sk) && tflag[kt] != 0) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
@@ -604,6 +624,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnParams P) {
     }
     for (int i = tid; i < win; i += 256) dlut_s[i] = 0.f;
   }
+  const float c_lo = HAS_BIAS ? P.lut[(long)h * L] * LOG2E : 0.f;  // saturated-range biases (log2-scaled)
+  const float c_hi = HAS_BIAS ? P.lut[(long)h * L + L - 1] * LOG2E : 0.f;
+  float sat_acc_lo = 0.f, sat_acc_hi = 0.f;                          // dS sums of saturated tiles
   bool key_ok = false;
   if (tid < BWD_BK) {
     const int kk = k0 + tid;
@@ -716,21 +739,36 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnParams P) {
         mw[4 * g + 3] = v.w;
       }
     }
+    // saturated tile (LUT indices kw0 - q0 - 31 + Sq - 1 .. kw0 + 31 - q0 + Sq - 1 in one constant range): scalar
+    // bias, and the dS sum is credited to the range's end entry instead of the per-diagonal shear
+    const int sat = !HAS_BIAS ? 0
+                    : (kw0 + 31 - q0 + P.Sq - 1 <= P.sat_lo ? 1 : (kw0 - q0 - 31 + P.Sq - 1 >= P.sat_hi ? 2 : 0));
     f32x16 pd, ds;
+    auto probs = [&](auto use_lut, float cbias) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int ql = crow(i, hh);
-      const int qg = q0 + ql;
-      float sv = sacc[i] * sl2 + km;
-      if (HAS_BIAS) sv += lrow_t[crow(i, 0)];
-      if (tile_causal && key > qg + P.causal_off) sv = -INFINITY;
-      const float pr = fast_exp2(sv - rv[ql]);  // lse = +inf for q >= Sq -> 0
-      float keepf = 1.f;
-      if (DROP) keepf = __uint_as_float((uint32_t)__builtin_amdgcn_sbfe((int)mw[i], mbit, 1) & dsbits);
-      pd[i] = pr * keepf;
-      ds[i] = pr * (dpacc[i] * keepf - rv[BWD_BQ + ql]);
-    }
-    if (HAS_BIAS) {
+      for (int i = 0; i < 16; ++i) {
+        const int ql = crow(i, hh);
+        const int qg = q0 + ql;
+        float sv = sacc[i] * sl2 + km;
+        if constexpr (decltype(use_lut)::value) sv += lrow_t[crow(i, 0)];
+        else if (HAS_BIAS) sv += cbias;
+        if (tile_causal && key > qg + P.causal_off) sv = -INFINITY;
+        const float pr = fast_exp2(sv - rv[ql]);  // lse = +inf for q >= Sq -> 0
+        float keepf = 1.f;
+        if (DROP) keepf = __uint_as_float((uint32_t)__builtin_amdgcn_sbfe((int)mw[i], mbit, 1) & dsbits);
+        pd[i] = pr * keepf;
+        ds[i] = pr * (dpacc[i] * keepf - rv[BWD_BQ + ql]);
+      }
+    };
+    if (HAS_BIAS && sat == 0) probs(std::true_type{}, 0.f);
+    else probs(std::false_type{}, sat == 1 ? c_lo : c_hi);
+    if (HAS_BIAS && sat != 0) {
+      float t = 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) t += ds[i];
+      if (sat == 1) sat_acc_lo += t;
+      else sat_acc_hi += t;
+    } else if (HAS_BIAS) {
       // diagonal sums of the wave's 32x32 dS tile: rotate register i (row rho = crow(i, hh)) left by rho
       // lanes so lane r receives element (rho, (r + rho) & 31) whose diagonal (col - row) is r or r - 32
       float pos = 0.f, neg = 0.f;
@@ -786,6 +824,11 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnParams P) {
       const int gi = k0 + i;
       const float v = dlut_s[i];
       if (gi < L && v != 0.f) atomicAdd(grow + gi, v);
+    }
+    const float a_lo = wave_sum(sat_acc_lo), a_hi = wave_sum(sat_acc_hi);
+    if (lane == 0) {
+      if (a_lo != 0.f) atomicAdd(grow, a_lo);
+      if (a_hi != 0.f) atomicAdd(grow + L - 1, a_hi);
     }
   }
 }

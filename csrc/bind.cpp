@@ -2,6 +2,8 @@
 // Host-side validation lives here: every shape / dtype / stride / alignment a kernel assumes is checked
 // BEFORE launch (a kernel that faults can reset every GPU on the node), then the C-ABI launchers in
 // csrc/*.hip run on the current torch HIP stream.
+#include <climits>
+
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 #include <c10/hip/HIPStream.h>
@@ -299,6 +301,18 @@ void fill_qkv(AttnParams& P, const Tensor& q, const Tensor& k, const Tensor& v, 
                 "bias_lut must be fp32 [H, Sq + Sk - 1] contiguous on GPU");
     P.lut = lut->data_ptr<float>();
   }
+  P.sat_lo = INT_MIN / 2;  // saturated-bias ranges off unless the caller declares them (set_sat)
+  P.sat_hi = INT_MAX / 2;
+}
+
+// sat_lo / sat_hi: LUT index ranges [0, sat_lo] and [sat_hi, L) of constant bias whose gradient is consumed per
+// bucket only (ops/attention.py relative_bias_lut); negative = off
+void set_sat(AttnParams& P, int64_t sat_lo, int64_t sat_hi) {
+  if (P.lut == nullptr || sat_lo < 0 || sat_hi < 0) return;
+  const int64_t L = (int64_t)P.Sq + P.Sk - 1;
+  TORCH_CHECK(sat_lo < L && sat_hi > sat_lo && sat_hi <= L, "attention: bad saturated-bias bounds");
+  P.sat_lo = (int)sat_lo;
+  P.sat_hi = (int)sat_hi;
 }
 
 int64_t dmask_numel(const AttnParams& P) {
@@ -308,9 +322,10 @@ int64_t dmask_numel(const AttnParams& P) {
 
 std::vector<Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, const optional<Tensor>& kpm,
                              const optional<Tensor>& lut, double scale, bool causal, double p, int64_t seed,
-                             const optional<Tensor>& dmask_in) {
+                             const optional<Tensor>& dmask_in, int64_t sat_lo, int64_t sat_hi) {
   AttnParams P{};
   fill_qkv(P, q, k, v, kpm, lut, scale, causal, p, seed);
+  set_sat(P, sat_lo, sat_hi);
   auto o = at::empty({P.B, P.Sq, P.H, 64}, q.options());
   auto lse = at::empty({P.B, P.H, P.Sq}, q.options().dtype(at::kFloat));
   P.o_out = reinterpret_cast<uint16_t*>(o.data_ptr());
@@ -351,9 +366,11 @@ std::vector<Tensor> attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& 
                              const Tensor& lse, const optional<Tensor>& kpm, const optional<Tensor>& lut,
                              double scale, bool causal, double p, int64_t seed, bool need_dlut,
                              const optional<Tensor>& dq_out, const optional<Tensor>& dk_out,
-                             const optional<Tensor>& dv_out, const optional<Tensor>& dmask) {
+                             const optional<Tensor>& dv_out, const optional<Tensor>& dmask, int64_t sat_lo,
+                             int64_t sat_hi) {
   AttnParams P{};
   fill_qkv(P, q, k, v, kpm, lut, scale, causal, p, seed);
+  set_sat(P, sat_lo, sat_hi);
   if (p > 0.0) {
     TORCH_CHECK(dmask.has_value() && dmask->defined() && dmask->scalar_type() == at::kInt && dmask->is_contiguous() &&
                     dmask->numel() == dmask_numel(P) && dmask->is_cuda(),
@@ -570,12 +587,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sq_norm", &sq_norm);
   m.def("adamw_step", &adamw_step);
   m.def("attn_fwd", &attn_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("kpm"), py::arg("lut"),
-        py::arg("scale"), py::arg("causal"), py::arg("p"), py::arg("seed"), py::arg("dmask_in") = py::none());
+        py::arg("scale"), py::arg("causal"), py::arg("p"), py::arg("seed"), py::arg("dmask_in") = py::none(),
+        py::arg("sat_lo") = -1, py::arg("sat_hi") = -1);
   m.def("attn_dropout_mask", &attn_dropout_mask);
   m.def("attn_bwd", &attn_bwd, py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"),
         py::arg("lse"), py::arg("kpm"), py::arg("lut"), py::arg("scale"), py::arg("causal"), py::arg("p"),
         py::arg("seed"), py::arg("need_dlut"), py::arg("dq_out") = py::none(), py::arg("dk_out") = py::none(),
-        py::arg("dv_out") = py::none(), py::arg("dmask") = py::none());
+        py::arg("dv_out") = py::none(), py::arg("dmask") = py::none(), py::arg("sat_lo") = -1,
+        py::arg("sat_hi") = -1);
   m.def("attn_params_size", []() { return dllm_attn_params_size(); });
   m.def("gemm_wgrad", &gemm_wgrad, "c (+)= a^T b (token-major bf16 operands)", py::arg("a"), py::arg("b"), py::arg("c"),
         py::arg("beta") = true, py::arg("variant") = 0, py::arg("splits") = 0);

@@ -61,14 +61,29 @@ def relative_bias_lut(table: torch.Tensor, q_len: int, k_len: int, bidirectional
     row ``i`` (absolute position ``i + q_offset``) and key ``j``.  Differentiable w.r.t. ``table``
     (shape ``[num_buckets, H]``).  Returns fp32 ``[H, q_len + k_len - 1]``."""
     key = (q_len, k_len, bidirectional, num_buckets, max_distance, q_offset, table.device)
-    idx = _bucket_cache.get(key)
-    if idx is None:
-        rel = torch.arange(-(q_len - 1), k_len, device=table.device, dtype=torch.long) - q_offset
+    hit = _bucket_cache.get(key)
+    if hit is None:
+        rel = torch.arange(-(q_len - 1), k_len, dtype=torch.long) - q_offset
         idx = relative_position_bucket(rel, bidirectional, num_buckets, max_distance)
+        hit = (idx.to(table.device), saturated_ranges(idx))
         if len(_bucket_cache) > 256:
             _bucket_cache.clear()
-        _bucket_cache[key] = idx
-    return table.float().index_select(0, idx).t().contiguous()
+        _bucket_cache[key] = hit
+    idx, sat = hit
+    lut = table.float().index_select(0, idx).t().contiguous()
+    # the kernels may treat tiles inside these constant-bucket ranges as scalar-bias tiles (csrc/attn_params.h):
+    # valid because this LUT's gradient only reaches the table through index_select (per bucket)
+    lut._dllm_sat = sat
+    return lut
+
+
+def saturated_ranges(idx: torch.Tensor) -> tuple[int, int]:
+    """(sat_lo, sat_hi) for a bucket index row over the LUT: entries [0, sat_lo] share idx[0]'s bucket and
+    [sat_hi, L) share idx[-1]'s (T5 buckets saturate at +-max_distance)."""
+    L = idx.numel()
+    same_lo = (idx == idx[0]).long().cumprod(0).sum().item()
+    same_hi = (idx.flip(0) == idx[-1]).long().cumprod(0).sum().item()
+    return int(same_lo) - 1, int(L - same_hi)
 
 
 # --------------------------------------------------------------------------- reference
@@ -125,9 +140,12 @@ class _AttnFn(torch.autograd.Function):
             cur = torch.cuda.current_stream(q.device)
             cur.wait_event(ev)
             dmask_in.record_stream(cur)
-        o, lse, dmask = C.attn_fwd(q, k, v, kpm, lut, float(scale), bool(causal), float(p), int(seed), dmask_in)
+        sat = getattr(lut, "_dllm_sat", None) if lut is not None else None
+        sat_lo, sat_hi = sat if sat is not None else (-1, -1)
+        o, lse, dmask = C.attn_fwd(q, k, v, kpm, lut, float(scale), bool(causal), float(p), int(seed), dmask_in,
+                                   sat_lo, sat_hi)
         ctx.save_for_backward(a, b, c, o, lse, lut, kpm, dmask)
-        ctx.cfg = (mode, scale, causal, p, seed, lut is not None and lut.requires_grad)
+        ctx.cfg = (mode, scale, causal, p, seed, lut is not None and lut.requires_grad, sat_lo, sat_hi)
         # ops/linear.py stacked_linear: the packed kv is a slice of a multi-layer projection and its
         # gradient has a home in the stacked gradient buffer — write dK/dV there directly
         ctx.grad_into = getattr(b, "_dllm_grad_into", None) if mode == "q_kv" else None
@@ -137,7 +155,7 @@ class _AttnFn(torch.autograd.Function):
     def backward(ctx, do):
         C = _ext.native()
         a, b, c, o, lse, lut, kpm, dmask = ctx.saved_tensors
-        mode, scale, causal, p, seed, need_dlut = ctx.cfg
+        mode, scale, causal, p, seed, need_dlut, sat_lo, sat_hi = ctx.cfg
         q, k, v = _split(mode, a, b, c)
         da = db = dc = None
         if mode == "qkv":
@@ -152,7 +170,7 @@ class _AttnFn(torch.autograd.Function):
         else:
             dq = dk = dv = None
         rq, rk, rv, dlut = C.attn_bwd(do.contiguous(), q, k, v, o, lse, kpm, lut, float(scale), bool(causal),
-                                      float(p), int(seed), bool(need_dlut), dq, dk, dv, dmask)
+                                      float(p), int(seed), bool(need_dlut), dq, dk, dv, dmask, sat_lo, sat_hi)
         if mode == "sep":
             da, db, dc = rq, rk, rv
         return None, da, db, dc, (dlut if need_dlut else None), None, None, None, None, None, None

@@ -374,3 +374,29 @@ def test_gemm_fused_rejects_unsupported_shapes():
     assert not C.gemm_fused_supported(x, w, False)
     with pytest.raises(RuntimeError):
         C.gemm_fused(x, w, False, 1, None, None, None, 0.0, 0, -1)
+
+
+@pytest.mark.parametrize("causal,S", [(False, 1024), (True, 384), (False, 300)])
+def test_attention_saturated_bias_tiles_match(causal, S):
+    """relative_bias_lut's LUT declares its constant-bucket ranges; the kernels' scalar-bias tiles and end-of-range
+    dS credit must give the same outputs and the same per-bucket table gradient as the full LUT path."""
+    torch.manual_seed(0)
+    B, H, D, p = 2, 4, 64, 0.1
+    qkv = torch.randn(B, S, 3, H, D, device=DEV).to(torch.bfloat16)
+    g = torch.randn(B, S, H, D, device=DEV).to(torch.bfloat16)
+    table = torch.randn(32, H, device=DEV)
+    outs = []
+    for use_sat in (False, True):
+        tb = table.clone().requires_grad_(True)
+        lut = A.relative_bias_lut(tb, S, S, not causal, 32, 128)
+        assert lut._dllm_sat[0] >= 0
+        if not use_sat:
+            lut._dllm_sat = None
+        x = qkv.clone().requires_grad_(True)
+        o = A.attention_qkv(x, bias_lut=lut, causal=causal, scale=1.0, dropout_p=p, seed=3)
+        o.backward(g)
+        outs.append((o.detach().float(), x.grad.float(), tb.grad.clone()))
+    (o0, gx0, gt0), (o1, gx1, gt1) = outs
+    assert _rel(o1, o0) < 1e-3, _rel(o1, o0)
+    assert _rel(gx1, gx0) < 1e-3, _rel(gx1, gx0)
+    assert _rel(gt1, gt0) < 1e-3, _rel(gt1, gt0)

@@ -12,7 +12,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from distributed_llms_example_amd.ops import attention as A
 
 
-def run(B, H, Sq, Sk, bias, kpm, causal, p, iters=20):
+def run(B, H, Sq, Sk, bias, kpm, causal, p, iters=20, sat=True):
     D = 64
     dev = "cuda"
     q = torch.randn(B, Sq, H, D, device=dev, dtype=torch.bfloat16, requires_grad=True)
@@ -21,10 +21,14 @@ def run(B, H, Sq, Sk, bias, kpm, causal, p, iters=20):
     tab = torch.randn(32, H, device=dev, requires_grad=True) if bias else None
     mask = torch.ones(B, Sk, dtype=torch.bool, device=dev) if kpm else None
     lut = A.relative_bias_lut(tab, Sq, Sk, not causal, 32, 128) if bias else None
+    if bias:  # sat=False: no saturated-bias ranges declared (every tile takes the LUT path)
+        sat_r = lut._dllm_sat if sat else None
+        lut = lut.detach()
+        lut._dllm_sat = sat_r
 
     def fwd():
         return A.attention(q, k, v, scale=1.0, causal=causal, key_padding_mask=mask,
-                           bias_lut=lut.detach() if bias else None, dropout_p=p, seed=1)
+                           bias_lut=lut if bias else None, dropout_p=p, seed=1)
     o = fwd()
     g = torch.randn_like(o)
     for _ in range(3):
@@ -36,6 +40,8 @@ def run(B, H, Sq, Sk, bias, kpm, causal, p, iters=20):
     torch.cuda.synchronize()
     tf = (time.perf_counter() - t0) / iters
     lut2 = A.relative_bias_lut(tab, Sq, Sk, not causal, 32, 128) if bias else None
+    if bias and not sat:
+        lut2._dllm_sat = None
     def fb():
         o = A.attention(q, k, v, scale=1.0, causal=causal, key_padding_mask=mask, bias_lut=lut2, dropout_p=p, seed=1)
         o.backward(g, retain_graph=True)
@@ -48,7 +54,8 @@ def run(B, H, Sq, Sk, bias, kpm, causal, p, iters=20):
     torch.cuda.synchronize()
     tb = (time.perf_counter() - t0) / iters - tf
     fl = 4 * B * H * Sq * Sk * D * (0.5 if causal else 1.0)
-    return {"B": B, "H": H, "Sq": Sq, "Sk": Sk, "bias": bias, "kpm": kpm, "causal": causal, "p": p,
+    return {"B": B, "H": H, "Sq": Sq, "Sk": Sk, "bias": bias, "sat": bool(bias and sat), "kpm": kpm,
+            "causal": causal, "p": p,
             "fwd_ms": tf * 1e3, "bwd_ms": tb * 1e3, "fwd_tflops": fl / tf / 1e12, "bwd_tflops": 2.5 * fl / tb / 1e12}
 
 
@@ -63,3 +70,5 @@ if __name__ == "__main__":
         cases = cases[:1]
     for c in cases:
         print(json.dumps(run(*c)), flush=True)
+        if c[4]:  # bias cases: also without the saturated-tile fast path (A/B in one process)
+            print(json.dumps(run(*c, sat=False)), flush=True)
