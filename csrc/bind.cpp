@@ -469,9 +469,9 @@ int64_t gemm_wgrad(const Tensor& a, const Tensor& b, Tensor& c, bool beta, int64
 // forwards also write the pre-activation to aux_out; the backward epilogues read aux (saved activation for
 // d-relu, pre-activation for d-gelu) and apply the matching dropout backward.
 int64_t gemm_fused_variant(int64_t K) {
-  // 16x16x32 MFMA, BK = 64, 2 stages: fastest of the four on every T5 / BART FFN shape measured
-  // (profiles/r1_gemm_fused_bench.jsonl: 8-25 % over the 32x32x16 variants, 5-24 % over hipBLASLt + act kernel)
-  return K % 64 == 0 ? 3 : 1;
+  // 16x16x32 MFMA, BK = 64, 2 stages, both k-steps' fragments read up front: fastest on every T5 / BART FFN shape
+  // measured (profiles/r1_gemm_fused_bench*.jsonl: 8-25 % over the 32x32x16 variants, then up to -12 % more)
+  return K % 64 == 0 ? 4 : 1;
 }
 
 bool gemm_fused_supported(const Tensor& a, const Tensor& b, bool b_kmajor) {
@@ -545,7 +545,7 @@ Tensor gemm_fused(const Tensor& a, const Tensor& b, bool b_kmajor, int64_t epi, 
     P.thr = t >= 65535.0 ? 0xFFFFu : (uint32_t)t;
   }
   const int v = variant >= 0 ? (int)variant : (int)gemm_fused_variant(K);
-  TORCH_CHECK(v >= 0 && v <= 3, "gemm_fused: bad variant ", v);
+  TORCH_CHECK(v >= 0 && v <= 4, "gemm_fused: bad variant ", v);
   check_rc(dllm_gemm_fused(&P, b_kmajor ? 1 : 0, v, stream()), "gemm_fused");
   return out;
 }

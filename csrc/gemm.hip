@@ -79,7 +79,9 @@ DLLM_DEVICE bf16x8v frag16(const uint16_t* T, int kk, int cb, int lane) {
 // 128x128 (one wave per SIMD, 256 fp32 accumulators in AGPRs, next k-step's fragments prefetched in VGPRs)
 // MF = 16: v_mfma_f32_16x16x32_bf16 with the NI = 2 geometry (8 waves of 128x64, 8x4 tiles of 16x16 per wave):
 // same cycles per FLOP as 32x32x16, higher sustained clock on random data (MI355X_MICROARCH.md "DVFS give-back" 7)
-template <int BK, int NBUF, bool PRIO, int NI, int MF = 32>
+// PRE (16x16, BK = 64): both 32-deep k-steps' fragments are read before the first MFMA of a stage.  Not used:
+// with both operands on transposed reads it needs > 256 VGPRs and spills (2x slower, r1_gemm_wgrad_bench_v4).
+template <int BK, int NBUF, bool PRIO, int NI, int MF = 32, bool PRE = false>
 __global__ __launch_bounds__((256 / (32 * NI)) * 2 * 64, 1) void gemm_wgrad_kernel(GemmWgradParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint16_t* lds = reinterpret_cast<uint16_t*>(smem);  // [NBUF][A tile | B tile], each [BK][256]
@@ -148,13 +150,13 @@ __global__ __launch_bounds__((256 / (32 * NI)) * 2 * 64, 1) void gemm_wgrad_kern
       stage_sync(it);
       const uint16_t* As = lds + (it % NBUF) * 2 * TILE;
       const uint16_t* Bs = As + TILE;
+      auto load_k = [&](int kk, bf16x8v (&a)[8], bf16x8v (&b)[4]) {
 #pragma unroll
-      for (int ks = 0; ks < BK / 32; ++ks) {
-        bf16x8v a[8], b[4];
+        for (int i = 0; i < 8; ++i) a[i] = frag16(As, kk, wm * 128 + 16 * i, lane);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) a[i] = frag16(As, 32 * ks, wm * 128 + 16 * i, lane);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) b[j] = frag16(Bs, 32 * ks, wn * 64 + 16 * j, lane);
+        for (int j = 0; j < 4; ++j) b[j] = frag16(Bs, kk, wn * 64 + 16 * j, lane);
+      };
+      auto mfma_block = [&](const bf16x8v (&a)[8], const bf16x8v (&b)[4]) {
         if (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int i = 0; i < 8; ++i)
@@ -162,6 +164,20 @@ __global__ __launch_bounds__((256 / (32 * NI)) * 2 * 64, 1) void gemm_wgrad_kern
           for (int j = 0; j < 4; ++j)  // swapped roles: lane holds row m = lane & 15, 4 consecutive columns n
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
         if (PRIO) __builtin_amdgcn_s_setprio(0);
+      };
+      if constexpr (PRE && BK == 64) {
+        bf16x8v a0[8], b0[4], a1[8], b1[4];
+        load_k(0, a0, b0);
+        load_k(32, a1, b1);
+        mfma_block(a0, b0);
+        mfma_block(a1, b1);
+      } else {
+#pragma unroll
+        for (int ks = 0; ks < BK / 32; ++ks) {
+          bf16x8v a[8], b[4];
+          load_k(32 * ks, a, b);
+          mfma_block(a, b);
+        }
       }
     }
     // acc[i][j][0..3] = C[m0 + wm*128 + 16i + (lane & 15)][n0 + wn*64 + 16j + 4 (lane >> 4) + 0..3]
@@ -282,18 +298,18 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   }
 }
 
-template <int BK, int NBUF, bool PRIO = false, int NI = 2, int MF = 32>
+template <int BK, int NBUF, bool PRIO = false, int NI = 2, int MF = 32, bool PRE = false>
 int launch_wgrad(const GemmWgradParams& p, hipStream_t st) {
   constexpr int threads = (256 / (32 * NI)) * 2 * 64;
   const size_t lds = (size_t)NBUF * 2 * BK * 256 * 2;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_wgrad_kernel<BK, NBUF, PRIO, NI, MF>,
+    (void)hipFuncSetAttribute((const void*)gemm_wgrad_kernel<BK, NBUF, PRIO, NI, MF, PRE>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
   const int nblk = p.ntiles * p.splits;
-  hipLaunchKernelGGL((gemm_wgrad_kernel<BK, NBUF, PRIO, NI, MF>), dim3(nblk), dim3(threads), lds, st, p);
+  hipLaunchKernelGGL((gemm_wgrad_kernel<BK, NBUF, PRIO, NI, MF, PRE>), dim3(nblk), dim3(threads), lds, st, p);
   DLLM_CHECK_LAUNCH();
   if (p.splits > 1) {
     const long n8 = (long)p.M * p.N / 8;
@@ -311,7 +327,8 @@ extern "C" int dllm_gemm_wgrad_bk() { return 64; }
 
 // variant: 0 = BK64 x 2 stages (128 KB LDS), 1 = BK32 x 4 stages (128 KB), 2 = BK32 x 3 stages (96 KB),
 // 3 / 4 = variants 0 / 1 with s_setprio raised around the MFMA block,
-// 5 / 6 = variants 0 / 1 with 4 waves of 128x128 (one wave per SIMD, accumulators in AGPRs)
+// 5 / 6 = variants 0 / 1 with 4 waves of 128x128 (one wave per SIMD, accumulators in AGPRs),
+// 7 / 8 / 9 = variants 0 / 4 / 3 on v_mfma_f32_16x16x32_bf16
 extern "C" int dllm_gemm_wgrad(const GemmWgradParams* pp, int variant, hipStream_t st) {
   const GemmWgradParams& p = *pp;
   if (p.M % BM || p.N % BN || p.K <= 0 || p.splits < 1 || p.ntiles != (p.M / BM) * (p.N / BN)) return -4;

@@ -128,10 +128,9 @@ DLLM_DEVICE f32x4 load4(const uint16_t* p) {
   return f32x4{bf2f(r.x), bf2f(r.y), bf2f(r.z), bf2f(r.w)};
 }
 
-// v = accumulators for C[m][n .. n+3] (n % 4 == 0)
+// v = accumulators (+ bias, added by the caller from registers loaded once) for C[m][n .. n+3] (n % 4 == 0)
 template <int EPI>
 DLLM_DEVICE void epilogue4(const GemmFusedParams& P, int m, int n, f32x4 v) {
-  if (P.bias) v += load4(P.bias + n);
   const bool drop = P.p > 0.f;
   const uint32_t e = (uint32_t)m * (uint32_t)P.N + (uint32_t)n;  // output element index (< 2^32, host-checked)
   if (EPI == EPI_RELU || EPI == EPI_GELU || EPI == EPI_GELU_TANH) {
@@ -158,7 +157,9 @@ DLLM_DEVICE void epilogue4(const GemmFusedParams& P, int m, int n, f32x4 v) {
 // MF = 16: v_mfma_f32_16x16x32_bf16, 8x4 tiles of 16x16 (same cycles per FLOP; on random data the chip holds a
 // higher clock on this shape, MI355X_MICROARCH.md "DVFS give-back" item 7) — both built, the faster picked by
 // measurement (tools/gemm_fused_bench.py).
-template <int BK, int NBUF, bool BKM, int EPI, int MF>
+// PRE (16x16 only): all fragments of both 32-deep k-steps of a stage are read before the first MFMA, so the second
+// k-step's LDS latency hides under the first k-step's MFMAs (+96 VGPRs of fragments instead of +48).
+template <int BK, int NBUF, bool BKM, int EPI, int MF, bool PRE = false>
 __global__ __launch_bounds__(NT, 1) void gemm_fused_kernel(GemmFusedParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint16_t* lds = reinterpret_cast<uint16_t*>(smem);  // [NBUF][A image | B image], BK*256 elements each
@@ -266,6 +267,12 @@ __global__ __launch_bounds__(NT, 1) void gemm_fused_kernel(GemmFusedParams P) {
 
     // epilogue: acc[i][j][4g + 0..3] = C[m0 + wm*128 + 32i + (lane & 31)][n0 + wn*64 + 32j + 8g + 4hh + 0..3]
     const int mrow = m0 + wm * 128 + (lane & 31);
+    f32x4 bv[2][4];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        bv[j][g] = P.bias ? load4(P.bias + n0 + wn * 64 + 32 * j + 8 * g + 4 * hh) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -273,7 +280,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_fused_kernel(GemmFusedParams P) {
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const f32x4 v = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
-          epilogue4<EPI>(P, mrow + 32 * i, n0 + wn * 64 + 32 * j + 8 * g + 4 * hh, v);
+          epilogue4<EPI>(P, mrow + 32 * i, n0 + wn * 64 + 32 * j + 8 * g + 4 * hh, v + bv[j][g]);
         }
   } else {
     static_assert(MF == 16 && BK == 64, "16x16x32 fragments are bank-conflict free on the BK = 64 images only");
@@ -283,48 +290,65 @@ __global__ __launch_bounds__(NT, 1) void gemm_fused_kernel(GemmFusedParams P) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+    auto mfma_block = [&](const bf16x8v (&a)[8], const bf16x8v (&b)[4]) {
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)  // swapped roles: lane holds row m = lane & 15, 4 consecutive n
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    };
+    auto load_k = [&](const uint16_t* As, const uint16_t* Bs, int kk, bf16x8v (&a)[8], bf16x8v (&b)[4]) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) a[i] = RI::frag16(As, kk, wm * 128 + 16 * i, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        b[j] = BKM ? frag_km16(Bs, kk, wn * 64 + 16 * j, lane) : RI::frag16(Bs, kk, wn * 64 + 16 * j, lane);
+    };
     for (int it = 0; it < nk; ++it) {
       stage_sync(it);
       const uint16_t* As = lds + (it % NBUF) * 2 * TILE;
       const uint16_t* Bs = As + TILE;
+      if constexpr (PRE) {
+        bf16x8v a0[8], b0[4], a1[8], b1[4];
+        load_k(As, Bs, 0, a0, b0);
+        load_k(As, Bs, 32, a1, b1);
+        mfma_block(a0, b0);
+        mfma_block(a1, b1);
+      } else {
 #pragma unroll
-      for (int ks = 0; ks < BK / 32; ++ks) {
-        bf16x8v a[8], b[4];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) a[i] = RI::frag16(As, 32 * ks, wm * 128 + 16 * i, lane);
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          b[j] = BKM ? frag_km16(Bs, 32 * ks, wn * 64 + 16 * j, lane) : RI::frag16(Bs, 32 * ks, wn * 64 + 16 * j, lane);
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j)  // swapped roles: lane holds row m = lane & 15, 4 consecutive n
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
-        __builtin_amdgcn_s_setprio(0);
+        for (int ks = 0; ks < BK / 32; ++ks) {
+          bf16x8v a[8], b[4];
+          load_k(As, Bs, 32 * ks, a, b);
+          mfma_block(a, b);
+        }
       }
     }
 
     // epilogue: acc[i][j][0..3] = C[m0 + wm*128 + 16i + (lane & 15)][n0 + wn*64 + 16j + 4 (lane >> 4) + 0..3]
     const int mrow = m0 + wm * 128 + (lane & 15);
     const int ncol = n0 + wn * 64 + 4 * (lane >> 4);
+    f32x4 bv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bv[j] = P.bias ? load4(P.bias + ncol + 16 * j) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) epilogue4<EPI>(P, mrow + 16 * i, ncol + 16 * j, acc[i][j]);
+      for (int j = 0; j < 4; ++j) epilogue4<EPI>(P, mrow + 16 * i, ncol + 16 * j, acc[i][j] + bv[j]);
   }
 }
 
-template <int BK, int NBUF, bool BKM, int EPI, int MF>
+template <int BK, int NBUF, bool BKM, int EPI, int MF, bool PRE = false>
 int launch(const GemmFusedParams& p, hipStream_t st) {
   const size_t lds = (size_t)NBUF * 2 * BK * 256 * 2;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_fused_kernel<BK, NBUF, BKM, EPI, MF>,
+    (void)hipFuncSetAttribute((const void*)gemm_fused_kernel<BK, NBUF, BKM, EPI, MF, PRE>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
-  hipLaunchKernelGGL((gemm_fused_kernel<BK, NBUF, BKM, EPI, MF>), dim3(p.tm * p.tn), dim3(NT), lds, st, p);
+  hipLaunchKernelGGL((gemm_fused_kernel<BK, NBUF, BKM, EPI, MF, PRE>), dim3(p.tm * p.tn), dim3(NT), lds, st, p);
   DLLM_CHECK_LAUNCH();
   return 0;
 }
@@ -335,6 +359,7 @@ int launch_v(const GemmFusedParams& p, int variant, hipStream_t st) {
     case 1: return launch<32, 4, BKM, EPI, 32>(p, st);
     case 2: return launch<32, 3, BKM, EPI, 32>(p, st);
     case 3: return launch<64, 2, BKM, EPI, 16>(p, st);
+    case 4: return launch<64, 2, BKM, EPI, 16, true>(p, st);
     default: return launch<64, 2, BKM, EPI, 32>(p, st);
   }
 }
@@ -356,10 +381,10 @@ int dispatch_epi(const GemmFusedParams& p, int variant, hipStream_t st) {
 }  // namespace
 
 // variant: 0 = BK64 x 2 stages, 1 = BK32 x 4 stages, 2 = BK32 x 3 stages (all 128 / 96 KB LDS, 32x32x16 MFMA),
-// 3 = BK64 x 2 stages with 16x16x32 MFMA
+// 3 = BK64 x 2 stages with 16x16x32 MFMA, 4 = variant 3 with both k-steps' fragments read up front
 extern "C" int dllm_gemm_fused(const GemmFusedParams* pp, int b_kmajor, int variant, hipStream_t st) {
   const GemmFusedParams& p = *pp;
-  const int bk = (variant == 0 || variant == 3) ? 64 : 32;
+  const int bk = (variant == 0 || variant >= 3) ? 64 : 32;
   if (p.M % BM || p.N % BN || p.K <= 0 || p.K % bk || p.tm * BM != p.M || p.tn * BN != p.N) return -4;
   return b_kmajor ? dispatch_epi<true>(p, variant, st) : dispatch_epi<false>(p, variant, st);
 }

@@ -319,7 +319,7 @@ _EPI_FWD = {None: 0, "relu": 1, "gelu": 2, "gelu_new": 5}
 _EPI_BWD = {"relu": 3, "gelu": 4, "gelu_new": 6}
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("act,p,bias", [(None, 0.0, False), ("relu", 0.1, False), ("gelu", 0.0, True),
                                         ("gelu_new", 0.1, True)])
 def test_gemm_fused_forward(variant, act, p, bias):
@@ -345,7 +345,7 @@ def test_gemm_fused_forward(variant, act, p, bias):
         assert _rel(aux, u) < 1e-2
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("act,p", [("relu", 0.1), ("relu", 0.0), ("gelu", 0.1), ("gelu_new", 0.0)])
 def test_gemm_fused_backward(variant, act, p):
     """dU = act'(U) * dropout'(dY Wo) with Wo k-major ([d, F]) vs fp32 autograd of the same composite."""
