@@ -28,10 +28,10 @@
 //   dK/dV kernel (key blocks of 128, key on the lane): P and dS accumulators are the B operands of
 //   dV^T += dO^T Pd and dK^T += Q^T dS (dO^T, Q^T by transposed reads); bias-LUT gradient = diagonal sums
 //   of dS via a register shear + 2 LDS atomics per lane per tile.
-// Saturated T5 bias tiles (backward only, AttnParams::sat_lo / sat_hi): a wave tile whose relative distances all
-// lie beyond the last exact bucket (|j - i| >= 91 for bidirectional T5) sees one constant bias — it adds a scalar
-// instead of reading the LUT, and dK/dV credits its whole dS sum to the range's end entry instead of shearing
-// diagonals (the LUT gradient is consumed per bucket).  dK/dV -12..20 %.
+// Saturated T5 bias tiles (AttnParams::sat_lo / sat_hi): a wave tile whose relative distances all lie beyond the
+// last exact bucket (|j - i| >= 91 for bidirectional T5) sees one constant bias — it adds a scalar instead of
+// reading the LUT, and dK/dV credits its whole dS sum to the range's end entry instead of shearing diagonals (the
+// LUT gradient is consumed per bucket).  dK/dV -12..20 %, forward -2 % (interleaved A/B, r1_attn_bench_v8_ab).
 #include "common.h"
 #include "attn_params.h"
 #include <stdlib.h>
@@ -173,6 +173,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
   const float sl2 = P.scale * LOG2E;
 
   const int lut_base = P.Sq - 1 - (q0 + FWD_BM - 1);  // lut_s[i] = LUT[lut_base + i]
+  float c_lo = 0.f, c_hi = 0.f;                        // saturated-range biases (log2-scaled)
   if (HAS_BIAS) {
     const int L = P.Sq + P.Sk - 1;
     const float* lrow = P.lut + (long)h * L;
@@ -180,6 +181,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
       const int gi = lut_base + i;
       lut_s[i] = (gi >= 0 && gi < L) ? lrow[gi] * LOG2E : 0.f;
     }
+    c_lo = lrow[0] * LOG2E;
+    c_hi = lrow[L - 1] * LOG2E;
   }
   bf16x8v qf[4];
   {
@@ -255,23 +258,33 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
     const bool tile_causal = CAUSAL && (kbase + FWD_BN - 1 > qw0 + P.causal_off);
     const int climit = qrow + P.causal_off - kbase;  // key offsets above this are masked (causal)
     const float* lb = lut_s + (kbase - qrow + P.Sq - 1 - lut_base);
-    // (no saturated-tile fast path here, unlike the backward kernels: with dropout hashing in this loop the
-    // scalar-bias body measured 12 % SLOWER than the LUT body, profiles/r1_attn_bench_v7_sat.jsonl)
+    // saturated tile (every LUT index of the wave's 32 rows x 64 keys in one constant-bias range): a scalar
+    // bias, no LDS lookups.  One wave-uniform branch around two fully unrolled bodies.
+    const int sat = !HAS_BIAS ? 0
+                    : (kbase + FWD_BN - 1 - qw0 + P.Sq - 1 <= P.sat_lo ? 1
+                       : (kbase - qw0 - 31 + P.Sq - 1 >= P.sat_hi ? 2 : 0));
+    auto bias_scale = [&](auto use_lut, float cbias) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int kl0 = crow(i, hh), kl1 = 32 + kl0;
-      float v0 = s0[i] * sl2, v1 = s1[i] * sl2;
-      if (HAS_BIAS) {
-        v0 += lb[kl0];
-        v1 += lb[kl1];
+      for (int i = 0; i < 16; ++i) {
+        const int kl0 = crow(i, hh), kl1 = 32 + kl0;
+        float v0, v1;
+        if constexpr (decltype(use_lut)::value) {
+          v0 = s0[i] * sl2 + lb[kl0];
+          v1 = s1[i] * sl2 + lb[kl1];
+        } else {
+          v0 = s0[i] * sl2 + cbias;
+          v1 = s1[i] * sl2 + cbias;
+        }
+        if (CAUSAL) {
+          v0 = (tile_causal && kl0 > climit) ? -INFINITY : v0;
+          v1 = (tile_causal && kl1 > climit) ? -INFINITY : v1;
+        }
+        s0[i] = v0;
+        s1[i] = v1;
       }
-      if (CAUSAL) {
-        v0 = (tile_causal && kl0 > climit) ? -INFINITY : v0;
-        v1 = (tile_causal && kl1 > climit) ? -INFINITY : v1;
-      }
-      s0[i] = v0;
-      s1[i] = v1;
-    }
+    };
+    if (HAS_BIAS && sat == 0) bias_scale(std::true_type{}, 0.f);
+    else bias_scale(std::false_type{}, sat == 1 ? c_lo : (sat == 2 ? c_hi : 0.f));
     // key mask (padding / past Sk): one uniform branch per tile around 8 vector LDS reads; a per-score `if`
     // made the compiler emit 16 branches each ending in s_waitcnt lgkmcnt(0)
     if ((HAS_KPM || kbase + FWD_BN > P.Sk) && tflag[kt] != 0) {

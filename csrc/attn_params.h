@@ -38,7 +38,7 @@ struct AttnParams {
   uint32_t* dmask;  // [B*H][n_ktiles][2][sq_pad] dropout keep bits written by fwd, read by bwd
   int dmask_ready;  // fwd: planes already generated (attn_dropout_mask) -> read instead of hash
   // Saturated bias ranges (T5 relative buckets): LUT entries [0, sat_lo] all equal lut[0] and [sat_hi, L) all
-  // equal lut[L-1], and the LUT gradient is only consumed per bucket.  A backward (dQ, dK/dV) tile whose LUT
+  // equal lut[L-1], and the LUT gradient is only consumed per bucket.  A (forward, dQ, dK/dV) tile whose LUT
   // indices all fall in one range adds a scalar bias (no LDS lookups) and its dS sum is credited to lut[0] /
   // lut[L-1] (no diagonal shear).  Disabled: sat_lo = INT_MIN / 2, sat_hi = INT_MAX / 2.
   int sat_lo;

@@ -142,8 +142,9 @@ class _AttnFn(torch.autograd.Function):
             dmask_in.record_stream(cur)
         sat = getattr(lut, "_dllm_sat", None) if lut is not None else None
         sat_lo, sat_hi = sat if sat is not None else (-1, -1)
+        fsat = os.environ.get("DLLM_ATTN_FWD_SAT", "1") == "1"  # forward scalar-bias tiles (A/B knob, -2 %)
         o, lse, dmask = C.attn_fwd(q, k, v, kpm, lut, float(scale), bool(causal), float(p), int(seed), dmask_in,
-                                   sat_lo, sat_hi)
+                                   sat_lo if fsat else -1, sat_hi if fsat else -1)
         ctx.save_for_backward(a, b, c, o, lse, lut, kpm, dmask)
         ctx.cfg = (mode, scale, causal, p, seed, lut is not None and lut.requires_grad, sat_lo, sat_hi)
         # ops/linear.py stacked_linear: the packed kv is a slice of a multi-layer projection and its
