@@ -31,7 +31,7 @@ def timeit(fn, iters):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--variants", default="4,5")
+    ap.add_argument("--variants", default="3,4")
     a = ap.parse_args()
     tunableop.enable(0)
     C = _ext.native()
