@@ -2,7 +2,9 @@
 // Host-side validation lives here: every shape / dtype / stride / alignment a kernel assumes is checked
 // BEFORE launch (a kernel that faults can reset every GPU on the node), then the C-ABI launchers in
 // csrc/*.hip run on the current torch HIP stream.
+#include <algorithm>
 #include <climits>
+#include <cstdlib>
 
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
@@ -469,9 +471,9 @@ int64_t gemm_wgrad(const Tensor& a, const Tensor& b, Tensor& c, bool beta, int64
 // forwards also write the pre-activation to aux_out; the backward epilogues read aux (saved activation for
 // d-relu, pre-activation for d-gelu) and apply the matching dropout backward.
 int64_t gemm_fused_variant(int64_t K) {
-  // 16x16x32 MFMA, BK = 64, 2 stages, both k-steps' fragments read up front: fastest on every T5 / BART FFN shape
-  // measured (profiles/r1_gemm_fused_bench*.jsonl: 8-25 % over the 32x32x16 variants, then up to -12 % more)
-  return K % 64 == 0 ? 4 : 1;
+  // ping-pong kernel (16x16x32 MFMA, BK = 64, two wave rows one barrier apart): fastest on every T5 / BART shape
+  // measured (profiles/r1_gemm_*_bench*.jsonl, r1_gemm_experiments.md); K % 64 != 0: BK = 32 x 4 stages
+  return K % 64 == 0 ? 8 : 1;
 }
 
 bool gemm_fused_supported(const Tensor& a, const Tensor& b, bool b_kmajor) {
@@ -544,8 +546,12 @@ Tensor gemm_fused(const Tensor& a, const Tensor& b, bool b_kmajor, int64_t epi, 
     const double t = p * 65536.0;
     P.thr = t >= 65535.0 ? 0xFFFFu : (uint32_t)t;
   }
+  {  // tile-order group size of the ping-pong kernel (read per call so microbenchmarks can A/B it in one process)
+    const char* e = std::getenv("DLLM_GEMM_GRP");
+    P.grp = e ? std::max(0, std::atoi(e)) : 4;  // 4: +1-3 % over row-major (profiles/r1_gemm_experiments.md)
+  }
   const int v = variant >= 0 ? (int)variant : (int)gemm_fused_variant(K);
-  TORCH_CHECK(v >= 0 && v <= 4, "gemm_fused: bad variant ", v);
+  TORCH_CHECK(v >= 0 && v <= 8, "gemm_fused: bad variant ", v);
   check_rc(dllm_gemm_fused(&P, b_kmajor ? 1 : 0, v, stream()), "gemm_fused");
   return out;
 }

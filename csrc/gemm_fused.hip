@@ -28,6 +28,8 @@
 // * bijective XCD remap of the 1-D grid, tiles of one 256-row block of A consecutive (L2 reuse of A).
 #include "common.h"
 
+#include <type_traits>
+
 using namespace dllm;
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8v;
@@ -80,12 +82,18 @@ DLLM_DEVICE bf16x8v frag_km16(const uint16_t* T, int kk, int cb, int lane) {
 }
 
 // ---- row-major [256][BK] image (k contiguous)
-template <int BK>
+// S16 (BK = 32 with 16x16x32 fragments): a ds_read_b128 lane group of frag16 touches rows {0-3, 12-15} at chunk c and
+// rows 4-11 at chunk c^1 (rows 16 apart repeat the pattern); with 4 rows per 256-B bank row, chunk c ^ (2 * bit 3 of r)
+// puts those 16 reads on 16 distinct bank slots (the BK = 32 32x32x16 swizzle (r / 4) & 3 would 2-way conflict).
+template <int BK, bool S16 = false>
 struct RowImg {
   static constexpr int CPR = BK / 8;          // 16-B chunks per row
   static constexpr int RPB = 256 / (BK * 2);  // rows per 256-B bank row
   static constexpr int RPI = 1024 / (BK * 2); // rows per 1-KB DMA wave-instruction
-  static DLLM_DEVICE int swz(int r) { return (r / RPB) & (CPR - 1); }
+  static DLLM_DEVICE int swz(int r) {
+    if constexpr (S16 && BK == 32) return ((r >> 3) & 1) << 1;
+    else return (r / RPB) & (CPR - 1);
+  }
   // 32x32x16 operand: lane l holds row cb + (l & 31), k = kk + 8 (l >> 5) + 0..7
   static DLLM_DEVICE bf16x8v frag(const uint16_t* T, int kk, int cb, int lane) {
     const int r = cb + (lane & 31);
@@ -163,11 +171,11 @@ template <int BK, int NBUF, bool BKM, int EPI, int MF, bool PRE = false>
 __global__ __launch_bounds__(NT, 1) void gemm_fused_kernel(GemmFusedParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint16_t* lds = reinterpret_cast<uint16_t*>(smem);  // [NBUF][A image | B image], BK*256 elements each
-  using RI = RowImg<BK>;
+  using RI = RowImg<BK, MF == 16>;
   constexpr int TILE = BK * 256;
   constexpr int PW = BK / 16;  // 1-KB DMA instructions per wave per operand per stage
   constexpr int LPS = 2 * PW;
-  static_assert(NBUF >= 2 && NBUF <= 4, "ring depth");
+  static_assert(NBUF >= 2 && NBUF <= 5 && NBUF * 2 * TILE * 2 <= 160 * 1024, "ring depth");
 
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, hh = lane >> 5;
   const int wm = w >> 2, wn = w & 3;
@@ -214,7 +222,8 @@ __global__ __launch_bounds__(NT, 1) void gemm_fused_kernel(GemmFusedParams P) {
   // buffer about to be refilled; then the refill of that buffer is issued
   auto stage_sync = [&](int it) {
     const int ahead = min(NBUF - 2, nk - 1 - it);
-    if (NBUF >= 4 && ahead >= 2) wait_vm<(NBUF >= 4 ? 2 * LPS : 0)>();
+    if (NBUF >= 5 && ahead >= 3) wait_vm<(NBUF >= 5 ? 3 * LPS : 0)>();
+    else if (NBUF >= 4 && ahead >= 2) wait_vm<(NBUF >= 4 ? 2 * LPS : 0)>();
     else if (NBUF >= 3 && ahead >= 1) wait_vm<(NBUF >= 3 ? LPS : 0)>();
     else wait_vm<0>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -283,7 +292,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_fused_kernel(GemmFusedParams P) {
           epilogue4<EPI>(P, mrow + 32 * i, n0 + wn * 64 + 32 * j + 8 * g + 4 * hh, v + bv[j][g]);
         }
   } else {
-    static_assert(MF == 16 && BK == 64, "16x16x32 fragments are bank-conflict free on the BK = 64 images only");
+    static_assert(MF == 16 && (BK == 64 || BK == 32) && (!PRE || BK == 64), "16x16x32 images: BK = 64, or 32 (S16)");
     f32x4 acc[8][4];
 #pragma unroll
     for (int i = 0; i < 8; ++i)
@@ -339,6 +348,248 @@ __global__ __launch_bounds__(NT, 1) void gemm_fused_kernel(GemmFusedParams P) {
   }
 }
 
+// ---- ping-pong kernel (variant 8; NT: A [M][K], B [N][K], both k-contiguous; BKM: B [K][N]) -----------------------
+// Same 256x256 tile, 8 waves as 2(M) x 4(N), 16x16x32 MFMA, BK = 64 double-buffered [256][64] images (128 KB), but the
+// k-tile is cut into 4 PHASES, one per 64x32 quadrant of a wave's 128x64 output (16 MFMAs each), and the two wave
+// rows (wm = 0 / 1, one wave of each on every SIMD) run one barrier apart:
+//
+//   wave row 0:  | L(P)  |b| M(P)  |b| L(P+1) |b| M(P+1) |b| ...     L = ds_reads of the phase's fragments, one
+//   wave row 1:  |b| ... | L(P)   |b| M(P)   |b| L(P+1)  |b| ...         8-KB DMA unit pair, counted vmcnt
+//                                                                    M = 16 MFMAs of the quadrant
+// so on every SIMD one wave's MFMAs cover the other wave's LDS reads and DMA issue (MI355X_MICROARCH.md: two
+// waves per SIMD, MFMA and LDS pipes independent).  Quadrants run (m0,n0) (m0,n1) (m1,n1) (m1,n0): phase 0 reads the
+// top 64 A rows + the n0 B fragments, phase 1 the n1 B fragments, phase 2 the bottom A rows, phase 3 nothing.
+//
+// DMA units: a k-tile is 8 units of 64 image rows (8 KB, one global_load_lds_dwordx4 per thread):
+//   U0 A 0-63 | U1 A 128-191 | U2 B {0-31, 64-95} | U3 B {128-159, 192-223} | U4 B {32-63, 96-127} | U5 B {160-191,
+//   224-255} | U6 A 64-127 | U7 A 192-255          (first read in phase 0, 0, 0, 0, 1, 1, 2, 2)
+// Phase q of k-tile kt issues U4,U5 (q = 0) / U6,U7 (q = 1) of kt + 1 and U0,U1 (q = 2) / U2,U3 (q = 3) of kt + 2, then
+// waits until everything issued 4 or more phases ago has landed (vmcnt = glds issued in the last 4 phases).  Every
+// unit is issued >= 5 phases before its read (RAW: the wait sits in the L section before the read phase's barrier)
+// and >= 2 phases after the previous read of its slot (WAR: the reads retire by lgkmcnt before the next barrier).
+//
+// BKM (dgrad, B = [K][N] k-major, [64][256] image with transposed reads): every quadrant's B fragments span all 64
+// k-rows, so phase 0 reads both n0 and n1 B fragments and the B units are k-row quarters (16 rows x 512 B):
+//   U0 A 0-63 | U1 A 128-191 | Bk0..Bk3 | U6 A 64-127 | U7 A 192-255 (first read 0, 0, 0 x 4, 2, 2).  Issue:
+//   q0 U6 (kt + 1), q1 U7 (kt + 1), q2 U0, U1, Bk0 (kt + 2), q3 Bk1-3 (kt + 2) -> 1 + 1 + 3 + 3 = 8 glds per 4 phases, so the
+//   same vmcnt(8) rule retires every unit >= 1 phase before its read, and every refill is >= 2 phases after its last read.
+template <int EPI, bool BKM>
+__global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(GemmFusedParams P) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint16_t* lds = reinterpret_cast<uint16_t*>(smem);  // [2][A image | B image], [256][64] each
+  using RI = RowImg<64>;
+  constexpr int TILE = 64 * 256;
+
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int wm = w >> 2, wn = w & 3;
+  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  int mb = t / P.tn, nb = t % P.tn;
+  if (P.grp > 0) {  // the 32 tiles an XCD runs at once cover a grp x (32 / grp) block of tiles (L2 reuse of A and B)
+    const int gs = P.grp * P.tn, g = t / gs, r = t % gs;
+    const int rows = min(P.grp, P.tm - g * P.grp);
+    mb = g * P.grp + r % rows;
+    nb = r / rows;
+  }
+  const int m0 = mb * BM, n0 = nb * BN;
+  const int nk = P.K / 64;
+
+  // per-thread DMA source rows: A units are 64 contiguous rows, B units two 32-row segments 64 apart.  Unit bases are
+  // multiples of 16 rows and the swizzle (r / 2) & 7 depends on r mod 16 only, so one chunk offset serves all units.
+  const int ra = 8 * w + (lane >> 3);
+  const int rb = (w < 4 ? 0 : 64) + 8 * (w & 3) + (lane >> 3);
+  const int cs = ((lane & 7) ^ RI::swz(ra)) * 8;
+  const uint16_t* Ag = P.A + (long)(m0 + ra) * P.lda + cs;
+  // k-major B: wave-instruction w of a 16-row unit covers k-rows 2w, 2w+1; lane -> (row 2w + lane/32, chunk lane%32),
+  // chunk pre-swizzled by gsw (depends on k-row mod 16 only)
+  const int kr = 2 * w + (lane >> 5);
+  const uint16_t* Bg = BKM ? P.B + (long)kr * P.ldb + n0 + (((lane & 31) ^ gsw(kr)) << 3)
+                           : P.B + (long)(n0 + rb) * P.ldb + cs;
+  const uint32_t lds0 = lds_addr(lds);
+  const uint32_t la = (uint32_t)(8 * w) * 128u;                              // wave's first image row, A units
+  const uint32_t lb = (uint32_t)((w < 4 ? 0 : 64) + 8 * (w & 3)) * 128u;     // B units
+  auto unitA = [&](int base, int kt) {
+    const uint32_t dst = lds0 + (uint32_t)((kt & 1) * 2 * TILE) * 2u + (uint32_t)base * 128u + la;
+    glds16(Ag + (long)base * P.lda + kt * 64, __builtin_amdgcn_readfirstlane(dst));
+  };
+  auto unitB = [&](int base, int kt) {
+    const uint32_t dst = lds0 + (uint32_t)((kt & 1) * 2 * TILE + TILE) * 2u + (uint32_t)base * 128u + lb;
+    glds16(Bg + (long)base * P.ldb + kt * 64, __builtin_amdgcn_readfirstlane(dst));
+  };
+  auto unitBk = [&](int u, int kt) {  // k-rows 16u .. 16u+15 of k-tile kt
+    const uint32_t dst = lds0 + (uint32_t)((kt & 1) * 2 * TILE + TILE) * 2u + (uint32_t)(16 * u + 2 * w) * 512u;
+    glds16(Bg + (long)(kt * 64 + 16 * u) * P.ldb, __builtin_amdgcn_readfirstlane(dst));
+  };
+  auto issue_units = [&](int q, int k) {
+    if constexpr (BKM) {
+      switch (q) {
+        case 0: unitA(64, k); break;
+        case 1: unitA(192, k); break;
+        case 2: unitA(0, k); unitA(128, k); unitBk(0, k); break;
+        default: unitBk(1, k); unitBk(2, k); unitBk(3, k); break;
+      }
+    } else {
+      switch (q) {
+        case 0: unitB(32, k); unitB(160, k); break;
+        case 1: unitA(64, k); unitA(192, k); break;
+        case 2: unitA(0, k); unitA(128, k); break;
+        default: unitB(0, k); unitB(128, k); break;
+      }
+    }
+  };
+  auto units_of = [](int q) { return BKM ? (q < 2 ? 1 : 3) : 2; };
+  // phase p (p = 4 kt + q, p >= -6) issues the unit pair of k-tile tgt(p); returns glds issued per thread
+  auto tgt = [](int p) { return (p >> 2) + ((p & 3) < 2 ? 1 : 2); };
+  auto issue = [&](int p) {
+    const int k = tgt(p);
+    if (k < nk) issue_units(p & 3, k);
+  };
+  // after phase p's issue: retire everything issued at phases <= p - 4
+  auto retire = [&](int p) {
+    int n = 0;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) n += tgt(p - d) < nk ? units_of((p - d) & 3) : 0;
+    switch (n) {
+      case 8: wait_vm<8>(); break;
+      case 7: wait_vm<7>(); break;
+      case 6: wait_vm<6>(); break;
+      case 5: wait_vm<5>(); break;
+      case 4: wait_vm<4>(); break;
+      case 3: wait_vm<3>(); break;
+      case 2: wait_vm<2>(); break;
+      case 1: wait_vm<1>(); break;
+      default: wait_vm<0>(); break;
+    }
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8v a[4][2], b0[2][2], b1[2][2];
+
+  // prologue: phases -6 .. -1 (issue only), then one barrier for everybody and the one-barrier stagger of wave row 1
+#pragma unroll
+  for (int p = -6; p < 0; ++p) issue(p);
+  retire(-1);
+  __builtin_amdgcn_s_barrier();
+  if (wm == 1) __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+
+  auto sync_l = [&]() {  // end of an L section
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto sync_m = [&]() {  // end of an M section
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto quad = [&](int qm, int qn, const bf16x8v (&bb)[2][2]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[4 * qm + i][2 * qn + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(bb[j][ks], a[i][ks], acc[4 * qm + i][2 * qn + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // one k-tile = 4 phases; FULL: every unit of the phase exists (kt + 2 < nk) -> unconditional issue, vmcnt(8)
+  auto ktile = [&](int kt, auto full) {
+    constexpr bool FULL = decltype(full)::value;
+    const uint16_t* As = lds + (kt & 1) * 2 * TILE;
+    const uint16_t* Bs = As + TILE;
+    const int p0 = 4 * kt;
+    auto iss = [&](int p) {
+      if constexpr (FULL) {
+        issue_units(p & 3, tgt(p));
+        wait_vm<8>();
+      } else {
+        issue(p);
+        retire(p);
+      }
+    };
+    // phase 0: quadrant (m0, n0)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i][ks] = RI::frag16(As, 32 * ks, wm * 128 + 16 * i, lane);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        if constexpr (BKM) {
+          b0[j][ks] = frag_km16(Bs, 32 * ks, wn * 64 + 16 * j, lane);
+          b1[j][ks] = frag_km16(Bs, 32 * ks, wn * 64 + 32 + 16 * j, lane);
+        } else {
+          b0[j][ks] = RI::frag16(Bs, 32 * ks, wn * 64 + 16 * j, lane);
+        }
+      }
+    }
+    iss(p0);
+    sync_l();
+    quad(0, 0, b0);
+    sync_m();
+    // phase 1: quadrant (m0, n1)
+    if constexpr (!BKM) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) b1[j][ks] = RI::frag16(Bs, 32 * ks, wn * 64 + 32 + 16 * j, lane);
+    }
+    iss(p0 + 1);
+    sync_l();
+    quad(0, 1, b1);
+    sync_m();
+    // phase 2: quadrant (m1, n1)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i][ks] = RI::frag16(As, 32 * ks, wm * 128 + 64 + 16 * i, lane);
+    iss(p0 + 2);
+    sync_l();
+    quad(1, 1, b1);
+    sync_m();
+    // phase 3: quadrant (m1, n0), no reads
+    iss(p0 + 3);
+    sync_l();
+    quad(1, 0, b0);
+    sync_m();
+  };
+  int kt = 0;
+  for (; kt + 2 < nk; ++kt) ktile(kt, std::true_type{});
+  for (; kt < nk; ++kt) ktile(kt, std::false_type{});
+  if (wm == 0) __builtin_amdgcn_s_barrier();  // undo the stagger: every wave has passed the same number of barriers
+
+  // epilogue: acc[i][j][0..3] = C[m0 + wm*128 + 16i + (lane & 15)][n0 + wn*64 + 16j + 4 (lane >> 4) + 0..3]
+  const int mrow = m0 + wm * 128 + (lane & 15);
+  const int ncol = n0 + wn * 64 + 4 * (lane >> 4);
+  f32x4 bv[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) bv[j] = P.bias ? load4(P.bias + ncol + 16 * j) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) epilogue4<EPI>(P, mrow + 16 * i, ncol + 16 * j, acc[i][j] + bv[j]);
+}
+
+template <int EPI, bool BKM>
+int launch_pp(const GemmFusedParams& p, hipStream_t st) {
+  const size_t lds = (size_t)2 * 2 * 64 * 256 * 2;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<EPI, BKM>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+    attr = true;
+  }
+  hipLaunchKernelGGL((gemm_pp_kernel<EPI, BKM>), dim3(p.tm * p.tn), dim3(NT), lds, st, p);
+  DLLM_CHECK_LAUNCH();
+  return 0;
+}
+
 template <int BK, int NBUF, bool BKM, int EPI, int MF, bool PRE = false>
 int launch(const GemmFusedParams& p, hipStream_t st) {
   const size_t lds = (size_t)NBUF * 2 * BK * 256 * 2;
@@ -360,6 +611,10 @@ int launch_v(const GemmFusedParams& p, int variant, hipStream_t st) {
     case 2: return launch<32, 3, BKM, EPI, 32>(p, st);
     case 3: return launch<64, 2, BKM, EPI, 16>(p, st);
     case 4: return launch<64, 2, BKM, EPI, 16, true>(p, st);
+    case 5: return launch<32, 3, BKM, EPI, 16>(p, st);
+    case 6: return launch<32, 4, BKM, EPI, 16>(p, st);
+    case 7: return launch<32, 5, BKM, EPI, 16>(p, st);
+    case 8: return launch_pp<EPI, BKM>(p, st);
     default: return launch<64, 2, BKM, EPI, 32>(p, st);
   }
 }
@@ -381,10 +636,12 @@ int dispatch_epi(const GemmFusedParams& p, int variant, hipStream_t st) {
 }  // namespace
 
 // variant: 0 = BK64 x 2 stages, 1 = BK32 x 4 stages, 2 = BK32 x 3 stages (all 128 / 96 KB LDS, 32x32x16 MFMA),
-// 3 = BK64 x 2 stages with 16x16x32 MFMA, 4 = variant 3 with both k-steps' fragments read up front
+// 3 = BK64 x 2 stages with 16x16x32 MFMA, 4 = variant 3 with both k-steps' fragments read up front,
+// 5 / 6 / 7 = BK32 x 3 / 4 / 5 stages with 16x16x32 MFMA (96 / 128 / 160 KB: 1-3 stages in flight behind the one
+// being read), 8 = ping-pong kernel gemm_pp_kernel
 extern "C" int dllm_gemm_fused(const GemmFusedParams* pp, int b_kmajor, int variant, hipStream_t st) {
   const GemmFusedParams& p = *pp;
-  const int bk = (variant == 0 || variant >= 3) ? 64 : 32;
+  const int bk = (variant == 0 || variant == 3 || variant == 4 || variant == 8) ? 64 : 32;
   if (p.M % BM || p.N % BN || p.K <= 0 || p.K % bk || p.tm * BM != p.M || p.tn * BN != p.N) return -4;
   return b_kmajor ? dispatch_epi<true>(p, variant, st) : dispatch_epi<false>(p, variant, st);
 }

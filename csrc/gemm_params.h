@@ -31,4 +31,5 @@ struct GemmFusedParams {
   float p;     // dropout probability on the activation output (forward element index m * N + n)
   float scale; // 1 / (1 - p), or 1
   uint32_t seed, thr;
+  int grp;     // tile order (gemm_pp_kernel): groups of grp 256-row blocks, column-major inside a group; 0 = row-major
 };

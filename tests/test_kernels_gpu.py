@@ -319,7 +319,7 @@ _EPI_FWD = {None: 0, "relu": 1, "gelu": 2, "gelu_new": 5}
 _EPI_BWD = {"relu": 3, "gelu": 4, "gelu_new": 6}
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8])
 @pytest.mark.parametrize("act,p,bias", [(None, 0.0, False), ("relu", 0.1, False), ("gelu", 0.0, True),
                                         ("gelu_new", 0.1, True)])
 def test_gemm_fused_forward(variant, act, p, bias):
@@ -345,7 +345,7 @@ def test_gemm_fused_forward(variant, act, p, bias):
         assert _rel(aux, u) < 1e-2
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8])
 @pytest.mark.parametrize("act,p", [("relu", 0.1), ("relu", 0.0), ("gelu", 0.1), ("gelu_new", 0.0)])
 def test_gemm_fused_backward(variant, act, p):
     """dU = act'(U) * dropout'(dY Wo) with Wo k-major ([d, F]) vs fp32 autograd of the same composite."""
@@ -365,6 +365,32 @@ def test_gemm_fused_backward(variant, act, p):
     (activations._act_ref(uf, act) * keep).backward(dy.float() @ wo.float())
     assert _rel(du, uf.grad) < 1e-2, _rel(du, uf.grad)
     _close(du, uf.grad, 2e-2, 2e-2, "fused bwd")
+
+
+@pytest.mark.parametrize("variant", [4, 5, 7, 8])
+@pytest.mark.parametrize("K", [64, 128, 192, 320])
+def test_gemm_fused_short_k(variant, K):
+    """Pipeline prologue / tail paths: k-tile counts 1..5 (fewer k-tiles than the DMA ring holds)."""
+    torch.manual_seed(2)
+    M, N = 768, 512
+    C = _ext.native()
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) * K ** -0.5).to(torch.bfloat16)
+    h = C.gemm_fused(x, w, False, 0, None, None, None, 0.0, 1, variant)
+    _close(h, x.float() @ w.float().t(), 2e-2, 2e-2, "short-k")
+
+
+@pytest.mark.parametrize("grp", [1, 2, 3, 4, 8])
+def test_gemm_pp_tile_order_groups(grp, monkeypatch):
+    """Grouped tile order of the ping-pong kernel (DLLM_GEMM_GRP), including a last group shorter than grp."""
+    monkeypatch.setenv("DLLM_GEMM_GRP", str(grp))
+    torch.manual_seed(3)
+    M, K, N = 1280, 256, 768
+    C = _ext.native()
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) * K ** -0.5).to(torch.bfloat16)
+    h = C.gemm_fused(x, w, False, 1, None, None, None, 0.0, 1, 8)
+    _close(h, torch.relu(x.float() @ w.float().t()), 2e-2, 2e-2, "pp grouped order")
 
 
 def test_gemm_fused_rejects_unsupported_shapes():

@@ -32,10 +32,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--variants", default="3,4")
+    ap.add_argument("--phases", default="fwd,dgrad")
     a = ap.parse_args()
     tunableop.enable(0)
     C = _ext.native()
-    variants = [int(v) for v in a.variants.split(",")]
+    # a variant "8g4" runs variant 8 with DLLM_GEMM_GRP=4 (tile-order group size, read per call by the binding)
+    variants = a.variants.split(",")
     # (name, tokens M, in K, out N): t5-base at b=64 (enc 65536 tokens, dec 8192), bart-large at b=32
     shapes = [("t5b enc qkv", 65536, 768, 2304), ("t5b enc o", 65536, 768, 768), ("t5b enc wi", 65536, 768, 3072),
               ("t5b enc wo", 65536, 3072, 768), ("t5b dec qkv", 8192, 768, 2304), ("t5b dec o", 8192, 768, 768),
@@ -47,7 +49,7 @@ def main():
         w = (torch.randn(N, K, device="cuda") * K ** -0.5).to(torch.bfloat16)
         dy = torch.randn(M, N, device="cuda").to(torch.bfloat16)
         fl = 2.0 * M * K * N
-        for phase in ("fwd", "dgrad"):
+        for phase in a.phases.split(","):
             rec = {"shape": name, "phase": phase, "M": M, "K": K if phase == "fwd" else N, "N": N if phase == "fwd" else K}
             if phase == "fwd":
                 lib = lambda: F.linear(x, w)  # noqa: E731
@@ -62,13 +64,16 @@ def main():
             rec["lib_us"] = round(t * 1e6, 1)
             rec["lib_tflops"] = round(fl / t / 1e12, 1)
             if ok:
-                for v in variants:
-                    fn = mk(v)
+                for vi, v in enumerate(variants):
+                    tag = f"v{v}" + ("b" * variants[:vi].count(v))  # a repeated variant (A/B/A order) gets its own key
+                    vv, _, grp = v.partition("g")
+                    os.environ["DLLM_GEMM_GRP"] = grp or "0"
+                    fn = mk(int(vv))
                     out = fn().float()
-                    rec[f"v{v}_relerr"] = float(f"{((out - ref).norm() / ref.norm()).item():.2e}")
+                    rec[f"{tag}_relerr"] = float(f"{((out - ref).norm() / ref.norm()).item():.2e}")
                     t = timeit(fn, a.iters)
-                    rec[f"v{v}_us"] = round(t * 1e6, 1)
-                    rec[f"v{v}_tflops"] = round(fl / t / 1e12, 1)
+                    rec[f"{tag}_us"] = round(t * 1e6, 1)
+                    rec[f"{tag}_tflops"] = round(fl / t / 1e12, 1)
             print(json.dumps(rec), flush=True)
         del x, w, dy
         torch.cuda.empty_cache()
