@@ -471,9 +471,10 @@ int64_t gemm_wgrad(const Tensor& a, const Tensor& b, Tensor& c, bool beta, int64
 // forwards also write the pre-activation to aux_out; the backward epilogues read aux (saved activation for
 // d-relu, pre-activation for d-gelu) and apply the matching dropout backward.
 int64_t gemm_fused_variant(int64_t K) {
-  // ping-pong kernel (16x16x32 MFMA, BK = 64, two wave rows one barrier apart): fastest on every T5 / BART shape
-  // measured (profiles/r1_gemm_*_bench*.jsonl, r1_gemm_experiments.md); K % 64 != 0: BK = 32 x 4 stages
-  return K % 64 == 0 ? 8 : 1;
+  // ping-pong kernel (16x16x32 MFMA, BK = 64, two wave rows one barrier apart), persistent for store-only epilogues:
+  // fastest on every T5 / BART shape measured (profiles/r1_gemm_*_bench*.jsonl, r1_gemm_experiments.md);
+  // K % 64 != 0: BK = 32 x 4 stages
+  return K % 64 == 0 ? 9 : 1;
 }
 
 bool gemm_fused_supported(const Tensor& a, const Tensor& b, bool b_kmajor) {
@@ -551,7 +552,7 @@ Tensor gemm_fused(const Tensor& a, const Tensor& b, bool b_kmajor, int64_t epi, 
     P.grp = e ? std::max(0, std::atoi(e)) : 4;  // 4: +1-3 % over row-major (profiles/r1_gemm_experiments.md)
   }
   const int v = variant >= 0 ? (int)variant : (int)gemm_fused_variant(K);
-  TORCH_CHECK(v >= 0 && v <= 8, "gemm_fused: bad variant ", v);
+  TORCH_CHECK(v >= 0 && v <= 9, "gemm_fused: bad variant ", v);
   check_rc(dllm_gemm_fused(&P, b_kmajor ? 1 : 0, v, stream()), "gemm_fused");
   return out;
 }

@@ -44,6 +44,24 @@ constexpr int BM = 256, BN = 256, NT = 512;
 enum Epi { EPI_NONE = 0, EPI_RELU = 1, EPI_GELU = 2, EPI_DRELU = 3, EPI_DGELU = 4, EPI_GELU_TANH = 5,
            EPI_DGELU_TANH = 6 };
 
+// LDS-DMA through a buffer descriptor: 16 B per lane from base + voff (bytes) to LDS lds_byte + 16 * lane.  base is
+// wave-uniform (SGPRs); num_records = 2^32 - 1, so voff only has to stay below 4 GB.  soffset = 0 (on gfx950 the LDS
+// form is used with a zero wave offset, as composable_kernel does).
+typedef __attribute__((ext_vector_type(4))) int i32x4;
+extern "C" __device__ void llvm_amdgcn_raw_buffer_load_lds(i32x4 rsrc, __attribute__((address_space(3))) uint32_t* lds,
+                                                           int size, int voffset, int soffset, int offset,
+                                                           int aux) __asm("llvm.amdgcn.raw.buffer.load.lds");
+DLLM_DEVICE void bld16(const void* base, uint32_t voff, uint32_t lds_byte) {
+  const uint64_t a = (uint64_t)base;
+  i32x4 r;
+  r.x = (int)(uint32_t)a;
+  r.y = (int)((uint32_t)(a >> 32) & 0xFFFFu);
+  r.z = -1;
+  r.w = 0x00020000;
+  llvm_amdgcn_raw_buffer_load_lds(r, (__attribute__((address_space(3))) uint32_t*)(uintptr_t)lds_byte, 16, (int)voff, 0,
+                                  0, 0);
+}
+
 DLLM_DEVICE int xcd_remap(int bid, int nblk) {
   const int q = nblk / 8, r = nblk % 8, x = bid % 8;
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
@@ -373,51 +391,109 @@ __global__ __launch_bounds__(NT, 1) void gemm_fused_kernel(GemmFusedParams P) {
 //   U0 A 0-63 | U1 A 128-191 | Bk0..Bk3 | U6 A 64-127 | U7 A 192-255 (first read 0, 0, 0 x 4, 2, 2).  Issue:
 //   q0 U6 (kt + 1), q1 U7 (kt + 1), q2 U0, U1, Bk0 (kt + 2), q3 Bk1-3 (kt + 2) -> 1 + 1 + 3 + 3 = 8 glds per 4 phases, so the
 //   same vmcnt(8) rule retires every unit >= 1 phase before its read, and every refill is >= 2 phases after its last read.
-template <int EPI, bool BKM>
+//
+// PERSIST: one workgroup per CU walks tiles vt0, vt0 + vstep, ... (the 32 workgroups of an XCD on 32 consecutive
+// virtual tiles, grouped as above); the DMA unit stream runs on across tile boundaries (global k-tile counter), so the
+// next tile's first units are in flight while the wave rows run the previous tile's epilogue, each inside its own
+// L slot (covered by the other row's MFMAs).  The epilogue's NST stores sit in the vmcnt queue between units: the 4
+// phases after an epilogue wait for vmcnt(8 + NST) (an under-count when the epilogue also loads: conservative).
+template <int EPI, bool BKM, bool PERSIST>
 __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(GemmFusedParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint16_t* lds = reinterpret_cast<uint16_t*>(smem);  // [2][A image | B image], [256][64] each
   using RI = RowImg<64>;
   constexpr int TILE = 64 * 256;
+  constexpr int NST = (EPI == EPI_GELU || EPI == EPI_GELU_TANH) ? 64 : 32;  // vector stores per lane per epilogue
+  constexpr int VM_POST = 8 + NST <= 63 ? 8 + NST : 63;
 
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int wm = w >> 2, wn = w & 3;
-  const int t = xcd_remap(blockIdx.x, gridDim.x);
-  int mb = t / P.tn, nb = t % P.tn;
-  if (P.grp > 0) {  // the 32 tiles an XCD runs at once cover a grp x (32 / grp) block of tiles (L2 reuse of A and B)
-    const int gs = P.grp * P.tn, g = t / gs, r = t % gs;
-    const int rows = min(P.grp, P.tm - g * P.grp);
-    mb = g * P.grp + r % rows;
-    nb = r / rows;
-  }
-  const int m0 = mb * BM, n0 = nb * BN;
+  const int T = P.tm * P.tn;
   const int nk = P.K / 64;
+  int vt0, vstep, ntw;
+  if constexpr (PERSIST) {
+    const int G = gridDim.x, b = blockIdx.x, x = b % 8, slot = b / 8;
+    const int nwx = G / 8 + (x < G % 8 ? 1 : 0);
+    const int ntx = T / 8 + (x < T % 8 ? 1 : 0);
+    vt0 = x * (T / 8) + min(x, T % 8) + slot;
+    vstep = nwx;
+    ntw = slot < ntx ? (ntx - slot + nwx - 1) / nwx : 0;
+  } else {
+    vt0 = xcd_remap(blockIdx.x, gridDim.x);
+    vstep = 0;
+    ntw = 1;
+  }
+  if (ntw == 0) return;
+  auto tile_mn = [&](int i, int& tm0, int& tn0) {
+    const int t = vt0 + i * vstep;
+    int mb = t / P.tn, nb = t % P.tn;
+    if (P.grp > 0) {  // the 32 tiles an XCD runs at once cover a grp x (32 / grp) block of tiles (L2 reuse of A, B)
+      const int gs = P.grp * P.tn, g = t / gs, r = t % gs;
+      const int rows = min(P.grp, P.tm - g * P.grp);
+      mb = g * P.grp + r % rows;
+      nb = r / rows;
+    }
+    tm0 = mb * BM;
+    tn0 = nb * BN;
+  };
 
-  // per-thread DMA source rows: A units are 64 contiguous rows, B units two 32-row segments 64 apart.  Unit bases are
-  // multiples of 16 rows and the swizzle (r / 2) & 7 depends on r mod 16 only, so one chunk offset serves all units.
+  // per-thread DMA source offsets: A units are 64 contiguous rows, B units two 32-row segments 64 apart.  Unit bases
+  // are multiples of 16 rows and the swizzle (r / 2) & 7 depends on r mod 16 only, so one chunk offset serves all.
   const int ra = 8 * w + (lane >> 3);
   const int rb = (w < 4 ? 0 : 64) + 8 * (w & 3) + (lane >> 3);
   const int cs = ((lane & 7) ^ RI::swz(ra)) * 8;
-  const uint16_t* Ag = P.A + (long)(m0 + ra) * P.lda + cs;
   // k-major B: wave-instruction w of a 16-row unit covers k-rows 2w, 2w+1; lane -> (row 2w + lane/32, chunk lane%32),
   // chunk pre-swizzled by gsw (depends on k-row mod 16 only)
   const int kr = 2 * w + (lane >> 5);
-  const uint16_t* Bg = BKM ? P.B + (long)kr * P.ldb + n0 + (((lane & 31) ^ gsw(kr)) << 3)
-                           : P.B + (long)(n0 + rb) * P.ldb + cs;
+  // byte offsets of the thread's 16 B inside a unit: buffer_load ... lds with the unit's (scalar) base in the
+  // descriptor keeps the whole address computation in SGPRs (2 VGPRs of offsets instead of 64-bit pointers per unit)
+  const uint32_t offA = (uint32_t)(ra * P.lda + cs) * 2u;
+  const uint32_t offB = (uint32_t)(BKM ? kr * P.ldb + (((lane & 31) ^ gsw(kr)) << 3) : rb * P.ldb + cs) * 2u;
+  auto tile_a = [&](int tm0) { return P.A + (long)tm0 * P.lda; };
+  auto tile_b = [&](int tn0) { return BKM ? P.B + tn0 : P.B + (long)tn0 * P.ldb; };
+  int m0, n0, m1 = 0, n1 = 0;
+  tile_mn(0, m0, n0);
+  if (ntw > 1) tile_mn(1, m1, n1);
+  const uint16_t *a_cur = tile_a(m0), *b_cur = tile_b(n0), *a_nxt = tile_a(m1), *b_nxt = tile_b(n1);
+  int g_cur = 0;  // global k-tile index of the current tile's first k-tile
+  const int total = ntw * nk;
+
   const uint32_t lds0 = lds_addr(lds);
   const uint32_t la = (uint32_t)(8 * w) * 128u;                              // wave's first image row, A units
   const uint32_t lb = (uint32_t)((w < 4 ? 0 : 64) + 8 * (w & 3)) * 128u;     // B units
-  auto unitA = [&](int base, int kt) {
-    const uint32_t dst = lds0 + (uint32_t)((kt & 1) * 2 * TILE) * 2u + (uint32_t)base * 128u + la;
-    glds16(Ag + (long)base * P.lda + kt * 64, __builtin_amdgcn_readfirstlane(dst));
+  // global k-tile g -> (source tile bases, k-tile inside that tile); g is in the current or the next tile
+  // (PERSIST launches only with nk >= 2)
+  auto src = [&](int g, const uint16_t*& ab, const uint16_t*& bb) {
+    int loc = g - g_cur;
+    ab = a_cur;
+    bb = b_cur;
+    if (PERSIST && loc >= nk) {
+      loc -= nk;
+      ab = a_nxt;
+      bb = b_nxt;
+    }
+    // opaque to the optimizer: otherwise it hoists every unit's descriptor for both tiles out of the loops and runs
+    // out of SGPRs (spilling into VGPR lanes); rebuilding a descriptor costs a few SALU ops per unit
+    asm volatile("" : "+s"(ab), "+s"(bb));
+    return loc;
   };
-  auto unitB = [&](int base, int kt) {
-    const uint32_t dst = lds0 + (uint32_t)((kt & 1) * 2 * TILE + TILE) * 2u + (uint32_t)base * 128u + lb;
-    glds16(Bg + (long)base * P.ldb + kt * 64, __builtin_amdgcn_readfirstlane(dst));
+  auto unitA = [&](int base, int g) {
+    const uint16_t *ab, *bb;
+    const int kt = src(g, ab, bb);
+    const uint32_t dst = lds0 + (uint32_t)((g & 1) * 2 * TILE) * 2u + (uint32_t)base * 128u + la;
+    bld16(ab + (long)base * P.lda + kt * 64, offA, __builtin_amdgcn_readfirstlane(dst));
   };
-  auto unitBk = [&](int u, int kt) {  // k-rows 16u .. 16u+15 of k-tile kt
-    const uint32_t dst = lds0 + (uint32_t)((kt & 1) * 2 * TILE + TILE) * 2u + (uint32_t)(16 * u + 2 * w) * 512u;
-    glds16(Bg + (long)(kt * 64 + 16 * u) * P.ldb, __builtin_amdgcn_readfirstlane(dst));
+  auto unitB = [&](int base, int g) {
+    const uint16_t *ab, *bb;
+    const int kt = src(g, ab, bb);
+    const uint32_t dst = lds0 + (uint32_t)((g & 1) * 2 * TILE + TILE) * 2u + (uint32_t)base * 128u + lb;
+    bld16(bb + (long)base * P.ldb + kt * 64, offB, __builtin_amdgcn_readfirstlane(dst));
+  };
+  auto unitBk = [&](int u, int g) {  // k-rows 16u .. 16u+15 of global k-tile g
+    const uint16_t *ab, *bb;
+    const int kt = src(g, ab, bb);
+    const uint32_t dst = lds0 + (uint32_t)((g & 1) * 2 * TILE + TILE) * 2u + (uint32_t)(16 * u + 2 * w) * 512u;
+    bld16(bb + (long)(kt * 64 + 16 * u) * P.ldb, offB, __builtin_amdgcn_readfirstlane(dst));
   };
   auto issue_units = [&](int q, int k) {
     if constexpr (BKM) {
@@ -437,17 +513,33 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(GemmFusedParams P) {
     }
   };
   auto units_of = [](int q) { return BKM ? (q < 2 ? 1 : 3) : 2; };
-  // phase p (p = 4 kt + q, p >= -6) issues the unit pair of k-tile tgt(p); returns glds issued per thread
+  // phase p (p = 4 g + q, p >= -6) issues the units of global k-tile tgt(p)
   auto tgt = [](int p) { return (p >> 2) + ((p & 3) < 2 ? 1 : 2); };
   auto issue = [&](int p) {
     const int k = tgt(p);
-    if (k < nk) issue_units(p & 3, k);
+    if (k < total) issue_units(p & 3, k);
   };
-  // after phase p's issue: retire everything issued at phases <= p - 4
-  auto retire = [&](int p) {
+  // after phase p's issue: retire everything issued at phases <= p - 4; POST: an epilogue's NST stores are queued
+  // between those units and this phase's
+  auto retire = [&](int p, bool post) {
     int n = 0;
 #pragma unroll
-    for (int d = 0; d < 4; ++d) n += tgt(p - d) < nk ? units_of((p - d) & 3) : 0;
+    for (int d = 0; d < 4; ++d) n += tgt(p - d) < total ? units_of((p - d) & 3) : 0;
+    if (post) {
+      // units of phases p-3 .. p-1 + NST stores + units of phase p may stay queued; n counts the units only
+      switch (n) {
+        case 8: wait_vm<(8 + NST <= 63 ? 8 + NST : 63)>(); break;
+        case 7: wait_vm<(7 + NST <= 63 ? 7 + NST : 63)>(); break;
+        case 6: wait_vm<(6 + NST <= 63 ? 6 + NST : 63)>(); break;
+        case 5: wait_vm<(5 + NST <= 63 ? 5 + NST : 63)>(); break;
+        case 4: wait_vm<(4 + NST <= 63 ? 4 + NST : 63)>(); break;
+        case 3: wait_vm<(3 + NST <= 63 ? 3 + NST : 63)>(); break;
+        case 2: wait_vm<(2 + NST <= 63 ? 2 + NST : 63)>(); break;
+        case 1: wait_vm<(1 + NST <= 63 ? 1 + NST : 63)>(); break;
+        default: wait_vm<0>(); break;
+      }
+      return;
+    }
     switch (n) {
       case 8: wait_vm<8>(); break;
       case 7: wait_vm<7>(); break;
@@ -471,7 +563,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(GemmFusedParams P) {
   // prologue: phases -6 .. -1 (issue only), then one barrier for everybody and the one-barrier stagger of wave row 1
 #pragma unroll
   for (int p = -6; p < 0; ++p) issue(p);
-  retire(-1);
+  retire(-1, false);
   __builtin_amdgcn_s_barrier();
   if (wm == 1) __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
@@ -499,19 +591,21 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(GemmFusedParams P) {
     __builtin_amdgcn_s_setprio(0);
   };
 
-  // one k-tile = 4 phases; FULL: every unit of the phase exists (kt + 2 < nk) -> unconditional issue, vmcnt(8)
-  auto ktile = [&](int kt, auto full) {
+  // one k-tile = 4 phases.  FULL: every unit of the 4 phases exists (g + 2 < total) -> unconditional issue, fixed vmcnt;
+  // POST: first k-tile after an epilogue (its stores are queued between the units)
+  auto ktile = [&](int g, auto full, bool post) {
     constexpr bool FULL = decltype(full)::value;
-    const uint16_t* As = lds + (kt & 1) * 2 * TILE;
+    const uint16_t* As = lds + (g & 1) * 2 * TILE;
     const uint16_t* Bs = As + TILE;
-    const int p0 = 4 * kt;
+    const int p0 = 4 * g;
     auto iss = [&](int p) {
       if constexpr (FULL) {
         issue_units(p & 3, tgt(p));
-        wait_vm<8>();
+        if (PERSIST && post) wait_vm<VM_POST>();
+        else wait_vm<8>();
       } else {
         issue(p);
-        retire(p);
+        retire(p, PERSIST && post);
       }
     };
     // phase 0: quadrant (m0, n0)
@@ -559,33 +653,91 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(GemmFusedParams P) {
     quad(1, 0, b0);
     sync_m();
   };
-  int kt = 0;
-  for (; kt + 2 < nk; ++kt) ktile(kt, std::true_type{});
-  for (; kt < nk; ++kt) ktile(kt, std::false_type{});
-  if (wm == 0) __builtin_amdgcn_s_barrier();  // undo the stagger: every wave has passed the same number of barriers
 
   // epilogue: acc[i][j][0..3] = C[m0 + wm*128 + 16i + (lane & 15)][n0 + wn*64 + 16j + 4 (lane >> 4) + 0..3]
-  const int mrow = m0 + wm * 128 + (lane & 15);
-  const int ncol = n0 + wn * 64 + 4 * (lane >> 4);
-  f32x4 bv[4];
+  auto epilogue = [&](int tm0, int tn0) {
+    // opaque lane id: otherwise the per-thread parts of the 32 store addresses are hoisted out of the tile loop
+    // (PERSIST) and stay live through the main loop
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const int mrow = tm0 + wm * 128 + (ln & 15);
+    const int ncol = tn0 + wn * 64 + 4 * (ln >> 4);
+    f32x4 bv[4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) bv[j] = P.bias ? load4(P.bias + ncol + 16 * j) : f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < 4; ++j) bv[j] = P.bias ? load4(P.bias + ncol + 16 * j) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) epilogue4<EPI>(P, mrow + 16 * i, ncol + 16 * j, acc[i][j] + bv[j]);
+      for (int j = 0; j < 4; ++j) epilogue4<EPI>(P, mrow + 16 * i, ncol + 16 * j, acc[i][j] + bv[j]);
+  };
+
+  int g = 0;
+  for (int i = 0; i < ntw; ++i) {
+    // post: first k-tile after an epilogue
+    int kt = 0;
+    for (; kt < nk && g + 2 < total; ++kt, ++g) ktile(g, std::true_type{}, i > 0 && kt == 0);
+    for (; kt < nk; ++kt, ++g) ktile(g, std::false_type{}, i > 0 && kt == 0);
+    if (i + 1 < ntw) {  // PERSIST only: epilogue inside the staggered stream, then the next tile becomes current
+      __builtin_amdgcn_sched_barrier(0);
+      epilogue(m0, n0);
+      __builtin_amdgcn_sched_barrier(0);  // keep the accumulator reset (and the next fragments) after the epilogue
+#pragma unroll
+      for (int r = 0; r < 8; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[r][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+      __builtin_amdgcn_sched_barrier(0);
+      m0 = m1;
+      n0 = n1;
+      a_cur = a_nxt;
+      b_cur = b_nxt;
+      g_cur += nk;
+      if (i + 2 < ntw) {
+        tile_mn(i + 2, m1, n1);
+        a_nxt = tile_a(m1);
+        b_nxt = tile_b(n1);
+      }
+    }
+  }
+  if (wm == 0) __builtin_amdgcn_s_barrier();  // undo the stagger: every wave has passed the same number of barriers
+  epilogue(m0, n0);
 }
 
+int num_cus() {
+  static int n = [] {
+    int dev = 0, cus = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    return cus > 0 ? cus : 256;
+  }();
+  return n;
+}
+
+// persist: one workgroup per CU when there are >= 2 tiles per CU and >= 2 k-tiles per tile, for the store-only
+// epilogues (none / ReLU).  The others load (aux) or store twice (GELU pre-activation): their first load waits in order
+// behind the next tile's queued DMA units and the persistent form measured 7-17 % SLOWER there
+// (profiles/r1_gemm_experiments.md), so they keep one tile per workgroup.
 template <int EPI, bool BKM>
-int launch_pp(const GemmFusedParams& p, hipStream_t st) {
+int launch_pp(const GemmFusedParams& p, bool persist, hipStream_t st) {
   const size_t lds = (size_t)2 * 2 * 64 * 256 * 2;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<EPI, BKM>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
-    attr = true;
+  const int T = p.tm * p.tn, cus = num_cus() / 8 * 8;
+  constexpr bool light = EPI == EPI_NONE || EPI == EPI_RELU;
+  if (light && persist && cus >= 8 && T >= 2 * cus && p.K >= 128) {
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<EPI, BKM, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds);
+      attr = true;
+    }
+    hipLaunchKernelGGL((gemm_pp_kernel<EPI, BKM, true>), dim3(cus), dim3(NT), lds, st, p);
+  } else {
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<EPI, BKM, false>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      attr = true;
+    }
+    hipLaunchKernelGGL((gemm_pp_kernel<EPI, BKM, false>), dim3(T), dim3(NT), lds, st, p);
   }
-  hipLaunchKernelGGL((gemm_pp_kernel<EPI, BKM>), dim3(p.tm * p.tn), dim3(NT), lds, st, p);
   DLLM_CHECK_LAUNCH();
   return 0;
 }
@@ -614,7 +766,8 @@ int launch_v(const GemmFusedParams& p, int variant, hipStream_t st) {
     case 5: return launch<32, 3, BKM, EPI, 16>(p, st);
     case 6: return launch<32, 4, BKM, EPI, 16>(p, st);
     case 7: return launch<32, 5, BKM, EPI, 16>(p, st);
-    case 8: return launch_pp<EPI, BKM>(p, st);
+    case 8: return launch_pp<EPI, BKM>(p, false, st);
+    case 9: return launch_pp<EPI, BKM>(p, true, st);
     default: return launch<64, 2, BKM, EPI, 32>(p, st);
   }
 }
@@ -638,10 +791,10 @@ int dispatch_epi(const GemmFusedParams& p, int variant, hipStream_t st) {
 // variant: 0 = BK64 x 2 stages, 1 = BK32 x 4 stages, 2 = BK32 x 3 stages (all 128 / 96 KB LDS, 32x32x16 MFMA),
 // 3 = BK64 x 2 stages with 16x16x32 MFMA, 4 = variant 3 with both k-steps' fragments read up front,
 // 5 / 6 / 7 = BK32 x 3 / 4 / 5 stages with 16x16x32 MFMA (96 / 128 / 160 KB: 1-3 stages in flight behind the one
-// being read), 8 = ping-pong kernel gemm_pp_kernel
+// being read), 8 = ping-pong kernel gemm_pp_kernel, 9 = its persistent form
 extern "C" int dllm_gemm_fused(const GemmFusedParams* pp, int b_kmajor, int variant, hipStream_t st) {
   const GemmFusedParams& p = *pp;
-  const int bk = (variant == 0 || variant == 3 || variant == 4 || variant == 8) ? 64 : 32;
+  const int bk = (variant == 0 || variant == 3 || variant == 4 || variant >= 8) ? 64 : 32;
   if (p.M % BM || p.N % BN || p.K <= 0 || p.K % bk || p.tm * BM != p.M || p.tn * BN != p.N) return -4;
   return b_kmajor ? dispatch_epi<true>(p, variant, st) : dispatch_epi<false>(p, variant, st);
 }

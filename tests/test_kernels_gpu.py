@@ -319,7 +319,7 @@ _EPI_FWD = {None: 0, "relu": 1, "gelu": 2, "gelu_new": 5}
 _EPI_BWD = {"relu": 3, "gelu": 4, "gelu_new": 6}
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
 @pytest.mark.parametrize("act,p,bias", [(None, 0.0, False), ("relu", 0.1, False), ("gelu", 0.0, True),
                                         ("gelu_new", 0.1, True)])
 def test_gemm_fused_forward(variant, act, p, bias):
@@ -345,7 +345,7 @@ def test_gemm_fused_forward(variant, act, p, bias):
         assert _rel(aux, u) < 1e-2
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
 @pytest.mark.parametrize("act,p", [("relu", 0.1), ("relu", 0.0), ("gelu", 0.1), ("gelu_new", 0.0)])
 def test_gemm_fused_backward(variant, act, p):
     """dU = act'(U) * dropout'(dY Wo) with Wo k-major ([d, F]) vs fp32 autograd of the same composite."""
@@ -367,7 +367,7 @@ def test_gemm_fused_backward(variant, act, p):
     _close(du, uf.grad, 2e-2, 2e-2, "fused bwd")
 
 
-@pytest.mark.parametrize("variant", [4, 5, 7, 8])
+@pytest.mark.parametrize("variant", [4, 5, 7, 8, 9])
 @pytest.mark.parametrize("K", [64, 128, 192, 320])
 def test_gemm_fused_short_k(variant, K):
     """Pipeline prologue / tail paths: k-tile counts 1..5 (fewer k-tiles than the DMA ring holds)."""
@@ -391,6 +391,30 @@ def test_gemm_pp_tile_order_groups(grp, monkeypatch):
     w = (torch.randn(N, K, device=DEV) * K ** -0.5).to(torch.bfloat16)
     h = C.gemm_fused(x, w, False, 1, None, None, None, 0.0, 1, 8)
     _close(h, torch.relu(x.float() @ w.float().t()), 2e-2, 2e-2, "pp grouped order")
+
+
+@pytest.mark.parametrize("K", [128, 192, 768])
+@pytest.mark.parametrize("kmajor", [False, True])
+def test_gemm_pp_persistent(K, kmajor):
+    """Persistent ping-pong kernel (variant 9: one workgroup per CU walking >= 2 tiles, the DMA stream running across
+    tile boundaries, epilogue stores queued between units): 528 tiles (uneven per CU), relu+dropout forward (NT) or
+    d-relu backward (k-major B), vs the fp32 reference."""
+    from distributed_llms_example_amd.ops.rng import keep_mask
+    torch.manual_seed(4)
+    M, N, p = 8448, 4096, 0.1
+    C = _ext.native()
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    if not kmajor:
+        w = (torch.randn(N, K, device=DEV) * K ** -0.5).to(torch.bfloat16)
+        h = C.gemm_fused(x, w, False, 1, None, None, None, p, 5, 9)
+        ref = torch.relu(x.float() @ w.float().t()) * keep_mask(5, p, (M, N), x.device).float() / (1.0 - p)
+        _close(h, ref, 2e-2, 2e-2, "pp persistent fwd")
+    else:
+        w = (torch.randn(K, N, device=DEV) * K ** -0.5).to(torch.bfloat16)
+        hs = (torch.relu(torch.randn(M, N, device=DEV)) * keep_mask(6, p, (M, N), x.device).float()).to(torch.bfloat16)
+        du = C.gemm_fused(x, w, True, 3, None, hs, None, p, 6, 9)
+        ref = (x.float() @ w.float()) * (hs.float() != 0).float() / (1.0 - p)
+        _close(du, ref, 2e-2, 2e-2, "pp persistent bwd")
 
 
 def test_gemm_fused_rejects_unsupported_shapes():
