@@ -44,24 +44,6 @@ constexpr int BM = 256, BN = 256, NT = 512;
 enum Epi { EPI_NONE = 0, EPI_RELU = 1, EPI_GELU = 2, EPI_DRELU = 3, EPI_DGELU = 4, EPI_GELU_TANH = 5,
            EPI_DGELU_TANH = 6 };
 
-// LDS-DMA through a buffer descriptor: 16 B per lane from base + voff (bytes) to LDS lds_byte + 16 * lane.  base is
-// wave-uniform (SGPRs); num_records = 2^32 - 1, so voff only has to stay below 4 GB.  soffset = 0 (on gfx950 the LDS
-// form is used with a zero wave offset, as composable_kernel does).
-typedef __attribute__((ext_vector_type(4))) int i32x4;
-extern "C" __device__ void llvm_amdgcn_raw_buffer_load_lds(i32x4 rsrc, __attribute__((address_space(3))) uint32_t* lds,
-                                                           int size, int voffset, int soffset, int offset,
-                                                           int aux) __asm("llvm.amdgcn.raw.buffer.load.lds");
-DLLM_DEVICE void bld16(const void* base, uint32_t voff, uint32_t lds_byte) {
-  const uint64_t a = (uint64_t)base;
-  i32x4 r;
-  r.x = (int)(uint32_t)a;
-  r.y = (int)((uint32_t)(a >> 32) & 0xFFFFu);
-  r.z = -1;
-  r.w = 0x00020000;
-  llvm_amdgcn_raw_buffer_load_lds(r, (__attribute__((address_space(3))) uint32_t*)(uintptr_t)lds_byte, 16, (int)voff, 0,
-                                  0, 0);
-}
-
 DLLM_DEVICE int xcd_remap(int bid, int nblk) {
   const int q = nblk / 8, r = nblk % 8, x = bid % 8;
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
