@@ -158,12 +158,10 @@ DLLM_DEVICE void glds4(const void* g, uint32_t lds_byte) {
 }
 
 // LDS-DMA through a buffer descriptor: 16 B per lane from base + voff (bytes) to LDS lds_byte + 16 * lane.  base is
-// wave-uniform (SGPRs); num_records = 2^32 - 1, so voff only has to stay below 4 GB.  soffset = 0 (on gfx950 the LDS
-// form is used with a zero wave offset, as composable_kernel does).
+// wave-uniform (the descriptor lives in SGPRs, so the address math is scalar and only the 32-bit voff is per lane);
+// num_records = 2^32 - 1, so voff only has to stay below 4 GB; soffset 0.  Inline asm for the same reason as glds16:
+// the llvm.amdgcn.raw.buffer.load.lds intrinsic makes hipcc wait vmcnt(0) before the next transposed LDS read.
 typedef __attribute__((ext_vector_type(4))) int i32x4;
-extern "C" __device__ void llvm_amdgcn_raw_buffer_load_lds(i32x4 rsrc, __attribute__((address_space(3))) uint32_t* lds,
-                                                           int size, int voffset, int soffset, int offset,
-                                                           int aux) __asm("llvm.amdgcn.raw.buffer.load.lds");
 DLLM_DEVICE void bld16(const void* base, uint32_t voff, uint32_t lds_byte) {
   const uint64_t a = (uint64_t)base;
   i32x4 r;
@@ -171,8 +169,12 @@ DLLM_DEVICE void bld16(const void* base, uint32_t voff, uint32_t lds_byte) {
   r.y = (int)((uint32_t)(a >> 32) & 0xFFFFu);
   r.z = -1;
   r.w = 0x00020000;
-  llvm_amdgcn_raw_buffer_load_lds(r, (__attribute__((address_space(3))) uint32_t*)(uintptr_t)lds_byte, 16, (int)voff, 0,
-                                  0, 0);
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
+               "s_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(r), "s"(lds_byte)
+               : "memory");
 }
 
 DLLM_DEVICE uint32_t lds_addr(const void* p) {
