@@ -492,12 +492,12 @@ bool gemm_fused_supported(const Tensor& a, const Tensor& b, bool b_kmajor) {
 
 Tensor gemm_fused(const Tensor& a, const Tensor& b, bool b_kmajor, int64_t epi, const optional<Tensor>& bias,
                   const optional<Tensor>& aux, const optional<Tensor>& aux_out, double p, int64_t seed,
-                  int64_t variant) {
+                  int64_t variant, const optional<Tensor>& mask) {
   TORCH_CHECK(gemm_fused_supported(a, b, b_kmajor),
               "gemm_fused: need bf16 GPU a [M,K], b [N,K] (or [K,N] k-major), unit inner stride, 16-B aligned rows, "
               "M and N multiples of 256, K % 64 == 0, M*N < 2^32");
   TORCH_CHECK(a.device() == b.device(), "gemm_fused: device mismatch");
-  TORCH_CHECK(epi >= 0 && epi <= 6, "gemm_fused: bad epilogue ", epi);
+  TORCH_CHECK(epi >= 0 && epi <= 7, "gemm_fused: bad epilogue ", epi);
   TORCH_CHECK(p >= 0.0 && p < 1.0, "gemm_fused: dropout p must be in [0, 1)");
   const int64_t M = a.size(0), K = a.size(1), N = b_kmajor ? b.size(1) : b.size(0);
   auto out = at::empty({M, N}, a.options());
@@ -553,6 +553,18 @@ Tensor gemm_fused(const Tensor& a, const Tensor& b, bool b_kmajor, int64_t epi, 
   }
   const int v = variant >= 0 ? (int)variant : (int)gemm_fused_variant(K);
   TORCH_CHECK(v >= 0 && v <= 9, "gemm_fused: bad variant ", v);
+  // ReLU derivative bit mask (ping-pong kernel only): epi 1 writes it when given, epi 7 (d-relu) reads it instead of aux
+  const bool has_mask = mask.has_value() && mask->defined();
+  TORCH_CHECK(epi != 7 || has_mask, "gemm_fused: epilogue 7 needs the ReLU mask");
+  if (has_mask) {
+    TORCH_CHECK(epi == 1 || epi == 7, "gemm_fused: a mask goes with epilogue 1 (write) or 7 (read)");
+    TORCH_CHECK(v == 8 || v == 9, "gemm_fused: the ReLU mask needs the ping-pong kernel (variant 8 / 9)");
+    TORCH_CHECK(mask->is_cuda() && mask->device() == a.device() && mask->scalar_type() == at::kInt &&
+                    mask->is_contiguous() && mask->numel() == M * N / 32 &&
+                    reinterpret_cast<uintptr_t>(mask->data_ptr()) % 16 == 0,
+                "gemm_fused: mask must be a contiguous 16-B aligned int32 GPU tensor of M*N/32 words");
+    P.mask = reinterpret_cast<uint32_t*>(mask->data_ptr());
+  }
   check_rc(dllm_gemm_fused(&P, b_kmajor ? 1 : 0, v, stream()), "gemm_fused");
   return out;
 }
@@ -609,8 +621,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_fused", &gemm_fused, "epi(a . b) with a fused bias / activation / dropout (or their backward) epilogue",
         py::arg("a"), py::arg("b"), py::arg("b_kmajor"), py::arg("epi"), py::arg("bias") = py::none(),
         py::arg("aux") = py::none(), py::arg("aux_out") = py::none(), py::arg("p") = 0.0, py::arg("seed") = 0,
-        py::arg("variant") = -1);
+        py::arg("variant") = -1, py::arg("mask") = py::none());
   m.def("gemm_fused_supported", &gemm_fused_supported);
+  m.def("gemm_fused_variant", &gemm_fused_variant, "default kernel variant for reduction length K");
   m.def("colsum_acc", &colsum_acc, "out += x.sum(0) for a token-major bf16 x (bias gradients)");
   dllm::bind_reducer(m);
   m.attr("arch") = "gfx950";

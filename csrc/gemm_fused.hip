@@ -42,7 +42,7 @@ namespace {
 constexpr int BM = 256, BN = 256, NT = 512;
 
 enum Epi { EPI_NONE = 0, EPI_RELU = 1, EPI_GELU = 2, EPI_DRELU = 3, EPI_DGELU = 4, EPI_GELU_TANH = 5,
-           EPI_DGELU_TANH = 6 };
+           EPI_DGELU_TANH = 6, EPI_DRELU_M = 7 };
 
 DLLM_DEVICE int xcd_remap(int bid, int nblk) {
   const int q = nblk / 8, r = nblk % 8, x = bid % 8;
@@ -138,7 +138,7 @@ DLLM_DEVICE f32x4 load4(const uint16_t* p) {
 
 // v = accumulators (+ bias, added by the caller from registers loaded once) for C[m][n .. n+3] (n % 4 == 0)
 template <int EPI>
-DLLM_DEVICE void epilogue4(const GemmFusedParams& P, int m, int n, f32x4 v) {
+DLLM_DEVICE f32x4 epilogue4(const GemmFusedParams& P, int m, int n, f32x4 v) {
   const bool drop = P.p > 0.f;
   const uint32_t e = (uint32_t)m * (uint32_t)P.N + (uint32_t)n;  // output element index (< 2^32, host-checked)
   if (EPI == EPI_RELU || EPI == EPI_GELU || EPI == EPI_GELU_TANH) {
@@ -159,6 +159,7 @@ DLLM_DEVICE void epilogue4(const GemmFusedParams& P, int m, int n, f32x4 v) {
     for (int k = 0; k < 4; ++k) v[k] *= EPI == EPI_DGELU ? gelu_df(u[k]) : gelu_tanh_df(u[k]);
   }
   store4(P.C + (long)m * P.ldc + n, v);
+  return v;
 }
 
 // MF = 32: v_mfma_f32_32x32x16_bf16, 4x2 accumulator tiles of 32x32 per wave;
@@ -636,8 +637,19 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(GemmFusedParams P) {
     sync_m();
   };
 
+  // ReLU derivative bit mask (P.mask): 128 bits per thread per tile, bit 16 i + 4 j + r <-> acc[i][j][r], stored as
+  // one 16-B word at tile (mb * tn + nb), thread tid — the forward (EPI_RELU) writes it, the backward (EPI_DRELU_M)
+  // stages it into LDS with one extra DMA unit at the start of the tile (double-buffered by tile parity) instead of
+  // reading the [M, N] bf16 activation back in its epilogue.
+  auto mask_word = [&](int tm0, int tn0) { return (long)((tm0 / BM) * P.tn + tn0 / BN) * NT * 4; };
+  const uint32_t lds_mask = lds0 + (uint32_t)(4 * TILE) * 2u;  // after the two [A | B] buffers
+  auto mask_unit = [&](int i, int tm0, int tn0) {
+    bld16(P.mask + mask_word(tm0, tn0), (uint32_t)tid * 16u,
+          __builtin_amdgcn_readfirstlane(lds_mask + (uint32_t)(i & 1) * 8192u + (uint32_t)w * 1024u));
+  };
+
   // epilogue: acc[i][j][0..3] = C[m0 + wm*128 + 16i + (lane & 15)][n0 + wn*64 + 16j + 4 (lane >> 4) + 0..3]
-  auto epilogue = [&](int tm0, int tn0) {
+  auto epilogue = [&](int tm0, int tn0, int ti) {
     // opaque lane id: otherwise the per-thread parts of the 32 store addresses are hoisted out of the tile loop
     // (PERSIST) and stay live through the main loop
     int ln = lane;
@@ -647,21 +659,43 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(GemmFusedParams P) {
     f32x4 bv[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) bv[j] = P.bias ? load4(P.bias + ncol + 16 * j) : f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (EPI == EPI_DRELU_M) {
+      const u32x4 mw = *reinterpret_cast<const u32x4*>(smem + 4 * TILE * 2 + (ti & 1) * 8192 + tid * 16);
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+      for (int i = 0; i < 8; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) epilogue4<EPI>(P, mrow + 16 * i, ncol + 16 * j, acc[i][j] + bv[j]);
+        for (int j = 0; j < 4; ++j) {
+          f32x4 v = acc[i][j];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = (mw[i >> 1] >> ((i & 1) * 16 + 4 * j + r)) & 1u ? v[r] * P.scale : 0.f;
+          store4(P.C + (long)(mrow + 16 * i) * P.ldc + ncol + 16 * j, v);
+        }
+    } else {
+      u32x4 bits = {0u, 0u, 0u, 0u};
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const f32x4 v = epilogue4<EPI>(P, mrow + 16 * i, ncol + 16 * j, acc[i][j] + bv[j]);
+          if (EPI == EPI_RELU) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) bits[i >> 1] |= (v[r] != 0.f ? 1u : 0u) << ((i & 1) * 16 + 4 * j + r);
+          }
+        }
+      if (EPI == EPI_RELU && P.mask) *reinterpret_cast<u32x4*>(P.mask + mask_word(tm0, tn0) + tid * 4) = bits;
+    }
   };
 
   int g = 0;
   for (int i = 0; i < ntw; ++i) {
+    if constexpr (EPI == EPI_DRELU_M) mask_unit(i, m0, n0);  // lands long before the epilogue (>= 8 phases, nk >= 2)
     // post: first k-tile after an epilogue
     int kt = 0;
     for (; kt < nk && g + 2 < total; ++kt, ++g) ktile(g, std::true_type{}, i > 0 && kt == 0);
     for (; kt < nk; ++kt, ++g) ktile(g, std::false_type{}, i > 0 && kt == 0);
     if (i + 1 < ntw) {  // PERSIST only: epilogue inside the staggered stream, then the next tile becomes current
       __builtin_amdgcn_sched_barrier(0);
-      epilogue(m0, n0);
+      epilogue(m0, n0, i);
       __builtin_amdgcn_sched_barrier(0);  // keep the accumulator reset (and the next fragments) after the epilogue
 #pragma unroll
       for (int r = 0; r < 8; ++r)
@@ -681,7 +715,11 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(GemmFusedParams P) {
     }
   }
   if (wm == 0) __builtin_amdgcn_s_barrier();  // undo the stagger: every wave has passed the same number of barriers
-  epilogue(m0, n0);
+  if constexpr (EPI == EPI_DRELU_M) {  // last tile: its mask unit may be < 4 phases old when nk == 1
+    wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+  }
+  epilogue(m0, n0, ntw - 1);
 }
 
 int num_cus() {
@@ -695,14 +733,14 @@ int num_cus() {
 }
 
 // persist: one workgroup per CU when there are >= 2 tiles per CU and >= 2 k-tiles per tile, for the store-only
-// epilogues (none / ReLU).  The others load (aux) or store twice (GELU pre-activation): their first load waits in order
+// epilogues (none / ReLU / ReLU backward from the bit mask, whose only load is an LDS-DMA unit).  The others load (aux) or store twice (GELU pre-activation): their first load waits in order
 // behind the next tile's queued DMA units and the persistent form measured 7-17 % SLOWER there
 // (profiles/r1_gemm_experiments.md), so they keep one tile per workgroup.
 template <int EPI, bool BKM>
 int launch_pp(const GemmFusedParams& p, bool persist, hipStream_t st) {
-  const size_t lds = (size_t)2 * 2 * 64 * 256 * 2;
+  const size_t lds = (size_t)2 * 2 * 64 * 256 * 2 + (EPI == EPI_DRELU_M ? 2 * 8192 : 0);
   const int T = p.tm * p.tn, cus = num_cus() / 8 * 8;
-  constexpr bool light = EPI == EPI_NONE || EPI == EPI_RELU;
+  constexpr bool light = EPI == EPI_NONE || EPI == EPI_RELU || EPI == EPI_DRELU_M;
   if (light && persist && cus >= 8 && T >= 2 * cus && p.K >= 128) {
     static bool attr = false;
     if (!attr) {
@@ -764,6 +802,8 @@ int dispatch_epi(const GemmFusedParams& p, int variant, hipStream_t st) {
     case EPI_DRELU: return launch_v<BKM, EPI_DRELU>(p, variant, st);
     case EPI_DGELU: return launch_v<BKM, EPI_DGELU>(p, variant, st);
     case EPI_DGELU_TANH: return launch_v<BKM, EPI_DGELU_TANH>(p, variant, st);
+    case EPI_DRELU_M: return variant == 8 ? launch_pp<EPI_DRELU_M, BKM>(p, false, st)
+                                          : variant == 9 ? launch_pp<EPI_DRELU_M, BKM>(p, true, st) : -6;
     default: return -5;
   }
 }

@@ -32,4 +32,5 @@ struct GemmFusedParams {
   float scale; // 1 / (1 - p), or 1
   uint32_t seed, thr;
   int grp;     // tile order (gemm_pp_kernel): groups of grp 256-row blocks, column-major inside a group; 0 = row-major
+  uint32_t* mask;  // ReLU derivative bits (ping-pong kernel): written by epi 1 when non-null, read by epi 7; M*N/32 words
 };

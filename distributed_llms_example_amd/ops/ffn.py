@@ -13,8 +13,11 @@ alive until backward.  Here (csrc/gemm_fused.hip):
   masks); GELU also writes its pre-activation ``U`` as a second output; ReLU stores nothing else;
 * backward: ``dU = act'(U) · dropout'(dY Wo)`` is ONE GEMM (``dY [M, d] x Wo [d, F]``, k-major B) whose
   epilogue applies the dropout and activation backward.  For ReLU the derivative mask is ``H != 0``
-  read back from the saved activation itself (ReLU and dropout both produce exact zeros), so the
-  pre-activation is never stored: one ``[tokens, d_ff]`` tensor less per layer;
+  (ReLU and dropout both produce exact zeros), so the pre-activation is never stored: one
+  ``[tokens, d_ff]`` tensor less per layer.  With the ping-pong kernel (variants 8 / 9, the default) the
+  forward epilogue also writes that mask as bits (``M * d_ff / 32`` int32 words, 1/16 of ``H``) and the
+  backward stages them through LDS instead of re-reading the bf16 ``H`` (which stays saved only as the
+  ``lin_out`` weight-gradient input);
 * weight gradients are accumulated straight into the flat gradient buffer (ops/gemm.py), and the
   reducer's post hooks are fired by hand exactly as ops/linear.py does.
 
@@ -22,7 +25,7 @@ Taken only when both linears carry FlatParams-managed gradients (``_dllm_fused_w
 bf16 on the GPU and the shapes suit the kernel (tokens and d_ff multiples of 256, d_model of 64); anything
 else (gated FLAN-T5 FFNs, CPU, odd token counts) runs the unfused modules with identical semantics.
 ``DLLM_FUSED_FFN=0`` forces the unfused path (A/B runs); ``DLLM_GEMM_FUSED_VARIANT=n`` forces a kernel
-variant (csrc/gemm_fused.hip).
+variant (csrc/gemm_fused.hip); ``DLLM_RELU_MASK=0`` makes the ReLU backward read ``H`` instead of the bits.
 """
 from __future__ import annotations
 
@@ -39,7 +42,13 @@ from .linear import _fire, _fusable
 # activation -> (forward epilogue, backward epilogue) of csrc/gemm_fused.hip
 EPILOGUES = {"relu": (1, 3), "gelu": (2, 4), "gelu_new": (5, 6), "gelu_fast": (5, 6)}
 _VARIANT = int(os.environ.get("DLLM_GEMM_FUSED_VARIANT", "-1"))  # -1: picked by K in csrc/bind.cpp
+_RELU_MASK = os.environ.get("DLLM_RELU_MASK", "1") != "0"  # 0: the backward re-reads H (A/B runs)
 fused_calls = 0  # number of FFN forwards that took the fused path (tests assert the kernel really ran)
+
+
+def _pingpong(C, K: int) -> bool:
+    """The kernel chosen for reduction length K is the ping-pong one (the only one with the ReLU bit mask)."""
+    return (_VARIANT if _VARIANT >= 0 else C.gemm_fused_variant(K)) in (8, 9)
 
 
 def _enabled() -> bool:
@@ -53,19 +62,21 @@ class _FusedFFNFn(torch.autograd.Function):
         shape = x.shape
         x2 = x.reshape(-1, shape[-1])
         efwd, _ = EPILOGUES[act]
-        u = None
+        u = mask = None
         if efwd != 1:  # GELU: the backward needs the pre-activation
             u = torch.empty(x2.shape[0], wi.shape[0], device=x.device, dtype=x.dtype)
-        h = C.gemm_fused(x2, wi, False, efwd, bi, None, u, float(p), int(seed), _VARIANT)
+        elif _RELU_MASK and _pingpong(C, x2.shape[1]) and _pingpong(C, wo.shape[0]):  # ReLU: bits for the backward
+            mask = torch.empty(x2.shape[0] * wi.shape[0] // 32, device=x.device, dtype=torch.int32)
+        h = C.gemm_fused(x2, wi, False, efwd, bi, None, u, float(p), int(seed), _VARIANT, mask)
         y = F.linear(h, wo, bo)
-        ctx.save_for_backward(x2, h, u)
+        ctx.save_for_backward(x2, h, u, mask)
         ctx.params = params
         ctx.cfg = (act, float(p), int(seed), shape)
         return y.view(*shape[:-1], wo.shape[0])
 
     @staticmethod
     def backward(ctx, dy):
-        x2, h, u = ctx.saved_tensors
+        x2, h, u, mask = ctx.saved_tensors
         Wi, Bi, Wo, Bo = ctx.params
         act, p, seed, shape = ctx.cfg
         C = _ext.native()
@@ -74,7 +85,10 @@ class _FusedFFNFn(torch.autograd.Function):
         dy2 = dy.reshape(-1, dy.shape[-1])
         if not C.gemm_fused_supported(dy2, wo, True):
             dy2 = dy2.contiguous()
-        du = C.gemm_fused(dy2, wo, True, ebwd, None, h if ebwd == 3 else u, None, p, seed, _VARIANT)
+        if mask is not None:  # d-relu from the bit mask
+            du = C.gemm_fused(dy2, wo, True, 7, None, None, None, p, seed, _VARIANT, mask)
+        else:
+            du = C.gemm_fused(dy2, wo, True, ebwd, None, h if ebwd == 3 else u, None, p, seed, _VARIANT)
         with torch.no_grad():
             wgrad_accumulate(Wo.grad, dy2, h)
             if Bo is not None:

@@ -417,6 +417,31 @@ def test_gemm_pp_persistent(K, kmajor):
         _close(du, ref, 2e-2, 2e-2, "pp persistent bwd")
 
 
+@pytest.mark.parametrize("variant", [8, 9])
+@pytest.mark.parametrize("M,d,F_", [(768, 512, 1024), (8448, 768, 4096)])
+def test_gemm_relu_bit_mask(variant, M, d, F_):
+    """ReLU derivative bits: the forward (epi 1) writes them next to H, the backward (epi 7) stages them through LDS;
+    both outputs must equal the aux-tensor path (epi 1 without mask / epi 3 reading H) bit for bit."""
+    torch.manual_seed(5)
+    p = 0.1
+    C = _ext.native()
+    x = torch.randn(M, d, device=DEV).to(torch.bfloat16)
+    wi = (torch.randn(F_, d, device=DEV) * d ** -0.5).to(torch.bfloat16)
+    bi = (0.1 * torch.randn(F_, device=DEV)).to(torch.bfloat16)
+    mask = torch.full((M * F_ // 32,), -1, device=DEV, dtype=torch.int32)
+    h0 = C.gemm_fused(x, wi, False, 1, bi, None, None, p, 11, variant)
+    h = C.gemm_fused(x, wi, False, 1, bi, None, None, p, 11, variant, mask)
+    torch.testing.assert_close(h, h0, rtol=0, atol=0)
+    dy = torch.randn(M, d, device=DEV).to(torch.bfloat16)
+    wo = (torch.randn(d, F_, device=DEV) * d ** -0.5).to(torch.bfloat16)
+    du0 = C.gemm_fused(dy, wo, True, 3, None, h, None, p, 11, variant)
+    du = C.gemm_fused(dy, wo, True, 7, None, None, None, p, 11, variant, mask)
+    torch.testing.assert_close(du, du0, rtol=0, atol=0)
+    assert (du == 0).float().mean().item() > 0.4  # the mask really zeroes (ReLU ~ half, dropout 10 %)
+    with pytest.raises(RuntimeError):
+        C.gemm_fused(dy, wo, True, 7, None, None, None, p, 11, 4, mask)  # mask needs the ping-pong kernel
+
+
 def test_gemm_fused_rejects_unsupported_shapes():
     C = _ext.native()
     x = torch.randn(300, 768, device=DEV).to(torch.bfloat16)  # tokens not a multiple of 256
