@@ -20,6 +20,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops import activations, attention as attn_ops, norms
+from ..parallel.context import context_parallel_encode, ring_attention
 from ..ops.ffn import ffn
 from ..ops.cross_entropy import cross_entropy
 from ..ops.linear import Linear, stacked_linear
@@ -73,6 +74,12 @@ class T5Attention(nn.Module):
         if self.cross:
             q = self.q(x).view(B, S, H, D)
             o = attn_ops.attention_q_kv(q, kv if kv is not None else self.project_kv(kv_in), **kw)
+        elif isinstance(lut, _CPBias):  # encoder sequence sharded over a CP group: ring attention
+            qkv = self.qkv(x).view(B, S, 3, H, D)
+            o = ring_attention(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], group=lut.group, scale=1.0,
+                               key_padding_mask=mask, bias_table=lut.table, bidirectional=True,
+                               num_buckets=self.cfg.relative_attention_num_buckets,
+                               max_distance=self.cfg.relative_attention_max_distance, dropout_p=p, seed=seed)
         else:
             pre = attn_ops.prefetch_dropout_mask(x, B, H, S, S, p, seed) if cache is None else None
             qkv = self.qkv(x).view(B, S, 3, H, D)
@@ -82,6 +89,15 @@ class T5Attention(nn.Module):
             else:
                 o = attn_ops.attention_qkv(qkv, pre=pre, **kw)
         return self.o(o.reshape(B, S, H * D))
+
+
+class _CPBias:
+    """Marker handed to encoder self-attention instead of a bias LUT when the sequence is sharded over a
+    context-parallel group (parallel/context.py builds the global-distance LUTs per ring step)."""
+
+    def __init__(self, group, table):
+        self.group = group
+        self.table = table
 
 
 class T5DenseActDense(nn.Module):
@@ -161,7 +177,11 @@ class T5Stack(nn.Module):
         x = F.embedding(input_ids, self._embed[0].weight)
         B, S = input_ids.shape
         k_len = S + q_offset
-        lut = self.block[0].layer[0].SelfAttention.bias_lut(S, k_len, q_offset=q_offset)
+        cp = getattr(self, "_cp_group", False)
+        if cp is not False and not self.is_decoder:
+            lut = _CPBias(cp, self.block[0].layer[0].SelfAttention.relative_attention_bias.weight)
+        else:
+            lut = self.block[0].layer[0].SelfAttention.bias_lut(S, k_len, q_offset=q_offset)
         blocks = list(self.block)
         # h = dropout(embeddings); normed = block0 self-attn norm(h)
         normed, h = norms.dropout_rms_norm(x, blocks[0].layer[0].layer_norm.weight, eps, p,
@@ -289,9 +309,25 @@ class T5ForConditionalGeneration(nn.Module):
         for st in (self.encoder, self.decoder):
             st.cfg = self.config
 
+    def enable_context_parallel(self, group=None, enable: bool = True):
+        """Shard the ENCODER sequence over ``group`` (None = the default group): ``forward`` then takes this
+        rank's contiguous slice of ``input_ids`` / ``attention_mask`` (:func:`parallel.context.shard_sequence`)
+        and the full decoder batch.  Encoder self-attention becomes ring attention (parallel/context.py); the
+        encoder output is all-gathered along the sequence for the decoder, which every CP rank runs on the
+        same batch.  The dropout seed stream must be identical on the ranks of one CP group."""
+        if enable:
+            self.encoder._cp_group = group
+        elif hasattr(self.encoder, "_cp_group"):
+            del self.encoder._cp_group
+        return self
+
     def forward(self, input_ids=None, attention_mask=None, decoder_input_ids=None, labels=None,
                 label_smoothing: float = 0.0, return_logits: bool = False, encoder_outputs=None):
-        enc = encoder_outputs if encoder_outputs is not None else self.encode(input_ids, attention_mask)
+        cp = getattr(self.encoder, "_cp_group", False)
+        if cp is not False and encoder_outputs is None:
+            enc, attention_mask = context_parallel_encode(self.encode, input_ids, attention_mask, cp)
+        else:
+            enc = encoder_outputs if encoder_outputs is not None else self.encode(input_ids, attention_mask)
         if decoder_input_ids is None:
             decoder_input_ids = self.shift_right(labels)
         dec = self.decode(decoder_input_ids, enc, attention_mask)

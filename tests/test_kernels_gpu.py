@@ -475,3 +475,104 @@ def test_attention_saturated_bias_tiles_match(causal, S):
     assert _rel(o1, o0) < 1e-3, _rel(o1, o0)
     assert _rel(gx1, gx0) < 1e-3, _rel(gx1, gx0)
     assert _rel(gt1, gt0) < 1e-3, _rel(gt1, gt0)
+
+
+@pytest.mark.parametrize("W,S,p", [(2, 512, 0.0), (4, 256, 0.0), (2, 384, 0.1)])
+def test_context_parallel_blocks(W, S, p):
+    """Ring attention numerics on one GPU: W virtual ranks run the native flash kernels per (q shard, kv shard)
+    block with global-distance T5 bias LUTs, merge by LSE, and run the backward per block with the global
+    o / lse (parallel/context.py); p = 0 must equal the unsharded fp32 attention, p > 0 its per-block-seed
+    reference."""
+    from distributed_llms_example_amd.parallel import context as cp
+    torch.manual_seed(W * 1000 + S)
+    B, H, D = 2, 4, 64
+    N = W * S
+    q, k, v = (torch.randn(B, N, H, D, device=DEV).to(torch.bfloat16) for _ in range(3))
+    table = torch.randn(32, H, device=DEV) * 0.5
+    mask = torch.ones(B, N, dtype=torch.bool, device=DEV)
+    mask[1, N - S // 2 - 7:] = False
+    km = mask.to(torch.uint8)
+    do = torch.randn(B, N, H, D, device=DEV).to(torch.bfloat16)
+    seed = 99
+    outs, lses = [], []
+    luts = {}
+    for r in range(W):
+        qr = q[:, r * S:(r + 1) * S]
+        o_acc = l_acc = None
+        for s in range(W):
+            lt = A.relative_bias_lut(table, S, S, True, 32, 128, q_offset=(r - s) * S)
+            luts[(r, s)] = lt
+            o_b, l_b, _ = cp._block_fwd(qr, k[:, s * S:(s + 1) * S], v[:, s * S:(s + 1) * S],
+                                        km[:, s * S:(s + 1) * S].contiguous(), lt, lt._dllm_sat, 1.0, p,
+                                        cp._block_seed(seed, r, s))
+            o_acc, l_acc = (o_b, l_b) if o_acc is None else cp._merge(o_acc, l_acc, o_b, l_b)
+        outs.append(o_acc.to(torch.bfloat16))
+        lses.append(l_acc.contiguous())
+    o = torch.cat(outs, 1)
+    dq = torch.zeros(B, N, H, D, device=DEV)
+    dk = torch.zeros_like(dq)
+    dv = torch.zeros_like(dq)
+    dlut = {}
+    for r in range(W):
+        for s in range(W):
+            lt = luts[(r, s)]
+            sl_q, sl_k = slice(r * S, (r + 1) * S), slice(s * S, (s + 1) * S)
+            dmask = None
+            if p > 0:  # the planes the forward would have produced for this block
+                dmask = _ext.native().attn_dropout_mask(B, H, S, S, p, cp._block_seed(seed, r, s), q)
+            a, b_, c, dl = cp._block_bwd(do[:, sl_q].contiguous(), q[:, sl_q], k[:, sl_k], v[:, sl_k],
+                                         outs[r], lses[r], km[:, sl_k].contiguous(), lt, lt._dllm_sat, 1.0, p,
+                                         cp._block_seed(seed, r, s), True, dmask)
+            dq[:, sl_q] += a
+            dk[:, sl_k] += b_
+            dv[:, sl_k] += c
+            dlut[(r, s)] = dl
+    # fp32 reference of the same math
+    qf, kf, vf = (t.float().requires_grad_(True) for t in (q, k, v))
+    tab = table.clone().requires_grad_(True)
+    if p == 0.0:
+        ref = A._reference(qf, kf, vf, 1.0, False, mask, A.relative_bias_lut(tab, N, N, True, 32, 128), 0.0, 0)
+    else:
+        rows = []
+        for r in range(W):
+            o_acc = l_acc = None
+            for s in range(W):
+                lt = A.relative_bias_lut(tab, S, S, True, 32, 128, q_offset=(r - s) * S)
+                o_b, l_b = cp._ref_block_fwd(qf[:, r * S:(r + 1) * S], kf[:, s * S:(s + 1) * S],
+                                             vf[:, s * S:(s + 1) * S], mask[:, s * S:(s + 1) * S], lt, 1.0, p,
+                                             cp._block_seed(seed, r, s))
+                o_acc, l_acc = (o_b, l_b) if o_acc is None else cp._merge(o_acc, l_acc, o_b, l_b)
+            rows.append(o_acc)
+        ref = torch.cat(rows, 1)
+    assert _rel(o, ref) < 2e-2, _rel(o, ref)
+    ref.backward(do.float())
+    for name, a_, b_ in (("dq", dq, qf.grad), ("dk", dk, kf.grad), ("dv", dv, vf.grad)):
+        assert _rel(a_, b_) < 3e-2, (name, _rel(a_, b_))
+    # bucket-table gradient through the W x W global-distance LUTs
+    tg = table.clone().requires_grad_(True)
+    tot = sum((A.relative_bias_lut(tg, S, S, True, 32, 128, q_offset=(r - s) * S) * dlut[(r, s)]).sum()
+              for r in range(W) for s in range(W))
+    tot.backward()
+    assert _rel(tg.grad, tab.grad) < 3e-2, _rel(tg.grad, tab.grad)
+
+
+def test_ring_attention_single_rank_equals_attention():
+    """ring_attention with no process group (W = 1) runs one native block: same as attention() incl. grads."""
+    from distributed_llms_example_amd.parallel.context import ring_attention
+    torch.manual_seed(3)
+    B, S, H, D = 2, 320, 4, 64
+    q, k, v = (torch.randn(B, S, H, D, device=DEV).to(torch.bfloat16) for _ in range(3))
+    mask = torch.ones(B, S, dtype=torch.bool, device=DEV)
+    mask[0, 250:] = False
+    table = torch.randn(32, H, device=DEV) * 0.5
+    t1, t2 = table.clone().requires_grad_(True), table.clone().requires_grad_(True)
+    a = [t.clone().requires_grad_(True) for t in (q, k, v)]
+    b = [t.clone().requires_grad_(True) for t in (q, k, v)]
+    o1 = ring_attention(*a, key_padding_mask=mask, bias_table=t1)
+    o2 = A.attention(*b, key_padding_mask=mask, bias_lut=A.relative_bias_lut(t2, S, S, True, 32, 128))
+    assert _rel(o1, o2) < 1e-2
+    g = torch.randn_like(o1)
+    (o1.float() * g.float()).sum().backward()
+    (o2.float() * g.float()).sum().backward()
+    for x, y in zip(a + [t1], b + [t2]):
+        assert _rel(x.grad, y.grad) < 2e-2, _rel(x.grad, y.grad)
