@@ -48,6 +48,8 @@ def base_parser(description: str, defaults: dict | None = None) -> argparse.Argu
     g.add_argument("--seed", type=int, default=42)
     g.add_argument("--gradient-checkpointing", action="store_true",
                    help="recompute each transformer block in backward (long sequences / large models)")
+    g.add_argument("--context-parallel", type=int, default=1,
+                   help="shard the encoder sequence over groups of N ranks (ring attention; T5 family)")
     g.add_argument("--model-overrides", type=str, default=None,
                    help="comma list key=value applied to the model config (e.g. num_layers=2)")
     return ap

@@ -229,6 +229,13 @@ class BartForConditionalGeneration(nn.Module):
         from .generation import generate
         return generate(self, input_ids, attention_mask=attention_mask, **kw)
 
+    def enable_context_parallel(self, group=None, enable: bool = True):
+        """BART is capped at 1024 learned positions (configuration_bart.py:50), so it has no long-sequence
+        config to shard; context parallelism is implemented for the T5 family (models/t5.py)."""
+        if enable:
+            raise NotImplementedError("context parallelism is implemented for T5 / FLAN-T5 encoders only")
+        return self
+
     def gradient_checkpointing_enable(self, enable: bool = True):
         """HF-style switch: recompute every layer in backward."""
         self.config.gradient_checkpointing = bool(enable)

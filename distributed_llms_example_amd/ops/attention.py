@@ -83,6 +83,8 @@ def saturated_ranges(idx: torch.Tensor) -> tuple[int, int]:
     L = idx.numel()
     same_lo = (idx == idx[0]).long().cumprod(0).sum().item()
     same_hi = (idx.flip(0) == idx[-1]).long().cumprod(0).sum().item()
+    if same_lo == L:  # one bucket everywhere (far-apart context-parallel shards): all of it is the low range
+        return L - 1, L
     return int(same_lo) - 1, int(L - same_hi)
 
 

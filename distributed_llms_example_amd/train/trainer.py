@@ -23,9 +23,11 @@ import time
 from dataclasses import dataclass, field
 
 import torch
+import torch.distributed as dist
 
 from ..ops.rng import manual_seed
 from ..parallel import collectives
+from ..parallel.context import shard_sequence
 from ..parallel.env import init_distributed
 from ..parallel.reducer import DEFAULT_BUCKET_MB
 from ..parallel.sampler import ShardedBatchSampler
@@ -72,6 +74,7 @@ class TrainingArguments:
     ddp_bucket_cap_mb: float | None = None
     ddp_timeout: int = 1800
     overlap_comm: bool = True
+    context_parallel_size: int = 1  # shard the encoder sequence over groups of this many consecutive ranks
     resume_from_checkpoint: str | None = None
     nan_guard: bool = True  # raise when the (logged, already synchronised) mean loss is NaN/Inf
     report_to: list = field(default_factory=list)
@@ -100,7 +103,18 @@ class Trainer:
         self.env = env or init_distributed(timeout_s=args.ddp_timeout)
         self.tokenizer = processing_class if processing_class is not None else tokenizer
         torch.manual_seed(args.seed)
-        manual_seed(args.seed + 7919 * self.env.rank)
+        # context parallelism (parallel/context.py): ranks [k*cp, (k+1)*cp) share one batch and one dropout stream
+        cp = max(1, int(args.context_parallel_size))
+        assert self.env.world_size % cp == 0, "world size must be a multiple of context_parallel_size"
+        self.dp_rank, self.dp_world = self.env.rank // cp, self.env.world_size // cp
+        self.cp_group = None
+        if cp > 1:
+            for k in range(self.dp_world):  # every rank creates every group (c10d requirement)
+                grp = dist.new_group(list(range(k * cp, (k + 1) * cp)))
+                if k == self.dp_rank:
+                    self.cp_group = grp
+            model.enable_context_parallel(self.cp_group)
+        manual_seed(args.seed + 7919 * self.dp_rank)
         bf16 = args.bf16 if args.bf16 is not None else self.env.device.type == "cuda"
         self.dtype = torch.bfloat16 if bf16 else torch.float32
         self.engine = TrainEngine(model, self.env, lr=args.learning_rate, weight_decay=args.weight_decay,
@@ -119,17 +133,23 @@ class Trainer:
         self.scheduler = None
 
     # ------------------------------------------------------------------ data
-    def _loader(self, dataset, batch_size, shuffle, epoch=0):
-        sampler = ShardedBatchSampler(len(dataset), batch_size, self.env.world_size, self.env.rank, shuffle=shuffle,
+    def _loader(self, dataset, batch_size, shuffle, epoch=0, cp=True):
+        world, rank = (self.dp_world, self.dp_rank) if cp else (self.env.world_size, self.env.rank)
+        sampler = ShardedBatchSampler(len(dataset), batch_size, world, rank, shuffle=shuffle,
                                       seed=self.args.seed, drop_last=self.args.dataloader_drop_last)
         sampler.set_epoch(epoch)
         return torch.utils.data.DataLoader(dataset, batch_sampler=sampler, collate_fn=self.data_collator,
                                            num_workers=self.args.dataloader_num_workers,
                                            pin_memory=self.env.device.type == "cuda"), sampler
 
-    def _to_device(self, batch):
+    def _to_device(self, batch, cp=False):
         nb = self.env.device.type == "cuda"
-        return {k: v.to(self.env.device, non_blocking=nb) for k, v in batch.items() if torch.is_tensor(v)}
+        out = {k: v.to(self.env.device, non_blocking=nb) for k, v in batch.items() if torch.is_tensor(v)}
+        if cp and self.cp_group is not None:  # this rank's slice of the encoder sequence
+            for k in ("input_ids", "attention_mask"):
+                if k in out:
+                    out[k] = shard_sequence(out[k], self.cp_group).contiguous()
+        return out
 
     # ------------------------------------------------------------------ main loop
     def train(self, resume_from_checkpoint: str | bool | None = None):
@@ -176,7 +196,7 @@ class Trainer:
                     continue
                 micro += 1
                 sync = micro % ga == 0
-                loss = eng.forward_backward(self._to_device(batch), grad_accum=ga, sync=sync)
+                loss = eng.forward_backward(self._to_device(batch, cp=True), grad_accum=ga, sync=sync)
                 tr_loss_sum += loss.float()
                 tr_loss_n += 1
                 if not sync:
@@ -218,7 +238,7 @@ class Trainer:
         runtime = time.perf_counter() - t_start
         train_loss = total_loss_sum / max(1, total_loss_n)
         n_samples = n_examples * args.num_train_epochs if args.max_steps <= 0 else \
-            max_steps * args.per_device_train_batch_size * ga * env.world_size
+            max_steps * args.per_device_train_batch_size * ga * self.dp_world
         metrics = {"train_runtime": round(runtime, 4), "train_samples_per_second": round(n_samples / runtime, 3),
                    "train_steps_per_second": round(self.state.global_step / runtime, 3),
                    "train_loss": train_loss, "epoch": round(self.state.epoch, 4)}
@@ -235,13 +255,20 @@ class Trainer:
     def evaluate(self, eval_dataset=None):
         ds = eval_dataset if eval_dataset is not None else self.eval_dataset
         self.engine.train(False)
-        loader, _ = self._loader(ds, self.args.per_device_eval_batch_size, False)
+        # evaluation shards samples over every rank, full sequences (no context parallelism)
+        loader, _ = self._loader(ds, self.args.per_device_eval_batch_size, False, cp=False)
         tot = torch.zeros((), device=self.env.device, dtype=torch.float64)
         n = 0
-        for batch in loader:
-            out = self.engine.forward(self._to_device(batch))
-            tot += out.loss.double()
-            n += 1
+        if self.cp_group is not None:
+            self.model.enable_context_parallel(enable=False)
+        try:
+            for batch in loader:
+                out = self.engine.forward(self._to_device(batch))
+                tot += out.loss.double()
+                n += 1
+        finally:
+            if self.cp_group is not None:
+                self.model.enable_context_parallel(self.cp_group)
         m = collectives.mean_across_processes({"eval_loss": float(tot) / max(1, n)}, self.env.device)
         metrics = {"eval_loss": m["eval_loss"], "epoch": round(self.state.epoch, 4)}
         self.log(metrics)

@@ -126,3 +126,20 @@ def test_fault_injection_then_resume_matches_uninterrupted(tmp_path):
     assert a.keys() == b.keys()
     for k in a:
         torch.testing.assert_close(a[k], b[k], rtol=0, atol=0, msg=k)
+
+
+@pytest.mark.slow
+def test_train_torchrun_context_parallel_two_ranks(tmp_path):
+    """train-torchrun with --context-parallel 2: both ranks share each batch, the encoder sequence is split in
+    two and attention runs as a ring (parallel/context.py); evaluation and the save run as usual."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "train-torchrun.py"), "--model-ckpt",
+           "t5-tiny", "--output-dir", "cp", "--batch-size", "4", "--grad-accum", "1", "--evaluation-steps", "2",
+           "--warmup-steps", "1", "--context-parallel", "2", *COMMON]
+    r = subprocess.run(cmd, env=_env(tmp_path), capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    logs = _json_lines(r.stdout)
+    assert any("eval_loss" in x for x in logs)
+    final = [x for x in logs if "train_samples_per_second" in x]
+    assert final and final[-1]["train_loss"] > 0
+    assert (tmp_path / "outputs" / "cp" / "model.safetensors").exists()
