@@ -20,7 +20,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops import activations, attention as attn_ops, norms
-from ..parallel.context import context_parallel_encode, ring_attention
+from ..parallel.context import chunked_attention, context_parallel_encode, long_sequence_chunk, ring_attention
 from ..ops.ffn import ffn
 from ..ops.cross_entropy import cross_entropy
 from ..ops.linear import Linear, stacked_linear
@@ -76,10 +76,13 @@ class T5Attention(nn.Module):
             o = attn_ops.attention_q_kv(q, kv if kv is not None else self.project_kv(kv_in), **kw)
         elif isinstance(lut, _CPBias):  # encoder sequence sharded over a CP group: ring attention
             qkv = self.qkv(x).view(B, S, 3, H, D)
-            o = ring_attention(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], group=lut.group, scale=1.0,
-                               key_padding_mask=mask, bias_table=lut.table, bidirectional=True,
-                               num_buckets=self.cfg.relative_attention_num_buckets,
-                               max_distance=self.cfg.relative_attention_max_distance, dropout_p=p, seed=seed)
+            kw2 = dict(scale=1.0, key_padding_mask=mask, bias_table=lut.table, bidirectional=True,
+                       num_buckets=self.cfg.relative_attention_num_buckets,
+                       max_distance=self.cfg.relative_attention_max_distance, dropout_p=p, seed=seed)
+            if lut.chunk is not None:
+                o = chunked_attention(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], chunk=lut.chunk, **kw2)
+            else:
+                o = ring_attention(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], group=lut.group, **kw2)
         else:
             pre = attn_ops.prefetch_dropout_mask(x, B, H, S, S, p, seed) if cache is None else None
             qkv = self.qkv(x).view(B, S, 3, H, D)
@@ -95,9 +98,10 @@ class _CPBias:
     """Marker handed to encoder self-attention instead of a bias LUT when the sequence is sharded over a
     context-parallel group (parallel/context.py builds the global-distance LUTs per ring step)."""
 
-    def __init__(self, group, table):
+    def __init__(self, group, table, chunk=None):
         self.group = group
         self.table = table
+        self.chunk = chunk  # set: one device, long sequence in chunk-token blocks (parallel/context.py)
 
 
 class T5DenseActDense(nn.Module):
@@ -178,8 +182,10 @@ class T5Stack(nn.Module):
         B, S = input_ids.shape
         k_len = S + q_offset
         cp = getattr(self, "_cp_group", False)
-        if cp is not False and not self.is_decoder:
-            lut = _CPBias(cp, self.block[0].layer[0].SelfAttention.relative_attention_bias.weight)
+        chunk = long_sequence_chunk(S) if not self.is_decoder and caches is None else None
+        if (cp is not False or chunk is not None) and not self.is_decoder:
+            lut = _CPBias(cp, self.block[0].layer[0].SelfAttention.relative_attention_bias.weight,
+                          chunk=chunk if cp is False else None)
         else:
             lut = self.block[0].layer[0].SelfAttention.bias_lut(S, k_len, q_offset=q_offset)
         blocks = list(self.block)

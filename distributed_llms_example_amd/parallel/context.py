@@ -320,3 +320,97 @@ def context_parallel_encode(encode_fn, input_ids, attention_mask, group=None):
         dist.all_gather(parts, mask.contiguous(), group=group)
         mask = torch.cat(parts, 1)
     return enc, mask
+
+
+# --------------------------------------------------------------------------- single-GPU long sequences
+
+
+class _ChunkedAttnFn(torch.autograd.Function):
+    """The ring's block algorithm inside one process: a (Wq x Wk) grid of C x C flash-attention blocks merged by
+    LSE.  The single-kernel path stages per-key state and the bias window in LDS, which bounds it to ~8K keys
+    (csrc/attn.hip launch checks); chunking lifts that bound for long encoders on one GPU, and 4K-token blocks
+    measured faster per FLOP than one 8K kernel (profiles/r1_cp_attention_bench.jsonl).  ``luts[d + W - 1]``
+    is the LUT of block offset d = qi - kj."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, luts, kpm, sats, C, scale, p, seed):
+        W = q.shape[1] // C
+        outs, lses, dmasks = [], [], {}
+        for qi in range(W):
+            qs = q[:, qi * C:(qi + 1) * C]
+            o_acc = l_acc = None
+            for kj in range(W):
+                d = qi - kj + W - 1
+                km = kpm[:, kj * C:(kj + 1) * C].contiguous() if kpm is not None else None
+                o_b, l_b, dmasks[(qi, kj)] = _block_fwd(qs, k[:, kj * C:(kj + 1) * C], v[:, kj * C:(kj + 1) * C], km,
+                                                        luts[d] if luts is not None else None,
+                                                        sats[d] if sats is not None else None, scale, p,
+                                                        _block_seed(seed, qi, kj))
+                o_acc, l_acc = (o_b, l_b) if o_acc is None else _merge(o_acc, l_acc, o_b, l_b)
+            outs.append(o_acc.to(q.dtype))
+            lses.append(l_acc.contiguous())
+        o = torch.cat(outs, 1)
+        ctx.save_for_backward(q, k, v, o, torch.stack(lses), luts, kpm)
+        ctx.cfg = (sats, C, scale, p, seed, luts is not None and luts.requires_grad)
+        ctx.dmasks = dmasks
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, lses, luts, kpm = ctx.saved_tensors
+        sats, C, scale, p, seed, need_dlut = ctx.cfg
+        dmasks, ctx.dmasks = ctx.dmasks, None
+        W = q.shape[1] // C
+        do = do.contiguous()
+        dq = torch.zeros(q.shape, dtype=torch.float32, device=q.device)
+        dk = torch.zeros(k.shape, dtype=torch.float32, device=k.device)
+        dv = torch.zeros(v.shape, dtype=torch.float32, device=v.device)
+        dluts = torch.zeros_like(luts) if need_dlut else None
+        for qi in range(W):
+            sq = slice(qi * C, (qi + 1) * C)
+            do_q, o_q = do[:, sq].contiguous(), o[:, sq].contiguous()
+            for kj in range(W):
+                sk = slice(kj * C, (kj + 1) * C)
+                d = qi - kj + W - 1
+                km = kpm[:, sk].contiguous() if kpm is not None else None
+                a, b, c, dl = _block_bwd(do_q, q[:, sq], k[:, sk], v[:, sk], o_q, lses[qi], km,
+                                         luts[d] if luts is not None else None, sats[d] if sats is not None else None,
+                                         scale, p, _block_seed(seed, qi, kj), need_dlut, dmasks[(qi, kj)])
+                dq[:, sq] += a
+                dk[:, sk] += b
+                dv[:, sk] += c
+                if need_dlut:
+                    dluts[d] += dl
+        return dq.to(q.dtype), dk.to(k.dtype), dv.to(v.dtype), dluts, None, None, None, None, None, None
+
+
+def chunked_attention(q, k, v, *, chunk: int, scale: float = 1.0, key_padding_mask=None, bias_table=None,
+                      bidirectional: bool = True, num_buckets: int = 32, max_distance: int = 128,
+                      dropout_p: float = 0.0, seed: int = 0):
+    """Bidirectional self-attention over a long sequence on one device in ``chunk``-token blocks (the length
+    must divide by ``chunk``).  Same arguments as :func:`ring_attention`."""
+    N = q.shape[1]
+    assert N % chunk == 0 and k.shape[1] == N, "chunked_attention: length must divide by the chunk"
+    W = N // chunk
+    luts = sats = None
+    if bias_table is not None:
+        ls = [relative_bias_lut(bias_table, chunk, chunk, bidirectional, num_buckets, max_distance,
+                                q_offset=(d - (W - 1)) * chunk) for d in range(2 * W - 1)]
+        sats = [lt._dllm_sat for lt in ls]
+        luts = torch.stack(ls)
+    kpm = key_padding_mask.to(torch.uint8).contiguous() if key_padding_mask is not None else None
+    return _ChunkedAttnFn.apply(q, k, v, luts, kpm, sats, int(chunk), float(scale), float(dropout_p), int(seed))
+
+
+def long_sequence_chunk(n: int) -> int | None:
+    """Chunk size for an encoder of ``n`` tokens, or None when the single kernel handles it
+    (``DLLM_ATTN_CHUNK`` = block length, default 4096, used above ``DLLM_ATTN_CHUNK_MIN`` = 8192 tokens;
+    0 disables)."""
+    import os
+    c = int(os.environ.get("DLLM_ATTN_CHUNK", "4096"))
+    if c <= 0 or n <= max(int(os.environ.get("DLLM_ATTN_CHUNK_MIN", "8192")), c):
+        return None
+    w = -(-n // c)
+    while n % w:
+        w += 1
+    return n // w

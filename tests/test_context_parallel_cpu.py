@@ -136,3 +136,38 @@ def test_t5_context_parallel_matches_single_process(world):
         assert float(loss) == pytest.approx(float(ref.loss), rel=1e-5, abs=1e-6)
         for (n, p), gr in zip(model.named_parameters(), grads):
             torch.testing.assert_close(torch.as_tensor(gr), p.grad, atol=1e-5, rtol=1e-4, msg=n)
+
+
+def test_chunked_attention_matches_full():
+    from distributed_llms_example_amd.parallel.context import chunked_attention
+    q, k, v, table, do, kpm = _inputs(S=24)
+    o, dq, dk, dv, dt = _full(q, k, v, table, do, kpm, 1.0)
+    a = [t.clone().requires_grad_(True) for t in (q, k, v, table)]
+    oc = chunked_attention(a[0], a[1], a[2], chunk=8, key_padding_mask=kpm, bias_table=a[3])
+    oc.backward(do)
+    torch.testing.assert_close(oc.detach(), o, atol=2e-5, rtol=1e-4)
+    for x, y in zip(a, (dq, dk, dv, dt)):
+        torch.testing.assert_close(x.grad, y, atol=5e-5, rtol=1e-4)
+
+
+def test_t5_long_sequence_chunked_encoder(monkeypatch):
+    """Above DLLM_ATTN_CHUNK_MIN tokens the T5 encoder runs chunked attention: same loss and gradients."""
+    from distributed_llms_example_amd.models import build_model
+    torch.manual_seed(0)
+    model = build_model("t5-tiny").eval()
+    g = torch.Generator().manual_seed(5)
+    ids = torch.randint(3, 500, (2, 24), generator=g)
+    mask = torch.ones(2, 24, dtype=torch.long)
+    mask[1, 17:] = 0
+    lab = torch.randint(3, 500, (2, 6), generator=g)
+    ref = model(input_ids=ids, attention_mask=mask, labels=lab)
+    ref.loss.backward()
+    g_ref = [p.grad.clone() for p in model.parameters()]
+    model.zero_grad(set_to_none=True)
+    monkeypatch.setenv("DLLM_ATTN_CHUNK", "8")
+    monkeypatch.setenv("DLLM_ATTN_CHUNK_MIN", "16")
+    out = model(input_ids=ids, attention_mask=mask, labels=lab)
+    out.loss.backward()
+    assert float(out.loss) == pytest.approx(float(ref.loss), rel=1e-5)
+    for (n, p), gr in zip(model.named_parameters(), g_ref):
+        torch.testing.assert_close(p.grad, gr, atol=1e-5, rtol=1e-4, msg=n)

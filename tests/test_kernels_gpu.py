@@ -576,3 +576,33 @@ def test_ring_attention_single_rank_equals_attention():
     (o2.float() * g.float()).sum().backward()
     for x, y in zip(a + [t1], b + [t2]):
         assert _rel(x.grad, y.grad) < 2e-2, _rel(x.grad, y.grad)
+
+
+def test_chunked_attention_long_sequence():
+    """Single-GPU long encoder: 4K-token blocks merged by LSE equal the single kernel at 8K and the fp32
+    reference at 16K (beyond the single kernel's LDS-bounded length)."""
+    from distributed_llms_example_amd.parallel.context import chunked_attention
+    torch.manual_seed(11)
+    for N, H, full in ((8192, 4, "kernel"), (16384, 2, "reference")):
+        B, D = 1, 64
+        q, k, v = (torch.randn(B, N, H, D, device=DEV).to(torch.bfloat16) for _ in range(3))
+        mask = torch.ones(B, N, dtype=torch.bool, device=DEV)
+        mask[0, N - 1000:] = False
+        table = torch.randn(32, H, device=DEV) * 0.5
+        t1, t2 = table.clone().requires_grad_(True), table.clone().requires_grad_(True)
+        a = [t.clone().requires_grad_(True) for t in (q, k, v)]
+        o1 = chunked_attention(*a, chunk=4096, key_padding_mask=mask, bias_table=t1)
+        if full == "kernel":
+            b = [t.clone().requires_grad_(True) for t in (q, k, v)]
+            o2 = A.attention(*b, key_padding_mask=mask, bias_lut=A.relative_bias_lut(t2, N, N, True, 32, 128))
+        else:
+            b = [t.float().requires_grad_(True) for t in (q, k, v)]
+            o2 = A._reference(*b, 1.0, False, mask, A.relative_bias_lut(t2, N, N, True, 32, 128), 0.0, 0)
+        assert _rel(o1, o2) < 2e-2, (N, _rel(o1, o2))
+        g = torch.randn_like(o1)
+        (o1.float() * g.float()).sum().backward()
+        (o2.float() * g.float()).sum().backward()
+        for x, y in zip(a + [t1], b + [t2]):
+            assert _rel(x.grad, y.grad) < 3e-2, (N, _rel(x.grad, y.grad))
+        del o2, b
+        torch.cuda.empty_cache()
