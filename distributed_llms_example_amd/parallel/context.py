@@ -199,13 +199,13 @@ class _RingAttnFn(torch.autograd.Function):
         S = k.shape[1]
         do = do.contiguous()
         kv = torch.stack([k, v]).contiguous()
-        dkv = torch.zeros(kv.shape, dtype=torch.float32, device=kv.device)
         dq = torch.zeros(q.shape, dtype=torch.float32, device=q.device)
         dluts = torch.zeros_like(luts) if need_dlut else None
+        dkv_in = dworks = sending = None
         for step in range(W):
             src = (r - step) % W
             nxt_kv = works = None
-            if step < W - 1:  # the K/V shard moves on while this block computes; its dK/dV follow after
+            if step < W - 1:  # the K/V shard moves on while this block computes
                 nxt_kv, works = ring.start(kv)
             kpm = kpm_full[:, src * S:(src + 1) * S].contiguous() if kpm_full is not None else None
             lut = luts[src] if luts is not None else None
@@ -213,18 +213,26 @@ class _RingAttnFn(torch.autograd.Function):
             dq_b, dk_b, dv_b, dlut_b = _block_bwd(do, q, kv[0], kv[1], o, lse, kpm, lut, sat, scale, p,
                                                   _block_seed(seed, r, src), need_dlut, dmasks[src])
             dq += dq_b
-            dkv[0] += dk_b
-            dkv[1] += dv_b
             if need_dlut:
                 dluts[src] += dlut_b
-            # hand this shard's dK/dV accumulator to the rank that computes with the shard next
-            if W > 1:
-                nxt_dkv, dworks = ring.start(dkv)
+            if dworks is None:
+                acc = torch.stack([dk_b, dv_b]).float()
+            else:  # this shard's fp32 dK/dV accumulator, sent by the previous rank during this block
                 ring.wait(dworks)
-                dkv = nxt_dkv
+                acc = dkv_in
+                acc[0] += dk_b
+                acc[1] += dv_b
+            if W > 1:  # pass it on; the transfer overlaps the next block's compute
+                sending = acc
+                dkv_in, dworks = ring.start(sending)
             if works is not None:
                 ring.wait(works)
                 kv = nxt_kv
+        if W > 1:
+            ring.wait(dworks)
+            acc = dkv_in
+        dkv = acc
+        del sending
         # after W hops the accumulator that arrived belongs to this rank's own K/V shard
         return (dq.to(q.dtype), dkv[0].to(k.dtype), dkv[1].to(v.dtype), dluts, None, None, None, None, None, None)
 
