@@ -20,7 +20,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops import activations, attention as attn_ops, norms
-from ..parallel.context import chunked_attention, context_parallel_encode, long_sequence_chunk, ring_attention
+from ..parallel.context import (chunked_attention, chunked_cross_attention, context_parallel_encode,
+                                long_sequence_chunk, ring_attention)
 from ..ops.ffn import ffn
 from ..ops.cross_entropy import cross_entropy
 from ..ops.linear import Linear, stacked_linear
@@ -73,7 +74,13 @@ class T5Attention(nn.Module):
         kw = dict(scale=1.0, causal=causal, key_padding_mask=mask, bias_lut=lut, dropout_p=p, seed=seed)
         if self.cross:
             q = self.q(x).view(B, S, H, D)
-            o = attn_ops.attention_q_kv(q, kv if kv is not None else self.project_kv(kv_in), **kw)
+            kv = kv if kv is not None else self.project_kv(kv_in)
+            chunk = long_sequence_chunk(kv.shape[1]) if cache is None else None
+            if chunk is not None:  # long encoder output: key-chunked blocks merged by LSE
+                o = chunked_cross_attention(q, kv[:, :, 0], kv[:, :, 1], chunk=chunk, scale=1.0,
+                                            key_padding_mask=mask, dropout_p=p, seed=seed)
+            else:
+                o = attn_ops.attention_q_kv(q, kv, **kw)
         elif isinstance(lut, _CPBias):  # encoder sequence sharded over a CP group: ring attention
             qkv = self.qkv(x).view(B, S, 3, H, D)
             kw2 = dict(scale=1.0, key_padding_mask=mask, bias_table=lut.table, bidirectional=True,

@@ -341,11 +341,11 @@ class _ChunkedAttnFn(torch.autograd.Function):
     is the LUT of block offset d = qi - kj."""
 
     @staticmethod
-    def forward(ctx, q, k, v, luts, kpm, sats, C, scale, p, seed):
-        W = q.shape[1] // C
+    def forward(ctx, q, k, v, luts, kpm, sats, C, Cq, scale, p, seed):
+        W, Wq = k.shape[1] // C, q.shape[1] // Cq
         outs, lses, dmasks = [], [], {}
-        for qi in range(W):
-            qs = q[:, qi * C:(qi + 1) * C]
+        for qi in range(Wq):
+            qs = q[:, qi * Cq:(qi + 1) * Cq]
             o_acc = l_acc = None
             for kj in range(W):
                 d = qi - kj + W - 1
@@ -359,23 +359,23 @@ class _ChunkedAttnFn(torch.autograd.Function):
             lses.append(l_acc.contiguous())
         o = torch.cat(outs, 1)
         ctx.save_for_backward(q, k, v, o, torch.stack(lses), luts, kpm)
-        ctx.cfg = (sats, C, scale, p, seed, luts is not None and luts.requires_grad)
+        ctx.cfg = (sats, C, Cq, scale, p, seed, luts is not None and luts.requires_grad)
         ctx.dmasks = dmasks
         return o
 
     @staticmethod
     def backward(ctx, do):
         q, k, v, o, lses, luts, kpm = ctx.saved_tensors
-        sats, C, scale, p, seed, need_dlut = ctx.cfg
+        sats, C, Cq, scale, p, seed, need_dlut = ctx.cfg
         dmasks, ctx.dmasks = ctx.dmasks, None
-        W = q.shape[1] // C
+        W, Wq = k.shape[1] // C, q.shape[1] // Cq
         do = do.contiguous()
         dq = torch.zeros(q.shape, dtype=torch.float32, device=q.device)
         dk = torch.zeros(k.shape, dtype=torch.float32, device=k.device)
         dv = torch.zeros(v.shape, dtype=torch.float32, device=v.device)
         dluts = torch.zeros_like(luts) if need_dlut else None
-        for qi in range(W):
-            sq = slice(qi * C, (qi + 1) * C)
+        for qi in range(Wq):
+            sq = slice(qi * Cq, (qi + 1) * Cq)
             do_q, o_q = do[:, sq].contiguous(), o[:, sq].contiguous()
             for kj in range(W):
                 sk = slice(kj * C, (kj + 1) * C)
@@ -389,7 +389,18 @@ class _ChunkedAttnFn(torch.autograd.Function):
                 dv[:, sk] += c
                 if need_dlut:
                     dluts[d] += dl
-        return dq.to(q.dtype), dk.to(k.dtype), dv.to(v.dtype), dluts, None, None, None, None, None, None
+        return dq.to(q.dtype), dk.to(k.dtype), dv.to(v.dtype), dluts, None, None, None, None, None, None, None
+
+
+def chunked_cross_attention(q, k, v, *, chunk: int, scale: float = 1.0, key_padding_mask=None,
+                            dropout_p: float = 0.0, seed: int = 0):
+    """Cross-attention (no bias, not causal) of a short query over a long key sequence in ``chunk``-key blocks
+    (decoder over a long encoder output)."""
+    Sk = k.shape[1]
+    assert Sk % chunk == 0, "chunked_cross_attention: key length must divide by the chunk"
+    kpm = key_padding_mask.to(torch.uint8).contiguous() if key_padding_mask is not None else None
+    return _ChunkedAttnFn.apply(q, k, v, None, kpm, None, int(chunk), int(q.shape[1]), float(scale),
+                                float(dropout_p), int(seed))
 
 
 def chunked_attention(q, k, v, *, chunk: int, scale: float = 1.0, key_padding_mask=None, bias_table=None,
@@ -407,7 +418,8 @@ def chunked_attention(q, k, v, *, chunk: int, scale: float = 1.0, key_padding_ma
         sats = [lt._dllm_sat for lt in ls]
         luts = torch.stack(ls)
     kpm = key_padding_mask.to(torch.uint8).contiguous() if key_padding_mask is not None else None
-    return _ChunkedAttnFn.apply(q, k, v, luts, kpm, sats, int(chunk), float(scale), float(dropout_p), int(seed))
+    return _ChunkedAttnFn.apply(q, k, v, luts, kpm, sats, int(chunk), int(chunk), float(scale), float(dropout_p),
+                                int(seed))
 
 
 def long_sequence_chunk(n: int) -> int | None:
