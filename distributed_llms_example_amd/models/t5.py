@@ -75,7 +75,7 @@ class T5Attention(nn.Module):
         if self.cross:
             q = self.q(x).view(B, S, H, D)
             kv = kv if kv is not None else self.project_kv(kv_in)
-            chunk = long_sequence_chunk(kv.shape[1]) if cache is None else None
+            chunk = long_sequence_chunk(kv.shape[1], cross=True)
             if chunk is not None:  # long encoder output: key-chunked blocks merged by LSE
                 o = chunked_cross_attention(q, kv[:, :, 0], kv[:, :, 1], chunk=chunk, scale=1.0,
                                             key_padding_mask=mask, dropout_p=p, seed=seed)

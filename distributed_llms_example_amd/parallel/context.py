@@ -422,13 +422,17 @@ def chunked_attention(q, k, v, *, chunk: int, scale: float = 1.0, key_padding_ma
                                 int(seed))
 
 
-def long_sequence_chunk(n: int) -> int | None:
+def long_sequence_chunk(n: int, cross: bool = False) -> int | None:
     """Chunk size for an encoder of ``n`` tokens, or None when the single kernel handles it
     (``DLLM_ATTN_CHUNK`` = block length, default 4096, used above ``DLLM_ATTN_CHUNK_MIN`` = 8192 tokens;
-    0 disables)."""
+    0 disables).  Cross-attention (a short query: few workgroups per block) keeps the single kernel up to
+    its 16K-key limit and then uses 16K-key blocks."""
     import os
     c = int(os.environ.get("DLLM_ATTN_CHUNK", "4096"))
-    if c <= 0 or n <= max(int(os.environ.get("DLLM_ATTN_CHUNK_MIN", "8192")), c):
+    lo = int(os.environ.get("DLLM_ATTN_CHUNK_MIN", "8192"))
+    if cross and c > 0 and lo >= 8192:  # (test overrides with a small DLLM_ATTN_CHUNK_MIN chunk cross too)
+        c, lo = max(c, 16384), max(lo, 16384)
+    if c <= 0 or n <= max(lo, c):
         return None
     w = -(-n // c)
     while n % w:
