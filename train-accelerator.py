@@ -128,4 +128,7 @@ def run(args):
 
 
 if __name__ == "__main__":
-    run(base_parser("Train a Seq2Seq model").parse_args())
+    args = base_parser("Train a Seq2Seq model").parse_args()
+    if args.context_parallel > 1:
+        raise SystemExit("--context-parallel is implemented in train-torchrun.py (Trainer path)")
+    run(args)

@@ -143,6 +143,8 @@ def main():
     p.add_argument("--master-port", type=int, default=1234)
     p.add_argument("--overlap", action="store_true", help="overlap the gradient all-reduce with backward")
     args = p.parse_args()
+    if getattr(args, "context_parallel", 1) > 1:
+        raise SystemExit("--context-parallel is implemented in train-torchrun.py (Trainer path)")
     mp.set_start_method("spawn", force=True)
     if args.local_procs and args.local_procs > 0:
         url = f"tcp://127.0.0.1:{args.master_port}"
