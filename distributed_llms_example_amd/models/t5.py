@@ -189,7 +189,7 @@ class T5Stack(nn.Module):
         B, S = input_ids.shape
         k_len = S + q_offset
         cp = getattr(self, "_cp_group", False)
-        chunk = long_sequence_chunk(S) if not self.is_decoder and caches is None else None
+        chunk = long_sequence_chunk(S, rows=B * cfg.num_heads) if not self.is_decoder and caches is None else None
         if (cp is not False or chunk is not None) and not self.is_decoder:
             lut = _CPBias(cp, self.block[0].layer[0].SelfAttention.relative_attention_bias.weight,
                           chunk=chunk if cp is False else None)

@@ -103,7 +103,7 @@ def _block_fwd(q, k, v, kpm, lut, sat, scale, p, seed):
         C = _ext.native()
         lo, hi = sat if sat is not None else (-1, -1)
         o, lse, dmask = C.attn_fwd(q, k, v, kpm, lut, float(scale), False, float(p), int(seed), None, lo, hi)
-        return o.float(), lse, dmask
+        return o, lse, dmask  # bf16: the fp32 merge promotes (no separate conversion kernels)
     o, lse = _ref_block_fwd(q, k, v, kpm, lut, scale, p, seed)
     return o, lse, None
 
@@ -114,7 +114,7 @@ def _block_bwd(do, q, k, v, o, lse, kpm, lut, sat, scale, p, seed, need_dlut, dm
         lo, hi = sat if sat is not None else (-1, -1)
         dq, dk, dv, dlut = C.attn_bwd(do, q, k, v, o, lse, kpm, lut, float(scale), False, float(p), int(seed),
                                       bool(need_dlut), None, None, None, dmask, lo, hi)
-        return dq.float(), dk.float(), dv.float(), dlut
+        return dq, dk, dv, dlut  # bf16; accumulated into fp32 buffers by promoting in-place adds
     return _ref_block_bwd(do, q, k, v, o, lse, kpm, lut, scale, p, seed, need_dlut)
 
 
@@ -422,13 +422,14 @@ def chunked_attention(q, k, v, *, chunk: int, scale: float = 1.0, key_padding_ma
                                 int(seed))
 
 
-def long_sequence_chunk(n: int, cross: bool = False) -> int | None:
+def long_sequence_chunk(n: int, cross: bool = False, rows: int = 0) -> int | None:
     """Chunk size for an encoder of ``n`` tokens, or None when the single kernel handles it
     (``DLLM_ATTN_CHUNK`` = block length, default 4096, used above ``DLLM_ATTN_CHUNK_MIN`` = 8192 tokens;
-    0 disables).  Cross-attention (a short query: few workgroups per block) keeps the single kernel up to
+    0 disables).  ``rows`` = batch x heads: with fewer than 32 rows a 4K block launches under 1024 query-tile
+    workgroups (4 per CU), so the default block grows to 8K.  Cross-attention (a short query: few workgroups per block) keeps the single kernel up to
     its 16K-key limit and then uses 16K-key blocks."""
     import os
-    c = int(os.environ.get("DLLM_ATTN_CHUNK", "4096"))
+    c = int(os.environ.get("DLLM_ATTN_CHUNK", "8192" if 0 < rows < 32 else "4096"))
     lo = int(os.environ.get("DLLM_ATTN_CHUNK_MIN", "8192"))
     if cross and c > 0 and lo >= 8192:  # (test overrides with a small DLLM_ATTN_CHUNK_MIN chunk cross too)
         c, lo = max(c, 16384), max(lo, 16384)
