@@ -53,6 +53,14 @@ def parse():
     return ap.parse_args()
 
 
+def _rccl_version():
+    try:
+        v = torch.cuda.nccl.version()
+        return ".".join(str(x) for x in v) if isinstance(v, tuple) else str(v)
+    except Exception:  # noqa: BLE001 - informational only
+        return None
+
+
 def main():
     a = parse()
     from distributed_llms_example_amd.models import build_model, resolve_config
@@ -63,8 +71,9 @@ def main():
 
     env = init_distributed()
     n = env.world_size
-    if a.gpus != n and env.is_main_process:
-        print(f"[bench] note: --gpus {a.gpus} but WORLD_SIZE={n}; using {n}", file=sys.stderr)
+    if a.gpus != n:
+        raise SystemExit(f"[bench] --gpus {a.gpus} but WORLD_SIZE={n}: launch one rank per GPU "
+                         f"(python -m torch.distributed.run --nproc-per-node {a.gpus} bench.py --gpus {a.gpus})")
     torch.manual_seed(a.seed)
     manual_seed(a.seed * 1000 + env.rank)
     cfg = resolve_config(a.model)
@@ -128,7 +137,11 @@ def main():
             "config": {"model": a.model, "global_batch": B * n, "per_gpu_batch": B, "seq_len": S,
                        "target_len": T, "parallelism": f"dp{n}", "grad_ckpt": bool(a.grad_ckpt),
                        "bucket_mb": eng.reducer.bucket_sizes_mb()[1] if eng.reducer and len(eng.reducer.buckets) > 1 else None,
-                       "tokens_per_s": round(value * (S + T), 1)},
+                       "tokens_per_s": round(value * (S + T), 1),
+                       "grad_dtype": str(eng.flat.grad_buf.dtype).replace("torch.", ""),
+                       "backend": env.backend, "world_size": n, "rccl_version": _rccl_version(),
+                       "overlap": bool(eng.reducer.overlap) if eng.reducer else None,
+                       "n_buckets": len(eng.reducer.buckets) if eng.reducer else None},
         }), flush=True)
     if n > 1:
         dist.barrier()

@@ -88,13 +88,20 @@ extern "C" int dllm_sq_norm(const void* g, long n, float* part, float* out, int 
 
 extern "C" int dllm_adamw(void* param, float* master, const void* grad, float* m, float* v, const uint8_t* wd_mask,
                           const float* coef, long n, float lr, float b1, float b2, float eps, float wd, float bc1,
-                          float bc2, int is_bf16, hipStream_t st) {
+                          float bc2, int is_bf16, int grad_f32, hipStream_t st) {
   if (n % 4) return -2;
   const long n4 = n / 4;
   const int G = grid_for(n4, 4096);
   const float step_size = lr / bc1;
   const float inv_sqrt_bc2 = 1.f / sqrtf(bc2);
-  if (is_bf16) {
+  if (is_bf16 && grad_f32) {  // bf16 params, fp32 gradients (accumulated across micro-batches in fp32)
+    if (master)
+      hipLaunchKernelGGL((adamw_kernel<uint16_t, float, true>), dim3(G), dim3(256), 0, st, (uint16_t*)param, master,
+                         (const float*)grad, m, v, wd_mask, coef, n4, lr, b1, b2, eps, wd, step_size, inv_sqrt_bc2);
+    else
+      hipLaunchKernelGGL((adamw_kernel<uint16_t, float, false>), dim3(G), dim3(256), 0, st, (uint16_t*)param, master,
+                         (const float*)grad, m, v, wd_mask, coef, n4, lr, b1, b2, eps, wd, step_size, inv_sqrt_bc2);
+  } else if (is_bf16) {
     if (master)
       hipLaunchKernelGGL((adamw_kernel<uint16_t, uint16_t, true>), dim3(G), dim3(256), 0, st, (uint16_t*)param,
                          master, (const uint16_t*)grad, m, v, wd_mask, coef, n4, lr, b1, b2, eps, wd, step_size,

@@ -18,7 +18,7 @@ int dllm_norm_fwd(const void*, const void*, const void*, const void*, void*, voi
                   float, uint32_t, int, int, hipStream_t);
 int dllm_norm_bwd_grid(int);
 int dllm_norm_bwd(const void*, const void*, const void*, const void*, const float*, const float*, void*, void*,
-                  float*, float*, float*, float*, void*, void*, int, int, float, uint32_t, int, int, hipStream_t);
+                  float*, float*, float*, float*, void*, void*, int, int, float, uint32_t, int, int, int, hipStream_t);
 int dllm_act_fwd(const void*, void*, long, int, int, int, float, uint32_t, int, hipStream_t);
 int dllm_act_bwd(const void*, const void*, void*, long, int, int, int, float, uint32_t, int, hipStream_t);
 int dllm_dropout(const void*, void*, long, float, uint32_t, int, hipStream_t);
@@ -27,7 +27,7 @@ int dllm_ce_bwd(const float*, const void*, const int64_t*, const float*, const f
                 int, hipStream_t);
 int dllm_sq_norm(const void*, long, float*, float*, int, hipStream_t);
 int dllm_adamw(void*, float*, const void*, float*, float*, const uint8_t*, const float*, long, float, float, float,
-               float, float, float, float, int, hipStream_t);
+               float, float, float, float, int, int, hipStream_t);
 int dllm_attn_fwd(AttnParams*, hipStream_t);
 int dllm_attn_bwd(AttnParams*, hipStream_t);
 int dllm_attn_params_size();
@@ -35,6 +35,8 @@ int dllm_attn_dropout_mask(AttnParams*, hipStream_t);
 int dllm_gemm_wgrad(const GemmWgradParams*, int, hipStream_t);
 int dllm_gemm_fused(const GemmFusedParams*, int, int, hipStream_t);
 int dllm_colsum_rows();
+int dllm_embed_bwd(const int64_t*, const int64_t*, const void*, long, long, int, float*, void*, long, long, int,
+                   hipStream_t);
 int dllm_colsum_acc(const void*, long, long, int, float*, void*, int, hipStream_t);
 }
 
@@ -120,10 +122,12 @@ std::vector<Tensor> norm_bwd(const optional<Tensor>& dout_o, const optional<Tens
   // dw_acc / db_acc: accumulate the parameter gradients in place (param dtype, contiguous, d elements)
   const bool acc = dw_acc.has_value() && dw_acc->defined();
   if (acc) {
-    TORCH_CHECK(dw_acc->numel() == d && dw_acc->is_contiguous() && dw_acc->scalar_type() == s.scalar_type(),
+    // the flat gradient buffer: param dtype or fp32 (FlatParams grad_dtype)
+    TORCH_CHECK(dw_acc->numel() == d && dw_acc->is_contiguous() &&
+                    (dw_acc->scalar_type() == s.scalar_type() || dw_acc->scalar_type() == at::kFloat),
                 "dw_acc mismatch");
     TORCH_CHECK(!has_b || (db_acc.has_value() && db_acc->defined() && db_acc->numel() == d &&
-                           db_acc->is_contiguous() && db_acc->scalar_type() == s.scalar_type()),
+                           db_acc->is_contiguous() && db_acc->scalar_type() == dw_acc->scalar_type()),
                 "db_acc mismatch");
   }
   Tensor dw = acc ? Tensor() : at::zeros({d}, f32);
@@ -136,7 +140,7 @@ std::vector<Tensor> norm_bwd(const optional<Tensor>& dout_o, const optional<Tens
                            has_b ? db_part.data_ptr<float>() : nullptr, acc ? nullptr : dw.data_ptr<float>(),
                            (has_b && !acc) ? db.data_ptr<float>() : nullptr, acc ? dw_acc->data_ptr() : nullptr,
                            (acc && has_b) ? db_acc->data_ptr() : nullptr, N, d, (float)p, (uint32_t)seed, (int)kind,
-                           is_bf16(s), stream()),
+                           is_bf16(s), acc && dw_acc->scalar_type() == at::kFloat, stream()),
              "norm_bwd");
   return {dx, dstream, dw, db};
 }
@@ -239,7 +243,9 @@ void adamw_step(Tensor param, const optional<Tensor>& master, const Tensor& grad
   const long n = param.numel();
   TORCH_CHECK(n % 4 == 0 && param.is_contiguous() && grad.numel() == n && m.numel() == n && v.numel() == n,
               "adamw: flat buffers must match, numel % 4 == 0");
-  TORCH_CHECK(grad.scalar_type() == param.scalar_type(), "adamw: grad dtype must equal param dtype");
+  TORCH_CHECK(grad.scalar_type() == param.scalar_type() || grad.scalar_type() == at::kFloat,
+              "adamw: grad dtype must be the param dtype or fp32");
+  check_aligned(grad, 16, "adamw grad");
   TORCH_CHECK(m.scalar_type() == at::kFloat && v.scalar_type() == at::kFloat, "adamw: moments fp32");
   if (master.has_value() && master->defined())
     TORCH_CHECK(master->numel() == n && master->scalar_type() == at::kFloat, "adamw: master fp32 [n]");
@@ -252,7 +258,7 @@ void adamw_step(Tensor param, const optional<Tensor>& master, const Tensor& grad
                       m.data_ptr<float>(), v.data_ptr<float>(),
                       wd_mask.has_value() && wd_mask->defined() ? wd_mask->data_ptr<uint8_t>() : nullptr,
                       coef.data_ptr<float>(), n, (float)lr, (float)b1, (float)b2, (float)eps, (float)wd, (float)bc1,
-                      (float)bc2, is_bf16(param), stream()),
+                      (float)bc2, is_bf16(param), grad.scalar_type() == at::kFloat, stream()),
            "adamw");
 }
 
@@ -424,22 +430,27 @@ bool gemm_wgrad_supported(const Tensor& a, const Tensor& b, const Tensor& c) {
     return t.is_cuda() && t.dim() == 2 && t.scalar_type() == at::kBFloat16 && t.stride(1) == 1 && t.stride(0) % 8 == 0 &&
            reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0;
   };
-  if (!ok2(a) || !ok2(b) || !ok2(c)) return false;
+  const bool c_ok = c.is_cuda() && c.dim() == 2 && c.stride(1) == 1 && c.stride(0) % 8 == 0 &&
+                    (c.scalar_type() == at::kBFloat16 || c.scalar_type() == at::kFloat) &&
+                    reinterpret_cast<uintptr_t>(c.data_ptr()) % 16 == 0;
+  if (!ok2(a) || !ok2(b) || !c_ok) return false;
   const int64_t K = a.size(0), M = a.size(1), N = b.size(1);
-  return b.size(0) == K && c.size(0) == M && c.size(1) == N && K % 64 == 0 && K > 0 && M % 256 == 0 && N % 256 == 0 &&
+  return b.size(0) == K && c.size(0) == M && c.size(1) == N && K % 64 == 0 && K > 0 && M % 8 == 0 && M >= 8 &&
+         N % 256 == 0 &&
          K < (1LL << 31) && M * N < (1LL << 31);
 }
 
 int64_t gemm_wgrad(const Tensor& a, const Tensor& b, Tensor& c, bool beta, int64_t variant, int64_t splits_req) {
   TORCH_CHECK(gemm_wgrad_supported(a, b, c),
-              "gemm_wgrad: need bf16 GPU [K,M] x [K,N] -> [M,N], unit inner stride, 16-B aligned rows, K % 64 == 0, "
-              "M and N multiples of 256");
+              "gemm_wgrad: need bf16 GPU [K,M] x [K,N] -> bf16/fp32 [M,N], unit inner stride, 16-B aligned rows, K % 64 == 0, "
+              "M % 8 == 0, N a multiple of 256");
   TORCH_CHECK(a.device() == b.device() && a.device() == c.device(), "gemm_wgrad: device mismatch");
   const int K = a.size(0), M = a.size(1), N = b.size(1);
   GemmWgradParams P{};
   P.A = reinterpret_cast<const uint16_t*>(a.data_ptr());
   P.B = reinterpret_cast<const uint16_t*>(b.data_ptr());
-  P.C = reinterpret_cast<uint16_t*>(c.data_ptr());
+  P.C = c.data_ptr();
+  P.c_f32 = c.scalar_type() == at::kFloat ? 1 : 0;
   P.lda = a.stride(0);
   P.ldb = b.stride(0);
   P.ldc = c.stride(0);
@@ -447,7 +458,7 @@ int64_t gemm_wgrad(const Tensor& a, const Tensor& b, Tensor& c, bool beta, int64
   P.N = N;
   P.K = K;
   P.tn = N / 256;
-  P.ntiles = (M / 256) * (N / 256);
+  P.ntiles = ((M + 255) / 256) * (N / 256);  // ragged last M tile (vocab-sized LM-head gradients)
   P.beta = beta ? 1 : 0;
   // fill the 256 CUs once: split K until tiles x splits ~ 256, at least 4 k-stages of 64 per split
   int splits = splits_req > 0 ? (int)splits_req : std::max(1, 256 / P.ntiles);
@@ -588,6 +599,28 @@ void colsum_acc(const Tensor& x, Tensor& out) {
            "colsum_acc");
 }
 
+// out[ids[t]] += dy[t] for every token (sorted ids + their positions), deterministic (csrc/embed.hip)
+void embed_bwd(const Tensor& ids_sorted, const Tensor& perm, const Tensor& dy, Tensor& out, int64_t padding_idx) {
+  check_gpu(dy, "dy");
+  TORCH_CHECK(ids_sorted.scalar_type() == at::kLong && perm.scalar_type() == at::kLong && ids_sorted.dim() == 1 &&
+                  perm.sizes() == ids_sorted.sizes() && ids_sorted.is_contiguous() && perm.is_contiguous(),
+              "embed_bwd: ids / perm must be contiguous int64 [T]");
+  TORCH_CHECK(dy.dim() == 2 && dy.scalar_type() == at::kBFloat16 && dy.stride(1) == 1 && dy.stride(0) % 8 == 0 &&
+                  reinterpret_cast<uintptr_t>(dy.data_ptr()) % 16 == 0 && dy.size(0) == ids_sorted.size(0),
+              "embed_bwd: dy must be bf16 [T, d] with 16-B aligned rows");
+  const int64_t T = dy.size(0), d = dy.size(1);
+  TORCH_CHECK(d % 8 == 0 && d <= 2048, "embed_bwd: d must be a multiple of 8 and <= 2048");
+  TORCH_CHECK(out.is_cuda() && out.dim() == 2 && out.size(1) == d && out.is_contiguous() &&
+                  (out.scalar_type() == at::kBFloat16 || out.scalar_type() == at::kFloat),
+              "embed_bwd: out must be a contiguous bf16/fp32 [V, d] GPU tensor");
+  if (T == 0) return;
+  auto ws = at::empty({(T + 63) / 64 * d}, dy.options().dtype(at::kFloat));
+  check_rc(dllm_embed_bwd(ids_sorted.data_ptr<int64_t>(), perm.data_ptr<int64_t>(), dy.data_ptr(), dy.stride(0), T,
+                          (int)d, ws.data_ptr<float>(), out.data_ptr(), out.size(0), padding_idx,
+                          out.scalar_type() == at::kFloat, stream()),
+           "embed_bwd");
+}
+
 namespace dllm {
 void bind_reducer(pybind11::module& m);  // csrc/reducer.cpp
 }
@@ -604,6 +637,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ce_fwd", &ce_fwd);
   m.def("ce_bwd", &ce_bwd);
   m.def("sq_norm", &sq_norm);
+  m.def("embed_bwd", &embed_bwd);
   m.def("adamw_step", &adamw_step);
   m.def("attn_fwd", &attn_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("kpm"), py::arg("lut"),
         py::arg("scale"), py::arg("causal"), py::arg("p"), py::arg("seed"), py::arg("dmask_in") = py::none(),

@@ -95,7 +95,7 @@ __global__ __launch_bounds__((256 / (32 * NI)) * 2 * 64, 1) void gemm_wgrad_kern
   const int wm = w / WAVES_N, wn = w % WAVES_N;
   const int logical = xcd_remap(blockIdx.x, gridDim.x);
   const int s = logical / P.ntiles, t = logical % P.ntiles;
-  const int m0 = (t / P.tn) * BM, n0 = (t % P.tn) * BN;
+  const int m0 = (t / P.tn) * BM, n0 = (t % P.tn) * BN;  // rows m >= P.M of the last M tile: computed, not stored
   const int kbeg = s * P.kchunk;
   const int nk = min(P.kchunk, P.K - kbeg) / BK;
 
@@ -109,6 +109,11 @@ __global__ __launch_bounds__((256 / (32 * NI)) * 2 * 64, 1) void gemm_wgrad_kern
     srow[i] = r;
     scol[i] = ((lane & 31) ^ gsw(r)) << 3;
   }
+  // ragged last M tile (LM-head weight gradient, M = vocab): A columns past M re-read column M - 8 (finite values
+  // whose output rows are never stored; M % 8 == 0 keeps every 16-B chunk inside the row)
+  int acol[PW];
+#pragma unroll
+  for (int i = 0; i < PW; ++i) acol[i] = min(m0 + scol[i], P.M - 8) - m0;
   const uint32_t lds0 = lds_addr(lds);
   auto issue = [&](int buf, int kt) {
     const long k0 = (long)kt * BK;
@@ -117,7 +122,7 @@ __global__ __launch_bounds__((256 / (32 * NI)) * 2 * 64, 1) void gemm_wgrad_kern
 #pragma unroll
     for (int i = 0; i < PW; ++i) {
       const uint32_t rp = __builtin_amdgcn_readfirstlane(w * PW + i);
-      glds16(Ag + (k0 + srow[i]) * P.lda + scol[i], __builtin_amdgcn_readfirstlane(Al + rp * 1024u));
+      glds16(Ag + (k0 + srow[i]) * P.lda + acol[i], __builtin_amdgcn_readfirstlane(Al + rp * 1024u));
       glds16(Bg + (k0 + srow[i]) * P.ldb + scol[i], __builtin_amdgcn_readfirstlane(Bl + rp * 1024u));
     }
   };
@@ -188,14 +193,22 @@ __global__ __launch_bounds__((256 / (32 * NI)) * 2 * 64, 1) void gemm_wgrad_kern
       for (int i = 0; i < 8; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          uint16_t* cp = P.C + (long)(mrow + 16 * i) * P.ldc + ncol4 + 16 * j;
+          if (mrow + 16 * i >= P.M) continue;
+          const long ci = (long)(mrow + 16 * i) * P.ldc + ncol4 + 16 * j;
           f32x4 v = acc[i][j];
-          if (P.beta) {
-            const u16x4 c = *reinterpret_cast<const u16x4*>(cp);
-            v += f32x4{bf2f(c.x), bf2f(c.y), bf2f(c.z), bf2f(c.w)};
+          if (P.c_f32) {
+            float* cp = reinterpret_cast<float*>(P.C) + ci;
+            if (P.beta) v += *reinterpret_cast<const f32x4*>(cp);
+            *reinterpret_cast<f32x4*>(cp) = v;
+          } else {
+            uint16_t* cp = reinterpret_cast<uint16_t*>(P.C) + ci;
+            if (P.beta) {
+              const u16x4 c = *reinterpret_cast<const u16x4*>(cp);
+              v += f32x4{bf2f(c.x), bf2f(c.y), bf2f(c.z), bf2f(c.w)};
+            }
+            const u16x4 o = {f2bf(v.x), f2bf(v.y), f2bf(v.z), f2bf(v.w)};
+            *reinterpret_cast<u16x4*>(cp) = o;
           }
-          const u16x4 o = {f2bf(v.x), f2bf(v.y), f2bf(v.z), f2bf(v.w)};
-          *reinterpret_cast<u16x4*>(cp) = o;
         }
     } else {
       float* W = P.ws + (long)s * P.M * P.N;
@@ -203,7 +216,8 @@ __global__ __launch_bounds__((256 / (32 * NI)) * 2 * 64, 1) void gemm_wgrad_kern
       for (int i = 0; i < 8; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          *reinterpret_cast<f32x4*>(W + (long)(mrow + 16 * i) * P.N + ncol4 + 16 * j) = acc[i][j];
+          if (mrow + 16 * i < P.M)
+            *reinterpret_cast<f32x4*>(W + (long)(mrow + 16 * i) * P.N + ncol4 + 16 * j) = acc[i][j];
     }
     return;
   } else {
@@ -253,10 +267,18 @@ __global__ __launch_bounds__((256 / (32 * NI)) * 2 * 64, 1) void gemm_wgrad_kern
 #pragma unroll
         for (int reg = 0; reg < 16; ++reg) {
           const int m = m0 + wm * 128 + 32 * i + crow(reg, hh);
-          uint16_t* cp = P.C + (long)m * P.ldc + ncol + 32 * j;
+          if (m >= P.M) continue;
+          const long ci = (long)m * P.ldc + ncol + 32 * j;
           float v = acc[i][j][reg];
-          if (P.beta) v += bf2f(*cp);
-          *cp = f2bf(v);
+          if (P.c_f32) {
+            float* cp = reinterpret_cast<float*>(P.C) + ci;
+            if (P.beta) v += *cp;
+            *cp = v;
+          } else {
+            uint16_t* cp = reinterpret_cast<uint16_t*>(P.C) + ci;
+            if (P.beta) v += bf2f(*cp);
+            *cp = f2bf(v);
+          }
         }
   } else {
     float* W = P.ws + (long)s * P.M * P.N;
@@ -267,14 +289,15 @@ __global__ __launch_bounds__((256 / (32 * NI)) * 2 * 64, 1) void gemm_wgrad_kern
 #pragma unroll
         for (int reg = 0; reg < 16; ++reg) {
           const int m = m0 + wm * 128 + 32 * i + crow(reg, hh);
-          W[(long)m * P.N + ncol + 32 * j] = acc[i][j][reg];
+          if (m < P.M) W[(long)m * P.N + ncol + 32 * j] = acc[i][j][reg];
         }
   }
   }  // MF == 32
 }
 
-// C[m][n] = bf16(sum_s ws[s][m][n] (+ C[m][n])), 8 columns per thread (N % 8 == 0)
-__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws, uint16_t* __restrict__ C,
+// C[m][n] = sum_s ws[s][m][n] (+ C[m][n]), 8 columns per thread (N % 8 == 0); C bf16 or fp32 (TC)
+template <typename TC>
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws, TC* __restrict__ C,
                                                             long ldc, int M, int N, int splits, int beta) {
   const long n8 = (long)M * N / 8;
   const long slab = (long)M * N;
@@ -287,14 +310,23 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
       a += *reinterpret_cast<const f32x4*>(ws + s * slab + e);
       b += *reinterpret_cast<const f32x4*>(ws + s * slab + e + 4);
     }
-    uint16_t* cp = C + (long)m * ldc + n;
-    if (beta) {
-      const u16x8 c = *reinterpret_cast<const u16x8*>(cp);
-      a.x += bf2f(c[0]); a.y += bf2f(c[1]); a.z += bf2f(c[2]); a.w += bf2f(c[3]);
-      b.x += bf2f(c[4]); b.y += bf2f(c[5]); b.z += bf2f(c[6]); b.w += bf2f(c[7]);
+    TC* cp = C + (long)m * ldc + n;
+    if constexpr (sizeof(TC) == 4) {
+      if (beta) {
+        a += *reinterpret_cast<const f32x4*>(cp);
+        b += *reinterpret_cast<const f32x4*>(cp + 4);
+      }
+      *reinterpret_cast<f32x4*>(cp) = a;
+      *reinterpret_cast<f32x4*>(cp + 4) = b;
+    } else {
+      if (beta) {
+        const u16x8 c = *reinterpret_cast<const u16x8*>(cp);
+        a.x += bf2f(c[0]); a.y += bf2f(c[1]); a.z += bf2f(c[2]); a.w += bf2f(c[3]);
+        b.x += bf2f(c[4]); b.y += bf2f(c[5]); b.z += bf2f(c[6]); b.w += bf2f(c[7]);
+      }
+      const u16x8 o = {f2bf(a.x), f2bf(a.y), f2bf(a.z), f2bf(a.w), f2bf(b.x), f2bf(b.y), f2bf(b.z), f2bf(b.w)};
+      *reinterpret_cast<u16x8*>(cp) = o;
     }
-    const u16x8 o = {f2bf(a.x), f2bf(a.y), f2bf(a.z), f2bf(a.w), f2bf(b.x), f2bf(b.y), f2bf(b.z), f2bf(b.w)};
-    *reinterpret_cast<u16x8*>(cp) = o;
   }
 }
 
@@ -314,8 +346,12 @@ int launch_wgrad(const GemmWgradParams& p, hipStream_t st) {
   if (p.splits > 1) {
     const long n8 = (long)p.M * p.N / 8;
     const int blocks = (int)std::min<long>((n8 + 255) / 256, 2048);
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, p.ws, p.C, p.ldc, p.M, p.N, p.splits,
-                       p.beta);
+    if (p.c_f32)
+      hipLaunchKernelGGL(splitk_reduce_kernel<float>, dim3(blocks), dim3(256), 0, st, p.ws, (float*)p.C, p.ldc, p.M,
+                         p.N, p.splits, p.beta);
+    else
+      hipLaunchKernelGGL(splitk_reduce_kernel<uint16_t>, dim3(blocks), dim3(256), 0, st, p.ws, (uint16_t*)p.C, p.ldc,
+                         p.M, p.N, p.splits, p.beta);
     DLLM_CHECK_LAUNCH();
   }
   return 0;
@@ -331,7 +367,8 @@ extern "C" int dllm_gemm_wgrad_bk() { return 64; }
 // 7 / 8 / 9 = variants 0 / 4 / 3 on v_mfma_f32_16x16x32_bf16
 extern "C" int dllm_gemm_wgrad(const GemmWgradParams* pp, int variant, hipStream_t st) {
   const GemmWgradParams& p = *pp;
-  if (p.M % BM || p.N % BN || p.K <= 0 || p.splits < 1 || p.ntiles != (p.M / BM) * (p.N / BN)) return -4;
+  if (p.M % 8 || p.M < 8 || p.N % BN || p.K <= 0 || p.splits < 1 || p.ntiles != ((p.M + BM - 1) / BM) * (p.N / BN))
+    return -4;
   if (variant < 0)  // auto: 16x16x32 MFMA, BK=64 x 2, prioritised MFMA issue — fastest on every T5 / BART wgrad
     variant = 9;     // shape measured (profiles/r1_gemm_wgrad_bench_v3.jsonl: +3-11 % over the 32x32x16 variants)
   switch (variant) {

@@ -5,7 +5,7 @@
 struct GemmWgradParams {
   const uint16_t* A;  // [K][lda]
   const uint16_t* B;  // [K][ldb]
-  uint16_t* C;        // [M][ldc]
+  void* C;            // [M][ldc], bf16 or fp32 (c_f32): the flat gradient buffer's view
   float* ws;          // [splits][M][N] fp32 (splits > 1)
   long lda, ldb, ldc;
   int M, N, K;
@@ -14,6 +14,7 @@ struct GemmWgradParams {
   int kchunk;  // k rows per split (multiple of BK)
   int splits;
   int beta;  // 1: C += A^T B, 0: C = A^T B
+  int c_f32;  // C is fp32 (fp32 gradient accumulation across micro-batches), else bf16
 };
 
 // csrc/gemm_fused.hip: C[M][N] = epi(A[M][K] . B), B = [N][K] (b_kmajor = 0) or [K][N] (b_kmajor = 1)

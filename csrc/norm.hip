@@ -250,7 +250,7 @@ int launch_fwd(const void* x, const void* resid, const void* w, const void* b, v
 template <typename T, int KIND>
 int launch_bwd(const void* dout, const void* ds_extra, const void* s, const void* w, const float* mean,
                const float* rstd, void* dx, void* dstream, float* dw_part, float* db_part, float* dw, float* db,
-               void* dw_acc, void* db_acc, int N, int d, float p, uint32_t seed, int G, hipStream_t st) {
+               void* dw_acc, void* db_acc, int N, int d, float p, uint32_t seed, int G, int acc_f32, hipStream_t st) {
   const int chunks = (d + 255) / 256;
   dim3 grid(G), block(256);
   const size_t lds = (size_t)4 * d * sizeof(float);
@@ -274,7 +274,13 @@ int launch_bwd(const void* dout, const void* ds_extra, const void* s, const void
   else return -1;
 #undef L
   DLLM_CHECK_LAUNCH();
-  if (dw_acc != nullptr) {
+  if (dw_acc != nullptr && acc_f32) {  // fp32 flat gradient buffer
+    hipLaunchKernelGGL(col_sum_acc_kernel<float>, dim3((d + 63) / 64), dim3(1024), 0, st, dw_part, (float*)dw_acc, G,
+                       d);
+    if (db_part != nullptr)
+      hipLaunchKernelGGL(col_sum_acc_kernel<float>, dim3((d + 63) / 64), dim3(1024), 0, st, db_part, (float*)db_acc,
+                         G, d);
+  } else if (dw_acc != nullptr) {
     hipLaunchKernelGGL(col_sum_acc_kernel<T>, dim3((d + 63) / 64), dim3(1024), 0, st, dw_part, (T*)dw_acc, G, d);
     if (db_part != nullptr)
       hipLaunchKernelGGL(col_sum_acc_kernel<T>, dim3((d + 63) / 64), dim3(1024), 0, st, db_part, (T*)db_acc, G, d);
@@ -310,17 +316,17 @@ extern "C" int dllm_norm_bwd_grid(int N) {
 extern "C" int dllm_norm_bwd(const void* dout, const void* ds_extra, const void* s, const void* w, const float* mean,
                              const float* rstd, void* dx, void* dstream, float* dw_part, float* db_part, float* dw,
                              float* db, void* dw_acc, void* db_acc, int N, int d, float p, uint32_t seed, int kind,
-                             int is_bf16, hipStream_t st) {
+                             int is_bf16, int acc_f32, hipStream_t st) {
   if (d % 4 != 0) return -2;
   const int G = dllm_norm_bwd_grid(N);
   if (is_bf16) {
     return kind ? launch_bwd<uint16_t, 1>(dout, ds_extra, s, w, mean, rstd, dx, dstream, dw_part, db_part, dw, db, dw_acc, db_acc, N,
-                                          d, p, seed, G, st)
+                                          d, p, seed, G, acc_f32, st)
                 : launch_bwd<uint16_t, 0>(dout, ds_extra, s, w, mean, rstd, dx, dstream, dw_part, db_part, dw, db, dw_acc, db_acc, N,
-                                          d, p, seed, G, st);
+                                          d, p, seed, G, acc_f32, st);
   }
   return kind ? launch_bwd<float, 1>(dout, ds_extra, s, w, mean, rstd, dx, dstream, dw_part, db_part, dw, db, dw_acc, db_acc, N, d, p,
-                                     seed, G, st)
+                                     seed, G, acc_f32, st)
               : launch_bwd<float, 0>(dout, ds_extra, s, w, mean, rstd, dx, dstream, dw_part, db_part, dw, db, dw_acc, db_acc, N, d, p,
-                                     seed, G, st);
+                                     seed, G, acc_f32, st);
 }

@@ -48,5 +48,5 @@ def use_native(t: torch.Tensor) -> bool:
     if _load() is None:
         raise RuntimeError(
             "distributed_llms_example_amd._C (HIP kernels for gfx950) is not built/loadable: "
-            f"{_err!r}. Build it with `python setup.py build_ext --inplace` (or __graft_entry__.build()).")
+            f"{_err!r}. Build it with `python tools/build_native.py` (or __graft_entry__.build()).")
     return True

@@ -14,12 +14,12 @@ import math
 
 import torch
 import torch.nn as nn
-import torch.nn.functional as F
 
 from ..ops import activations, attention as attn_ops, norms
 from ..ops.ffn import ffn
 from ..ops.cross_entropy import cross_entropy
-from ..ops.linear import Linear, stacked_linear
+from ..ops.embedding import embedding
+from ..ops.linear import Linear, linear, stacked_linear
 from ..ops.rng import default_rng
 from .blocks import run_block
 from .config import Seq2SeqConfig
@@ -132,11 +132,11 @@ class BartStack(nn.Module):
         cfg = self.cfg
         p = cfg.dropout_rate if self.training else 0.0
         B, S = input_ids.shape
-        x = F.embedding(input_ids, self._embed[0].weight, padding_idx=cfg.pad_token_id)
+        x = embedding(input_ids, self._embed[0].weight, padding_idx=cfg.pad_token_id)
         if self.embed_scale != 1.0:
             x = x * self.embed_scale
         pos = torch.arange(q_offset, q_offset + S, device=input_ids.device) + BartLearnedPositionalEmbedding.offset
-        x = x + F.embedding(pos, self.embed_positions.weight).unsqueeze(0)
+        x = x + embedding(pos, self.embed_positions.weight).unsqueeze(0)
         h = norms.layer_norm(x, self.layernorm_embedding.weight, self.layernorm_embedding.bias, cfg.layer_norm_epsilon)
         h = activations.dropout(h, p, default_rng().next_seed() if p > 0 else 0)
         if self.is_decoder and cross_kv is None and enc_out is not None:
@@ -213,7 +213,7 @@ class BartForConditionalGeneration(nn.Module):
         return self.final_logits_bias.view(-1)
 
     def lm_logits(self, hidden):
-        return F.linear(hidden, self.output_embedding()) + self.final_logits_bias.to(hidden.dtype)
+        return linear(hidden, self.output_embedding()) + self.final_logits_bias.to(hidden.dtype)
 
     def cross_attention_modules(self):
         return [layer.encoder_attn for layer in self.model.decoder.layers]
@@ -252,7 +252,7 @@ class BartForConditionalGeneration(nn.Module):
         dec = self.decode(decoder_input_ids, enc, attention_mask)
         loss = None
         if labels is not None and not return_logits:
-            raw = F.linear(dec, self.output_embedding())
+            raw = linear(dec, self.output_embedding())
             V = raw.shape[-1]
             loss = cross_entropy(raw.view(-1, V), labels.reshape(-1), bias=self.logits_bias(),
                                  label_smoothing=label_smoothing, inplace_grad=True)

@@ -17,14 +17,14 @@ from __future__ import annotations
 
 import torch
 import torch.nn as nn
-import torch.nn.functional as F
 
 from ..ops import activations, attention as attn_ops, norms
 from ..parallel.context import (chunked_attention, chunked_cross_attention, context_parallel_encode,
                                 long_sequence_chunk, ring_attention)
 from ..ops.ffn import ffn
 from ..ops.cross_entropy import cross_entropy
-from ..ops.linear import Linear, stacked_linear
+from ..ops.embedding import embedding
+from ..ops.linear import Linear, linear, stacked_linear
 from ..ops.rng import default_rng
 from .blocks import run_block
 from .config import Seq2SeqConfig
@@ -185,7 +185,7 @@ class T5Stack(nn.Module):
         pa = cfg.attention_dropout if self.training else 0.0
         eps = cfg.layer_norm_epsilon
         rng = default_rng()
-        x = F.embedding(input_ids, self._embed[0].weight)
+        x = embedding(input_ids, self._embed[0].weight)
         B, S = input_ids.shape
         k_len = S + q_offset
         cp = getattr(self, "_cp_group", False)
@@ -298,7 +298,7 @@ class T5ForConditionalGeneration(nn.Module):
     def lm_logits(self, hidden):
         if self.config.scale_decoder_outputs:
             hidden = hidden * (self.config.d_model ** -0.5)
-        return F.linear(hidden, self.output_embedding())
+        return linear(hidden, self.output_embedding())
 
     def logits_bias(self):
         return None

@@ -37,7 +37,7 @@ import torch.nn.functional as F
 from .. import _ext
 from .activations import act_dropout
 from .gemm import bias_grad_accumulate, wgrad_accumulate
-from .linear import _fire, _fusable
+from .linear import _fire, _fusable, _gbuf, _use
 
 # activation -> (forward epilogue, backward epilogue) of csrc/gemm_fused.hip
 EPILOGUES = {"relu": (1, 3), "gelu": (2, 4), "gelu_new": (5, 6), "gelu_fast": (5, 6)}
@@ -71,6 +71,8 @@ class _FusedFFNFn(torch.autograd.Function):
         y = F.linear(h, wo, bo)
         ctx.save_for_backward(x2, h, u, mask)
         ctx.params = params
+        for q in params:
+            _use(q)
         ctx.cfg = (act, float(p), int(seed), shape)
         return y.view(*shape[:-1], wo.shape[0])
 
@@ -90,17 +92,17 @@ class _FusedFFNFn(torch.autograd.Function):
         else:
             du = C.gemm_fused(dy2, wo, True, ebwd, None, h if ebwd == 3 else u, None, p, seed, _VARIANT)
         with torch.no_grad():
-            wgrad_accumulate(Wo.grad, dy2, h)
+            wgrad_accumulate(_gbuf(Wo), dy2, h)
             if Bo is not None:
-                bias_grad_accumulate(Bo.grad, dy2)
+                bias_grad_accumulate(_gbuf(Bo), dy2)
         _fire(Wo)
         if Bo is not None:
             _fire(Bo)
         dx = torch.matmul(du, Wi.detach()) if ctx.needs_input_grad[0] else None
         with torch.no_grad():
-            wgrad_accumulate(Wi.grad, du, x2)
+            wgrad_accumulate(_gbuf(Wi), du, x2)
             if Bi is not None:
-                bias_grad_accumulate(Bi.grad, du)
+                bias_grad_accumulate(_gbuf(Bi), du)
         _fire(Wi)
         if Bi is not None:
             _fire(Bi)

@@ -1,8 +1,9 @@
 """Weight-gradient GEMM ``dW (+)= dYᵀ X`` on the hand-written gfx950 kernel (csrc/gemm.hip).
 
 Both operands are token-major ([tokens, features]), the reduction runs over tokens (10⁴-10⁵), and the
-result is accumulated straight into the bf16 flat gradient buffer.  Shapes the kernel does not cover
-(feature dims not multiples of 256, token counts not multiples of 64, CPU tensors) go to
+result is accumulated straight into the flat gradient buffer (bf16, or fp32 for fp32 gradient
+accumulation).  Shapes the kernel does not cover (N not a multiple of 256, M not of 8, token counts not
+multiples of 64, CPU tensors) go to
 ``torch.addmm`` (hipBLASLt / CPU BLAS).  ``DLLM_NATIVE_WGRAD=0`` forces the library path (A/B runs).
 """
 from __future__ import annotations
@@ -28,6 +29,9 @@ def wgrad_accumulate(out: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, bet
     if _native_ok(dy2, x2, out):
         _ext.native().gemm_wgrad(dy2, x2, out, beta, _VARIANT, 0)
         return out
+    if out.dtype != dy2.dtype:  # fp32 gradient buffer, bf16 operands: library GEMM, then one fp32 add
+        g = torch.mm(dy2.t(), x2)
+        return out.add_(g) if beta else out.copy_(g)
     if beta:
         return out.addmm_(dy2.t(), x2)
     return torch.mm(dy2.t(), x2, out=out)

@@ -1,7 +1,7 @@
 """Linear layer whose weight gradient is accumulated by the GEMM itself into the flat gradient buffer.
 
-With parameters living in FlatParams (parallel/flat.py) every ``p.grad`` is a view of one gradient
-buffer.  Through plain autograd the weight-gradient GEMM writes a fresh ``[out, in]`` tensor and
+With parameters living in FlatParams (parallel/flat.py) every parameter's gradient is a slice of one
+gradient buffer (``p.grad`` itself, or ``p._dllm_gbuf`` when that buffer is fp32 for bf16 weights).  Through plain autograd the weight-gradient GEMM writes a fresh ``[out, in]`` tensor and
 AccumulateGrad then adds it into that view — an extra read+write of every weight gradient and one
 elementwise kernel per parameter per micro-batch (≈200 launches per T5-base step).  Here the backward
 issues ``grad.addmm_(dyᵀ, x)`` (β = 1): hipBLASLt accumulates straight into the flat buffer in its
@@ -9,7 +9,7 @@ epilogue, and the post-accumulate hooks the gradient reducer relies on (parallel
 by hand because AccumulateGrad never runs for the weight.
 
 The fused path is taken only when the weight is marked by FlatParams (``_dllm_fused_wgrad``) and its
-``.grad`` is a live tensor; anything else (plain modules, ``zero_grad(set_to_none=True)``) falls back to
+flat-buffer gradient slice is live; anything else (plain modules, ``zero_grad(set_to_none=True)``) falls back to
 ordinary autograd with identical results.
 """
 from __future__ import annotations
@@ -21,7 +21,37 @@ import torch.nn.functional as F
 from .gemm import bias_grad_accumulate, wgrad_accumulate
 
 
+def _gbuf(p: torch.Tensor | None) -> torch.Tensor | None:
+    """The slice of the flat gradient buffer a fused op accumulates ``p``'s gradient into (parallel/flat.py).
+
+    With fp32 gradients for bf16 parameters that slice cannot be ``p.grad`` (autograd insists on equal
+    dtypes), so FlatParams hands it over as ``p._dllm_gbuf``; otherwise it is ``p.grad`` itself."""
+    if p is None:
+        return None
+    g = getattr(p, "_dllm_gbuf", None)
+    return g if g is not None else p.grad
+
+
+def _use(p: torch.Tensor | None) -> None:
+    """Forward: one more fused gradient contribution to ``p`` is pending for the coming backward.
+
+    A parameter can feed several fused ops (the tied T5/BART embedding: encoder and decoder embedding
+    lookups + the LM head); its reducer hooks must fire once, after the LAST contribution.  Forwards
+    that run inside backward (activation-checkpoint recomputation) are not counted: their autograd
+    nodes are never run, the original forward's are."""
+    if p is None or torch._C._current_graph_task_id() != -1:
+        return
+    p._dllm_pending = getattr(p, "_dllm_pending", 0) + 1
+    p._dllm_fused_seen = True
+
+
 def _fire(p: torch.Tensor) -> None:
+    """Backward: one fused contribution to ``p`` has been accumulated; run the post-accumulate hooks
+    (gradient reducer) when it was the last one."""
+    n = getattr(p, "_dllm_pending", 1) - 1
+    p._dllm_pending = n if n > 0 else 0
+    if n > 0:
+        return
     for h in getattr(p, "_dllm_post_hooks", ()):
         h(p)
 
@@ -30,9 +60,11 @@ class _LinearAccumFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, params):
         # weight/bias arrive detached (no autograd edge → no AccumulateGrad node, no double hook);
-        # ``params`` carries the Parameters themselves, whose .grad views are accumulated into below
+        # ``params`` carries the Parameters themselves, whose flat-buffer gradients are accumulated into below
         ctx.save_for_backward(x)
         ctx.weight, ctx.bias = params
+        _use(params[0])
+        _use(params[1])
         return F.linear(x, weight, bias)
 
     @staticmethod
@@ -43,9 +75,9 @@ class _LinearAccumFn(torch.autograd.Function):
         dy2 = dy.reshape(-1, dy.shape[-1])
         x2 = x.reshape(-1, x.shape[-1])
         with torch.no_grad():
-            wgrad_accumulate(w.grad, dy2, x2)
+            wgrad_accumulate(_gbuf(w), dy2, x2)
             if bias is not None:
-                bias_grad_accumulate(bias.grad, dy2)
+                bias_grad_accumulate(_gbuf(bias), dy2)
         _fire(w)
         if bias is not None:
             _fire(bias)
@@ -53,17 +85,21 @@ class _LinearAccumFn(torch.autograd.Function):
 
 
 def _fusable(p: torch.Tensor | None) -> bool:
-    return p is None or (getattr(p, "_dllm_fused_wgrad", False) and p.grad is not None and p.requires_grad)
+    return p is None or (getattr(p, "_dllm_fused_wgrad", False) and p.requires_grad and _gbuf(p) is not None)
+
+
+def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Tensor:
+    """Functional ``F.linear`` with the weight gradient accumulated by the GEMM (e.g. a tied LM head)."""
+    if torch.is_grad_enabled() and _fusable(weight) and _fusable(bias):
+        return _LinearAccumFn.apply(x, weight.detach(), None if bias is None else bias.detach(), (weight, bias))
+    return F.linear(x, weight, bias)
 
 
 class Linear(nn.Linear):
     """Drop-in ``nn.Linear`` (same parameters / state-dict keys / init) with GEMM-fused grad accumulation."""
 
     def forward(self, x):
-        if torch.is_grad_enabled() and _fusable(self.weight) and _fusable(self.bias):
-            b = self.bias
-            return _LinearAccumFn.apply(x, self.weight.detach(), None if b is None else b.detach(), (self.weight, b))
-        return F.linear(x, self.weight, self.bias)
+        return linear(x, self.weight, self.bias)
 
 
 # ------------------------------------------------------------------------------------------------
@@ -99,6 +135,8 @@ class _StackedFn(torch.autograd.Function):
             outs.append(o)
         ctx.save_for_backward(x)
         ctx.W, ctx.gbuf, ctx.params, ctx.n = W, gbuf, (ws, bs), n
+        for q in list(ws) + list(bs):
+            _use(q)
         return tuple(outs)
 
     @staticmethod
@@ -118,21 +156,21 @@ class _StackedFn(torch.autograd.Function):
         x2 = x.reshape(-1, x.shape[-1])
         dx = torch.matmul(G2, W).view(x.shape) if ctx.needs_input_grad[0] else None
         with torch.no_grad():
-            gw = _adjacent([w.grad for w in ws])
+            gw = _adjacent([_gbuf(w) for w in ws])
             if gw is not None:
                 wgrad_accumulate(gw, G2, x2)
             else:
                 dW = G2.t() @ x2
                 for l, w in enumerate(ws):
-                    w.grad.add_(dW[l * n:(l + 1) * n])
+                    _gbuf(w).add_(dW[l * n:(l + 1) * n])
             if bs[0] is not None:
-                gb = _adjacent([bb.grad for bb in bs])
+                gb = _adjacent([_gbuf(bb) for bb in bs])
                 if gb is not None:
                     bias_grad_accumulate(gb, G2)
                 else:
                     db = G2.sum(0)
                     for l, bb in enumerate(bs):
-                        bb.grad.add_(db[l * n:(l + 1) * n])
+                        _gbuf(bb).add_(db[l * n:(l + 1) * n])
         ctx.gbuf = None
         for p in list(ws) + [bb for bb in bs if bb is not None]:
             _fire(p)

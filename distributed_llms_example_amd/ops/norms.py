@@ -15,7 +15,7 @@ from __future__ import annotations
 import torch
 
 from .. import _ext
-from .linear import _fire, _fusable
+from .linear import _fire, _fusable, _gbuf, _use
 from .rng import keep_mask
 
 RMS, LAYER = 0, 1
@@ -47,6 +47,8 @@ class _NormFn(torch.autograd.Function):
     def forward(ctx, x, resid, weight, bias, eps, p, seed, kind, params=None):
         C = _ext.native()
         ctx.params = params
+        for q in params or ():
+            _use(q)
         shape = x.shape
         d = shape[-1]
         x2 = x.reshape(-1, d)
@@ -83,6 +85,8 @@ class _NormOnlyFn(torch.autograd.Function):
     def forward(ctx, x, weight, bias, eps, kind, params=None):
         C = _ext.native()
         ctx.params = params
+        for q in params or ():
+            _use(q)
         shape = x.shape
         x2 = x.reshape(-1, shape[-1])
         out, _, mean, rstd = C.norm_fwd(x2, None, weight, bias, float(eps), 0.0, 0, int(kind), False)
@@ -105,7 +109,7 @@ def _acc_targets(params):
     if params is None:
         return None, None
     w, b = params
-    return w.grad, (b.grad if b is not None else None)
+    return _gbuf(w), _gbuf(b)
 
 
 def _param_grads(params, weight, bias, dw, db):

@@ -392,24 +392,50 @@ class _ChunkedAttnFn(torch.autograd.Function):
         return dq.to(q.dtype), dk.to(k.dtype), dv.to(v.dtype), dluts, None, None, None, None, None, None, None
 
 
+def _pad_seq(x, n):
+    """[B, S, ...] zero-padded at the end of the sequence dim to length n."""
+    S = x.shape[1]
+    if S == n:
+        return x
+    return torch.cat([x, x.new_zeros((x.shape[0], n - S) + tuple(x.shape[2:]))], 1)
+
+
+def _padded_kpm(key_padding_mask, B, S, n, device):
+    """uint8 key mask for a sequence padded from S to n keys (the padding is masked out), or None."""
+    if key_padding_mask is None and n == S:
+        return None
+    kpm = (key_padding_mask.to(torch.uint8) if key_padding_mask is not None
+           else torch.ones(B, S, dtype=torch.uint8, device=device))
+    return _pad_seq(kpm, n).contiguous()
+
+
 def chunked_cross_attention(q, k, v, *, chunk: int, scale: float = 1.0, key_padding_mask=None,
                             dropout_p: float = 0.0, seed: int = 0):
     """Cross-attention (no bias, not causal) of a short query over a long key sequence in ``chunk``-key blocks
-    (decoder over a long encoder output)."""
+    (decoder over a long encoder output).  A key length that is not a multiple of ``chunk`` is padded with
+    masked keys (ragged last block)."""
     Sk = k.shape[1]
-    assert Sk % chunk == 0, "chunked_cross_attention: key length must divide by the chunk"
-    kpm = key_padding_mask.to(torch.uint8).contiguous() if key_padding_mask is not None else None
-    return _ChunkedAttnFn.apply(q, k, v, None, kpm, None, int(chunk), int(q.shape[1]), float(scale),
-                                float(dropout_p), int(seed))
+    n = -(-Sk // chunk) * chunk
+    kpm = _padded_kpm(key_padding_mask, k.shape[0], Sk, n, k.device)
+    return _ChunkedAttnFn.apply(q, _pad_seq(k, n), _pad_seq(v, n), None, kpm, None, int(chunk), int(q.shape[1]),
+                                float(scale), float(dropout_p), int(seed))
 
 
 def chunked_attention(q, k, v, *, chunk: int, scale: float = 1.0, key_padding_mask=None, bias_table=None,
                       bidirectional: bool = True, num_buckets: int = 32, max_distance: int = 128,
                       dropout_p: float = 0.0, seed: int = 0):
-    """Bidirectional self-attention over a long sequence on one device in ``chunk``-token blocks (the length
-    must divide by ``chunk``).  Same arguments as :func:`ring_attention`."""
-    N = q.shape[1]
-    assert N % chunk == 0 and k.shape[1] == N, "chunked_attention: length must divide by the chunk"
+    """Bidirectional self-attention over a long sequence on one device in ``chunk``-token blocks.  Same arguments
+    as :func:`ring_attention`.  A length that is not a multiple of ``chunk`` is padded at the end (padded keys
+    masked, padded query rows dropped; real tokens keep their positions, so the relative bias is unchanged)."""
+    N0 = q.shape[1]
+    assert k.shape[1] == N0, "chunked_attention: self-attention needs equal query / key lengths"
+    N = -(-N0 // chunk) * chunk
+    if N != N0:
+        kpm = _padded_kpm(key_padding_mask, q.shape[0], N0, N, q.device)
+        o = chunked_attention(_pad_seq(q, N), _pad_seq(k, N), _pad_seq(v, N), chunk=chunk, scale=scale,
+                              key_padding_mask=kpm, bias_table=bias_table, bidirectional=bidirectional,
+                              num_buckets=num_buckets, max_distance=max_distance, dropout_p=dropout_p, seed=seed)
+        return o[:, :N0]
     W = N // chunk
     luts = sats = None
     if bias_table is not None:
@@ -435,7 +461,8 @@ def long_sequence_chunk(n: int, cross: bool = False, rows: int = 0) -> int | Non
         c, lo = max(c, 16384), max(lo, 16384)
     if c <= 0 or n <= max(lo, c):
         return None
+    # ceil(n / c) blocks of equal length (a multiple of 128, the kernels' query tile); chunked_attention pads the
+    # sequence to blocks x chunk with masked keys, so any n (primes too) keeps blocks near c
     w = -(-n // c)
-    while n % w:
-        w += 1
-    return n // w
+    g = min(128, c)
+    return -(-n // (w * g)) * g

@@ -1,7 +1,9 @@
 """Flat parameter / gradient storage.
 
-Every trainable parameter becomes a view into ONE contiguous parameter buffer and its ``.grad`` a
-view into ONE contiguous gradient buffer, laid out in reverse registration order (≈ the order in
+Every trainable parameter becomes a view into ONE contiguous parameter buffer and its gradient a
+view into ONE contiguous gradient buffer (``p.grad`` when the buffer has the parameter dtype; with
+fp32 gradients for bf16 weights — the default of train/engine.py, matching the reference's fp32
+gradients — ``p._dllm_gbuf``, which the fused ops accumulate into), laid out in reverse registration order (≈ the order in
 which backward produces gradients).  This is the memory layout the whole runtime is built on:
 
 * the gradient reducer (parallel/reducer.py) all-reduces contiguous slices of the gradient buffer
@@ -79,13 +81,25 @@ class FlatParams:
         self.numel = off
         self.param_buf = torch.zeros(off, dtype=self.dtype, device=self.device)
         self.grad_buf = torch.zeros(off, dtype=self.grad_dtype, device=self.device)
+        # autograd insists p.grad has p's dtype: with fp32 gradients for bf16 weights the flat slices are handed
+        # to the fused ops as p._dllm_gbuf instead, and p.grad stays None
+        self.views_as_grad = self.grad_dtype == self.dtype
+        fused = os.environ.get("DLLM_FUSED_WGRAD", "1") != "0"
+        if not self.views_as_grad and not fused:
+            raise ValueError("fp32 gradients for low-precision parameters need the fused gradient paths "
+                             "(DLLM_FUSED_WGRAD=1)")
+        self._hooks = []
         with torch.no_grad():
-            for seg, p in zip(self.segments, self.params):
+            for i, (seg, p) in enumerate(zip(self.segments, self.params)):
                 view = self.param_buf[seg.offset:seg.offset + seg.numel].view(seg.shape)
                 view.copy_(p.data)
                 p.data = view
                 # ops/linear.py may accumulate this parameter's weight gradient inside the GEMM
-                p._dllm_fused_wgrad = os.environ.get("DLLM_FUSED_WGRAD", "1") != "0"
+                p._dllm_fused_wgrad = fused
+                p._dllm_gbuf = self.grad_view(i)
+                p._dllm_pending = 0
+                p._dllm_fused_seen = False
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._autograd_hook))
         self.attach_grads()
 
     # -------------------------------------------------------------------------------------------
@@ -93,18 +107,48 @@ class FlatParams:
         seg = self.segments[i]
         return self.grad_buf[seg.offset:seg.offset + seg.numel].view(seg.shape)
 
+    @staticmethod
+    def _autograd_hook(p) -> None:
+        """A gradient that arrived through ordinary autograd (AccumulateGrad: e.g. T5's relative-position
+        bias table): fold it into the flat buffer when ``p.grad`` is not the flat slice itself (fp32 buffer,
+        or a user-replaced .grad), then run the reducer hooks like the fused ops do (ops/linear.py)."""
+        g = p.grad
+        gb = p._dllm_gbuf
+        if getattr(p, "_dllm_fused_seen", False):
+            raise RuntimeError(f"parameter {tuple(p.shape)} receives gradients both from fused ops and from autograd; route all of "
+                               "its uses through ops.linear / ops.embedding (or none)")
+        if g is not None and g.data_ptr() != gb.data_ptr():
+            gb.add_(g)
+            p.grad = gb if gb.dtype == p.dtype else None
+        for h in getattr(p, "_dllm_post_hooks", ()):
+            h(p)
+
     def attach_grads(self) -> None:
-        """(Re)bind every ``p.grad`` to its slice of the flat gradient buffer."""
+        """(Re)bind every ``p.grad`` to its slice of the flat gradient buffer (same-dtype buffer only)."""
         for i, p in enumerate(self.params):
-            p.grad = self.grad_view(i)
+            p.grad = self.grad_view(i) if self.views_as_grad else None
+
+    def reset_pending(self) -> None:
+        """Forget fused-use counts of a forward that never ran backward (ops/linear.py ``_use``)."""
+        for p in self.params:
+            p._dllm_pending = 0
+            p._dllm_fused_seen = False
 
     def zero_grad(self) -> None:
         self.grad_buf.zero_()
+        self.reset_pending()
         # something (e.g. user code) may have replaced a .grad: re-bind cheaply
         for i, p in enumerate(self.params):
             g = p.grad
-            if g is None or g.data_ptr() != self.grad_buf.data_ptr() + self.segments[i].offset * self.grad_buf.element_size():
+            if not self.views_as_grad:
+                if g is not None:
+                    p.grad = None
+            elif g is None or g.data_ptr() != self.grad_buf.data_ptr() + self.segments[i].offset * self.grad_buf.element_size():
                 p.grad = self.grad_view(i)
+
+    def grads(self) -> list[torch.Tensor]:
+        """Per-parameter gradient views of the flat buffer (fp32 or param dtype), in ``params`` order."""
+        return [self.grad_view(i) for i in range(len(self.params))]
 
     def decay_mask(self, no_decay_pred) -> torch.Tensor | None:
         """uint8 mask over the flat buffer: 1 where weight decay applies; None if uniform."""

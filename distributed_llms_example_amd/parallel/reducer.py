@@ -18,8 +18,9 @@ Replaces torch DDP's C++ Reducer that the reference reaches through HF Trainer /
 * ``overlap=False`` → one coalesced all-reduce after backward (train-task semantics, same math).
 
 Two engines implement the same bucket/launch policy: the native one (csrc/reducer.cpp,
-``NativeReducer``: C++ post hooks on the AccumulateGrad nodes, bucket state machine and c10d
-``ProcessGroup::allreduce`` launches in C++ — the counterpart of DDP's C++ Reducer) is used whenever the
+``NativeReducer``: bucket state machine and c10d ``ProcessGroup::allreduce`` launches in C++ — the
+counterpart of DDP's C++ Reducer; readiness is signalled per parameter by FlatParams' post-accumulate
+hooks and by the fused ops, ops/linear.py ``_fire``) is used whenever the
 extension is built (``DLLM_NATIVE_REDUCER=0`` selects the Python engine below, kept as the readable
 reference and for A/B tests).  Bucket layout is computed here once and handed to either engine.
 """
@@ -86,8 +87,7 @@ class GradReducer:
             bounds = [x for se in self.buckets for x in se]
             self.native = _ext.native().NativeReducer(flat.grad_buf, bounds, self.seg_bucket, pg, average,
                                                       self.backend == "nccl")
-            if overlap:
-                self.native.attach_hooks(list(flat.params))
+            if overlap:  # readiness comes from FlatParams' hooks / the fused ops (ops/linear.py _fire)
                 for i, p in enumerate(flat.params):
                     p._dllm_post_hooks = getattr(p, "_dllm_post_hooks", []) + [
                         (lambda _q, i=i, nat=self.native: nat.mark_ready(i))]
@@ -95,8 +95,8 @@ class GradReducer:
         elif self.world > 1 and overlap:
             for i, p in enumerate(flat.params):
                 h = self._make_hook(i)
-                self._hooks.append(p.register_post_accumulate_grad_hook(h))
-                # fired by ops/linear.py when the GEMM accumulated the gradient (AccumulateGrad skipped)
+                # run by FlatParams' post-accumulate hook (autograd gradients) or by the fused op that accumulated
+                # the gradient in its kernel (ops/linear.py _fire), once per backward after the last contribution
                 p._dllm_post_hooks = getattr(p, "_dllm_post_hooks", []) + [h]
                 self._manual.append(p)
 

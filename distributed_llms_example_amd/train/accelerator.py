@@ -31,6 +31,7 @@ from ..parallel.env import init_distributed
 from ..parallel.flat import FlatParams
 from ..parallel.reducer import DEFAULT_BUCKET_MB, GradReducer
 from ..parallel.sampler import ShardedBatchSampler
+from .engine import default_grad_dtype
 from .schedule import LRScheduler
 
 
@@ -188,7 +189,7 @@ class Accelerator:
 
     def prepare_model(self, model):
         model = model.to(device=self.device, dtype=self.dtype)
-        flat = FlatParams(model)
+        flat = FlatParams(model, grad_dtype=default_grad_dtype(self.dtype))  # fp32 gradients (train/engine.py)
         reducer = None
         if self.env.world_size > 1:
             reducer = GradReducer(flat, bucket_mb=self.bucket_mb, overlap=self.overlap_comm)

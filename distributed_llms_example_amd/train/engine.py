@@ -8,6 +8,7 @@ north star: "both loops dispatch to the same kernel library").
 from __future__ import annotations
 
 import contextlib
+import os
 
 import torch
 
@@ -22,15 +23,30 @@ def default_no_decay(name: str) -> bool:
     return n.endswith(".bias") or "layer_norm" in n or "layernorm" in n or "norm.weight" in n
 
 
+def default_grad_dtype(param_dtype: torch.dtype) -> torch.dtype:
+    """Gradient buffer dtype: fp32 (the reference's HF Trainer / Accelerate keep fp32 gradients, and GA sums
+    16 micro-batches, ref/train-torchrun.py:126) unless ``DLLM_GRAD_DTYPE=bf16`` opts into param-dtype
+    gradients (half the all-reduce bytes, every accumulation rounded to 8 mantissa bits)."""
+    choice = os.environ.get("DLLM_GRAD_DTYPE", "fp32").lower()
+    if choice in ("bf16", "param", "same"):
+        return param_dtype
+    return torch.float32
+
+
+def token_count(labels: torch.Tensor, ignore_index: int = -100) -> torch.Tensor:
+    """Non-ignored target tokens of a micro-batch, as a device scalar (no host sync)."""
+    return (labels != ignore_index).sum()
+
+
 class TrainEngine:
     def __init__(self, model: torch.nn.Module, env: DistEnv, *, lr: float = 5e-5, weight_decay: float = 0.0,
                  betas=(0.9, 0.999), eps: float = 1e-8, max_grad_norm: float | None = 1.0,
                  dtype: torch.dtype = torch.bfloat16, bucket_mb: float = DEFAULT_BUCKET_MB, overlap: bool = True,
-                 no_decay=default_no_decay, label_smoothing: float = 0.0):
+                 no_decay=default_no_decay, label_smoothing: float = 0.0, grad_dtype: torch.dtype | None = None):
         self.env = env
         self.model = model.to(device=env.device, dtype=dtype)
         self.dtype = dtype
-        self.flat = FlatParams(self.model)
+        self.flat = FlatParams(self.model, grad_dtype=grad_dtype or default_grad_dtype(dtype))
         self.reducer = GradReducer(self.flat, bucket_mb=bucket_mb, overlap=overlap) if env.world_size > 1 else None
         if self.reducer is not None:
             self.reducer.broadcast_params(self.model)
@@ -43,6 +59,7 @@ class TrainEngine:
         return self.reducer.no_sync() if self.reducer is not None else contextlib.nullcontext()
 
     def forward(self, batch: dict):
+        self.flat.reset_pending()
         return self.model(input_ids=batch["input_ids"], attention_mask=batch.get("attention_mask"),
                           decoder_input_ids=batch.get("decoder_input_ids"), labels=batch["labels"],
                           label_smoothing=self.label_smoothing)
@@ -54,12 +71,27 @@ class TrainEngine:
         if sync and self.reducer is not None:
             self.reducer.post_backward()
 
-    def forward_backward(self, batch: dict, grad_accum: int = 1, sync: bool = True) -> torch.Tensor:
+    def forward_backward(self, batch: dict, grad_accum: int = 1, sync: bool = True,
+                         num_items: torch.Tensor | None = None, dp_ranks: int | None = None) -> torch.Tensor:
+        """Forward + backward of one micro-batch; returns its mean loss (detached).
+
+        ``num_items``: the GLOBAL number of non-ignored target tokens of the whole optimizer step (all GA
+        micro-batches on all data-parallel ranks, a device scalar).  Given, the gradient is that of
+        Σ token losses / num_items — every token weighs the same however the tokens are spread over
+        micro-batches and ranks (HF Trainer ``num_items_in_batch``); the reducer's average
+        over ranks is undone by the number of data-parallel ranks ``dp_ranks`` whose tokens ``num_items``
+        counts (default: the reducer's world; context-parallel ranks share one batch and count once).  Without it each micro-batch mean is divided by
+        ``grad_accum`` (identical when every micro-batch has the same token count)."""
         ctx = contextlib.nullcontext() if sync else self.no_sync()
         with ctx:
             out = self.forward(batch)
             loss = out.loss
-            (loss / grad_accum if grad_accum > 1 else loss).backward()
+            if num_items is not None:
+                w = dp_ranks if dp_ranks is not None else (self.reducer.world if self.reducer is not None else 1)
+                scale = token_count(batch["labels"]).to(torch.float32) * w / num_items.to(torch.float32)
+                (loss * scale).backward()
+            else:
+                (loss / grad_accum if grad_accum > 1 else loss).backward()
         if sync and self.reducer is not None:
             self.reducer.post_backward()
         return loss.detach()

@@ -35,7 +35,7 @@ from ..utils.logging import get_logger
 from .callbacks import CallbackHandler, DefaultFlowCallback, TrainerControl, TrainerState
 from ..utils import faults
 from .checkpoint import latest_checkpoint, load_checkpoint, save_checkpoint
-from .engine import TrainEngine, default_no_decay
+from .engine import TrainEngine, default_no_decay, token_count
 from .schedule import LRScheduler
 
 logger = get_logger(__name__)
@@ -155,7 +155,8 @@ class Trainer:
     def train(self, resume_from_checkpoint: str | bool | None = None):
         args, eng, env = self.args, self.engine, self.env
         _, probe = self._loader(self.train_dataset, args.per_device_train_batch_size, True)
-        steps_per_epoch = max(1, len(probe) // args.gradient_accumulation_steps)
+        # an epoch's last optimizer step takes the leftover micro-batches (HF Trainer: ceil(len / ga) updates)
+        steps_per_epoch = max(1, math.ceil(len(probe) / args.gradient_accumulation_steps))
         if args.max_steps > 0:
             max_steps = args.max_steps
             epochs = math.ceil(max_steps / steps_per_epoch)
@@ -190,21 +191,30 @@ class Trainer:
         for epoch in range(start_epoch, epochs):
             loader, sampler = self._loader(self.train_dataset, args.per_device_train_batch_size, True, epoch)
             self.handler.fire("on_epoch_begin", args, self.state, self.control)
-            micro = 0
-            for i, batch in enumerate(loader):
-                if epoch == start_epoch and i < skip:
-                    continue
-                micro += 1
-                sync = micro % ga == 0
-                loss = eng.forward_backward(self._to_device(batch, cp=True), grad_accum=ga, sync=sync)
-                tr_loss_sum += loss.float()
-                tr_loss_n += 1
-                if not sync:
-                    continue
+            n_micro = len(loader)
+            it = iter(loader)
+            for _ in range(skip if epoch == start_epoch else 0):
+                next(it)
+            done = skip if epoch == start_epoch else 0
+            while done < n_micro:
+                # one optimizer step = the next ga micro-batches (fewer at the end of the epoch), normalised by
+                # their global non-ignored target-token count (one int64 all-reduce per step)
+                group = [self._to_device(next(it), cp=True) for _ in range(min(ga, n_micro - done))]
+                done += len(group)
+                num_items = sum(token_count(b["labels"]) for b in group)
+                if self.dp_world > 1:
+                    dist.all_reduce(num_items)
+                    if self.cp_group is not None:  # every CP rank of a DP group counted the same batch
+                        num_items = num_items // (self.env.world_size // self.dp_world)
+                for j, b in enumerate(group):
+                    loss = eng.forward_backward(b, sync=j + 1 == len(group), num_items=num_items,
+                                                dp_ranks=self.dp_world)
+                    tr_loss_sum += loss.float()
+                    tr_loss_n += 1
                 last_norm = eng.step(self.scheduler.get_last_lr()[0])
                 self.scheduler.step()
                 self.state.global_step += 1
-                self.state.epoch = epoch + micro / max(1, len(loader))
+                self.state.epoch = epoch + done / max(1, n_micro)
                 self.control = self.handler.fire("on_step_end", args, self.state, self.control)
                 if self.control.should_log:
                     mean = collectives.mean_across_processes({"loss": float(tr_loss_sum) / max(1, tr_loss_n)},

@@ -171,3 +171,29 @@ def test_t5_long_sequence_chunked_encoder(monkeypatch):
     assert float(out.loss) == pytest.approx(float(ref.loss), rel=1e-5)
     for (n, p), gr in zip(model.named_parameters(), g_ref):
         torch.testing.assert_close(p.grad, gr, atol=1e-5, rtol=1e-4, msg=n)
+
+
+def test_chunked_attention_ragged_length():
+    """A length with no divisor near the chunk (a prime) is padded to whole blocks with masked keys."""
+    from distributed_llms_example_amd.parallel.context import chunked_attention
+    q, k, v, table, do, kpm = _inputs(S=23)
+    o, dq, dk, dv, dt = _full(q, k, v, table, do, kpm, 1.0)
+    a = [t.clone().requires_grad_(True) for t in (q, k, v, table)]
+    oc = chunked_attention(a[0], a[1], a[2], chunk=8, key_padding_mask=kpm, bias_table=a[3])
+    oc.backward(do)
+    torch.testing.assert_close(oc.detach(), o, atol=2e-5, rtol=1e-4)
+    for x, y in zip(a, (dq, dk, dv, dt)):
+        torch.testing.assert_close(x.grad, y, atol=5e-5, rtol=1e-4)
+
+
+def test_long_sequence_chunk_prime_lengths(monkeypatch):
+    from distributed_llms_example_amd.parallel.context import long_sequence_chunk
+    monkeypatch.delenv("DLLM_ATTN_CHUNK", raising=False)
+    monkeypatch.delenv("DLLM_ATTN_CHUNK_MIN", raising=False)
+    for n in (9001, 10007, 8200, 16384, 32768, 65521):
+        c = long_sequence_chunk(n, rows=64)
+        blocks = -(-n // c)
+        assert c % 128 == 0 and 2048 <= c <= 4096 + 128 and blocks * c - n < 128 * blocks, (n, c)
+    assert long_sequence_chunk(16384, rows=64) == 4096
+    assert long_sequence_chunk(32768, rows=12) == 8192
+    assert long_sequence_chunk(8192, rows=64) is None

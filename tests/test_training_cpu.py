@@ -153,3 +153,79 @@ def test_calculate_metric_on_test_ds_cpu():
     scores = calculate_metric_on_test_ds(m, tok, ds, batch_size=2, max_source_length=16, num_beams=2, max_length=6)
     assert set(scores) >= {"rouge1", "rouge2", "rougeL", "rougeLsum"}
     assert all(0.0 <= v <= 1.0 for v in scores.values())
+
+
+def test_trainer_steps_on_epoch_remainder(tmp_path):
+    """len(loader) % ga != 0: the epoch's last optimizer step takes the leftover micro-batches (HF Trainer), so
+    no gradient is carried into the next epoch and ceil(len / ga) steps run per epoch."""
+    from distributed_llms_example_amd.data.dataset import SyntheticSeq2Seq
+    from distributed_llms_example_amd.parallel.env import init_distributed
+    from distributed_llms_example_amd.train.trainer import Trainer, TrainingArguments
+    env = init_distributed(cpu=True)
+    ds = SyntheticSeq2Seq(5, 12, 6, 500, seed=1)  # 5 micro-batches of 1, ga = 2 -> 3 steps / epoch
+    torch.manual_seed(0)
+    args = TrainingArguments(output_dir=str(tmp_path), num_train_epochs=2, per_device_train_batch_size=1,
+                             gradient_accumulation_steps=2, learning_rate=1e-3, logging_steps=100,
+                             save_steps=1000, bf16=False, seed=3)
+    t = Trainer(build_model("t5-tiny"), args, train_dataset=ds, data_collator=DataCollatorForSeq2Seq(0, 0), env=env)
+    t.train()
+    assert t.state.global_step == 6
+    assert float(t.engine.flat.grad_buf.abs().sum()) == 0.0  # nothing left accumulated
+
+
+def test_global_token_normalisation_cpu():
+    """num_items over micro-batches with different ignored-token counts == full-batch token mean (fp32, exact)."""
+    from distributed_llms_example_amd.parallel.env import init_distributed
+    from distributed_llms_example_amd.train.engine import TrainEngine, token_count
+    env = init_distributed(cpu=True)
+    g = torch.Generator().manual_seed(0)
+    ids = torch.randint(3, 500, (4, 12), generator=g)
+    lab = torch.randint(3, 500, (4, 6), generator=g)
+    lab[0, 1:] = -100
+    lab[3, 4:] = -100
+    mbs = [{"input_ids": ids[i:i + 2], "attention_mask": torch.ones(2, 12, dtype=torch.long), "labels": lab[i:i + 2]}
+           for i in (0, 2)]
+    torch.manual_seed(0)
+    sd = build_model("t5-tiny").state_dict()
+
+    def eng():
+        m = build_model("t5-tiny")
+        m.load_state_dict(sd)
+        return TrainEngine(m, env, dtype=torch.float32).train(False)
+
+    e1 = eng()
+    n = sum(token_count(b["labels"]) for b in mbs)
+    for i, b in enumerate(mbs):
+        e1.forward_backward(b, sync=i == 1, num_items=n)
+    e2 = eng()
+    e2.forward_backward({"input_ids": ids, "attention_mask": torch.ones(4, 12, dtype=torch.long), "labels": lab})
+    torch.testing.assert_close(e1.flat.grad_buf, e2.flat.grad_buf, atol=1e-6, rtol=1e-4)
+
+
+def test_bf16_params_fp32_grad_buffer_cpu():
+    """bf16 parameters with the default fp32 gradient buffer: p.grad stays None, fused ops and the autograd
+    fold-in hook (relative-position bias table) both land in the fp32 buffer; matches the fp32 model closely."""
+    from distributed_llms_example_amd.parallel.env import init_distributed
+    from distributed_llms_example_amd.train.engine import TrainEngine
+    env = init_distributed(cpu=True)
+    torch.manual_seed(0)
+    sd = build_model("t5-tiny").state_dict()
+    g = torch.Generator().manual_seed(1)
+    b = {"input_ids": torch.randint(3, 500, (2, 16), generator=g), "attention_mask": torch.ones(2, 16, dtype=torch.long),
+         "labels": torch.randint(3, 500, (2, 8), generator=g)}
+    m16 = build_model("t5-tiny")
+    m16.load_state_dict(sd)
+    e16 = TrainEngine(m16, env, dtype=torch.bfloat16).train(False)
+    assert e16.flat.grad_buf.dtype == torch.float32
+    e16.forward_backward(b)
+    assert all(p.grad is None for p in e16.flat.params)
+    m32 = build_model("t5-tiny").eval()  # plain autograd (no FlatParams: F.embedding / F.linear paths)
+    m32.load_state_dict(sd)
+    m32(**b).loss.backward()
+    ref = dict(m32.named_parameters())
+    for seg in e16.flat.segments:
+        a = e16.flat.grad_buf[seg.offset:seg.offset + seg.numel]
+        r = ref[seg.name].grad.flatten()
+        assert float(a.abs().sum()) > 0, seg.name
+        cos = torch.nn.functional.cosine_similarity(a.double(), r.double(), dim=0).item()
+        assert cos > 0.98, (seg.name, cos)

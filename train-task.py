@@ -10,7 +10,7 @@ and trains on its ``DataPartitioner`` shard (seed 1234) with per-tensor ``all_re
 Here the same launch contract is kept, plus ``--local-procs N`` to run N ranks on one node (one per
 GPU — BASELINE.json's "t5-large train-task torch.multiprocessing spawn, 8 RCCL ranks on one node").
 Gradient averaging is the coalesced flat-buffer all-reduce (same math as the per-tensor loop, one RCCL
-call instead of ~500), optionally overlapped with backward (``--overlap``).  Deviations
+call instead of ~500), overlapped with backward by default (``--no-overlap``: after backward).  Deviations
 (SURVEY.md Appendix A Q4/Q9): ``--batch-size`` is honoured (the reference uses ceil(2/world)); the
 eval set is sharded and gathered instead of decoded redundantly on every rank — the aggregated
 ROUGE is the same; loss is synced to the host only at log steps.
@@ -80,7 +80,7 @@ def run(env, args):
     dtype = torch.bfloat16 if (args.precision or ("bf16" if env.device.type == "cuda" else "fp32")) == "bf16" \
         else torch.float32
     eng = TrainEngine(model, env, lr=args.learning_rate, weight_decay=0.0, max_grad_norm=None, dtype=dtype,
-                      bucket_mb=args.bucket_mb or 128.0, overlap=args.overlap, no_decay=None)
+                      bucket_mb=args.bucket_mb or 128.0, overlap=not args.no_overlap, no_decay=None)
     collator = DataCollatorForSeq2Seq.for_model(cfg, pad_to_multiple_of=8)
     # partition_dataset (ref/train-task.py:176-191)
     world = env.world_size
@@ -130,6 +130,8 @@ def run(env, args):
         if env.is_main_process:
             print("Metrics aggregated across all machines: ")
         dump_metrics(avg, env.is_main_process)
+        if completed >= max_steps:  # --max-steps: no further epochs (each would run a step and a full eval)
+            break
     if output_dir is not None:
         env.barrier()
         from distributed_llms_example_amd.platform.valohai import save_valohai_metadata
@@ -141,7 +143,9 @@ def main():
     p = base_parser("Train a Seq2Seq model", defaults={"batch_size": 6})
     p.add_argument("--local-procs", type=int, default=0, help="spawn N ranks on this node (one per GPU)")
     p.add_argument("--master-port", type=int, default=1234)
-    p.add_argument("--overlap", action="store_true", help="overlap the gradient all-reduce with backward")
+    p.add_argument("--overlap", action="store_true",
+                   help="(default) overlap the bucketed gradient all-reduce with backward; --no-overlap: one coalesced "
+                        "all-reduce after backward, the ref/train-task.py:65-69 call pattern (same math)")
     args = p.parse_args()
     if getattr(args, "context_parallel", 1) > 1:
         raise SystemExit("--context-parallel is implemented in train-torchrun.py (Trainer path)")
