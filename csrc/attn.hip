@@ -41,6 +41,7 @@ using namespace dllm;
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8v;
 typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((ext_vector_type(8))) float f32x8;
 
 namespace {
 
@@ -55,7 +56,6 @@ constexpr float LOG2E = 1.4426950408889634f;
 constexpr float LN2 = 0.6931471805599453f;
 constexpr float RESCALE_THR = 8.f;
 constexpr uint32_t HG = 0x9E3779B1u;
-constexpr uint32_t HC = 0x85EBCA6Bu;
 
 DLLM_DEVICE bf16x8v as_frag(u16x8 v) { return __builtin_bit_cast(bf16x8v, v); }
 
@@ -63,11 +63,10 @@ DLLM_DEVICE bf16x8v as_frag(u16x8 v) { return __builtin_bit_cast(bf16x8v, v); }
 // 5 extra VALU ops per score; softmax probabilities below 2^-126 are irrelevant (flushed to 0).
 DLLM_DEVICE float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// 8 consecutive accumulator registers -> one bf16 MFMA operand (4 v_cvt_pk_bf16_f32)
 DLLM_DEVICE bf16x8v pack8(const f32x16& a, int base) {
-  u16x8 r;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = f2bf(a[base + j]);
-  return as_frag(r);
+  const f32x8 v = {a[base], a[base + 1], a[base + 2], a[base + 3], a[base + 4], a[base + 5], a[base + 6], a[base + 7]};
+  return __builtin_convertvector(v, bf16x8v);
 }
 
 DLLM_DEVICE f32x16 mfma32(bf16x8v a, bf16x8v b, f32x16 c) {
@@ -110,24 +109,39 @@ DLLM_DEVICE bf16x8v ld_tr_operand(const uint16_t* T, int kb0, int t, int r) {
   return as_frag(v);
 }
 
-// attention dropout: x = (rowhash ^ (key>>1)*HG) * HC; x ^= x >> 16; key keeps iff half (key & 1) >= thr16
-DLLM_DEVICE uint32_t pair_hash(uint32_t rh, uint32_t kpg) {
-  uint32_t x = (rh ^ kpg) * HC;
-  return x ^ (x >> 16);
+// attention dropout (ops/rng.py attention_keep_mask): per query row rh = mix32(seed, row); per key pair kp = key >> 1:
+// h = ((rh + kp * HG) & 0xFFFFFF) * C24 (v_mul_u32_u24: full rate, unlike the quarter-rate v_mul_lo_u32);
+// y = h ^ (h >> 16); the even key keeps iff (y & 0xFFFF) >= thr16, the odd key iff (h >> 16) >= thr16.
+constexpr uint32_t C24 = 0x9E3779u;
+DLLM_DEVICE uint32_t attn_pair_hash(uint32_t x) { return __umul24(x, C24); }
+
+// x kept where the lane's bit of `keep` (a compare's lane mask) is set, else 0 (one v_cndmask)
+DLLM_DEVICE float lane_select(uint64_t keep, float x) {
+  float r;
+  asm("v_cndmask_b32 %0, 0, %1, %2" : "=v"(r) : "v"(x), "s"(keep));
+  return r;
+}
+
+// (w << 1) | (this lane's bit of `keep`): one v_addc_co_u32 with the compare mask as carry-in
+DLLM_DEVICE uint32_t shift_in(uint32_t w, uint64_t keep) {
+  uint32_t r;
+  uint64_t co;
+  asm("v_addc_co_u32 %0, %1, %2, %2, %3" : "=v"(r), "=s"(co) : "v"(w), "s"(keep));
+  return r;
 }
 
 // Dropout keep bits of one (row, 64-key tile, lane half): bit i <-> key kbase + crow(i, hh) (the forward's
 // s0[i]), bit 16 + i <-> key kbase + 32 + crow(i, hh) (s1[i]); one hash per adjacent key pair (ops/rng.py).
 DLLM_DEVICE uint32_t dropout_word(uint32_t rh, int kbase, int hh, uint32_t thr) {
-  const uint32_t tbase = (uint32_t)(kbase >> 1) * HG + (uint32_t)(2 * hh) * HG;
+  const uint32_t base = rh + ((uint32_t)(kbase >> 1) + 2u * (uint32_t)hh) * HG;
   uint32_t word = 0;
 #pragma unroll
   for (int i = 0; i < 16; i += 2) {
-    const uint32_t kpg = tbase + (uint32_t)(((i & 3) >> 1) + 4 * (i >> 2)) * HG;
-    const uint32_t x0 = pair_hash(rh, kpg);
-    const uint32_t x1 = pair_hash(rh, kpg + 16u * HG);  // keys + 32
-    word |= ((x0 & 0xFFFFu) >= thr ? 1u << i : 0u) | ((x0 >> 16) >= thr ? 2u << i : 0u) |
-            ((x1 & 0xFFFFu) >= thr ? 0x10000u << i : 0u) | ((x1 >> 16) >= thr ? 0x20000u << i : 0u);
+    const uint32_t pair = (uint32_t)(((i & 3) >> 1) + 4 * (i >> 2));
+    const uint32_t h0 = attn_pair_hash(base + pair * HG), h1 = attn_pair_hash(base + (pair + 16u) * HG);  // keys + 32
+    const uint32_t y0 = h0 ^ (h0 >> 16), y1 = h1 ^ (h1 >> 16);
+    word |= ((y0 & 0xFFFFu) >= thr ? 1u << i : 0u) | ((h0 >> 16) >= thr ? 2u << i : 0u) |
+            ((y1 & 0xFFFFu) >= thr ? 0x10000u << i : 0u) | ((h1 >> 16) >= thr ? 0x20000u << i : 0u);
   }
   return word;
 }
@@ -161,7 +175,9 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
   int* tflag = reinterpret_cast<int*>(kmask + P.n_ktiles * FWD_BN);  // [ntiles]: tile has a masked key
   float* lut_s = reinterpret_cast<float*>(tflag + P.n_ktiles);   // [Sk + FWD_BM + FWD_BN], log2-scaled
 
-  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 31, hh = lane >> 5;
+  // w through readfirstlane: wave-uniform to the compiler, so per-wave tile decisions are scalar branches
+  const int tid = threadIdx.x, w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, r = lane & 31,
+            hh = lane >> 5;
   const int logical = xcd_remap(blockIdx.x, gridDim.x);
   const int qt = logical % P.n_tiles;
   const int bh = logical / P.n_tiles;
@@ -210,18 +226,26 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
   // Keys past Sk re-read row Sk-1 (finite values; masked to -inf / P = 0).  No staging VGPRs, no ds_write.
   const uint32_t kv_lds = lds_addr(KV);
   const uint32_t mw_lds = lds_addr(mwl);
+  // buffer-descriptor DMA: wave-uniform (b, h) bases in SGPRs, per-lane 32-bit byte offsets from one v_mad_u32_u24
+  // (the launcher checks strides and lengths fit), instead of 64-bit address arithmetic per DMA
+  const uint16_t* kbase_p = P.k + b * P.k_sb + h * P.k_sh;
+  const uint16_t* vbase_p = P.v + b * P.v_sb + h * P.v_sh;
+  const uint32_t kss2 = (uint32_t)P.k_ss * 2u, vss2 = (uint32_t)P.v_ss * 2u;
+  int drow[2];
+  uint32_t dc16[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    drow[i] = 8 * (2 * w + i) + (lane >> 3);
+    dc16[i] = (uint32_t)(((lane & 7) ^ swz(drow[i])) * 16);
+  }
   auto issue_tile = [&](int buf, int kt) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int j = 2 * w + i;
-      const int row = 8 * j + (lane >> 3);
-      int kk = kt * FWD_BN + row;
-      kk = kk < P.Sk ? kk : P.Sk - 1;
-      const int c = (lane & 7) ^ swz(row);
+      const uint32_t kk = (uint32_t)min(kt * FWD_BN + drow[i], P.Sk - 1);  // keys past Sk re-read row Sk-1
       const uint32_t dst = kv_lds + (uint32_t)(buf * 2 * TILE64 * 2 + j * 1024);
-      glds16(P.k + b * P.k_sb + (long)kk * P.k_ss + h * P.k_sh + c * 8, __builtin_amdgcn_readfirstlane(dst));
-      glds16(P.v + b * P.v_sb + (long)kk * P.v_ss + h * P.v_sh + c * 8,
-             __builtin_amdgcn_readfirstlane(dst + TILE64 * 2));
+      bld16(kbase_p, __umul24(kk, kss2) + dc16[i], __builtin_amdgcn_readfirstlane(dst));
+      bld16(vbase_p, __umul24(kk, vss2) + dc16[i], __builtin_amdgcn_readfirstlane(dst + TILE64 * 2));
     }
     if (DROP && DROP_IN)  // this wave's 32 rows x 2 lane halves of keep bits: lane L -> half L/32, row qw0 + L%32
       glds4(P.dmask + ((long)bh * P.n_ktiles * 2 + 2 * kt + hh) * P.sq_pad + qrow,
@@ -263,28 +287,27 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
     const int sat = !HAS_BIAS ? 0
                     : (kbase + FWD_BN - 1 - qw0 + P.Sq - 1 <= P.sat_lo ? 1
                        : (kbase - qw0 - 31 + P.Sq - 1 >= P.sat_hi ? 2 : 0));
-    auto bias_scale = [&](auto use_lut, float cbias) {
+    // Per score, in VALU instructions (the forward is VALU-bound: MI355X_MICROARCH.md issue costs): scale + bias 1
+    // (LUT tiles 2), max 0.5 (v_max3), exp 1, row sum 1, dropout ~4, bf16 pack 0.5.  Saturated / bias-free tiles
+    // stay in the raw QK^T domain until the exponent: max(s * sl2 + c) = max(s) * sl2 + c (sl2 > 0), and
+    // p = exp2(fma(s, sl2, c - m)) is one FMA.
+    const bool use_lut = HAS_BIAS && sat == 0;
+    const float cb = sat == 1 ? c_lo : (sat == 2 ? c_hi : 0.f);
+    if (use_lut) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const int kl0 = crow(i, hh), kl1 = 32 + kl0;
-        float v0, v1;
-        if constexpr (decltype(use_lut)::value) {
-          v0 = s0[i] * sl2 + lb[kl0];
-          v1 = s1[i] * sl2 + lb[kl1];
-        } else {
-          v0 = s0[i] * sl2 + cbias;
-          v1 = s1[i] * sl2 + cbias;
-        }
-        if (CAUSAL) {
-          v0 = (tile_causal && kl0 > climit) ? -INFINITY : v0;
-          v1 = (tile_causal && kl1 > climit) ? -INFINITY : v1;
-        }
-        s0[i] = v0;
-        s1[i] = v1;
+        s0[i] = fmaf(s0[i], sl2, lb[crow(i, hh)]);
+        s1[i] = fmaf(s1[i], sl2, lb[32 + crow(i, hh)]);
       }
-    };
-    if (HAS_BIAS && sat == 0) bias_scale(std::true_type{}, 0.f);
-    else bias_scale(std::false_type{}, sat == 1 ? c_lo : (sat == 2 ? c_hi : 0.f));
+    }
+    if (CAUSAL && tile_causal) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int kl0 = crow(i, hh);
+        s0[i] = kl0 > climit ? -INFINITY : s0[i];
+        s1[i] = kl0 + 32 > climit ? -INFINITY : s1[i];
+      }
+    }
     // key mask (padding / past Sk): one uniform branch per tile around 8 vector LDS reads; a per-score `if`
     // made the compiler emit 16 branches each ending in s_waitcnt lgkmcnt(0)
     if ((HAS_KPM || kbase + FWD_BN > P.Sk) && tflag[kt] != 0) {
@@ -299,10 +322,15 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
         }
       }
     }
-    float mloc = -INFINITY;
+    float ma = fmaxf(fmaxf(s0[0], s0[1]), s0[2]), mb = fmaxf(fmaxf(s1[0], s1[1]), s1[2]);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) mloc = fmaxf(mloc, fmaxf(s0[i], s1[i]));
+    for (int i = 3; i < 15; i += 2) {
+      ma = fmaxf(fmaxf(ma, s0[i]), s0[i + 1]);
+      mb = fmaxf(fmaxf(mb, s1[i]), s1[i + 1]);
+    }
+    float mloc = fmaxf(fmaxf(ma, mb), fmaxf(s0[15], s1[15]));
     mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+    if (!use_lut) mloc = fmaf(mloc, sl2, cb);  // -inf stays -inf
     // deferred rescale (T13): keep the running max unless the tile max exceeds it by > 8 (log2 units)
     const bool grow = mloc > m_run + RESCALE_THR;
     float alpha = 1.f;
@@ -311,14 +339,26 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
       m_run = mloc;
     }
     const float m_use = m_run == -INFINITY ? 0.f : m_run;
-    float lsum = 0.f;
+    float la = 0.f, lb2 = 0.f;
+    if (use_lut) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      s0[i] = fast_exp2(s0[i] - m_use);
-      s1[i] = fast_exp2(s1[i] - m_use);
-      lsum += s0[i] + s1[i];
+      for (int i = 0; i < 16; ++i) {
+        s0[i] = fast_exp2(s0[i] - m_use);
+        s1[i] = fast_exp2(s1[i] - m_use);
+        la += s0[i];
+        lb2 += s1[i];
+      }
+    } else {
+      const float cm = cb - m_use;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        s0[i] = fast_exp2(fmaf(s0[i], sl2, cm));
+        s1[i] = fast_exp2(fmaf(s1[i], sl2, cm));
+        la += s0[i];
+        lb2 += s1[i];
+      }
     }
-    l_run = l_run * alpha + lsum;
+    l_run = l_run * alpha + (la + lb2);
     if (__any(grow)) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
@@ -334,21 +374,28 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
       }
     } else if (DROP) {
       // keep decisions -> P (the 1/(1-p) scale is applied once to O at the end) and one bit word per lane and
-      // tile for the backward kernels (bit i <-> s0[i], bit 16+i <-> s1[i]): they never re-hash
-      const uint32_t tbase = (uint32_t)(kbase >> 1) * HG + (uint32_t)(2 * hh) * HG;
+      // tile for the backward kernels (bit i <-> s0[i], bit 16+i <-> s1[i]): they never re-hash.  Per key pair
+      // one add, one full-rate 24-bit multiply and a shift-xor (attn_pair_hash); each compare's lane mask drives
+      // both the select that zeroes P and a carry-in add that shifts the bit into the word (s1[15] first, so it
+      // ends at bit 31).
+      const uint32_t base = rh + ((uint32_t)(kbase >> 1) + 2u * (uint32_t)hh) * HG;
+      const uint32_t thr_hi = P.thr << 16;
       uint32_t word = 0;
+      auto one = [&](float v, bool keep) {
+        word = word + word + (keep ? 1u : 0u);  // v_addc_co_u32 with the compare as carry-in
+        return keep ? v : 0.f;
+      };
 #pragma unroll
-      for (int i = 0; i < 16; i += 2) {
-        const uint32_t kpg = tbase + (uint32_t)(((i & 3) >> 1) + 4 * (i >> 2)) * HG;
-        const uint32_t x0 = pair_hash(rh, kpg);
-        const uint32_t x1 = pair_hash(rh, kpg + 16u * HG);  // keys + 32
-        const bool k0a = (x0 & 0xFFFFu) >= P.thr, k0b = (x0 >> 16) >= P.thr;
-        const bool k1a = (x1 & 0xFFFFu) >= P.thr, k1b = (x1 >> 16) >= P.thr;
-        s0[i] = k0a ? s0[i] : 0.f;
-        s0[i + 1] = k0b ? s0[i + 1] : 0.f;
-        s1[i] = k1a ? s1[i] : 0.f;
-        s1[i + 1] = k1b ? s1[i + 1] : 0.f;
-        word |= (k0a ? 1u << i : 0u) | (k0b ? 2u << i : 0u) | (k1a ? 0x10000u << i : 0u) | (k1b ? 0x20000u << i : 0u);
+      for (int t = 1; t >= 0; --t) {
+        f32x16& sv = t == 0 ? s0 : s1;
+#pragma unroll
+        for (int i = 14; i >= 0; i -= 2) {
+          const uint32_t pair = (uint32_t)(((i & 3) >> 1) + 4 * (i >> 2) + 16 * t);  // (key - kbase - 4hh) / 2
+          const uint32_t h = attn_pair_hash(base + pair * HG);
+          const uint32_t y = h ^ (h >> 16);
+          sv[i + 1] = one(sv[i + 1], h >= thr_hi);
+          sv[i] = one(sv[i], (y & 0xFFFFu) >= P.thr);
+        }
       }
       P.dmask[((long)bh * P.n_ktiles * 2 + 2 * kt + hh) * P.sq_pad + qrow] = word;
     }
@@ -417,7 +464,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnParams P) {
   int* tflag = reinterpret_cast<int*>(kmask + P.n_ktiles * FWD_BN);  // [ntiles]: tile has a masked key
   float* lut_s = reinterpret_cast<float*>(tflag + P.n_ktiles);   // [Sk + FWD_BM + FWD_BN]
 
-  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 31, hh = lane >> 5;
+  // w through readfirstlane: wave-uniform to the compiler, so per-wave tile decisions are scalar branches
+  const int tid = threadIdx.x, w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, r = lane & 31,
+            hh = lane >> 5;
   const int logical = xcd_remap(blockIdx.x, gridDim.x);
   const int qt = logical % P.n_tiles;
   const int bh = logical / P.n_tiles;
@@ -463,6 +512,19 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnParams P) {
   const long row_g = (long)(b * P.H + h) * P.Sq + qrow;
   if (qvalid && hh == 0) P.delta[row_g] = delta;
   const float lse2 = qvalid ? P.lse[row_g] : INFINITY;
+  if (P.rowrec != nullptr) {  // dK/dV's per-row terms, field-major per 64-row chunk (attn_bwd_dkdv2_kernel)
+    float c0 = 0.f, c1 = 0.f;
+    if (HAS_BIAS) {
+      const int L = P.Sq + P.Sk - 1;
+      c0 = P.lut[(long)h * L] * LOG2E;
+      c1 = P.lut[(long)h * L + L - 1] * LOG2E;
+    }
+    float* rec = P.rowrec + ((long)bh * (P.sq_pad >> 6) + (qrow >> 6)) * 256 + (qrow & 63);
+    const float f = hh == 0 ? -lse2 : (hh == 1 ? c0 - lse2 : 0.f);  // lanes 0-31: fields 0 / 3, 32-63: 1 / 2
+    const float g = hh == 0 ? (qvalid ? -delta : 0.f) : c1 - lse2;
+    rec[hh == 0 ? 0 : 64] = f;
+    rec[hh == 0 ? 192 : 128] = g;
+  }
   const float dscale = DROP ? 1.f / (1.f - P.p_drop) : 1.f;
 
   int kend = P.Sk;
@@ -473,18 +535,26 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnParams P) {
   const int ntiles = kend > 0 ? (kend + FWD_BN - 1) / FWD_BN : 0;
   // K/V tiles by LDS-DMA into 2 buffers (see the forward kernel); per-key mask + tile flags up front
   const uint32_t kv_lds = lds_addr(KV);
+  // buffer-descriptor DMA: wave-uniform (b, h) bases in SGPRs, per-lane 32-bit byte offsets from one v_mad_u32_u24
+  // (the launcher checks strides and lengths fit), instead of 64-bit address arithmetic per DMA
+  const uint16_t* kbase_p = P.k + b * P.k_sb + h * P.k_sh;
+  const uint16_t* vbase_p = P.v + b * P.v_sb + h * P.v_sh;
+  const uint32_t kss2 = (uint32_t)P.k_ss * 2u, vss2 = (uint32_t)P.v_ss * 2u;
+  int drow[2];
+  uint32_t dc16[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    drow[i] = 8 * (2 * w + i) + (lane >> 3);
+    dc16[i] = (uint32_t)(((lane & 7) ^ swz(drow[i])) * 16);
+  }
   auto issue_tile = [&](int buf, int kt) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int j = 2 * w + i;
-      const int row = 8 * j + (lane >> 3);
-      int kk = kt * FWD_BN + row;
-      kk = kk < P.Sk ? kk : P.Sk - 1;
-      const int c = (lane & 7) ^ swz(row);
+      const uint32_t kk = (uint32_t)min(kt * FWD_BN + drow[i], P.Sk - 1);  // keys past Sk re-read row Sk-1
       const uint32_t dst = kv_lds + (uint32_t)(buf * 2 * TILE64 * 2 + j * 1024);
-      glds16(P.k + b * P.k_sb + (long)kk * P.k_ss + h * P.k_sh + c * 8, __builtin_amdgcn_readfirstlane(dst));
-      glds16(P.v + b * P.v_sb + (long)kk * P.v_ss + h * P.v_sh + c * 8,
-             __builtin_amdgcn_readfirstlane(dst + TILE64 * 2));
+      bld16(kbase_p, __umul24(kk, kss2) + dc16[i], __builtin_amdgcn_readfirstlane(dst));
+      bld16(vbase_p, __umul24(kk, vss2) + dc16[i], __builtin_amdgcn_readfirstlane(dst + TILE64 * 2));
     }
   };
   for (int t = w; t < ntiles; t += 4) {
@@ -530,28 +600,31 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnParams P) {
     const int sat = !HAS_BIAS ? 0
                     : (kbase + FWD_BN - 1 - qw0 + P.Sq - 1 <= P.sat_lo ? 1
                        : (kbase - qw0 - 31 + P.Sq - 1 >= P.sat_hi ? 2 : 0));
-    auto bias_scale = [&](auto use_lut, float cbias) {  // as in the forward: saturated tiles add a scalar
+    // P = exp2(s * sl2 + bias - lse): saturated / bias-free tiles fold the constant bias and the row's lse into one
+    // FMA operand (cl), LUT tiles add the bias by FMA and subtract lse.  dS = P * (dP * keep / (1 - p) - delta).
+    const bool use_lut = HAS_BIAS && sat == 0;
+    const float cl = (sat == 1 ? c_lo : (sat == 2 ? c_hi : 0.f)) - lse2;
+    if (use_lut) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const int kl0 = crow(i, hh), kl1 = 32 + kl0;
-        float v0, v1;
-        if constexpr (decltype(use_lut)::value) {
-          v0 = s0[i] * sl2 + lb[kl0];
-          v1 = s1[i] * sl2 + lb[kl1];
-        } else {
-          v0 = s0[i] * sl2 + cbias;
-          v1 = s1[i] * sl2 + cbias;
-        }
-        if (CAUSAL) {
-          v0 = (tile_causal && kl0 > climit) ? -INFINITY : v0;
-          v1 = (tile_causal && kl1 > climit) ? -INFINITY : v1;
-        }
-        s0[i] = v0;
-        s1[i] = v1;
+        s0[i] = fmaf(s0[i], sl2, lb[crow(i, hh)]) - lse2;
+        s1[i] = fmaf(s1[i], sl2, lb[32 + crow(i, hh)]) - lse2;
       }
-    };
-    if (HAS_BIAS && sat == 0) bias_scale(std::true_type{}, 0.f);
-    else bias_scale(std::false_type{}, sat == 1 ? c_lo : (sat == 2 ? c_hi : 0.f));
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        s0[i] = fmaf(s0[i], sl2, cl);
+        s1[i] = fmaf(s1[i], sl2, cl);
+      }
+    }
+    if (CAUSAL && tile_causal) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int kl0 = crow(i, hh);
+        s0[i] = kl0 > climit ? -INFINITY : s0[i];
+        s1[i] = kl0 + 32 > climit ? -INFINITY : s1[i];
+      }
+    }
     if ((HAS_KPM || kbase + FWD_BN > P.Sk) && tflag[kt] != 0) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
@@ -566,14 +639,14 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnParams P) {
     }
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const float pr0 = fast_exp2(s0[i] - lse2), pr1 = fast_exp2(s1[i] - lse2);
+      const float pr0 = fast_exp2(s0[i]), pr1 = fast_exp2(s1[i]);  // lse = +inf for rows >= Sq -> 0
       float k0 = 1.f, k1 = 1.f;
       if (DROP) {  // sign-extended bit -> all-ones mask -> dscale or 0.0f
         k0 = __uint_as_float((uint32_t)__builtin_amdgcn_sbfe((int)mword, i, 1) & dsbits);
         k1 = __uint_as_float((uint32_t)__builtin_amdgcn_sbfe((int)mword, 16 + i, 1) & dsbits);
       }
-      s0[i] = pr0 * (p0[i] * k0 - delta);
-      s1[i] = pr1 * (p1[i] * k1 - delta);
+      s0[i] = pr0 * fmaf(p0[i], k0, -delta);
+      s1[i] = pr1 * fmaf(p1[i], k1, -delta);
     }
     // dQ^T += K^T dS^T
     const bf16x8v da0 = pack8(s0, 0), da1 = pack8(s0, 8), db0 = pack8(s1, 0), db1 = pack8(s1, 8);
@@ -614,7 +687,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnParams P) {
   float* lut_r = reinterpret_cast<float*>(mwd + 2 * 4 * BWD_BQ); // [Sq + 128 + 32] reversed, log2-scaled
   float* dlut_s = lut_r + (HAS_BIAS ? P.Sq + BWD_BK + BWD_BQ : 0);  // [Sq + 128]
 
-  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 31, hh = lane >> 5;
+  // w through readfirstlane: wave-uniform to the compiler, so per-wave tile decisions are scalar branches
+  const int tid = threadIdx.x, w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, r = lane & 31,
+            hh = lane >> 5;
   const int logical = xcd_remap(blockIdx.x, gridDim.x);
   const int kblk = logical % P.n_tiles;
   const int bh = logical / P.n_tiles;
@@ -846,6 +921,252 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnParams P) {
   }
 }
 
+
+// ================================================================================== backward: dK, dV (v2)
+// Key blocks of 128 (4 waves x 32 keys, key on the lane as in v1), query tiles of 64 rows per pipeline stage: the
+// Q / dO tile, the per-row terms (attn_bwd_dq_kernel's rowrec: -lse, c_lo - lse, c_hi - lse, -delta) and the dropout
+// keep words of the tile are moved by LDS-DMA two stages ahead into a 3-slot ring (no VGPR staging, one barrier per
+// 64 rows; v1 moved 32 rows per barrier through registers one tile ahead, and its waves sat parked on the barrier
+// and on the per-score lse / delta arithmetic half the time, profiles/r1_attn_pmc.txt).  Per score (saturated /
+// bias-free tile): P = exp2(fma(s, sl2, rt)), keep = sbfe & dscale bits, Pd = P keep, dS = P fma(dP, keep, -delta).
+constexpr int K2_QT = 64;
+constexpr int K2_NBUF = 3;
+constexpr int K2_STAGE = 2 * 64 * D * 2 + 1024 + 1024;  // Q, dO [64][64] bf16 + rowrec [4][64] f32 + keep [4][64] u32
+
+template <bool HAS_BIAS, bool HAS_KPM, bool CAUSAL, bool DROP>
+__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv2_kernel(AttnParams P) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float* kmask = reinterpret_cast<float*>(smem + K2_NBUF * K2_STAGE);  // [128]
+  float* lut_r = kmask + BWD_BK;                                       // [Sq + 128 + 64] reversed, log2-scaled
+  float* dlut_s = lut_r + (HAS_BIAS ? P.Sq + BWD_BK + K2_QT : 0);      // [Sq + 128]
+
+  const int tid = threadIdx.x, w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, r = lane & 31,
+            hh = lane >> 5;
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int kblk = logical % P.n_tiles;
+  const int bh = logical / P.n_tiles;
+  const int h = bh % P.H, b = bh / P.H;
+  const int k0 = kblk * BWD_BK;
+  const int kw0 = k0 + w * 32;
+  const int key = kw0 + r;
+  const bool kvalid = key < P.Sk;
+  const int L = P.Sq + P.Sk - 1;
+  const int win = P.Sq + BWD_BK;
+  const float sl2 = P.scale * LOG2E;
+
+  if (HAS_BIAS) {
+    const float* lrow = P.lut + (long)h * L;
+    for (int t = tid; t < win + K2_QT; t += 256) {
+      const int i = win - 1 - t, gi = k0 + i;
+      lut_r[t] = (i >= 0 && gi < L) ? lrow[gi] * LOG2E : 0.f;
+    }
+    for (int i = tid; i < win; i += 256) dlut_s[i] = 0.f;
+  }
+  float sat_acc_lo = 0.f, sat_acc_hi = 0.f;
+  bool key_ok = false;
+  if (tid < BWD_BK) {
+    const int kk = k0 + tid;
+    key_ok = kk < P.Sk;
+    if (HAS_KPM && key_ok) key_ok = P.kpm[(long)b * P.Sk + kk] != 0;
+    kmask[tid] = key_ok ? 0.f : -INFINITY;
+  }
+  const bool block_live = !HAS_KPM || __syncthreads_or(key_ok ? 1 : 0);
+  // some key of the block is padding or past Sk: the exponent gets the per-key mask (else nothing to add)
+  const bool block_masked = __syncthreads_or((tid < BWD_BK && !key_ok) ? 1 : 0);
+  bf16x8v kf[4], vf[4];
+  {
+    const uint16_t* kp = P.k + b * P.k_sb + (long)key * P.k_ss + h * P.k_sh;
+    const uint16_t* vp = P.v + b * P.v_sb + (long)key * P.v_ss + h * P.v_sh;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      u16x8 a = {0, 0, 0, 0, 0, 0, 0, 0}, c = a;
+      if (kvalid) {
+        a = *reinterpret_cast<const u16x8*>(kp + 16 * s + 8 * hh);
+        c = *reinterpret_cast<const u16x8*>(vp + 16 * s + 8 * hh);
+      }
+      kf[s] = as_frag(a);
+      vf[s] = as_frag(c);
+    }
+  }
+  const float km = kmask[w * 32 + r];
+  // this lane's dropout bit: the forward's lane (hh_f) and register (bit) that held (q, key)
+  const int kl = key - k0, kc = kl & 31;
+  const int mcol = (kl >> 6) * 2 + ((kc >> 2) & 1);
+  const int mbit = (kc & 3) + 4 * (kc >> 3) + 16 * ((kl >> 5) & 1);
+  const float dscale = DROP ? 1.f / (1.f - P.p_drop) : 1.f;
+  const uint32_t dsbits = __float_as_uint(dscale);
+  int qt_begin = 0;
+  if (CAUSAL) {
+    const int qmin = k0 - P.causal_off;  // first query that can see key k0
+    qt_begin = qmin > 0 ? qmin / K2_QT : 0;
+  }
+  const int nqt = block_live ? (P.Sq + K2_QT - 1) / K2_QT : qt_begin;
+
+  // ---- stage DMA (per wave and stage: 2 + 2 Q / dO pieces of 8 rows, a quarter of the rowrec chunk, one keep column)
+  const uint32_t st_lds = lds_addr(smem);
+  const uint16_t* qbase_p = P.q + b * P.q_sb + h * P.q_sh;
+  const uint16_t* dbase_p = P.dout + b * P.do_sb + h * P.do_sh;
+  const uint32_t qss2 = (uint32_t)P.q_ss * 2u, dss2 = (uint32_t)P.do_ss * 2u;
+  int drow[2];
+  uint32_t dc16[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    drow[i] = 8 * (2 * w + i) + (lane >> 3);
+    dc16[i] = (uint32_t)(((lane & 7) ^ swz(drow[i])) * 16);
+  }
+  const float* rec_src = P.rowrec + (long)bh * (P.sq_pad >> 6) * 256 + w * 64 + lane;
+  const int ktf = min((k0 >> 6) + (w >> 1), P.n_ktiles - 1);
+  const uint32_t* keep_src = DROP ? P.dmask + (((long)bh * P.n_ktiles + ktf) * 2 + (w & 1)) * P.sq_pad + lane : nullptr;
+  auto issue = [&](int slot, int qt) {
+    const uint32_t base = st_lds + (uint32_t)(slot * K2_STAGE);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const uint32_t qq = (uint32_t)min(qt * K2_QT + drow[i], P.Sq - 1);
+      const uint32_t dst = base + (uint32_t)((2 * w + i) * 1024);
+      bld16(qbase_p, __umul24(qq, qss2) + dc16[i], __builtin_amdgcn_readfirstlane(dst));
+      bld16(dbase_p, __umul24(qq, dss2) + dc16[i], __builtin_amdgcn_readfirstlane(dst + TILE64 * 2));
+    }
+    glds4(rec_src + (long)qt * 256, __builtin_amdgcn_readfirstlane(base + 4 * TILE64 + w * 256));
+    if (DROP) glds4(keep_src + qt * K2_QT, __builtin_amdgcn_readfirstlane(base + 4 * TILE64 + 1024 + w * 256));
+  };
+  constexpr int DPT = DROP ? 6 : 5;  // DMAs per wave and stage
+
+  f32x16 dv0 = {}, dv1 = {}, dk0 = {}, dk1 = {};
+  if (qt_begin < nqt) issue(0, qt_begin);
+  if (qt_begin + 1 < nqt) issue(1, qt_begin + 1);
+  for (int qt = qt_begin; qt < nqt; ++qt) {
+    const int it = qt - qt_begin;
+    if (qt + 1 < nqt) wait_vm<DPT>();
+    else wait_vm<0>();
+    __syncthreads();  // stage qt landed for every wave; every wave is done with stage qt - 1 (the slot refilled next)
+    if (qt + 2 < nqt) issue((it + 2) % K2_NBUF, qt + 2);
+    const unsigned char* stg = smem + (it % K2_NBUF) * K2_STAGE;
+    const uint16_t* Qb = reinterpret_cast<const uint16_t*>(stg);
+    const uint16_t* dOb = Qb + TILE64;
+    const float* rec = reinterpret_cast<const float*>(stg + 4 * TILE64);
+    const uint32_t* mwd = reinterpret_cast<const uint32_t*>(stg + 4 * TILE64 + 1024);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int q0 = qt * K2_QT + 32 * u;
+      f32x16 sacc = {}, dpacc = {};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        sacc = mfma32(as_frag(ld_row(Qb, 32 * u + r, 2 * s + hh)), kf[s], sacc);
+        dpacc = mfma32(as_frag(ld_row(dOb, 32 * u + r, 2 * s + hh)), vf[s], dpacc);
+      }
+      const int sat = !HAS_BIAS ? 0
+                      : (kw0 + 31 - q0 + P.Sq - 1 <= P.sat_lo ? 1 : (kw0 - q0 - 31 + P.Sq - 1 >= P.sat_hi ? 2 : 0));
+      const bool use_lut = HAS_BIAS && sat == 0;
+      // rows 32u + crow(i, hh): four consecutive rows per 16-B read
+      const float* rt_row = rec + (use_lut ? 0 : (sat == 1 ? 64 : 128)) + 32 * u + 4 * hh;
+      const float* nd_row = rec + 192 + 32 * u + 4 * hh;
+      float rt[16], nd[16];
+      uint32_t mw[16];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 a = *reinterpret_cast<const f32x4*>(rt_row + 8 * g);
+        const f32x4 c = *reinterpret_cast<const f32x4*>(nd_row + 8 * g);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          rt[4 * g + e] = a[e];
+          nd[4 * g + e] = c[e];
+        }
+        if (DROP) {
+          const u32x4 v = *reinterpret_cast<const u32x4*>(mwd + mcol * 64 + 32 * u + 8 * g + 4 * hh);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) mw[4 * g + e] = v[e];
+        }
+      }
+      if (use_lut) {  // bias per (key - row) from the reversed LUT: immediate ds_read offsets per register
+        const float* lrow_t = lut_r + (win - 1 - (key - q0 - 4 * hh + P.Sq - 1 - k0));
+#pragma unroll
+        for (int i = 0; i < 16; ++i) rt[i] += lrow_t[crow(i, 0)];
+      }
+      if (block_masked) {  // padding / tail keys: -inf on the lane's whole column
+#pragma unroll
+        for (int i = 0; i < 16; ++i) rt[i] += km;
+      }
+      const bool tile_causal = CAUSAL && (kw0 + 31 > q0 + P.causal_off);
+      f32x16 pd, ds;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        float pr = fast_exp2(fmaf(sacc[i], sl2, rt[i]));  // rows >= Sq: rt = -inf -> 0
+        if (CAUSAL && tile_causal && key > q0 + crow(i, hh) + P.causal_off) pr = 0.f;
+        float keepf = 1.f;
+        if (DROP) keepf = __uint_as_float((uint32_t)__builtin_amdgcn_sbfe((int)mw[i], mbit, 1) & dsbits);
+        pd[i] = pr * keepf;
+        ds[i] = pr * fmaf(dpacc[i], keepf, nd[i]);
+      }
+      if (HAS_BIAS && sat != 0) {
+        float t = 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) t += ds[i];
+        if (sat == 1) sat_acc_lo += t;
+        else sat_acc_hi += t;
+      } else if (HAS_BIAS) {
+        // diagonal sums of the wave's 32x32 dS tile: rotate register i (row rho = crow(i, hh)) left by rho
+        // lanes so lane r receives element (rho, (r + rho) & 31) whose diagonal (col - row) is r or r - 32
+        float pos = 0.f, neg = 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int rho = crow(i, hh);
+          const float v = __shfl(ds[i], ((r + rho) & 31) + 32 * hh, 64);
+          if (r + rho < 32) pos += v; else neg += v;
+        }
+        pos += __shfl_xor(pos, 32, 64);
+        neg += __shfl_xor(neg, 32, 64);
+        if (hh == 0) {
+          const int li = w * 32 + r - q0 + P.Sq - 1;
+          atomicAdd(&dlut_s[li], pos);
+          if (li >= 32) atomicAdd(&dlut_s[li - 32], neg);
+        }
+      }
+      const bf16x8v pf0 = pack8(pd, 0), pf1 = pack8(pd, 8), sf0 = pack8(ds, 0), sf1 = pack8(ds, 8);
+#pragma unroll
+      for (int sp = 0; sp < 2; ++sp) {
+        const int c0 = 32 * u + 16 * sp + 4 * hh;
+        const bf16x8v pfv = sp == 0 ? pf0 : pf1, sfv = sp == 0 ? sf0 : sf1;
+        dv0 = mfma32(ld_tr_operand(dOb, c0, 0, r), pfv, dv0);
+        dv1 = mfma32(ld_tr_operand(dOb, c0, 1, r), pfv, dv1);
+        dk0 = mfma32(ld_tr_operand(Qb, c0, 0, r), sfv, dk0);
+        dk1 = mfma32(ld_tr_operand(Qb, c0, 1, r), sfv, dk1);
+      }
+    }
+  }
+
+  if (kvalid) {
+    uint16_t* dkp = P.dk + b * P.dk_sb + (long)key * P.dk_ss + h * P.dk_sh;
+    uint16_t* dvp = P.dv + b * P.dv_sb + (long)key * P.dv_ss + h * P.dv_sh;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const f32x16& ak = t == 0 ? dk0 : dk1;
+      const f32x16& av = t == 0 ? dv0 : dv1;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        u16x4 pk = {f2bf(ak[4 * g] * P.scale), f2bf(ak[4 * g + 1] * P.scale), f2bf(ak[4 * g + 2] * P.scale),
+                    f2bf(ak[4 * g + 3] * P.scale)};
+        u16x4 pv = {f2bf(av[4 * g]), f2bf(av[4 * g + 1]), f2bf(av[4 * g + 2]), f2bf(av[4 * g + 3])};
+        *reinterpret_cast<u16x4*>(dkp + 32 * t + 8 * g + 4 * hh) = pk;
+        *reinterpret_cast<u16x4*>(dvp + 32 * t + 8 * g + 4 * hh) = pv;
+      }
+    }
+  }
+  if (HAS_BIAS) {
+    __syncthreads();
+    float* grow = P.dlut + (long)h * L;
+    for (int i = tid; i < win; i += 256) {
+      const int gi = k0 + i;
+      const float v = dlut_s[i];
+      if (gi < L && v != 0.f) atomicAdd(grow + gi, v);
+    }
+    const float a_lo = wave_sum(sat_acc_lo), a_hi = wave_sum(sat_acc_hi);
+    if (lane == 0) {
+      if (a_lo != 0.f) atomicAdd(grow, a_lo);
+      if (a_hi != 0.f) atomicAdd(grow + L - 1, a_hi);
+    }
+  }
+}
+
 #define DISPATCH4(FN, hb, hk, ca, dr, ...)                                              \
   do {                                                                                  \
     if (hb) {                                                                           \
@@ -876,12 +1197,30 @@ template <bool HB, bool HK, bool CA, bool DR>
 void launch_bwd_dkdv_t(const AttnParams& p, int nblk, size_t lds, hipStream_t st) {
   hipLaunchKernelGGL((attn_bwd_dkdv_kernel<HB, HK, CA, DR>), dim3(nblk), dim3(256), lds, st, p);
 }
+template <bool HB, bool HK, bool CA, bool DR>
+void launch_bwd_dkdv2_t(const AttnParams& p, int nblk, size_t lds, hipStream_t st) {
+  static size_t attr = 64 * 1024;  // dynamic LDS above 64 KB (long sequences with bias) must be opted into
+  if (lds > attr) {
+    (void)hipFuncSetAttribute((const void*)attn_bwd_dkdv2_kernel<HB, HK, CA, DR>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = lds;
+  }
+  hipLaunchKernelGGL((attn_bwd_dkdv2_kernel<HB, HK, CA, DR>), dim3(nblk), dim3(256), lds, st, p);
+}
 
 
 }  // namespace
 
+// The K/V tile DMA addresses rows with 32-bit byte offsets from v_mad_u32_u24 (csrc/attn.hip issue_tile).
+static bool kv_offsets_fit(const AttnParams& p) {
+  const long kss2 = p.k_ss * 2, vss2 = p.v_ss * 2;
+  return kss2 > 0 && vss2 > 0 && kss2 < (1L << 24) && vss2 < (1L << 24) && p.Sk < (1 << 24) &&
+         (long)p.Sk * (kss2 > vss2 ? kss2 : vss2) + 256 < (1L << 31);
+}
+
 extern "C" int dllm_attn_fwd(AttnParams* pp, hipStream_t st) {
   AttnParams p = *pp;
+  if (!kv_offsets_fit(p)) return -6;
   p.thr = drop_threshold(p.p_drop);
   p.n_tiles = (p.Sq + FWD_BM - 1) / FWD_BM;
   const long nblk = (long)p.n_tiles * p.H * p.B;
@@ -899,6 +1238,7 @@ extern "C" int dllm_attn_fwd(AttnParams* pp, hipStream_t st) {
 
 extern "C" int dllm_attn_bwd(AttnParams* pp, hipStream_t st) {
   AttnParams p = *pp;
+  if (!kv_offsets_fit(p)) return -6;
   p.thr = drop_threshold(p.p_drop);
   // 1) dQ (+ delta): query blocks, forward geometry
   p.n_tiles = (p.Sq + FWD_BM - 1) / FWD_BM;
@@ -916,6 +1256,15 @@ extern "C" int dllm_attn_bwd(AttnParams* pp, hipStream_t st) {
   // 2) dK, dV (+ bias-LUT gradient): key blocks
   p.n_tiles = (p.Sk + BWD_BK - 1) / BWD_BK;
   nblk = (long)p.n_tiles * p.H * p.B;
+  if (p.rowrec != nullptr) {  // v2: 64-row stages through an LDS-DMA ring (per-row terms from the dQ kernel)
+    lds = (size_t)K2_NBUF * K2_STAGE + BWD_BK * 4;
+    if (p.lut) lds += (size_t)(2 * (p.Sq + BWD_BK) + K2_QT) * 4;
+    if (nblk <= 0 || nblk > 0x7fffffff || lds > 160 * 1024) return -4;
+    DISPATCH4(launch_bwd_dkdv2_t, p.lut != nullptr, p.kpm != nullptr, p.causal != 0, p.p_drop > 0.f, p, (int)nblk,
+              lds, st);
+    DLLM_CHECK_LAUNCH();
+    return 0;
+  }
   lds = (size_t)4 * TILE32 * 2 + (size_t)2 * 3 * BWD_BQ * 4 + BWD_BK * 4 + (size_t)2 * 4 * BWD_BQ * 4;
   if (p.lut) lds += (size_t)(2 * (p.Sq + BWD_BK) + BWD_BQ) * 4;
   if (nblk <= 0 || nblk > 0x7fffffff || lds > 160 * 1024) return -4;

@@ -11,6 +11,8 @@ struct AttnParams {
   uint16_t* o_out;
   float* lse;          // [B, H, Sq]
   float* delta;        // [B, H, Sq] (bwd, written by the dQ kernel)
+  float* rowrec;       // [B*H][sq_pad / 64][4][64] per-row terms for dK/dV (written by the dQ kernel):
+                       // -lse2, c_lo - lse2, c_hi - lse2, -delta (rows >= Sq: -inf, -inf, -inf, 0)
   uint16_t* dq;        // [B, Sq, H, D] strided (bwd)
   uint16_t* dk;        // [B, Sk, H, D]
   uint16_t* dv;

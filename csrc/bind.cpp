@@ -402,6 +402,11 @@ std::vector<Tensor> attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& 
   Tensor dk = pick(dk_out, P.Sk, "dk_out");
   Tensor dv = pick(dv_out, P.Sk, "dv_out");
   auto delta = at::empty({P.B, P.H, P.Sq}, f32);
+  // per-row terms the dQ kernel hands to the v2 dK/dV kernel ([B*H][sq_pad/64][4][64]); DLLM_ATTN_DKDV=1: v1 kernel
+  static const bool dkdv_v1 = [] { const char* e = std::getenv("DLLM_ATTN_DKDV"); return e && e[0] == '1'; }();
+  Tensor rowrec;
+  if (!dkdv_v1) rowrec = at::empty({(int64_t)P.B * P.H * ((P.Sq + 127) / 128 * 128) * 4}, f32);
+  P.rowrec = rowrec.defined() ? rowrec.data_ptr<float>() : nullptr;
   Tensor dlut;
   if (P.lut != nullptr) dlut = at::zeros({P.H, P.Sq + P.Sk - 1}, f32);
   P.o = reinterpret_cast<const uint16_t*>(o.data_ptr());

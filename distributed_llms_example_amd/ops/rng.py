@@ -50,23 +50,22 @@ def keep_mask(seed: int, p: float, shape, device, numel_offset: int = 0) -> torc
 
 
 _G = 0x9E3779B1
-_C = 0x85EBCA6B
+_C24 = 0x9E3779
 
 
 def attention_keep_mask(seed: int, p: float, B: int, H: int, Sq: int, Sk: int, device) -> torch.Tensor:
-    """Attention-probability mask [B, H, Sq, Sk] (mirrors csrc/attn.hip ``attn_keep``).
+    """Attention-probability mask [B, H, Sq, Sk] (mirrors csrc/attn.hip ``attn_pair_hash``).
 
     Per query row ``r = (b*H + h)*Sq + i``: ``rh = mix32(seed, r)`` (computed once per row in the
-    kernels); per key pair ``kp = j >> 1``: ``x = (rh ^ kp*G) * C; x ^= x >> 16``; key ``j`` keeps iff
-    the 16-bit half ``j & 1`` of ``x`` is ``>= threshold16(p)``.  One multiply per two keys inside the
-    attention kernels instead of a full hash per element."""
+    kernels); per key pair ``kp = j >> 1``: ``h = ((rh + kp*G) & 0xFFFFFF) * C24`` (mod 2^32 — one
+    full-rate 24-bit multiply per two keys inside the attention kernels), ``y = h ^ (h >> 16)``; the
+    even key keeps iff ``y & 0xFFFF >= threshold16(p)``, the odd key iff ``h >> 16 >= threshold16(p)``."""
     rows = torch.arange(B * H * Sq, device=device, dtype=torch.int64)
     rh = mix32(seed, rows).view(B, H, Sq, 1)
     j = torch.arange(Sk, device=device, dtype=torch.int64).view(1, 1, 1, Sk)
-    x = rh ^ (((j >> 1) * _G) & _MASK)
-    x = (x * _C) & _MASK
-    x = x ^ (x >> 16)
-    half = torch.where((j & 1) == 1, x >> 16, x & 0xFFFF)
+    x = (rh + (j >> 1) * _G) & 0xFFFFFF
+    h = (x * _C24) & _MASK
+    half = torch.where((j & 1) == 1, h >> 16, (h ^ (h >> 16)) & 0xFFFF)
     return half >= threshold16(p)
 
 

@@ -229,3 +229,20 @@ def test_bf16_params_fp32_grad_buffer_cpu():
         assert float(a.abs().sum()) > 0, seg.name
         cos = torch.nn.functional.cosine_similarity(a.double(), r.double(), dim=0).item()
         assert cos > 0.98, (seg.name, cos)
+
+
+def test_attention_dropout_hash_statistics():
+    """The attention keep-mask hash (one 24-bit multiply per key pair): rate, pair / row / column independence."""
+    p = 0.1
+    k = rng.attention_keep_mask(77, p, 2, 4, 256, 512, "cpu").double()
+    d = 1 - k
+    assert abs(d.mean().item() - p) < 0.002
+    both_pair = (d[..., 0::2] * d[..., 1::2]).mean().item()      # the two keys of one hash
+    both_row = (d[:, :, 0::2, :] * d[:, :, 1::2, :]).mean().item()  # adjacent query rows
+    both_far = (d[..., :256] * d[..., 256:]).mean().item()
+    for v in (both_pair, both_row, both_far):
+        assert abs(v - p * p) < 0.0015, (both_pair, both_row, both_far)
+    # per-key-column and per-row drop rates stay near p (no stuck columns / rows)
+    col = d.mean(dim=(0, 1, 2))
+    row = d.mean(dim=(0, 1, 3))
+    assert (col - p).abs().max().item() < 0.06 and (row - p).abs().max().item() < 0.06

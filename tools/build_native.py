@@ -27,6 +27,12 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CXX = os.environ.get("CXX", "g++")
 
 
+# Per-source flags.  attn.hip: no SLP vectorisation — packing independent f32 adds / FMAs into v_pk_* beside MFMAs
+# costs more issue cycles than the scalar ops (MI355X_MICROARCH.md, per-instruction constants) and the compiler adds
+# v_mov shuffles to form the register pairs.
+EXTRA_FLAGS = {"attn.hip": ["-fno-slp-vectorize"]}
+
+
 def _torch_paths():
     import torch
     from torch.utils import cpp_extension as ce
@@ -67,7 +73,8 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = True) -> str:
         objs.append(obj)
         if force or _newer([src] + headers, obj):
             jobs_list.append([HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-ffp-contract=fast",
-                              "-munsafe-fp-atomics", "-I", CSRC, "-c", src, "-o", obj])
+                              "-munsafe-fp-atomics"] + EXTRA_FLAGS.get(os.path.basename(src), []) +
+                             ["-I", CSRC, "-c", src, "-o", obj])
     # host C++ (torch + pybind11 glue, native runtime pieces): every csrc/*.cpp
     for cpp_src in sorted(glob.glob(os.path.join(CSRC, "*.cpp"))):
         cpp_obj = os.path.join(BUILD, os.path.basename(cpp_src) + ".o")

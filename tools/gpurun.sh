@@ -5,7 +5,7 @@
 #
 # Every step runs under its own time limit, logs to gpurun_out/TAG/, and the first failing step ends
 # the call (no GPU work after a fault, abort or timeout).  Steps:
-#   tests[:PYTEST_ARGS]      pytest -m gpu (default: all GPU tests)
+#   tests[:KEXPR]            pytest -m gpu [-k KEXPR] (default: all GPU tests)
 #   smoke                    __graft_entry__.smoke()
 #   bench[:BENCH_ARGS]       python bench.py BENCH_ARGS        (prints the JSON line)
 #   prof[:BENCH_ARGS]        rocprofv3 --kernel-trace --stats of bench.py -> summary.txt (per step, warmup incl.)
@@ -26,7 +26,9 @@ for step in "$@"; do
   echo "[gpurun.sh] step $n: $step" | tee -a "$OUT/steps.txt"
   case $kind in
     tests)
-      timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread ${arg} > "$log" 2>&1
+      kx=()
+      [ -n "$arg" ] && kx=(-k "$arg")
+      timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread "${kx[@]}" > "$log" 2>&1
       rc=$?; tail -3 "$log" ;;
     smoke)
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$log" 2>&1
