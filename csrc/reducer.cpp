@@ -20,9 +20,27 @@
 #include <torch/csrc/autograd/utils/lambda_post_hook.h>
 #include <torch/csrc/distributed/c10d/ProcessGroup.hpp>
 
+#include <dlfcn.h>
+
+#include <cstdio>
+#include <cstdlib>
 #include <mutex>
 
 namespace dllm {
+
+// roctx marker at every bucket launch (rocprofv3 --marker-trace), resolved at run time so the extension does not
+// link libroctx64; DLLM_ROCTX=0 or a missing library makes it a no-op (utils/profiling.py is the Python side)
+static void roctx_mark(const char* msg) {
+  using MarkFn = void (*)(const char*);
+  static MarkFn fn = [] {
+    const char* e = std::getenv("DLLM_ROCTX");
+    if (e && e[0] == '0') return (MarkFn) nullptr;
+    void* h = dlopen("libroctx64.so", RTLD_LAZY | RTLD_NOLOAD);
+    if (!h) h = dlopen("/opt/rocm/lib/libroctx64.so", RTLD_LAZY);
+    return h ? (MarkFn)dlsym(h, "roctxMarkA") : (MarkFn) nullptr;
+  }();
+  if (fn) fn(msg);
+}
 
 class NativeReducer {
  public:
@@ -115,6 +133,10 @@ class NativeReducer {
 
   void launch_locked(int64_t b) {
     const int64_t s = bounds_[2 * b], e = bounds_[2 * b + 1];
+    char msg[64];
+    std::snprintf(msg, sizeof msg, "allreduce bucket %ld (%.1f MiB)", (long)b,
+                  (double)(e - s) * grad_buf_.element_size() / 1048576.0);
+    roctx_mark(msg);
     std::vector<at::Tensor> ts{grad_buf_.narrow(0, s, e - s)};
     c10d::AllreduceOptions opts;
     opts.reduceOp = use_avg_op_ && average_ ? c10d::ReduceOp::AVG : c10d::ReduceOp::SUM;

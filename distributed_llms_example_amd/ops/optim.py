@@ -40,6 +40,8 @@ class FusedAdamW:
             # uniform: either all decay or none
             if all(no_decay(s.name) for s in flat.segments):
                 self.weight_decay = 0.0
+        for attr in ("master", "exp_avg", "exp_avg_sq", "wd_mask"):
+            flat.register_companion(self, attr)  # kept in step with a reducer-driven relayout (parallel/flat.py)
         self._one = torch.ones((), dtype=torch.float32, device=flat.device)
         # param_groups-like view for schedulers / logging parity with torch optimizers
         self.param_groups = [{"lr": lr, "initial_lr": lr, "weight_decay": weight_decay, "betas": betas, "eps": eps}]
@@ -93,17 +95,24 @@ class FusedAdamW:
 
     # ------------------------------------------------------------------------------------------
     def state_dict(self) -> dict:
-        return {"step": self.step_count, "exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq,
-                "master": self.master, "lr": self.param_groups[0]["lr"], "betas": list(self.betas), "eps": self.eps,
-                "weight_decay": self.weight_decay, "layout": self.flat.state_layout()}
+        """Flat state in the model's canonical (construction) segment order, whatever the current layout."""
+        f = self.flat
+        can = f.to_canonical
+        return {"step": self.step_count, "exp_avg": can(self.exp_avg), "exp_avg_sq": can(self.exp_avg_sq),
+                "master": can(self.master) if self.master is not None else None, "lr": self.param_groups[0]["lr"],
+                "betas": list(self.betas), "eps": self.eps, "weight_decay": self.weight_decay,
+                "layout": [{"name": n, "numel": s.numel} for n, s in
+                           zip(f.canonical, sorted(f.segments, key=lambda s: f.canonical.index(s.name)))]}
 
     def load_state_dict(self, d: dict) -> None:
-        if [s["numel"] for s in d["layout"]] != [s.numel for s in self.flat.segments]:
+        f = self.flat
+        by_name = {s.name: s.numel for s in f.segments}
+        if [s["numel"] for s in d["layout"]] != [by_name.get(n) for n in f.canonical]:
             raise ValueError("optimizer state layout does not match the model")
         self.step_count = int(d["step"])
-        self.exp_avg.copy_(d["exp_avg"])
-        self.exp_avg_sq.copy_(d["exp_avg_sq"])
+        self.exp_avg.copy_(f.from_canonical(d["exp_avg"].to(self.exp_avg.device)))
+        self.exp_avg_sq.copy_(f.from_canonical(d["exp_avg_sq"].to(self.exp_avg_sq.device)))
         if self.master is not None and d.get("master") is not None:
-            self.master.copy_(d["master"])
+            self.master.copy_(f.from_canonical(d["master"].to(self.master.device)))
             self.flat.param_buf.copy_(self.master)
         self.param_groups[0]["lr"] = d.get("lr", self.param_groups[0]["lr"])

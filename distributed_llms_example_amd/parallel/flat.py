@@ -20,6 +20,7 @@ loads in csrc/adamw.hip.  Tied parameters (T5 ``shared`` == ``lm_head``) appear 
 """
 from __future__ import annotations
 
+import builtins
 import os
 from dataclasses import dataclass
 
@@ -27,6 +28,7 @@ import torch
 import torch.nn as nn
 
 ALIGN = 64
+builtins_range = builtins.range
 
 
 @dataclass
@@ -79,6 +81,8 @@ class FlatParams:
             self.params.append(p)
             off += (p.numel() + ALIGN - 1) // ALIGN * ALIGN
         self.numel = off
+        self._companions: list[tuple[object, str]] = []  # flat-indexed tensors kept in step with relayout()
+        self.canonical = [s.name for s in self.segments]  # construction order (optimizer state is saved in it)
         self.param_buf = torch.zeros(off, dtype=self.dtype, device=self.device)
         self.grad_buf = torch.zeros(off, dtype=self.grad_dtype, device=self.device)
         # autograd insists p.grad has p's dtype: with fp32 gradients for bf16 weights the flat slices are handed
@@ -145,6 +149,62 @@ class FlatParams:
                     p.grad = None
             elif g is None or g.data_ptr() != self.grad_buf.data_ptr() + self.segments[i].offset * self.grad_buf.element_size():
                 p.grad = self.grad_view(i)
+
+    # ------------------------------------------------------------------------------------------- layout
+    def register_companion(self, obj, attr: str) -> None:
+        """``getattr(obj, attr)`` is indexed like the flat buffers (optimizer master weights / moments, weight-decay
+        mask): relayout() permutes it together with the parameters."""
+        self._companions.append((obj, attr))
+
+    def _offsets(self, order: list[int]) -> tuple[list[int], int]:
+        offs, off = [0] * len(self.segments), 0
+        for i in order:
+            offs[i] = off
+            off += (self.segments[i].numel + ALIGN - 1) // ALIGN * ALIGN
+        return offs, off
+
+    def _permute(self, t: torch.Tensor, src_offs: list[int], dst_offs: list[int], n: int) -> torch.Tensor:
+        out = torch.zeros(n, dtype=t.dtype, device=t.device)
+        for i, seg in enumerate(self.segments):
+            out[dst_offs[i]:dst_offs[i] + seg.numel] = t[src_offs[i]:src_offs[i] + seg.numel]
+        return out
+
+    @torch.no_grad()
+    def relayout(self, order: list[int]) -> None:
+        """Re-lay the flat buffers with segment ``order[0]`` first, ``order[1]`` next, ... (the reducer's observed
+        gradient-ready order, parallel/reducer.py).  Parameters, gradients (values kept) and every registered
+        companion buffer move together; parameter views and gradient slices are re-pointed."""
+        assert sorted(order) == list(builtins_range(len(self.segments))), "order must be a permutation of segments"
+        src = [seg.offset for seg in self.segments]
+        dst, n = self._offsets(order)
+        self.param_buf = self._permute(self.param_buf, src, dst, n)
+        self.grad_buf = self._permute(self.grad_buf, src, dst, n)
+        for obj, attr in self._companions:
+            t = getattr(obj, attr)
+            if t is not None:
+                setattr(obj, attr, self._permute(t, src, dst, n))
+        segs = [Segment(self.segments[i].name, dst[i], self.segments[i].numel, self.segments[i].shape) for i in order]
+        params = [self.params[i] for i in order]
+        self.segments, self.params, self.numel = segs, params, n
+        for i, (seg, p) in enumerate(zip(self.segments, self.params)):
+            p.data = self.param_buf[seg.offset:seg.offset + seg.numel].view(seg.shape)
+            p._dllm_gbuf = self.grad_view(i)
+        self.attach_grads()
+
+    def canonical_offsets(self) -> tuple[list[int], list[int], int]:
+        """(current offsets, canonical offsets, canonical numel) per current segment."""
+        pos = {name: i for i, name in enumerate(self.canonical)}
+        order = sorted(builtins_range(len(self.segments)), key=lambda i: pos[self.segments[i].name])
+        can, n = self._offsets(order)
+        return [seg.offset for seg in self.segments], can, n
+
+    def to_canonical(self, t: torch.Tensor) -> torch.Tensor:
+        cur, can, n = self.canonical_offsets()
+        return t if cur == can else self._permute(t, cur, can, n)
+
+    def from_canonical(self, t: torch.Tensor) -> torch.Tensor:
+        cur, can, n = self.canonical_offsets()
+        return t if cur == can else self._permute(t, can, cur, self.numel)
 
     def grads(self) -> list[torch.Tensor]:
         """Per-parameter gradient views of the flat buffer (fp32 or param dtype), in ``params`` order."""

@@ -34,6 +34,7 @@ import torch
 import torch.distributed as dist
 
 from .. import _ext
+from ..utils import profiling
 from .flat import FlatParams
 
 DEFAULT_BUCKET_MB = 128.0
@@ -43,7 +44,7 @@ FIRST_BUCKET_MB = 1.0
 class GradReducer:
     def __init__(self, flat: FlatParams, group=None, bucket_mb: float = DEFAULT_BUCKET_MB,
                  first_bucket_mb: float = FIRST_BUCKET_MB, overlap: bool = True, average: bool = True,
-                 native: bool | None = None):
+                 native: bool | None = None, rebuild: bool | None = None):
         self.flat = flat
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -51,10 +52,41 @@ class GradReducer:
         self.overlap = overlap
         self.average = average
         self.enabled = True
+        self.bucket_mb, self.first_bucket_mb = bucket_mb, first_bucket_mb
+        if native is None:
+            native = os.environ.get("DLLM_NATIVE_REDUCER", "1") != "0" and _ext.native() is not None
+        self.use_native = bool(native)
+        # DDP's _rebuild_buckets: after the first synchronised backward the flat layout (and with it the buckets)
+        # is re-laid in the order gradients actually became ready, broadcast from rank 0 so every rank agrees
+        if rebuild is None:
+            rebuild = os.environ.get("DLLM_REBUILD_BUCKETS", "1") != "0"
+        self._rebuild_pending = bool(rebuild) and overlap and self.world > 1
+        # per synchronised backward (diagnostics / tests): segment indices in readiness order, and (bucket, number of
+        # segments ready at its launch) in launch order; the previous backward's logs are kept in *_last
+        self.ready_log: list[int] = []
+        self.launch_log: list[tuple[int, int]] = []
+        self.ready_log_last: list[int] = []
+        self.launch_log_last: list[tuple[int, int]] = []
+        self.rebuilt = False
+        self._manual = []
+        self._hooks = []
+        self.native = None
+        self._build()
+        if self.world > 1 and overlap:
+            for p in flat.params:
+                # run by FlatParams' post-accumulate hook (autograd gradients) or by the fused op that accumulated
+                # the gradient in its kernel (ops/linear.py _fire), once per backward after the last contribution
+                p._dllm_post_hooks = getattr(p, "_dllm_post_hooks", []) + [self._on_ready]
+                self._manual.append(p)
+
+    def _build(self):
+        """Buckets over the current flat layout (segment order) and the engine that launches them."""
+        flat = self.flat
         esz = flat.grad_buf.element_size()
         self.buckets: list[tuple[int, int]] = []
         self.seg_bucket: list[int] = []
-        limit = min(first_bucket_mb, bucket_mb) * 2**20
+        self._seg_of = {id(p): i for i, p in enumerate(flat.params)}
+        limit = min(self.first_bucket_mb, self.bucket_mb) * 2**20
         start = flat.segments[0].offset
         cur_bytes = 0
         counts = []
@@ -70,59 +102,79 @@ class GradReducer:
                 start = seg_end
                 cur_bytes = 0
                 n_in = 0
-                limit = bucket_mb * 2**20
+                limit = self.bucket_mb * 2**20
         self._counts = counts
         self._pending = list(counts)
         self._ready = [False] * len(self.buckets)
         self._next = 0
         self._works = []
         self._callback_queued = False
-        self._hooks = []
-        self._manual = []
-        self.native = None
-        if native is None:
-            native = os.environ.get("DLLM_NATIVE_REDUCER", "1") != "0" and _ext.native() is not None
-        if native and self.world > 1:
-            pg = group if group is not None else dist.distributed_c10d._get_default_group()
+        if self.native is not None:
+            self.native.detach()
+            self.native = None
+        if self.use_native and self.world > 1:
+            pg = self.group if self.group is not None else dist.distributed_c10d._get_default_group()
             bounds = [x for se in self.buckets for x in se]
-            self.native = _ext.native().NativeReducer(flat.grad_buf, bounds, self.seg_bucket, pg, average,
+            self.native = _ext.native().NativeReducer(flat.grad_buf, bounds, self.seg_bucket, pg, self.average,
                                                       self.backend == "nccl")
-            if overlap:  # readiness comes from FlatParams' hooks / the fused ops (ops/linear.py _fire)
-                for i, p in enumerate(flat.params):
-                    p._dllm_post_hooks = getattr(p, "_dllm_post_hooks", []) + [
-                        (lambda _q, i=i, nat=self.native: nat.mark_ready(i))]
-                    self._manual.append(p)
-        elif self.world > 1 and overlap:
-            for i, p in enumerate(flat.params):
-                h = self._make_hook(i)
-                # run by FlatParams' post-accumulate hook (autograd gradients) or by the fused op that accumulated
-                # the gradient in its kernel (ops/linear.py _fire), once per backward after the last contribution
-                p._dllm_post_hooks = getattr(p, "_dllm_post_hooks", []) + [h]
-                self._manual.append(p)
 
     # --------------------------------------------------------------------------------- hooks
-    def _make_hook(self, seg_index: int):
-        def hook(_p):
-            if not self.enabled:
-                return
-            if not self._callback_queued:
-                self._callback_queued = True
-                torch.autograd.Variable._execution_engine.queue_callback(self.finish)
-            b = self.seg_bucket[seg_index]
-            self._pending[b] -= 1
-            if self._pending[b] == 0:
-                self._ready[b] = True
-                self._launch_ready()
-        return hook
+    def _on_ready(self, p):
+        if not self.enabled:
+            return
+        i = self._seg_of[id(p)]
+        self.ready_log.append(i)
+        if self.native is not None:
+            before = self.native.launched()
+            self.native.mark_ready(i)
+            self.launch_log.extend((b, len(self.ready_log)) for b in range(before, self.native.launched()))
+            return
+        if not self._callback_queued:
+            self._callback_queued = True
+            torch.autograd.Variable._execution_engine.queue_callback(self.finish)
+        b = self.seg_bucket[i]
+        self._pending[b] -= 1
+        if self._pending[b] == 0:
+            self._ready[b] = True
+            self._launch_ready()
+
+    @torch.no_grad()
+    def maybe_rebuild(self):
+        """After the first synchronised backward (gradients final and reduced): re-lay the flat buffers in the
+        observed ready order (rank 0's, broadcast) and rebuild the buckets, so bucket k holds the k-th group of
+        gradients to become ready and launches as soon as they are — e.g. the decoder's stacked cross-attention
+        K/V weights, whose gradient only appears at the end of the decoder backward, no longer hold back the
+        bucket of the decoder's last layer.  A no-op when the order already matches."""
+        if not self._rebuild_pending or not self.ready_log:
+            return False
+        self._rebuild_pending = False
+        n = len(self.flat.segments)
+        seen, order = set(), []
+        for i in self.ready_log:
+            if i not in seen:
+                seen.add(i)
+                order.append(i)
+        order += [i for i in range(n) if i not in seen]  # never-ready (unused) parameters last, in layout order
+        t = torch.tensor(order, dtype=torch.int64, device=self.flat.device if self.backend == "nccl" else "cpu")
+        dist.broadcast(t, src=dist.get_global_rank(self.group, 0) if self.group is not None else 0, group=self.group)
+        order = t.tolist()
+        if order == list(range(n)):
+            return False
+        self.flat.relayout(order)
+        self._build()
+        self.rebuilt = True
+        return True
 
     def _launch(self, b: int):
         s, e = self.buckets[b]
         view = self.flat.grad_buf[s:e]
+        profiling.mark(f"allreduce bucket {b} ({(e - s) * view.element_size() / 2**20:.1f} MiB)")
         if self.average and self.backend == "nccl":
             w = dist.all_reduce(view, op=dist.ReduceOp.AVG, group=self.group, async_op=True)
         else:
             w = dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         self._works.append((b, w))
+        self.launch_log.append((b, len(self.ready_log)))
 
     def _launch_ready(self):
         while self._next < len(self.buckets) and self._ready[self._next]:
@@ -176,9 +228,17 @@ class GradReducer:
                 g.div_(self.world)
 
     def post_backward(self):
-        """Call after ``loss.backward()``: completes the reduction for the non-overlapped mode."""
+        """Call after a synchronised ``loss.backward()``: completes the reduction for the non-overlapped mode, rebuilds
+        the buckets in ready order after the first one (maybe_rebuild) and rotates the readiness / launch logs."""
         if self.world > 1 and not self.overlap and self.enabled:
             self.sync_now()
+        if self.ready_log:
+            if self.native is not None:  # leftovers launched by the native finalize
+                n = len(self.ready_log)
+                self.launch_log.extend((b, n) for b in range(len(self.launch_log), len(self.buckets)))
+            self.ready_log_last, self.launch_log_last = list(self.ready_log), list(self.launch_log)
+            self.maybe_rebuild()
+        self.ready_log, self.launch_log = [], []
 
     def broadcast_params(self, module=None, src: int = 0):
         """DDP construction broadcast (distributed.py:864-870): one collective over the flat

@@ -13,6 +13,7 @@ import os
 import torch
 
 from ..ops.optim import FusedAdamW
+from ..utils import profiling
 from ..parallel.env import DistEnv
 from ..parallel.flat import FlatParams
 from ..parallel.reducer import DEFAULT_BUCKET_MB, GradReducer
@@ -84,24 +85,28 @@ class TrainEngine:
         ``grad_accum`` (identical when every micro-batch has the same token count)."""
         ctx = contextlib.nullcontext() if sync else self.no_sync()
         with ctx:
-            out = self.forward(batch)
-            loss = out.loss
-            if num_items is not None:
-                w = dp_ranks if dp_ranks is not None else (self.reducer.world if self.reducer is not None else 1)
-                scale = token_count(batch["labels"]).to(torch.float32) * w / num_items.to(torch.float32)
-                (loss * scale).backward()
-            else:
-                (loss / grad_accum if grad_accum > 1 else loss).backward()
+            with profiling.range("forward"):
+                out = self.forward(batch)
+                loss = out.loss
+            with profiling.range("backward" if sync else "backward(no_sync)"):
+                if num_items is not None:
+                    w = dp_ranks if dp_ranks is not None else (self.reducer.world if self.reducer is not None else 1)
+                    scale = token_count(batch["labels"]).to(torch.float32) * w / num_items.to(torch.float32)
+                    (loss * scale).backward()
+                else:
+                    (loss / grad_accum if grad_accum > 1 else loss).backward()
         if sync and self.reducer is not None:
-            self.reducer.post_backward()
+            with profiling.range("allreduce(post_backward)"):
+                self.reducer.post_backward()
         return loss.detach()
 
     def step(self, lr: float | None = None):
         """Clip + AdamW + zero_grad.  Returns the pre-clip grad norm as a device tensor (or None)."""
         if lr is not None:
             self.optimizer.param_groups[0]["lr"] = lr
-        norm = self.optimizer.step(self.max_grad_norm)
-        self.optimizer.zero_grad()
+        with profiling.range("optimizer(clip+adamw)"):
+            norm = self.optimizer.step(self.max_grad_norm)
+            self.optimizer.zero_grad()
         return norm
 
     def train(self, mode: bool = True):

@@ -1,8 +1,10 @@
 """Tracing / throughput instrumentation.
 
-* ``range(name)``: roctx push/pop ranges (``/opt/rocm/lib/libroctx64.so`` via ctypes) around
-  forward / backward / optimizer / comm so ``rocprofv3 --marker-trace`` timelines are annotated; a
-  no-op when the library is absent or ``DLLM_ROCTX=0``.
+* ``range(name)`` / ``mark(name)``: roctx push/pop ranges and markers (``/opt/rocm/lib/libroctx64.so``
+  via ctypes) around forward / backward / all-reduce / optimizer (train/engine.py) and at every gradient
+  bucket launch (parallel/reducer.py; the native reducer marks through csrc/reducer.cpp), so
+  ``rocprofv3 --marker-trace`` timelines are annotated; a no-op when the library is absent or
+  ``DLLM_ROCTX=0``.
 * ``StepTimer``: wall-clock per step synchronised on the device, samples/s, tokens/s and model FLOP
   utilisation (6 × params × tokens + attention terms, against the MI355X dense bf16 peak).
 """
@@ -29,10 +31,18 @@ def _lib():
                 try:
                     _roctx = ctypes.CDLL(p)
                     _roctx.roctxRangePushA.argtypes = [ctypes.c_char_p]
+                    _roctx.roctxMarkA.argtypes = [ctypes.c_char_p]
                     break
                 except OSError:
                     continue
     return _roctx
+
+
+def mark(name: str) -> None:
+    """Instantaneous roctx marker (bucket launches, step boundaries)."""
+    lib = _lib()
+    if lib is not None:
+        lib.roctxMarkA(name.encode())
 
 
 @contextlib.contextmanager

@@ -81,7 +81,9 @@ def _grad_case(rank, world, overlap=True, ga=1, bucket_mb=0.05, native=None):
         s = slice(rank * 4 + i * mb, rank * 4 + (i + 1) * mb)
         eng.forward_backward({"input_ids": ids[s], "attention_mask": torch.ones_like(ids[s]), "labels": lab[s]},
                              grad_accum=ga, sync=(i == ga - 1))
-    return eng.flat.grad_buf.clone(), eng.flat.param_buf.clone(), len(eng.reducer.buckets)
+    # canonical (construction) layout: the reducer may have re-laid the flat buffers in gradient-ready order
+    return (eng.flat.to_canonical(eng.flat.grad_buf).clone(), eng.flat.to_canonical(eng.flat.param_buf).clone(),
+            len(eng.reducer.buckets))
 
 
 def _reference_grad(world):
@@ -127,6 +129,51 @@ def test_grad_accumulation_no_sync(native):
     a, b = torch.as_tensor(out[0][0]), torch.as_tensor(out[1][0])
     torch.testing.assert_close(a, b)
     torch.testing.assert_close(a, ref, atol=1e-5, rtol=1e-4)
+
+
+def _rebuild_case(rank, world, native):
+    """Two synchronised backwards: the first records the gradient-ready order and re-lays the buckets in it."""
+    from distributed_llms_example_amd.models import build_model
+    from distributed_llms_example_amd.parallel.env import DistEnv
+    from distributed_llms_example_amd.train.engine import TrainEngine
+    os.environ["DLLM_NATIVE_REDUCER"] = "1" if native else "0"
+    torch.manual_seed(0)
+    model = build_model("t5-tiny")
+    env = DistEnv(rank=rank, world_size=world, backend="gloo", device=torch.device("cpu"))
+    eng = TrainEngine(model, env, lr=1e-3, dtype=torch.float32, bucket_mb=0.02, overlap=True)
+    eng.train(False)
+    red = eng.reducer
+    g = torch.Generator().manual_seed(7)
+    ids = torch.randint(3, 500, (4 * world, 10), generator=g)
+    lab = torch.randint(3, 500, (4 * world, 5), generator=g)
+    s = slice(rank * 4, rank * 4 + 4)
+    batch = {"input_ids": ids[s], "attention_mask": torch.ones_like(ids[s]), "labels": lab[s]}
+    eng.forward_backward(batch)
+    first_order = list(red.ready_log_last)
+    rebuilt = red.rebuilt
+    eng.optimizer.zero_grad()
+    eng.forward_backward(batch)
+    ready, launches = list(red.ready_log_last), list(red.launch_log_last)
+    seg_bucket = list(red.seg_bucket)
+    return (first_order, rebuilt, ready, launches, seg_bucket, len(eng.flat.segments),
+            eng.flat.to_canonical(eng.flat.grad_buf).clone())
+
+
+@pytest.mark.parametrize("native", [False, pytest.param(True, marks=pytest.mark.skipif(
+    not _native_available(), reason="native extension not built"))])
+def test_bucket_rebuild_by_ready_order(native):
+    out = run_ranks(functools.partial(_rebuild_case, native=native))
+    first, rebuilt, ready, launches, seg_bucket, nseg, grad = out[0]
+    assert rebuilt, "the registration layout differs from the observed ready order (cross-attention K/V group)"
+    # after the rebuild, segments become ready in layout order and buckets launch in order, each as soon as its
+    # segments are all ready
+    assert ready == sorted(ready) and len(ready) == nseg
+    assert [b for b, _ in launches] == list(range(len(launches))) and len(launches) > 4
+    for b, k in launches:
+        assert max(i for i in range(nseg) if seg_bucket[i] == b) < k
+    assert launches[0][1] < nseg // 2, "the first bucket must launch before the midpoint of backward"
+    torch.testing.assert_close(torch.as_tensor(grad), torch.as_tensor(out[1][6]))
+    torch.testing.assert_close(torch.as_tensor(grad), _reference_grad(2), atol=1e-5, rtol=1e-4)
 
 
 def _collectives(rank, world):
