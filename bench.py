@@ -141,7 +141,8 @@ def main():
                        "grad_dtype": str(eng.flat.grad_buf.dtype).replace("torch.", ""),
                        "backend": env.backend, "world_size": n, "rccl_version": _rccl_version(),
                        "overlap": bool(eng.reducer.overlap) if eng.reducer else None,
-                       "n_buckets": len(eng.reducer.buckets) if eng.reducer else None},
+                       "n_buckets": len(eng.reducer.buckets) if eng.reducer else None,
+                       "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 2)},
         }), flush=True)
     if n > 1:
         dist.barrier()

@@ -35,6 +35,10 @@ int dllm_attn_dropout_mask(AttnParams*, hipStream_t);
 int dllm_gemm_wgrad(const GemmWgradParams*, int, hipStream_t);
 int dllm_gemm_fused(const GemmFusedParams*, int, int, hipStream_t);
 int dllm_colsum_rows();
+int dllm_ce_chunk_fwd(const void*, long, const int64_t*, const float*, float*, float*, float*, long, int, int, int, float,
+                      long, int, int, int, hipStream_t);
+int dllm_ce_chunk_bwd(const float*, void*, long, const int64_t*, const float*, const float*, long, int, int, int, float,
+                      long, int, hipStream_t);
 int dllm_embed_bwd(const int64_t*, const int64_t*, const void*, long, long, int, float*, void*, long, long, int,
                    hipStream_t);
 int dllm_colsum_acc(const void*, long, long, int, float*, void*, int, hipStream_t);
@@ -220,6 +224,47 @@ Tensor ce_bwd(const Tensor& scale, Tensor logits, const Tensor& labels, const Te
                          (float)eps, ignore, is_bf16(logits), stream()),
              "ce_bwd");
   return out;
+}
+
+// vocab-chunked LM head + CE (ops/lm_head.py): logits chunk [N, Vc] bf16 (row stride ld) holding vocab ids c0..c0+Vc-1
+void ce_chunk_fwd(const Tensor& logits, const Tensor& labels, const optional<Tensor>& bias, Tensor& state, Tensor& loss,
+                  Tensor& lse, int64_t c0, int64_t V, double eps, int64_t ignore, bool first, bool last, int64_t skip) {
+  check_gpu(logits, "logits");
+  TORCH_CHECK(logits.dim() == 2 && logits.scalar_type() == at::kBFloat16 && logits.stride(1) == 1 &&
+                  logits.stride(0) % 4 == 0 && logits.size(1) % 4 == 0 && reinterpret_cast<uintptr_t>(logits.data_ptr()) % 8 == 0,
+              "ce_chunk: logits must be bf16 [N, Vc] with Vc % 4 == 0 and 8-B aligned rows");
+  const int64_t N = logits.size(0), Vc = logits.size(1);
+  TORCH_CHECK(labels.scalar_type() == at::kLong && labels.numel() == N && labels.is_contiguous(), "ce_chunk: labels");
+  TORCH_CHECK(state.scalar_type() == at::kFloat && state.numel() == 4 * N && state.is_contiguous(), "ce_chunk: state");
+  TORCH_CHECK(loss.numel() == N && lse.numel() == N && loss.scalar_type() == at::kFloat && lse.scalar_type() == at::kFloat,
+              "ce_chunk: loss / lse");
+  TORCH_CHECK(c0 >= 0 && c0 + Vc <= V, "ce_chunk: chunk outside the vocabulary");
+  const float* bp = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->numel() == V && bias->is_contiguous(), "ce_chunk: bias fp32 [V]");
+    bp = bias->data_ptr<float>();
+  }
+  if (N == 0) return;
+  check_rc(dllm_ce_chunk_fwd(logits.data_ptr(), logits.stride(0), labels.data_ptr<int64_t>(), bp, state.data_ptr<float>(),
+                             loss.data_ptr<float>(), lse.data_ptr<float>(), N, (int)Vc, (int)c0, (int)V, (float)eps,
+                             ignore, first, last, (int)skip, stream()),
+           "ce_chunk_fwd");
+}
+
+void ce_chunk_bwd(const Tensor& scale, Tensor& logits, const Tensor& labels, const Tensor& lse,
+                  const optional<Tensor>& bias, int64_t c0, int64_t V, double eps, int64_t ignore, int64_t skip) {
+  check_gpu(logits, "logits");
+  TORCH_CHECK(logits.dim() == 2 && logits.scalar_type() == at::kBFloat16 && logits.stride(1) == 1 &&
+                  logits.stride(0) % 4 == 0 && logits.size(1) % 4 == 0, "ce_chunk_bwd: logits");
+  const int64_t N = logits.size(0), Vc = logits.size(1);
+  TORCH_CHECK(scale.scalar_type() == at::kFloat && scale.is_cuda() && labels.numel() == N && lse.numel() == N,
+              "ce_chunk_bwd: args");
+  const float* bp = (bias.has_value() && bias->defined()) ? bias->data_ptr<float>() : nullptr;
+  if (N == 0) return;
+  check_rc(dllm_ce_chunk_bwd(scale.data_ptr<float>(), logits.data_ptr(), logits.stride(0), labels.data_ptr<int64_t>(),
+                             lse.data_ptr<float>(), bp, N, (int)Vc, (int)c0, (int)V, (float)eps, ignore, (int)skip,
+                             stream()),
+           "ce_chunk_bwd");
 }
 
 // ------------------------------------------------------------------------------------------- optimizer
@@ -643,6 +688,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ce_bwd", &ce_bwd);
   m.def("sq_norm", &sq_norm);
   m.def("embed_bwd", &embed_bwd);
+  m.def("ce_chunk_fwd", &ce_chunk_fwd);
+  m.def("ce_chunk_bwd", &ce_chunk_bwd);
   m.def("adamw_step", &adamw_step);
   m.def("attn_fwd", &attn_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("kpm"), py::arg("lut"),
         py::arg("scale"), py::arg("causal"), py::arg("p"), py::arg("seed"), py::arg("dmask_in") = py::none(),

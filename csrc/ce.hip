@@ -88,7 +88,108 @@ __global__ __launch_bounds__(256) void ce_bwd_kernel(const float* __restrict__ s
   }
 }
 
+// ---- vocab-chunked LM head + CE (ops/lm_head.py): the logits exist one [N, Vc] chunk at a time
+// Per row running state st[row] = {max, sum exp(x - max), sum x, x_label} merged over chunks; the last chunk writes
+// loss_row and lse.  Chunk columns are global vocab ids c0 .. c0 + Vc - 1; eps / V uses the full vocab size.
+__global__ __launch_bounds__(256) void ce_chunk_fwd_kernel(const uint16_t* __restrict__ logits, long ld,
+                                                           const int64_t* __restrict__ labels,
+                                                           const float* __restrict__ bias, f32x4* __restrict__ st,
+                                                           float* __restrict__ loss_out, float* __restrict__ lse_out,
+                                                           int Vc, int c0, int V, float eps, long ignore, int first,
+                                                           int last, int skip) {
+  __shared__ float red[4];
+  const long row = blockIdx.x;
+  const uint16_t* x = logits + row * ld;
+  float m = -INFINITY, s = 0.f, sx = 0.f;
+  for (int c = threadIdx.x * 4; c < Vc; c += 256 * 4) {  // Vc % 4 == 0
+    f32x4 v = Elem<uint16_t>::load4(x + c);
+    if (bias != nullptr) v += *reinterpret_cast<const f32x4*>(bias + c0 + c);
+    if (c < skip) {  // leading columns already covered by the previous chunk (ragged vocab tail)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = c + k < skip ? -INFINITY : v[k];
+    }
+    const float lm = fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w));
+    const float nm = fmaxf(m, lm);
+    if (nm != -INFINITY) {
+      s = s * __expf(m - nm) + __expf(v.x - nm) + __expf(v.y - nm) + __expf(v.z - nm) + __expf(v.w - nm);
+      m = nm;
+    }
+    if (c < skip) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) sx += c + k < skip ? 0.f : v[k];
+    } else {
+      sx += (v.x + v.y) + (v.z + v.w);
+    }
+  }
+  const float M = block_max<256>(m, red);
+  const float scaled = (m == -INFINITY) ? 0.f : s * __expf(m - M);
+  const float S = block_sum<256>(scaled, red);
+  const float SX = block_sum<256>(sx, red);
+  if (threadIdx.x == 0) {
+    const long y = labels[row];
+    f32x4 cur = first ? f32x4{-INFINITY, 0.f, 0.f, 0.f} : st[row];
+    const float nm = fmaxf(cur.x, M);
+    cur.y = (cur.x == -INFINITY ? 0.f : cur.y * __expf(cur.x - nm)) + (M == -INFINITY ? 0.f : S * __expf(M - nm));
+    cur.x = nm;
+    cur.z += SX;
+    if (y >= c0 + skip && y < c0 + Vc) cur.w = Elem<uint16_t>::load(x + (y - c0)) + (bias != nullptr ? bias[y] : 0.f);
+    st[row] = cur;
+    if (last) {
+      const float lse = cur.x + __logf(cur.y);
+      const bool valid = y != ignore && y >= 0 && y < V;
+      loss_out[row] = valid ? lse - (1.f - eps) * cur.w - eps * cur.z / (float)V : 0.f;
+      lse_out[row] = lse;
+    }
+  }
+}
+
+// dlogits of one chunk, in place: g * (exp(x - lse) - eps / V - (1 - eps) [c0 + col == y])
+__global__ __launch_bounds__(256) void ce_chunk_bwd_kernel(const float* __restrict__ scale, uint16_t* __restrict__ x_io,
+                                                           long ld, const int64_t* __restrict__ labels,
+                                                           const float* __restrict__ lse_in,
+                                                           const float* __restrict__ bias, int Vc, int c0, int V,
+                                                           float eps, long ignore, int skip) {
+  const long row = blockIdx.x;
+  uint16_t* x = x_io + row * ld;
+  const long y = labels[row];
+  const bool valid = (y != ignore && y >= 0 && y < V);
+  const float g = valid ? scale[0] : 0.f;
+  const float lse = lse_in[row];
+  const float off = eps / (float)V;
+  const float hit = 1.f - eps;
+  const long yl = y - c0;
+  for (int c = threadIdx.x * 4; c < Vc; c += 256 * 4) {
+    f32x4 v = Elem<uint16_t>::load4(x + c);
+    if (bias != nullptr) v += *reinterpret_cast<const f32x4*>(bias + c0 + c);
+    f32x4 r;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      r[k] = c + k < skip ? 0.f : g * (__expf(v[k] - lse) - off - ((c + k) == yl ? hit : 0.f));
+    Elem<uint16_t>::store4(x + c, r);
+  }
+}
+
 }  // namespace
+
+extern "C" int dllm_ce_chunk_fwd(const void* logits, long ld, const int64_t* labels, const float* bias, float* state,
+                                 float* loss, float* lse, long N, int Vc, int c0, int V, float eps, long ignore,
+                                 int first, int last, int skip, hipStream_t st) {
+  if (Vc % 4 || ld % 4 || N <= 0 || skip < 0 || skip >= Vc) return -2;
+  hipLaunchKernelGGL(ce_chunk_fwd_kernel, dim3(N), dim3(256), 0, st, (const uint16_t*)logits, ld, labels, bias,
+                     (f32x4*)state, loss, lse, Vc, c0, V, eps, ignore, first, last, skip);
+  DLLM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dllm_ce_chunk_bwd(const float* scale, void* logits, long ld, const int64_t* labels, const float* lse,
+                                 const float* bias, long N, int Vc, int c0, int V, float eps, long ignore, int skip,
+                                 hipStream_t st) {
+  if (Vc % 4 || ld % 4 || N <= 0 || skip < 0 || skip >= Vc) return -2;
+  hipLaunchKernelGGL(ce_chunk_bwd_kernel, dim3(N), dim3(256), 0, st, scale, (uint16_t*)logits, ld, labels, lse, bias,
+                     Vc, c0, V, eps, ignore, skip);
+  DLLM_CHECK_LAUNCH();
+  return 0;
+}
 
 extern "C" int dllm_ce_fwd(const void* logits, const int64_t* labels, const float* bias, float* loss, float* lse,
                            long N, int V, float eps, long ignore, int is_bf16, hipStream_t st) {

@@ -20,6 +20,7 @@ from ..ops.ffn import ffn
 from ..ops.cross_entropy import cross_entropy
 from ..ops.embedding import embedding
 from ..ops.linear import Linear, linear, stacked_linear
+from ..ops.lm_head import lm_head_loss, use_chunked
 from ..ops.rng import default_rng
 from .blocks import run_block
 from .config import Seq2SeqConfig
@@ -251,6 +252,11 @@ class BartForConditionalGeneration(nn.Module):
             decoder_input_ids = self.shift_right(labels)
         dec = self.decode(decoder_input_ids, enc, attention_mask)
         loss = None
+        if labels is not None and not return_logits and use_chunked(labels.numel(), self.config.vocab_size):
+            # vocabulary-chunked LM head + CE with final_logits_bias (ops/lm_head.py)
+            loss = lm_head_loss(dec, self.output_embedding(), labels, bias=self.logits_bias(),
+                                label_smoothing=label_smoothing)
+            return Seq2SeqLMOutput(loss=loss, logits=None, encoder_last_hidden_state=enc)
         if labels is not None and not return_logits:
             raw = linear(dec, self.output_embedding())
             V = raw.shape[-1]

@@ -25,6 +25,7 @@ from ..ops.ffn import ffn
 from ..ops.cross_entropy import cross_entropy
 from ..ops.embedding import embedding
 from ..ops.linear import Linear, linear, stacked_linear
+from ..ops.lm_head import lm_head_loss, use_chunked
 from ..ops.rng import default_rng
 from .blocks import run_block
 from .config import Seq2SeqConfig
@@ -344,6 +345,11 @@ class T5ForConditionalGeneration(nn.Module):
         if decoder_input_ids is None:
             decoder_input_ids = self.shift_right(labels)
         dec = self.decode(decoder_input_ids, enc, attention_mask)
+        if labels is not None and not return_logits and use_chunked(labels.numel(), self.config.vocab_size):
+            # vocabulary-chunked LM head + CE: the [tokens, V] logits never exist (ops/lm_head.py)
+            scale = self.config.d_model ** -0.5 if self.config.scale_decoder_outputs else None
+            loss = lm_head_loss(dec, self.output_embedding(), labels, scale=scale, label_smoothing=label_smoothing)
+            return Seq2SeqLMOutput(loss=loss, logits=None, encoder_last_hidden_state=enc)
         logits = self.lm_logits(dec)
         loss = None
         if labels is not None:

@@ -1,0 +1,145 @@
+"""LM head + (label-smoothed) cross-entropy over vocabulary chunks: the ``[tokens, V]`` logits never exist.
+
+Reference path: ``model(**batch).loss`` (ref/train-accelerator.py:220-221, ref/train-task.py:289-290) computes
+``lm_head(decoder_output)`` → ``[B·T, V]`` logits → ``CrossEntropyLoss`` (T5: ``d_model^-0.5`` on the decoder
+output, modeling_t5.py:1044-1045; BART: ``+ final_logits_bias``, modeling_bart.py:940; the Trainer's label
+smoother for ``label_smoothing_factor``).  Materialised in bf16 that is ``B·T·V·2`` bytes (1.05 GB at t5-base,
+b=128; 3.3 GB for BART-large b=32 at 1024 target tokens), written by the GEMM, read by the CE forward, read +
+written by its backward, read twice more by the input- and weight-gradient GEMMs.
+
+Here the vocabulary is processed in chunks of ``Vc`` columns sized so a chunk of logits (``N·Vc·2`` bytes,
+≤ ``DLLM_LMHEAD_CHUNK_MB``, default 128 MiB) stays resident in the MI355X's 256 MiB Infinity Cache:
+
+* forward: per chunk one GEMM ``h·W_cᵀ`` into a reused buffer, then csrc/ce.hip ``ce_chunk_fwd`` merges the
+  chunk into a per-row online state {max, Σexp, Σx, x_label}; the last chunk writes loss_row and lse;
+* backward: per chunk the logits GEMM again, ``ce_chunk_bwd`` turns them into ``g·(softmax - target)`` in place,
+  then the input-gradient GEMM (accumulated in fp32) and the weight-gradient GEMM straight into the weight's
+  slice of the flat gradient buffer (ops/gemm.py, ragged-M wgrad kernel), reducer hooks fired once at the end.
+
+The price is one extra logits GEMM per step (the recompute); the gain is memory (no ``[N, V]`` tensor, no
+``[N, V]`` gradient) and cache-resident CE passes.  Used when the full logits would exceed
+``DLLM_LMHEAD_FULL_MB`` (default 2048 MiB; ``0`` = always chunked, ``-1`` = never), or explicitly by callers.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.nn.functional as F
+
+from .. import _ext
+from .gemm import wgrad_accumulate
+from .linear import _fire, _fusable, _gbuf, _use
+
+
+def _chunk_cols(N: int, V: int) -> int:
+    mb = float(os.environ.get("DLLM_LMHEAD_CHUNK_MB", "128"))
+    c = int(mb * 2**20 / (2 * max(N, 1))) // 256 * 256
+    c = max(256, min(c, (V + 255) // 256 * 256))
+    if V % 8 and c >= V:  # a ragged vocabulary needs >= 2 chunks (the tail chunk re-covers aligned columns)
+        c = max(8, (V // 2 + 255) // 256 * 256)
+    return c
+
+
+def _chunks(V: int, vc: int):
+    """(first column, width, leading columns to skip) per chunk.  Widths are multiples of 8 (the CE kernels' 4-wide
+    vectors, 16-B aligned logits rows): a ragged vocabulary tail (BART: 50265) re-covers the last few columns of the
+    previous chunk and skips them."""
+    out = []
+    for c0 in range(0, V, vc):
+        n = min(vc, V - c0)
+        if n % 8 and V >= 8:
+            n8 = min(V, (n + 7) // 8 * 8)
+            out.append((V - n8, n8, n8 - n))
+        else:
+            out.append((c0, n, 0))
+    return out
+
+
+def use_chunked(N: int, V: int) -> bool:
+    lim = float(os.environ.get("DLLM_LMHEAD_FULL_MB", "2048"))
+    if lim < 0:
+        return False
+    return N * V * 2 > lim * 2**20
+
+
+def _reference(h, w, labels, bias, smoothing, ignore_index):
+    logits = F.linear(h.float(), w.float())
+    if bias is not None:
+        logits = logits + bias.float()
+    return F.cross_entropy(logits, labels, ignore_index=ignore_index, label_smoothing=smoothing)
+
+
+class _LMHeadCEFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h, w, bias, labels, smoothing, ignore_index, params):
+        C = _ext.native()
+        N, d = h.shape
+        V = w.shape[0]
+        vc = _chunk_cols(N, V)
+        buf = torch.empty(N * min(vc + 8, V), dtype=h.dtype, device=h.device)
+        state = torch.empty(N, 4, dtype=torch.float32, device=h.device)
+        loss_rows = torch.empty(N, dtype=torch.float32, device=h.device)
+        lse = torch.empty(N, dtype=torch.float32, device=h.device)
+        bias32 = bias.float().contiguous() if bias is not None else None
+        chunks = _chunks(V, vc)
+        for j, (c0, n, skip) in enumerate(chunks):
+            lg = buf[:N * n].view(N, n)
+            torch.mm(h, w[c0:c0 + n].t(), out=lg)
+            C.ce_chunk_fwd(lg, labels, bias32, state, loss_rows, lse, c0, V, float(smoothing), int(ignore_index),
+                           j == 0, j + 1 == len(chunks), skip)
+        count = (labels != ignore_index).sum().clamp_min(1).to(torch.float32)
+        ctx.save_for_backward(h, w, labels, lse, count)
+        ctx.bias32 = bias32
+        ctx.cfg = (float(smoothing), int(ignore_index), vc)
+        ctx.params = params
+        if params is not None:
+            _use(params[0])
+        return loss_rows.sum() / count
+
+    @staticmethod
+    def backward(ctx, g):
+        C = _ext.native()
+        h, w, labels, lse, count = ctx.saved_tensors
+        smoothing, ignore_index, vc = ctx.cfg
+        N, d = h.shape
+        V = w.shape[0]
+        scale = (g.float() / count).reshape(1)
+        p = ctx.params[0] if ctx.params is not None else None
+        gw = _gbuf(p) if p is not None else None
+        dw = torch.zeros_like(w, dtype=torch.float32) if (gw is None and ctx.needs_input_grad[1]) else None
+        dh = torch.zeros(N, d, dtype=torch.float32, device=h.device)
+        buf = torch.empty(N * min(vc + 8, V), dtype=h.dtype, device=h.device)
+        for c0, n, skip in _chunks(V, vc):
+            lg = buf[:N * n].view(N, n)
+            wc = w[c0:c0 + n]
+            torch.mm(h, wc.t(), out=lg)
+            C.ce_chunk_bwd(scale, lg, labels, lse, ctx.bias32, c0, V, smoothing, ignore_index, skip)  # skipped -> 0
+            dh += torch.mm(lg, wc)
+            with torch.no_grad():
+                if gw is not None:
+                    wgrad_accumulate(gw[c0:c0 + n], lg, h)
+                elif dw is not None:
+                    dw[c0:c0 + n] += torch.mm(lg.t(), h)
+        if p is not None:
+            _fire(p)
+        return dh.to(h.dtype), (dw.to(w.dtype) if dw is not None else None), None, None, None, None, None
+
+
+def lm_head_loss(hidden: torch.Tensor, weight: torch.Tensor, labels: torch.Tensor, *, scale: float | None = None,
+                 bias: torch.Tensor | None = None, label_smoothing: float = 0.0, ignore_index: int = -100):
+    """Mean (label-smoothed) CE of ``(hidden * scale) @ weightᵀ (+ bias)`` against ``labels`` over non-ignored rows,
+    computed in vocabulary chunks (module docstring).  ``hidden [..., d]``, ``labels [...]``."""
+    d = hidden.shape[-1]
+    h = hidden.reshape(-1, d)
+    if scale is not None:
+        h = h * scale
+    lab = labels.reshape(-1)
+    if not _ext.use_native(h):
+        return _reference(h, weight, lab, bias, label_smoothing, ignore_index)
+    params = None
+    w = weight
+    if torch.is_grad_enabled() and _fusable(weight) and weight.requires_grad:
+        params = (weight,)
+        w = weight.detach()
+    return _LMHeadCEFn.apply(h.contiguous(), w, bias, lab.contiguous(), label_smoothing, ignore_index, params)

@@ -220,3 +220,47 @@ def test_global_token_normalisation_equals_full_batch_mean():
     for i, b in enumerate(mbs):
         alt.forward_backward(b, grad_accum=len(mbs), sync=i + 1 == len(mbs))
     assert _rel(alt.flat.grad_buf, ref_eng.flat.grad_buf) > 3 * _rel(g, ref_eng.flat.grad_buf)
+
+
+@pytest.mark.parametrize("bias,smooth,V", [(False, 0.0, 32128), (True, 0.1, 50265), (False, 0.1, 4000)])
+def test_lm_head_chunked_ce_matches_fp32(bias, smooth, V, monkeypatch):
+    """Vocab-chunked LM head + CE (ops/lm_head.py) vs F.cross_entropy on fp32 logits: loss, dh, dW (flat buffer)."""
+    from distributed_llms_example_amd.ops.lm_head import lm_head_loss
+    from distributed_llms_example_amd.parallel.flat import FlatParams
+    monkeypatch.setenv("DLLM_LMHEAD_CHUNK_MB", "8")  # several chunks, ragged last one
+    torch.manual_seed(0)
+    N, d = 1000, 768
+    emb = torch.nn.Embedding(V, d).cuda().to(torch.bfloat16)
+    with torch.no_grad():
+        emb.weight.normal_(0, 0.05)
+    flat = FlatParams(emb, grad_dtype=torch.float32)
+    h = (torch.randn(N, d, device=DEV) * 0.5).to(torch.bfloat16).requires_grad_(True)
+    labels = torch.randint(0, V, (N,), device=DEV)
+    labels[::7] = -100
+    b = (torch.randn(V, device=DEV) * 0.1) if bias else None
+    loss = lm_head_loss(h, emb.weight, labels, scale=0.5, bias=b, label_smoothing=smooth)
+    loss.backward()
+    hr = h.detach().float().requires_grad_(True)
+    wr = emb.weight.detach().float().requires_grad_(True)
+    logits = (hr * 0.5) @ wr.t() + (b if bias else 0)
+    ref = torch.nn.functional.cross_entropy(logits, labels, ignore_index=-100, label_smoothing=smooth)
+    ref.backward()
+    assert abs(loss.item() - ref.item()) < 2e-3 * ref.item(), (loss.item(), ref.item())
+    assert _rel(h.grad, hr.grad) < 1e-2, _rel(h.grad, hr.grad)
+    assert _rel(flat.grad_view(0), wr.grad) < 1e-2, _rel(flat.grad_view(0), wr.grad)
+
+
+def test_t5_chunked_lm_head_matches_full(monkeypatch):
+    """The T5 model's loss / flat gradient with the chunked LM head == with materialised logits."""
+    cfg = _small_cfg()
+    torch.manual_seed(0)
+    sd = build_model(cfg).state_dict()
+    b = _micro_batches(cfg, n=1, B=4)[0]
+    res = []
+    for full_mb in ("-1", "0"):
+        monkeypatch.setenv("DLLM_LMHEAD_FULL_MB", full_mb)
+        eng = _engine(cfg, sd, torch.float32)
+        loss = eng.forward_backward(b)
+        res.append((float(loss), eng.flat.grad_buf.clone()))
+    assert abs(res[0][0] - res[1][0]) < 1e-3 * res[0][0]
+    assert _rel(res[1][1], res[0][1]) < 1e-2, _rel(res[1][1], res[0][1])
