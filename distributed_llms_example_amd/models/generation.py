@@ -16,6 +16,8 @@ projected once per generate call, and every decode step runs the same fused kern
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from ..ops.attention import relative_bias_lut  # noqa: F401  (documented dependency)
@@ -37,8 +39,10 @@ class KVCache:
         return self.k[:, :self.len], self.v[:, :self.len]
 
     def reorder(self, idx):
-        self.k = self.k.index_select(0, idx)
-        self.v = self.v.index_select(0, idx)
+        """Beam reorder of the live prefix only (the preallocated tail holds nothing yet)."""
+        n = self.len
+        self.k[:, :n] = self.k[:, :n].index_select(0, idx)
+        self.v[:, :n] = self.v[:, :n].index_select(0, idx)
 
 
 def _head_geom(model):
@@ -46,6 +50,35 @@ def _head_geom(model):
     if cfg.model_type == "t5":
         return cfg.num_heads, cfg.d_kv
     return cfg.num_heads, cfg.d_model // cfg.num_heads
+
+
+def _ban_ngrams(logp, seqs, cur_len: int, n: int):
+    """no_repeat_ngram_size on the device: every earlier n-gram whose first n-1 tokens equal the last n-1 generated
+    tokens bans its n-th token (transformers NoRepeatNGramLogitsProcessor), without a host round trip."""
+    if n <= 0 or cur_len < n:  # no complete earlier n-gram yet
+        return logp
+    prev = seqs[:, :cur_len]
+    if n == 1:
+        return logp.scatter_(1, prev, float("-inf"))
+    wins = prev.unfold(1, n, 1)  # [N, cur_len - n + 1, n]
+    match = (wins[:, :, :n - 1] == prev[:, cur_len - n + 1:cur_len].unsqueeze(1)).all(-1)
+    tok = wins[:, :, n - 1]
+    vals = torch.where(match, torch.full_like(tok, 0, dtype=logp.dtype) - float("inf"),
+                       torch.full_like(tok, 0, dtype=logp.dtype) + float("inf"))
+    return logp.scatter_reduce_(1, tok, vals, reduce="amin", include_self=True)
+
+
+def _apply_processors_device(logp, seqs, cur_len, min_length, no_repeat_ngram_size, forced_bos, forced_eos,
+                             max_length, eos):
+    if min_length is not None and cur_len < min_length and eos is not None:
+        logp[:, eos] = -float("inf")
+    if forced_bos is not None and cur_len == 1:
+        logp.fill_(-float("inf"))
+        logp[:, forced_bos] = 0.0
+    if forced_eos is not None and cur_len == max_length - 1:
+        logp.fill_(-float("inf"))
+        logp[:, forced_eos] = 0.0
+    return _ban_ngrams(logp, seqs, cur_len, no_repeat_ngram_size or 0)
 
 
 def _apply_processors(logp, seqs, cur_len, cfg, min_length, no_repeat_ngram_size, forced_bos, forced_eos,
@@ -71,6 +104,85 @@ def _apply_processors(logp, seqs, cur_len, cfg, min_length, no_repeat_ngram_size
             if banned:
                 logp[b, [t for t in banned if t < V]] = -float("inf")
     return logp
+
+
+def _beam_search_device(model, seqs, enc, attention_mask, caches, cross, B, nb, max_length, process, eos, pad,
+                        length_penalty, early_stopping, check_every):
+    """Beam search with all bookkeeping on the device (transformers BeamSearchScorer semantics): top-2·nb candidates
+    over nb·V, eos candidates ranked < nb scored ``sum_logprobs / len**length_penalty`` into a per-batch top-nb of
+    finished hypotheses, the first nb non-eos candidates become the next beams, ``is_done`` per batch; the host only
+    looks at ``done.all()`` every ``check_every`` steps and at the final length."""
+    dev = seqs.device
+    L = max_length
+    inf = float("inf")
+    beam_scores = torch.zeros(B, nb, device=dev)
+    beam_scores[:, 1:] = -1e9
+    fin_scores = torch.full((B, nb), -inf, device=dev)
+    fin_seqs = torch.full((B, nb, L), pad, dtype=torch.long, device=dev)
+    fin_len = torch.zeros(B, nb, dtype=torch.long, device=dev)
+    fin_cnt = torch.zeros(B, dtype=torch.long, device=dev)
+    done = torch.zeros(B, dtype=torch.bool, device=dev)
+    base = torch.arange(B, device=dev).unsqueeze(1) * nb
+    rank = torch.arange(2 * nb, device=dev).unsqueeze(0)
+
+    def add_finished(scores, cand_seqs, cand_len):
+        nonlocal fin_scores, fin_seqs, fin_len
+        all_s = torch.cat([fin_scores, scores], 1)
+        keep_s, keep_i = all_s.topk(nb, dim=1)
+        all_seq = torch.cat([fin_seqs, cand_seqs], 1)
+        fin_seqs = all_seq.gather(1, keep_i.unsqueeze(-1).expand(-1, -1, L))
+        fin_len = torch.cat([fin_len, cand_len], 1).gather(1, keep_i)
+        fin_scores = keep_s
+
+    cur = 1
+    while cur < max_length:
+        h = model.decode(seqs[:, cur - 1:cur], enc, attention_mask, caches=caches, q_offset=cur - 1, cross_kv=cross)
+        logp = process(torch.log_softmax(model.lm_logits(h[:, -1]).float(), dim=-1), seqs, cur)
+        V = logp.shape[-1]
+        top_s, top_i = (beam_scores.view(-1, 1) + logp).view(B, nb * V).topk(2 * nb, dim=1)
+        src = base + top_i // V
+        tok = top_i % V
+        is_eos = tok == eos if eos is not None else torch.zeros_like(tok, dtype=torch.bool)
+        # finished hypotheses: eos candidates among the top nb of a live batch
+        add = is_eos & (rank < nb) & ~done.unsqueeze(1)
+        if eos is not None:
+            sc = torch.where(add, top_s / (max(cur, 1) ** length_penalty), torch.full_like(top_s, -inf))
+            cand = seqs.index_select(0, src.reshape(-1)).view(B, 2 * nb, L)
+            cand[:, :, cur] = tok
+            add_finished(sc, cand, torch.full_like(tok, cur + 1))
+            fin_cnt = torch.clamp(fin_cnt + add.sum(1), max=nb)
+        # next beams: the first nb non-eos candidates in rank order; finished batches stay frozen on pad
+        order = (is_eos.long() * (2 * nb) + rank).argsort(dim=1)[:, :nb]
+        new_scores = top_s.gather(1, order)
+        new_src = src.gather(1, order)
+        new_tok = tok.gather(1, order)
+        dn = done.unsqueeze(1)
+        new_scores = torch.where(dn, torch.full_like(new_scores, -1e9), new_scores)
+        new_src = torch.where(dn, base.expand(-1, nb), new_src)
+        new_tok = torch.where(dn, torch.full_like(new_tok, pad), new_tok)
+        # BeamHypotheses.is_done
+        full = fin_cnt >= nb
+        if early_stopping is True:
+            now = full
+        else:
+            gl = cur if early_stopping is False else max_length - 1
+            now = full & (fin_scores.min(1).values >= new_scores.max(1).values / (max(gl, 1) ** length_penalty))
+        done = done | now
+        idx = new_src.reshape(-1)
+        seqs = seqs.index_select(0, idx)
+        seqs[:, cur] = new_tok.reshape(-1)
+        for c in caches:
+            c.reorder(idx)
+        beam_scores = new_scores
+        cur += 1
+        if cur % check_every == 0 and bool(done.all()):
+            break
+    # finalize: the running beams of unfinished batches join the finished hypotheses, best one per batch
+    live = ~done.unsqueeze(1)
+    sc = torch.where(live, beam_scores / (max(cur - 1, 1) ** length_penalty), torch.full_like(beam_scores, -inf))
+    add_finished(sc, seqs.view(B, nb, L), torch.full((B, nb), cur, dtype=torch.long, device=dev))
+    best, best_len = fin_seqs[:, 0], fin_len[:, 0]
+    return best[:, :int(best_len.max())]
 
 
 @torch.no_grad()
@@ -110,23 +222,37 @@ def generate(model, input_ids, attention_mask=None, max_length: int | None = Non
         seqs = torch.full((N, max_length), pad, dtype=torch.long, device=dev)
         seqs[:, 0] = start
         cur = 1
-        if nb == 1:
+        check_every = max(1, int(os.environ.get("DLLM_GEN_CHECK_EVERY", "8")))
+
+        def process(logp, sq, c):
+            return _apply_processors_device(logp, sq, c, min_length, no_repeat_ngram_size, forced_bos, forced_eos,
+                                            max_length, eos)
+
+        if nb == 1:  # greedy: device-side done flags, one host check every check_every steps
             done = torch.zeros(B, dtype=torch.bool, device=dev)
+            all_done_at = []
             while cur < max_length:
                 h = model.decode(seqs[:, cur - 1:cur], enc, attention_mask, caches=caches, q_offset=cur - 1,
                                  cross_kv=cross)
-                logp = torch.log_softmax(model.lm_logits(h[:, -1]).float(), dim=-1)
-                logp = _apply_processors(logp, seqs[:, :cur], cur, cfg, min_length, no_repeat_ngram_size, forced_bos,
-                                         forced_eos, max_length, eos)
+                logp = process(torch.log_softmax(model.lm_logits(h[:, -1]).float(), dim=-1), seqs, cur)
                 nxt = logp.argmax(-1)
                 nxt = torch.where(done, torch.full_like(nxt, pad), nxt)
                 seqs[:, cur] = nxt
-                done |= nxt == eos
+                if eos is not None:
+                    done |= nxt == eos
+                all_done_at.append(done.all())
                 cur += 1
-                if bool(done.all()):
+                if cur % check_every == 0 and bool(all_done_at[-1]):
                     break
-            return seqs[:, :cur]
-        # ---------------------------------------------------------------- beam search
+            # trim the steps run after every sequence had finished (at most check_every - 1)
+            flags = torch.stack(all_done_at).tolist() if all_done_at else []
+            end = next((i + 2 for i, f in enumerate(flags) if f), cur)
+            return seqs[:, :end]
+        if os.environ.get("DLLM_GEN_HOST", "0") != "1":
+            return _beam_search_device(model, seqs, enc, attention_mask, caches, cross, B, nb, max_length, process,
+                                       eos, pad, length_penalty, early_stopping, check_every)
+        # ---------------------------------------------------------------- beam search, host bookkeeping
+        # (DLLM_GEN_HOST=1: the original per-step host loop, kept as the A/B oracle of the device version)
         beam_scores = torch.zeros(B, nb, device=dev)
         beam_scores[:, 1:] = -1e9
         beam_scores = beam_scores.view(-1)
