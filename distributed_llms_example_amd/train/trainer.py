@@ -188,6 +188,8 @@ class Trainer:
         total_loss_sum, total_loss_n = 0.0, 0
         last_norm = None
         ga = args.gradient_accumulation_steps
+        warm_step = self.state.global_step + min(2, max(0, max_steps - self.state.global_step - 1))
+        t_warm = t_last = None
         for epoch in range(start_epoch, epochs):
             loader, sampler = self._loader(self.train_dataset, args.per_device_train_batch_size, True, epoch)
             self.handler.fire("on_epoch_begin", args, self.state, self.control)
@@ -214,6 +216,13 @@ class Trainer:
                 last_norm = eng.step(self.scheduler.get_last_lr()[0])
                 self.scheduler.step()
                 self.state.global_step += 1
+                if self.state.global_step in (warm_step, max_steps):  # steady-state clock: after the first steps,
+                    if env.device.type == "cuda":                      # before the final eval / checkpoint
+                        torch.cuda.synchronize()
+                    if self.state.global_step == warm_step:
+                        t_warm = time.perf_counter()
+                    else:
+                        t_last = time.perf_counter()
                 self.state.epoch = epoch + done / max(1, n_micro)
                 self.control = self.handler.fire("on_step_end", args, self.state, self.control)
                 if self.control.should_log:
@@ -252,6 +261,12 @@ class Trainer:
         metrics = {"train_runtime": round(runtime, 4), "train_samples_per_second": round(n_samples / runtime, 3),
                    "train_steps_per_second": round(self.state.global_step / runtime, 3),
                    "train_loss": train_loss, "epoch": round(self.state.epoch, 4)}
+        if t_warm is not None and t_last is not None and self.state.global_step > warm_step:
+            # loop throughput without the first steps (allocator / kernel warm-up) and without the final evaluation /
+            # checkpoint: the number comparable with bench.py
+            per_step = args.per_device_train_batch_size * ga * self.dp_world
+            dt = t_last - t_warm
+            metrics["train_steady_samples_per_second"] = round(per_step * (self.state.global_step - warm_step) / dt, 3)
         self.log(metrics)
         self.handler.fire("on_train_end", args, self.state, self.control)
         return TrainOutput(self.state.global_step, train_loss, metrics)

@@ -12,6 +12,7 @@ reducer, fused AdamW).  Deviation: ``--batch-size`` is honoured (the reference h
 the default is still 1), SURVEY.md Appendix A Q4.
 """
 import json
+import time
 import os
 import sys
 
@@ -80,6 +81,8 @@ class ModelTrainer:
         metric = rouge.load("rouge")
         self.logger.info(f"***** Running training ***** examples={len(train_ds)} epochs={a.num_epochs}")
         completed = 0
+        t0 = time.perf_counter()
+        t_warm, warm = None, min(2, max(0, max_train_steps - 1))
         for epoch in range(a.num_epochs):
             model.train()
             train_dl.set_epoch(epoch)
@@ -91,11 +94,21 @@ class ModelTrainer:
                 lr_scheduler.step()
                 optimizer.zero_grad()
                 completed += 1
+                if completed == warm:
+                    torch.cuda.synchronize() if acc.device.type == "cuda" else None
+                    t_warm = time.perf_counter()
                 faults.maybe_inject(completed, acc.process_index)
                 if completed % 300 == 0:
                     self.dump({"loss": loss.item(), "step": completed})
                 if completed >= max_train_steps:
                     break
+            torch.cuda.synchronize() if acc.device.type == "cuda" else None
+            t1 = time.perf_counter()
+            per_step = a.batch_size * acc.num_processes
+            tp = {"train_samples_per_second": round(per_step * completed / (t1 - t0), 3), "epoch": epoch}
+            if t_warm is not None and completed > warm:
+                tp["train_steady_samples_per_second"] = round(per_step * (completed - warm) / (t1 - t_warm), 3)
+            self.dump(tp)
             model.eval()
             for batch in eval_dl:
                 with torch.no_grad():
