@@ -5,6 +5,8 @@
 //          w *= 1 - lr*wd; m = b1 m + (1-b1) g; v = b2 v + (1-b2) g^2;
 //          w -= lr/bc1 * m / (sqrt(v)/sqrt(bc2) + eps).
 #include "common.h"
+#include <stdlib.h>
+#include <type_traits>
 
 using namespace dllm;
 
@@ -65,6 +67,83 @@ __global__ __launch_bounds__(256) void adamw_kernel(TP* __restrict__ param, floa
   }
 }
 
+// Bandwidth version (n % 8 == 0, the flat buffers are 64-element aligned): 8 elements per thread and iteration, every
+// load of both halves issued before any math (two 16-B loads in flight per stream).  It moves 31 B per parameter with
+// fp32 gradients and master weights (17 read, 14 written) at ~4.9 TB/s, i.e. HBM-bound; nontemporal access
+// (DLLM_ADAMW_NT=1) measured 1.8x slower (tools/adamw_bench.py, profiles/r2_adamw_bench.jsonl).
+template <bool NT, typename T>
+DLLM_DEVICE f32x4 ld4_nt(T* p) {
+  if constexpr (!NT) {
+    return Elem<std::remove_const_t<T>>::load4(p);
+  } else if constexpr (sizeof(T) == 4) {
+    return __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+  } else {
+    typedef __attribute__((ext_vector_type(2))) unsigned int u32x2v;
+    const u32x2v r = __builtin_nontemporal_load(reinterpret_cast<const u32x2v*>(p));
+    return f32x4{__uint_as_float(r.x << 16), __uint_as_float(r.x & 0xFFFF0000u), __uint_as_float(r.y << 16),
+                 __uint_as_float(r.y & 0xFFFF0000u)};
+  }
+}
+template <bool NT, typename T>
+DLLM_DEVICE void st4_nt(T* p, f32x4 v) {
+  if constexpr (!NT) {
+    Elem<T>::store4(p, v);
+  } else if constexpr (sizeof(T) == 4) {
+    __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p));
+  } else {
+    typedef __attribute__((ext_vector_type(2))) unsigned int u32x2v;
+    const u32x2v r = {pack_bf16x2(v.x, v.y), pack_bf16x2(v.z, v.w)};
+    __builtin_nontemporal_store(r, reinterpret_cast<u32x2v*>(p));
+  }
+}
+
+template <typename TP, typename TG, bool MASTER, bool NT>
+__global__ __launch_bounds__(256) void adamw8_kernel(TP* __restrict__ param, float* __restrict__ master,
+                                                     const TG* __restrict__ grad, float* __restrict__ m,
+                                                     float* __restrict__ v, const uint8_t* __restrict__ wd_mask,
+                                                     const float* __restrict__ coef_p, long n8, float lr, float b1,
+                                                     float b2, float eps, float wd, float step_size,
+                                                     float inv_sqrt_bc2) {
+  const float coef = coef_p[0];
+  const float dec = lr * wd;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
+    const long o = i * 8;
+    f32x4 g[2], w[2], mm[2], vv[2];
+    uint2 mk = {0x01010101u, 0x01010101u};
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      g[h] = ld4_nt<NT>(grad + o + 4 * h);
+      w[h] = MASTER ? ld4_nt<NT>(master + o + 4 * h) : ld4_nt<NT>(param + o + 4 * h);
+      mm[h] = ld4_nt<NT>(m + o + 4 * h);
+      vv[h] = ld4_nt<NT>(v + o + 4 * h);
+    }
+    if (wd_mask != nullptr) mk = *reinterpret_cast<const uint2*>(wd_mask + o);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const uint32_t mw = h == 0 ? mk.x : mk.y;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float gk = g[h][k] * coef;
+        const float d = ((mw >> (8 * k)) & 0xFFu) ? dec : 0.f;
+        float wk = w[h][k] * (1.f - d);
+        const float mk2 = mm[h][k] + (1.f - b1) * (gk - mm[h][k]);
+        const float vk = b2 * vv[h][k] + (1.f - b2) * gk * gk;
+        wk -= step_size * mk2 / (sqrtf(vk) * inv_sqrt_bc2 + eps);
+        w[h][k] = wk;
+        mm[h][k] = mk2;
+        vv[h][k] = vk;
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      st4_nt<NT>(m + o + 4 * h, mm[h]);
+      st4_nt<NT>(v + o + 4 * h, vv[h]);
+      if (MASTER) st4_nt<NT>(master + o + 4 * h, w[h]);
+      st4_nt<NT>(param + o + 4 * h, w[h]);
+    }
+  }
+}
+
 inline int grid_for(long n4, int cap) {
   long g = (n4 + 255) / 256;
   return (int)(g < cap ? (g > 0 ? g : 1) : cap);
@@ -94,6 +173,27 @@ extern "C" int dllm_adamw(void* param, float* master, const void* grad, float* m
   const int G = grid_for(n4, 4096);
   const float step_size = lr / bc1;
   const float inv_sqrt_bc2 = 1.f / sqrtf(bc2);
+  if (n % 8 == 0 && getenv("DLLM_ADAMW_V1") == nullptr) {
+    const long n8 = n / 8;
+    const char* ge = getenv("DLLM_ADAMW_GRID");
+    const int G8 = grid_for(n8, ge ? atoi(ge) : 1024);  // tools/adamw_bench.py: ~4.9 TB/s moved (nt: 2.8, slower)
+    const bool nt = getenv("DLLM_ADAMW_NT") != nullptr && getenv("DLLM_ADAMW_NT")[0] == '1';
+#define A8(TP, TG, MS)                                                                                                  \
+  do {                                                                                                                  \
+    if (nt)                                                                                                             \
+      hipLaunchKernelGGL((adamw8_kernel<TP, TG, MS, true>), dim3(G8), dim3(256), 0, st, (TP*)param, master,             \
+                         (const TG*)grad, m, v, wd_mask, coef, n8, lr, b1, b2, eps, wd, step_size, inv_sqrt_bc2);       \
+    else                                                                                                                \
+      hipLaunchKernelGGL((adamw8_kernel<TP, TG, MS, false>), dim3(G8), dim3(256), 0, st, (TP*)param, master,            \
+                         (const TG*)grad, m, v, wd_mask, coef, n8, lr, b1, b2, eps, wd, step_size, inv_sqrt_bc2);       \
+  } while (0)
+    if (is_bf16 && grad_f32) { if (master) A8(uint16_t, float, true); else A8(uint16_t, float, false); }
+    else if (is_bf16) { if (master) A8(uint16_t, uint16_t, true); else A8(uint16_t, uint16_t, false); }
+    else { if (master) A8(float, float, true); else A8(float, float, false); }
+#undef A8
+    DLLM_CHECK_LAUNCH();
+    return 0;
+  }
   if (is_bf16 && grad_f32) {  // bf16 params, fp32 gradients (accumulated across micro-batches in fp32)
     if (master)
       hipLaunchKernelGGL((adamw_kernel<uint16_t, float, true>), dim3(G), dim3(256), 0, st, (uint16_t*)param, master,
