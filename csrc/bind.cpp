@@ -529,8 +529,8 @@ int64_t gemm_wgrad(const Tensor& a, const Tensor& b, Tensor& c, bool beta, int64
 // c[M][N] = epi(a[M][K] . b) with b = [N][K] (nn.Linear weight, b_kmajor = false) or [K][N] (b_kmajor = true).
 // epi (csrc/gemm_fused.hip): 0 none, 1 relu, 2 gelu-erf, 3 d-relu, 4 d-gelu-erf, 5 gelu-tanh, 6 d-gelu-tanh.
 // Forward activations apply dropout(p, seed) on the output element index m * N + n (ops/rng.py); the GELU
-// forwards also write the pre-activation to aux_out; the backward epilogues read aux (saved activation for
-// d-relu, pre-activation for d-gelu) and apply the matching dropout backward.
+// forwards also write G = dropout'(act'(u)) to aux_out; the backward epilogues read aux (saved activation for
+// d-relu, whose dropout backward they apply; G for d-gelu, which they multiply in).
 int64_t gemm_fused_variant(int64_t K) {
   // ping-pong kernel (16x16x32 MFMA, BK = 64, two wave rows one barrier apart), persistent for store-only epilogues:
   // fastest on every T5 / BART shape measured (profiles/r1_gemm_*_bench*.jsonl, r1_gemm_experiments.md);

@@ -11,7 +11,8 @@
 // counter hash of ops/rng.py on the output element index), and the wo dgrad GEMM applies the activation /
 // dropout backward to its accumulators before its store: for ReLU the mask is `H != 0` read back from the
 // saved activation itself (ReLU and dropout both produce exact zeros), so the pre-activation is never
-// stored at all.  GELU keeps its pre-activation (written by the forward epilogue as a second output).
+// stored at all.  GELU writes its derivative, dropout mask and scale applied, as a second output instead of the
+// pre-activation: the backward epilogue is then a single multiply.
 //
 // Structure (same machinery as csrc/gemm.hip, the weight-gradient kernel):
 // * 256x256 output tile per 512-thread workgroup, 8 waves as 2(M) x 4(N), 128x64 per wave = 4x2
@@ -114,16 +115,25 @@ constexpr float kInvSqrt2 = 0.7071067811865476f;
 constexpr float kInvSqrt2Pi = 0.3989422804014327f;
 constexpr float kSqrt2OverPi = 0.7978845608028654f;
 
-DLLM_DEVICE float gelu_f(float x) { return 0.5f * x * (1.f + erff(x * kInvSqrt2)); }
-DLLM_DEVICE float gelu_df(float x) {
-  return 0.5f * (1.f + erff(x * kInvSqrt2)) + x * kInvSqrt2Pi * __expf(-0.5f * x * x);
+// GELU and its derivative from ONE exp and ONE reciprocal: erf by Abramowitz-Stegun 7.1.26 (|error| <= 1.5e-7, far
+// below bf16 output rounding), whose exp(-x^2) at x = u / sqrt(2) is exactly the exp(-u^2 / 2) of the Gaussian density
+// in the derivative.  libm erff + expf cost ~40 VALU instructions per element, a large share of the GEMM itself.
+DLLM_DEVICE void gelu_pair(float u, float& g, float& dg) {
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f * kInvSqrt2, fabsf(u), 1.f));
+  const float poly =
+      fmaf(fmaf(fmaf(fmaf(1.061405429f, t, -1.453152027f), t, 1.421413741f), t, -0.284496736f), t, 0.254829592f) * t;
+  const float e = __builtin_amdgcn_exp2f(u * u * (-0.5f * 1.4426950408889634f));  // exp(-u^2 / 2)
+  const float cdf = fmaf(0.5f, copysignf(fmaf(-poly, e, 1.f), u), 0.5f);         // Phi(u) = (1 + erf(u / sqrt 2)) / 2
+  g = u * cdf;
+  dg = fmaf(u * kInvSqrt2Pi, e, cdf);
 }
-DLLM_DEVICE float gelu_tanh_f(float x) {
-  return 0.5f * x * (1.f + tanhf(kSqrt2OverPi * (x + 0.044715f * x * x * x)));
-}
-DLLM_DEVICE float gelu_tanh_df(float x) {
-  const float t = tanhf(kSqrt2OverPi * (x + 0.044715f * x * x * x));
-  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * kSqrt2OverPi * (1.f + 3.f * 0.044715f * x * x);
+// tanh approximation (gelu_new): tanh(z) = 1 - 2 / (exp(2z) + 1), saturating correctly at both ends
+DLLM_DEVICE void gelu_tanh_pair(float u, float& g, float& dg) {
+  const float u2 = u * u;
+  const float z = kSqrt2OverPi * fmaf(0.044715f * u2, u, u);
+  const float th = 1.f - 2.f * __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(z * (2.f * 1.4426950408889634f)) + 1.f);
+  g = 0.5f * u * (1.f + th);
+  dg = fmaf(0.5f * u * fmaf(-th, th, 1.f), kSqrt2OverPi * fmaf(3.f * 0.044715f, u2, 1.f), 0.5f * (1.f + th));
 }
 
 DLLM_DEVICE void store4(uint16_t* p, f32x4 v) {
@@ -137,26 +147,42 @@ DLLM_DEVICE f32x4 load4(const uint16_t* p) {
 }
 
 // v = accumulators (+ bias, added by the caller from registers loaded once) for C[m][n .. n+3] (n % 4 == 0)
+// GELU forwards write G = dropout'(.) * act'(U) (the keep mask and 1/(1-p) already applied) as the second output, so
+// their backward epilogues are one multiply: dU = (dY Wo) * G — no activation math and no hash in the backward.
 template <int EPI>
 DLLM_DEVICE f32x4 epilogue4(const GemmFusedParams& P, int m, int n, f32x4 v) {
   const bool drop = P.p > 0.f;
   const uint32_t e = (uint32_t)m * (uint32_t)P.N + (uint32_t)n;  // output element index (< 2^32, host-checked)
-  if (EPI == EPI_RELU || EPI == EPI_GELU || EPI == EPI_GELU_TANH) {
-    if (EPI != EPI_RELU) store4(P.aux_out + (long)m * P.ldaux + n, v);  // pre-activation for the backward
+  if (EPI == EPI_RELU) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-      v[k] = EPI == EPI_RELU ? fmaxf(v[k], 0.f) : (EPI == EPI_GELU ? gelu_f(v[k]) : gelu_tanh_f(v[k]));
+    for (int k = 0; k < 4; ++k) v[k] = fmaxf(v[k], 0.f);
     if (drop) dropout4(v, P.seed, P.thr, e, P.scale);
+  } else if (EPI == EPI_GELU || EPI == EPI_GELU_TANH) {
+    f32x4 dg;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float g, d;
+      if (EPI == EPI_GELU) gelu_pair(v[k], g, d);
+      else gelu_tanh_pair(v[k], g, d);
+      v[k] = g;
+      dg[k] = d;
+    }
+    if (drop) {
+      bool k0, k1, k2, k3;
+      keep_two(P.seed, P.thr, e, k0, k1);
+      keep_two(P.seed, P.thr, e + 2u, k2, k3);
+      const float s0 = k0 ? P.scale : 0.f, s1 = k1 ? P.scale : 0.f, s2 = k2 ? P.scale : 0.f, s3 = k3 ? P.scale : 0.f;
+      v = v * f32x4{s0, s1, s2, s3};
+      dg = dg * f32x4{s0, s1, s2, s3};
+    }
+    store4(P.aux_out + (long)m * P.ldaux + n, dg);
   } else if (EPI == EPI_DRELU) {
     // H = dropout(relu(u)) was stored by the forward: dH/du = (H != 0) * scale
     const u16x4 h = *reinterpret_cast<const u16x4*>(P.aux + (long)m * P.ldaux + n);
 #pragma unroll
     for (int k = 0; k < 4; ++k) v[k] = (h[k] & 0x7fff) ? v[k] * P.scale : 0.f;
   } else if (EPI == EPI_DGELU || EPI == EPI_DGELU_TANH) {
-    if (drop) dropout4(v, P.seed, P.thr, e, P.scale);
-    const f32x4 u = load4(P.aux + (long)m * P.ldaux + n);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) v[k] *= EPI == EPI_DGELU ? gelu_df(u[k]) : gelu_tanh_df(u[k]);
+    v = v * load4(P.aux + (long)m * P.ldaux + n);
   }
   store4(P.C + (long)m * P.ldc + n, v);
   return v;

@@ -10,7 +10,8 @@ alive until backward.  Here (csrc/gemm_fused.hip):
 
 * forward:  ``H = dropout(act(X Wiᵀ + bi))`` is ONE GEMM whose epilogue applies bias, activation and the
   counter-based dropout mask (ops/rng.py, same element index as csrc/act.hip, so both paths draw identical
-  masks); GELU also writes its pre-activation ``U`` as a second output; ReLU stores nothing else;
+  masks); GELU also writes ``G = dropout'(act'(U))`` (derivative with the keep mask and scale applied) as a
+  second output, so its backward epilogue is one multiply; ReLU stores nothing else;
 * backward: ``dU = act'(U) · dropout'(dY Wo)`` is ONE GEMM (``dY [M, d] x Wo [d, F]``, k-major B) whose
   epilogue applies the dropout and activation backward.  For ReLU the derivative mask is ``H != 0``
   (ReLU and dropout both produce exact zeros), so the pre-activation is never stored: one
@@ -63,7 +64,7 @@ class _FusedFFNFn(torch.autograd.Function):
         x2 = x.reshape(-1, shape[-1])
         efwd, _ = EPILOGUES[act]
         u = mask = None
-        if efwd != 1:  # GELU: the backward needs the pre-activation
+        if efwd != 1:  # GELU: the backward multiplies by the stored derivative
             u = torch.empty(x2.shape[0], wi.shape[0], device=x.device, dtype=x.dtype)
         elif _RELU_MASK and _pingpong(C, x2.shape[1]) and _pingpong(C, wo.shape[0]):  # ReLU: bits for the backward
             mask = torch.empty(x2.shape[0] * wi.shape[0] // 32, device=x.device, dtype=torch.int32)

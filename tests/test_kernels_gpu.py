@@ -341,8 +341,19 @@ def test_gemm_fused_forward(variant, act, p, bias):
         ref = ref * keep_mask(77, p, ref.shape, ref.device).float() / (1.0 - p)
     assert _rel(h, ref) < 1e-2, _rel(h, ref)
     _close(h, ref, 2e-2, 2e-2, "fused fwd")
-    if aux is not None:
-        assert _rel(aux, u) < 1e-2
+    if aux is not None:  # GELU: the derivative with the dropout mask and scale applied (the backward's multiplier)
+        assert _rel(aux, _act_grad(u, act, 77, p)) < 1e-2, _rel(aux, _act_grad(u, act, 77, p))
+
+
+def _act_grad(u, act, seed, p):
+    """act'(u) * dropout'(.) in fp32 (what the GELU forward epilogues write as their second output)."""
+    from distributed_llms_example_amd.ops.rng import keep_mask
+    uf = u.float().requires_grad_(True)
+    activations._act_ref(uf, act).sum().backward()
+    g = uf.grad
+    if p > 0:
+        g = g * keep_mask(seed, p, g.shape, g.device).float() / (1.0 - p)
+    return g
 
 
 @pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
@@ -358,7 +369,8 @@ def test_gemm_fused_backward(variant, act, p):
     u = torch.randn(M, F_, device=DEV).to(torch.bfloat16)
     keep = (keep_mask(9, p, (M, F_), u.device).float() / (1.0 - p)) if p > 0 else torch.ones(M, F_, device=DEV)
     h = (activations._act_ref(u.float(), act) * keep).to(torch.bfloat16)
-    aux = h if act == "relu" else u  # ReLU derives its mask from the saved activation itself
+    # ReLU derives its mask from the saved activation itself; GELU multiplies by the derivative its forward stored
+    aux = h if act == "relu" else _act_grad(u, act, 9, p).to(torch.bfloat16)
     assert C.gemm_fused_supported(dy, wo, True)
     du = C.gemm_fused(dy, wo, True, _EPI_BWD[act], None, aux, None, p, 9, variant)
     uf = u.float().requires_grad_(True)
@@ -608,3 +620,42 @@ def test_chunked_attention_long_sequence():
             assert _rel(x.grad, y.grad) < tol, (N, name, _rel(x.grad, y.grad))
         del o2, b
         torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_chunked_attention_8k_blocks_vs_fp32(p):
+    """The default long-sequence path at batch x heads < 32 (8K-token blocks, parallel/context.py
+    long_sequence_chunk) vs an fp32 reference of the same block math at 16K tokens: off-diagonal bias LUTs with
+    saturated ranges, key padding, attention dropout (per-block seeds); outputs and dq / dk / dv / dtable."""
+    from distributed_llms_example_amd.parallel import context as cp
+    torch.manual_seed(12)
+    B, N, H, D = 1, 16384, 2, 64
+    chunk = cp.long_sequence_chunk(N, rows=B * H)
+    assert chunk == 8192, chunk
+    q, k, v = (torch.randn(B, N, H, D, device=DEV).to(torch.bfloat16) for _ in range(3))
+    mask = torch.ones(B, N, dtype=torch.bool, device=DEV)
+    mask[0, N - 1500:] = False
+    table = torch.randn(32, H, device=DEV) * 0.5
+    seed = 4321
+    t1 = table.clone().requires_grad_(True)
+    a = [t.clone().requires_grad_(True) for t in (q, k, v)]
+    o = cp.chunked_attention(*a, chunk=chunk, key_padding_mask=mask, bias_table=t1, dropout_p=p, seed=seed)
+    qf, kf, vf = (t.float().requires_grad_(True) for t in (q, k, v))
+    tab = table.clone().requires_grad_(True)
+    W, S = N // chunk, chunk
+    rows = []
+    for r in range(W):
+        o_acc = l_acc = None
+        for s in range(W):
+            lt = A.relative_bias_lut(tab, S, S, True, 32, 128, q_offset=(r - s) * S)
+            o_b, l_b = cp._ref_block_fwd(qf[:, r * S:(r + 1) * S], kf[:, s * S:(s + 1) * S], vf[:, s * S:(s + 1) * S],
+                                         mask[:, s * S:(s + 1) * S], lt, 1.0, p, cp._block_seed(seed, r, s))
+            o_acc, l_acc = (o_b, l_b) if o_acc is None else cp._merge(o_acc, l_acc, o_b, l_b)
+        rows.append(o_acc)
+    ref = torch.cat(rows, 1)
+    assert _rel(o, ref) < 2e-2, _rel(o, ref)
+    g = torch.randn_like(ref)
+    (o.float() * g).sum().backward()
+    (ref * g).sum().backward()
+    for name, x, y in zip(("dq", "dk", "dv", "dtable"), a + [t1], [qf, kf, vf, tab]):
+        assert _rel(x.grad, y.grad) < 5e-2, (name, _rel(x.grad, y.grad))
