@@ -264,7 +264,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
   float m_run = -INFINITY, l_run = 0.f;
 
   // S^T = K Q^T for the tile in LDS buffer `buf` (8 MFMAs, two independent accumulation chains)
-  auto scores = [&](int buf, f32x16& s0, f32x16& s1) {
+  auto scores = [&](int buf, f32x16& s0, f32x16& s1) __attribute__((always_inline)) {
     const uint16_t* Kb = KV + buf * 2 * TILE64;
     s0 = f32x16{};
     s1 = f32x16{};
@@ -275,7 +275,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
     }
   };
   // online softmax of tile kt's scores (in s0/s1) and O^T += V^T P^T with V from buffer `buf`
-  auto softmax_pv = [&](int kt, int buf, f32x16& s0, f32x16& s1) {
+  auto softmax_pv = [&](int kt, int buf, f32x16& s0, f32x16& s1) __attribute__((always_inline)) {
     const uint32_t mword = (DROP && DROP_IN) ? mwl[buf * 256 + w * 64 + hh * 32 + r] : 0u;
     const int kbase = kt * FWD_BN;
     const uint16_t* Vb = KV + buf * 2 * TILE64 + TILE64;
@@ -420,7 +420,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
   if (ntiles > 1) issue_tile(1, 1);
   wait_vm<0>();
   __syncthreads();
-  for (int kt = 0; kt < ntiles; ++kt) {
+  // the ring slot of a tile is a compile-time constant (loop unrolled by the ring depth): every LDS read address is a
+  // loop-invariant per-lane offset plus an immediate
+  auto step = [&](int kt, auto buf_c) __attribute__((always_inline)) {
+    constexpr int BUF = decltype(buf_c)::value;
     if (kt > 0) {
       // tile kt landed (this wave's 4 DMAs of tile kt+1, issued one tile later, may stay in flight)
       if (kt + 1 < ntiles) wait_vm<((DROP && DROP_IN) ? 5 : 4)>();
@@ -428,10 +431,15 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
       __syncthreads();
     }
     if (!HAS_KPM || tflag[kt] != 2) {  // a fully padded key tile contributes exactly nothing
-      scores(kt % 3, sa0, sa1);
-      softmax_pv(kt, kt % 3, sa0, sa1);
+      scores(BUF, sa0, sa1);
+      softmax_pv(kt, BUF, sa0, sa1);
     }
-    if (kt + 2 < ntiles) issue_tile((kt + 2) % 3, kt + 2);
+    if (kt + 2 < ntiles) issue_tile((BUF + 2) % 3, kt + 2);
+  };
+  for (int kt = 0; kt < ntiles; kt += 3) {
+    step(kt, std::integral_constant<int, 0>{});
+    if (kt + 1 < ntiles) step(kt + 1, std::integral_constant<int, 1>{});
+    if (kt + 2 < ntiles) step(kt + 2, std::integral_constant<int, 2>{});
   }
 
   const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
@@ -573,8 +581,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnParams P) {
 
   f32x16 dq0 = {}, dq1 = {};
   if (ntiles > 0) issue_tile(0, 0);
-  for (int kt = 0; kt < ntiles; ++kt) {
-    const int cur = kt & 1;
+  // the buffer of a tile is a compile-time constant (loop unrolled by 2): LDS read addresses are loop-invariant
+  // per-lane offsets plus immediates
+  auto step = [&](int kt, auto cur_c) __attribute__((always_inline)) {
+    constexpr int cur = decltype(cur_c)::value;
     const int kbase = kt * FWD_BN;
     wait_vm<0>();
     __syncthreads();  // tile kt visible; every wave is done with tile kt-1 (buffer cur ^ 1)
@@ -583,7 +593,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnParams P) {
       mword = mnext;
       if (kt + 1 < ntiles) mnext = mrow[(long)(kt + 1) * 2 * P.sq_pad];
     }
-    if (HAS_KPM && tflag[kt] == 2) continue;  // fully padded key tile: P = 0, no dQ contribution
+    if (HAS_KPM && tflag[kt] == 2) return;  // fully padded key tile: P = 0, no dQ contribution
     const uint16_t* Kb = KV + cur * 2 * TILE64;
     const uint16_t* Vb = Kb + TILE64;
     f32x16 s0 = {}, s1 = {}, p0 = {}, p1 = {};
@@ -660,6 +670,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnParams P) {
         dq1 = mfma32(ld_tr_operand(Kb, kb0, 1, r), bf, dq1);
       }
     }
+  };
+  for (int kt = 0; kt < ntiles; kt += 2) {
+    step(kt, std::integral_constant<int, 0>{});
+    if (kt + 1 < ntiles) step(kt + 1, std::integral_constant<int, 1>{});
   }
   if (qvalid) {
     uint16_t* dqp = P.dq + b * P.dq_sb + (long)qrow * P.dq_ss + h * P.dq_sh;
@@ -1034,13 +1048,15 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv2_kernel(AttnParams P) {
   f32x16 dv0 = {}, dv1 = {}, dk0 = {}, dk1 = {};
   if (qt_begin < nqt) issue(0, qt_begin);
   if (qt_begin + 1 < nqt) issue(1, qt_begin + 1);
-  for (int qt = qt_begin; qt < nqt; ++qt) {
-    const int it = qt - qt_begin;
+  // one pipeline stage; the ring slot is a compile-time constant (the loop below is unrolled by the ring depth) so
+  // every LDS read address is a loop-invariant per-lane offset plus an immediate: no per-stage address arithmetic
+  auto stage = [&](int qt, auto slot_c) __attribute__((always_inline)) {
+    constexpr int SLOT = decltype(slot_c)::value;
     if (qt + 1 < nqt) wait_vm<DPT>();
     else wait_vm<0>();
     __syncthreads();  // stage qt landed for every wave; every wave is done with stage qt - 1 (the slot refilled next)
-    if (qt + 2 < nqt) issue((it + 2) % K2_NBUF, qt + 2);
-    const unsigned char* stg = smem + (it % K2_NBUF) * K2_STAGE;
+    if (qt + 2 < nqt) issue((SLOT + 2) % K2_NBUF, qt + 2);
+    const unsigned char* stg = smem + SLOT * K2_STAGE;
     const uint16_t* Qb = reinterpret_cast<const uint16_t*>(stg);
     const uint16_t* dOb = Qb + TILE64;
     const float* rec = reinterpret_cast<const float*>(stg + 4 * TILE64);
@@ -1132,6 +1148,12 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv2_kernel(AttnParams P) {
         dk1 = mfma32(ld_tr_operand(Qb, c0, 1, r), sfv, dk1);
       }
     }
+  };
+  static_assert(K2_NBUF == 3, "the stage loop is unrolled by the ring depth");
+  for (int qt = qt_begin; qt < nqt; qt += 3) {
+    stage(qt, std::integral_constant<int, 0>{});
+    if (qt + 1 < nqt) stage(qt + 1, std::integral_constant<int, 1>{});
+    if (qt + 2 < nqt) stage(qt + 2, std::integral_constant<int, 2>{});
   }
 
   if (kvalid) {
