@@ -20,8 +20,11 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, fn, q):
+def _worker(rank, world, port, fn, q, env=None):
     os.environ["DLLM_FORCE_CPU"] = "1"
+    os.environ.update(env or {})
+    if env and "TORCH_DISTRIBUTED_DEBUG" in env:
+        dist.set_debug_level_from_env()  # torch read the variable at import, before it was set here
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     def by_value(x):  # tensors through a Queue travel as shared-memory fds that die with the child
         if torch.is_tensor(x):
@@ -39,11 +42,11 @@ def _worker(rank, world, port, fn, q):
         dist.destroy_process_group()
 
 
-def run_ranks(fn, world=2):
+def run_ranks(fn, world=2, env=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, fn, q)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, fn, q, env)) for r in range(world)]
     for p in ps:
         p.start()
     out = dict(q.get(timeout=240) for _ in ps)
@@ -228,3 +231,61 @@ def test_data_partitioner_matches_reference_semantics():
     rng.shuffle(idx)
     assert [parts.use(0)[i] for i in range(len(parts.use(0)))] == idx[:9]
     assert sum(len(parts.use(r)) for r in range(4)) == 36
+
+
+# ---------------------------------------------------------------------------------------------- collective checking
+# the reference relies on torch's TORCH_DISTRIBUTED_DEBUG=DETAIL (ProcessGroupWrapper: every
+# collective's op / shapes / dtypes are cross-checked between ranks before it runs).  The whole training step
+# (parameter broadcast, bucket rebuild broadcast, bucketed all-reduces, token-count all-reduce, optimizer) must pass
+# that check, and a rank-divergent collective must be reported instead of hanging.
+_DEBUG_ENV = {"TORCH_DISTRIBUTED_DEBUG": "DETAIL"}
+
+
+def _debug_steps(rank, world, native):
+    from distributed_llms_example_amd.models import build_model
+    from distributed_llms_example_amd.parallel.env import DistEnv
+    from distributed_llms_example_amd.train.engine import TrainEngine, token_count
+    assert dist.get_debug_level() == dist.DebugLevel.DETAIL
+    os.environ["DLLM_NATIVE_REDUCER"] = "1" if native else "0"
+    torch.manual_seed(0)
+    model = build_model("t5-tiny")
+    env = DistEnv(rank=rank, world_size=world, backend="gloo", device=torch.device("cpu"))
+    eng = TrainEngine(model, env, lr=1e-3, dtype=torch.float32, bucket_mb=0.02, overlap=True)
+    eng.train(False)
+    g = torch.Generator().manual_seed(7 + rank)
+    for step in range(3):  # step 0 rebuilds the buckets (broadcast of rank 0's order) and re-lays the flat buffers
+        mbs = []
+        for _ in range(2):
+            lab = torch.randint(3, 500, (4, 5), generator=g)
+            lab[:, 3 + rank:] = -100  # rank-dependent token counts: the global count needs its all-reduce
+            ids = torch.randint(3, 500, (4, 10), generator=g)
+            mbs.append({"input_ids": ids, "attention_mask": torch.ones_like(ids), "labels": lab})
+        n = sum(token_count(b["labels"]) for b in mbs)
+        dist.all_reduce(n)
+        for i, b in enumerate(mbs):
+            eng.forward_backward(b, sync=i == 1, num_items=n)
+        eng.optimizer.step(max_grad_norm=1.0)
+        eng.optimizer.zero_grad()
+    return eng.flat.to_canonical(eng.flat.param_buf).clone()
+
+
+@pytest.mark.parametrize("native", [False, pytest.param(True, marks=pytest.mark.skipif(
+    not _native_available(), reason="native extension not built"))])
+def test_training_steps_pass_collective_consistency_check(native):
+    out = run_ranks(functools.partial(_debug_steps, native=native), env=_DEBUG_ENV)
+    torch.testing.assert_close(torch.as_tensor(out[0]), torch.as_tensor(out[1]))  # replicas stay identical
+
+
+def _divergent_collective(rank, world):
+    t = torch.ones(4 if rank == 0 else 5)
+    try:
+        dist.all_reduce(t)
+    except RuntimeError as e:
+        return "caught: " + str(e)[:400]
+    return "not detected"
+
+
+def test_divergent_collective_is_reported():
+    out = run_ranks(_divergent_collective, env=_DEBUG_ENV)
+    for r in (0, 1):
+        assert out[r].startswith("caught:") and "mismatch" in out[r].lower(), out[r]
