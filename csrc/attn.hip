@@ -188,32 +188,6 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
   const bool qvalid = qrow < P.Sq;
   const float sl2 = P.scale * LOG2E;
 
-  const int lut_base = P.Sq - 1 - (q0 + FWD_BM - 1);  // lut_s[i] = LUT[lut_base + i]
-  float c_lo = 0.f, c_hi = 0.f;                        // saturated-range biases (log2-scaled)
-  if (HAS_BIAS) {
-    const int L = P.Sq + P.Sk - 1;
-    const float* lrow = P.lut + (long)h * L;
-    for (int i = tid; i < P.Sk + FWD_BM + FWD_BN; i += 256) {
-      const int gi = lut_base + i;
-      lut_s[i] = (gi >= 0 && gi < L) ? lrow[gi] * LOG2E : 0.f;
-    }
-    c_lo = lrow[0] * LOG2E;
-    c_hi = lrow[L - 1] * LOG2E;
-  }
-  bf16x8v qf[4];
-  {
-    const uint16_t* qp = P.q + b * P.q_sb + (long)qrow * P.q_ss + h * P.q_sh;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      u16x8 t = {0, 0, 0, 0, 0, 0, 0, 0};
-      if (qvalid) t = *reinterpret_cast<const u16x8*>(qp + 16 * s + 8 * hh);
-      qf[s] = as_frag(t);
-    }
-  }
-  const long row_g = (long)(b * P.H + h) * P.Sq + qrow;
-  const uint32_t rh = DROP ? mix32(P.seed, (uint32_t)row_g) : 0u;
-  const float dscale = DROP ? 1.f / (1.f - P.p_drop) : 1.f;
-
   int kend = P.Sk;
   if (CAUSAL) {
     const int lim = q0 + FWD_BM + P.causal_off;  // keys <= last row + off
@@ -251,6 +225,36 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
       glds4(P.dmask + ((long)bh * P.n_ktiles * 2 + 2 * kt + hh) * P.sq_pad + qrow,
             __builtin_amdgcn_readfirstlane(mw_lds + (uint32_t)((buf * 256 + w * 64) * 4)));
   };
+  // tiles 0 and 1 are issued before the prologue's global reads (bias LUT, Q fragments, key mask) so their latencies
+  // overlap instead of adding up
+  if (ntiles > 0) issue_tile(0, 0);
+  if (ntiles > 1) issue_tile(1, 1);
+  const int lut_base = P.Sq - 1 - (q0 + FWD_BM - 1);  // lut_s[i] = LUT[lut_base + i]
+  float c_lo = 0.f, c_hi = 0.f;                        // saturated-range biases (log2-scaled)
+  if (HAS_BIAS) {
+    const int L = P.Sq + P.Sk - 1;
+    const float* lrow = P.lut + (long)h * L;
+    for (int i = tid; i < P.Sk + FWD_BM + FWD_BN; i += 256) {
+      const int gi = lut_base + i;
+      lut_s[i] = (gi >= 0 && gi < L) ? lrow[gi] * LOG2E : 0.f;
+    }
+    c_lo = lrow[0] * LOG2E;
+    c_hi = lrow[L - 1] * LOG2E;
+  }
+  bf16x8v qf[4];
+  {
+    const uint16_t* qp = P.q + b * P.q_sb + (long)qrow * P.q_ss + h * P.q_sh;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      u16x8 t = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (qvalid) t = *reinterpret_cast<const u16x8*>(qp + 16 * s + 8 * hh);
+      qf[s] = as_frag(t);
+    }
+  }
+  const long row_g = (long)(b * P.H + h) * P.Sq + qrow;
+  const uint32_t rh = DROP ? mix32(P.seed, (uint32_t)row_g) : 0u;
+  const float dscale = DROP ? 1.f / (1.f - P.p_drop) : 1.f;
+
   for (int t = w; t < ntiles; t += 4) {  // wave-per-tile: per-key mask + "tile has a masked key" flag
     const int j = t * FWD_BN + lane;
     bool ok = j < P.Sk;
@@ -416,8 +420,6 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
   // 3-buffer K/V ring: tile kt+2's DMA goes into the buffer tile kt-1 vacated and has a whole tile of compute to
   // land; one barrier per tile.
   f32x16 sa0, sa1;
-  if (ntiles > 0) issue_tile(0, 0);
-  if (ntiles > 1) issue_tile(1, 1);
   wait_vm<0>();
   __syncthreads();
   // the ring slot of a tile is a compile-time constant (loop unrolled by the ring depth): every LDS read address is a
@@ -484,6 +486,39 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnParams P) {
   const int qrow = qw0 + r;
   const bool qvalid = qrow < P.Sq;
   const float sl2 = P.scale * LOG2E;
+  int kend = P.Sk;
+  if (CAUSAL) {
+    const int lim = q0 + FWD_BM + P.causal_off;
+    kend = lim < kend ? lim : kend;
+  }
+  const int ntiles = kend > 0 ? (kend + FWD_BN - 1) / FWD_BN : 0;
+  // K/V tiles by LDS-DMA into 2 buffers (see the forward kernel); per-key mask + tile flags up front
+  const uint32_t kv_lds = lds_addr(KV);
+  // buffer-descriptor DMA: wave-uniform (b, h) bases in SGPRs, per-lane 32-bit byte offsets from one v_mad_u32_u24
+  // (the launcher checks strides and lengths fit), instead of 64-bit address arithmetic per DMA
+  const uint16_t* kbase_p = P.k + b * P.k_sb + h * P.k_sh;
+  const uint16_t* vbase_p = P.v + b * P.v_sb + h * P.v_sh;
+  const uint32_t kss2 = (uint32_t)P.k_ss * 2u, vss2 = (uint32_t)P.v_ss * 2u;
+  int drow[2];
+  uint32_t dc16[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    drow[i] = 8 * (2 * w + i) + (lane >> 3);
+    dc16[i] = (uint32_t)(((lane & 7) ^ swz(drow[i])) * 16);
+  }
+  auto issue_tile = [&](int buf, int kt) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int j = 2 * w + i;
+      const uint32_t kk = (uint32_t)min(kt * FWD_BN + drow[i], P.Sk - 1);  // keys past Sk re-read row Sk-1
+      const uint32_t dst = kv_lds + (uint32_t)(buf * 2 * TILE64 * 2 + j * 1024);
+      bld16(kbase_p, __umul24(kk, kss2) + dc16[i], __builtin_amdgcn_readfirstlane(dst));
+      bld16(vbase_p, __umul24(kk, vss2) + dc16[i], __builtin_amdgcn_readfirstlane(dst + TILE64 * 2));
+    }
+  };
+  // tile 0 is issued before the prologue's global reads (bias LUT, Q / dO / O rows, lse, key mask) so their latencies
+  // overlap instead of adding up
+  if (ntiles > 0) issue_tile(0, 0);
   const int lut_base = P.Sq - 1 - (q0 + FWD_BM - 1);
   float c_lo = 0.f, c_hi = 0.f;
   if (HAS_BIAS) {
@@ -535,36 +570,6 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnParams P) {
   }
   const float dscale = DROP ? 1.f / (1.f - P.p_drop) : 1.f;
 
-  int kend = P.Sk;
-  if (CAUSAL) {
-    const int lim = q0 + FWD_BM + P.causal_off;
-    kend = lim < kend ? lim : kend;
-  }
-  const int ntiles = kend > 0 ? (kend + FWD_BN - 1) / FWD_BN : 0;
-  // K/V tiles by LDS-DMA into 2 buffers (see the forward kernel); per-key mask + tile flags up front
-  const uint32_t kv_lds = lds_addr(KV);
-  // buffer-descriptor DMA: wave-uniform (b, h) bases in SGPRs, per-lane 32-bit byte offsets from one v_mad_u32_u24
-  // (the launcher checks strides and lengths fit), instead of 64-bit address arithmetic per DMA
-  const uint16_t* kbase_p = P.k + b * P.k_sb + h * P.k_sh;
-  const uint16_t* vbase_p = P.v + b * P.v_sb + h * P.v_sh;
-  const uint32_t kss2 = (uint32_t)P.k_ss * 2u, vss2 = (uint32_t)P.v_ss * 2u;
-  int drow[2];
-  uint32_t dc16[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    drow[i] = 8 * (2 * w + i) + (lane >> 3);
-    dc16[i] = (uint32_t)(((lane & 7) ^ swz(drow[i])) * 16);
-  }
-  auto issue_tile = [&](int buf, int kt) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int j = 2 * w + i;
-      const uint32_t kk = (uint32_t)min(kt * FWD_BN + drow[i], P.Sk - 1);  // keys past Sk re-read row Sk-1
-      const uint32_t dst = kv_lds + (uint32_t)(buf * 2 * TILE64 * 2 + j * 1024);
-      bld16(kbase_p, __umul24(kk, kss2) + dc16[i], __builtin_amdgcn_readfirstlane(dst));
-      bld16(vbase_p, __umul24(kk, vss2) + dc16[i], __builtin_amdgcn_readfirstlane(dst + TILE64 * 2));
-    }
-  };
   for (int t = w; t < ntiles; t += 4) {
     const int j = t * FWD_BN + lane;
     bool ok = j < P.Sk;
@@ -580,7 +585,6 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnParams P) {
   if (DROP && ntiles > 0) mnext = mrow[0];
 
   f32x16 dq0 = {}, dq1 = {};
-  if (ntiles > 0) issue_tile(0, 0);
   // the buffer of a tile is a compile-time constant (loop unrolled by 2): LDS read addresses are loop-invariant
   // per-lane offsets plus immediates
   auto step = [&](int kt, auto cur_c) __attribute__((always_inline)) {
@@ -968,6 +972,46 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv2_kernel(AttnParams P) {
   const int win = P.Sq + BWD_BK;
   const float sl2 = P.scale * LOG2E;
 
+  int qt_begin = 0;
+  if (CAUSAL) {
+    const int qmin = k0 - P.causal_off;  // first query that can see key k0
+    qt_begin = qmin > 0 ? qmin / K2_QT : 0;
+  }
+  const int nqt_all = (P.Sq + K2_QT - 1) / K2_QT;
+  // ---- stage DMA (per wave and stage: 2 + 2 Q / dO pieces of 8 rows, a quarter of the rowrec chunk, one keep column)
+  const uint32_t st_lds = lds_addr(smem);
+  const uint16_t* qbase_p = P.q + b * P.q_sb + h * P.q_sh;
+  const uint16_t* dbase_p = P.dout + b * P.do_sb + h * P.do_sh;
+  const uint32_t qss2 = (uint32_t)P.q_ss * 2u, dss2 = (uint32_t)P.do_ss * 2u;
+  int drow[2];
+  uint32_t dc16[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    drow[i] = 8 * (2 * w + i) + (lane >> 3);
+    dc16[i] = (uint32_t)(((lane & 7) ^ swz(drow[i])) * 16);
+  }
+  const float* rec_src = P.rowrec + (long)bh * (P.sq_pad >> 6) * 256 + w * 64 + lane;
+  const int ktf = min((k0 >> 6) + (w >> 1), P.n_ktiles - 1);
+  const uint32_t* keep_src = DROP ? P.dmask + (((long)bh * P.n_ktiles + ktf) * 2 + (w & 1)) * P.sq_pad + lane : nullptr;
+  auto issue = [&](int slot, int qt) {
+    const uint32_t base = st_lds + (uint32_t)(slot * K2_STAGE);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const uint32_t qq = (uint32_t)min(qt * K2_QT + drow[i], P.Sq - 1);
+      const uint32_t dst = base + (uint32_t)((2 * w + i) * 1024);
+      bld16(qbase_p, __umul24(qq, qss2) + dc16[i], __builtin_amdgcn_readfirstlane(dst));
+      bld16(dbase_p, __umul24(qq, dss2) + dc16[i], __builtin_amdgcn_readfirstlane(dst + TILE64 * 2));
+    }
+    glds4(rec_src + (long)qt * 256, __builtin_amdgcn_readfirstlane(base + 4 * TILE64 + w * 256));
+    if (DROP) glds4(keep_src + qt * K2_QT, __builtin_amdgcn_readfirstlane(base + 4 * TILE64 + 1024 + w * 256));
+  };
+  constexpr int DPT = DROP ? 6 : 5;  // DMAs per wave and stage
+
+  // the first two stages are issued before the prologue's global reads (bias LUT, key mask, K / V fragments): their
+  // latencies overlap instead of adding up (short-Sq cross-attention blocks are prologue-bound).  A block whose keys
+  // are all padding drains them unused (wait_vm<0> below) before it exits.
+  if (qt_begin < nqt_all) issue(0, qt_begin);
+  if (qt_begin + 1 < nqt_all) issue(1, qt_begin + 1);
   if (HAS_BIAS) {
     const float* lrow = P.lut + (long)h * L;
     for (int t = tid; t < win + K2_QT; t += 256) {
@@ -1009,45 +1053,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv2_kernel(AttnParams P) {
   const int mbit = (kc & 3) + 4 * (kc >> 3) + 16 * ((kl >> 5) & 1);
   const float dscale = DROP ? 1.f / (1.f - P.p_drop) : 1.f;
   const uint32_t dsbits = __float_as_uint(dscale);
-  int qt_begin = 0;
-  if (CAUSAL) {
-    const int qmin = k0 - P.causal_off;  // first query that can see key k0
-    qt_begin = qmin > 0 ? qmin / K2_QT : 0;
-  }
-  const int nqt = block_live ? (P.Sq + K2_QT - 1) / K2_QT : qt_begin;
 
-  // ---- stage DMA (per wave and stage: 2 + 2 Q / dO pieces of 8 rows, a quarter of the rowrec chunk, one keep column)
-  const uint32_t st_lds = lds_addr(smem);
-  const uint16_t* qbase_p = P.q + b * P.q_sb + h * P.q_sh;
-  const uint16_t* dbase_p = P.dout + b * P.do_sb + h * P.do_sh;
-  const uint32_t qss2 = (uint32_t)P.q_ss * 2u, dss2 = (uint32_t)P.do_ss * 2u;
-  int drow[2];
-  uint32_t dc16[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    drow[i] = 8 * (2 * w + i) + (lane >> 3);
-    dc16[i] = (uint32_t)(((lane & 7) ^ swz(drow[i])) * 16);
-  }
-  const float* rec_src = P.rowrec + (long)bh * (P.sq_pad >> 6) * 256 + w * 64 + lane;
-  const int ktf = min((k0 >> 6) + (w >> 1), P.n_ktiles - 1);
-  const uint32_t* keep_src = DROP ? P.dmask + (((long)bh * P.n_ktiles + ktf) * 2 + (w & 1)) * P.sq_pad + lane : nullptr;
-  auto issue = [&](int slot, int qt) {
-    const uint32_t base = st_lds + (uint32_t)(slot * K2_STAGE);
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const uint32_t qq = (uint32_t)min(qt * K2_QT + drow[i], P.Sq - 1);
-      const uint32_t dst = base + (uint32_t)((2 * w + i) * 1024);
-      bld16(qbase_p, __umul24(qq, qss2) + dc16[i], __builtin_amdgcn_readfirstlane(dst));
-      bld16(dbase_p, __umul24(qq, dss2) + dc16[i], __builtin_amdgcn_readfirstlane(dst + TILE64 * 2));
-    }
-    glds4(rec_src + (long)qt * 256, __builtin_amdgcn_readfirstlane(base + 4 * TILE64 + w * 256));
-    if (DROP) glds4(keep_src + qt * K2_QT, __builtin_amdgcn_readfirstlane(base + 4 * TILE64 + 1024 + w * 256));
-  };
-  constexpr int DPT = DROP ? 6 : 5;  // DMAs per wave and stage
-
+  const int nqt = block_live ? nqt_all : qt_begin;
+  if (!block_live) wait_vm<0>();
   f32x16 dv0 = {}, dv1 = {}, dk0 = {}, dk1 = {};
-  if (qt_begin < nqt) issue(0, qt_begin);
-  if (qt_begin + 1 < nqt) issue(1, qt_begin + 1);
   // one pipeline stage; the ring slot is a compile-time constant (the loop below is unrolled by the ring depth) so
   // every LDS read address is a loop-invariant per-lane offset plus an immediate: no per-stage address arithmetic
   auto stage = [&](int qt, auto slot_c) __attribute__((always_inline)) {
