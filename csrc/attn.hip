@@ -166,12 +166,15 @@ __global__ __launch_bounds__(256) void attn_dropout_mask_kernel(AttnParams P, lo
 // ================================================================================== forward
 // DROP_IN: dropout keep bits are read from precomputed planes (attn_dropout_mask_kernel on a side stream);
 // otherwise the forward hashes them itself (hidden in its MFMA/LDS latency) and stores the planes for backward.
-template <bool HAS_BIAS, bool HAS_KPM, bool CAUSAL, bool DROP, bool DROP_IN>
-__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
+// FNB = K/V ring depth: 3 (two tiles in flight, 2 workgroups per CU) or 2 (one tile in flight, a 2/3-size LDS
+// footprint and a 168-VGPR budget so 3 workgroups share a CU: more waves to hide latency with).
+template <bool HAS_BIAS, bool HAS_KPM, bool CAUSAL, bool DROP, bool DROP_IN, int FNB>
+__global__ __launch_bounds__(256, FNB == 3 ? 2 : 3) void attn_fwd_kernel(AttnParams P) {
+  static_assert(FNB == 2 || FNB == 3, "K/V ring depth");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  uint16_t* KV = reinterpret_cast<uint16_t*>(smem);            // [3 buffers][K tile | V tile]
-  uint32_t* mwl = reinterpret_cast<uint32_t*>(KV + 6 * TILE64); // [3][4 waves][2 halves][32 rows] keep bits (DROP_IN)
-  float* kmask = reinterpret_cast<float*>(mwl + 3 * 256);       // [ntiles * 64]: 0 or -inf per key
+  uint16_t* KV = reinterpret_cast<uint16_t*>(smem);            // [FNB buffers][K tile | V tile]
+  uint32_t* mwl = reinterpret_cast<uint32_t*>(KV + 2 * FNB * TILE64); // [FNB][4 waves][2 halves][32 rows] keep bits
+  float* kmask = reinterpret_cast<float*>(mwl + FNB * 256);     // [ntiles * 64]: 0 or -inf per key
   int* tflag = reinterpret_cast<int*>(kmask + P.n_ktiles * FWD_BN);  // [ntiles]: tile has a masked key
   float* lut_s = reinterpret_cast<float*>(tflag + P.n_ktiles);   // [Sk + FWD_BM + FWD_BN], log2-scaled
 
@@ -225,10 +228,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
       glds4(P.dmask + ((long)bh * P.n_ktiles * 2 + 2 * kt + hh) * P.sq_pad + qrow,
             __builtin_amdgcn_readfirstlane(mw_lds + (uint32_t)((buf * 256 + w * 64) * 4)));
   };
-  // tiles 0 and 1 are issued before the prologue's global reads (bias LUT, Q fragments, key mask) so their latencies
-  // overlap instead of adding up
+  // the first FNB - 1 tiles are issued before the prologue's global reads (bias LUT, Q fragments, key mask) so their
+  // latencies overlap instead of adding up
   if (ntiles > 0) issue_tile(0, 0);
-  if (ntiles > 1) issue_tile(1, 1);
+  if (FNB == 3 && ntiles > 1) issue_tile(1, 1);
   const int lut_base = P.Sq - 1 - (q0 + FWD_BM - 1);  // lut_s[i] = LUT[lut_base + i]
   float c_lo = 0.f, c_hi = 0.f;                        // saturated-range biases (log2-scaled)
   if (HAS_BIAS) {
@@ -417,8 +420,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
     }
   };
 
-  // 3-buffer K/V ring: tile kt+2's DMA goes into the buffer tile kt-1 vacated and has a whole tile of compute to
-  // land; one barrier per tile.
+  // K/V ring: right after the barrier that retires tile kt - 1, tile kt + FNB - 1 is issued into the buffer tile
+  // kt - 1 vacated (FNB = 3: a whole extra tile of compute to land); one barrier per tile.
   f32x16 sa0, sa1;
   wait_vm<0>();
   __syncthreads();
@@ -427,21 +430,24 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
   auto step = [&](int kt, auto buf_c) __attribute__((always_inline)) {
     constexpr int BUF = decltype(buf_c)::value;
     if (kt > 0) {
-      // tile kt landed (this wave's 4 DMAs of tile kt+1, issued one tile later, may stay in flight)
-      if (kt + 1 < ntiles) wait_vm<((DROP && DROP_IN) ? 5 : 4)>();
+      // tile kt landed (FNB = 3: this wave's 4 DMAs of tile kt+1, issued one tile later, and then either its keep-word
+      // DMA (DROP_IN) or tile kt-1's keep-word store (vmcnt counts stores too) may stay in flight)
+      if (FNB == 3 && kt + 1 < ntiles) wait_vm<(DROP ? 5 : 4)>();
       else wait_vm<0>();
       __syncthreads();
     }
+    if (kt + FNB - 1 < ntiles) issue_tile((BUF + FNB - 1) % FNB, kt + FNB - 1);
     if (!HAS_KPM || tflag[kt] != 2) {  // a fully padded key tile contributes exactly nothing
       scores(BUF, sa0, sa1);
       softmax_pv(kt, BUF, sa0, sa1);
     }
-    if (kt + 2 < ntiles) issue_tile((BUF + 2) % 3, kt + 2);
   };
-  for (int kt = 0; kt < ntiles; kt += 3) {
+  for (int kt = 0; kt < ntiles; kt += FNB) {
     step(kt, std::integral_constant<int, 0>{});
     if (kt + 1 < ntiles) step(kt + 1, std::integral_constant<int, 1>{});
-    if (kt + 2 < ntiles) step(kt + 2, std::integral_constant<int, 2>{});
+    if constexpr (FNB == 3) {
+      if (kt + 2 < ntiles) step(kt + 2, std::integral_constant<int, 2>{});
+    }
   }
 
   const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
@@ -1215,10 +1221,23 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv2_kernel(AttnParams P) {
 
 template <bool HB, bool HK, bool CA, bool DR>
 void launch_fwd_t(const AttnParams& p, int nblk, size_t lds, hipStream_t st) {
+  // lds was sized for the 3-deep ring; the 2-deep one drops one K/V buffer pair and one keep-bit slot
+  const size_t lds2 = lds - (size_t)2 * TILE64 * 2 - 256 * 4;
+  static const int occ = [] {
+    const char* e = getenv("DLLM_ATTN_FWD_OCC");
+    return e != nullptr ? atoi(e) : 3;  // 3: t5-base encoder forward -10 % (profiles/r2_attn_fwd_occ3.txt)
+  }();
+  if (occ == 3 && 3 * lds2 <= 160 * 1024) {
+    if (DR && p.dmask_ready)
+      hipLaunchKernelGGL((attn_fwd_kernel<HB, HK, CA, DR, true, 2>), dim3(nblk), dim3(256), lds2, st, p);
+    else
+      hipLaunchKernelGGL((attn_fwd_kernel<HB, HK, CA, DR, false, 2>), dim3(nblk), dim3(256), lds2, st, p);
+    return;
+  }
   if (DR && p.dmask_ready)
-    hipLaunchKernelGGL((attn_fwd_kernel<HB, HK, CA, DR, true>), dim3(nblk), dim3(256), lds, st, p);
+    hipLaunchKernelGGL((attn_fwd_kernel<HB, HK, CA, DR, true, 3>), dim3(nblk), dim3(256), lds, st, p);
   else
-    hipLaunchKernelGGL((attn_fwd_kernel<HB, HK, CA, DR, false>), dim3(nblk), dim3(256), lds, st, p);
+    hipLaunchKernelGGL((attn_fwd_kernel<HB, HK, CA, DR, false, 3>), dim3(nblk), dim3(256), lds, st, p);
 }
 template <bool HB, bool HK, bool CA, bool DR>
 void launch_bwd_dq_t(const AttnParams& p, int nblk, size_t lds, hipStream_t st) {
