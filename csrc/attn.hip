@@ -472,8 +472,9 @@ __global__ __launch_bounds__(256, FNB == 3 ? 2 : 3) void attn_fwd_kernel(AttnPar
 }
 
 // ================================================================================== backward: dQ
-template <bool HAS_BIAS, bool HAS_KPM, bool CAUSAL, bool DROP>
-__global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnParams P) {
+// OCC = workgroups per CU the register budget is cut for (2: 256 VGPRs, 3: 168)
+template <bool HAS_BIAS, bool HAS_KPM, bool CAUSAL, bool DROP, int OCC>
+__global__ __launch_bounds__(256, OCC) void attn_bwd_dq_kernel(AttnParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint16_t* KV = reinterpret_cast<uint16_t*>(smem);            // [2][K | V]
   float* kmask = reinterpret_cast<float*>(KV + 4 * TILE64);     // [ntiles * 64]: 0 or -inf per key
@@ -606,14 +607,6 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnParams P) {
     if (HAS_KPM && tflag[kt] == 2) return;  // fully padded key tile: P = 0, no dQ contribution
     const uint16_t* Kb = KV + cur * 2 * TILE64;
     const uint16_t* Vb = Kb + TILE64;
-    f32x16 s0 = {}, s1 = {}, p0 = {}, p1 = {};
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      s0 = mfma32(as_frag(ld_row(Kb, r, 2 * s + hh)), qf[s], s0);
-      s1 = mfma32(as_frag(ld_row(Kb, 32 + r, 2 * s + hh)), qf[s], s1);
-      p0 = mfma32(as_frag(ld_row(Vb, r, 2 * s + hh)), dof[s], p0);
-      p1 = mfma32(as_frag(ld_row(Vb, 32 + r, 2 * s + hh)), dof[s], p1);
-    }
     const bool tile_causal = CAUSAL && (kbase + FWD_BN - 1 > qw0 + P.causal_off);
     const int climit = qrow + P.causal_off - kbase;
     const float* lb = lut_s + (kbase - qrow + P.Sq - 1 - lut_base);
@@ -624,60 +617,51 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnParams P) {
     // FMA operand (cl), LUT tiles add the bias by FMA and subtract lse.  dS = P * (dP * keep / (1 - p) - delta).
     const bool use_lut = HAS_BIAS && sat == 0;
     const float cl = (sat == 1 ? c_lo : (sat == 2 ? c_hi : 0.f)) - lse2;
-    if (use_lut) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        s0[i] = fmaf(s0[i], sl2, lb[crow(i, hh)]) - lse2;
-        s1[i] = fmaf(s1[i], sl2, lb[32 + crow(i, hh)]) - lse2;
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        s0[i] = fmaf(s0[i], sl2, cl);
-        s1[i] = fmaf(s1[i], sl2, cl);
-      }
-    }
-    if (CAUSAL && tile_causal) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int kl0 = crow(i, hh);
-        s0[i] = kl0 > climit ? -INFINITY : s0[i];
-        s1[i] = kl0 + 32 > climit ? -INFINITY : s1[i];
-      }
-    }
-    if ((HAS_KPM || kbase + FWD_BN > P.Sk) && tflag[kt] != 0) {
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const f32x4 m0 = *reinterpret_cast<const f32x4*>(kmask + kbase + 8 * g + 4 * hh);
-        const f32x4 m1 = *reinterpret_cast<const f32x4*>(kmask + kbase + 32 + 8 * g + 4 * hh);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          s0[4 * g + e] += m0[e];
-          s1[4 * g + e] += m1[e];
-        }
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const float pr0 = fast_exp2(s0[i]), pr1 = fast_exp2(s1[i]);  // lse = +inf for rows >= Sq -> 0
-      float k0 = 1.f, k1 = 1.f;
-      if (DROP) {  // sign-extended bit -> all-ones mask -> dscale or 0.0f
-        k0 = __uint_as_float((uint32_t)__builtin_amdgcn_sbfe((int)mword, i, 1) & dsbits);
-        k1 = __uint_as_float((uint32_t)__builtin_amdgcn_sbfe((int)mword, 16 + i, 1) & dsbits);
-      }
-      s0[i] = pr0 * fmaf(p0[i], k0, -delta);
-      s1[i] = pr1 * fmaf(p1[i], k1, -delta);
-    }
-    // dQ^T += K^T dS^T
-    const bf16x8v da0 = pack8(s0, 0), da1 = pack8(s0, 8), db0 = pack8(s1, 0), db1 = pack8(s1, 8);
+    const bool masked = (HAS_KPM || kbase + FWD_BN > P.Sk) && tflag[kt] != 0;
+    // the tile's two 32-key halves one after the other: S / dP accumulators of one half live at a time (32 fewer
+    // VGPRs: the kernel fits the 168-register budget of 3 workgroups per CU)
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
+      f32x16 sv = {}, pv = {};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        sv = mfma32(as_frag(ld_row(Kb, 32 * kb + r, 2 * s + hh)), qf[s], sv);
+        pv = mfma32(as_frag(ld_row(Vb, 32 * kb + r, 2 * s + hh)), dof[s], pv);
+      }
+      if (use_lut) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sv[i] = fmaf(sv[i], sl2, lb[32 * kb + crow(i, hh)]) - lse2;
+      } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sv[i] = fmaf(sv[i], sl2, cl);
+      }
+      if (CAUSAL && tile_causal) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sv[i] = crow(i, hh) + 32 * kb > climit ? -INFINITY : sv[i];
+      }
+      if (masked) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 m = *reinterpret_cast<const f32x4*>(kmask + kbase + 32 * kb + 8 * g + 4 * hh);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) sv[4 * g + e] += m[e];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float pr = fast_exp2(sv[i]);  // lse = +inf for rows >= Sq -> 0
+        float kf = 1.f;
+        if (DROP)  // sign-extended bit -> all-ones mask -> dscale or 0.0f
+          kf = __uint_as_float((uint32_t)__builtin_amdgcn_sbfe((int)mword, 16 * kb + i, 1) & dsbits);
+        sv[i] = pr * fmaf(pv[i], kf, -delta);
+      }
+      // dQ^T += K^T dS^T over this half's 32 keys
+      const bf16x8v d0 = pack8(sv, 0), d1 = pack8(sv, 8);
 #pragma unroll
       for (int sp = 0; sp < 2; ++sp) {
         const int kb0 = kb * 32 + 16 * sp + 4 * hh;
-        const bf16x8v bf = kb == 0 ? (sp == 0 ? da0 : da1) : (sp == 0 ? db0 : db1);
-        dq0 = mfma32(ld_tr_operand(Kb, kb0, 0, r), bf, dq0);
-        dq1 = mfma32(ld_tr_operand(Kb, kb0, 1, r), bf, dq1);
+        dq0 = mfma32(ld_tr_operand(Kb, kb0, 0, r), sp == 0 ? d0 : d1, dq0);
+        dq1 = mfma32(ld_tr_operand(Kb, kb0, 1, r), sp == 0 ? d0 : d1, dq1);
       }
     }
   };
@@ -1241,7 +1225,14 @@ void launch_fwd_t(const AttnParams& p, int nblk, size_t lds, hipStream_t st) {
 }
 template <bool HB, bool HK, bool CA, bool DR>
 void launch_bwd_dq_t(const AttnParams& p, int nblk, size_t lds, hipStream_t st) {
-  hipLaunchKernelGGL((attn_bwd_dq_kernel<HB, HK, CA, DR>), dim3(nblk), dim3(256), lds, st, p);
+  static const int occ = [] {
+    const char* e = getenv("DLLM_ATTN_DQ_OCC");
+    return e != nullptr ? atoi(e) : 2;  // 3 measured equal (profiles/r2_ab_attn_dq_halves.txt)
+  }();
+  if (occ == 3 && !CA && 3 * lds <= 160 * 1024)  // the causal variant spills at 168 VGPRs
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<HB, HK, CA, DR, 3>), dim3(nblk), dim3(256), lds, st, p);
+  else
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<HB, HK, CA, DR, 2>), dim3(nblk), dim3(256), lds, st, p);
 }
 template <bool HB, bool HK, bool CA, bool DR>
 void launch_bwd_dkdv_t(const AttnParams& p, int nblk, size_t lds, hipStream_t st) {
