@@ -941,10 +941,13 @@ constexpr int K2_QT = 64;
 constexpr int K2_NBUF = 3;
 constexpr int K2_STAGE = 2 * 64 * D * 2 + 1024 + 1024;  // Q, dO [64][64] bf16 + rowrec [4][64] f32 + keep [4][64] u32
 
-template <bool HAS_BIAS, bool HAS_KPM, bool CAUSAL, bool DROP>
-__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv2_kernel(AttnParams P) {
+// NB = stage ring depth: 3 (two stages in flight, 2 workgroups per CU) or 2 (one in flight, a 168-VGPR budget so 3
+// workgroups share a CU; taken for the bias-free variants, which fit it)
+template <bool HAS_BIAS, bool HAS_KPM, bool CAUSAL, bool DROP, int NB>
+__global__ __launch_bounds__(256, NB == 3 ? 2 : 3) void attn_bwd_dkdv2_kernel(AttnParams P) {
+  static_assert(NB == 2 || NB == 3, "stage ring depth");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  float* kmask = reinterpret_cast<float*>(smem + K2_NBUF * K2_STAGE);  // [128]
+  float* kmask = reinterpret_cast<float*>(smem + NB * K2_STAGE);  // [128]
   float* lut_r = kmask + BWD_BK;                                       // [Sq + 128 + 64] reversed, log2-scaled
   float* dlut_s = lut_r + (HAS_BIAS ? P.Sq + BWD_BK + K2_QT : 0);      // [Sq + 128]
 
@@ -1001,7 +1004,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv2_kernel(AttnParams P) {
   // latencies overlap instead of adding up (short-Sq cross-attention blocks are prologue-bound).  A block whose keys
   // are all padding drains them unused (wait_vm<0> below) before it exits.
   if (qt_begin < nqt_all) issue(0, qt_begin);
-  if (qt_begin + 1 < nqt_all) issue(1, qt_begin + 1);
+  if (NB == 3 && qt_begin + 1 < nqt_all) issue(1, qt_begin + 1);
   if (HAS_BIAS) {
     const float* lrow = P.lut + (long)h * L;
     for (int t = tid; t < win + K2_QT; t += 256) {
@@ -1051,10 +1054,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv2_kernel(AttnParams P) {
   // every LDS read address is a loop-invariant per-lane offset plus an immediate: no per-stage address arithmetic
   auto stage = [&](int qt, auto slot_c) __attribute__((always_inline)) {
     constexpr int SLOT = decltype(slot_c)::value;
-    if (qt + 1 < nqt) wait_vm<DPT>();
+    if (NB == 3 && qt + 1 < nqt) wait_vm<DPT>();
     else wait_vm<0>();
     __syncthreads();  // stage qt landed for every wave; every wave is done with stage qt - 1 (the slot refilled next)
-    if (qt + 2 < nqt) issue((SLOT + 2) % K2_NBUF, qt + 2);
+    if (qt + NB - 1 < nqt) issue((SLOT + NB - 1) % NB, qt + NB - 1);
     const unsigned char* stg = smem + SLOT * K2_STAGE;
     const uint16_t* Qb = reinterpret_cast<const uint16_t*>(stg);
     const uint16_t* dOb = Qb + TILE64;
@@ -1072,46 +1075,34 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv2_kernel(AttnParams P) {
       const int sat = !HAS_BIAS ? 0
                       : (kw0 + 31 - q0 + P.Sq - 1 <= P.sat_lo ? 1 : (kw0 - q0 - 31 + P.Sq - 1 >= P.sat_hi ? 2 : 0));
       const bool use_lut = HAS_BIAS && sat == 0;
-      // rows 32u + crow(i, hh): four consecutive rows per 16-B read
+      // rows 32u + crow(i, hh): four consecutive rows per 16-B read, consumed group by group (12 live registers of
+      // row terms instead of 48); P keep -> sacc, dS -> dpacc in place
       const float* rt_row = rec + (use_lut ? 0 : (sat == 1 ? 64 : 128)) + 32 * u + 4 * hh;
       const float* nd_row = rec + 192 + 32 * u + 4 * hh;
-      float rt[16], nd[16];
-      uint32_t mw[16];
+      const float* lrow_t = lut_r + (win - 1 - (key - q0 - 4 * hh + P.Sq - 1 - k0));
+      const bool tile_causal = CAUSAL && (kw0 + 31 > q0 + P.causal_off);
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const f32x4 a = *reinterpret_cast<const f32x4*>(rt_row + 8 * g);
-        const f32x4 c = *reinterpret_cast<const f32x4*>(nd_row + 8 * g);
+        f32x4 rt4 = *reinterpret_cast<const f32x4*>(rt_row + 8 * g);
+        const f32x4 nd4 = *reinterpret_cast<const f32x4*>(nd_row + 8 * g);
+        u32x4 mw4 = {0u, 0u, 0u, 0u};
+        if (DROP) mw4 = *reinterpret_cast<const u32x4*>(mwd + mcol * 64 + 32 * u + 8 * g + 4 * hh);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          rt[4 * g + e] = a[e];
-          nd[4 * g + e] = c[e];
+          const int i = 4 * g + e;
+          float t = rt4[e];
+          if (use_lut) t += lrow_t[crow(i, 0)];  // bias per (key - row) from the reversed LUT (immediate offsets)
+          if (block_masked) t += km;             // padding / tail keys: -inf on the lane's whole column
+          float pr = fast_exp2(fmaf(sacc[i], sl2, t));  // rows >= Sq: rt = -inf -> 0
+          if (CAUSAL && tile_causal && key > q0 + crow(i, hh) + P.causal_off) pr = 0.f;
+          float keepf = 1.f;
+          if (DROP) keepf = __uint_as_float((uint32_t)__builtin_amdgcn_sbfe((int)mw4[e], mbit, 1) & dsbits);
+          sacc[i] = pr * keepf;
+          dpacc[i] = pr * fmaf(dpacc[i], keepf, nd4[e]);
         }
-        if (DROP) {
-          const u32x4 v = *reinterpret_cast<const u32x4*>(mwd + mcol * 64 + 32 * u + 8 * g + 4 * hh);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) mw[4 * g + e] = v[e];
-        }
       }
-      if (use_lut) {  // bias per (key - row) from the reversed LUT: immediate ds_read offsets per register
-        const float* lrow_t = lut_r + (win - 1 - (key - q0 - 4 * hh + P.Sq - 1 - k0));
-#pragma unroll
-        for (int i = 0; i < 16; ++i) rt[i] += lrow_t[crow(i, 0)];
-      }
-      if (block_masked) {  // padding / tail keys: -inf on the lane's whole column
-#pragma unroll
-        for (int i = 0; i < 16; ++i) rt[i] += km;
-      }
-      const bool tile_causal = CAUSAL && (kw0 + 31 > q0 + P.causal_off);
-      f32x16 pd, ds;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        float pr = fast_exp2(fmaf(sacc[i], sl2, rt[i]));  // rows >= Sq: rt = -inf -> 0
-        if (CAUSAL && tile_causal && key > q0 + crow(i, hh) + P.causal_off) pr = 0.f;
-        float keepf = 1.f;
-        if (DROP) keepf = __uint_as_float((uint32_t)__builtin_amdgcn_sbfe((int)mw[i], mbit, 1) & dsbits);
-        pd[i] = pr * keepf;
-        ds[i] = pr * fmaf(dpacc[i], keepf, nd[i]);
-      }
+      const f32x16& pd = sacc;
+      const f32x16& ds = dpacc;
       if (HAS_BIAS && sat != 0) {
         float t = 0.f;
 #pragma unroll
@@ -1148,11 +1139,12 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv2_kernel(AttnParams P) {
       }
     }
   };
-  static_assert(K2_NBUF == 3, "the stage loop is unrolled by the ring depth");
-  for (int qt = qt_begin; qt < nqt; qt += 3) {
+  for (int qt = qt_begin; qt < nqt; qt += NB) {  // unrolled by the ring depth
     stage(qt, std::integral_constant<int, 0>{});
     if (qt + 1 < nqt) stage(qt + 1, std::integral_constant<int, 1>{});
-    if (qt + 2 < nqt) stage(qt + 2, std::integral_constant<int, 2>{});
+    if constexpr (NB == 3) {
+      if (qt + 2 < nqt) stage(qt + 2, std::integral_constant<int, 2>{});
+    }
   }
 
   if (kvalid) {
@@ -1240,13 +1232,24 @@ void launch_bwd_dkdv_t(const AttnParams& p, int nblk, size_t lds, hipStream_t st
 }
 template <bool HB, bool HK, bool CA, bool DR>
 void launch_bwd_dkdv2_t(const AttnParams& p, int nblk, size_t lds, hipStream_t st) {
+  static const int occ = [] {
+    const char* e = getenv("DLLM_ATTN_DKDV_OCC");
+    return e != nullptr ? atoi(e) : 3;
+  }();
+  const size_t lds2 = lds - K2_STAGE;  // lds was sized for the 3-deep ring
+  // bias- and dropout-free variants only: they fit 168 VGPRs without spills (BART-large shapes: bwd -4..6 %, bench
+  // +0.8 %, profiles/r2_attn_dkdv_occ3.txt); the dropout variant spills and measured 2 % slower
+  if (occ == 3 && !HB && !DR && 3 * lds2 <= 160 * 1024) {
+    hipLaunchKernelGGL((attn_bwd_dkdv2_kernel<HB, HK, CA, DR, 2>), dim3(nblk), dim3(256), lds2, st, p);
+    return;
+  }
   static size_t attr = 64 * 1024;  // dynamic LDS above 64 KB (long sequences with bias) must be opted into
   if (lds > attr) {
-    (void)hipFuncSetAttribute((const void*)attn_bwd_dkdv2_kernel<HB, HK, CA, DR>,
+    (void)hipFuncSetAttribute((const void*)attn_bwd_dkdv2_kernel<HB, HK, CA, DR, 3>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = lds;
   }
-  hipLaunchKernelGGL((attn_bwd_dkdv2_kernel<HB, HK, CA, DR>), dim3(nblk), dim3(256), lds, st, p);
+  hipLaunchKernelGGL((attn_bwd_dkdv2_kernel<HB, HK, CA, DR, 3>), dim3(nblk), dim3(256), lds, st, p);
 }
 
 
