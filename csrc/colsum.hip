@@ -1,9 +1,9 @@
 // Column sums of a token-major bf16 matrix, accumulated into a parameter gradient: the bias gradient of a
 // linear layer (db = sum over tokens of dY).  torch's generic reduction needs ~31 us per BART-large bias
 // (profiles/r1_bart_large_b32_prof18_summary.txt, plus a separate add into the flat gradient buffer);
-// here: pass 1 = grid (N/128 column blocks, R row chunks), each lane sums 2 adjacent columns over its
-// rows with 4 independent accumulators (bf16x2 loads, 256-B coalesced rows), fp32 partials [R][N];
-// pass 2 = one block per 64 columns sums the R partials and adds into the bf16/fp32 gradient in place.
+// here: pass 1 = grid (N/512 column blocks, R row chunks), each lane sums 8 adjacent columns over its
+// rows (16-B loads, 1-KB coalesced rows per wave, 2 independent accumulator sets), fp32 partials [R][N];
+// pass 2 = one thread per column sums the R partials (independent loads) and adds into the gradient in place.
 #include "common.h"
 
 using namespace dllm;
@@ -12,53 +12,81 @@ namespace {
 
 constexpr int kRowChunks = 64;
 
+// pass 1: a lane sums 8 adjacent columns (one 16-B load per row) over the rows of its chunk, 2 independent
+// accumulator sets; a wave covers 512 columns of one row per load (1 KB coalesced), the block's 4 waves interleave
+// rows.  VEC = false: 2 columns per lane (rows only 4-B aligned / N not a multiple of 8).
+template <bool VEC>
 __global__ __launch_bounds__(256) void colsum_partial_kernel(const uint16_t* __restrict__ x, long ld, long T, int N,
                                                              float* __restrict__ part) {
-  __shared__ float red[4][128];
+  constexpr int CPL = VEC ? 8 : 2;       // columns per lane
+  constexpr int CPB = 64 * CPL;          // columns per block
+  __shared__ float red[4][CPB];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int c = blockIdx.x * 128 + 2 * lane;
+  const int c = blockIdx.x * CPB + CPL * lane;
   const long per = (T + gridDim.y - 1) / gridDim.y;
   const long r0 = (long)blockIdx.y * per;
   const long r1 = r0 + per < T ? r0 + per : T;
-  float a0[4] = {0.f, 0.f, 0.f, 0.f}, a1[4] = {0.f, 0.f, 0.f, 0.f};
+  float a0[CPL], a1[CPL];
+#pragma unroll
+  for (int k = 0; k < CPL; ++k) a0[k] = a1[k] = 0.f;
   if (c < N) {
     long r = r0 + w;
-    for (; r + 12 < r1; r += 16) {
+    for (; r + 4 < r1; r += 8) {
+      if constexpr (VEC) {
+        const u16x8 v0 = *reinterpret_cast<const u16x8*>(x + r * ld + c);
+        const u16x8 v1 = *reinterpret_cast<const u16x8*>(x + (r + 4) * ld + c);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const uint32_t v = *reinterpret_cast<const uint32_t*>(x + (r + 4 * u) * ld + c);
-        a0[u] += bf2f((uint16_t)(v & 0xFFFFu));
-        a1[u] += bf2f((uint16_t)(v >> 16));
+        for (int k = 0; k < 8; ++k) {
+          a0[k] += bf2f(v0[k]);
+          a1[k] += bf2f(v1[k]);
+        }
+      } else {
+        const uint32_t v0 = *reinterpret_cast<const uint32_t*>(x + r * ld + c);
+        const uint32_t v1 = *reinterpret_cast<const uint32_t*>(x + (r + 4) * ld + c);
+        a0[0] += bf2f((uint16_t)(v0 & 0xFFFFu));
+        a0[1] += bf2f((uint16_t)(v0 >> 16));
+        a1[0] += bf2f((uint16_t)(v1 & 0xFFFFu));
+        a1[1] += bf2f((uint16_t)(v1 >> 16));
       }
     }
     for (; r < r1; r += 4) {
-      const uint32_t v = *reinterpret_cast<const uint32_t*>(x + r * ld + c);
-      a0[0] += bf2f((uint16_t)(v & 0xFFFFu));
-      a1[0] += bf2f((uint16_t)(v >> 16));
+      if constexpr (VEC) {
+        const u16x8 v0 = *reinterpret_cast<const u16x8*>(x + r * ld + c);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) a0[k] += bf2f(v0[k]);
+      } else {
+        const uint32_t v0 = *reinterpret_cast<const uint32_t*>(x + r * ld + c);
+        a0[0] += bf2f((uint16_t)(v0 & 0xFFFFu));
+        a0[1] += bf2f((uint16_t)(v0 >> 16));
+      }
     }
   }
-  red[w][2 * lane] = (a0[0] + a0[1]) + (a0[2] + a0[3]);
-  red[w][2 * lane + 1] = (a1[0] + a1[1]) + (a1[2] + a1[3]);
+#pragma unroll
+  for (int k = 0; k < CPL; ++k) red[w][CPL * lane + k] = a0[k] + a1[k];
   __syncthreads();
-  for (int i = threadIdx.x; i < 128; i += 256) {
-    const int col = blockIdx.x * 128 + i;
-    if (col < N) part[(long)blockIdx.y * N + col] = red[0][i] + red[1][i] + red[2][i] + red[3][i];
+  for (int i = threadIdx.x; i < CPB; i += 256) {
+    const int col = blockIdx.x * CPB + i;
+    if (col < N) part[(long)blockIdx.y * N + col] = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
   }
 }
 
+// pass 2: one thread per column; the R partial loads are issued back to back (independent), then summed in order
 template <typename T>
 __global__ __launch_bounds__(256) void colsum_finish_kernel(const float* __restrict__ part, int R, int N,
                                                            T* __restrict__ out) {
-  __shared__ float red[4][64];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int col = blockIdx.x * 64 + lane;
+  const int col = blockIdx.x * 256 + threadIdx.x;
+  if (col >= N) return;
   float acc = 0.f;
-  if (col < N)
-    for (int g = w; g < R; g += 4) acc += part[(long)g * N + col];
-  red[w][lane] = acc;
-  __syncthreads();
-  if (w == 0 && col < N)
-    Elem<T>::store(out + col, Elem<T>::load(out + col) + red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane]);
+  int g = 0;
+  for (; g + 8 <= R; g += 8) {
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = part[(long)(g + k) * N + col];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc += v[k];
+  }
+  for (; g < R; ++g) acc += part[(long)g * N + col];
+  Elem<T>::store(out + col, Elem<T>::load(out + col) + acc);
 }
 
 }  // namespace
@@ -70,14 +98,19 @@ extern "C" int dllm_colsum_acc(const void* x, long ld, long T, int N, float* par
                                hipStream_t st) {
   if (N <= 0 || T <= 0 || (N & 1) || (ld & 1)) return -2;
   const int R = (int)(T < kRowChunks ? T : kRowChunks);
-  hipLaunchKernelGGL(colsum_partial_kernel, dim3((N + 127) / 128, R), dim3(256), 0, st, (const uint16_t*)x, ld, T, N,
-                     part);
+  const bool vec = (N % 8) == 0 && (ld % 8) == 0 && ((uintptr_t)x % 16) == 0;
+  if (vec)
+    hipLaunchKernelGGL(colsum_partial_kernel<true>, dim3((N + 511) / 512, R), dim3(256), 0, st, (const uint16_t*)x, ld,
+                       T, N, part);
+  else
+    hipLaunchKernelGGL(colsum_partial_kernel<false>, dim3((N + 127) / 128, R), dim3(256), 0, st, (const uint16_t*)x,
+                       ld, T, N, part);
   DLLM_CHECK_LAUNCH();
   if (out_is_bf16)
-    hipLaunchKernelGGL(colsum_finish_kernel<uint16_t>, dim3((N + 63) / 64), dim3(256), 0, st, part, R, N,
+    hipLaunchKernelGGL(colsum_finish_kernel<uint16_t>, dim3((N + 255) / 256), dim3(256), 0, st, part, R, N,
                        (uint16_t*)out);
   else
-    hipLaunchKernelGGL(colsum_finish_kernel<float>, dim3((N + 63) / 64), dim3(256), 0, st, part, R, N, (float*)out);
+    hipLaunchKernelGGL(colsum_finish_kernel<float>, dim3((N + 255) / 256), dim3(256), 0, st, part, R, N, (float*)out);
   DLLM_CHECK_LAUNCH();
   return 0;
 }

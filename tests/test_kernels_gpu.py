@@ -283,11 +283,14 @@ def test_linear_wgrad_path_uses_native_gemm():
     assert _rel(g, 2 * (dy.float().t() @ x.float())) < 5e-3
 
 
-@pytest.mark.parametrize("T,N,dt", [(32768, 1024, torch.bfloat16), (1000, 4096, torch.bfloat16), (37, 770, torch.float32)])
-def test_colsum_acc_bias_grad(T, N, dt):
+@pytest.mark.parametrize("aligned", [False, True])
+@pytest.mark.parametrize("T,N,dt", [(32768, 1024, torch.bfloat16), (1000, 4096, torch.bfloat16), (37, 770, torch.float32),
+                                    (4099, 3072, torch.float32)])
+def test_colsum_acc_bias_grad(T, N, dt, aligned):
+    """aligned: 16-B rows (8 columns per lane); else strided rows at a 4-B offset (2 columns per lane)."""
     torch.manual_seed(0)
-    x_full = torch.randn(T, N + 6, device=DEV, dtype=torch.bfloat16)
-    x = x_full[:, 2:N + 2]  # strided rows
+    x_full = torch.randn(T, N + 8, device=DEV, dtype=torch.bfloat16)
+    x = x_full[:, :N] if aligned else x_full[:, 2:N + 2]
     out0 = torch.randn(N, device=DEV, dtype=dt)
     out = out0.clone()
     _ext.native().colsum_acc(x, out)
