@@ -1075,34 +1075,77 @@ __global__ __launch_bounds__(256, NB == 3 ? 2 : 3) void attn_bwd_dkdv2_kernel(At
       const int sat = !HAS_BIAS ? 0
                       : (kw0 + 31 - q0 + P.Sq - 1 <= P.sat_lo ? 1 : (kw0 - q0 - 31 + P.Sq - 1 >= P.sat_hi ? 2 : 0));
       const bool use_lut = HAS_BIAS && sat == 0;
-      // rows 32u + crow(i, hh): four consecutive rows per 16-B read, consumed group by group (12 live registers of
-      // row terms instead of 48); P keep -> sacc, dS -> dpacc in place
-      const float* rt_row = rec + (use_lut ? 0 : (sat == 1 ? 64 : 128)) + 32 * u + 4 * hh;
-      const float* nd_row = rec + 192 + 32 * u + 4 * hh;
-      const float* lrow_t = lut_r + (win - 1 - (key - q0 - 4 * hh + P.Sq - 1 - k0));
-      const bool tile_causal = CAUSAL && (kw0 + 31 > q0 + P.causal_off);
+      f32x16 pd, ds;
+      if constexpr (NB == 3) {  // all 16 row terms read up front: their LDS latency hides under the MFMAs
+        // rows 32u + crow(i, hh): four consecutive rows per 16-B read
+        const float* rt_row = rec + (use_lut ? 0 : (sat == 1 ? 64 : 128)) + 32 * u + 4 * hh;
+        const float* nd_row = rec + 192 + 32 * u + 4 * hh;
+        float rt[16], nd[16];
+        uint32_t mw[16];
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        f32x4 rt4 = *reinterpret_cast<const f32x4*>(rt_row + 8 * g);
-        const f32x4 nd4 = *reinterpret_cast<const f32x4*>(nd_row + 8 * g);
-        u32x4 mw4 = {0u, 0u, 0u, 0u};
-        if (DROP) mw4 = *reinterpret_cast<const u32x4*>(mwd + mcol * 64 + 32 * u + 8 * g + 4 * hh);
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 a = *reinterpret_cast<const f32x4*>(rt_row + 8 * g);
+          const f32x4 c = *reinterpret_cast<const f32x4*>(nd_row + 8 * g);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int i = 4 * g + e;
-          float t = rt4[e];
-          if (use_lut) t += lrow_t[crow(i, 0)];  // bias per (key - row) from the reversed LUT (immediate offsets)
-          if (block_masked) t += km;             // padding / tail keys: -inf on the lane's whole column
-          float pr = fast_exp2(fmaf(sacc[i], sl2, t));  // rows >= Sq: rt = -inf -> 0
+          for (int e = 0; e < 4; ++e) {
+            rt[4 * g + e] = a[e];
+            nd[4 * g + e] = c[e];
+          }
+          if (DROP) {
+            const u32x4 v = *reinterpret_cast<const u32x4*>(mwd + mcol * 64 + 32 * u + 8 * g + 4 * hh);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) mw[4 * g + e] = v[e];
+          }
+        }
+        if (use_lut) {  // bias per (key - row) from the reversed LUT: immediate ds_read offsets per register
+          const float* lrow_t = lut_r + (win - 1 - (key - q0 - 4 * hh + P.Sq - 1 - k0));
+#pragma unroll
+          for (int i = 0; i < 16; ++i) rt[i] += lrow_t[crow(i, 0)];
+        }
+        if (block_masked) {  // padding / tail keys: -inf on the lane's whole column
+#pragma unroll
+          for (int i = 0; i < 16; ++i) rt[i] += km;
+        }
+        const bool tile_causal = CAUSAL && (kw0 + 31 > q0 + P.causal_off);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          float pr = fast_exp2(fmaf(sacc[i], sl2, rt[i]));  // rows >= Sq: rt = -inf -> 0
           if (CAUSAL && tile_causal && key > q0 + crow(i, hh) + P.causal_off) pr = 0.f;
           float keepf = 1.f;
-          if (DROP) keepf = __uint_as_float((uint32_t)__builtin_amdgcn_sbfe((int)mw4[e], mbit, 1) & dsbits);
-          sacc[i] = pr * keepf;
-          dpacc[i] = pr * fmaf(dpacc[i], keepf, nd4[e]);
+          if (DROP) keepf = __uint_as_float((uint32_t)__builtin_amdgcn_sbfe((int)mw[i], mbit, 1) & dsbits);
+          pd[i] = pr * keepf;
+          ds[i] = pr * fmaf(dpacc[i], keepf, nd[i]);
         }
+      } else {  // 2-deep ring at 168 VGPRs: row terms consumed group by group, P / dS in place
+        // rows 32u + crow(i, hh): four consecutive rows per 16-B read, consumed group by group (12 live registers of
+        // row terms instead of 48); P keep -> sacc, dS -> dpacc in place
+        const float* rt_row = rec + (use_lut ? 0 : (sat == 1 ? 64 : 128)) + 32 * u + 4 * hh;
+        const float* nd_row = rec + 192 + 32 * u + 4 * hh;
+        const float* lrow_t = lut_r + (win - 1 - (key - q0 - 4 * hh + P.Sq - 1 - k0));
+        const bool tile_causal = CAUSAL && (kw0 + 31 > q0 + P.causal_off);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          f32x4 rt4 = *reinterpret_cast<const f32x4*>(rt_row + 8 * g);
+          const f32x4 nd4 = *reinterpret_cast<const f32x4*>(nd_row + 8 * g);
+          u32x4 mw4 = {0u, 0u, 0u, 0u};
+          if (DROP) mw4 = *reinterpret_cast<const u32x4*>(mwd + mcol * 64 + 32 * u + 8 * g + 4 * hh);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int i = 4 * g + e;
+            float t = rt4[e];
+            if (use_lut) t += lrow_t[crow(i, 0)];  // bias per (key - row) from the reversed LUT (immediate offsets)
+            if (block_masked) t += km;             // padding / tail keys: -inf on the lane's whole column
+            float pr = fast_exp2(fmaf(sacc[i], sl2, t));  // rows >= Sq: rt = -inf -> 0
+            if (CAUSAL && tile_causal && key > q0 + crow(i, hh) + P.causal_off) pr = 0.f;
+            float keepf = 1.f;
+            if (DROP) keepf = __uint_as_float((uint32_t)__builtin_amdgcn_sbfe((int)mw4[e], mbit, 1) & dsbits);
+            sacc[i] = pr * keepf;
+            dpacc[i] = pr * fmaf(dpacc[i], keepf, nd4[e]);
+          }
+        }
+        pd = sacc;
+        ds = dpacc;
       }
-      const f32x16& pd = sacc;
-      const f32x16& ds = dpacc;
       if (HAS_BIAS && sat != 0) {
         float t = 0.f;
 #pragma unroll
