@@ -115,19 +115,30 @@ DLLM_DEVICE bf16x8v ld_tr_operand(const uint16_t* T, int kb0, int t, int r) {
 constexpr uint32_t C24 = 0x9E3779u;
 DLLM_DEVICE uint32_t attn_pair_hash(uint32_t x) { return __umul24(x, C24); }
 
-// x kept where the lane's bit of `keep` (a compare's lane mask) is set, else 0 (one v_cndmask)
-DLLM_DEVICE float lane_select(uint64_t keep, float x) {
-  float r;
-  asm("v_cndmask_b32 %0, 0, %1, %2" : "=v"(r) : "v"(x), "s"(keep));
-  return r;
-}
-
-// (w << 1) | (this lane's bit of `keep`): one v_addc_co_u32 with the compare mask as carry-in
-DLLM_DEVICE uint32_t shift_in(uint32_t w, uint64_t keep) {
-  uint32_t r;
-  uint64_t co;
-  asm("v_addc_co_u32 %0, %1, %2, %2, %3" : "=v"(r), "=s"(co) : "v"(w), "s"(keep));
-  return r;
+// Two key pairs (A, then B) of the forward's dropout: the four keep compares write SGPR-pair lane masks, then per key
+// one v_cndmask zeroes P and one v_addc_co_u32 shifts the keep bit into the word (word = 2 word + keep), odd key first
+// within a pair.  Compares and their consumers sit in ONE statement, each mask read >= 3 instructions after its
+// write (a VALU-written SGPR read as a lane mask needs wait states hipcc does not insert around inline asm).  The
+// compiler's select + or form of the same costs 4 instructions per pair more.
+DLLM_DEVICE void keep_pairs2(uint32_t& word, float& a_odd, float& a_even, float& b_odd, float& b_even, uint32_t ha,
+                             uint32_t ya, uint32_t hb, uint32_t yb, uint32_t thr_hi, uint32_t thr16) {
+  uint64_t m0, m1, m2, m3, co;
+  asm volatile(
+      "v_cmp_le_u32_e64 %[m0], %[thi], %[ha]\n\t"
+      "v_cmp_le_u32_e64 %[m1], %[t16], %[ya]\n\t"
+      "v_cmp_le_u32_e64 %[m2], %[thi], %[hb]\n\t"
+      "v_cmp_le_u32_e64 %[m3], %[t16], %[yb]\n\t"
+      "v_cndmask_b32_e64 %[ao], 0, %[ao], %[m0]\n\t"
+      "v_addc_co_u32_e64 %[w], %[co], %[w], %[w], %[m0]\n\t"
+      "v_cndmask_b32_e64 %[ae], 0, %[ae], %[m1]\n\t"
+      "v_addc_co_u32_e64 %[w], %[co], %[w], %[w], %[m1]\n\t"
+      "v_cndmask_b32_e64 %[bo], 0, %[bo], %[m2]\n\t"
+      "v_addc_co_u32_e64 %[w], %[co], %[w], %[w], %[m2]\n\t"
+      "v_cndmask_b32_e64 %[be], 0, %[be], %[m3]\n\t"
+      "v_addc_co_u32_e64 %[w], %[co], %[w], %[w], %[m3]"
+      : [ao] "+v"(a_odd), [ae] "+v"(a_even), [bo] "+v"(b_odd), [be] "+v"(b_even), [w] "+v"(word), [m0] "=&s"(m0),
+        [m1] "=&s"(m1), [m2] "=&s"(m2), [m3] "=&s"(m3), [co] "=&s"(co)
+      : [thi] "s"(thr_hi), [t16] "s"(thr16), [ha] "v"(ha), [ya] "v"(ya), [hb] "v"(hb), [yb] "v"(yb));
 }
 
 // Dropout keep bits of one (row, 64-key tile, lane half): bit i <-> key kbase + crow(i, hh) (the forward's
@@ -388,20 +399,21 @@ __global__ __launch_bounds__(256, FNB == 3 ? 2 : 3) void attn_fwd_kernel(AttnPar
       const uint32_t base = rh + ((uint32_t)(kbase >> 1) + 2u * (uint32_t)hh) * HG;
       const uint32_t thr_hi = P.thr << 16;
       uint32_t word = 0;
-      auto one = [&](float v, bool keep) {
-        word = word + word + (keep ? 1u : 0u);  // v_addc_co_u32 with the compare as carry-in
-        return keep ? v : 0.f;
-      };
 #pragma unroll
       for (int t = 1; t >= 0; --t) {
         f32x16& sv = t == 0 ? s0 : s1;
 #pragma unroll
-        for (int i = 14; i >= 0; i -= 2) {
-          const uint32_t pair = (uint32_t)(((i & 3) >> 1) + 4 * (i >> 2) + 16 * t);  // (key - kbase - 4hh) / 2
-          const uint32_t h = attn_pair_hash(base + pair * HG);
-          const uint32_t y = h ^ (h >> 16);
-          sv[i + 1] = one(sv[i + 1], h >= thr_hi);
-          sv[i] = one(sv[i], (y & 0xFFFFu) >= P.thr);
+        for (int i = 14; i >= 0; i -= 4) {  // pairs (i, i + 1) then (i - 2, i - 1)
+          const uint32_t pa = (uint32_t)(((i & 3) >> 1) + 4 * (i >> 2) + 16 * t);  // (key - kbase - 4hh) / 2
+          const uint32_t pb = (uint32_t)((((i - 2) & 3) >> 1) + 4 * ((i - 2) >> 2) + 16 * t);
+          const uint32_t ha = attn_pair_hash(base + pa * HG), hb = attn_pair_hash(base + pb * HG);
+          const uint32_t ya = (ha ^ (ha >> 16)) & 0xFFFFu, yb = (hb ^ (hb >> 16)) & 0xFFFFu;
+          float ao = sv[i + 1], ae = sv[i], bo = sv[i - 1], be = sv[i - 2];
+          keep_pairs2(word, ao, ae, bo, be, ha, ya, hb, yb, thr_hi, P.thr);
+          sv[i + 1] = ao;
+          sv[i] = ae;
+          sv[i - 1] = bo;
+          sv[i - 2] = be;
         }
       }
       P.dmask[((long)bh * P.n_ktiles * 2 + 2 * kt + hh) * P.sq_pad + qrow] = word;
