@@ -630,6 +630,71 @@ Tensor gemm_fused(const Tensor& a, const Tensor& b, bool b_kmajor, int64_t epi, 
   return out;
 }
 
+// Gated-GELU FFN (FLAN-T5 / T5 v1.1 "gated-gelu", tanh GELU) on the ping-pong kernel, csrc/gemm_fused.hip epi 8 / 9.
+// forward: x [M, d] . [wi_0; wi_1]^T ([2F, d], the stacked wi weight) -> h = dropout(gelu(x wi_0^T) * (x wi_1^T)) [M, F]
+//          plus G1 = s gelu'(gate) up and G2 = s gelu(gate) ([M, F] each, s = keep / (1 - p)) for the backward;
+// backward: dH = dy [M, d] . wo [d, F] (k-major) -> [dH G1 | dH G2] = d(stacked wi output) [M, 2F].
+// M % 256 == 0, F % 256 == 0, d % 64 == 0 (the fused FFN's shape rule, ops/ffn.py).
+static GemmFusedParams geglu_params(const Tensor& a, const Tensor& b, bool b_kmajor, int epi) {
+  TORCH_CHECK(gemm_fused_supported(a, b, b_kmajor), "gemm_geglu: unsupported operands (bf16 GPU, M / N % 256, K % 64)");
+  TORCH_CHECK(a.device() == b.device(), "gemm_geglu: device mismatch");
+  const int64_t M = a.size(0), K = a.size(1), N = b_kmajor ? b.size(1) : b.size(0);
+  GemmFusedParams P{};
+  P.A = reinterpret_cast<const uint16_t*>(a.data_ptr());
+  P.B = reinterpret_cast<const uint16_t*>(b.data_ptr());
+  P.lda = a.stride(0);
+  P.ldb = b.stride(0);
+  P.M = (int)M;
+  P.N = (int)N;
+  P.K = (int)K;
+  P.tm = (int)(M / 256);
+  P.tn = (int)(N / 256);
+  P.epi = epi;
+  P.scale = 1.f;
+  const char* e = std::getenv("DLLM_GEMM_GRP");
+  P.grp = e ? std::max(0, std::atoi(e)) : 4;
+  return P;
+}
+
+std::vector<Tensor> gemm_geglu(const Tensor& x, const Tensor& wi, double p, int64_t seed) {
+  TORCH_CHECK(p >= 0.0 && p < 1.0, "gemm_geglu: dropout p must be in [0, 1)");
+  GemmFusedParams P = geglu_params(x, wi, false, 8);
+  const int64_t M = P.M, F = P.N / 2;
+  TORCH_CHECK(F % 256 == 0, "gemm_geglu: d_ff must be a multiple of 256");
+  auto h = at::empty({M, F}, x.options());
+  auto g1 = at::empty({M, F}, x.options());
+  auto g2 = at::empty({M, F}, x.options());
+  P.C = reinterpret_cast<uint16_t*>(h.data_ptr());
+  P.ldc = F;
+  P.aux_out = reinterpret_cast<uint16_t*>(g1.data_ptr());
+  P.aux_out2 = reinterpret_cast<uint16_t*>(g2.data_ptr());
+  P.ldaux = F;
+  P.p = (float)p;
+  P.scale = p > 0.0 ? (float)(1.0 / (1.0 - p)) : 1.f;
+  P.seed = (uint32_t)seed;
+  const double t = p * 65536.0;
+  P.thr = t >= 65535.0 ? 0xFFFFu : (uint32_t)t;
+  check_rc(dllm_gemm_fused(&P, 0, 9, stream()), "gemm_geglu");
+  return {h, g1, g2};
+}
+
+Tensor gemm_dgeglu(const Tensor& dy, const Tensor& wo, const Tensor& g1, const Tensor& g2) {
+  GemmFusedParams P = geglu_params(dy, wo, true, 9);
+  const int64_t M = P.M, F = P.N;
+  for (const Tensor* t : {&g1, &g2})
+    TORCH_CHECK(t->is_cuda() && t->device() == dy.device() && t->scalar_type() == at::kBFloat16 && t->is_contiguous() &&
+                    t->dim() == 2 && t->size(0) == M && t->size(1) == F,
+                "gemm_dgeglu: G1 / G2 must be contiguous bf16 [M, F] GPU tensors");
+  auto du = at::empty({M, 2 * F}, dy.options());
+  P.C = reinterpret_cast<uint16_t*>(du.data_ptr());
+  P.ldc = 2 * F;
+  P.aux = reinterpret_cast<const uint16_t*>(g1.data_ptr());
+  P.aux2 = reinterpret_cast<const uint16_t*>(g2.data_ptr());
+  P.ldaux = F;
+  check_rc(dllm_gemm_fused(&P, 1, 9, stream()), "gemm_dgeglu");
+  return du;
+}
+
 // out (+)= column sums of x ([T, N] bf16, unit inner stride): bias gradients accumulated in place
 void colsum_acc(const Tensor& x, Tensor& out) {
   check_gpu(x, "x");
@@ -709,6 +774,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("aux") = py::none(), py::arg("aux_out") = py::none(), py::arg("p") = 0.0, py::arg("seed") = 0,
         py::arg("variant") = -1, py::arg("mask") = py::none());
   m.def("gemm_fused_supported", &gemm_fused_supported);
+  m.def("gemm_geglu", &gemm_geglu, "gated-GELU FFN input GEMM: (h, G1, G2) from x and the stacked [wi_0; wi_1]");
+  m.def("gemm_dgeglu", &gemm_dgeglu, "gated-GELU FFN backward GEMM: d(stacked wi output) from dy, wo, G1, G2");
   m.def("gemm_fused_variant", &gemm_fused_variant, "default kernel variant for reduction length K");
   m.def("colsum_acc", &colsum_acc, "out += x.sum(0) for a token-major bf16 x (bias gradients)");
   dllm::bind_reducer(m);

@@ -29,6 +29,7 @@
 // * bijective XCD remap of the 1-D grid, tiles of one 256-row block of A consecutive (L2 reuse of A).
 #include "common.h"
 
+#include <cstdlib>
 #include <type_traits>
 
 using namespace dllm;
@@ -43,7 +44,7 @@ namespace {
 constexpr int BM = 256, BN = 256, NT = 512;
 
 enum Epi { EPI_NONE = 0, EPI_RELU = 1, EPI_GELU = 2, EPI_DRELU = 3, EPI_DGELU = 4, EPI_GELU_TANH = 5,
-           EPI_DGELU_TANH = 6, EPI_DRELU_M = 7 };
+           EPI_DGELU_TANH = 6, EPI_DRELU_M = 7, EPI_GEGLU = 8, EPI_DGEGLU = 9 };
 
 DLLM_DEVICE int xcd_remap(int bid, int nblk) {
   const int q = nblk / 8, r = nblk % 8, x = bid % 8;
@@ -183,6 +184,13 @@ DLLM_DEVICE f32x4 epilogue4(const GemmFusedParams& P, int m, int n, f32x4 v) {
     for (int k = 0; k < 4; ++k) v[k] = (h[k] & 0x7fff) ? v[k] * P.scale : 0.f;
   } else if (EPI == EPI_DGELU || EPI == EPI_DGELU_TANH) {
     v = v * load4(P.aux + (long)m * P.ldaux + n);
+  } else if (EPI == EPI_DGEGLU) {
+    // gated backward: dH (this GEMM, N = F columns) -> [d gate | d up] = [dH * G1 | dH * G2] in the [M][2F] layout of
+    // the stacked wi output; G1 = s * gelu'(gate) * up, G2 = s * gelu(gate) stored by the forward (s = keep / (1 - p))
+    const f32x4 g1 = load4(P.aux + (long)m * P.ldaux + n);
+    const f32x4 g2 = load4(P.aux2 + (long)m * P.ldaux + n);
+    store4(P.C + (long)m * P.ldc + P.N + n, v * g2);
+    v = v * g1;
   }
   store4(P.C + (long)m * P.ldc + n, v);
   return v;
@@ -412,7 +420,14 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(GemmFusedParams P) {
   uint16_t* lds = reinterpret_cast<uint16_t*>(smem);  // [2][A image | B image], [256][64] each
   using RI = RowImg<64>;
   constexpr int TILE = 64 * 256;
-  constexpr int NST = (EPI == EPI_GELU || EPI == EPI_GELU_TANH) ? 64 : 32;  // vector stores per lane per epilogue
+  constexpr int NST = (EPI == EPI_GELU || EPI == EPI_GELU_TANH || EPI == EPI_DGEGLU) ? 64 : EPI == EPI_GEGLU ? 48 : 32;
+  // gated forward (EPI_GEGLU, NT only): B = the stacked [wi_0; wi_1] weight [2F][K]; tile column block nb covers hidden
+  // units f0 = 128 nb .. f0 + 127: image rows 0-127 are wi_0 rows f0.., rows 128-255 wi_1 rows f0.. (two DMA sources),
+  // and each wave reads its fragments so that accumulator columns j = 0, 2 are gate and j = 1, 3 the matching up
+  // values of the same 16 hidden units (brow below): gelu(gate) * up is formed in registers, the [M][2F] product is
+  // never stored.
+  constexpr bool GATED = EPI == EPI_GEGLU;
+  static_assert(!GATED || !BKM, "gated forward is NT only");
   constexpr int VM_POST = 8 + NST <= 63 ? 8 + NST : 63;
 
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
@@ -459,7 +474,9 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(GemmFusedParams P) {
   const uint32_t offA = (uint32_t)(ra * P.lda + cs) * 2u;
   const uint32_t offB = (uint32_t)(BKM ? kr * P.ldb + (((lane & 31) ^ gsw(kr)) << 3) : rb * P.ldb + cs) * 2u;
   auto tile_a = [&](int tm0) { return P.A + (long)tm0 * P.lda; };
-  auto tile_b = [&](int tn0) { return BKM ? P.B + tn0 : P.B + (long)tn0 * P.ldb; };
+  auto tile_b = [&](int tn0) { return BKM ? P.B + tn0 : P.B + (long)(GATED ? tn0 / 2 : tn0) * P.ldb; };
+  // gated: image rows 128.. come from wi_1 = rows F.. of B (F = N / 2)
+  const long up_rows = GATED ? (long)(P.N / 2 - 128) * P.ldb : 0;
   int m0, n0, m1 = 0, n1 = 0;
   tile_mn(0, m0, n0);
   if (ntw > 1) tile_mn(1, m1, n1);
@@ -496,7 +513,8 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(GemmFusedParams P) {
     const uint16_t *ab, *bb;
     const int kt = src(g, ab, bb);
     const uint32_t dst = lds0 + (uint32_t)((g & 1) * 2 * TILE + TILE) * 2u + (uint32_t)base * 128u + lb;
-    bld16(bb + (long)base * P.ldb + kt * 64, offB, __builtin_amdgcn_readfirstlane(dst));
+    bld16(bb + (long)base * P.ldb + (GATED && base >= 128 ? up_rows : 0) + kt * 64, offB,
+          __builtin_amdgcn_readfirstlane(dst));
   };
   auto unitBk = [&](int u, int g) {  // k-rows 16u .. 16u+15 of global k-tile g
     const uint16_t *ab, *bb;
@@ -602,6 +620,13 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(GemmFusedParams P) {
 
   // one k-tile = 4 phases.  FULL: every unit of the 4 phases exists (g + 2 < total) -> unconditional issue, fixed vmcnt;
   // POST: first k-tile after an epilogue (its stores are queued between the units)
+  // image row of the wave's B fragment for accumulator column block jq (0..3).  The DMA schedule fills image rows
+  // {0-31, 64-95, 128-159, 192-223} (read by phase 0's b0) one phase earlier than {32-63, 96-127, 160-191, 224-255}
+  // (phase 1's b1), so the gated placement keeps b0 inside the first set: wave wn's gate block for b0 is rows
+  // 64 (wn >> 1) + 16 (wn & 1) .. + 15, its up block the same + 128, and b1 takes the blocks 32 rows further.
+  auto brow = [&](int jq) {
+    return GATED ? (jq & 1) * 128 + (wn >> 1) * 64 + (wn & 1) * 16 + 32 * (jq >> 1) : wn * 64 + 16 * jq;
+  };
   auto ktile = [&](int g, auto full, bool post) {
     constexpr bool FULL = decltype(full)::value;
     const uint16_t* As = lds + (g & 1) * 2 * TILE;
@@ -628,7 +653,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(GemmFusedParams P) {
           b0[j][ks] = frag_km16(Bs, 32 * ks, wn * 64 + 16 * j, lane);
           b1[j][ks] = frag_km16(Bs, 32 * ks, wn * 64 + 32 + 16 * j, lane);
         } else {
-          b0[j][ks] = RI::frag16(Bs, 32 * ks, wn * 64 + 16 * j, lane);
+          b0[j][ks] = RI::frag16(Bs, 32 * ks, brow(j), lane);
         }
       }
     }
@@ -641,7 +666,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(GemmFusedParams P) {
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) b1[j][ks] = RI::frag16(Bs, 32 * ks, wn * 64 + 32 + 16 * j, lane);
+        for (int j = 0; j < 2; ++j) b1[j][ks] = RI::frag16(Bs, 32 * ks, brow(2 + j), lane);
     }
     iss(p0 + 1);
     sync_l();
@@ -685,7 +710,39 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(GemmFusedParams P) {
     f32x4 bv[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) bv[j] = P.bias ? load4(P.bias + ncol + 16 * j) : f32x4{0.f, 0.f, 0.f, 0.f};
-    if constexpr (EPI == EPI_DRELU_M) {
+    if constexpr (GATED) {
+      // acc[i][2 jj] = gate, acc[i][2 jj + 1] = up for hidden units f .. f + 3 (f - f0 = the gate block's image row, brow)
+      const int F = P.N / 2;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+          const int m = mrow + 16 * i, f = tn0 / 2 + (wn >> 1) * 64 + (wn & 1) * 16 + 32 * jj + 4 * (ln >> 4);
+          const f32x4 gt = acc[i][2 * jj], up = acc[i][2 * jj + 1];
+          f32x4 h, g1, g2;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float a, d;
+            gelu_tanh_pair(gt[r], a, d);
+            h[r] = a * up[r];
+            g1[r] = d * up[r];
+            g2[r] = a;
+          }
+          if (P.p > 0.f) {  // keep decision on the OUTPUT element m * F + f, as csrc/act.hip's gated path
+            bool k0, k1, k2, k3;
+            const uint32_t e = (uint32_t)m * (uint32_t)F + (uint32_t)f;
+            keep_two(P.seed, P.thr, e, k0, k1);
+            keep_two(P.seed, P.thr, e + 2u, k2, k3);
+            const f32x4 s = {k0 ? P.scale : 0.f, k1 ? P.scale : 0.f, k2 ? P.scale : 0.f, k3 ? P.scale : 0.f};
+            h = h * s;
+            g1 = g1 * s;
+            g2 = g2 * s;
+          }
+          store4(P.C + (long)m * P.ldc + f, h);
+          store4(P.aux_out + (long)m * P.ldaux + f, g1);
+          store4(P.aux_out2 + (long)m * P.ldaux + f, g2);
+        }
+    } else if constexpr (EPI == EPI_DRELU_M) {
       const u32x4 mw = *reinterpret_cast<const u32x4*>(smem + 4 * TILE * 2 + (ti & 1) * 8192 + tid * 16);
 #pragma unroll
       for (int i = 0; i < 8; ++i)
@@ -766,7 +823,14 @@ template <int EPI, bool BKM>
 int launch_pp(const GemmFusedParams& p, bool persist, hipStream_t st) {
   const size_t lds = (size_t)2 * 2 * 64 * 256 * 2 + (EPI == EPI_DRELU_M ? 2 * 8192 : 0);
   const int T = p.tm * p.tn, cus = num_cus() / 8 * 8;
-  constexpr bool light = EPI == EPI_NONE || EPI == EPI_RELU || EPI == EPI_DRELU_M;
+  // the gated forward is store-only too; its backward (two aux loads per accumulator block) measured 6-10 % faster
+  // persistent as well (profiles/r2_geglu_bench.jsonl); DLLM_GEGLU_BWD_PERSIST=0 keeps one tile per workgroup
+  static const bool dgeglu_persist = [] {
+    const char* e = std::getenv("DLLM_GEGLU_BWD_PERSIST");
+    return !(e && e[0] == '0');
+  }();
+  const bool light = EPI == EPI_NONE || EPI == EPI_RELU || EPI == EPI_DRELU_M || EPI == EPI_GEGLU ||
+                     (EPI == EPI_DGEGLU && dgeglu_persist);
   if (light && persist && cus >= 8 && T >= 2 * cus && p.K >= 128) {
     static bool attr = false;
     if (!attr) {
@@ -830,6 +894,10 @@ int dispatch_epi(const GemmFusedParams& p, int variant, hipStream_t st) {
     case EPI_DGELU_TANH: return launch_v<BKM, EPI_DGELU_TANH>(p, variant, st);
     case EPI_DRELU_M: return variant == 8 ? launch_pp<EPI_DRELU_M, BKM>(p, false, st)
                                           : variant == 9 ? launch_pp<EPI_DRELU_M, BKM>(p, true, st) : -6;
+    case EPI_GEGLU:  // ping-pong kernel only (its fragment placement pairs gate and up), NT only
+      if constexpr (BKM) return -6;
+      else return variant == 8 || variant == 9 ? launch_pp<EPI_GEGLU, false>(p, variant == 9, st) : -6;
+    case EPI_DGEGLU: return variant == 8 || variant == 9 ? launch_pp<EPI_DGEGLU, BKM>(p, variant == 9, st) : -6;
     default: return -5;
   }
 }

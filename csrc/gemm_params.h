@@ -25,10 +25,13 @@ struct GemmFusedParams {
   const uint16_t* bias;  // [N] or null (added before the activation)
   const uint16_t* aux;   // backward epilogues: saved activation (ReLU) / pre-activation (GELU), [M][ldaux]
   uint16_t* aux_out;     // GELU forward: pre-activation output, [M][ldaux]
+  const uint16_t* aux2;  // gated backward (epi 9): second saved factor, [M][ldaux]
+  uint16_t* aux_out2;    // gated forward (epi 8): second saved factor, [M][ldaux]
   long lda, ldb, ldc, ldaux;
   int M, N, K;
   int tm, tn;  // M / 256, N / 256
-  int epi;     // 0 none, 1 relu, 2 gelu(erf), 3 d-relu, 4 d-gelu(erf), 5 gelu(tanh), 6 d-gelu(tanh)
+  int epi;     // 0 none, 1 relu, 2 gelu(erf), 3 d-relu, 4 d-gelu(erf), 5 gelu(tanh), 6 d-gelu(tanh),
+               // 7 d-relu from bits, 8 gated gelu(tanh) (N = 2F, output [M][F]), 9 its backward (N = F, output [M][2F])
   float p;     // dropout probability on the activation output (forward element index m * N + n)
   float scale; // 1 / (1 - p), or 1
   uint32_t seed, thr;

@@ -21,7 +21,7 @@ import torch.nn as nn
 from ..ops import activations, attention as attn_ops, norms
 from ..parallel.context import (chunked_attention, chunked_cross_attention, context_parallel_encode,
                                 long_sequence_chunk, ring_attention)
-from ..ops.ffn import ffn
+from ..ops.ffn import ffn, gated_ffn
 from ..ops.cross_entropy import cross_entropy
 from ..ops.embedding import embedding
 from ..ops.linear import Linear, linear, stacked_linear
@@ -124,8 +124,7 @@ class T5DenseActDense(nn.Module):
         seed = default_rng().next_seed() if p > 0 else 0
         if not self.gated:  # activation + dropout in the GEMM epilogues where possible (ops/ffn.py)
             return ffn(x, self.wi, self.wo, self.act, p, seed)
-        h = activations.act_dropout(self.wi(x), self.act, p, seed, gated=True)
-        return self.wo(h)
+        return gated_ffn(x, self.wi, self.wo, self.act, p, seed)
 
 
 class T5LayerSelfAttention(nn.Module):

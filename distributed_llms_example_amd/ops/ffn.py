@@ -24,7 +24,8 @@ alive until backward.  Here (csrc/gemm_fused.hip):
 
 Taken only when both linears carry FlatParams-managed gradients (``_dllm_fused_wgrad``), the input is
 bf16 on the GPU and the shapes suit the kernel (tokens and d_ff multiples of 256, d_model of 64); anything
-else (gated FLAN-T5 FFNs, CPU, odd token counts) runs the unfused modules with identical semantics.
+else (CPU, odd token counts) runs the unfused modules with identical semantics.  Gated FLAN-T5 FFNs take
+``gated_ffn`` (one GEMM pairs gate and up columns in registers, epilogues 8 / 9).
 ``DLLM_FUSED_FFN=0`` forces the unfused path (A/B runs); ``DLLM_GEMM_FUSED_VARIANT=n`` forces a kernel
 variant (csrc/gemm_fused.hip); ``DLLM_RELU_MASK=0`` makes the ReLU backward read ``H`` instead of the bits.
 """
@@ -116,6 +117,80 @@ def _fusable_shapes(x2: torch.Tensor, wi: torch.Tensor, wo: torch.Tensor) -> boo
     Fd = wi.shape[0]
     return (tuple(wo.shape) == (d, Fd) and M % 256 == 0 and Fd % 256 == 0 and d % 64 == 0 and M * Fd < 2**32
             and C.gemm_fused_supported(x2, wi, False) and C.gemm_fused_supported(x2, wo, True))
+
+
+class _FusedGatedFFNFn(torch.autograd.Function):
+    """``wo(dropout(gelu_new(x wi_0ᵀ) * (x wi_1ᵀ)))`` with ``wi = [wi_0; wi_1]`` stacked (models/t5.py).
+
+    Forward: ONE GEMM (csrc/gemm_fused.hip epilogue 8) pairs each gate column with its up column in registers
+    and writes ``h`` plus the two backward factors ``G1 = s·gelu'(gate)·up`` and ``G2 = s·gelu(gate)``; the
+    ``[tokens, 2·d_ff]`` product is never stored and there is no activation kernel.  Backward: ONE GEMM
+    ``dH = dy · wo`` (epilogue 9) writes ``[dH·G1 | dH·G2]`` straight in the stacked layout that the wi
+    weight gradient and dgrad consume.  Unfused: GEMM store of ``[M, 2F]`` + act kernel (read 2F, write F)
+    forward, act-backward kernel (read F + 2F, write 2F) backward."""
+
+    @staticmethod
+    def forward(ctx, x, wi, wo, p, seed, params):
+        C = _ext.native()
+        shape = x.shape
+        x2 = x.reshape(-1, shape[-1])
+        h, g1, g2 = C.gemm_geglu(x2, wi, float(p), int(seed))
+        y = F.linear(h, wo)
+        ctx.save_for_backward(x2, h, g1, g2)
+        ctx.params = params
+        for q in params:
+            _use(q)
+        ctx.shape = shape
+        return y.view(*shape[:-1], wo.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, h, g1, g2 = ctx.saved_tensors
+        Wi, Wo = ctx.params
+        C = _ext.native()
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        if not C.gemm_fused_supported(dy2, Wo.detach(), True):
+            dy2 = dy2.contiguous()
+        du = C.gemm_dgeglu(dy2, Wo.detach(), g1, g2)
+        with torch.no_grad():
+            wgrad_accumulate(_gbuf(Wo), dy2, h)
+        _fire(Wo)
+        dx = torch.matmul(du, Wi.detach()) if ctx.needs_input_grad[0] else None
+        with torch.no_grad():
+            wgrad_accumulate(_gbuf(Wi), du, x2)
+        _fire(Wi)
+        return (None if dx is None else dx.view(ctx.shape)), None, None, None, None, None
+
+
+gated_calls = 0  # number of gated FFN forwards that took the fused path
+# Where the fused gated GEMMs win (tools/geglu_bench.py, profiles/r2_geglu_bench.jsonl, flan-t5 A/Bs in
+# profiles/r2_geglu_ab.txt): they need >= 2 output tiles per CU to run persistent (epilogue stores / loads under the
+# next tile's MFMAs), so tokens x d_ff >= _GATED_MIN_MF; and with a long reduction (d_model >= 1024) hipBLASLt's
+# GEMM outruns the ping-pong kernel by more than the two activation passes cost (flan-t5-large -3 %, flan-t5-xl
+# encoder -10 % in the model), so d_model <= _GATED_MAX_D.  flan-t5-base at b=64: +0.6 % samples/s.
+_GATED_MIN_MF = int(os.environ.get("DLLM_GATED_MIN_MF", str(2 * 256 * 256 * 256)))
+_GATED_MAX_D = int(os.environ.get("DLLM_GATED_MAX_D", "768"))
+
+
+def gated_ffn(x: torch.Tensor, lin_in, lin_out, act: str, p: float = 0.0, seed: int = 0) -> torch.Tensor:
+    """``lin_out(dropout(act(x wi_0ᵀ) * (x wi_1ᵀ)))`` with ``lin_in.weight = [wi_0; wi_1]``, fused where possible
+    (tanh GELU, bias-free, tokens and d_ff multiples of 256, tokens x d_ff >= ``_GATED_MIN_MF``,
+    d_model <= ``_GATED_MAX_D``)."""
+    global gated_calls
+    wi, wo = lin_in.weight, lin_out.weight
+    if (act in ("gelu_new", "gelu_fast") and _enabled() and x.dtype == torch.bfloat16 and _ext.use_native(x)
+            and torch.is_grad_enabled() and lin_in.bias is None and lin_out.bias is None
+            and _fusable(wi) and _fusable(wo)):
+        C = _ext.native()
+        x2 = x.reshape(-1, x.shape[-1])
+        Fd = wo.shape[1]
+        if (tuple(wi.shape) == (2 * Fd, x2.shape[1]) and tuple(wo.shape) == (x2.shape[1], Fd) and Fd % 256 == 0
+                and x2.shape[0] % 256 == 0 and 2 * x2.shape[0] * Fd < 2**32 and x2.shape[0] * Fd >= _GATED_MIN_MF
+                and x2.shape[1] <= _GATED_MAX_D
+                and C.gemm_fused_supported(x2, wi, False) and C.gemm_fused_supported(x2, wo, True)):
+            gated_calls += 1
+            return _FusedGatedFFNFn.apply(x, wi.detach(), wo.detach(), p, seed, (wi, wo))
+    return lin_out(act_dropout(lin_in(x), act, p, seed, gated=True))
 
 
 def ffn(x: torch.Tensor, lin_in, lin_out, act: str, p: float = 0.0, seed: int = 0) -> torch.Tensor:

@@ -457,6 +457,68 @@ def test_gemm_relu_bit_mask(variant, M, d, F_):
         C.gemm_fused(dy, wo, True, 7, None, None, None, p, 11, 4, mask)  # mask needs the ping-pong kernel
 
 
+def _geglu_ref(gate, up, seed, p):
+    """fp32 h = dropout(gelu_tanh(gate) * up) and the two factors the gated forward epilogue stores."""
+    from distributed_llms_example_amd.ops.rng import keep_mask
+    s = (keep_mask(seed, p, gate.shape, gate.device).float() / (1.0 - p)) if p > 0 else torch.ones_like(gate)
+    g = gate.detach().float().clone().requires_grad_(True)
+    a = activations._act_ref(g, "gelu_new")
+    (da,) = torch.autograd.grad(a.sum(), g)
+    a = a.detach()
+    return a * up * s, da * up * s, a * s
+
+
+@pytest.mark.parametrize("M,d,F_", [(512, 768, 1024), (768, 512, 1280), (2048, 2048, 5120), (4096, 1024, 4096)])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_gemm_geglu_forward(M, d, F_, p):
+    """Gated-GELU input GEMM (epi 8): one GEMM over the stacked [wi_0; wi_1] whose epilogue pairs gate and up columns
+    in registers (4096 x 4096: 512 tiles, the persistent launch); h, G1 = s·gelu'(gate)·up, G2 = s·gelu(gate) vs fp32 torch (same counter-hash dropout mask as
+    csrc/act.hip's gated path)."""
+    torch.manual_seed(6)
+    C = _ext.native()
+    x = torch.randn(M, d, device=DEV).to(torch.bfloat16)
+    wi = (torch.randn(2 * F_, d, device=DEV) * d ** -0.5).to(torch.bfloat16)
+    h, g1, g2 = C.gemm_geglu(x, wi, p, 21)
+    u = x.float() @ wi.float().t()
+    rh, r1, r2 = _geglu_ref(u[:, :F_], u[:, F_:], 21, p)
+    for name, got, ref in (("h", h, rh), ("G1", g1, r1), ("G2", g2, r2)):
+        assert _rel(got, ref) < 1e-2, (name, _rel(got, ref))
+        _close(got, ref, 2e-2, 2e-2, f"geglu {name}")
+    if p > 0:  # the unfused path (hipBLASLt + csrc/act.hip gated kernel) drops exactly the same elements
+        from distributed_llms_example_amd.ops.rng import keep_mask
+        dropped = ~keep_mask(21, p, (M, F_), x.device)
+        h_unf = activations.act_dropout(x @ wi.t(), "gelu_new", p, 21, gated=True)
+        assert bool((h[dropped] == 0).all()) and bool((h_unf[dropped] == 0).all())
+        assert _rel(h_unf, h) < 1e-2
+
+
+@pytest.mark.parametrize("M,d,F_", [(512, 768, 1024), (768, 512, 1280), (8192, 1024, 4096)])
+def test_gemm_geglu_backward(M, d, F_):
+    """Gated backward GEMM (epi 9): dH = dy · wo (k-major wo [d, F]) -> [dH·G1 | dH·G2] in the stacked [M, 2F] layout,
+    vs fp32 autograd of the gated composite."""
+    torch.manual_seed(7)
+    p = 0.1
+    C = _ext.native()
+    gate = torch.randn(M, F_, device=DEV)
+    up = torch.randn(M, F_, device=DEV)
+    _, r1, r2 = _geglu_ref(gate, up, 33, p)
+    g1, g2 = r1.to(torch.bfloat16), r2.to(torch.bfloat16)
+    dy = torch.randn(M, d, device=DEV).to(torch.bfloat16)
+    wo = (torch.randn(d, F_, device=DEV) * d ** -0.5).to(torch.bfloat16)
+    du = C.gemm_dgeglu(dy, wo, g1, g2)
+    dh = dy.float() @ wo.float()
+    ref = torch.cat([dh * g1.float(), dh * g2.float()], dim=1)
+    assert du.shape == (M, 2 * F_)
+    assert _rel(du, ref) < 1e-2, _rel(du, ref)
+    _close(du, ref, 2e-2, 2e-2, "dgeglu")
+    # end to end against autograd of dropout(gelu(gate) * up)
+    gf, uf = gate.detach().clone().requires_grad_(True), up.detach().clone().requires_grad_(True)
+    from distributed_llms_example_amd.ops.rng import keep_mask
+    keep = keep_mask(33, p, (M, F_), gate.device).float() / (1.0 - p)
+    (activations._act_ref(gf, "gelu_new") * uf * keep).backward(dh)
+    assert _rel(du, torch.cat([gf.grad, uf.grad], dim=1)) < 2e-2
+
+
 def test_gemm_fused_rejects_unsupported_shapes():
     C = _ext.native()
     x = torch.randn(300, 768, device=DEV).to(torch.bfloat16)  # tokens not a multiple of 256

@@ -85,7 +85,7 @@ def test_engine_steps_reduce_loss_on_gpu():
     assert _ext.native() is not None
 
 
-@pytest.mark.parametrize("name", ["t5-base", "bart-base"])
+@pytest.mark.parametrize("name", ["t5-base", "bart-base", "flan-t5-base"])
 def test_fused_ffn_matches_unfused_in_engine(name, monkeypatch):
     """TrainEngine (FlatParams: the FFN runs as GEMMs with activation/dropout epilogues, ops/ffn.py) vs the same
     step with DLLM_FUSED_FFN=0 (hipBLASLt + activation kernels): same loss, same flat gradient."""
@@ -95,6 +95,8 @@ def test_fused_ffn_matches_unfused_in_engine(name, monkeypatch):
     from distributed_llms_example_amd.train.engine import TrainEngine
     env = init_distributed()
     cfg = _cfg(name)
+    monkeypatch.setattr(ffn_mod, "_GATED_MIN_MF", 0)  # small shapes: force the fused gated path as well
+    monkeypatch.setattr(ffn_mod, "_GATED_MAX_D", 1 << 30)
     torch.manual_seed(0)
     sd = build_model(cfg).state_dict()
     b = _batch(cfg, B=4, S=256, T=64)  # 1024 / 256 tokens: the fused kernel's shapes
@@ -105,10 +107,11 @@ def test_fused_ffn_matches_unfused_in_engine(name, monkeypatch):
         m.load_state_dict(sd)
         eng = TrainEngine(m, env, lr=1e-4, dtype=torch.bfloat16)
         eng.train()
-        before = ffn_mod.fused_calls
+        counter = "gated_calls" if cfg.is_gated else "fused_calls"  # flan: gated-GELU GEMM epilogues 8 / 9
+        before = getattr(ffn_mod, counter)
         manual_seed(5)
         loss = eng.forward_backward(b)
-        used = ffn_mod.fused_calls - before
+        used = getattr(ffn_mod, counter) - before
         res.append((float(loss), eng.flat.grad_buf.float().clone(), used))
     (l0, g0, n0), (l1, g1, n1) = res
     assert n0 == 0 and n1 == cfg.num_layers + cfg.num_decoder_layers, (n0, n1)
