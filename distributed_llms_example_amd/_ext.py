@@ -8,7 +8,9 @@ reference implementations (used as numerics oracles in tests and on CPU).
 from __future__ import annotations
 
 import importlib
+import importlib.util
 import os
+import sys
 
 import torch
 
@@ -21,8 +23,16 @@ def _load():
     if _C is not None or _err is not None:
         return _C
     try:
-        _C = importlib.import_module("distributed_llms_example_amd._C")
+        path = os.environ.get("DLLM_NATIVE_SO")  # an alternative build of _C (tools/asan_host.py: host ASAN/UBSan)
+        if path:
+            spec = importlib.util.spec_from_file_location("distributed_llms_example_amd._C", path)
+            _C = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(_C)
+            sys.modules["distributed_llms_example_amd._C"] = _C
+        else:
+            _C = importlib.import_module("distributed_llms_example_amd._C")
     except Exception as e:  # pragma: no cover - depends on build state
+        _C = None
         _err = e
     return _C
 
