@@ -34,6 +34,9 @@ def base_parser(description: str, defaults: dict | None = None) -> argparse.Argu
     g.add_argument("--ignore-pad-labels", action="store_true", help="mask pad tokens out of the loss")
     g.add_argument("--precision", choices=["bf16", "fp32"], default=None, help="default: bf16 on GPU, fp32 on CPU")
     g.add_argument("--grad-accum", type=int, default=None)
+    g.add_argument("--coalesce-grad-accum", type=str, default="auto",
+                   help="run gradient-accumulation micro-batches as fewer larger passes: 'auto' (as many as the "
+                        "first step's measured activation memory allows in 60%% of HBM), N (max samples per pass), 0 off")
     g.add_argument("--learning-rate", type=float, default=5e-5)
     g.add_argument("--max-steps", type=int, default=-1)
     g.add_argument("--bucket-mb", type=float, default=None, help="gradient all-reduce bucket size (MiB)")

@@ -77,6 +77,14 @@ class TrainingArguments:
     context_parallel_size: int = 1  # shard the encoder sequence over groups of this many consecutive ranks
     resume_from_checkpoint: str | None = None
     nan_guard: bool = True  # raise when the (logged, already synchronised) mean loss is NaN/Inf
+    # Run an optimizer step's gradient-accumulation micro-batches as fewer, larger forward/backward passes (same
+    # samples, same token-count normalisation, same single optimizer step).  The reference accumulates 16 micro-batches
+    # of 8 because its GPUs lack memory; a 288 GB MI355X holds the whole group, and one pass of 128 runs ~2x the
+    # samples/s of 16 launch-bound passes of 8 (profiles/r2_entry_points.md).  "auto": as many micro-batches per pass
+    # as the first step's measured activation memory allows within coalesce_memory_fraction of the device (GPU only);
+    # an int caps the samples per pass (0 / 1: off).  env DLLM_COALESCE_GA overrides.
+    coalesce_grad_accum: str | int = "auto"
+    coalesce_memory_fraction: float = 0.6
     report_to: list = field(default_factory=list)
 
     def __post_init__(self):
@@ -142,6 +150,49 @@ class Trainer:
                                            num_workers=self.args.dataloader_num_workers,
                                            pin_memory=self.env.device.type == "cuda"), sampler
 
+    def _coalesce_cap(self) -> int | None:
+        """Max samples per forward/backward pass when coalescing micro-batches, None = off, -1 = decide after step 1."""
+        v = os.environ.get("DLLM_COALESCE_GA", self.args.coalesce_grad_accum)
+        if self.cp_group is not None or self.args.gradient_accumulation_steps <= 1:
+            return None
+        if str(v) == "auto":
+            return -1 if self.env.device.type == "cuda" else None
+        v = int(v)
+        return v if v > 1 else None
+
+    def _auto_cap(self, base_bytes: int, peak_bytes: int) -> int | None:
+        """Samples per pass from the first step: peak - base = one micro-batch's activations (+ transient buffers)."""
+        total = torch.cuda.get_device_properties(self.env.device).total_memory
+        act = max(1, peak_bytes - base_bytes)
+        k = int((self.args.coalesce_memory_fraction * total - base_bytes) // act)
+        k = min(k, self.args.gradient_accumulation_steps)
+        if self.dp_world > 1:  # every rank must make the same choice (same number of passes, same collectives)
+            t = torch.tensor([k], device=self.env.device)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            k = int(t)
+        logger.info(f"gradient accumulation: {k} micro-batches per forward/backward pass "
+                    f"(activations ~{act / 2**30:.1f} GiB per micro-batch, base {base_bytes / 2**30:.1f} GiB)")
+        return k * self.args.per_device_train_batch_size if k > 1 else None
+
+    @staticmethod
+    def _merge(group, pad_id: int):
+        """Concatenate micro-batches along the batch dim, padding sequence dims to the group max (input / decoder ids
+        with the pad token, masks with 0, labels with -100 — what the collator would have produced for one batch)."""
+        if len(group) == 1:
+            return group[0]
+        fill = {"labels": -100, "attention_mask": 0, "decoder_attention_mask": 0}
+        out, padded = {}, False
+        for k in group[0]:
+            ts = [g[k] for g in group]
+            if ts[0].dim() >= 2 and len({t.shape[1] for t in ts}) > 1:
+                n = max(t.shape[1] for t in ts)
+                ts = [torch.nn.functional.pad(t, (0, n - t.shape[1]), value=fill.get(k, pad_id)) for t in ts]
+                padded = True
+            out[k] = torch.cat(ts, 0)
+        if padded and "labels" in out:  # shift_right(labels) inside the model rebuilds them for the longer labels
+            out.pop("decoder_input_ids", None)
+        return out
+
     def _to_device(self, batch, cp=False):
         nb = self.env.device.type == "cuda"
         out = {k: v.to(self.env.device, non_blocking=nb) for k, v in batch.items() if torch.is_tensor(v)}
@@ -188,6 +239,12 @@ class Trainer:
         total_loss_sum, total_loss_n = 0.0, 0
         last_norm = None
         ga = args.gradient_accumulation_steps
+        cap = self._coalesce_cap()
+        pad_id = getattr(getattr(self.model, "config", None), "pad_token_id", 0) or 0
+        if cap == -1:
+            torch.cuda.synchronize()
+            torch.cuda.reset_peak_memory_stats(env.device)
+            mem_base = torch.cuda.memory_allocated(env.device)
         warm_step = self.state.global_step + min(2, max(0, max_steps - self.state.global_step - 1))
         t_warm = t_last = None
         for epoch in range(start_epoch, epochs):
@@ -208,11 +265,25 @@ class Trainer:
                     dist.all_reduce(num_items)
                     if self.cp_group is not None:  # every CP rank of a DP group counted the same batch
                         num_items = num_items // (self.env.world_size // self.dp_world)
-                for j, b in enumerate(group):
-                    loss = eng.forward_backward(b, sync=j + 1 == len(group), num_items=num_items,
-                                                dp_ranks=self.dp_world)
-                    tr_loss_sum += loss.float()
-                    tr_loss_n += 1
+                passes = [[b] for b in group]
+                if cap is not None and cap > 0:  # coalesced: consecutive micro-batches, <= cap samples per pass
+                    passes, cur, n = [], [], 0
+                    for b in group:
+                        nb = b["labels"].shape[0]
+                        if cur and n + nb > cap:
+                            passes.append(cur)
+                            cur, n = [], 0
+                        cur.append(b)
+                        n += nb
+                    passes.append(cur)
+                for j, pb in enumerate(passes):
+                    loss = eng.forward_backward(self._merge(pb, pad_id), sync=j + 1 == len(passes),
+                                                num_items=num_items, dp_ranks=self.dp_world)
+                    tr_loss_sum += loss.float() * len(pb)  # logged loss: mean over micro-batches, as before
+                    tr_loss_n += len(pb)
+                if cap == -1:  # decide from the first (uncoalesced) step's measured activation memory
+                    torch.cuda.synchronize()
+                    cap = self._auto_cap(mem_base, torch.cuda.max_memory_allocated(env.device))
                 last_norm = eng.step(self.scheduler.get_last_lr()[0])
                 self.scheduler.step()
                 self.state.global_step += 1

@@ -173,6 +173,56 @@ def test_trainer_steps_on_epoch_remainder(tmp_path):
     assert float(t.engine.flat.grad_buf.abs().sum()) == 0.0  # nothing left accumulated
 
 
+def test_trainer_coalesced_grad_accumulation_cpu(tmp_path):
+    """Gradient-accumulation micro-batches run as one padded forward/backward (coalesce_grad_accum) give the same
+    training trajectory as one pass per micro-batch: same samples, same global token normalisation, one step."""
+    from distributed_llms_example_amd.data.dataset import SyntheticSeq2Seq
+    from distributed_llms_example_amd.models import resolve_config
+    from distributed_llms_example_amd.parallel.env import init_distributed
+    from distributed_llms_example_amd.train.trainer import Trainer, TrainingArguments
+    env = init_distributed(cpu=True)
+    ds = SyntheticSeq2Seq(12, 12, 6, 500, seed=2)
+    cfg = resolve_config("t5-tiny").replace(dropout_rate=0.0, attention_dropout=0.0)
+    torch.manual_seed(0)
+    sd = build_model(cfg).state_dict()
+    out = {}
+    for cap in (0, 4, 3):  # off / whole group in one pass / passes of 3 + 1 micro-batches
+        m = build_model(cfg)
+        m.load_state_dict(sd)
+        args = TrainingArguments(output_dir=str(tmp_path / str(cap)), num_train_epochs=1, per_device_train_batch_size=1,
+                                 gradient_accumulation_steps=4, learning_rate=1e-3, logging_steps=1, save_steps=1000,
+                                 bf16=False, seed=3, coalesce_grad_accum=cap)
+        t = Trainer(m, args, train_dataset=ds, data_collator=DataCollatorForSeq2Seq(0, 0), env=env)
+        t.train()
+        assert t.state.global_step == 3
+        out[cap] = (torch.cat([p.detach().flatten() for p in m.parameters()]),
+                    [h["loss"] for h in t.state.log_history if "loss" in h])
+    for cap in (4, 3):
+        torch.testing.assert_close(out[cap][0], out[0][0], atol=2e-5, rtol=1e-4)
+        assert all(abs(a - b) < 1e-3 for a, b in zip(out[cap][1], out[0][1])), (out[cap][1], out[0][1])
+
+
+def test_trainer_merge_pads_like_one_collated_batch():
+    """Coalescing micro-batches of different padded lengths == collating all their samples as one batch."""
+    from distributed_llms_example_amd.train.trainer import Trainer
+    rng = torch.Generator().manual_seed(4)
+    feats = [{"input_ids": torch.randint(3, 99, (int(n),), generator=rng).tolist(),
+              "labels": torch.randint(3, 99, (int(t),), generator=rng).tolist()}
+             for n, t in zip(torch.randint(4, 15, (6,), generator=rng), torch.randint(2, 9, (6,), generator=rng))]
+    col = DataCollatorForSeq2Seq(pad_token_id=1, decoder_start_token_id=2)
+    groups = [col(feats[i:i + 2]) for i in (0, 2, 4)]
+    merged = Trainer._merge(groups, pad_id=1)
+    whole = col(feats)
+    # decoder inputs are left to the model's shift_right of the merged labels (the collator's own rule)
+    assert "decoder_input_ids" not in merged and set(merged) | {"decoder_input_ids"} == set(whole)
+    for k in merged:
+        assert torch.equal(merged[k], whole[k]), k
+    lab = merged["labels"]
+    dec = torch.cat([torch.full_like(lab[:, :1], 2), lab[:, :-1]], 1).masked_fill(
+        torch.cat([torch.zeros_like(lab[:, :1], dtype=torch.bool), lab[:, :-1] == -100], 1), 1)
+    assert torch.equal(dec, whole["decoder_input_ids"])  # what the model's shift_right rebuilds (D10)
+
+
 def test_global_token_normalisation_cpu():
     """num_items over micro-batches with different ignored-token counts == full-batch token mean (fp32, exact)."""
     from distributed_llms_example_amd.parallel.env import init_distributed

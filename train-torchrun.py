@@ -60,7 +60,8 @@ def run(args):
         learning_rate=args.learning_rate, max_steps=args.max_steps, seed=args.seed,
         bf16=None if args.precision is None else args.precision == "bf16",
         ddp_bucket_cap_mb=args.bucket_mb, overlap_comm=not args.no_overlap,
-        context_parallel_size=args.context_parallel)
+        context_parallel_size=args.context_parallel,
+        coalesce_grad_accum=getattr(args, "coalesce_grad_accum", "auto"))
     trainer = Trainer(model=model, args=targs, tokenizer=tok, data_collator=DataCollatorForSeq2Seq.for_model(cfg),
                       train_dataset=train_ds, eval_dataset=eval_ds, callbacks=[PrinterCallback], env=env)
     resume = True if args.resume_from == "latest" else args.resume_from
