@@ -14,3 +14,4 @@ run ours_t5_large_b32 --model t5-large --batch-per-gpu 32 --steps 8 --warmup 3
 run ours_flan_t5_xl_b16 --model flan-t5-xl --batch-per-gpu 16 --steps 5 --warmup 2
 run ours_t5base_b64_ckpt --model t5-base --batch-per-gpu 64 --grad-ckpt --steps 10 --warmup 3
 run ours_flan_xl_long_s4096_b8_ckpt --model flan-t5-xl --batch-per-gpu 8 --src-len 4096 --grad-ckpt --steps 4 --warmup 2
+run ours_flan_xl_long_s4096_b8 --model flan-t5-xl --batch-per-gpu 8 --src-len 4096 --steps 4 --warmup 2  # 124 GB peak: no recompute needed on 288 GB
