@@ -10,7 +10,9 @@ run() {
   cut -c1-160 gpurun_out/configs/$name.json
 }
 run ours_bart_large_b32 --model bart-large --batch-per-gpu 32 --steps 10 --warmup 3
+run ours_bart_large_b256 --model bart-large --batch-per-gpu 256 --steps 5 --warmup 2  # 144 GB peak
 run ours_t5_large_b32 --model t5-large --batch-per-gpu 32 --steps 8 --warmup 3
+run ours_t5_large_b128 --model t5-large --batch-per-gpu 128 --steps 5 --warmup 2  # 132 GB peak
 run ours_flan_t5_xl_b16 --model flan-t5-xl --batch-per-gpu 16 --steps 5 --warmup 2
 run ours_t5base_b64_ckpt --model t5-base --batch-per-gpu 64 --grad-ckpt --steps 10 --warmup 3
 run ours_flan_xl_long_s4096_b8_ckpt --model flan-t5-xl --batch-per-gpu 8 --src-len 4096 --grad-ckpt --steps 4 --warmup 2
