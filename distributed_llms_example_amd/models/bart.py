@@ -16,10 +16,10 @@ import torch
 import torch.nn as nn
 
 from ..ops import activations, attention as attn_ops, norms
-from ..ops.ffn import ffn
+from ..ops.ffn import ffn_res
 from ..ops.cross_entropy import cross_entropy
 from ..ops.embedding import embedding
-from ..ops.linear import Linear, linear, stacked_linear
+from ..ops.linear import Linear, linear, linear_res, stacked_linear
 from ..ops.lm_head import lm_head_loss, use_chunked
 from ..ops.rng import default_rng
 from .blocks import run_block
@@ -46,22 +46,34 @@ class BartAttention(nn.Module):
         B, S, _ = kv_in.shape
         return self.kv_proj(kv_in).view(B, S, 2, self.n_heads, self.head_dim)
 
-    def forward(self, x, kv_in=None, mask=None, causal=False, p=0.0, cache=None, kv=None):
+    def forward(self, x, kv_in=None, mask=None, causal=False, p=0.0, cache=None, kv=None, residual=False):
+        """Attention block output; with ``residual`` also ``x`` for the post-LN residual, its gradient accumulated by
+        the input projection's dgrad GEMM (ops/linear.py linear_res)."""
         B, S, _ = x.shape
+        res = x
         H, D = self.n_heads, self.head_dim
         seed = default_rng().next_seed() if p > 0 else 0
         kw = dict(scale=self.scaling, causal=causal, key_padding_mask=mask, dropout_p=p, seed=seed)
         if self.cross:
-            q = self.q_proj(x).view(B, S, H, D)
+            if residual:
+                q, res = linear_res(x, self.q_proj)
+                q = q.view(B, S, H, D)
+            else:
+                q = self.q_proj(x).view(B, S, H, D)
             o = attn_ops.attention_q_kv(q, kv if kv is not None else self.project_kv(kv_in), **kw)
         else:
-            qkv = self.qkv_proj(x).view(B, S, 3, H, D)
+            if residual:
+                qkv, res = linear_res(x, self.qkv_proj)
+                qkv = qkv.view(B, S, 3, H, D)
+            else:
+                qkv = self.qkv_proj(x).view(B, S, 3, H, D)
             if cache is not None:
                 k, v = cache.append(qkv[:, :, 1], qkv[:, :, 2])
                 o = attn_ops.attention(qkv[:, :, 0], k, v, **kw)
             else:
                 o = attn_ops.attention_qkv(qkv, **kw)
-        return self.out_proj(o.reshape(B, S, H * D))
+        out = self.out_proj(o.reshape(B, S, H * D))
+        return (out, res) if residual else out
 
 
 class BartLayer(nn.Module):
@@ -87,15 +99,18 @@ class BartLayer(nn.Module):
         pact = cfg.activation_dropout if tr else 0.0
         eps = cfg.layer_norm_epsilon
         rng = default_rng()
-        a = self.self_attn(h, mask=None if self.is_decoder else mask, causal=self.is_decoder, p=pa, cache=cache)
+        # post-LN blocks: each block's input is both the sublayer input and the residual; the sublayers hand the
+        # residual back from their input projection so its gradient is summed inside that projection's dgrad GEMM
+        a, h = self.self_attn(h, mask=None if self.is_decoder else mask, causal=self.is_decoder, p=pa, cache=cache,
+                              residual=True)
         h = norms.add_dropout_layer_norm(h, a, self.self_attn_layer_norm.weight, self.self_attn_layer_norm.bias, eps,
                                          p, rng.next_seed() if p > 0 else 0)
         if self.is_decoder:
-            c = self.encoder_attn(h, kv_in=enc_out, mask=enc_mask, p=pa, kv=cross_kv)
+            c, h = self.encoder_attn(h, kv_in=enc_out, mask=enc_mask, p=pa, kv=cross_kv, residual=True)
             h = norms.add_dropout_layer_norm(h, c, self.encoder_attn_layer_norm.weight,
                                              self.encoder_attn_layer_norm.bias, eps, p,
                                              rng.next_seed() if p > 0 else 0)
-        f = ffn(h, self.fc1, self.fc2, cfg.act, pact, rng.next_seed() if pact > 0 else 0)
+        f, h = ffn_res(h, self.fc1, self.fc2, cfg.act, pact, rng.next_seed() if pact > 0 else 0)
         return norms.add_dropout_layer_norm(h, f, self.final_layer_norm.weight, self.final_layer_norm.bias, eps, p,
                                             rng.next_seed() if p > 0 else 0)
 

@@ -39,7 +39,7 @@ import torch.nn.functional as F
 from .. import _ext
 from .activations import act_dropout
 from .gemm import bias_grad_accumulate, wgrad_accumulate
-from .linear import _fire, _fusable, _gbuf, _use
+from .linear import _RES_GEMM, _fire, _fusable, _gbuf, _use
 
 # activation -> (forward epilogue, backward epilogue) of csrc/gemm_fused.hip
 EPILOGUES = {"relu": (1, 3), "gelu": (2, 4), "gelu_new": (5, 6), "gelu_fast": (5, 6)}
@@ -71,15 +71,16 @@ class _FusedFFNFn(torch.autograd.Function):
             mask = torch.empty(x2.shape[0] * wi.shape[0] // 32, device=x.device, dtype=torch.int32)
         h = C.gemm_fused(x2, wi, False, efwd, bi, None, u, float(p), int(seed), _VARIANT, mask)
         y = F.linear(h, wo, bo)
+        ctx.set_materialize_grads(False)  # the residual alias's gradient is None when the caller does not use it
         ctx.save_for_backward(x2, h, u, mask)
         ctx.params = params
         for q in params:
             _use(q)
         ctx.cfg = (act, float(p), int(seed), shape)
-        return y.view(*shape[:-1], wo.shape[0])
+        return y.view(*shape[:-1], wo.shape[0]), x.view_as(x)
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, dy, dres):
         x2, h, u, mask = ctx.saved_tensors
         Wi, Bi, Wo, Bo = ctx.params
         act, p, seed, shape = ctx.cfg
@@ -100,7 +101,14 @@ class _FusedFFNFn(torch.autograd.Function):
         _fire(Wo)
         if Bo is not None:
             _fire(Bo)
-        dx = torch.matmul(du, Wi.detach()) if ctx.needs_input_grad[0] else None
+        dx = None
+        if ctx.needs_input_grad[0]:  # post-LN residual (ffn_res): its gradient accumulated by this GEMM (beta = 1)
+            if dres is not None and dres.is_contiguous() and dres.dtype == du.dtype and dres.shape == shape:
+                dx = dres.view(-1, shape[-1]).addmm_(du, Wi.detach())
+            else:
+                dx = torch.matmul(du, Wi.detach())
+                if dres is not None:
+                    dx = dx + dres.reshape(dx.shape)
         with torch.no_grad():
             wgrad_accumulate(_gbuf(Wi), du, x2)
             if Bi is not None:
@@ -195,6 +203,12 @@ def gated_ffn(x: torch.Tensor, lin_in, lin_out, act: str, p: float = 0.0, seed: 
 
 def ffn(x: torch.Tensor, lin_in, lin_out, act: str, p: float = 0.0, seed: int = 0) -> torch.Tensor:
     """``lin_out(act_dropout(lin_in(x), act, p, seed))`` (non-gated), fused where possible."""
+    return ffn_res(x, lin_in, lin_out, act, p, seed, residual=False)
+
+
+def ffn_res(x: torch.Tensor, lin_in, lin_out, act: str, p: float = 0.0, seed: int = 0, residual: bool = True):
+    """``ffn(x)`` and, with ``residual``, ``x`` again for the caller's post-LN residual connection: on the fused path
+    that residual's gradient is accumulated by the FFN's input-gradient GEMM instead of an autograd add kernel."""
     global fused_calls
     if (act in EPILOGUES and _enabled() and x.dtype == torch.bfloat16 and _ext.use_native(x)
             and torch.is_grad_enabled()
@@ -203,7 +217,9 @@ def ffn(x: torch.Tensor, lin_in, lin_out, act: str, p: float = 0.0, seed: int = 
         if _fusable_shapes(x2, lin_in.weight, lin_out.weight):
             fused_calls += 1
             bi, bo = lin_in.bias, lin_out.bias
-            return _FusedFFNFn.apply(x, lin_in.weight.detach(), None if bi is None else bi.detach(),
-                                     lin_out.weight.detach(), None if bo is None else bo.detach(), act, p, seed,
-                                     (lin_in.weight, bi, lin_out.weight, bo))
-    return lin_out(act_dropout(lin_in(x), act, p, seed))
+            y, res = _FusedFFNFn.apply(x, lin_in.weight.detach(), None if bi is None else bi.detach(),
+                                       lin_out.weight.detach(), None if bo is None else bo.detach(), act, p, seed,
+                                       (lin_in.weight, bi, lin_out.weight, bo))
+            return (y, res) if residual and _RES_GEMM else (y, x) if residual else y
+    y = lin_out(act_dropout(lin_in(x), act, p, seed))
+    return (y, x) if residual else y

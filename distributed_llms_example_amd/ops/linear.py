@@ -14,6 +14,8 @@ ordinary autograd with identical results.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -82,6 +84,59 @@ class _LinearAccumFn(torch.autograd.Function):
         if bias is not None:
             _fire(bias)
         return dx, None, None, None
+
+
+class _LinearResFn(torch.autograd.Function):
+    """``(x Wᵀ + b, x)``: a linear layer whose input is ALSO the residual of a post-LN block (BART).
+
+    The input's gradient is then ``d_residual + dY W``; through autograd the two halves come back from two consumers
+    and are summed by a separate elementwise kernel (one [tokens, d] read-read-write per block).  Returning the
+    residual as a second output of this op hands ``d_residual`` to this backward, where the input-gradient GEMM
+    accumulates into it in its epilogue (``addmm_``, beta = 1): no add kernel."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, params):
+        ctx.set_materialize_grads(False)
+        ctx.save_for_backward(x)
+        ctx.weight, ctx.bias = params
+        _use(params[0])
+        _use(params[1])
+        return F.linear(x, weight, bias), x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, dy, dres):
+        (x,) = ctx.saved_tensors
+        w, bias = ctx.weight, ctx.bias
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        dx = None
+        if ctx.needs_input_grad[0]:
+            if (dres is not None and dres.is_contiguous() and dres.dtype == dy.dtype and dres.shape == x.shape):
+                dx = dres.view(-1, dres.shape[-1]).addmm_(dy2, w.detach()).view(x.shape)
+            else:
+                dx = torch.matmul(dy, w.detach())
+                if dres is not None:
+                    dx = dx + dres
+        x2 = x.reshape(-1, x.shape[-1])
+        with torch.no_grad():
+            wgrad_accumulate(_gbuf(w), dy2, x2)
+            if bias is not None:
+                bias_grad_accumulate(_gbuf(bias), dy2)
+        _fire(w)
+        if bias is not None:
+            _fire(bias)
+        return dx, None, None, None
+
+
+_RES_GEMM = os.environ.get("DLLM_RESID_GEMM", "1") != "0"  # 0: residual gradient summed by autograd (A/B)
+
+
+def linear_res(x: torch.Tensor, mod) -> tuple[torch.Tensor, torch.Tensor]:
+    """``(mod(x), residual)`` where ``residual`` is ``x`` for the caller's residual connection; on the fused path the
+    residual's gradient is accumulated by this linear's input-gradient GEMM (``_LinearResFn``)."""
+    w, b = mod.weight, mod.bias
+    if _RES_GEMM and torch.is_grad_enabled() and x.requires_grad and _fusable(w) and _fusable(b):
+        return _LinearResFn.apply(x, w.detach(), None if b is None else b.detach(), (w, b))
+    return mod(x), x
 
 
 def _fusable(p: torch.Tensor | None) -> bool:
