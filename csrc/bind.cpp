@@ -553,7 +553,7 @@ bool gemm_fused_supported(const Tensor& a, const Tensor& b, bool b_kmajor) {
 
 Tensor gemm_fused(const Tensor& a, const Tensor& b, bool b_kmajor, int64_t epi, const optional<Tensor>& bias,
                   const optional<Tensor>& aux, const optional<Tensor>& aux_out, double p, int64_t seed,
-                  int64_t variant, const optional<Tensor>& mask) {
+                  int64_t variant, const optional<Tensor>& mask, const optional<Tensor>& colsum) {
   TORCH_CHECK(gemm_fused_supported(a, b, b_kmajor),
               "gemm_fused: need bf16 GPU a [M,K], b [N,K] (or [K,N] k-major), unit inner stride, 16-B aligned rows, "
               "M and N multiples of 256, K % 64 == 0, M*N < 2^32");
@@ -625,6 +625,14 @@ Tensor gemm_fused(const Tensor& a, const Tensor& b, bool b_kmajor, int64_t epi, 
                     reinterpret_cast<uintptr_t>(mask->data_ptr()) % 16 == 0,
                 "gemm_fused: mask must be a contiguous 16-B aligned int32 GPU tensor of M*N/32 words");
     P.mask = reinterpret_cast<uint32_t*>(mask->data_ptr());
+  }
+  if (colsum.has_value() && colsum->defined()) {  // per-128-row column sums of the output (GELU backward: bias grad)
+    TORCH_CHECK(epi == 4 || epi == 6, "gemm_fused: colsum goes with the GELU backward epilogues (4 / 6)");
+    TORCH_CHECK(v == 8 || v == 9, "gemm_fused: colsum needs the ping-pong kernel (variant 8 / 9)");
+    TORCH_CHECK(colsum->is_cuda() && colsum->device() == a.device() && colsum->scalar_type() == at::kFloat &&
+                    colsum->is_contiguous() && colsum->dim() == 2 && colsum->size(0) == M / 128 && colsum->size(1) == N,
+                "gemm_fused: colsum must be a contiguous fp32 [M / 128, N] GPU tensor");
+    P.colsum = colsum->data_ptr<float>();
   }
   check_rc(dllm_gemm_fused(&P, b_kmajor ? 1 : 0, v, stream()), "gemm_fused");
   return out;
@@ -772,7 +780,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_fused", &gemm_fused, "epi(a . b) with a fused bias / activation / dropout (or their backward) epilogue",
         py::arg("a"), py::arg("b"), py::arg("b_kmajor"), py::arg("epi"), py::arg("bias") = py::none(),
         py::arg("aux") = py::none(), py::arg("aux_out") = py::none(), py::arg("p") = 0.0, py::arg("seed") = 0,
-        py::arg("variant") = -1, py::arg("mask") = py::none());
+        py::arg("variant") = -1, py::arg("mask") = py::none(), py::arg("colsum") = py::none());
   m.def("gemm_fused_supported", &gemm_fused_supported);
   m.def("gemm_geglu", &gemm_geglu, "gated-GELU FFN input GEMM: (h, G1, G2) from x and the stacked [wi_0; wi_1]");
   m.def("gemm_dgeglu", &gemm_dgeglu, "gated-GELU FFN backward GEMM: d(stacked wi output) from dy, wo, G1, G2");

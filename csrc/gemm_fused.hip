@@ -755,6 +755,10 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(GemmFusedParams P) {
         }
     } else {
       u32x4 bits = {0u, 0u, 0u, 0u};
+      // GELU backward: column sums of the stored dU over the wave's 128 rows — the fc1 bias gradient — from registers
+      // (otherwise a separate pass re-reads all of dU, [tokens, d_ff] bf16)
+      constexpr bool CS = EPI == EPI_DGELU || EPI == EPI_DGELU_TANH;
+      f32x4 cs[4] = {};
 #pragma unroll
       for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -764,8 +768,29 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(GemmFusedParams P) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) bits[i >> 1] |= (v[r] != 0.f ? 1u : 0u) << ((i & 1) * 16 + 4 * j + r);
           }
+          if constexpr (CS) cs[j] += v;
         }
       if (EPI == EPI_RELU && P.mask) *reinterpret_cast<u32x4*>(P.mask + mask_word(tm0, tn0) + tid * 4) = bits;
+      if constexpr (CS) {
+        if (P.colsum) {  // the 16 lanes of a lane group hold the same 16 columns on 16 different rows
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              float x = cs[j][r];
+              x += __shfl_xor(x, 1);
+              x += __shfl_xor(x, 2);
+              x += __shfl_xor(x, 4);
+              x += __shfl_xor(x, 8);
+              cs[j][r] = x;
+            }
+          if ((ln & 15) == 0) {
+            float* cp = P.colsum + (long)(tm0 / 128 + wm) * P.N + ncol;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) *reinterpret_cast<f32x4*>(cp + 16 * j) = cs[j];
+          }
+        }
+      }
     }
   };
 

@@ -37,4 +37,5 @@ struct GemmFusedParams {
   uint32_t seed, thr;
   int grp;     // tile order (gemm_pp_kernel): groups of grp 256-row blocks, column-major inside a group; 0 = row-major
   uint32_t* mask;  // ReLU derivative bits (ping-pong kernel): written by epi 1 when non-null, read by epi 7; M*N/32 words
+  float* colsum;   // optional (ping-pong kernel, epi 4 / 6): [M / 128][N] per-128-row column sums of the output C
 };

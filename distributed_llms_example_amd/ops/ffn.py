@@ -45,6 +45,7 @@ from .linear import _RES_GEMM, _fire, _fusable, _gbuf, _use
 EPILOGUES = {"relu": (1, 3), "gelu": (2, 4), "gelu_new": (5, 6), "gelu_fast": (5, 6)}
 _VARIANT = int(os.environ.get("DLLM_GEMM_FUSED_VARIANT", "-1"))  # -1: picked by K in csrc/bind.cpp
 _RELU_MASK = os.environ.get("DLLM_RELU_MASK", "1") != "0"  # 0: the backward re-reads H (A/B runs)
+_COLSUM = os.environ.get("DLLM_FFN_BIAS_COLSUM", "1") != "0"  # 0: wi bias gradient by a separate column-sum pass
 fused_calls = 0  # number of FFN forwards that took the fused path (tests assert the kernel really ran)
 
 
@@ -90,10 +91,14 @@ class _FusedFFNFn(torch.autograd.Function):
         dy2 = dy.reshape(-1, dy.shape[-1])
         if not C.gemm_fused_supported(dy2, wo, True):
             dy2 = dy2.contiguous()
+        # GELU: the wi bias gradient comes out of the same GEMM's epilogue as per-128-row column sums of dU
+        bsum = None
+        if Bi is not None and ebwd in (4, 6) and _COLSUM and _pingpong(C, wo.shape[0]):
+            bsum = torch.empty(dy2.shape[0] // 128, wo.shape[1], device=dy2.device, dtype=torch.float32)
         if mask is not None:  # d-relu from the bit mask
             du = C.gemm_fused(dy2, wo, True, 7, None, None, None, p, seed, _VARIANT, mask)
         else:
-            du = C.gemm_fused(dy2, wo, True, ebwd, None, h if ebwd == 3 else u, None, p, seed, _VARIANT)
+            du = C.gemm_fused(dy2, wo, True, ebwd, None, h if ebwd == 3 else u, None, p, seed, _VARIANT, None, bsum)
         with torch.no_grad():
             wgrad_accumulate(_gbuf(Wo), dy2, h)
             if Bo is not None:
@@ -111,7 +116,10 @@ class _FusedFFNFn(torch.autograd.Function):
                     dx = dx + dres.reshape(dx.shape)
         with torch.no_grad():
             wgrad_accumulate(_gbuf(Wi), du, x2)
-            if Bi is not None:
+            if bsum is not None:
+                gb = _gbuf(Bi)
+                gb.add_(bsum.sum(0).to(gb.dtype))
+            elif Bi is not None:
                 bias_grad_accumulate(_gbuf(Bi), du)
         _fire(Wi)
         if Bi is not None:

@@ -519,6 +519,25 @@ def test_gemm_geglu_backward(M, d, F_):
     assert _rel(du, torch.cat([gf.grad, uf.grad], dim=1)) < 2e-2
 
 
+@pytest.mark.parametrize("variant", [8, 9])
+@pytest.mark.parametrize("act,M,d,F_", [("gelu", 768, 512, 1024), ("gelu_new", 8448, 1024, 4096)])
+def test_gemm_fused_gelu_bwd_colsum(variant, act, M, d, F_):
+    """GELU backward GEMM epilogue also writes per-128-row column sums of dU (the fc1 bias gradient) vs fp32 sums."""
+    torch.manual_seed(9)
+    C = _ext.native()
+    dy = torch.randn(M, d, device=DEV).to(torch.bfloat16)
+    wo = (torch.randn(d, F_, device=DEV) * d ** -0.5).to(torch.bfloat16)
+    u = torch.randn(M, F_, device=DEV).to(torch.bfloat16)
+    aux = _act_grad(u, act, 9, 0.1).to(torch.bfloat16)
+    part = torch.full((M // 128, F_), float("nan"), device=DEV)
+    du = C.gemm_fused(dy, wo, True, _EPI_BWD[act], None, aux, None, 0.1, 9, variant, None, part)
+    du0 = C.gemm_fused(dy, wo, True, _EPI_BWD[act], None, aux, None, 0.1, 9, variant)
+    torch.testing.assert_close(du, du0, rtol=0, atol=0)
+    ref = du.float().view(M // 128, 128, F_).sum(1)  # sums of the stored (bf16-rounded) values: fp32 accumulators
+    assert _rel(part, ref) < 1e-2, _rel(part, ref)
+    assert _rel(part.sum(0), du.float().sum(0)) < 1e-2
+
+
 def test_gemm_fused_rejects_unsupported_shapes():
     C = _ext.native()
     x = torch.randn(300, 768, device=DEV).to(torch.bfloat16)  # tokens not a multiple of 256
