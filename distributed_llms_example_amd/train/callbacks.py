@@ -21,6 +21,7 @@ class TrainerState:
     best_metric: float | None = None
     total_flos: float = 0.0
     is_world_process_zero: bool = True
+    coalesce_cap: int | None = None  # samples per pass chosen for coalesced gradient accumulation (0 = off); resume reuses it
 
     def save_to_json(self, path):
         with open(path, "w") as f:

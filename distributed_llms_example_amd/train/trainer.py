@@ -226,6 +226,7 @@ class Trainer:
                 info = load_checkpoint(path, self.model, eng.optimizer, self.scheduler, rank=env.rank)
                 ts = info.get("trainer_state", {})
                 self.state.global_step = ts.get("global_step", 0)
+                self.state.coalesce_cap = ts.get("coalesce_cap")
                 self.state.log_history = ts.get("log_history", [])
                 start_epoch = self.state.global_step // steps_per_epoch
                 skip = (self.state.global_step % steps_per_epoch) * args.gradient_accumulation_steps
@@ -240,6 +241,8 @@ class Trainer:
         last_norm = None
         ga = args.gradient_accumulation_steps
         cap = self._coalesce_cap()
+        if cap == -1 and self.state.coalesce_cap is not None:  # resumed: the original run's choice (same RNG stream)
+            cap = self.state.coalesce_cap or None
         pad_id = getattr(getattr(self.model, "config", None), "pad_token_id", 0) or 0
         if cap == -1:
             torch.cuda.synchronize()
@@ -284,6 +287,7 @@ class Trainer:
                 if cap == -1:  # decide from the first (uncoalesced) step's measured activation memory
                     torch.cuda.synchronize()
                     cap = self._auto_cap(mem_base, torch.cuda.max_memory_allocated(env.device))
+                    self.state.coalesce_cap = cap or 0
                 last_norm = eng.step(self.scheduler.get_last_lr()[0])
                 self.scheduler.step()
                 self.state.global_step += 1
