@@ -148,3 +148,31 @@ def test_bart_residual_grad_in_dgrad_gemm(monkeypatch):
     cos = torch.nn.functional.cosine_similarity(g0, g1, dim=0).item()
     assert cos > 0.9999, cos
     assert ((g0 - g1).norm() / g0.norm()).item() < 1e-2
+
+
+def test_trainer_coalesced_grad_accumulation_on_gpu(tmp_path):
+    """Trainer on the GPU with coalesce_grad_accum="auto": step 1 runs micro-batch by micro-batch and measures the
+    activation memory, later steps run the whole GA group as one pass; same trajectory as the uncoalesced run (no
+    dropout), and the choice is recorded for resume."""
+    from distributed_llms_example_amd.data.collator import DataCollatorForSeq2Seq
+    from distributed_llms_example_amd.data.dataset import SyntheticSeq2Seq
+    from distributed_llms_example_amd.parallel.env import init_distributed
+    from distributed_llms_example_amd.train.trainer import Trainer, TrainingArguments
+    env = init_distributed()
+    cfg = _cfg("t5-base").replace(dropout_rate=0.0, attention_dropout=0.0)
+    ds = SyntheticSeq2Seq(24, 256, 64, cfg.vocab_size, seed=3)
+    torch.manual_seed(0)
+    sd = build_model(cfg).state_dict()
+    out = {}
+    for mode in ("0", "auto"):
+        m = build_model(cfg)
+        m.load_state_dict(sd)
+        args = TrainingArguments(output_dir=str(tmp_path / mode), num_train_epochs=1, per_device_train_batch_size=2,
+                                 gradient_accumulation_steps=4, learning_rate=1e-4, logging_steps=1, save_steps=1000,
+                                 seed=3, coalesce_grad_accum=mode)
+        t = Trainer(m, args, train_dataset=ds, data_collator=DataCollatorForSeq2Seq(0, 0), env=env)
+        t.train()
+        out[mode] = (torch.cat([p.detach().float().flatten() for p in m.parameters()]), t.state.coalesce_cap)
+    assert out["auto"][1] == 8, out["auto"][1]  # 4 micro-batches of 2 per pass
+    a, b = out["auto"][0], out["0"][0]
+    assert torch.nn.functional.cosine_similarity(a, b, dim=0).item() > 0.99999
