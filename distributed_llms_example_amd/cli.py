@@ -58,6 +58,21 @@ def base_parser(description: str, defaults: dict | None = None) -> argparse.Argu
     return ap
 
 
+# Evaluation / generation batch when --eval-batch-size is not given.  Beam-search generation is launch-bound at small
+# batches (t5-base, 818 samples, num_beams=2, one MI355X: 107 samples/s at batch 64, 195 at 128, 299 at 256, 480 with
+# all 818 at once; tools/eval_bench.py, profiles/r2_eval_batch.txt), and a 288 GB GPU holds the caches of hundreds of
+# sequences, so GPU runs evaluate in batches of at least this many samples (the reference evaluates with its training
+# batch size, or 1 in train-accelerator).  Results are the same per sample.
+GPU_EVAL_BATCH = int(os.environ.get("DLLM_EVAL_BATCH", "256"))
+
+
+def eval_batch_size(args, device) -> int:
+    if getattr(args, "eval_batch_size", None):
+        return args.eval_batch_size
+    bs = args.batch_size or 1
+    return max(bs, GPU_EVAL_BATCH) if getattr(device, "type", str(device)) == "cuda" else bs
+
+
 def apply_overrides(cfg, spec: str | None):
     if not spec:
         return cfg

@@ -24,7 +24,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 from torch.utils.data import DataLoader  # noqa: E402
 
-from distributed_llms_example_amd.cli import base_parser, build_data, model_config  # noqa: E402
+from distributed_llms_example_amd.cli import base_parser, build_data, eval_batch_size, model_config  # noqa: E402
 from distributed_llms_example_amd.data.collator import DataCollatorForSeq2Seq  # noqa: E402
 from distributed_llms_example_amd.models import build_model, from_pretrained  # noqa: E402
 from distributed_llms_example_amd.utils import faults  # noqa: E402
@@ -64,7 +64,7 @@ class ModelTrainer:
         a, acc = self.args, self.accelerator
         collator = DataCollatorForSeq2Seq.for_model(self.cfg)
         train_dl = DataLoader(train_ds, shuffle=True, collate_fn=collator, batch_size=a.batch_size)
-        eval_dl = DataLoader(eval_ds, collate_fn=collator, batch_size=a.eval_batch_size or a.batch_size)
+        eval_dl = DataLoader(eval_ds, collate_fn=collator, batch_size=eval_batch_size(a, self.accelerator.device))
         no_decay = ["bias", "LayerNorm.weight"]
         groups = [
             {"params": [p for n, p in self.model.named_parameters() if not any(nd in n for nd in no_decay)],

@@ -15,6 +15,7 @@ call instead of ~500), overlapped with backward by default (``--no-overlap``: af
 eval set is sharded and gathered instead of decoded redundantly on every rank — the aggregated
 ROUGE is the same; loss is synced to the host only at log steps.
 """
+import argparse
 import json
 import math
 import os
@@ -27,7 +28,7 @@ os.environ.setdefault("TRANSFORMERS_NO_ADVISORY_WARNINGS", "true")
 import torch  # noqa: E402
 import torch.multiprocessing as mp  # noqa: E402
 
-from distributed_llms_example_amd.cli import base_parser  # noqa: E402
+from distributed_llms_example_amd.cli import base_parser, eval_batch_size  # noqa: E402
 from distributed_llms_example_amd.platform import valohai  # noqa: E402
 
 
@@ -87,7 +88,8 @@ def run(env, args):
     part = DataPartitioner(train_ds, [1.0 / world for _ in range(world)], seed=1234).use(env.rank)
     bsz = args.batch_size if args.batch_size else math.ceil(2 / float(world))
     train_dl = DataLoader(part, batch_size=bsz, shuffle=True, collate_fn=collator)
-    ev_sampler = ShardedBatchSampler(len(eval_ds), args.eval_batch_size or bsz, world, env.rank)
+    ev_sampler = ShardedBatchSampler(len(eval_ds), eval_batch_size(argparse.Namespace(**{**vars(args), "batch_size": bsz}), env.device),
+                                     world, env.rank)
     eval_dl = DataLoader(eval_ds, batch_sampler=ev_sampler, collate_fn=collator)
     max_steps = args.num_epochs * len(train_dl)
     if args.max_steps > 0:

@@ -20,7 +20,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 os.environ.setdefault("TRANSFORMERS_NO_ADVISORY_WARNINGS", "true")
 
-from distributed_llms_example_amd.cli import base_parser, build_data, model_config  # noqa: E402
+from distributed_llms_example_amd.cli import base_parser, build_data, eval_batch_size, model_config  # noqa: E402
 from distributed_llms_example_amd.data.collator import DataCollatorForSeq2Seq  # noqa: E402
 from distributed_llms_example_amd.models import build_model, from_pretrained  # noqa: E402
 from distributed_llms_example_amd.parallel.env import init_distributed  # noqa: E402
@@ -54,7 +54,7 @@ def run(args):
         model.gradient_checkpointing_enable()
     targs = TrainingArguments(
         output_dir=output_dir, num_train_epochs=args.num_epochs, warmup_steps=args.warmup_steps,
-        per_device_train_batch_size=args.batch_size, per_device_eval_batch_size=args.eval_batch_size or args.batch_size,
+        per_device_train_batch_size=args.batch_size, per_device_eval_batch_size=eval_batch_size(args, env.device),
         weight_decay=0.01, logging_steps=10, evaluation_strategy="steps", eval_steps=args.evaluation_steps,
         save_steps=args.save_steps or 1e6, gradient_accumulation_steps=args.grad_accum or 16, ddp_find_unused_parameters=False,
         learning_rate=args.learning_rate, max_steps=args.max_steps, seed=args.seed,
