@@ -110,10 +110,17 @@ DLLM_DEVICE bf16x8v ld_tr_operand(const uint16_t* T, int kb0, int t, int r) {
 }
 
 // attention dropout (ops/rng.py attention_keep_mask): per query row rh = mix32(seed, row); per key pair kp = key >> 1:
-// h = ((rh + kp * HG) & 0xFFFFFF) * C24 (v_mul_u32_u24: full rate, unlike the quarter-rate v_mul_lo_u32);
-// y = h ^ (h >> 16); the even key keeps iff (y & 0xFFFF) >= thr16, the odd key iff (h >> 16) >= thr16.
-constexpr uint32_t C24 = 0x9E3779u;
-DLLM_DEVICE uint32_t attn_pair_hash(uint32_t x) { return __umul24(x, C24); }
+// g = ((rh + kp * HG) & 0xFFFFFF) * C24, h = ((g ^ (g >> 15)) & 0xFFFFFF) * C24B (two v_mul_u32_u24: full rate, unlike
+// the quarter-rate v_mul_lo_u32); y = h ^ (h >> 16); the even key keeps iff (y & 0xFFFF) >= thr16, the odd key iff
+// (h >> 16) >= thr16.  The second round matters: g alone is linear in kp (a Weyl sequence times a constant), so at
+// p = 0.1 two odd keys two apart were NEVER both dropped and per-row drop counts had 1/8 of the binomial variance;
+// with the xorshift + multiply every lag-1/2/3/16 joint drop rate and the row-count variance match independent
+// Bernoulli draws (tests/test_training_cpu.py test_attention_dropout_hash_statistics).
+constexpr uint32_t C24 = 0x9E3779u, C24B = 0x85EBCBu;
+DLLM_DEVICE uint32_t attn_pair_hash(uint32_t x) {
+  const uint32_t g = __umul24(x, C24);
+  return __umul24(g ^ (g >> 15), C24B);
+}
 
 // Two key pairs (A, then B) of the forward's dropout: the four keep compares write SGPR-pair lane masks, then per key
 // one v_cndmask zeroes P and one v_addc_co_u32 shifts the keep bit into the word (word = 2 word + keep), odd key first
@@ -393,7 +400,7 @@ __global__ __launch_bounds__(256, FNB == 3 ? 2 : 3) void attn_fwd_kernel(AttnPar
     } else if (DROP) {
       // keep decisions -> P (the 1/(1-p) scale is applied once to O at the end) and one bit word per lane and
       // tile for the backward kernels (bit i <-> s0[i], bit 16+i <-> s1[i]): they never re-hash.  Per key pair
-      // one add, one full-rate 24-bit multiply and a shift-xor (attn_pair_hash); each compare's lane mask drives
+      // one add, two full-rate 24-bit multiplies and two shift-xors (attn_pair_hash); each compare's lane mask drives
       // both the select that zeroes P and a carry-in add that shifts the bit into the word (s1[15] first, so it
       // ends at bit 31).
       const uint32_t base = rh + ((uint32_t)(kbase >> 1) + 2u * (uint32_t)hh) * HG;

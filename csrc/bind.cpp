@@ -34,6 +34,7 @@ int dllm_attn_params_size();
 int dllm_attn_dropout_mask(AttnParams*, hipStream_t);
 int dllm_gemm_wgrad(const GemmWgradParams*, int, hipStream_t);
 int dllm_gemm_fused(const GemmFusedParams*, int, int, hipStream_t);
+int dllm_gemm_w4(const GemmW4Params*, int, hipStream_t);
 int dllm_colsum_rows();
 int dllm_ce_chunk_fwd(const void*, long, const int64_t*, const float*, float*, float*, float*, long, int, int, int, float,
                       long, int, int, int, hipStream_t);
@@ -638,6 +639,65 @@ Tensor gemm_fused(const Tensor& a, const Tensor& b, bool b_kmajor, int64_t epi, 
   return out;
 }
 
+// ---- one-wave-per-SIMD projection GEMM (csrc/gemm_w4.hip): out (+)= a . b (+ bias), b = [N][K] (nn.Linear weight)
+// or [K][N] (b_kmajor, the input-gradient GEMM).  Ragged M / N; K % 64 == 0; N % 8 == 0.
+bool gemm_w4_supported(const Tensor& a, const Tensor& b, bool b_kmajor) {
+  auto ok2 = [](const Tensor& t) {
+    return t.is_cuda() && t.dim() == 2 && t.scalar_type() == at::kBFloat16 && t.stride(1) == 1 && t.stride(0) % 8 == 0 &&
+           t.stride(0) >= t.size(1) && reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0;
+  };
+  if (!ok2(a) || !ok2(b)) return false;
+  const int64_t M = a.size(0), K = a.size(1);
+  const int64_t N = b_kmajor ? b.size(1) : b.size(0);
+  const int64_t Kb = b_kmajor ? b.size(0) : b.size(1);
+  // buffer-descriptor offsets are 32-bit with 0x80000000 as the out-of-range marker: every per-tile byte range < 2^31
+  const bool ranges = 256 * a.stride(0) * 2 < (1LL << 31) &&
+                      (b_kmajor ? K * b.stride(0) * 2 < (1LL << 31) : 256 * b.stride(0) * 2 < (1LL << 31));
+  return Kb == K && K > 0 && K % 64 == 0 && M > 0 && N > 0 && N % 8 == 0 && ranges && (M + 255) / 256 * ((N + 255) / 256) < INT_MAX;
+}
+
+Tensor gemm_w4(const Tensor& a, const Tensor& b, bool b_kmajor, const optional<Tensor>& bias, const optional<Tensor>& out,
+               bool accumulate, int64_t grp) {
+  TORCH_CHECK(gemm_w4_supported(a, b, b_kmajor),
+              "gemm_w4: need bf16 GPU a [M,K], b [N,K] (or [K,N] k-major), unit inner stride, 16-B aligned rows, K % 64 == 0, "
+              "N % 8 == 0");
+  TORCH_CHECK(a.device() == b.device(), "gemm_w4: device mismatch");
+  const int64_t M = a.size(0), K = a.size(1), N = b_kmajor ? b.size(1) : b.size(0);
+  Tensor c;
+  if (out.has_value() && out->defined()) {
+    c = *out;
+    TORCH_CHECK(c.is_cuda() && c.device() == a.device() && c.scalar_type() == at::kBFloat16 && c.dim() == 2 &&
+                    c.size(0) == M && c.size(1) == N && c.stride(1) == 1 && c.stride(0) % 8 == 0 &&
+                    reinterpret_cast<uintptr_t>(c.data_ptr()) % 16 == 0,
+                "gemm_w4: out must be a bf16 [M, N] GPU tensor with unit inner stride and 16-B aligned rows");
+  } else {
+    TORCH_CHECK(!accumulate, "gemm_w4: accumulate needs out");
+    c = at::empty({M, N}, a.options());
+  }
+  GemmW4Params P{};
+  P.A = reinterpret_cast<const uint16_t*>(a.data_ptr());
+  P.B = reinterpret_cast<const uint16_t*>(b.data_ptr());
+  P.C = reinterpret_cast<uint16_t*>(c.data_ptr());
+  if (bias.has_value() && bias->defined()) {
+    TORCH_CHECK(bias->is_cuda() && bias->device() == a.device() && bias->scalar_type() == at::kBFloat16 &&
+                    bias->is_contiguous() && bias->numel() == N && reinterpret_cast<uintptr_t>(bias->data_ptr()) % 8 == 0,
+                "gemm_w4: bias must be a contiguous 8-B aligned bf16 [N] GPU tensor");
+    P.bias = reinterpret_cast<const uint16_t*>(bias->data_ptr());
+  }
+  P.lda = a.stride(0);
+  P.ldb = b.stride(0);
+  P.ldc = c.stride(0);
+  P.M = (int)M;
+  P.N = (int)N;
+  P.K = (int)K;
+  P.tm = (int)((M + 255) / 256);
+  P.tn = (int)((N + 255) / 256);
+  P.grp = grp >= 0 ? (int)grp : 4;
+  P.accumulate = accumulate ? 1 : 0;
+  check_rc(dllm_gemm_w4(&P, b_kmajor ? 1 : 0, stream()), "gemm_w4");
+  return c;
+}
+
 // Gated-GELU FFN (FLAN-T5 / T5 v1.1 "gated-gelu", tanh GELU) on the ping-pong kernel, csrc/gemm_fused.hip epi 8 / 9.
 // forward: x [M, d] . [wi_0; wi_1]^T ([2F, d], the stacked wi weight) -> h = dropout(gelu(x wi_0^T) * (x wi_1^T)) [M, F]
 //          plus G1 = s gelu'(gate) up and G2 = s gelu(gate) ([M, F] each, s = keep / (1 - p)) for the backward;
@@ -785,6 +845,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_geglu", &gemm_geglu, "gated-GELU FFN input GEMM: (h, G1, G2) from x and the stacked [wi_0; wi_1]");
   m.def("gemm_dgeglu", &gemm_dgeglu, "gated-GELU FFN backward GEMM: d(stacked wi output) from dy, wo, G1, G2");
   m.def("gemm_fused_variant", &gemm_fused_variant, "default kernel variant for reduction length K");
+  m.def("gemm_w4", &gemm_w4, "out (+)= a . b (+ bias) on the one-wave-per-SIMD GEMM (csrc/gemm_w4.hip)", py::arg("a"),
+        py::arg("b"), py::arg("b_kmajor"), py::arg("bias") = py::none(), py::arg("out") = py::none(),
+        py::arg("accumulate") = false, py::arg("grp") = -1);
+  m.def("gemm_w4_supported", &gemm_w4_supported);
   m.def("colsum_acc", &colsum_acc, "out += x.sum(0) for a token-major bf16 x (bias gradients)");
   dllm::bind_reducer(m);
   m.attr("arch") = "gfx950";

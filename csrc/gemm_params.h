@@ -17,6 +17,21 @@ struct GemmWgradParams {
   int c_f32;  // C is fp32 (fp32 gradient accumulation across micro-batches), else bf16
 };
 
+// csrc/gemm_w4.hip: C[M][N] (+)= A[M][K] . B (+ bias), B = [N][K] (b_kmajor = 0) or [K][N] (b_kmajor = 1).
+// Ragged M and N (loads past the edge return 0 through the buffer descriptor's range check, stores are masked);
+// K % 64 == 0.
+struct GemmW4Params {
+  const uint16_t* A;
+  const uint16_t* B;
+  uint16_t* C;
+  const uint16_t* bias;  // [N] or null
+  long lda, ldb, ldc;
+  int M, N, K;
+  int tm, tn;      // ceil(M / 256), ceil(N / 256)
+  int grp;         // tile order: groups of grp 256-row blocks, column-major inside a group; 0 = row-major
+  int accumulate;  // 1: C += A . B (bf16 read-modify-write), 0: C = A . B
+};
+
 // csrc/gemm_fused.hip: C[M][N] = epi(A[M][K] . B), B = [N][K] (b_kmajor = 0) or [K][N] (b_kmajor = 1)
 struct GemmFusedParams {
   const uint16_t* A;

@@ -1,0 +1,352 @@
+// Projection GEMMs on ONE WAVE PER SIMD for gfx950 (MI355X / CDNA4):
+//
+//   NT (forward):  C[M][N] (+)= A[M][K] . B[N][K]^T (+ bias)   A = activations [tokens][in], B = nn.Linear weight [out][in]
+//   NN (dgrad):    C[M][N] (+)= A[M][K] . B[K][N]              A = output gradient [tokens][out], B = weight (k-major)
+//
+// Why this shape of kernel (profiles/r2_gemm_pmc_pp_vs_hipblaslt.txt): the 8-wave ping-pong kernel of
+// csrc/gemm_fused.hip re-reads A/B fragments for 128x64 sub-tiles, rebuilds buffer descriptors around every DMA
+// (4x hipBLASLt's SALU count) and parks its waves 38 % of their cycles at barriers.  Here:
+//
+// * 256x256 output tile per 256-thread workgroup, 4 waves as 2(M) x 2(N), 128x128 per wave = 8x8
+//   v_mfma_f32_16x16x32_bf16 accumulators: 256 fp32 per lane, which the allocator places in the AGPR half of the
+//   unified 512-register file (__launch_bounds__(256, 1): one wave per SIMD).  Per 64-deep k-tile a wave issues 128
+//   MFMAs against 32 fragment reads (ds_read_b128 / 2x ds_read_b64_tr_b16): 4 MFMAs per LDS read, twice the ratio of
+//   the 8-wave kernel;
+// * operands go global -> LDS by LDS-DMA (buffer_load_dwordx4 ... lds), 16 per wave per k-tile.  Descriptors are
+//   built ONCE per tile in SGPRs, the per-lane offsets live in 16 VGPRs, the k-tile advance is one VALU add per DMA
+//   and M0 is written by the DMA statement itself (no save / restore): 1 SALU per DMA;
+// * two 64-KB LDS buffers (k-tile t in buffer t & 1), ONE barrier per k-tile, placed 8 MFMAs into the k-tile's
+//   second 32-deep sub-step: after it the DMA of k-tile t+2 (into the buffer k-tile t just left) and the fragment
+//   reads of k-tile t+1 are issued between the remaining 56 MFMAs, so the LDS latency of the next sub-step and the
+//   DMA issue hide under matrix work and the DMA has one full k-tile of MFMAs to land;
+// * the instruction interleave is pinned in 8-MFMA chunks (sched_barrier between chunks; inside a chunk the
+//   compiler's own lgkmcnt bookkeeping places the waits);
+// * ragged M / N: the descriptors' range check returns 0 for rows past the edge (NT) and per-lane offsets of columns
+//   past N are pushed out of range (NN); stores are masked.  K % 64 == 0;
+// * epilogue: accumulators of row blocks 2i / 2i+1 are packed to bf16 and exchanged between lane rows with
+//   v_permlane16_swap, so every lane stores 16 contiguous bytes (32 stores per wave instead of 64 of 8 B,
+//   cdna_hip_programming.md T21);
+// * bijective XCD remap of the 1-D grid, tiles grouped grp x (32 / grp) per XCD for L2 reuse of A and B.
+#include "common.h"
+
+#include "gemm_params.h"
+
+using namespace dllm;
+
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8v;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+
+constexpr int NT = 256, BK = 64;
+constexpr uint32_t kOOB = 0x80000000u;  // a buffer offset past every descriptor's range: the load returns 0
+
+DLLM_DEVICE int xcd_remap(int bid, int nblk) {
+  const int q = nblk / 8, r = nblk % 8, x = bid % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+}
+
+// raw buffer descriptor over [base, base + bytes): offsets >= bytes read as 0 (stride 0 -> byte range check)
+DLLM_DEVICE i32x4 make_srd(const void* base, uint32_t bytes) {
+  const uint64_t a = (uint64_t)base;
+  i32x4 r;
+  r.x = __builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+  r.y = __builtin_amdgcn_readfirstlane((int)((uint32_t)(a >> 32) & 0xFFFFu));
+  r.z = __builtin_amdgcn_readfirstlane((int)bytes);
+  r.w = 0x00020000;
+  return r;
+}
+
+// 16 B per lane from srd + voff to LDS byte lds + 16 * lane.  M0 is written here and nowhere else in the kernel
+// (clobbered, not saved): 1 SALU per DMA.  Invisible to the compiler's vmcnt bookkeeping (as glds16 in common.h);
+// retired by the explicit counted waits below.
+DLLM_DEVICE void dma16(const i32x4& srd, uint32_t voff, uint32_t lds) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds"
+               :
+               : "v"(voff), "s"(srd), "s"(lds)
+               : "memory", "m0");
+}
+
+// ---- k-major [64][256] image (512-B rows) of the NN B operand, transposed reads (csrc/gemm_fused.hip layout)
+DLLM_DEVICE int gsw(int r) { return ((r & 3) << 2) ^ (((r >> 3) & 1) << 1); }
+DLLM_DEVICE uint32_t boff_km(int r, int col) {  // byte offset of (k-row r, column col)
+  return (uint32_t)((r << 9) + ((((col >> 3) ^ gsw(r)) << 3) + (col & 7)) * 2);
+}
+
+template <typename T>
+DLLM_DEVICE T lds_ld(const unsigned char* smem, uint32_t off) {
+  return *reinterpret_cast<const T*>(smem + off);
+}
+
+// 16x16x32 operand from the k-major image: lane l holds column cb + (l & 15), k = kk + 8 (l >> 4) + 0..7
+DLLM_DEVICE bf16x8v frag_km16(const unsigned char* smem, uint32_t img, int kk, int cb, int lane) {
+  const int i = lane & 15;
+  const int r = kk + 8 * (lane >> 4) + (i >> 2);
+  const int col = cb + 4 * (i & 3);
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(smem + img + boff_km(r, col)));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(smem + img + boff_km(r + 4, col)));
+  const s16x4 v0 = lo, v1 = hi;
+  const u16x8 v = {(uint16_t)v0.x, (uint16_t)v0.y, (uint16_t)v0.z, (uint16_t)v0.w,
+                   (uint16_t)v1.x, (uint16_t)v1.y, (uint16_t)v1.z, (uint16_t)v1.w};
+  return __builtin_bit_cast(bf16x8v, v);
+}
+
+DLLM_DEVICE uint32_t pk2(float a, float b) { return pack_bf16x2(a, b); }
+
+// c += b . a^T (16x16x32, bf16): inline asm so the accumulator is pinned to AGPRs ("+a") and the fragments to VGPRs.
+// With the builtin, hipcc (ROCm 7.2) spreads the 256 accumulators and 128 fragment registers over both halves of the
+// register file and spills ~200 VGPRs.  The asm is opaque to hipcc's hazard recognizer, so the kernel pads the two
+// places the builtin would have been padded: after the accumulator zeroing (mfma_init) and before the epilogue reads.
+DLLM_DEVICE void mfma(f32x4& c, const bf16x8v& b, const bf16x8v& a) {
+  asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(b), "v"(a));
+}
+// first k-step of a tile: C input 0 (no accumulator zeroing pass)
+DLLM_DEVICE void mfma0(f32x4& c, const bf16x8v& b, const bf16x8v& a) {
+  asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(c) : "v"(b), "v"(a));
+}
+
+template <bool BKM, bool BIAS, bool ACC>
+__global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr uint32_t TB = 256 * BK * 2;  // one operand image: 32 KB
+  constexpr uint32_t BUF = 2 * TB;       // [A | B] of one k-tile: 64 KB; two buffers
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w >> 1, wn = w & 1;
+
+  // ---- tile of this workgroup
+  const int vt = xcd_remap(blockIdx.x, gridDim.x);
+  int mb = vt / P.tn, nb = vt % P.tn;
+  if (P.grp > 0) {  // the tiles an XCD runs at once cover a grp x (32 / grp) block (L2 reuse of A and B)
+    const int gs = P.grp * P.tn, g = vt / gs, r = vt % gs;
+    const int rows = min(P.grp, P.tm - g * P.grp);
+    mb = g * P.grp + r % rows;
+    nb = r / rows;
+  }
+  const int m0 = mb * 256, n0 = nb * 256;
+  const int nk = P.K / BK;
+
+  // ---- descriptors (scalar) and per-lane DMA offsets.  Row image ([256][64], 128-B rows): wave-instruction q covers
+  // rows 8q .. 8q+7, lane -> (row 8q + l/8, 16-B chunk (l%8) ^ ((row/2)&7)).  K-major image ([64][256], 512-B rows):
+  // instruction q covers k-rows 2q, 2q+1, lane -> (k-row 2q + l/32, chunk (l%32) ^ gsw(k-row)).
+  const i32x4 srdA = make_srd(P.A + (long)m0 * P.lda, (uint32_t)(min(P.M - m0, 256) * P.lda * 2));
+  const i32x4 srdB = BKM ? make_srd(P.B + n0, (uint32_t)(((long)P.K * P.ldb - n0) * 2))
+                         : make_srd(P.B + (long)n0 * P.ldb, (uint32_t)(min(P.N - n0, 256) * P.ldb * 2));
+  uint32_t va[8], vb[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int q = w * 8 + i;
+    const int r = 8 * q + (lane >> 3);
+    const int c = (lane & 7) ^ ((r >> 1) & 7);
+    va[i] = (uint32_t)(r * P.lda + c * 8) * 2u;
+    if (BKM) {
+      const int kr = 2 * q + (lane >> 5);
+      const int col = ((lane & 31) ^ gsw(kr)) * 8;
+      vb[i] = n0 + col < P.N ? (uint32_t)(kr * P.ldb + col) * 2u : kOOB;
+    } else {
+      vb[i] = (uint32_t)(r * P.ldb + c * 8) * 2u;
+    }
+  }
+  const uint32_t lds0 = lds_addr(smem);
+  const uint32_t kstepB = BKM ? (uint32_t)(BK * P.ldb * 2) : (uint32_t)(BK * 2);
+  // DMA of k-tile kt into buffer b: instruction i of operand X -> image bytes (8 w + i) * 1 KB
+  auto dma_a = [&](int i, int kt, int b) {
+    dma16(srdA, va[i] + (uint32_t)kt * (BK * 2), lds0 + (uint32_t)b * BUF + (uint32_t)(8 * w + i) * 1024u);
+  };
+  auto dma_b = [&](int i, int kt, int b) {
+    dma16(srdB, vb[i] + (uint32_t)kt * kstepB, lds0 + (uint32_t)b * BUF + TB + (uint32_t)(8 * w + i) * 1024u);
+  };
+
+  // ---- fragment reads.  Row image: a[i] = rows wm*128 + 16 i + (l & 15), k chunk kk/8 + (l >> 4), swizzled by
+  // ((row / 2) & 7), which does not depend on i: one base offset per 32-deep half, +2 KB per i.
+  const int rl = lane & 15, qd = lane >> 4;
+  const uint32_t arow = (uint32_t)(wm * 128 + rl), brow = (uint32_t)(wn * 128 + rl);
+  const int asw = (int)((arow >> 1) & 7), bsw = (int)((brow >> 1) & 7);
+  const uint32_t aoff[2] = {arow * 128u + (uint32_t)((qd ^ asw) << 4), arow * 128u + (uint32_t)(((qd + 4) ^ asw) << 4)};
+  const uint32_t boff[2] = {brow * 128u + (uint32_t)((qd ^ bsw) << 4), brow * 128u + (uint32_t)(((qd + 4) ^ bsw) << 4)};
+  auto rd_a = [&](int b, int h, int i) { return lds_ld<bf16x8v>(smem, (uint32_t)b * BUF + aoff[h] + (uint32_t)i * 2048u); };
+  auto rd_b = [&](int b, int h, int j) {
+    if constexpr (BKM) return frag_km16(smem, (uint32_t)b * BUF + TB, 32 * h, wn * 128 + 16 * j, lane);
+    else return lds_ld<bf16x8v>(smem, (uint32_t)b * BUF + TB + boff[h] + (uint32_t)j * 2048u);
+  };
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8v fa0[8], fb0[8], fa1[8], fb1[8];
+
+  // ---- prologue: k-tiles 0 and 1 in flight, wait for k-tile 0, read its first half
+  const int k1 = min(1, nk - 1);  // nk == 1: k-tile 0 again into buffer 1 (never read)
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    dma_a(i, 0, 0);
+    dma_b(i, 0, 0);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    dma_a(i, k1, 1);
+    dma_b(i, k1, 1);
+  }
+  wait_vm<16>();
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) fb0[j] = rd_b(0, 0, j);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) fa0[i] = rd_a(0, 0, i);
+
+  // one chunk = the 8 MFMAs of accumulator row i (swapped roles: lane holds row m = 16 i + (l & 15), 4 consecutive n)
+  auto chunk = [&](const bf16x8v (&fa)[8], const bf16x8v (&fb)[8], int i) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) mfma(acc[i][j], fb[j], fa[i]);
+  };
+  // sub-step 0 of k-tile t (k 0..31, fragments fa0 / fb0): read the k 32..63 fragments into fa1 / fb1, two per chunk,
+  // B first (the next sub-step's first chunk needs all of B and a[0])
+  auto substep0 = [&](int b) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      chunk(fa0, fb0, i);
+      if (i < 4) {
+        fb1[2 * i] = rd_b(b, 1, 2 * i);
+        fb1[2 * i + 1] = rd_b(b, 1, 2 * i + 1);
+      } else {
+        fa1[2 * i - 8] = rd_a(b, 1, 2 * i - 8);
+        fa1[2 * i - 7] = rd_a(b, 1, 2 * i - 7);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  // every k-tile runs the same branch-free body (a peeled last k-tile makes the allocator re-assign all 256 AGPRs
+  // between loop and tail, ~600 v_accvgpr copies): the prefetch index is clamped, so the last k-tiles re-load k-tile
+  // nk-1 into the buffer their predecessor just left, and the last k-tile's "next fragments" are read and dropped
+  // do-while: nk >= 1 (host-checked); with a for loop the zero-trip path keeps a VGPR copy of the zero accumulators
+  // alive and the allocator shuffles all 256 of them at the loop exit
+  int t = 0;
+  do {
+    // the accumulator zeroing (v_accvgpr_write, sunk by the compiler next to the loop) must be 2+ wait states before
+    // the first asm MFMA reads it as C; hipcc cannot see that read
+    asm volatile("s_nop 2" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    const int b = t & 1;
+    substep0(b);
+    // sub-step 1 (k 32..63, fa1 / fb1).  After its first chunk: k-tile t+1 landed (its DMA was the last issued) and
+    // every wave is past its reads of buffer b -> barrier; then DMA k-tile t+2 into buffer b and read k-tile t+1's
+    // first half into fa0 / fb0, spread over the remaining 7 chunks
+    chunk(fa1, fb1, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    const int kn = min(t + 2, nk - 1);
+#pragma unroll
+    for (int i = 1; i < 8; ++i) {
+      chunk(fa1, fb1, i);
+      // DMA: instructions 0..7 of A then of B, spread over chunks 1..7 (2, 2, 2, 3, 2, 2, 3)
+      const int lo = (i - 1) * 16 / 7, hi = i * 16 / 7;
+#pragma unroll
+      for (int d = lo; d < hi; ++d) {
+        if (d < 8) dma_a(d, kn, b);
+        else dma_b(d - 8, kn, b);
+      }
+      // fragments of k-tile t+1 (buffer b ^ 1), first half: B in chunks 1..4, A in chunks 5..7
+      if (i <= 4) {
+        fb0[2 * i - 2] = rd_b(b ^ 1, 0, 2 * i - 2);
+        fb0[2 * i - 1] = rd_b(b ^ 1, 0, 2 * i - 1);
+      } else if (i < 7) {
+        fa0[3 * (i - 5)] = rd_a(b ^ 1, 0, 3 * (i - 5));
+        fa0[3 * (i - 5) + 1] = rd_a(b ^ 1, 0, 3 * (i - 5) + 1);
+        fa0[3 * (i - 5) + 2] = rd_a(b ^ 1, 0, 3 * (i - 5) + 2);
+      } else {
+        fa0[6] = rd_a(b ^ 1, 0, 6);
+        fa0[7] = rd_a(b ^ 1, 0, 7);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  } while (++t < nk);
+  wait_vm<0>();  // the clamped re-loads of the last k-tile
+
+  // the last MFMAs' results are read by VALU below: 8-pass XDL write -> VALU read needs 11 wait states, which
+  // hipcc cannot see through the asm
+  asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+  // ---- epilogue.  acc[i][j][r] = C[m0 + wm*128 + 16 i + (l & 15)][n0 + wn*128 + 16 j + 4 (l >> 4) + r].
+  // Row blocks 2ii / 2ii+1 packed to bf16 and exchanged with v_permlane16_swap (odd 16-lane rows of X <-> even rows
+  // of Y): afterwards lane l holds 8 consecutive columns 16 j + 8 (qd >> 1) of row 32 ii + 16 (qd & 1) + (l & 15).
+  __builtin_amdgcn_sched_barrier(0);
+  const int mrow = m0 + wm * 128 + 16 * (qd & 1) + rl;
+  const int ncol = n0 + wn * 128 + 8 * (qd >> 1);
+  f32x4 bv[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    bv[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (BIAS) {
+      const int nb4 = n0 + wn * 128 + 16 * j + 4 * qd;
+      if (nb4 < P.N) bv[j] = Elem<uint16_t>::load4(P.bias + nb4);
+    }
+  }
+#pragma unroll
+  for (int ii = 0; ii < 4; ++ii) {
+    const int m = mrow + 32 * ii;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const f32x4 x = acc[2 * ii][j] + bv[j], y = acc[2 * ii + 1][j] + bv[j];
+      uint32_t x0 = pk2(x.x, x.y), x1 = pk2(x.z, x.w), y0 = pk2(y.x, y.y), y1 = pk2(y.z, y.w);
+      {
+        const auto r0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
+        const auto r1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
+        x0 = r0[0];
+        y0 = r0[1];
+        x1 = r1[0];
+        y1 = r1[1];
+      }
+      const int n = ncol + 16 * j;
+      if (m < P.M && n < P.N) {
+        uint16_t* cp = P.C + (long)m * P.ldc + n;
+        u32x4 o = {x0, x1, y0, y1};
+        if constexpr (ACC) {
+          const u32x4 c = *reinterpret_cast<const u32x4*>(cp);
+          auto add2 = [](uint32_t u, uint32_t v) {
+            return pk2(bf2f((uint16_t)(u & 0xFFFFu)) + bf2f((uint16_t)(v & 0xFFFFu)),
+                       bf2f((uint16_t)(u >> 16)) + bf2f((uint16_t)(v >> 16)));
+          };
+          o = u32x4{add2(o.x, c.x), add2(o.y, c.y), add2(o.z, c.z), add2(o.w, c.w)};
+        }
+        *reinterpret_cast<u32x4*>(cp) = o;
+      }
+      // bound the live ranges: otherwise the scheduler hoists all 256 accumulator reads and runs out of VGPRs
+      if (j & 1) __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+}
+
+template <bool BKM, bool BIAS, bool ACC>
+int launch(const GemmW4Params& p, hipStream_t st) {
+  constexpr size_t lds = 2 * 2 * 256 * BK * 2;  // 128 KB
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm_w4_kernel<BKM, BIAS, ACC>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+    attr = true;
+  }
+  hipLaunchKernelGGL((gemm_w4_kernel<BKM, BIAS, ACC>), dim3(p.tm * p.tn), dim3(NT), lds, st, p);
+  DLLM_CHECK_LAUNCH();
+  return 0;
+}
+
+template <bool BKM>
+int dispatch(const GemmW4Params& p, hipStream_t st) {
+  if (p.accumulate) return p.bias ? launch<BKM, true, true>(p, st) : launch<BKM, false, true>(p, st);
+  return p.bias ? launch<BKM, true, false>(p, st) : launch<BKM, false, false>(p, st);
+}
+
+}  // namespace
+
+extern "C" int dllm_gemm_w4(const GemmW4Params* pp, int b_kmajor, hipStream_t st) {
+  const GemmW4Params& p = *pp;
+  if (p.M <= 0 || p.N <= 0 || p.K <= 0 || p.K % BK || p.N % 8 || p.tm * 256 < p.M || p.tn * 256 < p.N) return -4;
+  return b_kmajor ? dispatch<true>(p, st) : dispatch<false>(p, st);
+}

@@ -51,20 +51,23 @@ def keep_mask(seed: int, p: float, shape, device, numel_offset: int = 0) -> torc
 
 _G = 0x9E3779B1
 _C24 = 0x9E3779
+_C24B = 0x85EBCB
 
 
 def attention_keep_mask(seed: int, p: float, B: int, H: int, Sq: int, Sk: int, device) -> torch.Tensor:
     """Attention-probability mask [B, H, Sq, Sk] (mirrors csrc/attn.hip ``attn_pair_hash``).
 
     Per query row ``r = (b*H + h)*Sq + i``: ``rh = mix32(seed, r)`` (computed once per row in the
-    kernels); per key pair ``kp = j >> 1``: ``h = ((rh + kp*G) & 0xFFFFFF) * C24`` (mod 2^32 — one
-    full-rate 24-bit multiply per two keys inside the attention kernels), ``y = h ^ (h >> 16)``; the
-    even key keeps iff ``y & 0xFFFF >= threshold16(p)``, the odd key iff ``h >> 16 >= threshold16(p)``."""
+    kernels); per key pair ``kp = j >> 1``: ``g = ((rh + kp*G) & 0xFFFFFF) * C24``,
+    ``h = ((g ^ (g >> 15)) & 0xFFFFFF) * C24B`` (mod 2^32 — two full-rate 24-bit multiplies per two keys inside the
+    attention kernels; ``g`` alone is linear in ``kp`` and leaves lag-2 drops anti-correlated), ``y = h ^ (h >> 16)``;
+    the even key keeps iff ``y & 0xFFFF >= threshold16(p)``, the odd key iff ``h >> 16 >= threshold16(p)``."""
     rows = torch.arange(B * H * Sq, device=device, dtype=torch.int64)
     rh = mix32(seed, rows).view(B, H, Sq, 1)
     j = torch.arange(Sk, device=device, dtype=torch.int64).view(1, 1, 1, Sk)
     x = (rh + (j >> 1) * _G) & 0xFFFFFF
-    h = (x * _C24) & _MASK
+    g = (x * _C24) & _MASK
+    h = (((g ^ (g >> 15)) & 0xFFFFFF) * _C24B) & _MASK
     half = torch.where((j & 1) == 1, h >> 16, (h ^ (h >> 16)) & 0xFFFF)
     return half >= threshold16(p)
 

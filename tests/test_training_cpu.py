@@ -292,6 +292,18 @@ def test_attention_dropout_hash_statistics():
     both_far = (d[..., :256] * d[..., 256:]).mean().item()
     for v in (both_pair, both_row, both_far):
         assert abs(v - p * p) < 0.0015, (both_pair, both_row, both_far)
+    # lag-2 (odd-odd, even-even: successive hashes of one row), lag-3 and lag-16 keys: independent draws give p^2
+    dd = d.reshape(-1, d.shape[-1])
+    oo = (dd[:, 1::2][:, :-1] * dd[:, 1::2][:, 1:]).mean().item()
+    ee = (dd[:, 0::2][:, :-1] * dd[:, 0::2][:, 1:]).mean().item()
+    l3 = (dd[:, :-3] * dd[:, 3:]).mean().item()
+    l16 = (dd[:, :-16] * dd[:, 16:]).mean().item()
+    for v in (oo, ee, l3, l16):
+        assert abs(v - p * p) < 0.0015, (oo, ee, l3, l16)
+    # per-row drop counts: binomial variance Sk p (1 - p) (a hash linear in the key index had ~1/8 of it)
+    var = dd.sum(1).var().item()
+    binom = dd.shape[1] * p * (1 - p)
+    assert 0.75 * binom < var < 1.3 * binom, (var, binom)
     # per-key-column and per-row drop rates stay near p (no stuck columns / rows)
     col = d.mean(dim=(0, 1, 2))
     row = d.mean(dim=(0, 1, 3))
