@@ -9,6 +9,19 @@ backward, gradient all-reduce, global-norm clip and AdamW update.  Synthetic SAM
 weights with HF's initialisation (no network).  Weak scaling: fixed per-GPU micro-batch.
 
     python bench.py --gpus N --steps K --warmup W
+
+Multi-GPU self-diagnosis (N > 1; every field is also produced on a gloo CPU rehearsal, DLLM_FORCE_CPU=1):
+  * before timing, every rank's world size, RCCL version, bucket layout (bounds + segment sizes) and parameter count
+    are all-gathered and compared: a mismatch aborts the run with the differing ranks named;
+  * ``comm.exposed_ms_per_step``: per synchronised backward, the time between the last backward kernel and the last
+    bucket all-reduce completing on the compute stream (GPU events around the reducer's end-of-backward wait) — the
+    communication NOT hidden under backward; ``comm.exposed_frac`` = that / ms_per_step;
+  * ``comm.bucket_launch``: the last backward's bucket launch order and, per launch, the fraction of gradient
+    segments already ready (overlap works when early buckets launch at small fractions);
+  * ``--comm-stress``: per-GPU micro-batch 8 (unless --batch-per-gpu is given), so all-reduce time is comparable to
+    compute and the 1->N curve measures the reducer's overlap, not just weak-scaled compute;
+  * ``--grad-accum G``: G micro-batches per optimizer step, ``no_sync`` on all but the last (reference
+    train-torchrun: batch 1 x GA 16, ref/train-torchrun.py:119,126); never coalesced into one pass here.
 """
 from __future__ import annotations
 
@@ -51,7 +64,16 @@ def parse():
     ap.add_argument("--dropout", type=float, default=None, help="override model dropout (default: config 0.1)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--grad-ckpt", action="store_true", help="activation checkpointing per block")
-    return ap.parse_args()
+    ap.add_argument("--grad-accum", type=int, default=1, help="micro-batches per optimizer step (no_sync on all but the "
+                                                               "last; samples/s counts every micro-batch)")
+    ap.add_argument("--comm-stress", action="store_true",
+                    help="small per-GPU batch (8 unless --batch-per-gpu is given): all-reduce ~ compute")
+    ap.add_argument("--dtype", default=None, choices=["bf16", "fp32"],
+                    help="weights/activations dtype (default bf16; fp32 on a CPU rehearsal)")
+    a = ap.parse_args()
+    if a.comm_stress and "--batch-per-gpu" not in " ".join(sys.argv):
+        a.batch_per_gpu = 8
+    return a
 
 
 def _rccl_version():
@@ -60,6 +82,30 @@ def _rccl_version():
         return ".".join(str(x) for x in v) if isinstance(v, tuple) else str(v)
     except Exception:  # noqa: BLE001 - informational only
         return None
+
+
+def _sync(dev):
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+
+
+def check_rank_consistency(env, eng, model_name: str, batch: int):
+    """All-gather what every rank must agree on (RCCL matches collectives by order and size: a mismatch deadlocks or
+    silently mixes gradients) and fail loudly, naming the ranks, when anything differs."""
+    import hashlib
+    red = eng.reducer
+    sig = red.layout_signature() if red is not None else []
+    mine = {"world_size": env.world_size, "rccl_version": _rccl_version() if env.backend == "nccl" else None,
+            "backend": env.backend, "model": model_name, "per_gpu_batch": batch,
+            "n_params": sum(p.numel() for p in eng.flat.params),
+            "bucket_layout_sha": hashlib.sha1(json.dumps(sig).encode()).hexdigest()[:16],
+            "n_buckets": len(red.buckets) if red is not None else 0}
+    allv = [None] * env.world_size
+    dist.all_gather_object(allv, mine)
+    bad = {k: {r: v[k] for r, v in enumerate(allv)} for k in mine if len({json.dumps(v[k]) for v in allv}) > 1}
+    if bad:
+        raise SystemExit(f"[bench] rank {env.rank}: ranks disagree on {sorted(bad)}: {json.dumps(bad)}")
+    return {"status": "ok", "checked": sorted(mine), **{k: mine[k] for k in ("bucket_layout_sha", "n_buckets")}}
 
 
 def main():
@@ -83,13 +129,16 @@ def main():
     if a.grad_ckpt:
         cfg = cfg.replace(gradient_checkpointing=True)
     model = build_model(cfg)
-    eng = TrainEngine(model, env, lr=5e-5, weight_decay=0.01, max_grad_norm=1.0, dtype=torch.bfloat16,
+    dtype_name = a.dtype or ("bf16" if env.device.type == "cuda" else "fp32")
+    dtype = torch.bfloat16 if dtype_name == "bf16" else torch.float32
+    eng = TrainEngine(model, env, lr=5e-5, weight_decay=0.01, max_grad_norm=1.0, dtype=dtype,
                       bucket_mb=a.bucket_mb or DEFAULT_BUCKET_MB, overlap=not a.no_overlap)
     eng.train()
     B, S, T, V = a.batch_per_gpu, a.src_len, a.tgt_len, cfg.vocab_size
+    GA = max(1, a.grad_accum)
     g = torch.Generator(device="cpu").manual_seed(1000 + env.rank)
     batches = []
-    for _ in range(2):
+    for _ in range(2 * GA):
         batches.append({
             "input_ids": torch.randint(2, V, (B, S), generator=g).to(env.device),
             "attention_mask": torch.ones(B, S, dtype=torch.long).to(env.device),
@@ -97,25 +146,43 @@ def main():
         })
 
     def step(i):
-        eng.forward_backward(batches[i % len(batches)])
+        for k in range(GA):  # GA micro-batches, gradient sync (and the all-reduce) on the last only
+            eng.forward_backward(batches[(i * GA + k) % len(batches)], grad_accum=GA, sync=k == GA - 1)
         eng.step()
 
     for i in range(a.warmup):
         step(i)
+    consistency = check_rank_consistency(env, eng, a.model, B) if n > 1 else None  # after warmup: buckets rebuilt
+    if eng.reducer is not None:
+        eng.reducer.take_exposed_ms()
+        eng.reducer.set_timing(True)
     env.barrier()
-    torch.cuda.synchronize()
+    _sync(env.device)
     t0 = time.perf_counter()
     for i in range(a.steps):
         step(i)
     env.barrier()
-    torch.cuda.synchronize()
+    _sync(env.device)
     dt = time.perf_counter() - t0
+    comm = None
+    if eng.reducer is not None:
+        eng.reducer.set_timing(False)
+        ex = eng.reducer.take_exposed_ms()
+        ex_t = torch.tensor([sum(ex) / max(1, len(ex)), max(ex, default=0.0)], dtype=torch.float64,
+                            device=env.device if env.backend == "nccl" else "cpu")
+        dist.all_reduce(ex_t, op=dist.ReduceOp.MAX)  # the slowest rank's exposure sets the step
+        comm = {"exposed_ms_per_step": round(ex_t[0].item(), 3), "exposed_ms_max": round(ex_t[1].item(), 3),
+                "timed_backwards": len(ex), "bucket_launch": eng.reducer.launch_summary(),
+                "bucket_mb": [round(x, 2) for x in eng.reducer.bucket_sizes_mb()[:4]],
+                "consistency": consistency}
     t = torch.tensor([dt], device=env.device if env.backend == "nccl" else "cpu", dtype=torch.float64)
     if n > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = t.item()
     ms = dt / a.steps * 1e3
-    value = B * n * a.steps / dt
+    value = B * GA * n * a.steps / dt
+    if comm is not None:
+        comm["exposed_frac"] = round(comm["exposed_ms_per_step"] / ms, 4)
     if a.model == "t5-base":
         metric = "samples/sec (whole node) T5-base summarization fine-tune at 1/2/4/8 MI355X"
         # the HF stack at the same per-GPU batch, or at its largest measured one below it (it does not fit above 128)
@@ -133,12 +200,12 @@ def main():
             "metric": metric,
             "value": round(value, 2), "unit": "samples/s", "n_gpus": n, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": round(value / (base * n), 3) if base else None,
+            "vs_baseline": round(value / (base * n), 3) if base and B >= 16 else None,
             "baseline_note": f"HF transformers+torch stack measured on 1x MI355X at the same sequence shapes (its "
                              f"per-GPU batch {base_batch}, samples/s compared per sample) x N (BASELINE.md publishes "
                              f"no number)",
-            "dtype": "bf16", "data": "synthetic (random token ids, random-init weights)",
-            "config": {"model": a.model, "global_batch": B * n, "per_gpu_batch": B, "seq_len": S,
+            "dtype": dtype_name, "data": "synthetic (random token ids, random-init weights)",
+            "config": {"model": a.model, "global_batch": B * GA * n, "per_gpu_batch": B, "grad_accum": GA, "seq_len": S,
                        "target_len": T, "parallelism": f"dp{n}", "grad_ckpt": bool(a.grad_ckpt),
                        "bucket_mb": eng.reducer.bucket_sizes_mb()[1] if eng.reducer and len(eng.reducer.buckets) > 1 else None,
                        "tokens_per_s": round(value * (S + T), 1),
@@ -146,7 +213,10 @@ def main():
                        "backend": env.backend, "world_size": n, "rccl_version": _rccl_version(),
                        "overlap": bool(eng.reducer.overlap) if eng.reducer else None,
                        "n_buckets": len(eng.reducer.buckets) if eng.reducer else None,
-                       "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 2)},
+                       "comm_stress": bool(a.comm_stress),
+                       "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 2)
+                       if env.device.type == "cuda" else None},
+            "comm": comm,
         }), flush=True)
     if n > 1:
         dist.barrier()

@@ -34,7 +34,7 @@ int dllm_attn_params_size();
 int dllm_attn_dropout_mask(AttnParams*, hipStream_t);
 int dllm_gemm_wgrad(const GemmWgradParams*, int, hipStream_t);
 int dllm_gemm_fused(const GemmFusedParams*, int, int, hipStream_t);
-int dllm_gemm_w4(const GemmW4Params*, int, hipStream_t);
+int dllm_gemm_w4(const GemmW4Params*, int, int, hipStream_t);
 int dllm_colsum_rows();
 int dllm_ce_chunk_fwd(const void*, long, const int64_t*, const float*, float*, float*, float*, long, int, int, int, float,
                       long, int, int, int, hipStream_t);
@@ -657,7 +657,7 @@ bool gemm_w4_supported(const Tensor& a, const Tensor& b, bool b_kmajor) {
 }
 
 Tensor gemm_w4(const Tensor& a, const Tensor& b, bool b_kmajor, const optional<Tensor>& bias, const optional<Tensor>& out,
-               bool accumulate, int64_t grp) {
+               bool accumulate, int64_t grp, bool persist) {
   TORCH_CHECK(gemm_w4_supported(a, b, b_kmajor),
               "gemm_w4: need bf16 GPU a [M,K], b [N,K] (or [K,N] k-major), unit inner stride, 16-B aligned rows, K % 64 == 0, "
               "N % 8 == 0");
@@ -694,7 +694,7 @@ Tensor gemm_w4(const Tensor& a, const Tensor& b, bool b_kmajor, const optional<T
   P.tn = (int)((N + 255) / 256);
   P.grp = grp >= 0 ? (int)grp : 4;
   P.accumulate = accumulate ? 1 : 0;
-  check_rc(dllm_gemm_w4(&P, b_kmajor ? 1 : 0, stream()), "gemm_w4");
+  check_rc(dllm_gemm_w4(&P, b_kmajor ? 1 : 0, persist ? 1 : 0, stream()), "gemm_w4");
   return c;
 }
 
@@ -847,7 +847,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_fused_variant", &gemm_fused_variant, "default kernel variant for reduction length K");
   m.def("gemm_w4", &gemm_w4, "out (+)= a . b (+ bias) on the one-wave-per-SIMD GEMM (csrc/gemm_w4.hip)", py::arg("a"),
         py::arg("b"), py::arg("b_kmajor"), py::arg("bias") = py::none(), py::arg("out") = py::none(),
-        py::arg("accumulate") = false, py::arg("grp") = -1);
+        py::arg("accumulate") = false, py::arg("grp") = -1, py::arg("persist") = true);
   m.def("gemm_w4_supported", &gemm_w4_supported);
   m.def("colsum_acc", &colsum_acc, "out += x.sum(0) for a token-major bf16 x (bias gradients)");
   dllm::bind_reducer(m);

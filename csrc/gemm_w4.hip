@@ -115,26 +115,42 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = w >> 1, wn = w & 1;
-
-  // ---- tile of this workgroup
-  const int vt = xcd_remap(blockIdx.x, gridDim.x);
-  int mb = vt / P.tn, nb = vt % P.tn;
-  if (P.grp > 0) {  // the tiles an XCD runs at once cover a grp x (32 / grp) block (L2 reuse of A and B)
-    const int gs = P.grp * P.tn, g = vt / gs, r = vt % gs;
-    const int rows = min(P.grp, P.tm - g * P.grp);
-    mb = g * P.grp + r % rows;
-    nb = r / rows;
-  }
-  const int m0 = mb * 256, n0 = nb * 256;
   const int nk = P.K / BK;
 
-  // ---- descriptors (scalar) and per-lane DMA offsets.  Row image ([256][64], 128-B rows): wave-instruction q covers
-  // rows 8q .. 8q+7, lane -> (row 8q + l/8, 16-B chunk (l%8) ^ ((row/2)&7)).  K-major image ([64][256], 512-B rows):
-  // instruction q covers k-rows 2q, 2q+1, lane -> (k-row 2q + l/32, chunk (l%32) ^ gsw(k-row)).
-  const i32x4 srdA = make_srd(P.A + (long)m0 * P.lda, (uint32_t)(min(P.M - m0, 256) * P.lda * 2));
-  const i32x4 srdB = BKM ? make_srd(P.B + n0, (uint32_t)(((long)P.K * P.ldb - n0) * 2))
-                         : make_srd(P.B + (long)n0 * P.ldb, (uint32_t)(min(P.N - n0, 256) * P.ldb * 2));
+  // ---- tiles of this workgroup.  Blocks are dealt round-robin over the 8 XCDs (b % 8 share one), so XCD x takes a
+  // contiguous range of virtual tiles and its slot-th workgroup walks vbase + slot, + nwx, ... (grid == #tiles: one
+  // tile each, the bijective XCD remap); virtual tile -> (row block, column block) in groups of grp row blocks,
+  // column-major inside a group, so the 32 tiles an XCD runs at once share A and B panels in its L2.
+  const int T = P.tm * P.tn, G = gridDim.x, bid = blockIdx.x, xcd = bid % 8, slot = bid / 8;
+  const int nwx = G / 8 + (xcd < G % 8 ? 1 : 0);
+  const int ntx = T / 8 + (xcd < T % 8 ? 1 : 0);
+  const int vbase = xcd * (T / 8) + min(xcd, T % 8) + slot;
+  const int ntw = slot < ntx ? (ntx - slot + nwx - 1) / nwx : 0;
+  if (ntw == 0) return;
+  auto tile_mn = [&](int i, int& m0, int& n0) {
+    const int vt = vbase + i * nwx;
+    int mb = vt / P.tn, nb = vt % P.tn;
+    if (P.grp > 0) {
+      const int gs = P.grp * P.tn, g = vt / gs, r = vt % gs;
+      const int rows = min(P.grp, P.tm - g * P.grp);
+      mb = g * P.grp + r % rows;
+      nb = r / rows;
+    }
+    m0 = mb * 256;
+    n0 = nb * 256;
+  };
+  auto srd_a = [&](int m0) { return make_srd(P.A + (long)m0 * P.lda, (uint32_t)(min(P.M - m0, 256) * P.lda * 2)); };
+  auto srd_b = [&](int n0) {
+    return BKM ? make_srd(P.B + n0, (uint32_t)(((long)P.K * P.ldb - n0) * 2))
+               : make_srd(P.B + (long)n0 * P.ldb, (uint32_t)(min(P.N - n0, 256) * P.ldb * 2));
+  };
+
+  // ---- per-lane DMA offsets.  Row image ([256][64], 128-B rows): wave-instruction q covers rows 8q .. 8q+7,
+  // lane -> (row 8q + l/8, 16-B chunk (l%8) ^ ((row/2)&7)).  K-major image ([64][256], 512-B rows): instruction q covers
+  // k-rows 2q, 2q+1, lane -> (k-row 2q + l/32, chunk (l%32) ^ gsw(k-row)); columns past N read 0 (offset pushed out of
+  // range per tile: colb).
   uint32_t va[8], vb[8];
+  int colb[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int q = w * 8 + i;
@@ -143,20 +159,22 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
     va[i] = (uint32_t)(r * P.lda + c * 8) * 2u;
     if (BKM) {
       const int kr = 2 * q + (lane >> 5);
-      const int col = ((lane & 31) ^ gsw(kr)) * 8;
-      vb[i] = n0 + col < P.N ? (uint32_t)(kr * P.ldb + col) * 2u : kOOB;
+      colb[i] = ((lane & 31) ^ gsw(kr)) * 8;
+      vb[i] = (uint32_t)(kr * P.ldb + colb[i]) * 2u;
     } else {
+      colb[i] = 0;
       vb[i] = (uint32_t)(r * P.ldb + c * 8) * 2u;
     }
   }
   const uint32_t lds0 = lds_addr(smem);
   const uint32_t kstepB = BKM ? (uint32_t)(BK * P.ldb * 2) : (uint32_t)(BK * 2);
-  // DMA of k-tile kt into buffer b: instruction i of operand X -> image bytes (8 w + i) * 1 KB
-  auto dma_a = [&](int i, int kt, int b) {
-    dma16(srdA, va[i] + (uint32_t)kt * (BK * 2), lds0 + (uint32_t)b * BUF + (uint32_t)(8 * w + i) * 1024u);
+  // DMA of k-tile kt of the tile (sa, sb, n0) into buffer b: instruction i of operand X -> image bytes (8 w + i) * 1 KB
+  auto dma_a = [&](const i32x4& sa, int i, int kt, int b) {
+    dma16(sa, va[i] + (uint32_t)kt * (BK * 2), lds0 + (uint32_t)b * BUF + (uint32_t)(8 * w + i) * 1024u);
   };
-  auto dma_b = [&](int i, int kt, int b) {
-    dma16(srdB, vb[i] + (uint32_t)kt * kstepB, lds0 + (uint32_t)b * BUF + TB + (uint32_t)(8 * w + i) * 1024u);
+  auto dma_b = [&](const i32x4& sb, int n0, int i, int kt, int b) {
+    const uint32_t off = BKM && n0 + colb[i] >= P.N ? kOOB : vb[i] + (uint32_t)kt * kstepB;
+    dma16(sb, off, lds0 + (uint32_t)b * BUF + TB + (uint32_t)(8 * w + i) * 1024u);
   };
 
   // ---- fragment reads.  Row image: a[i] = rows wm*128 + 16 i + (l & 15), k chunk kk/8 + (l >> 4), swizzled by
@@ -173,24 +191,32 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
   };
 
   f32x4 acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   bf16x8v fa0[8], fb0[8], fa1[8], fb1[8];
 
+  // ---- current / next tile.  The DMA stream runs on across tile boundaries: the last two k-tiles of a tile prefetch
+  // the first two of the next, which land while the wave rows run the epilogue.  Persistent mode needs nk >= 2
+  // (host-checked); with one tile per workgroup the prefetch past the end is clamped to the last k-tile.
+  int m0, n0, m1 = 0, n1 = 0;
+  tile_mn(0, m0, n0);
+  if (ntw > 1) tile_mn(1, m1, n1);
+  i32x4 sa0 = srd_a(m0), sb0 = srd_b(n0), sa1 = srd_a(m1), sb1 = srd_b(n1);
+  // source of the DMA for k-tile kt + 2 of tile i (tile-local numbering; >= nk means the next tile)
+  auto dma_next = [&](int i, int kt, int d, int b) {
+    const int kn = kt + 2;
+    const bool cross = kn >= nk && i + 1 < ntw;
+    const int kk = cross ? kn - nk : min(kn, nk - 1);
+    if (d < 8) dma_a(cross ? sa1 : sa0, d, kk, b);
+    else dma_b(cross ? sb1 : sb0, cross ? n1 : n0, d - 8, kk, b);
+  };
+
   // ---- prologue: k-tiles 0 and 1 in flight, wait for k-tile 0, read its first half
-  const int k1 = min(1, nk - 1);  // nk == 1: k-tile 0 again into buffer 1 (never read)
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    dma_a(i, 0, 0);
-    dma_b(i, 0, 0);
+  for (int d = 0; d < 16; ++d) {
+    if (d < 8) dma_a(sa0, d, 0, 0);
+    else dma_b(sb0, n0, d - 8, 0, 0);
   }
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    dma_a(i, k1, 1);
-    dma_b(i, k1, 1);
-  }
+  for (int d = 0; d < 16; ++d) dma_next(0, -1, d, 1);
   wait_vm<16>();
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
@@ -204,127 +230,161 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) mfma(acc[i][j], fb[j], fa[i]);
   };
-  // sub-step 0 of k-tile t (k 0..31, fragments fa0 / fb0): read the k 32..63 fragments into fa1 / fb1, two per chunk,
-  // B first (the next sub-step's first chunk needs all of B and a[0])
-  auto substep0 = [&](int b) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      chunk(fa0, fb0, i);
-      if (i < 4) {
-        fb1[2 * i] = rd_b(b, 1, 2 * i);
-        fb1[2 * i + 1] = rd_b(b, 1, 2 * i + 1);
-      } else {
-        fa1[2 * i - 8] = rd_a(b, 1, 2 * i - 8);
-        fa1[2 * i - 7] = rd_a(b, 1, 2 * i - 7);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  };
 
-  // every k-tile runs the same branch-free body (a peeled last k-tile makes the allocator re-assign all 256 AGPRs
-  // between loop and tail, ~600 v_accvgpr copies): the prefetch index is clamped, so the last k-tiles re-load k-tile
-  // nk-1 into the buffer their predecessor just left, and the last k-tile's "next fragments" are read and dropped
-  // do-while: nk >= 1 (host-checked); with a for loop the zero-trip path keeps a VGPR copy of the zero accumulators
-  // alive and the allocator shuffles all 256 of them at the loop exit
-  int t = 0;
-  do {
-    // the accumulator zeroing (v_accvgpr_write, sunk by the compiler next to the loop) must be 2+ wait states before
-    // the first asm MFMA reads it as C; hipcc cannot see that read
-    asm volatile("s_nop 2" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    const int b = t & 1;
-    substep0(b);
-    // sub-step 1 (k 32..63, fa1 / fb1).  After its first chunk: k-tile t+1 landed (its DMA was the last issued) and
-    // every wave is past its reads of buffer b -> barrier; then DMA k-tile t+2 into buffer b and read k-tile t+1's
-    // first half into fa0 / fb0, spread over the remaining 7 chunks
-    chunk(fa1, fb1, 0);
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    const int kn = min(t + 2, nk - 1);
+  int g = 0;  // global k-tile counter (buffer parity)
+  int ti = 0;
+  do {  // tiles
 #pragma unroll
-    for (int i = 1; i < 8; ++i) {
-      chunk(fa1, fb1, i);
-      // DMA: instructions 0..7 of A then of B, spread over chunks 1..7 (2, 2, 2, 3, 2, 2, 3)
-      const int lo = (i - 1) * 16 / 7, hi = i * 16 / 7;
+    for (int i = 0; i < 8; ++i)
 #pragma unroll
-      for (int d = lo; d < hi; ++d) {
-        if (d < 8) dma_a(d, kn, b);
-        else dma_b(d - 8, kn, b);
-      }
-      // fragments of k-tile t+1 (buffer b ^ 1), first half: B in chunks 1..4, A in chunks 5..7
-      if (i <= 4) {
-        fb0[2 * i - 2] = rd_b(b ^ 1, 0, 2 * i - 2);
-        fb0[2 * i - 1] = rd_b(b ^ 1, 0, 2 * i - 1);
-      } else if (i < 7) {
-        fa0[3 * (i - 5)] = rd_a(b ^ 1, 0, 3 * (i - 5));
-        fa0[3 * (i - 5) + 1] = rd_a(b ^ 1, 0, 3 * (i - 5) + 1);
-        fa0[3 * (i - 5) + 2] = rd_a(b ^ 1, 0, 3 * (i - 5) + 2);
-      } else {
-        fa0[6] = rd_a(b ^ 1, 0, 6);
-        fa0[7] = rd_a(b ^ 1, 0, 7);
-      }
+      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // every k-tile runs the same branch-free body: a peeled last k-tile makes the allocator re-assign all 256 AGPRs
+    // between loop and tail (~600 v_accvgpr copies), and with a zero-trip path it keeps a VGPR copy of the zeroed
+    // accumulators alive (do-while, nk >= 1)
+    int kt = 0;
+    do {
+      // the accumulator zeroing (v_accvgpr_write) must be 2+ wait states before the first asm MFMA reads it as C; hipcc
+      // cannot see that read
+      asm volatile("s_nop 2" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
-    }
-  } while (++t < nk);
-  wait_vm<0>();  // the clamped re-loads of the last k-tile
-
-  // the last MFMAs' results are read by VALU below: 8-pass XDL write -> VALU read needs 11 wait states, which
-  // hipcc cannot see through the asm
-  asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
-  // ---- epilogue.  acc[i][j][r] = C[m0 + wm*128 + 16 i + (l & 15)][n0 + wn*128 + 16 j + 4 (l >> 4) + r].
-  // Row blocks 2ii / 2ii+1 packed to bf16 and exchanged with v_permlane16_swap (odd 16-lane rows of X <-> even rows
-  // of Y): afterwards lane l holds 8 consecutive columns 16 j + 8 (qd >> 1) of row 32 ii + 16 (qd & 1) + (l & 15).
-  __builtin_amdgcn_sched_barrier(0);
-  const int mrow = m0 + wm * 128 + 16 * (qd & 1) + rl;
-  const int ncol = n0 + wn * 128 + 8 * (qd >> 1);
-  f32x4 bv[8];
+      const int b = g & 1;
+      // sub-step 0 (k 0..31, fragments fa0 / fb0): read the k 32..63 fragments into fa1 / fb1, two per chunk, B first
+      // (the next sub-step's first chunk needs all of B and a[0])
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    bv[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if constexpr (BIAS) {
-      const int nb4 = n0 + wn * 128 + 16 * j + 4 * qd;
-      if (nb4 < P.N) bv[j] = Elem<uint16_t>::load4(P.bias + nb4);
-    }
-  }
-#pragma unroll
-  for (int ii = 0; ii < 4; ++ii) {
-    const int m = mrow + 32 * ii;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const f32x4 x = acc[2 * ii][j] + bv[j], y = acc[2 * ii + 1][j] + bv[j];
-      uint32_t x0 = pk2(x.x, x.y), x1 = pk2(x.z, x.w), y0 = pk2(y.x, y.y), y1 = pk2(y.z, y.w);
-      {
-        const auto r0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
-        const auto r1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
-        x0 = r0[0];
-        y0 = r0[1];
-        x1 = r1[0];
-        y1 = r1[1];
-      }
-      const int n = ncol + 16 * j;
-      if (m < P.M && n < P.N) {
-        uint16_t* cp = P.C + (long)m * P.ldc + n;
-        u32x4 o = {x0, x1, y0, y1};
-        if constexpr (ACC) {
-          const u32x4 c = *reinterpret_cast<const u32x4*>(cp);
-          auto add2 = [](uint32_t u, uint32_t v) {
-            return pk2(bf2f((uint16_t)(u & 0xFFFFu)) + bf2f((uint16_t)(v & 0xFFFFu)),
-                       bf2f((uint16_t)(u >> 16)) + bf2f((uint16_t)(v >> 16)));
-          };
-          o = u32x4{add2(o.x, c.x), add2(o.y, c.y), add2(o.z, c.z), add2(o.w, c.w)};
+      for (int i = 0; i < 8; ++i) {
+        chunk(fa0, fb0, i);
+        if (i < 4) {
+          fb1[2 * i] = rd_b(b, 1, 2 * i);
+          fb1[2 * i + 1] = rd_b(b, 1, 2 * i + 1);
+        } else {
+          fa1[2 * i - 8] = rd_a(b, 1, 2 * i - 8);
+          fa1[2 * i - 7] = rd_a(b, 1, 2 * i - 7);
         }
-        *reinterpret_cast<u32x4*>(cp) = o;
+        __builtin_amdgcn_sched_barrier(0);
       }
-      // bound the live ranges: otherwise the scheduler hoists all 256 accumulator reads and runs out of VGPRs
-      if (j & 1) __builtin_amdgcn_sched_barrier(0);
+      // sub-step 1 (k 32..63, fa1 / fb1).  After its first chunk: k-tile g+1 landed (its DMA was the last issued; after
+      // an epilogue its 32 stores are queued behind it) and every wave is past its reads of buffer b -> barrier; then
+      // DMA k-tile g+2 into buffer b and read k-tile g+1's first half into fa0 / fb0, spread over the remaining 7 chunks
+      chunk(fa1, fb1, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (kt == 0 && g > 0 && !ACC) asm volatile("s_waitcnt vmcnt(32) lgkmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 1; i < 8; ++i) {
+        chunk(fa1, fb1, i);
+        // DMA: instructions 0..7 of A then of B, spread over chunks 1..7 (2, 2, 2, 3, 2, 2, 3)
+        const int lo = (i - 1) * 16 / 7, hi = i * 16 / 7;
+#pragma unroll
+        for (int d = lo; d < hi; ++d) dma_next(ti, kt, d, b);
+        // fragments of k-tile g+1 (buffer b ^ 1), first half: B in chunks 1..4, A in chunks 5..7
+        if (i <= 4) {
+          fb0[2 * i - 2] = rd_b(b ^ 1, 0, 2 * i - 2);
+          fb0[2 * i - 1] = rd_b(b ^ 1, 0, 2 * i - 1);
+        } else if (i < 7) {
+          fa0[3 * (i - 5)] = rd_a(b ^ 1, 0, 3 * (i - 5));
+          fa0[3 * (i - 5) + 1] = rd_a(b ^ 1, 0, 3 * (i - 5) + 1);
+          fa0[3 * (i - 5) + 2] = rd_a(b ^ 1, 0, 3 * (i - 5) + 2);
+        } else {
+          fa0[6] = rd_a(b ^ 1, 0, 6);
+          fa0[7] = rd_a(b ^ 1, 0, 7);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      ++g;
+    } while (++kt < nk);
+
+    // the last MFMAs' results are read by VALU below: 8-pass XDL write -> VALU read needs 11 wait states, which
+    // hipcc cannot see through the asm
+    asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- epilogue.  acc[i][j][r] = C[m0 + wm*128 + 16 i + (l & 15)][n0 + wn*128 + 16 j + 4 (l >> 4) + r].
+    // Row blocks 2ii / 2ii+1 packed to bf16 and exchanged with v_permlane16_swap (odd 16-lane rows of X <-> even rows
+    // of Y): afterwards lane l holds 8 consecutive columns 16 j + 8 (qd >> 1) of row 32 ii + 16 (qd & 1) + (l & 15).
+    // Stores through a buffer descriptor over the tile's rows: rows past M fall out of its range, columns past N are
+    // pushed out per lane, so every wave issues exactly 32 stores (the vmcnt(32) above counts them).
+    {
+      // descriptor inputs made provably wave-uniform (readfirstlane), or hipcc wraps every store in a waterfall loop
+      const uint64_t cb = (uint64_t)(P.C + (long)m0 * P.ldc);
+      const uint32_t clo = __builtin_amdgcn_readfirstlane((uint32_t)cb), chi = __builtin_amdgcn_readfirstlane((uint32_t)(cb >> 32));
+      const __amdgpu_buffer_rsrc_t srdC = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(((uint64_t)chi << 32) | clo), (short)0,
+          (int)__builtin_amdgcn_readfirstlane((uint32_t)(min(P.M - m0, 256) * P.ldc * 2)), 0x00020000);
+      const int mr = wm * 128 + 16 * (qd & 1) + rl;  // tile-local row of ii = 0
+      const int nc = wn * 128 + 8 * (qd >> 1);       // tile-local column of j = 0
+      f32x4 bv[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        bv[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if constexpr (BIAS) {
+          const int nb4 = n0 + wn * 128 + 16 * j + 4 * qd;
+          if (nb4 < P.N) bv[j] = Elem<uint16_t>::load4(P.bias + nb4);
+        }
+      }
+#pragma unroll
+      for (int ii = 0; ii < 4; ++ii) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          // opaque re-definition in place: the AGPR -> VGPR copies cannot be hoisted above this point (otherwise all 256
+          // accumulators are copied out at the loop exit: 256 VGPRs + spills)
+          asm volatile("" : "+a"(acc[2 * ii][j]), "+a"(acc[2 * ii + 1][j]));
+          const f32x4 xv = acc[2 * ii][j] + bv[j], yv = acc[2 * ii + 1][j] + bv[j];
+          uint32_t x0 = pk2(xv.x, xv.y), x1 = pk2(xv.z, xv.w), y0 = pk2(yv.x, yv.y), y1 = pk2(yv.z, yv.w);
+          {
+            const auto r0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
+            const auto r1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
+            x0 = r0[0];
+            y0 = r0[1];
+            x1 = r1[0];
+            y1 = r1[1];
+          }
+          const int nl = nc + 16 * j;
+          const uint32_t off = n0 + nl < P.N ? (uint32_t)((mr + 32 * ii) * P.ldc + nl) * 2u : kOOB;
+          u32x4 o = {x0, x1, y0, y1};
+          if constexpr (ACC) {
+            const u32x4 c = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(srdC, off, 0, 0));
+            auto add2 = [](uint32_t u, uint32_t v) {
+              return pk2(bf2f((uint16_t)(u & 0xFFFFu)) + bf2f((uint16_t)(v & 0xFFFFu)),
+                         bf2f((uint16_t)(u >> 16)) + bf2f((uint16_t)(v >> 16)));
+            };
+            o = u32x4{add2(o.x, c.x), add2(o.y, c.y), add2(o.z, c.z), add2(o.w, c.w)};
+          }
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, o), srdC, off, 0, 0);
+          // bound the live ranges
+          if (j & 1) __builtin_amdgcn_sched_barrier(0);
+        }
+      }
     }
-  }
+    __builtin_amdgcn_sched_barrier(0);
+    // next tile becomes current
+    m0 = m1;
+    n0 = n1;
+    sa0 = sa1;
+    sb0 = sb1;
+    if (ti + 2 < ntw) {
+      tile_mn(ti + 2, m1, n1);
+      sa1 = srd_a(m1);
+      sb1 = srd_b(n1);
+    }
+  } while (++ti < ntw);
+  wait_vm<0>();  // clamped prefetches of the last tile may still be landing in LDS
 }
 
+int num_cus() {
+  static int n = [] {
+    int dev = 0, cus = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    return cus > 0 ? cus : 256;
+  }();
+  return n;
+}
+
+// persist: one workgroup per CU (LDS and registers admit one) walking its tiles, when there are more tiles than CUs
+// and at least 2 k-tiles per tile; otherwise one tile per workgroup
 template <bool BKM, bool BIAS, bool ACC>
-int launch(const GemmW4Params& p, hipStream_t st) {
+int launch(const GemmW4Params& p, bool persist, hipStream_t st) {
   constexpr size_t lds = 2 * 2 * 256 * BK * 2;  // 128 KB
   static bool attr = false;
   if (!attr) {
@@ -332,21 +392,23 @@ int launch(const GemmW4Params& p, hipStream_t st) {
                               (int)lds);
     attr = true;
   }
-  hipLaunchKernelGGL((gemm_w4_kernel<BKM, BIAS, ACC>), dim3(p.tm * p.tn), dim3(NT), lds, st, p);
+  const int T = p.tm * p.tn, cus = num_cus() / 8 * 8;
+  const int grid = persist && p.K >= 2 * BK && cus >= 8 && T > cus ? cus : T;
+  hipLaunchKernelGGL((gemm_w4_kernel<BKM, BIAS, ACC>), dim3(grid), dim3(NT), lds, st, p);
   DLLM_CHECK_LAUNCH();
   return 0;
 }
 
 template <bool BKM>
-int dispatch(const GemmW4Params& p, hipStream_t st) {
-  if (p.accumulate) return p.bias ? launch<BKM, true, true>(p, st) : launch<BKM, false, true>(p, st);
-  return p.bias ? launch<BKM, true, false>(p, st) : launch<BKM, false, false>(p, st);
+int dispatch(const GemmW4Params& p, bool persist, hipStream_t st) {
+  if (p.accumulate) return p.bias ? launch<BKM, true, true>(p, persist, st) : launch<BKM, false, true>(p, persist, st);
+  return p.bias ? launch<BKM, true, false>(p, persist, st) : launch<BKM, false, false>(p, persist, st);
 }
 
 }  // namespace
 
-extern "C" int dllm_gemm_w4(const GemmW4Params* pp, int b_kmajor, hipStream_t st) {
+extern "C" int dllm_gemm_w4(const GemmW4Params* pp, int b_kmajor, int persist, hipStream_t st) {
   const GemmW4Params& p = *pp;
   if (p.M <= 0 || p.N <= 0 || p.K <= 0 || p.K % BK || p.N % 8 || p.tm * 256 < p.M || p.tn * 256 < p.N) return -4;
-  return b_kmajor ? dispatch<true>(p, st) : dispatch<false>(p, st);
+  return b_kmajor ? dispatch<true>(p, persist != 0, st) : dispatch<false>(p, persist != 0, st);
 }

@@ -19,9 +19,12 @@
 #include <torch/csrc/autograd/functions/accumulate_grad.h>
 #include <torch/csrc/autograd/utils/lambda_post_hook.h>
 #include <torch/csrc/distributed/c10d/ProcessGroup.hpp>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime_api.h>
 
 #include <dlfcn.h>
 
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <mutex>
@@ -95,12 +98,33 @@ class NativeReducer {
   }
 
   // End of backward (queued on the engine): launch leftovers in order, order the compute stream after them.
+  // With timing on (GPU buffers only) two events bracket that wait on the compute stream: the first fires when the
+  // last backward kernel has run, the second when the last bucket's all-reduce has — their distance is the
+  // communication NOT hidden under backward ("exposed" ms, bench.py reports it per step).
   void finalize() {
     std::lock_guard<std::mutex> g(mu_);
     const int64_t nb = num_buckets();
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    const bool timed = timing_ && grad_buf_.is_cuda();
+    hipStream_t st = nullptr;
+    if (timed) {
+      st = c10::hip::getCurrentHIPStream(grad_buf_.device().index()).stream();
+      if (hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess) {
+        (void)hipEventRecord(e0, st);
+      } else {
+        e0 = e1 = nullptr;
+      }
+    }
+    const auto h0 = std::chrono::steady_clock::now();
     while (next_ < nb) launch_locked(next_++);
     for (auto& w : works_) w->wait();
     works_.clear();
+    if (timed && e0) {
+      (void)hipEventRecord(e1, st);
+      events_.emplace_back(e0, e1);
+    } else if (timing_ && !grad_buf_.is_cuda()) {  // CPU (gloo) rehearsal: wait() blocks the host
+      host_ms_.push_back(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count());
+    }
     if (average_ && !use_avg_op_) grad_buf_.div_(pg_->getSize());
     reset_state();
   }
@@ -117,6 +141,25 @@ class NativeReducer {
   void set_enabled(bool e) {
     std::lock_guard<std::mutex> g(mu_);
     enabled_ = e;
+  }
+  void set_timing(bool on) {
+    std::lock_guard<std::mutex> g(mu_);
+    timing_ = on;
+  }
+  // exposed-communication ms of every timed backward since the last call (blocks until their events completed)
+  std::vector<double> take_exposed_ms() {
+    std::lock_guard<std::mutex> g(mu_);
+    std::vector<double> out(host_ms_);
+    host_ms_.clear();
+    for (auto& pr : events_) {
+      float ms = 0.f;
+      if (hipEventSynchronize(pr.second) == hipSuccess && hipEventElapsedTime(&ms, pr.first, pr.second) == hipSuccess)
+        out.push_back((double)ms);
+      (void)hipEventDestroy(pr.first);
+      (void)hipEventDestroy(pr.second);
+    }
+    events_.clear();
+    return out;
   }
   bool enabled() const { return enabled_; }
   int64_t num_buckets() const { return (int64_t)bounds_.size() / 2; }
@@ -154,6 +197,9 @@ class NativeReducer {
   c10::intrusive_ptr<c10d::ProcessGroup> pg_;
   bool average_, use_avg_op_;
   bool enabled_ = true;
+  bool timing_ = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> events_;
+  std::vector<double> host_ms_;
   bool callback_queued_ = false;
   int64_t next_ = 0;
   std::vector<c10::intrusive_ptr<c10d::Work>> works_;
@@ -173,6 +219,8 @@ void bind_reducer(pybind11::module& m) {
       .def("finalize", &NativeReducer::finalize, py::call_guard<py::gil_scoped_release>())
       .def("sync_all", &NativeReducer::sync_all, py::call_guard<py::gil_scoped_release>())
       .def("set_enabled", &NativeReducer::set_enabled)
+      .def("set_timing", &NativeReducer::set_timing)
+      .def("take_exposed_ms", &NativeReducer::take_exposed_ms, py::call_guard<py::gil_scoped_release>())
       .def("enabled", &NativeReducer::enabled)
       .def("num_buckets", &NativeReducer::num_buckets)
       .def("launched", &NativeReducer::launched)

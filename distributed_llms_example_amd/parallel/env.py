@@ -92,8 +92,10 @@ def init_distributed(init_method: str | None = None, rank: int | None = None, wo
         if be == "nccl":
             kw["device_id"] = device
         dist.init_process_group(**kw)
+    if dist.is_initialized():  # a process group set up by the caller (or just now) is the truth
         rk = dist.get_rank()
         ws = dist.get_world_size()
+        be = dist.get_backend()
     _ENV = DistEnv(rank=rk, world_size=ws, local_rank=local_rank, local_world_size=local_ws,
                    backend=be if ws > 1 else "none", device=device)
     return _ENV

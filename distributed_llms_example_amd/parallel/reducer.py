@@ -27,8 +27,8 @@ reference and for A/B tests).  Bucket layout is computed here once and handed to
 from __future__ import annotations
 
 import contextlib
-
 import os
+import time
 
 import torch
 import torch.distributed as dist
@@ -68,6 +68,9 @@ class GradReducer:
         self.ready_log_last: list[int] = []
         self.launch_log_last: list[tuple[int, int]] = []
         self.rebuilt = False
+        self.timing = False  # set_timing(): exposed-communication events around the end-of-backward wait
+        self._events: list = []
+        self._host_ms: list[float] = []
         self._manual = []
         self._hooks = []
         self.native = None
@@ -185,11 +188,21 @@ class GradReducer:
         """End of backward: launch what is left (unused params) in order, wait on the GPU stream."""
         if self.world <= 1:
             return
+        ev = None
+        if self.timing and self.flat.grad_buf.is_cuda:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
+        h0 = time.perf_counter()
         while self._next < len(self.buckets):
             self._launch(self._next)
             self._next += 1
         for _, w in self._works:
             w.wait()
+        if ev is not None:
+            ev[1].record()
+            self._events.append(ev)
+        elif self.timing:  # CPU (gloo) rehearsal: wait() blocks the host
+            self._host_ms.append((time.perf_counter() - h0) * 1e3)
         if self.average and self.backend != "nccl":
             self.flat.grad_buf.div_(self.world)
         self._works.clear()
@@ -249,6 +262,40 @@ class GradReducer:
         if module is not None:
             for b in module.buffers():
                 dist.broadcast(b.data, src=src, group=self.group)
+
+    def set_timing(self, on: bool = True):
+        """Bracket the end-of-backward wait with GPU events: ``take_exposed_ms()`` then returns, per synchronised
+        backward, the ms between the last backward kernel and the last bucket's all-reduce completing on the compute
+        stream (communication not hidden under backward)."""
+        self.timing = bool(on)
+        if self.native is not None:
+            self.native.set_timing(self.timing)
+
+    def take_exposed_ms(self) -> list[float]:
+        if self.native is not None:
+            return list(self.native.take_exposed_ms())
+        out, self._host_ms = list(self._host_ms), []
+        for e0, e1 in self._events:
+            e1.synchronize()
+            out.append(e0.elapsed_time(e1))
+        self._events.clear()
+        return out
+
+    def layout_signature(self) -> list[int]:
+        """Bucket bounds + segment sizes: must be identical on every rank (RCCL matches collectives by order and
+        size; a mismatch deadlocks or silently mixes gradients)."""
+        sig = [len(self.buckets)] + [x for se in self.buckets for x in se]
+        sig += [s.numel for s in self.flat.segments]
+        return sig
+
+    def launch_summary(self) -> dict:
+        """The last synchronised backward's launch timeline: for each bucket (launch order) the fraction of gradient
+        segments that were ready when it launched.  Overlap works when early buckets launch at small fractions."""
+        n = max(1, len(self.flat.segments))
+        log = self.launch_log_last
+        fr = [round(k / n, 3) for _, k in log]
+        return {"order": [b for b, _ in log], "ready_frac_at_launch": fr,
+                "launched_before_backward_end": sum(1 for x in fr if x < 1.0), "n_buckets": len(self.buckets)}
 
     def bucket_sizes_mb(self) -> list[float]:
         esz = self.flat.grad_buf.element_size()

@@ -289,3 +289,53 @@ def test_divergent_collective_is_reported():
     out = run_ranks(_divergent_collective, env=_DEBUG_ENV)
     for r in (0, 1):
         assert out[r].startswith("caught:") and "mismatch" in out[r].lower(), out[r]
+
+
+# ---------------------------------------------------------------- bench.py multi-rank self-diagnosis (gloo rehearsal)
+def _bench_consistency_case(rank, world):
+    import bench
+    from distributed_llms_example_amd.models import build_model
+    from distributed_llms_example_amd.parallel.env import init_distributed
+    from distributed_llms_example_amd.train.engine import TrainEngine
+    env = init_distributed()
+    eng = TrainEngine(build_model("t5-tiny"), env, dtype=torch.float32, bucket_mb=0.05)
+    ok = bench.check_rank_consistency(env, eng, "t5-tiny", 4)
+    try:  # rank 1 claims another micro-batch: every rank must refuse, naming the field and the ranks
+        bench.check_rank_consistency(env, eng, "t5-tiny", 4 + rank)
+        bad = None
+    except SystemExit as e:
+        bad = str(e)
+    return ok["status"], ok["n_buckets"], bad
+
+
+def test_bench_rank_consistency_check():
+    out = run_ranks(_bench_consistency_case, world=2)
+    for r in (0, 1):
+        status, nb, bad = out[r]
+        assert status == "ok" and nb >= 2
+        assert bad is not None and "per_gpu_batch" in bad and '"0": 4' in bad and '"1": 5' in bad
+
+
+def test_bench_multirank_diagnostics_on_gloo():
+    """bench.py under torchrun with 2 CPU ranks: the JSON line carries the exposed-communication time, the bucket
+    launch timeline and the consistency verdict (the fields the driver's 8-GPU run reports)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, DLLM_FORCE_CPU="1", OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr=127.0.0.1",
+           f"--master-port={_free_port()}", os.path.join(root, "bench.py"), "--gpus", "2", "--model", "t5-tiny",
+           "--steps", "2", "--warmup", "2", "--batch-per-gpu", "2", "--src-len", "32", "--tgt-len", "8",
+           "--bucket-mb", "0.1", "--grad-accum", "2"]
+    r = subprocess.run(cmd, env=env, cwd=root, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:]
+    line = next(l for l in r.stdout.splitlines() if l.startswith("{") and '"metric"' in l)
+    d = json.loads(line)
+    assert d["n_gpus"] == 2 and d["config"]["grad_accum"] == 2 and d["config"]["global_batch"] == 8
+    c = d["comm"]
+    assert c["consistency"]["status"] == "ok"
+    assert c["timed_backwards"] == 2 and c["exposed_ms_per_step"] >= 0 and 0 <= c["exposed_frac"] < 1
+    bl = c["bucket_launch"]
+    assert bl["n_buckets"] >= 2 and sorted(bl["order"]) == list(range(bl["n_buckets"]))
+    assert bl["ready_frac_at_launch"][-1] == 1.0 and bl["launched_before_backward_end"] >= 1

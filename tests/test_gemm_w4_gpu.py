@@ -18,7 +18,10 @@ def _rel(a, b):
 
 
 SHAPES = [(256, 64, 256), (512, 128, 512), (300, 192, 264), (1000, 768, 2304), (64, 64, 8), (257, 64, 520),
-          (4096, 1024, 1024), (768, 3072, 768)]
+          (4096, 1024, 1024), (768, 3072, 768),
+          # > 256 tiles: the persistent form (one workgroup per CU walking 1-2 tiles, DMA crossing tile boundaries;
+          # K = 128 crosses at every other k-tile), ragged M / N on the last tiles
+          (8192, 128, 2304), (9000, 192, 2000), (70000, 64, 264)]
 
 
 @pytest.mark.parametrize("M,K,N", SHAPES)
@@ -39,6 +42,9 @@ def test_gemm_w4(M, K, N, kmajor, bias, acc):
         ref = ref + out.float()
     assert C.gemm_w4_supported(a, b, kmajor)
     got = C.gemm_w4(a, b, kmajor, bv, out, acc)
+    if not acc:  # one tile per workgroup: the same numbers
+        again = C.gemm_w4(a, b, kmajor, bv, None, False, -1, False)
+        assert torch.equal(again, got)
     if acc:
         assert got.data_ptr() == out.data_ptr()
     assert got.shape == (M, N)

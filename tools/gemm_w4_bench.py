@@ -60,12 +60,14 @@ def main():
         for phase in a.phases.split(","):
             if phase == "fwd":
                 fl = 2.0 * M * K * N
-                arms = {"lib": lambda: F.linear(x, w), "w4": lambda: C.gemm_w4(x, w, False, None, None, False, a.grp)}
+                arms = {"lib": lambda: F.linear(x, w), "w4": lambda: C.gemm_w4(x, w, False, None, None, False, a.grp),
+                        "w4np": lambda: C.gemm_w4(x, w, False, None, None, False, a.grp, False)}
                 if C.gemm_fused_supported(x, w, False):
                     arms["pp9"] = lambda: C.gemm_fused(x, w, False, 0, None, None, None, 0.0, 0, 9)
             else:
                 fl = 2.0 * M * K * N
-                arms = {"lib": lambda: torch.matmul(dy, w), "w4": lambda: C.gemm_w4(dy, w, True, None, None, False, a.grp)}
+                arms = {"lib": lambda: torch.matmul(dy, w), "w4": lambda: C.gemm_w4(dy, w, True, None, None, False, a.grp),
+                        "w4np": lambda: C.gemm_w4(dy, w, True, None, None, False, a.grp, False)}
                 if C.gemm_fused_supported(dy, w, True):
                     arms["pp9"] = lambda: C.gemm_fused(dy, w, True, 0, None, None, None, 0.0, 0, 9)
             ref = arms["lib"]().float()
