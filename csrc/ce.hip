@@ -88,6 +88,13 @@ __global__ __launch_bounds__(256) void ce_bwd_kernel(const float* __restrict__ s
   }
 }
 
+// bias[c0 + c .. + 3]: one 16-B load when that address is 16-B aligned, else four scalar loads (the ragged vocab tail
+// chunk starts at c0 = V - Vc, odd for BART's V = 50265)
+DLLM_DEVICE f32x4 bias4(const float* __restrict__ bias, int i) {
+  if ((i & 3) == 0) return *reinterpret_cast<const f32x4*>(bias + i);
+  return f32x4{bias[i], bias[i + 1], bias[i + 2], bias[i + 3]};
+}
+
 // ---- vocab-chunked LM head + CE (ops/lm_head.py): the logits exist one [N, Vc] chunk at a time
 // Per row running state st[row] = {max, sum exp(x - max), sum x, x_label} merged over chunks; the last chunk writes
 // loss_row and lse.  Chunk columns are global vocab ids c0 .. c0 + Vc - 1; eps / V uses the full vocab size.
@@ -103,7 +110,7 @@ __global__ __launch_bounds__(256) void ce_chunk_fwd_kernel(const uint16_t* __res
   float m = -INFINITY, s = 0.f, sx = 0.f;
   for (int c = threadIdx.x * 4; c < Vc; c += 256 * 4) {  // Vc % 4 == 0
     f32x4 v = Elem<uint16_t>::load4(x + c);
-    if (bias != nullptr) v += *reinterpret_cast<const f32x4*>(bias + c0 + c);
+    if (bias != nullptr) v += bias4(bias, c0 + c);
     if (c < skip) {  // leading columns already covered by the previous chunk (ragged vocab tail)
 #pragma unroll
       for (int k = 0; k < 4; ++k) v[k] = c + k < skip ? -INFINITY : v[k];
@@ -160,7 +167,7 @@ __global__ __launch_bounds__(256) void ce_chunk_bwd_kernel(const float* __restri
   const long yl = y - c0;
   for (int c = threadIdx.x * 4; c < Vc; c += 256 * 4) {
     f32x4 v = Elem<uint16_t>::load4(x + c);
-    if (bias != nullptr) v += *reinterpret_cast<const f32x4*>(bias + c0 + c);
+    if (bias != nullptr) v += bias4(bias, c0 + c);
     f32x4 r;
 #pragma unroll
     for (int k = 0; k < 4; ++k)

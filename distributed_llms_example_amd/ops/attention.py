@@ -185,18 +185,27 @@ def _prep_kpm(kpm):
     return kpm.contiguous() if kpm is not None else None
 
 
+def _native(t) -> bool:
+    """The HIP flash kernels take bf16.  Other dtypes on the GPU — fp32 training, the reference's own precision
+    (ref/train-torchrun.py:115-128 sets neither bf16 nor fp16; Accelerate's default mixed_precision is 'no') — are
+    routed explicitly to the fp32 composite below (scores, bias, masks and dropout in fp32; the GEMMs run as fp32
+    library matmuls), which is the exact-math oracle the bf16 kernels are tested against.  Memory is O(S^2) per head
+    there, fine at the reference's fp32 batch sizes (1-6 per GPU)."""
+    return _ext.use_native(t) and t.dtype == torch.bfloat16
+
+
 def attention(q, k, v, *, scale: float = 1.0, causal: bool = False, key_padding_mask=None, bias_lut=None,
               dropout_p: float = 0.0, seed: int = 0):
     """Multi-head attention.  q ``[B,Sq,H,D]``, k/v ``[B,Sk,H,D]``; ``key_padding_mask`` bool
     ``[B,Sk]`` (True = attend); ``bias_lut`` from :func:`relative_bias_lut`."""
-    if _ext.use_native(q):
+    if _native(q):
         return _AttnFn.apply("sep", q, k, v, bias_lut, _prep_kpm(key_padding_mask), scale, causal, dropout_p, seed)
     return _reference(q, k, v, scale, causal, key_padding_mask, bias_lut, dropout_p, seed)
 
 
 def attention_qkv(qkv, pre=None, **kw):
     """Self-attention on the fused projection output ``qkv`` = [B, S, 3, H, D]."""
-    if _ext.use_native(qkv):
+    if _native(qkv):
         return _AttnFn.apply("qkv", qkv, None, None, kw.get("bias_lut"), _prep_kpm(kw.get("key_padding_mask")),
                              kw.get("scale", 1.0), kw.get("causal", False), kw.get("dropout_p", 0.0), kw.get("seed", 0),
                              pre)
@@ -210,7 +219,7 @@ def prefetch_dropout_mask(like: torch.Tensor, B: int, H: int, Sq: int, Sk: int, 
     """``DLLM_ATTN_MASK_STREAM=1``: generate the attention-dropout keep bits for an upcoming call on a side HIP
     stream, so the VALU-only mask kernel overlaps the (MFMA-bound) projection GEMM issued meanwhile on the
     compute stream.  Returns a handle for ``attention_qkv(pre=...)`` or None (mask hashed inside the forward)."""
-    if p <= 0.0 or os.environ.get("DLLM_ATTN_MASK_STREAM", "0") != "1" or not _ext.use_native(like):
+    if p <= 0.0 or os.environ.get("DLLM_ATTN_MASK_STREAM", "0") != "1" or not _native(like):
         return None
     dev = like.device
     side = _SIDE.get(dev)
@@ -225,7 +234,7 @@ def prefetch_dropout_mask(like: torch.Tensor, B: int, H: int, Sq: int, Sk: int, 
 
 def attention_q_kv(q, kv, **kw):
     """Cross-attention with q = [B, Sq, H, D] and the fused key/value projection kv = [B, Sk, 2, H, D]."""
-    if _ext.use_native(q):
+    if _native(q):
         return _AttnFn.apply("q_kv", q, kv, None, kw.get("bias_lut"), _prep_kpm(kw.get("key_padding_mask")),
                              kw.get("scale", 1.0), kw.get("causal", False), kw.get("dropout_p", 0.0), kw.get("seed", 0))
     return attention(q, kv[:, :, 0], kv[:, :, 1], **kw)

@@ -135,7 +135,7 @@ def lm_head_loss(hidden: torch.Tensor, weight: torch.Tensor, labels: torch.Tenso
     if scale is not None:
         h = h * scale
     lab = labels.reshape(-1)
-    if not _ext.use_native(h):
+    if not _ext.use_native(h) or h.dtype != torch.bfloat16:  # the chunk kernels take bf16 logits; fp32: composite
         return _reference(h, weight, lab, bias, label_smoothing, ignore_index)
     params = None
     w = weight

@@ -54,11 +54,13 @@ class FlatParams:
         # decoder's per-layer cross-attention K/V weights) are placed back-to-back, in group order,
         # where the group's first member would have gone
         groups = module._dllm_param_groups() if hasattr(module, "_dllm_param_groups") else []
+        self.groups: list[list[int]] = []  # id()s of each stacked group, kept adjacent by relayout() too
         for grp in groups:
             ids = [id(p) for p in grp]
             pos = {id(p): i for i, (_, p) in enumerate(named)}
             if not all(i in pos for i in ids):
                 continue
+            self.groups.append(ids)
             first = min(pos[i] for i in ids)
             members = {id(p): (n, p) for n, p in named if id(p) in ids}
             rest = [(n, p) for n, p in named if id(p) not in members]
@@ -175,6 +177,7 @@ class FlatParams:
         gradient-ready order, parallel/reducer.py).  Parameters, gradients (values kept) and every registered
         companion buffer move together; parameter views and gradient slices are re-pointed."""
         assert sorted(order) == list(builtins_range(len(self.segments))), "order must be a permutation of segments"
+        order = self.keep_groups_adjacent(order)
         src = [seg.offset for seg in self.segments]
         dst, n = self._offsets(order)
         self.param_buf = self._permute(self.param_buf, src, dst, n)
@@ -190,6 +193,32 @@ class FlatParams:
             p.data = self.param_buf[seg.offset:seg.offset + seg.numel].view(seg.shape)
             p._dllm_gbuf = self.grad_view(i)
         self.attach_grads()
+        # a stacked group that is no longer one block would send ops/linear.py stacked_linear to its slow torch.cat
+        # path on every forward (same results): fail here instead
+        idx = {id(p): i for i, p in enumerate(self.params)}
+        for ids in self.groups:
+            at = [idx[i] for i in ids]
+            assert at == list(builtins_range(at[0], at[0] + len(at))), f"stacked parameter group split by relayout: {at}"
+
+    def keep_groups_adjacent(self, order: list[int]) -> list[int]:
+        """``order`` with every stacked group's members moved back-to-back (in group order) to where its first
+        member appears: the reducer's ready order interleaves them whenever another hook fires in between."""
+        if not self.groups:
+            return list(order)
+        seg_of = {id(p): i for i, p in enumerate(self.params)}
+        member = {}
+        for gi, ids in enumerate(self.groups):
+            for i in ids:
+                member[seg_of[i]] = gi
+        out, placed = [], set()
+        for i in order:
+            gi = member.get(i)
+            if gi is None:
+                out.append(i)
+            elif gi not in placed:
+                placed.add(gi)
+                out.extend(seg_of[j] for j in self.groups[gi])
+        return out
 
     def canonical_offsets(self) -> tuple[list[int], list[int], int]:
         """(current offsets, canonical offsets, canonical numel) per current segment."""

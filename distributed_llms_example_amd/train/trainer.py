@@ -151,7 +151,9 @@ class Trainer:
                                            pin_memory=self.env.device.type == "cuda"), sampler
 
     def _coalesce_cap(self) -> int | None:
-        """Max samples per forward/backward pass when coalescing micro-batches, None = off, -1 = decide after step 1."""
+        """Max padded tokens (samples x padded sequence lengths, _padded_tokens) per forward/backward pass when coalescing
+        micro-batches; None = off, -1 = decide after step 1.  An explicit integer setting counts micro-batches of the
+        configured batch size at the first group's padded lengths."""
         v = os.environ.get("DLLM_COALESCE_GA", self.args.coalesce_grad_accum)
         if self.cp_group is not None or self.args.gradient_accumulation_steps <= 1:
             return None
@@ -160,8 +162,21 @@ class Trainer:
         v = int(v)
         return v if v > 1 else None
 
-    def _auto_cap(self, base_bytes: int, peak_bytes: int) -> int | None:
-        """Samples per pass from the first step: peak - base = one micro-batch's activations (+ transient buffers)."""
+    @staticmethod
+    def _padded_tokens(batches) -> int:
+        """Tokens of ONE pass over ``batches`` after _merge pads every sequence dim to the group maximum: samples x
+        (max source length + max target length).  The coalescing budget is counted in these, not in samples, so a
+        later group of longer (dynamically padded) sequences cannot exceed the memory measured at step 1."""
+        n = sum(b["labels"].shape[0] for b in batches)
+        src = max((b["input_ids"].shape[1] for b in batches if "input_ids" in b), default=0)
+        tgt = max(b["labels"].shape[1] for b in batches)
+        return n * (src + tgt)
+
+    def _auto_cap(self, base_bytes: int, peak_bytes: int, step1_tokens: int) -> int | None:
+        """Padded-token budget per pass from the first step: peak - base = the activations of one micro-batch of the
+        step's largest padded size (+ transient buffers).  Attention memory grows faster than linearly with sequence
+        length (the S^2 score tiles are never materialised here, but the dropout bit planes are), so the budget keeps
+        a margin below the memory fraction."""
         total = torch.cuda.get_device_properties(self.env.device).total_memory
         act = max(1, peak_bytes - base_bytes)
         k = int((self.args.coalesce_memory_fraction * total - base_bytes) // act)
@@ -170,9 +185,10 @@ class Trainer:
             t = torch.tensor([k], device=self.env.device)
             dist.all_reduce(t, op=dist.ReduceOp.MIN)
             k = int(t)
-        logger.info(f"gradient accumulation: {k} micro-batches per forward/backward pass "
-                    f"(activations ~{act / 2**30:.1f} GiB per micro-batch, base {base_bytes / 2**30:.1f} GiB)")
-        return k * self.args.per_device_train_batch_size if k > 1 else None
+        logger.info(f"gradient accumulation: up to {k} micro-batches ({k * step1_tokens} padded tokens) per "
+                    f"forward/backward pass (activations ~{act / 2**30:.1f} GiB per micro-batch, base "
+                    f"{base_bytes / 2**30:.1f} GiB)")
+        return k * step1_tokens if k > 1 else None
 
     @staticmethod
     def _merge(group, pad_id: int):
@@ -236,11 +252,12 @@ class Trainer:
         eng.train()
         t_start = time.perf_counter()
         tr_loss_sum = torch.zeros((), device=env.device)
-        tr_loss_n = 0
+        tr_loss_n = torch.zeros((), device=env.device)
         total_loss_sum, total_loss_n = 0.0, 0
         last_norm = None
         ga = args.gradient_accumulation_steps
         cap = self._coalesce_cap()
+        cap_units = "micro" if cap is not None and cap > 0 else "tokens"
         if cap == -1 and self.state.coalesce_cap is not None:  # resumed: the original run's choice (same RNG stream)
             cap = self.state.coalesce_cap or None
         pad_id = getattr(getattr(self.model, "config", None), "pad_token_id", 0) or 0
@@ -269,24 +286,28 @@ class Trainer:
                     if self.cp_group is not None:  # every CP rank of a DP group counted the same batch
                         num_items = num_items // (self.env.world_size // self.dp_world)
                 passes = [[b] for b in group]
-                if cap is not None and cap > 0:  # coalesced: consecutive micro-batches, <= cap samples per pass
-                    passes, cur, n = [], [], 0
+                if cap is not None and cap > 0 and cap_units == "micro":  # explicit setting: k micro-batches
+                    cap, cap_units = cap * self._padded_tokens(group[:1]), "tokens"
+                if cap is not None and cap > 0:  # coalesced: consecutive micro-batches, <= cap padded tokens per pass
+                    passes, cur = [], []
                     for b in group:
-                        nb = b["labels"].shape[0]
-                        if cur and n + nb > cap:
+                        if cur and self._padded_tokens(cur + [b]) > cap:
                             passes.append(cur)
-                            cur, n = [], 0
+                            cur = []
                         cur.append(b)
-                        n += nb
                     passes.append(cur)
                 for j, pb in enumerate(passes):
                     loss = eng.forward_backward(self._merge(pb, pad_id), sync=j + 1 == len(passes),
                                                 num_items=num_items, dp_ranks=self.dp_world)
-                    tr_loss_sum += loss.float() * len(pb)  # logged loss: mean over micro-batches, as before
-                    tr_loss_n += len(pb)
+                    # logged loss: token-weighted mean (sum of token losses / tokens), the same number whether the
+                    # micro-batches run one by one or merged into passes of different token counts
+                    ntok = sum(token_count(b["labels"]) for b in pb).float()
+                    tr_loss_sum += loss.float() * ntok
+                    tr_loss_n += ntok
                 if cap == -1:  # decide from the first (uncoalesced) step's measured activation memory
                     torch.cuda.synchronize()
-                    cap = self._auto_cap(mem_base, torch.cuda.max_memory_allocated(env.device))
+                    cap = self._auto_cap(mem_base, torch.cuda.max_memory_allocated(env.device),
+                                         max(self._padded_tokens([b]) for b in group))
                     self.state.coalesce_cap = cap or 0
                 last_norm = eng.step(self.scheduler.get_last_lr()[0])
                 self.scheduler.step()
@@ -301,12 +322,13 @@ class Trainer:
                 self.state.epoch = epoch + done / max(1, n_micro)
                 self.control = self.handler.fire("on_step_end", args, self.state, self.control)
                 if self.control.should_log:
-                    mean = collectives.mean_across_processes({"loss": float(tr_loss_sum) / max(1, tr_loss_n)},
+                    nt = float(tr_loss_n)
+                    mean = collectives.mean_across_processes({"loss": float(tr_loss_sum) / max(1.0, nt)},
                                                              env.device)["loss"]
-                    total_loss_sum += mean * tr_loss_n
-                    total_loss_n += tr_loss_n
+                    total_loss_sum += mean * nt
+                    total_loss_n += nt
                     tr_loss_sum.zero_()
-                    tr_loss_n = 0
+                    tr_loss_n.zero_()
                     if args.nan_guard and not math.isfinite(mean):  # NaN/Inf guard on loss
                         raise FloatingPointError(f"non-finite training loss {mean} at step {self.state.global_step}")
                     self.log({"loss": round(mean, 4), "grad_norm": float(last_norm) if last_norm is not None else None,
@@ -323,10 +345,11 @@ class Trainer:
             self.control = self.handler.fire("on_epoch_end", args, self.state, self.control)
             if self.state.global_step >= max_steps:
                 break
-        if tr_loss_n:
-            mean = collectives.mean_across_processes({"loss": float(tr_loss_sum) / tr_loss_n}, env.device)["loss"]
-            total_loss_sum += mean * tr_loss_n
-            total_loss_n += tr_loss_n
+        nt = float(tr_loss_n)
+        if nt > 0:
+            mean = collectives.mean_across_processes({"loss": float(tr_loss_sum) / nt}, env.device)["loss"]
+            total_loss_sum += mean * nt
+            total_loss_n += nt
         if env.device.type == "cuda":
             torch.cuda.synchronize()
         runtime = time.perf_counter() - t_start

@@ -28,11 +28,32 @@ def _batch(cfg, B=4, S=200, T=40):
     return {k: v.cuda() for k, v in dict(input_ids=ids, attention_mask=am, labels=lab).items()}
 
 
-@pytest.mark.parametrize("name", ["t5-base", "flan-t5-base", "bart-base"])
-def test_native_bf16_matches_fp32_reference(name):
-    cfg = _cfg(name)
+def _grad_report(m_test, m_ref):
+    """Per parameter: relative L2 error and cosine of the test model's gradient against the reference's."""
+    rep = []
+    for (n, pt), (_, pr) in zip(m_test.named_parameters(), m_ref.named_parameters()):
+        if pr.grad is None or pr.grad.norm() == 0:
+            continue
+        gt, gr = pt.grad.float().flatten(), pr.grad.float().flatten()
+        rel = ((gt - gr).norm() / gr.norm()).item()
+        cos = torch.nn.functional.cosine_similarity(gt, gr, dim=0).item()
+        rep.append((rel, cos, n))
+    return rep
+
+
+@pytest.mark.parametrize("name,layers", [("t5-base", 2), ("flan-t5-base", 2), ("bart-base", 2), ("t5-base", 4),
+                                         ("bart-base", 4)])
+def test_native_bf16_matches_fp32_reference(name, layers):
+    """The bf16 HIP-kernel path vs the fp32 torch reference on the same (bf16-representable) weights and dropout
+    masks: loss within 1 %, and EVERY parameter's gradient (relative_attention_bias included) within 3e-2 relative L2
+    error and cosine > 0.999 — a bug confined to one layer's gradient cannot hide behind a global average."""
+    cfg = _cfg(name).replace(num_layers=layers, num_decoder_layers=layers)
     torch.manual_seed(0)
-    m32 = build_model(cfg).cuda().train()
+    m32 = build_model(cfg).cuda()
+    with torch.no_grad():  # weights exactly representable in bf16: the comparison measures compute, not weight rounding
+        for p in m32.parameters():
+            p.copy_(p.to(torch.bfloat16).float())
+    m32.train()
     m16 = build_model(cfg).cuda()
     m16.load_state_dict(m32.state_dict())
     m16 = m16.to(torch.bfloat16).train()
@@ -48,15 +69,52 @@ def test_native_bf16_matches_fp32_reference(name):
     manual_seed(5)  # same dropout masks on both paths
     out = m16(**b)
     out.loss.backward()
-    assert abs(out.loss.item() - ref.loss.item()) < 0.02 * ref.loss.item(), (out.loss.item(), ref.loss.item())
-    cos = []
-    for (n, p16), (_, p32) in zip(m16.named_parameters(), m32.named_parameters()):
-        if p32.grad is None or p32.grad.norm() == 0:
-            continue
-        c = torch.nn.functional.cosine_similarity(p16.grad.float().flatten(), p32.grad.flatten(), dim=0).item()
-        cos.append((c, n))
-    worst = min(cos)
-    assert worst[0] > 0.98, worst
+    assert abs(out.loss.item() - ref.loss.item()) < 0.01 * ref.loss.item(), (out.loss.item(), ref.loss.item())
+    rep = _grad_report(m16, m32)
+    names = {n for _, _, n in rep}
+    if cfg.model_type == "t5":
+        assert any("relative_attention_bias" in n for n in names)
+    worst_rel = max(rep)
+    worst_cos = min(rep, key=lambda r: r[1])
+    print(f"[parity {name} {layers}+{layers}] worst rel {worst_rel}, worst cos {worst_cos}")
+    assert worst_rel[0] < 3e-2, sorted(rep, reverse=True)[:5]
+    assert worst_cos[1] > 0.999, sorted(rep, key=lambda r: r[1])[:5]
+
+
+@pytest.mark.parametrize("name", ["t5-base", "bart-base"])
+def test_fp32_training_on_gpu_matches_reference(name):
+    """fp32 end to end on the GPU (the reference's own precision, ref/train-torchrun.py:115-128): attention and the LM
+    head take the explicit fp32 composite (ops/attention.py _native), norms / CE / AdamW run their fp32 HIP kernels.
+    One engine step vs the pure-torch reference step: same loss and gradients to fp32 rounding, same update."""
+    from distributed_llms_example_amd.ops.rng import manual_seed
+    from distributed_llms_example_amd.parallel.env import init_distributed
+    from distributed_llms_example_amd.train.engine import TrainEngine
+    env = init_distributed()
+    cfg = _cfg(name)
+    torch.manual_seed(0)
+    sd = build_model(cfg).state_dict()
+    b = _batch(cfg)
+    res = []
+    for ref in (True, False):
+        if ref:
+            os.environ["DLLM_REFERENCE_OPS"] = "1"
+        try:
+            m = build_model(cfg)
+            m.load_state_dict(sd)
+            eng = TrainEngine(m, env, lr=1e-3, dtype=torch.float32)
+            eng.train()
+            manual_seed(5)
+            loss = eng.forward_backward(b)
+            g = eng.flat.grad_buf.clone()
+            eng.step()
+            res.append((float(loss), g, eng.flat.param_buf.clone()))
+        finally:
+            os.environ.pop("DLLM_REFERENCE_OPS", None)
+    (l0, g0, p0), (l1, g1, p1) = res
+    assert g1.dtype == torch.float32 and p1.dtype == torch.float32
+    assert abs(l0 - l1) < 1e-4 * abs(l0), (l0, l1)
+    assert ((g1 - g0).norm() / g0.norm()).item() < 1e-3
+    assert ((p1 - p0).norm() / p0.norm()).item() < 1e-5
 
 
 def test_generate_on_gpu():

@@ -308,3 +308,23 @@ def test_attention_dropout_hash_statistics():
     col = d.mean(dim=(0, 1, 2))
     row = d.mean(dim=(0, 1, 3))
     assert (col - p).abs().max().item() < 0.06 and (row - p).abs().max().item() < 0.06
+
+
+def test_relayout_keeps_stacked_groups_adjacent():
+    """FlatParams.relayout with an order that splits a stacked group (the decoder's cross-attention K/V weights,
+    consumed as ONE tensor by ops/linear.py stacked_linear): the group is re-joined at its first member's position,
+    parameter values survive, and stacked_linear still finds the adjacent view."""
+    import random
+    from distributed_llms_example_amd.ops.linear import _adjacent
+    from distributed_llms_example_amd.parallel.flat import FlatParams
+    m = build_model("t5-tiny")
+    flat = FlatParams(m)
+    assert flat.groups, "t5 declares stacked cross-attention K/V groups"
+    before = {n: p.detach().clone() for n, p in m.named_parameters()}
+    order = list(range(len(flat.segments)))
+    random.Random(0).shuffle(order)
+    flat.relayout(order)
+    for n, p in m.named_parameters():
+        assert torch.equal(p.detach(), before[n]), n
+    for grp in m._dllm_param_groups():
+        assert _adjacent([p for p in grp]) is not None
