@@ -38,7 +38,7 @@ import torch.nn.functional as F
 
 from .. import _ext
 from .activations import act_dropout
-from .gemm import bias_grad_accumulate, wgrad_accumulate
+from .gemm import bias_grad_accumulate, linear_dgrad, linear_fwd, wgrad_accumulate
 from .linear import _RES_GEMM, _fire, _fusable, _gbuf, _use
 
 # activation -> (forward epilogue, backward epilogue) of csrc/gemm_fused.hip
@@ -71,7 +71,7 @@ class _FusedFFNFn(torch.autograd.Function):
         elif _RELU_MASK and _pingpong(C, x2.shape[1]) and _pingpong(C, wo.shape[0]):  # ReLU: bits for the backward
             mask = torch.empty(x2.shape[0] * wi.shape[0] // 32, device=x.device, dtype=torch.int32)
         h = C.gemm_fused(x2, wi, False, efwd, bi, None, u, float(p), int(seed), _VARIANT, mask)
-        y = F.linear(h, wo, bo)
+        y = linear_fwd(h, wo, bo)
         ctx.set_materialize_grads(False)  # the residual alias's gradient is None when the caller does not use it
         ctx.save_for_backward(x2, h, u, mask)
         ctx.params = params
@@ -109,9 +109,9 @@ class _FusedFFNFn(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:  # post-LN residual (ffn_res): its gradient accumulated by this GEMM (beta = 1)
             if dres is not None and dres.is_contiguous() and dres.dtype == du.dtype and dres.shape == shape:
-                dx = dres.view(-1, shape[-1]).addmm_(du, Wi.detach())
+                dx = linear_dgrad(du, Wi.detach(), out=dres.view(-1, shape[-1]))
             else:
-                dx = torch.matmul(du, Wi.detach())
+                dx = linear_dgrad(du, Wi.detach())
                 if dres is not None:
                     dx = dx + dres.reshape(dx.shape)
         with torch.no_grad():
@@ -151,7 +151,7 @@ class _FusedGatedFFNFn(torch.autograd.Function):
         shape = x.shape
         x2 = x.reshape(-1, shape[-1])
         h, g1, g2 = C.gemm_geglu(x2, wi, float(p), int(seed))
-        y = F.linear(h, wo)
+        y = linear_fwd(h, wo)
         ctx.save_for_backward(x2, h, g1, g2)
         ctx.params = params
         for q in params:
@@ -171,7 +171,7 @@ class _FusedGatedFFNFn(torch.autograd.Function):
         with torch.no_grad():
             wgrad_accumulate(_gbuf(Wo), dy2, h)
         _fire(Wo)
-        dx = torch.matmul(du, Wi.detach()) if ctx.needs_input_grad[0] else None
+        dx = linear_dgrad(du, Wi.detach()) if ctx.needs_input_grad[0] else None
         with torch.no_grad():
             wgrad_accumulate(_gbuf(Wi), du, x2)
         _fire(Wi)

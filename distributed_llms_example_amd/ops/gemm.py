@@ -1,4 +1,10 @@
-"""Weight-gradient GEMM ``dW (+)= dYᵀ X`` on the hand-written gfx950 kernel (csrc/gemm.hip).
+"""Hand-written gfx950 GEMMs for every linear layer of a training step:
+
+* projections, forward ``Y = X Wᵀ (+ b)`` and input gradient ``dX (+)= dY W`` (linear_fwd / linear_dgrad):
+  csrc/gemm_w4.hip, the one-wave-per-SIMD 256x256 kernel (``DLLM_W4_GEMM=0`` selects hipBLASLt, A/B runs);
+* weight gradient ``dW (+)= dYᵀ X`` (wgrad_accumulate): csrc/gemm.hip.
+
+Weight-gradient GEMM notes:
 
 Both operands are token-major ([tokens, features]), the reduction runs over tokens (10⁴-10⁵), and the
 result is accumulated straight into the flat gradient buffer (bf16, or fp32 for fp32 gradient
@@ -11,8 +17,44 @@ from __future__ import annotations
 import os
 
 import torch
+import torch.nn.functional as F
 
 from .. import _ext
+
+_W4 = os.environ.get("DLLM_W4_GEMM", "1") != "0"
+w4_calls = 0  # projections that ran on csrc/gemm_w4.hip (tests assert the kernel really ran)
+
+
+def _w4_ok(a: torch.Tensor, b: torch.Tensor, kmajor: bool) -> bool:
+    return (_W4 and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and _ext.use_native(a)
+            and bool(_ext.native().gemm_w4_supported(a, b, kmajor)))
+
+
+def linear_fwd(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Tensor:
+    """``x @ wᵀ (+ bias)`` for x ``[..., K]``, w ``[N, K]`` (nn.Linear layout)."""
+    global w4_calls
+    x2 = x.reshape(-1, x.shape[-1])
+    if _w4_ok(x2, w, False) and (bias is None or (bias.dtype == torch.bfloat16 and bias.is_contiguous())):
+        w4_calls += 1
+        return _ext.native().gemm_w4(x2, w, False, bias).view(*x.shape[:-1], w.shape[0])
+    return F.linear(x, w, bias)
+
+
+def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """Input gradient ``dy @ w`` for dy ``[..., N]``, w ``[N, K]``; with ``out`` (``[..., K]``, contiguous) the product
+    is accumulated into it in the GEMM epilogue (``out += dy @ w``, the post-LN residual's gradient)."""
+    global w4_calls
+    dy2 = dy.reshape(-1, dy.shape[-1])
+    if _w4_ok(dy2, w, True):
+        w4_calls += 1
+        if out is not None:
+            _ext.native().gemm_w4(dy2, w, True, None, out.view(-1, out.shape[-1]), True)
+            return out
+        return _ext.native().gemm_w4(dy2, w, True).view(*dy.shape[:-1], w.shape[1])
+    if out is not None:
+        out.view(-1, out.shape[-1]).addmm_(dy2, w)
+        return out
+    return torch.matmul(dy, w)
 
 _VARIANT = int(os.environ.get("DLLM_WGRAD_VARIANT", "-1"))  # -1: pick by K (csrc/gemm.hip)
 

@@ -20,7 +20,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .gemm import bias_grad_accumulate, wgrad_accumulate
+from .gemm import bias_grad_accumulate, linear_dgrad, linear_fwd, wgrad_accumulate
 
 
 def _gbuf(p: torch.Tensor | None) -> torch.Tensor | None:
@@ -67,13 +67,13 @@ class _LinearAccumFn(torch.autograd.Function):
         ctx.weight, ctx.bias = params
         _use(params[0])
         _use(params[1])
-        return F.linear(x, weight, bias)
+        return linear_fwd(x, weight, bias)
 
     @staticmethod
     def backward(ctx, dy):
         (x,) = ctx.saved_tensors
         w, bias = ctx.weight, ctx.bias
-        dx = torch.matmul(dy, w) if ctx.needs_input_grad[0] else None
+        dx = linear_dgrad(dy, w.detach()) if ctx.needs_input_grad[0] else None
         dy2 = dy.reshape(-1, dy.shape[-1])
         x2 = x.reshape(-1, x.shape[-1])
         with torch.no_grad():
@@ -101,7 +101,7 @@ class _LinearResFn(torch.autograd.Function):
         ctx.weight, ctx.bias = params
         _use(params[0])
         _use(params[1])
-        return F.linear(x, weight, bias), x.view_as(x)
+        return linear_fwd(x, weight, bias), x.view_as(x)
 
     @staticmethod
     def backward(ctx, dy, dres):
@@ -111,9 +111,9 @@ class _LinearResFn(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             if (dres is not None and dres.is_contiguous() and dres.dtype == dy.dtype and dres.shape == x.shape):
-                dx = dres.view(-1, dres.shape[-1]).addmm_(dy2, w.detach()).view(x.shape)
+                dx = linear_dgrad(dy, w.detach(), out=dres)
             else:
-                dx = torch.matmul(dy, w.detach())
+                dx = linear_dgrad(dy, w.detach())
                 if dres is not None:
                     dx = dx + dres
         x2 = x.reshape(-1, x.shape[-1])
@@ -180,7 +180,7 @@ def _adjacent(ts):
 class _StackedFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, W, b, ws, bs, shape):
-        y = F.linear(x, W, b)
+        y = linear_fwd(x, W, b)
         n = ws[0].shape[0]
         gbuf = torch.empty_like(y)
         outs = []
@@ -209,7 +209,7 @@ class _StackedFn(torch.autograd.Function):
                 mine.copy_(g)  # consumer produced its own buffer
         G2 = gbuf.view(-1, gbuf.shape[-1])
         x2 = x.reshape(-1, x.shape[-1])
-        dx = torch.matmul(G2, W).view(x.shape) if ctx.needs_input_grad[0] else None
+        dx = linear_dgrad(G2, W).view(x.shape) if ctx.needs_input_grad[0] else None
         with torch.no_grad():
             gw = _adjacent([_gbuf(w) for w in ws])
             if gw is not None:
