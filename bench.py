@@ -115,6 +115,7 @@ def main():
     from distributed_llms_example_amd.parallel.env import init_distributed
     from distributed_llms_example_amd.parallel.reducer import DEFAULT_BUCKET_MB
     from distributed_llms_example_amd.train.engine import TrainEngine
+    from distributed_llms_example_amd.utils.profiling import MI355X_BF16_DENSE_PEAK, seq2seq_train_flops
 
     env = init_distributed()
     n = env.world_size
@@ -183,6 +184,10 @@ def main():
     value = B * GA * n * a.steps / dt
     if comm is not None:
         comm["exposed_frac"] = round(comm["exposed_ms_per_step"] / ms, 4)
+    # model FLOPs utilisation against the dense bf16 peak (2.5 PF per GPU; no 2:1-sparsity figure): analytic training
+    # FLOPs of the step (GEMMs + attention + LM head, fwd + bwd = 3 x fwd; utils/profiling.py)
+    step_flops = seq2seq_train_flops(cfg, B * GA, S, T)
+    mfu = step_flops / (ms * 1e-3) / (MI355X_BF16_DENSE_PEAK * n)
     if a.model == "t5-base":
         metric = "samples/sec (whole node) T5-base summarization fine-tune at 1/2/4/8 MI355X"
         # the HF stack at the same per-GPU batch, or at its largest measured one below it (it does not fit above 128)
@@ -200,6 +205,7 @@ def main():
             "metric": metric,
             "value": round(value, 2), "unit": "samples/s", "n_gpus": n, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
+            "mfu": round(mfu, 4), "tflops_per_gpu": round(step_flops / (ms * 1e-3) / n / 1e12, 1),
             "vs_baseline": round(value / (base * n), 3) if base and B >= 16 else None,
             "baseline_note": f"HF transformers+torch stack measured on 1x MI355X at the same sequence shapes (its "
                              f"per-GPU batch {base_batch}, samples/s compared per sample) x N (BASELINE.md publishes "

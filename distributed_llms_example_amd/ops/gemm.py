@@ -71,8 +71,11 @@ def wgrad_accumulate(out: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, bet
     if _native_ok(dy2, x2, out):
         _ext.native().gemm_wgrad(dy2, x2, out, beta, _VARIANT, 0)
         return out
-    if out.dtype != dy2.dtype:  # fp32 gradient buffer, bf16 operands: library GEMM, then one fp32 add
-        g = torch.mm(dy2.t(), x2)
+    if out.dtype != dy2.dtype:  # fp32 gradient buffer, bf16 operands: the product itself in fp32, then one fp32 add
+        if dy2.is_cuda:
+            g = torch.mm(dy2.t(), x2, out_dtype=out.dtype)  # fp32 output from bf16 operands (no bf16 rounding)
+        else:
+            g = torch.mm(dy2.t().to(out.dtype), x2.to(out.dtype))
         return out.add_(g) if beta else out.copy_(g)
     if beta:
         return out.addmm_(dy2.t(), x2)

@@ -5,17 +5,14 @@
   bucket launch (parallel/reducer.py; the native reducer marks through csrc/reducer.cpp), so
   ``rocprofv3 --marker-trace`` timelines are annotated; a no-op when the library is absent or
   ``DLLM_ROCTX=0``.
-* ``StepTimer``: wall-clock per step synchronised on the device, samples/s, tokens/s and model FLOP
-  utilisation (6 × params × tokens + attention terms, against the MI355X dense bf16 peak).
+* ``seq2seq_train_flops``: analytic training FLOPs of one encoder-decoder step (GEMMs, attention, LM head;
+  fwd + bwd = 3 x fwd), from which bench.py reports model FLOP utilisation against the MI355X dense bf16 peak.
 """
 from __future__ import annotations
 
 import contextlib
 import ctypes
 import os
-import time
-
-import torch
 
 _roctx = None
 _roctx_tried = False
@@ -67,35 +64,3 @@ def seq2seq_train_flops(cfg, batch: int, src: int, tgt: int) -> float:
                                     + 2 * tgt * d * f * ff_mult + 4 * tgt * tgt * inner + 4 * tgt * src * inner)
     head = 2 * tgt * d * cfg.vocab_size
     return 3.0 * batch * (enc + dec + head)
-
-
-class StepTimer:
-    def __init__(self, device=None):
-        self.device = device
-        self.t0 = None
-        self.times = []
-
-    def _sync(self):
-        if self.device is not None and getattr(self.device, "type", "cpu") == "cuda":
-            torch.cuda.synchronize(self.device)
-
-    def start(self):
-        self._sync()
-        self.t0 = time.perf_counter()
-
-    def stop(self):
-        self._sync()
-        dt = time.perf_counter() - self.t0
-        self.times.append(dt)
-        return dt
-
-    def summary(self, samples_per_step: int, tokens_per_step: int, flops_per_step: float | None = None,
-                n_gpus: int = 1) -> dict:
-        if not self.times:
-            return {}
-        avg = sum(self.times) / len(self.times)
-        out = {"step_time_s": avg, "samples_per_second": samples_per_step / avg,
-               "tokens_per_second": tokens_per_step / avg}
-        if flops_per_step:
-            out["mfu"] = flops_per_step / avg / (MI355X_BF16_DENSE_PEAK * n_gpus)
-        return out
