@@ -68,6 +68,10 @@ def parse():
                                                                "last; samples/s counts every micro-batch)")
     ap.add_argument("--comm-stress", action="store_true",
                     help="small per-GPU batch (8 unless --batch-per-gpu is given): all-reduce ~ compute")
+    ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
+                    help="capture the whole step (forward, backward, GA micro-steps, clip, AdamW) in one HIP graph and "
+                         "replay it (train/graph.py); auto: on for one GPU, off for N > 1 (the all-reduce is launched "
+                         "from autograd hooks)")
     ap.add_argument("--dtype", default=None, choices=["bf16", "fp32"],
                     help="weights/activations dtype (default bf16; fp32 on a CPU rehearsal)")
     a = ap.parse_args()
@@ -146,9 +150,26 @@ def main():
             "labels": torch.randint(2, V, (B, T), generator=g).to(env.device),
         })
 
+    use_graph = a.graph == "on" or (a.graph == "auto" and n == 1 and env.device.type == "cuda")
+    graphed = None
+    if use_graph:
+        from distributed_llms_example_amd.train.graph import GraphedStep
+        try:
+            graphed = GraphedStep(eng, batches[:GA], warmup=2)
+        except Exception as e:  # noqa: BLE001 - a capture problem must not cost the measurement: run eager
+            if a.graph == "on":
+                raise
+            print(f"[bench] graph capture failed ({type(e).__name__}: {e}); eager steps", file=sys.stderr)
+            graphed = None
+            torch.cuda.synchronize()
+
     def step(i):
+        mbs = [batches[(i * GA + k) % len(batches)] for k in range(GA)]
+        if graphed is not None:
+            graphed.replay(mbs)
+            return
         for k in range(GA):  # GA micro-batches, gradient sync (and the all-reduce) on the last only
-            eng.forward_backward(batches[(i * GA + k) % len(batches)], grad_accum=GA, sync=k == GA - 1)
+            eng.forward_backward(mbs[k], grad_accum=GA, sync=k == GA - 1)
         eng.step()
 
     for i in range(a.warmup):
@@ -219,7 +240,7 @@ def main():
                        "backend": env.backend, "world_size": n, "rccl_version": _rccl_version(),
                        "overlap": bool(eng.reducer.overlap) if eng.reducer else None,
                        "n_buckets": len(eng.reducer.buckets) if eng.reducer else None,
-                       "comm_stress": bool(a.comm_stress),
+                       "comm_stress": bool(a.comm_stress), "hip_graph": graphed is not None,
                        "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 2)
                        if env.device.type == "cuda" else None},
             "comm": comm,

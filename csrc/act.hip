@@ -6,6 +6,8 @@
 
 using namespace dllm;
 
+DLLM_SEED_STEP_TU(act)
+
 namespace {
 
 constexpr float kSqrt2OverPi = 0.7978845608028654f;
@@ -37,6 +39,7 @@ DLLM_DEVICE float act_df(float x) {
 template <typename T, int ACT, bool GATED>
 __global__ __launch_bounds__(256) void act_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, long total4, int F,
                                                       float p, uint32_t seed, uint32_t thr) {
+  if (p > 0.f) seed = eff_seed(seed);
   const float dscale = p > 0.f ? 1.f / (1.f - p) : 1.f;
   const int F4 = F / 4;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < total4; i += (long)gridDim.x * 256) {
@@ -63,6 +66,7 @@ template <typename T, int ACT, bool GATED>
 __global__ __launch_bounds__(256) void act_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                       T* __restrict__ dx, long total4, int F, float p, uint32_t seed,
                                                       uint32_t thr) {
+  if (p > 0.f) seed = eff_seed(seed);
   const float dscale = p > 0.f ? 1.f / (1.f - p) : 1.f;
   const int F4 = F / 4;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < total4; i += (long)gridDim.x * 256) {
@@ -94,6 +98,7 @@ __global__ __launch_bounds__(256) void act_bwd_kernel(const T* __restrict__ dy, 
 template <typename T>
 __global__ __launch_bounds__(256) void dropout_kernel(const T* __restrict__ x, T* __restrict__ y, long total4, float p,
                                                       uint32_t seed, uint32_t thr) {
+  seed = eff_seed(seed);
   const float dscale = 1.f / (1.f - p);
   for (long i = blockIdx.x * 256L + threadIdx.x; i < total4; i += (long)gridDim.x * 256) {
     f32x4 v = Elem<T>::load4(x + i * 4);

@@ -38,8 +38,13 @@ __global__ __launch_bounds__(256) void adamw_kernel(TP* __restrict__ param, floa
                                                     float* __restrict__ v, const uint8_t* __restrict__ wd_mask,
                                                     const float* __restrict__ coef_p, long n4, float lr, float b1,
                                                     float b2, float eps, float wd, float step_size,
-                                                    float inv_sqrt_bc2) {
+                                                    float inv_sqrt_bc2, const float* __restrict__ hyper) {
   const float coef = coef_p[0];
+  if (hyper != nullptr) {  // graph-replayed steps: lr / bias corrections computed on the device (ops/optim.py)
+    lr = hyper[0];
+    step_size = hyper[1];
+    inv_sqrt_bc2 = hyper[2];
+  }
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
     const long o = i * 4;
     f32x4 g = Elem<TG>::load4(grad + o) * coef;
@@ -103,8 +108,13 @@ __global__ __launch_bounds__(256) void adamw8_kernel(TP* __restrict__ param, flo
                                                      float* __restrict__ v, const uint8_t* __restrict__ wd_mask,
                                                      const float* __restrict__ coef_p, long n8, float lr, float b1,
                                                      float b2, float eps, float wd, float step_size,
-                                                     float inv_sqrt_bc2) {
+                                                     float inv_sqrt_bc2, const float* __restrict__ hyper) {
   const float coef = coef_p[0];
+  if (hyper != nullptr) {  // graph-replayed steps: lr / bias corrections computed on the device (ops/optim.py)
+    lr = hyper[0];
+    step_size = hyper[1];
+    inv_sqrt_bc2 = hyper[2];
+  }
   const float dec = lr * wd;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
     const long o = i * 8;
@@ -167,7 +177,7 @@ extern "C" int dllm_sq_norm(const void* g, long n, float* part, float* out, int 
 
 extern "C" int dllm_adamw(void* param, float* master, const void* grad, float* m, float* v, const uint8_t* wd_mask,
                           const float* coef, long n, float lr, float b1, float b2, float eps, float wd, float bc1,
-                          float bc2, int is_bf16, int grad_f32, hipStream_t st) {
+                          float bc2, int is_bf16, int grad_f32, const float* hyper, hipStream_t st) {
   if (n % 4) return -2;
   const long n4 = n / 4;
   const int G = grid_for(n4, 4096);
@@ -182,10 +192,10 @@ extern "C" int dllm_adamw(void* param, float* master, const void* grad, float* m
   do {                                                                                                                  \
     if (nt)                                                                                                             \
       hipLaunchKernelGGL((adamw8_kernel<TP, TG, MS, true>), dim3(G8), dim3(256), 0, st, (TP*)param, master,             \
-                         (const TG*)grad, m, v, wd_mask, coef, n8, lr, b1, b2, eps, wd, step_size, inv_sqrt_bc2);       \
+                         (const TG*)grad, m, v, wd_mask, coef, n8, lr, b1, b2, eps, wd, step_size, inv_sqrt_bc2, hyper);       \
     else                                                                                                                \
       hipLaunchKernelGGL((adamw8_kernel<TP, TG, MS, false>), dim3(G8), dim3(256), 0, st, (TP*)param, master,            \
-                         (const TG*)grad, m, v, wd_mask, coef, n8, lr, b1, b2, eps, wd, step_size, inv_sqrt_bc2);       \
+                         (const TG*)grad, m, v, wd_mask, coef, n8, lr, b1, b2, eps, wd, step_size, inv_sqrt_bc2, hyper);       \
   } while (0)
     if (is_bf16 && grad_f32) { if (master) A8(uint16_t, float, true); else A8(uint16_t, float, false); }
     else if (is_bf16) { if (master) A8(uint16_t, uint16_t, true); else A8(uint16_t, uint16_t, false); }
@@ -197,26 +207,26 @@ extern "C" int dllm_adamw(void* param, float* master, const void* grad, float* m
   if (is_bf16 && grad_f32) {  // bf16 params, fp32 gradients (accumulated across micro-batches in fp32)
     if (master)
       hipLaunchKernelGGL((adamw_kernel<uint16_t, float, true>), dim3(G), dim3(256), 0, st, (uint16_t*)param, master,
-                         (const float*)grad, m, v, wd_mask, coef, n4, lr, b1, b2, eps, wd, step_size, inv_sqrt_bc2);
+                         (const float*)grad, m, v, wd_mask, coef, n4, lr, b1, b2, eps, wd, step_size, inv_sqrt_bc2, hyper);
     else
       hipLaunchKernelGGL((adamw_kernel<uint16_t, float, false>), dim3(G), dim3(256), 0, st, (uint16_t*)param, master,
-                         (const float*)grad, m, v, wd_mask, coef, n4, lr, b1, b2, eps, wd, step_size, inv_sqrt_bc2);
+                         (const float*)grad, m, v, wd_mask, coef, n4, lr, b1, b2, eps, wd, step_size, inv_sqrt_bc2, hyper);
   } else if (is_bf16) {
     if (master)
       hipLaunchKernelGGL((adamw_kernel<uint16_t, uint16_t, true>), dim3(G), dim3(256), 0, st, (uint16_t*)param,
                          master, (const uint16_t*)grad, m, v, wd_mask, coef, n4, lr, b1, b2, eps, wd, step_size,
-                         inv_sqrt_bc2);
+                         inv_sqrt_bc2, hyper);
     else
       hipLaunchKernelGGL((adamw_kernel<uint16_t, uint16_t, false>), dim3(G), dim3(256), 0, st, (uint16_t*)param,
                          master, (const uint16_t*)grad, m, v, wd_mask, coef, n4, lr, b1, b2, eps, wd, step_size,
-                         inv_sqrt_bc2);
+                         inv_sqrt_bc2, hyper);
   } else {
     if (master)
       hipLaunchKernelGGL((adamw_kernel<float, float, true>), dim3(G), dim3(256), 0, st, (float*)param, master,
-                         (const float*)grad, m, v, wd_mask, coef, n4, lr, b1, b2, eps, wd, step_size, inv_sqrt_bc2);
+                         (const float*)grad, m, v, wd_mask, coef, n4, lr, b1, b2, eps, wd, step_size, inv_sqrt_bc2, hyper);
     else
       hipLaunchKernelGGL((adamw_kernel<float, float, false>), dim3(G), dim3(256), 0, st, (float*)param, master,
-                         (const float*)grad, m, v, wd_mask, coef, n4, lr, b1, b2, eps, wd, step_size, inv_sqrt_bc2);
+                         (const float*)grad, m, v, wd_mask, coef, n4, lr, b1, b2, eps, wd, step_size, inv_sqrt_bc2, hyper);
   }
   DLLM_CHECK_LAUNCH();
   return 0;

@@ -39,6 +39,8 @@
 
 using namespace dllm;
 
+DLLM_SEED_STEP_TU(attn)
+
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8v;
 typedef __attribute__((ext_vector_type(4))) short s16x4;
 typedef __attribute__((ext_vector_type(8))) float f32x8;
@@ -176,7 +178,7 @@ __global__ __launch_bounds__(256) void attn_dropout_mask_kernel(AttnParams P, lo
     const long t2 = r >> 1;
     const int kt = (int)(t2 % P.n_ktiles);
     const long bh = t2 / P.n_ktiles;
-    const uint32_t rh = mix32(P.seed, (uint32_t)(bh * P.Sq + q));
+    const uint32_t rh = mix32(eff_seed(P.seed), (uint32_t)(bh * P.Sq + q));
     P.dmask[w] = dropout_word(rh, kt * FWD_BN, hh, P.thr);
   }
 }
@@ -273,7 +275,7 @@ __global__ __launch_bounds__(256, FNB == 3 ? 2 : 3) void attn_fwd_kernel(AttnPar
     }
   }
   const long row_g = (long)(b * P.H + h) * P.Sq + qrow;
-  const uint32_t rh = DROP ? mix32(P.seed, (uint32_t)row_g) : 0u;
+  const uint32_t rh = DROP ? mix32(eff_seed(P.seed), (uint32_t)row_g) : 0u;
   const float dscale = DROP ? 1.f / (1.f - P.p_drop) : 1.f;
 
   for (int t = w; t < ntiles; t += 4) {  // wave-per-tile: per-key mask + "tile has a masked key" flag

@@ -27,7 +27,11 @@ int dllm_ce_bwd(const float*, const void*, const int64_t*, const float*, const f
                 int, hipStream_t);
 int dllm_sq_norm(const void*, long, float*, float*, int, hipStream_t);
 int dllm_adamw(void*, float*, const void*, float*, float*, const uint8_t*, const float*, long, float, float, float,
-               float, float, float, float, int, int, hipStream_t);
+               float, float, float, float, int, int, const float*, hipStream_t);
+int dllm_set_seed_step_norm(const uint32_t*);
+int dllm_set_seed_step_act(const uint32_t*);
+int dllm_set_seed_step_attn(const uint32_t*);
+int dllm_set_seed_step_gemm_fused(const uint32_t*);
 int dllm_attn_fwd(AttnParams*, hipStream_t);
 int dllm_attn_bwd(AttnParams*, hipStream_t);
 int dllm_attn_params_size();
@@ -284,7 +288,7 @@ Tensor sq_norm(const Tensor& g) {
 
 void adamw_step(Tensor param, const optional<Tensor>& master, const Tensor& grad, Tensor m, Tensor v,
                 const optional<Tensor>& wd_mask, const Tensor& coef, double lr, double b1, double b2, double eps,
-                double wd, double bc1, double bc2) {
+                double wd, double bc1, double bc2, const optional<Tensor>& hyper) {
   check_gpu(param, "param");
   const long n = param.numel();
   TORCH_CHECK(n % 4 == 0 && param.is_contiguous() && grad.numel() == n && m.numel() == n && v.numel() == n,
@@ -298,13 +302,18 @@ void adamw_step(Tensor param, const optional<Tensor>& master, const Tensor& grad
   if (wd_mask.has_value() && wd_mask->defined())
     TORCH_CHECK(wd_mask->numel() == n && wd_mask->scalar_type() == at::kByte, "adamw: wd_mask u8 [n]");
   TORCH_CHECK(coef.scalar_type() == at::kFloat && coef.is_cuda(), "adamw: coef fp32 device scalar");
+  const bool has_hyper = hyper.has_value() && hyper->defined();
+  if (has_hyper)
+    TORCH_CHECK(hyper->is_cuda() && hyper->scalar_type() == at::kFloat && hyper->numel() >= 3 && hyper->is_contiguous(),
+                "adamw: hyper must be a contiguous fp32 device tensor [lr, lr / bc1, 1 / sqrt(bc2)]");
   for (auto* t : {&param, &m, &v}) check_aligned(*t, 16, "adamw buffer");
   check_rc(dllm_adamw(param.data_ptr(),
                       master.has_value() && master->defined() ? master->data_ptr<float>() : nullptr, grad.data_ptr(),
                       m.data_ptr<float>(), v.data_ptr<float>(),
                       wd_mask.has_value() && wd_mask->defined() ? wd_mask->data_ptr<uint8_t>() : nullptr,
                       coef.data_ptr<float>(), n, (float)lr, (float)b1, (float)b2, (float)eps, (float)wd, (float)bc1,
-                      (float)bc2, is_bf16(param), grad.scalar_type() == at::kFloat, stream()),
+                      (float)bc2, is_bf16(param), grad.scalar_type() == at::kFloat,
+                      has_hyper ? hyper->data_ptr<float>() : nullptr, stream()),
            "adamw");
 }
 
@@ -804,6 +813,21 @@ void embed_bwd(const Tensor& ids_sorted, const Tensor& perm, const Tensor& dy, T
            "embed_bwd");
 }
 
+// Device step counter for graph-replayable dropout (csrc/common.h DLLM_SEED_STEP_TU): every dropout kernel mixes
+// *step into its site seed; None turns it off (site seeds used as given).  The tensor must outlive its use.
+void set_seed_step(const optional<Tensor>& step) {
+  const uint32_t* p = nullptr;
+  if (step.has_value() && step->defined()) {
+    TORCH_CHECK(step->is_cuda() && step->scalar_type() == at::kInt && step->numel() == 1,
+                "set_seed_step: a 1-element int32 GPU tensor");
+    p = reinterpret_cast<const uint32_t*>(step->data_ptr());
+  }
+  check_rc(dllm_set_seed_step_norm(p), "set_seed_step(norm)");
+  check_rc(dllm_set_seed_step_act(p), "set_seed_step(act)");
+  check_rc(dllm_set_seed_step_attn(p), "set_seed_step(attn)");
+  check_rc(dllm_set_seed_step_gemm_fused(p), "set_seed_step(gemm_fused)");
+}
+
 namespace dllm {
 void bind_reducer(pybind11::module& m);  // csrc/reducer.cpp
 }
@@ -823,7 +847,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("embed_bwd", &embed_bwd);
   m.def("ce_chunk_fwd", &ce_chunk_fwd);
   m.def("ce_chunk_bwd", &ce_chunk_bwd);
-  m.def("adamw_step", &adamw_step);
+  m.def("adamw_step", &adamw_step, py::arg("param"), py::arg("master"), py::arg("grad"), py::arg("m"), py::arg("v"),
+        py::arg("wd_mask"), py::arg("coef"), py::arg("lr"), py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("wd"),
+        py::arg("bc1"), py::arg("bc2"), py::arg("hyper") = py::none());
+  m.def("set_seed_step", &set_seed_step, "device step counter mixed into every dropout site seed (None: off)");
   m.def("attn_fwd", &attn_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("kpm"), py::arg("lut"),
         py::arg("scale"), py::arg("causal"), py::arg("p"), py::arg("seed"), py::arg("dmask_in") = py::none(),
         py::arg("sat_lo") = -1, py::arg("sat_hi") = -1);

@@ -97,6 +97,23 @@ DLLM_DEVICE void dropout4(f32x4& v, uint32_t seed, uint32_t thr16, uint32_t e4, 
   v.w = k3 ? v.w * scale : 0.f;
 }
 
+// ---- graph-replayable dropout seeds ----------------------------------------------------------------------------
+// A captured HIP graph replays its kernel arguments verbatim, so a per-site seed passed by value would draw the SAME
+// mask every replayed step.  Every translation unit with dropout therefore keeps a device pointer to ONE 32-bit step
+// counter (set once by dllm_set_seed_step_<tu>, bumped on the device by a captured add each step): kernels use
+// mix32(site_seed, *step) when it is set, the site seed itself when not (eager mode: identical masks to before).
+#define DLLM_SEED_STEP_TU(TU)                                                                           \
+  namespace {                                                                                           \
+  __device__ const uint32_t* g_seed_step = nullptr;                                                     \
+  DLLM_DEVICE uint32_t eff_seed(uint32_t seed) {                                                        \
+    const uint32_t* p = g_seed_step;                                                                    \
+    return p ? dllm::mix32(seed, *p) : seed;                                                            \
+  }                                                                                                     \
+  }                                                                                                     \
+  extern "C" int dllm_set_seed_step_##TU(const uint32_t* p) {                                           \
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_seed_step), &p, sizeof(p));                              \
+  }
+
 // ---- wave64 reductions -------------------------------------------------------------------------
 DLLM_DEVICE float wave_sum(float v) {
 #pragma unroll

@@ -34,6 +34,8 @@
 
 using namespace dllm;
 
+DLLM_SEED_STEP_TU(gemm_fused)
+
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8v;
 typedef __attribute__((ext_vector_type(4))) short s16x4;
 
@@ -151,13 +153,13 @@ DLLM_DEVICE f32x4 load4(const uint16_t* p) {
 // GELU forwards write G = dropout'(.) * act'(U) (the keep mask and 1/(1-p) already applied) as the second output, so
 // their backward epilogues are one multiply: dU = (dY Wo) * G — no activation math and no hash in the backward.
 template <int EPI>
-DLLM_DEVICE f32x4 epilogue4(const GemmFusedParams& P, int m, int n, f32x4 v) {
+DLLM_DEVICE f32x4 epilogue4(const GemmFusedParams& P, uint32_t seed, int m, int n, f32x4 v) {
   const bool drop = P.p > 0.f;
   const uint32_t e = (uint32_t)m * (uint32_t)P.N + (uint32_t)n;  // output element index (< 2^32, host-checked)
   if (EPI == EPI_RELU) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) v[k] = fmaxf(v[k], 0.f);
-    if (drop) dropout4(v, P.seed, P.thr, e, P.scale);
+    if (drop) dropout4(v, seed, P.thr, e, P.scale);
   } else if (EPI == EPI_GELU || EPI == EPI_GELU_TANH) {
     f32x4 dg;
 #pragma unroll
@@ -170,8 +172,8 @@ DLLM_DEVICE f32x4 epilogue4(const GemmFusedParams& P, int m, int n, f32x4 v) {
     }
     if (drop) {
       bool k0, k1, k2, k3;
-      keep_two(P.seed, P.thr, e, k0, k1);
-      keep_two(P.seed, P.thr, e + 2u, k2, k3);
+      keep_two(seed, P.thr, e, k0, k1);
+      keep_two(seed, P.thr, e + 2u, k2, k3);
       const float s0 = k0 ? P.scale : 0.f, s1 = k1 ? P.scale : 0.f, s2 = k2 ? P.scale : 0.f, s3 = k3 ? P.scale : 0.f;
       v = v * f32x4{s0, s1, s2, s3};
       dg = dg * f32x4{s0, s1, s2, s3};
@@ -205,6 +207,7 @@ DLLM_DEVICE f32x4 epilogue4(const GemmFusedParams& P, int m, int n, f32x4 v) {
 template <int BK, int NBUF, bool BKM, int EPI, int MF, bool PRE = false>
 __global__ __launch_bounds__(NT, 1) void gemm_fused_kernel(GemmFusedParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const uint32_t seed = P.p > 0.f ? eff_seed(P.seed) : P.seed;
   uint16_t* lds = reinterpret_cast<uint16_t*>(smem);  // [NBUF][A image | B image], BK*256 elements each
   using RI = RowImg<BK, MF == 16>;
   constexpr int TILE = BK * 256;
@@ -324,7 +327,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_fused_kernel(GemmFusedParams P) {
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const f32x4 v = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
-          epilogue4<EPI>(P, mrow + 32 * i, n0 + wn * 64 + 32 * j + 8 * g + 4 * hh, v + bv[j][g]);
+          epilogue4<EPI>(P, seed, mrow + 32 * i, n0 + wn * 64 + 32 * j + 8 * g + 4 * hh, v + bv[j][g]);
         }
   } else {
     static_assert(MF == 16 && (BK == 64 || BK == 32) && (!PRE || BK == 64), "16x16x32 images: BK = 64, or 32 (S16)");
@@ -379,7 +382,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_fused_kernel(GemmFusedParams P) {
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) epilogue4<EPI>(P, mrow + 16 * i, ncol + 16 * j, acc[i][j] + bv[j]);
+      for (int j = 0; j < 4; ++j) epilogue4<EPI>(P, seed, mrow + 16 * i, ncol + 16 * j, acc[i][j] + bv[j]);
   }
 }
 
@@ -417,6 +420,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_fused_kernel(GemmFusedParams P) {
 template <int EPI, bool BKM, bool PERSIST>
 __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(GemmFusedParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const uint32_t seed = P.p > 0.f ? eff_seed(P.seed) : P.seed;
   uint16_t* lds = reinterpret_cast<uint16_t*>(smem);  // [2][A image | B image], [256][64] each
   using RI = RowImg<64>;
   constexpr int TILE = 64 * 256;
@@ -731,8 +735,8 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(GemmFusedParams P) {
           if (P.p > 0.f) {  // keep decision on the OUTPUT element m * F + f, as csrc/act.hip's gated path
             bool k0, k1, k2, k3;
             const uint32_t e = (uint32_t)m * (uint32_t)F + (uint32_t)f;
-            keep_two(P.seed, P.thr, e, k0, k1);
-            keep_two(P.seed, P.thr, e + 2u, k2, k3);
+            keep_two(seed, P.thr, e, k0, k1);
+            keep_two(seed, P.thr, e + 2u, k2, k3);
             const f32x4 s = {k0 ? P.scale : 0.f, k1 ? P.scale : 0.f, k2 ? P.scale : 0.f, k3 ? P.scale : 0.f};
             h = h * s;
             g1 = g1 * s;
@@ -763,7 +767,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(GemmFusedParams P) {
       for (int i = 0; i < 8; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const f32x4 v = epilogue4<EPI>(P, mrow + 16 * i, ncol + 16 * j, acc[i][j] + bv[j]);
+          const f32x4 v = epilogue4<EPI>(P, seed, mrow + 16 * i, ncol + 16 * j, acc[i][j] + bv[j]);
           if (EPI == EPI_RELU) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) bits[i >> 1] |= (v[r] != 0.f ? 1u : 0u) << ((i & 1) * 16 + 4 * j + r);

@@ -11,6 +11,8 @@
 
 using namespace dllm;
 
+DLLM_SEED_STEP_TU(norm)
+
 namespace {
 
 template <typename T, int KIND, int MAXV>
@@ -20,6 +22,7 @@ __global__ __launch_bounds__(256) void norm_fwd_kernel(const T* __restrict__ x, 
                                                        float* __restrict__ mean_out, float* __restrict__ rstd_out,
                                                        int N, int d, float eps, float p, uint32_t seed,
                                                        uint32_t thr) {
+  if (p > 0.f) seed = eff_seed(seed);
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= N) return;
@@ -91,6 +94,7 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(const T* __restrict__ dou
                                                        T* __restrict__ dstream, float* __restrict__ dw_part,
                                                        float* __restrict__ db_part, int N, int d, float p,
                                                        uint32_t seed, uint32_t thr) {
+  if (p > 0.f) seed = eff_seed(seed);
   extern __shared__ __attribute__((aligned(16))) float red[];  // [4][d]
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const bool drop = p > 0.f;

@@ -53,8 +53,19 @@ class FusedAdamW:
             return _ext.native().sq_norm(g).sqrt()
         return torch.linalg.vector_norm(g.float())
 
+    def device_hyper(self, t: torch.Tensor, lr) -> torch.Tensor:
+        """[lr, lr / bc1, 1 / sqrt(bc2)] as a device tensor from a device step count ``t`` (float, already incremented)
+        and ``lr`` (float or device scalar): the AdamW kernel reads it instead of host floats, so a captured graph
+        replays with the right bias corrections and learning rate every step."""
+        b1, b2 = self.betas
+        lr_t = lr if torch.is_tensor(lr) else torch.full_like(t, float(lr))
+        bc1 = 1.0 - torch.pow(torch.full_like(t, b1), t)
+        bc2 = 1.0 - torch.pow(torch.full_like(t, b2), t)
+        return torch.stack([lr_t, lr_t / bc1, torch.rsqrt(bc2)]).reshape(3).float().contiguous()
+
     @torch.no_grad()
-    def step(self, max_grad_norm: float | None = None) -> torch.Tensor | None:
+    def step(self, max_grad_norm: float | None = None, hyper: torch.Tensor | None = None) -> torch.Tensor | None:
+        """One clip + AdamW update.  ``hyper`` (device_hyper) replaces the host lr / bias corrections (graph mode)."""
         lr = self.param_groups[0]["lr"]
         self.step_count += 1
         norm = None
@@ -70,8 +81,10 @@ class FusedAdamW:
         if _ext.use_native(p):
             _ext.native().adamw_step(p, self.master, g, self.exp_avg, self.exp_avg_sq, self.wd_mask, coef, float(lr),
                                      float(b1), float(b2), float(self.eps), float(self.weight_decay), float(bc1),
-                                     float(bc2))
+                                     float(bc2), hyper)
         else:
+            if hyper is not None:
+                lr, bc1, bc2 = float(hyper[0]), float(hyper[0] / hyper[1]), float(1.0 / hyper[2] ** 2)
             self._reference_step(p, g, coef, lr, b1, b2, bc1, bc2)
         return norm
 

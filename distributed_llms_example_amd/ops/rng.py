@@ -35,7 +35,7 @@ def threshold16(p: float) -> int:
 
 def keep_from_index(seed: int, p: float, idx: torch.Tensor) -> torch.Tensor:
     """Keep decision for element indices ``idx`` (any shape, int64)."""
-    h = mix32(seed, idx >> 1)
+    h = mix32(effective_seed(seed), idx >> 1)
     half = torch.where((idx & 1) == 1, h >> 16, h & 0xFFFF)
     return half >= threshold16(p)
 
@@ -63,7 +63,7 @@ def attention_keep_mask(seed: int, p: float, B: int, H: int, Sq: int, Sk: int, d
     attention kernels; ``g`` alone is linear in ``kp`` and leaves lag-2 drops anti-correlated), ``y = h ^ (h >> 16)``;
     the even key keeps iff ``y & 0xFFFF >= threshold16(p)``, the odd key iff ``h >> 16 >= threshold16(p)``."""
     rows = torch.arange(B * H * Sq, device=device, dtype=torch.int64)
-    rh = mix32(seed, rows).view(B, H, Sq, 1)
+    rh = mix32(effective_seed(seed), rows).view(B, H, Sq, 1)
     j = torch.arange(Sk, device=device, dtype=torch.int64).view(1, 1, 1, Sk)
     x = (rh + (j >> 1) * _G) & 0xFFFFFF
     g = (x * _C24) & _MASK
@@ -84,15 +84,24 @@ def mix_host(seed: int, idx: int) -> int:
 
 class DropoutRNG:
     """Per-process seed stream.  ``next_seed()`` is called once per dropout site per forward; the
-    seed is saved for the backward.  ``state_dict`` makes resumed runs reproduce the stream."""
+    seed is saved for the backward.  ``state_dict`` makes resumed runs reproduce the stream.
+
+    Step-seed mode (``StepSeed``, for HIP-graph replay): the kernels mix a DEVICE step counter into every site seed,
+    so the host stream restarts at the same point every micro-step (``begin_micro_step``) — the seeds a captured graph
+    baked in are exactly the ones an eager step would draw, and the masks still change every step."""
 
     def __init__(self, seed: int = 42):
         self.base = seed & _MASK
         self.counter = 0
+        self.site_mode = False
 
     def next_seed(self) -> int:
         self.counter += 1
         return mix_host(self.base, self.counter)
+
+    def begin_micro_step(self):
+        if self.site_mode:
+            self.counter = 0
 
     def state_dict(self):
         return {"base": self.base, "counter": self.counter}
@@ -100,6 +109,48 @@ class DropoutRNG:
     def load_state_dict(self, d):
         self.base = int(d["base"])
         self.counter = int(d["counter"])
+
+
+class StepSeed:
+    """Device step counter mixed into every dropout site seed by the HIP kernels (csrc/common.h DLLM_SEED_STEP_TU):
+    effective seed = mix32(site seed, step).  ``advance()`` is a device add (captured by a graph, so each replay draws
+    new masks); ``host`` mirrors it for the reference ops and for checkpoints (no device read)."""
+
+    def __init__(self, device, start: int = 0):
+        self.t = torch.full((1,), start, dtype=torch.int32, device=device)
+        self.host = start
+        self.enabled = False
+
+    def enable(self):
+        from .. import _ext
+        if self.t.is_cuda and _ext.native() is not None:
+            _ext.native().set_seed_step(self.t)
+        self.enabled = True
+        _active_step[0] = self
+
+    def disable(self):
+        from .. import _ext
+        if self.t.is_cuda and _ext.native() is not None:
+            _ext.native().set_seed_step(None)
+        self.enabled = False
+        if _active_step[0] is self:
+            _active_step[0] = None
+
+    def advance(self, n: int = 1):
+        self.t.add_(n)
+        self.host += n
+
+
+_active_step: list = [None]
+
+
+def effective_seed(seed: int) -> int:
+    """The seed a kernel actually hashes with (the reference ops mirror it): the site seed, mixed with the device step
+    counter's host mirror in step-seed mode."""
+    st = _active_step[0]
+    if st is None or not st.enabled:
+        return seed
+    return mix_host(seed & _MASK, st.host & _MASK)
 
 
 _global = DropoutRNG(42)

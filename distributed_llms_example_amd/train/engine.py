@@ -12,6 +12,7 @@ import os
 
 import torch
 
+from ..ops import rng as rng_mod
 from ..ops.optim import FusedAdamW
 from ..utils import profiling
 from ..parallel.env import DistEnv
@@ -55,6 +56,17 @@ class TrainEngine:
                                     no_decay=no_decay)
         self.max_grad_norm = max_grad_norm
         self.label_smoothing = label_smoothing
+        self.step_seed: rng_mod.StepSeed | None = None
+
+    def enable_step_seeds(self) -> rng_mod.StepSeed:
+        """Dropout seeds that a captured HIP graph can replay (ops/rng.py StepSeed): from now on every micro-step
+        advances a device counter the kernels mix into each site seed, and the host seed stream restarts per micro-step.
+        Masks differ from the default mode's (another, equally uniform, stream), so enable it before training."""
+        if self.step_seed is None:
+            self.step_seed = rng_mod.StepSeed(self.env.device)
+            self.step_seed.enable()
+            rng_mod.default_rng().site_mode = True
+        return self.step_seed
 
     def no_sync(self):
         return self.reducer.no_sync() if self.reducer is not None else contextlib.nullcontext()
@@ -84,6 +96,9 @@ class TrainEngine:
         counts (default: the reducer's world; context-parallel ranks share one batch and count once).  Without it each micro-batch mean is divided by
         ``grad_accum`` (identical when every micro-batch has the same token count)."""
         ctx = contextlib.nullcontext() if sync else self.no_sync()
+        if self.step_seed is not None:
+            self.step_seed.advance()
+            rng_mod.default_rng().begin_micro_step()
         with ctx:
             with profiling.range("forward"):
                 out = self.forward(batch)
@@ -100,12 +115,13 @@ class TrainEngine:
                 self.reducer.post_backward()
         return loss.detach()
 
-    def step(self, lr: float | None = None):
-        """Clip + AdamW + zero_grad.  Returns the pre-clip grad norm as a device tensor (or None)."""
+    def step(self, lr: float | None = None, hyper: torch.Tensor | None = None):
+        """Clip + AdamW + zero_grad.  Returns the pre-clip grad norm as a device tensor (or None).  ``hyper``: device
+        [lr, lr / bc1, 1 / sqrt(bc2)] (graph mode, ops/optim.py device_hyper)."""
         if lr is not None:
             self.optimizer.param_groups[0]["lr"] = lr
         with profiling.range("optimizer(clip+adamw)"):
-            norm = self.optimizer.step(self.max_grad_norm)
+            norm = self.optimizer.step(self.max_grad_norm, hyper=hyper)
             self.optimizer.zero_grad()
         return norm
 

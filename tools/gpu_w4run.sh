@@ -6,8 +6,10 @@ O=gpurun_out/w4c
 mkdir -p $O
 step() { echo "[w4run] $*"; }
 step tests
-timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gemm_w4_gpu.py \
-  tests/test_model_gpu.py > $O/test.log 2>&1 || { tail -40 $O/test.log; exit 1; }
+timeout -k 10 900 python -u -m pytest -q --timeout 200 --timeout-method thread tests/test_gemm_w4_gpu.py \
+  tests/test_model_gpu.py tests/test_graph_gpu.py tests/test_kernels_gpu.py tests/test_grads_gpu.py -s > $O/test.log 2>&1
+rc=$?; [ $rc -gt 1 ] && { tail -40 $O/test.log; exit 1; }
+grep -E "FAILED|passed|failed" $O/test.log | tail -15
 tail -2 $O/test.log
 grep -E "^\[parity" $O/test.log | head
 step microbench
