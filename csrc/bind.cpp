@@ -677,8 +677,9 @@ Tensor gemm_w4(const Tensor& a, const Tensor& b, bool b_kmajor, const optional<T
     c = *out;
     TORCH_CHECK(c.is_cuda() && c.device() == a.device() && c.scalar_type() == at::kBFloat16 && c.dim() == 2 &&
                     c.size(0) == M && c.size(1) == N && c.stride(1) == 1 && c.stride(0) % 8 == 0 &&
-                    reinterpret_cast<uintptr_t>(c.data_ptr()) % 16 == 0,
-                "gemm_w4: out must be a bf16 [M, N] GPU tensor with unit inner stride and 16-B aligned rows");
+                    reinterpret_cast<uintptr_t>(c.data_ptr()) % 16 == 0 && 256 * c.stride(0) * 2 < (1LL << 31),
+                "gemm_w4: out must be a bf16 [M, N] GPU tensor with unit inner stride, 16-B aligned rows and a 256-row "
+                "byte range < 2^31");
   } else {
     TORCH_CHECK(!accumulate, "gemm_w4: accumulate needs out");
     c = at::empty({M, N}, a.options());

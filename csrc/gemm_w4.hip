@@ -29,6 +29,8 @@
 // * bijective XCD remap of the 1-D grid, tiles grouped grp x (32 / grp) per XCD for L2 reuse of A and B.
 #include "common.h"
 
+#include <cstdlib>
+
 #include "gemm_params.h"
 
 using namespace dllm;
@@ -106,7 +108,9 @@ DLLM_DEVICE void mfma0(f32x4& c, const bf16x8v& b, const bf16x8v& a) {
   asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(c) : "v"(b), "v"(a));
 }
 
-template <bool BKM, bool BIAS, bool ACC>
+// RS = fragment read schedule: 0 spreads the 16 next-sub-step reads over the 8 chunks (2 per chunk), 1 issues them
+// 4 per chunk in the first 4 chunks after they become legal (more MFMA cover for their latency)
+template <bool BKM, bool BIAS, bool ACC, int RS>
 __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr uint32_t TB = 256 * BK * 2;  // one operand image: 32 KB
@@ -253,12 +257,22 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         chunk(fa0, fb0, i);
-        if (i < 4) {
-          fb1[2 * i] = rd_b(b, 1, 2 * i);
-          fb1[2 * i + 1] = rd_b(b, 1, 2 * i + 1);
+        if constexpr (RS == 0) {
+          if (i < 4) {
+            fb1[2 * i] = rd_b(b, 1, 2 * i);
+            fb1[2 * i + 1] = rd_b(b, 1, 2 * i + 1);
+          } else {
+            fa1[2 * i - 8] = rd_a(b, 1, 2 * i - 8);
+            fa1[2 * i - 7] = rd_a(b, 1, 2 * i - 7);
+          }
         } else {
-          fa1[2 * i - 8] = rd_a(b, 1, 2 * i - 8);
-          fa1[2 * i - 7] = rd_a(b, 1, 2 * i - 7);
+          if (i < 2) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) fb1[4 * i + e] = rd_b(b, 1, 4 * i + e);
+          } else if (i < 4) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) fa1[4 * (i - 2) + e] = rd_a(b, 1, 4 * (i - 2) + e);
+          }
         }
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -279,16 +293,26 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
 #pragma unroll
         for (int d = lo; d < hi; ++d) dma_next(ti, kt, d, b);
         // fragments of k-tile g+1 (buffer b ^ 1), first half: B in chunks 1..4, A in chunks 5..7
-        if (i <= 4) {
-          fb0[2 * i - 2] = rd_b(b ^ 1, 0, 2 * i - 2);
-          fb0[2 * i - 1] = rd_b(b ^ 1, 0, 2 * i - 1);
-        } else if (i < 7) {
-          fa0[3 * (i - 5)] = rd_a(b ^ 1, 0, 3 * (i - 5));
-          fa0[3 * (i - 5) + 1] = rd_a(b ^ 1, 0, 3 * (i - 5) + 1);
-          fa0[3 * (i - 5) + 2] = rd_a(b ^ 1, 0, 3 * (i - 5) + 2);
+        if constexpr (RS == 0) {
+          if (i <= 4) {
+            fb0[2 * i - 2] = rd_b(b ^ 1, 0, 2 * i - 2);
+            fb0[2 * i - 1] = rd_b(b ^ 1, 0, 2 * i - 1);
+          } else if (i < 7) {
+            fa0[3 * (i - 5)] = rd_a(b ^ 1, 0, 3 * (i - 5));
+            fa0[3 * (i - 5) + 1] = rd_a(b ^ 1, 0, 3 * (i - 5) + 1);
+            fa0[3 * (i - 5) + 2] = rd_a(b ^ 1, 0, 3 * (i - 5) + 2);
+          } else {
+            fa0[6] = rd_a(b ^ 1, 0, 6);
+            fa0[7] = rd_a(b ^ 1, 0, 7);
+          }
         } else {
-          fa0[6] = rd_a(b ^ 1, 0, 6);
-          fa0[7] = rd_a(b ^ 1, 0, 7);
+          if (i <= 2) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) fb0[4 * (i - 1) + e] = rd_b(b ^ 1, 0, 4 * (i - 1) + e);
+          } else if (i <= 4) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) fa0[4 * (i - 3) + e] = rd_a(b ^ 1, 0, 4 * (i - 3) + e);
+          }
         }
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -340,7 +364,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
             y1 = r1[1];
           }
           const int nl = nc + 16 * j;
-          const uint32_t off = n0 + nl < P.N ? (uint32_t)((mr + 32 * ii) * P.ldc + nl) * 2u : kOOB;
+          const uint32_t off = n0 + nl < P.N ? (uint32_t)((mr + 32 * ii) * P.ldc + n0 + nl) * 2u : kOOB;
           u32x4 o = {x0, x1, y0, y1};
           if constexpr (ACC) {
             const u32x4 c = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(srdC, off, 0, 0));
@@ -383,20 +407,28 @@ int num_cus() {
 
 // persist: one workgroup per CU (LDS and registers admit one) walking its tiles, when there are more tiles than CUs
 // and at least 2 k-tiles per tile; otherwise one tile per workgroup
-template <bool BKM, bool BIAS, bool ACC>
-int launch(const GemmW4Params& p, bool persist, hipStream_t st) {
+template <bool BKM, bool BIAS, bool ACC, int RS>
+int launch_rs(const GemmW4Params& p, bool persist, hipStream_t st) {
   constexpr size_t lds = 2 * 2 * 256 * BK * 2;  // 128 KB
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_w4_kernel<BKM, BIAS, ACC>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
+    (void)hipFuncSetAttribute((const void*)gemm_w4_kernel<BKM, BIAS, ACC, RS>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
   const int T = p.tm * p.tn, cus = num_cus() / 8 * 8;
   const int grid = persist && p.K >= 2 * BK && cus >= 8 && T > cus ? cus : T;
-  hipLaunchKernelGGL((gemm_w4_kernel<BKM, BIAS, ACC>), dim3(grid), dim3(NT), lds, st, p);
+  hipLaunchKernelGGL((gemm_w4_kernel<BKM, BIAS, ACC, RS>), dim3(grid), dim3(NT), lds, st, p);
   DLLM_CHECK_LAUNCH();
   return 0;
+}
+
+// DLLM_W4_RS: fragment read schedule (kernel template RS), read per call so microbenchmarks can A/B it in one process
+template <bool BKM, bool BIAS, bool ACC>
+int launch(const GemmW4Params& p, bool persist, hipStream_t st) {
+  const char* e = getenv("DLLM_W4_RS");
+  if (e && e[0] == '1') return launch_rs<BKM, BIAS, ACC, 1>(p, persist, st);
+  return launch_rs<BKM, BIAS, ACC, 0>(p, persist, st);
 }
 
 template <bool BKM>

@@ -281,17 +281,18 @@ def test_bf16_params_fp32_grad_buffer_cpu():
         assert cos > 0.98, (seg.name, cos)
 
 
-def test_attention_dropout_hash_statistics():
-    """The attention keep-mask hash (one 24-bit multiply per key pair): rate, pair / row / column independence."""
-    p = 0.1
+@pytest.mark.parametrize("p", [0.1, 0.5])
+def test_attention_dropout_hash_statistics(p):
+    """The attention keep-mask hash (two 24-bit multiplies per key pair): rate, pair / row / column independence."""
     k = rng.attention_keep_mask(77, p, 2, 4, 256, 512, "cpu").double()
     d = 1 - k
-    assert abs(d.mean().item() - p) < 0.002
+    assert abs(d.mean().item() - p) < 0.004
     both_pair = (d[..., 0::2] * d[..., 1::2]).mean().item()      # the two keys of one hash
     both_row = (d[:, :, 0::2, :] * d[:, :, 1::2, :]).mean().item()  # adjacent query rows
     both_far = (d[..., :256] * d[..., 256:]).mean().item()
+    tol = 0.0015 if p < 0.3 else 0.006
     for v in (both_pair, both_row, both_far):
-        assert abs(v - p * p) < 0.0015, (both_pair, both_row, both_far)
+        assert abs(v - p * p) < tol, (both_pair, both_row, both_far)
     # lag-2 (odd-odd, even-even: successive hashes of one row), lag-3 and lag-16 keys: independent draws give p^2
     dd = d.reshape(-1, d.shape[-1])
     oo = (dd[:, 1::2][:, :-1] * dd[:, 1::2][:, 1:]).mean().item()
@@ -299,7 +300,7 @@ def test_attention_dropout_hash_statistics():
     l3 = (dd[:, :-3] * dd[:, 3:]).mean().item()
     l16 = (dd[:, :-16] * dd[:, 16:]).mean().item()
     for v in (oo, ee, l3, l16):
-        assert abs(v - p * p) < 0.0015, (oo, ee, l3, l16)
+        assert abs(v - p * p) < tol, (oo, ee, l3, l16)
     # per-row drop counts: binomial variance Sk p (1 - p) (a hash linear in the key index had ~1/8 of it)
     var = dd.sum(1).var().item()
     binom = dd.shape[1] * p * (1 - p)

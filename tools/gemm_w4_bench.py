@@ -75,10 +75,13 @@ def main():
             for k, fn in arms.items():
                 if k != "lib":
                     rec[f"{k}_relerr"] = float(f"{((fn().float() - ref).norm() / ref.norm()).item():.2e}")
+            arms["w4rs1"] = arms["w4"]  # same call, DLLM_W4_RS=1 (early fragment reads), set per arm below
             times = {k: [] for k in arms}
             for _ in range(a.rounds):
                 for k, fn in arms.items():
+                    os.environ["DLLM_W4_RS"] = "1" if k == "w4rs1" else "0"
                     times[k].append(timeit(fn, a.iters))
+            os.environ["DLLM_W4_RS"] = "0"
             for k, ts in times.items():
                 t = statistics.median(ts)
                 rec[f"{k}_us"] = round(t * 1e6, 1)
