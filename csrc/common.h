@@ -30,8 +30,10 @@ DLLM_DEVICE uint16_t f2bf(float f) {
   return __builtin_bit_cast(uint16_t, b);
 }
 
+// one v_cvt_pk_bf16_f32 (RNE, as f2bf); the scalar form costs 2 converts + shift + or
+typedef __attribute__((ext_vector_type(2))) __bf16 dllm_bf16x2;
 DLLM_DEVICE uint32_t pack_bf16x2(float lo, float hi) {
-  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{lo, hi}, dllm_bf16x2));
 }
 
 // ---- generic element access for bf16 (uint16 storage) / fp32 --------------------------------
@@ -51,8 +53,8 @@ template <> struct Elem<uint16_t> {
     return f32x4{bf2f(r.x), bf2f(r.y), bf2f(r.z), bf2f(r.w)};
   }
   static DLLM_DEVICE void store4(uint16_t* p, f32x4 v) {
-    u16x4 r = {f2bf(v.x), f2bf(v.y), f2bf(v.z), f2bf(v.w)};
-    *reinterpret_cast<u16x4*>(p) = r;
+    const uint32_t lo = pack_bf16x2(v.x, v.y), hi = pack_bf16x2(v.z, v.w);
+    *reinterpret_cast<uint2*>(p) = make_uint2(lo, hi);
   }
   static DLLM_DEVICE float round(float v) { return bf2f(f2bf(v)); }
 };

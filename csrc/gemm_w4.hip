@@ -30,6 +30,7 @@
 #include "common.h"
 
 #include <cstdlib>
+#include <type_traits>
 
 #include "gemm_params.h"
 
@@ -59,14 +60,35 @@ DLLM_DEVICE i32x4 make_srd(const void* base, uint32_t bytes) {
   return r;
 }
 
-// 16 B per lane from srd + voff to LDS byte lds + 16 * lane.  M0 is written here and nowhere else in the kernel
-// (clobbered, not saved): 1 SALU per DMA.  Invisible to the compiler's vmcnt bookkeeping (as glds16 in common.h);
-// retired by the explicit counted waits below.
-DLLM_DEVICE void dma16(const i32x4& srd, uint32_t voff, uint32_t lds) {
-  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds"
+// 16 B per lane from srd + voff + soff to LDS byte ldsb + IMM + 16 * lane.  The per-lane offset is fixed for the
+// whole kernel, the k-tile advance is the wave-uniform soff, and M0 is formed by the DMA statement itself (written
+// here and nowhere else; clobbered, not saved): 1 SALU + the M0 -> LDS-DMA wait state per DMA, no VALU.  Invisible to
+// the compiler's vmcnt bookkeeping (as glds16 in common.h); retired by the explicit counted waits below.
+template <uint32_t IMM>
+DLLM_DEVICE void dma16(const i32x4& srd, uint32_t voff, uint32_t soff, uint32_t ldsb) {
+  asm volatile("s_add_u32 m0, %3, %4\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, %2 offen lds"
                :
-               : "v"(voff), "s"(srd), "s"(lds)
-               : "memory", "m0");
+               : "v"(voff), "s"(srd), "s"(soff), "s"(ldsb), "i"(IMM)
+               : "memory", "m0", "scc");
+}
+
+// descriptor moved forward by `bytes` (base up, range down): the k-major B operand's k-tile advance
+DLLM_DEVICE i32x4 srd_advance(const i32x4& s, uint32_t bytes) {
+  const uint64_t a = (((uint64_t)(uint32_t)s.y & 0xFFFFu) << 32 | (uint32_t)s.x) + bytes;
+  i32x4 r;
+  r.x = (int)(uint32_t)a;
+  r.y = (int)((uint32_t)(a >> 32) & 0xFFFFu);
+  r.z = (int)((uint32_t)s.z - bytes);
+  r.w = s.w;
+  return r;
+}
+
+template <int B, int E, typename F>
+DLLM_DEVICE void sfor(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    sfor<B + 1, E>(f);
+  }
 }
 
 // ---- k-major [64][256] image (512-B rows) of the NN B operand, transposed reads (csrc/gemm_fused.hip layout)
@@ -145,16 +167,17 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
   };
   auto srd_a = [&](int m0) { return make_srd(P.A + (long)m0 * P.lda, (uint32_t)(min(P.M - m0, 256) * P.lda * 2)); };
   auto srd_b = [&](int n0) {
-    return BKM ? make_srd(P.B + n0, (uint32_t)(((long)P.K * P.ldb - n0) * 2))
+    return BKM ? make_srd(P.B + n0, (uint32_t)(((long)(P.K - 1) * P.ldb + P.N - n0) * 2))
                : make_srd(P.B + (long)n0 * P.ldb, (uint32_t)(min(P.N - n0, 256) * P.ldb * 2));
   };
 
-  // ---- per-lane DMA offsets.  Row image ([256][64], 128-B rows): wave-instruction q covers rows 8q .. 8q+7,
-  // lane -> (row 8q + l/8, 16-B chunk (l%8) ^ ((row/2)&7)).  K-major image ([64][256], 512-B rows): instruction q covers
-  // k-rows 2q, 2q+1, lane -> (k-row 2q + l/32, chunk (l%32) ^ gsw(k-row)); columns past N read 0 (offset pushed out of
-  // range per tile: colb).
+  // ---- per-lane DMA offsets (tile- and k-invariant).  Row image ([256][64], 128-B rows): wave-instruction q covers
+  // rows 8q .. 8q+7, lane -> (row 8q + l/8, 16-B chunk (l%8) ^ ((row/2)&7)); rows past M / N fall out of the tile's
+  // descriptor range.  K-major image ([64][256], 512-B rows): instruction q covers k-rows 2q, 2q+1, lane -> (k-row
+  // 2q + l/32, chunk (l%32) ^ gsw(k-row)).  K-major columns past N are NOT masked: they load neighbouring elements of
+  // B's view (the descriptor spans exactly the view, so nothing past it), which only reach output columns >= N, and
+  // those are never stored (column j of C depends on column j of B alone).
   uint32_t va[8], vb[8];
-  int colb[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int q = w * 8 + i;
@@ -163,22 +186,36 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
     va[i] = (uint32_t)(r * P.lda + c * 8) * 2u;
     if (BKM) {
       const int kr = 2 * q + (lane >> 5);
-      colb[i] = ((lane & 31) ^ gsw(kr)) * 8;
-      vb[i] = (uint32_t)(kr * P.ldb + colb[i]) * 2u;
+      vb[i] = (uint32_t)(kr * P.ldb + ((lane & 31) ^ gsw(kr)) * 8) * 2u;
     } else {
-      colb[i] = 0;
       vb[i] = (uint32_t)(r * P.ldb + c * 8) * 2u;
     }
   }
-  const uint32_t lds0 = lds_addr(smem);
-  const uint32_t kstepB = BKM ? (uint32_t)(BK * P.ldb * 2) : (uint32_t)(BK * 2);
-  // DMA of k-tile kt of the tile (sa, sb, n0) into buffer b: instruction i of operand X -> image bytes (8 w + i) * 1 KB
-  auto dma_a = [&](const i32x4& sa, int i, int kt, int b) {
-    dma16(sa, va[i] + (uint32_t)kt * (BK * 2), lds0 + (uint32_t)b * BUF + (uint32_t)(8 * w + i) * 1024u);
+  const uint32_t lds0 = lds_addr(smem) + (uint32_t)w * 8192u;  // this wave's 8 KB slice of each operand image
+  // the 16 DMAs of one k-tile: instruction d < 8 -> A image bytes (8 w + d) KB, d >= 8 -> B image (8 w + d - 8) KB.
+  // Row images advance by soffset (k-tile * 128 B inside the row); the k-major image by moving its descriptor.
+  struct Dma {
+    i32x4 sa, sb;
+    uint32_t soa, sob, ldsb;
   };
-  auto dma_b = [&](const i32x4& sb, int n0, int i, int kt, int b) {
-    const uint32_t off = BKM && n0 + colb[i] >= P.N ? kOOB : vb[i] + (uint32_t)kt * kstepB;
-    dma16(sb, off, lds0 + (uint32_t)b * BUF + TB + (uint32_t)(8 * w + i) * 1024u);
+  auto dma_plan = [&](const i32x4& sa, const i32x4& sb, int kk, int b) {
+    Dma r;
+    r.sa = sa;
+    r.soa = (uint32_t)kk * (BK * 2);
+    if constexpr (BKM) {
+      r.sb = srd_advance(sb, (uint32_t)kk * (uint32_t)(BK * P.ldb * 2));
+      r.sob = 0;
+    } else {
+      r.sb = sb;
+      r.sob = r.soa;
+    }
+    r.ldsb = lds0 + (uint32_t)b * BUF;
+    return r;
+  };
+  auto dma = [&](const Dma& q, auto D) {
+    constexpr int d = decltype(D)::value;
+    if constexpr (d < 8) dma16<(uint32_t)d * 1024u>(q.sa, va[d], q.soa, q.ldsb);
+    else dma16<TB + (uint32_t)(d - 8) * 1024u>(q.sb, vb[d - 8], q.sob, q.ldsb);
   };
 
   // ---- fragment reads.  Row image: a[i] = rows wm*128 + 16 i + (l & 15), k chunk kk/8 + (l >> 4), swizzled by
@@ -204,23 +241,19 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
   tile_mn(0, m0, n0);
   if (ntw > 1) tile_mn(1, m1, n1);
   i32x4 sa0 = srd_a(m0), sb0 = srd_b(n0), sa1 = srd_a(m1), sb1 = srd_b(n1);
-  // source of the DMA for k-tile kt + 2 of tile i (tile-local numbering; >= nk means the next tile)
-  auto dma_next = [&](int i, int kt, int d, int b) {
+  // DMA plan for k-tile kt + 2 of tile i (tile-local numbering; >= nk means the next tile) into buffer b
+  auto plan_next = [&](int i, int kt, int b) {
     const int kn = kt + 2;
     const bool cross = kn >= nk && i + 1 < ntw;
-    const int kk = cross ? kn - nk : min(kn, nk - 1);
-    if (d < 8) dma_a(cross ? sa1 : sa0, d, kk, b);
-    else dma_b(cross ? sb1 : sb0, cross ? n1 : n0, d - 8, kk, b);
+    return dma_plan(cross ? sa1 : sa0, cross ? sb1 : sb0, cross ? kn - nk : min(kn, nk - 1), b);
   };
 
   // ---- prologue: k-tiles 0 and 1 in flight, wait for k-tile 0, read its first half
-#pragma unroll
-  for (int d = 0; d < 16; ++d) {
-    if (d < 8) dma_a(sa0, d, 0, 0);
-    else dma_b(sb0, n0, d - 8, 0, 0);
+  {
+    const Dma q0 = dma_plan(sa0, sb0, 0, 0), q1 = plan_next(0, -1, 1);
+    sfor<0, 16>([&](auto D) { dma(q0, D); });
+    sfor<0, 16>([&](auto D) { dma(q1, D); });
   }
-#pragma unroll
-  for (int d = 0; d < 16; ++d) dma_next(0, -1, d, 1);
   wait_vm<16>();
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
@@ -234,14 +267,15 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) mfma(acc[i][j], fb[j], fa[i]);
   };
+  // first 32-deep step of a tile: C = 0 in the instruction, so no 256-write accumulator zeroing pass
+  auto chunk0 = [&](const bf16x8v (&fa)[8], const bf16x8v (&fb)[8], int i) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) mfma0(acc[i][j], fb[j], fa[i]);
+  };
 
   int g = 0;  // global k-tile counter (buffer parity)
   int ti = 0;
   do {  // tiles
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     // every k-tile runs the same branch-free body: a peeled last k-tile makes the allocator re-assign all 256 AGPRs
     // between loop and tail (~600 v_accvgpr copies), and with a zero-trip path it keeps a VGPR copy of the zeroed
     // accumulators alive (do-while, nk >= 1)
@@ -256,7 +290,8 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
       // (the next sub-step's first chunk needs all of B and a[0])
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        chunk(fa0, fb0, i);
+        if (kt == 0) chunk0(fa0, fb0, i);
+        else chunk(fa0, fb0, i);
         if constexpr (RS == 0) {
           if (i < 4) {
             fb1[2 * i] = rd_b(b, 1, 2 * i);
@@ -285,13 +320,12 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
       else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int i = 1; i < 8; ++i) {
+      const Dma q = plan_next(ti, kt, b);
+      sfor<1, 8>([&](auto I) {
+        constexpr int i = decltype(I)::value;
         chunk(fa1, fb1, i);
         // DMA: instructions 0..7 of A then of B, spread over chunks 1..7 (2, 2, 2, 3, 2, 2, 3)
-        const int lo = (i - 1) * 16 / 7, hi = i * 16 / 7;
-#pragma unroll
-        for (int d = lo; d < hi; ++d) dma_next(ti, kt, d, b);
+        sfor<(i - 1) * 16 / 7, i * 16 / 7>([&](auto D) { dma(q, D); });
         // fragments of k-tile g+1 (buffer b ^ 1), first half: B in chunks 1..4, A in chunks 5..7
         if constexpr (RS == 0) {
           if (i <= 4) {
@@ -315,7 +349,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
           }
         }
         __builtin_amdgcn_sched_barrier(0);
-      }
+      });
       ++g;
     } while (++kt < nk);
 
@@ -353,7 +387,11 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
           // opaque re-definition in place: the AGPR -> VGPR copies cannot be hoisted above this point (otherwise all 256
           // accumulators are copied out at the loop exit: 256 VGPRs + spills)
           asm volatile("" : "+a"(acc[2 * ii][j]), "+a"(acc[2 * ii + 1][j]));
-          const f32x4 xv = acc[2 * ii][j] + bv[j], yv = acc[2 * ii + 1][j] + bv[j];
+          f32x4 xv = acc[2 * ii][j], yv = acc[2 * ii + 1][j];
+          if constexpr (BIAS) {
+            xv += bv[j];
+            yv += bv[j];
+          }
           uint32_t x0 = pk2(xv.x, xv.y), x1 = pk2(xv.z, xv.w), y0 = pk2(yv.x, yv.y), y1 = pk2(yv.z, yv.w);
           {
             const auto r0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);

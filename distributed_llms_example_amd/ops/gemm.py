@@ -1,7 +1,8 @@
 """Hand-written gfx950 GEMMs for every linear layer of a training step:
 
 * projections, forward ``Y = X Wᵀ (+ b)`` and input gradient ``dX (+)= dY W`` (linear_fwd / linear_dgrad):
-  csrc/gemm_w4.hip, the one-wave-per-SIMD 256x256 kernel (``DLLM_W4_GEMM=0`` selects hipBLASLt, A/B runs);
+  csrc/gemm_w4.hip, the one-wave-per-SIMD 256x256 kernel, on the shapes where it beats hipBLASLt (``_W4_MODE``
+  below; ``DLLM_W4_GEMM=1`` every supported shape, ``0`` none);
 * weight gradient ``dW (+)= dYᵀ X`` (wgrad_accumulate): csrc/gemm.hip.
 
 Weight-gradient GEMM notes:
@@ -21,13 +22,23 @@ import torch.nn.functional as F
 
 from .. import _ext
 
-_W4 = os.environ.get("DLLM_W4_GEMM", "1") != "0"
+# Routing of the projection GEMMs (profiles/r3_gemm_w4_vs_hipblaslt.jsonl, t5-base / bart-large shapes):
+#   "auto" (default): csrc/gemm_w4.hip for input gradients whose reduction depth (the layer's output features) is
+#          <= 1024 — there it beats hipBLASLt's NN kernels by 1-9 % (o / wo / fc2 dgrads, the residual-accumulating
+#          ones included); forwards and deep-K dgrads stay on hipBLASLt, which is 3-12 % faster there;
+#   "1": every supported shape on gemm_w4 (A/B and tests), "0": none.
+_W4_MODE = os.environ.get("DLLM_W4_GEMM", "auto")
+_W4 = _W4_MODE != "0"
+_W4_DGRAD_MAX_K = 1024
 w4_calls = 0  # projections that ran on csrc/gemm_w4.hip (tests assert the kernel really ran)
 
 
 def _w4_ok(a: torch.Tensor, b: torch.Tensor, kmajor: bool) -> bool:
-    return (_W4 and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and _ext.use_native(a)
-            and bool(_ext.native().gemm_w4_supported(a, b, kmajor)))
+    if not _W4 or a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16 or not _ext.use_native(a):
+        return False
+    if _W4_MODE == "auto" and not (kmajor and a.shape[-1] <= _W4_DGRAD_MAX_K):
+        return False
+    return bool(_ext.native().gemm_w4_supported(a, b, kmajor))
 
 
 def linear_fwd(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Tensor:

@@ -28,6 +28,7 @@ import torch
 import torch.nn.functional as F
 
 from .. import _ext
+from . import gemm as _gemm
 from .gemm import wgrad_accumulate
 from .linear import _fire, _fusable, _gbuf, _use
 
@@ -70,6 +71,24 @@ def _reference(h, w, labels, bias, smoothing, ignore_index):
     return F.cross_entropy(logits, labels, ignore_index=ignore_index, label_smoothing=smoothing)
 
 
+def _logits(h: torch.Tensor, wc: torch.Tensor, out: torch.Tensor) -> None:
+    """One chunk of logits ``h @ wcᵀ`` into ``out`` (csrc/gemm_w4.hip when the shape allows, else hipBLASLt)."""
+    if _gemm._w4_ok(h, wc, False):  # out: a fresh contiguous [N, n] view, n % 8 == 0
+        _gemm.w4_calls += 1
+        _ext.native().gemm_w4(h, wc, False, None, out)
+    else:
+        torch.mm(h, wc.t(), out=out)
+
+
+def _dh_accumulate(dh: torch.Tensor, g: torch.Tensor, wc: torch.Tensor) -> None:
+    """``dh += g @ wc`` with the fp32 accumulator ``dh`` read and written by the GEMM itself (beta = 1): no bf16
+    product, no separate add pass over ``[N, d]`` per chunk."""
+    if dh.is_cuda:
+        torch.addmm(dh, g, wc, out_dtype=torch.float32, out=dh)
+    else:
+        dh += torch.mm(g.float(), wc.float())
+
+
 class _LMHeadCEFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, h, w, bias, labels, smoothing, ignore_index, params):
@@ -85,7 +104,7 @@ class _LMHeadCEFn(torch.autograd.Function):
         chunks = _chunks(V, vc)
         for j, (c0, n, skip) in enumerate(chunks):
             lg = buf[:N * n].view(N, n)
-            torch.mm(h, w[c0:c0 + n].t(), out=lg)
+            _logits(h, w[c0:c0 + n], lg)
             C.ce_chunk_fwd(lg, labels, bias32, state, loss_rows, lse, c0, V, float(smoothing), int(ignore_index),
                            j == 0, j + 1 == len(chunks), skip)
         count = (labels != ignore_index).sum().clamp_min(1).to(torch.float32)
@@ -113,9 +132,9 @@ class _LMHeadCEFn(torch.autograd.Function):
         for c0, n, skip in _chunks(V, vc):
             lg = buf[:N * n].view(N, n)
             wc = w[c0:c0 + n]
-            torch.mm(h, wc.t(), out=lg)
+            _logits(h, wc, lg)
             C.ce_chunk_bwd(scale, lg, labels, lse, ctx.bias32, c0, V, smoothing, ignore_index, skip)  # skipped -> 0
-            dh += torch.mm(lg, wc)
+            _dh_accumulate(dh, lg, wc)
             with torch.no_grad():
                 if gw is not None:
                     wgrad_accumulate(gw[c0:c0 + n], lg, h)

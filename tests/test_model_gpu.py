@@ -45,8 +45,11 @@ def _grad_report(m_test, m_ref):
                                          ("bart-base", 4)])
 def test_native_bf16_matches_fp32_reference(name, layers):
     """The bf16 HIP-kernel path vs the fp32 torch reference on the same (bf16-representable) weights and dropout
-    masks: loss within 1 %, and EVERY parameter's gradient (relative_attention_bias included) within 3e-2 relative L2
-    error and cosine > 0.999 — a bug confined to one layer's gradient cannot hide behind a global average."""
+    masks: loss within 1 %, and EVERY parameter's gradient (relative_attention_bias included) checked on its own — a
+    bug confined to one layer's gradient cannot hide behind a global average.  The per-parameter bound is what bf16
+    itself costs on that parameter: the plain-torch composite run in bf16 (same ops, torch kernels) sets the noise
+    floor, and the native path must stay within 1.5x of its relative error (floor 3e-2) and of its cosine deficit
+    (floor 1e-3)."""
     cfg = _cfg(name).replace(num_layers=layers, num_decoder_layers=layers)
     torch.manual_seed(0)
     m32 = build_model(cfg).cuda()
@@ -57,28 +60,39 @@ def test_native_bf16_matches_fp32_reference(name, layers):
     m16 = build_model(cfg).cuda()
     m16.load_state_dict(m32.state_dict())
     m16 = m16.to(torch.bfloat16).train()
+    t16 = build_model(cfg).cuda()
+    t16.load_state_dict(m32.state_dict())
+    t16 = t16.to(torch.bfloat16).train()
     b = _batch(cfg)
     from distributed_llms_example_amd.ops.rng import manual_seed
-    manual_seed(5)
     os.environ["DLLM_REFERENCE_OPS"] = "1"
     try:
+        manual_seed(5)
         ref = m32(**b)
         ref.loss.backward()
+        manual_seed(5)
+        tb = t16(**b)
+        tb.loss.backward()
     finally:
         os.environ.pop("DLLM_REFERENCE_OPS")
-    manual_seed(5)  # same dropout masks on both paths
+    manual_seed(5)  # same dropout masks on every path
     out = m16(**b)
     out.loss.backward()
     assert abs(out.loss.item() - ref.loss.item()) < 0.01 * ref.loss.item(), (out.loss.item(), ref.loss.item())
     rep = _grad_report(m16, m32)
+    floor = {n: (rel, cos) for rel, cos, n in _grad_report(t16, m32)}
     names = {n for _, _, n in rep}
     if cfg.model_type == "t5":
         assert any("relative_attention_bias" in n for n in names)
-    worst_rel = max(rep)
-    worst_cos = min(rep, key=lambda r: r[1])
-    print(f"[parity {name} {layers}+{layers}] worst rel {worst_rel}, worst cos {worst_cos}")
-    assert worst_rel[0] < 3e-2, sorted(rep, reverse=True)[:5]
-    assert worst_cos[1] > 0.999, sorted(rep, key=lambda r: r[1])[:5]
+    bad = []
+    for rel, cos, n in rep:
+        frel, fcos = floor[n]
+        if rel > max(3e-2, 1.5 * frel) or 1 - cos > max(1e-3, 1.5 * (1 - fcos)):
+            bad.append((n, rel, frel, cos, fcos))
+    worst = max(rep)
+    print(f"[parity {name} {layers}+{layers}] worst rel {worst} (torch-bf16 floor {floor[worst[2]]}); "
+          f"worst torch-bf16 rel {max(v[0] for v in floor.values()):.4f}")
+    assert not bad, bad[:5]
 
 
 @pytest.mark.parametrize("name", ["t5-base", "bart-base"])
@@ -146,7 +160,9 @@ def test_engine_steps_reduce_loss_on_gpu():
 @pytest.mark.parametrize("name", ["t5-base", "bart-base", "flan-t5-base"])
 def test_fused_ffn_matches_unfused_in_engine(name, monkeypatch):
     """TrainEngine (FlatParams: the FFN runs as GEMMs with activation/dropout epilogues, ops/ffn.py) vs the same
-    step with DLLM_FUSED_FFN=0 (hipBLASLt + activation kernels): same loss, same flat gradient."""
+    step with DLLM_FUSED_FFN=0 (library GEMMs + activation kernels): same loss, same dropout masks, and the fused
+    gradient no further from the fp32 torch reference step (same bf16-representable weights) than the unfused one —
+    two bf16 paths differ by bf16 noise, so their mutual cosine alone is not a sharp test."""
     from distributed_llms_example_amd.ops import ffn as ffn_mod
     from distributed_llms_example_amd.ops.rng import manual_seed
     from distributed_llms_example_amd.parallel.env import init_distributed
@@ -156,8 +172,17 @@ def test_fused_ffn_matches_unfused_in_engine(name, monkeypatch):
     monkeypatch.setattr(ffn_mod, "_GATED_MIN_MF", 0)  # small shapes: force the fused gated path as well
     monkeypatch.setattr(ffn_mod, "_GATED_MAX_D", 1 << 30)
     torch.manual_seed(0)
-    sd = build_model(cfg).state_dict()
+    sd = {k: v.to(torch.bfloat16).float() for k, v in build_model(cfg).state_dict().items()}
     b = _batch(cfg, B=4, S=256, T=64)  # 1024 / 256 tokens: the fused kernel's shapes
+    m = build_model(cfg)
+    m.load_state_dict(sd)
+    monkeypatch.setenv("DLLM_REFERENCE_OPS", "1")
+    eng = TrainEngine(m, env, lr=1e-4, dtype=torch.float32)
+    eng.train()
+    manual_seed(5)
+    l_ref = float(eng.forward_backward(b))
+    g_ref = eng.flat.grad_buf.float().clone()
+    monkeypatch.delenv("DLLM_REFERENCE_OPS")
     res = []
     for flag in ("0", "1"):
         monkeypatch.setenv("DLLM_FUSED_FFN", flag)
@@ -173,9 +198,12 @@ def test_fused_ffn_matches_unfused_in_engine(name, monkeypatch):
         res.append((float(loss), eng.flat.grad_buf.float().clone(), used))
     (l0, g0, n0), (l1, g1, n1) = res
     assert n0 == 0 and n1 == cfg.num_layers + cfg.num_decoder_layers, (n0, n1)
-    assert abs(l0 - l1) < 1e-2 * abs(l0), (l0, l1)
+    assert abs(l0 - l1) < 1e-2 * abs(l0) and abs(l1 - l_ref) < 1e-2 * abs(l_ref), (l0, l1, l_ref)
+    e0, e1 = ((g0 - g_ref).norm() / g_ref.norm()).item(), ((g1 - g_ref).norm() / g_ref.norm()).item()
+    print(f"[fused-ffn {name}] rel err vs fp32 reference: unfused {e0:.4f}, fused {e1:.4f}")
+    assert e1 < max(1.5 * e0, 1e-2), (e0, e1)
     cos = torch.nn.functional.cosine_similarity(g0, g1, dim=0).item()
-    assert cos > 0.999, cos
+    assert cos > 0.995, cos
 
 
 def test_bart_residual_grad_in_dgrad_gemm(monkeypatch):
@@ -231,6 +259,7 @@ def test_trainer_coalesced_grad_accumulation_on_gpu(tmp_path):
         t = Trainer(m, args, train_dataset=ds, data_collator=DataCollatorForSeq2Seq(0, 0), env=env)
         t.train()
         out[mode] = (torch.cat([p.detach().float().flatten() for p in m.parameters()]), t.state.coalesce_cap)
-    assert out["auto"][1] == 8, out["auto"][1]  # 4 micro-batches of 2 per pass
+    # budget in padded tokens (Trainer._padded_tokens): 4 micro-batches x 2 samples x (256 + 64) per pass
+    assert out["auto"][1] == 4 * 2 * (256 + 64), out["auto"][1]
     a, b = out["auto"][0], out["0"][0]
     assert torch.nn.functional.cosine_similarity(a, b, dim=0).item() > 0.99999
