@@ -47,6 +47,8 @@ int dllm_ce_chunk_bwd(const float*, void*, long, const int64_t*, const float*, c
 int dllm_embed_bwd(const int64_t*, const int64_t*, const void*, long, long, int, float*, void*, long, long, int,
                    hipStream_t);
 int dllm_colsum_acc(const void*, long, long, int, float*, void*, int, hipStream_t);
+int dllm_beam_topk(const void*, long, int, const float*, const int64_t*, long, int, int, int, int, int, int, int, int,
+                   float*, int64_t*, hipStream_t);
 }
 
 namespace {
@@ -650,6 +652,33 @@ Tensor gemm_fused(const Tensor& a, const Tensor& b, bool b_kmajor, int64_t epi, 
 
 // ---- one-wave-per-SIMD projection GEMM (csrc/gemm_w4.hip): out (+)= a . b (+ bias), b = [N][K] (nn.Linear weight)
 // or [K][N] (b_kmajor, the input-gradient GEMM).  Ragged M / N; K % 64 == 0; N % 8 == 0.
+// One beam-search step (csrc/beam.hip): logits [B * nb, V] (bf16 / fp32, unit inner stride), beam scores [B * nb]
+// fp32, generated prefix seqs [B * nb, L] int64 -> (top scores [B, k_out] fp32, flat indices [B, k_out] int64).
+std::vector<Tensor> beam_topk(const Tensor& logits, const Tensor& beam_scores, const Tensor& seqs, int64_t cur,
+                              int64_t ngram, int64_t ban_tok, int64_t force_tok, int64_t nb, int64_t k_out) {
+  TORCH_CHECK(logits.is_cuda() && logits.dim() == 2 && logits.stride(1) == 1 &&
+                  (logits.scalar_type() == at::kBFloat16 || logits.scalar_type() == at::kFloat),
+              "beam_topk: logits must be a 2-D bf16 / fp32 GPU tensor with unit inner stride");
+  TORCH_CHECK(beam_scores.is_cuda() && beam_scores.scalar_type() == at::kFloat && beam_scores.is_contiguous() &&
+                  beam_scores.numel() == logits.size(0),
+              "beam_topk: beam_scores must be a contiguous fp32 [rows] GPU tensor");
+  TORCH_CHECK(seqs.is_cuda() && seqs.scalar_type() == at::kLong && seqs.dim() == 2 && seqs.stride(1) == 1 &&
+                  seqs.size(0) == logits.size(0) && cur <= seqs.size(1),
+              "beam_topk: seqs must be an int64 [rows, L >= cur] GPU tensor with unit inner stride");
+  TORCH_CHECK(nb > 0 && logits.size(0) % nb == 0, "beam_topk: rows must be a multiple of nb");
+  const int64_t B = logits.size(0) / nb, V = logits.size(1);
+  TORCH_CHECK(force_tok < V && ban_tok < V, "beam_topk: token id out of range");
+  auto top_s = at::empty({B, k_out}, beam_scores.options());
+  auto top_i = at::empty({B, k_out}, seqs.options());
+  if (B > 0)
+    check_rc(dllm_beam_topk(logits.data_ptr(), logits.stride(0), logits.scalar_type() == at::kBFloat16,
+                            beam_scores.data_ptr<float>(), seqs.data_ptr<int64_t>(), seqs.stride(0), (int)cur,
+                            (int)ngram, (int)ban_tok, (int)force_tok, (int)B, (int)nb, (int)V, (int)k_out,
+                            top_s.data_ptr<float>(), top_i.data_ptr<int64_t>(), stream()),
+             "beam_topk");
+  return {top_s, top_i};
+}
+
 bool gemm_w4_supported(const Tensor& a, const Tensor& b, bool b_kmajor) {
   auto ok2 = [](const Tensor& t) {
     return t.is_cuda() && t.dim() == 2 && t.scalar_type() == at::kBFloat16 && t.stride(1) == 1 && t.stride(0) % 8 == 0 &&
@@ -877,6 +906,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("b"), py::arg("b_kmajor"), py::arg("bias") = py::none(), py::arg("out") = py::none(),
         py::arg("accumulate") = false, py::arg("grp") = -1, py::arg("persist") = true);
   m.def("gemm_w4_supported", &gemm_w4_supported);
+  m.def("beam_topk", &beam_topk);
   m.def("colsum_acc", &colsum_acc, "out += x.sum(0) for a token-major bf16 x (bias gradients)");
   dllm::bind_reducer(m);
   m.attr("arch") = "gfx950";

@@ -70,15 +70,46 @@ def _ban_ngrams(logp, seqs, cur_len: int, n: int):
 
 def _apply_processors_device(logp, seqs, cur_len, min_length, no_repeat_ngram_size, forced_bos, forced_eos,
                              max_length, eos):
+    """transformers' processor order: NoRepeatNGram and MinLength, then ForcedBOS / ForcedEOS (a forced token wins
+    over a ban)."""
     if min_length is not None and cur_len < min_length and eos is not None:
         logp[:, eos] = -float("inf")
+    logp = _ban_ngrams(logp, seqs, cur_len, no_repeat_ngram_size or 0)
     if forced_bos is not None and cur_len == 1:
         logp.fill_(-float("inf"))
         logp[:, forced_bos] = 0.0
     if forced_eos is not None and cur_len == max_length - 1:
         logp.fill_(-float("inf"))
         logp[:, forced_eos] = 0.0
-    return _ban_ngrams(logp, seqs, cur_len, no_repeat_ngram_size or 0)
+    return logp
+
+
+def _fused_beam_ok(logits, nb: int) -> bool:
+    from .. import _ext
+    return (os.environ.get("DLLM_GEN_FUSED_BEAM", "1") != "0" and nb <= 8 and 2 * nb <= 16 and logits.dim() == 2
+            and logits.dtype in (torch.bfloat16, torch.float32) and _ext.use_native(logits))
+
+
+def _beam_candidates(logits, beam_scores, seqs, cur, B, nb, proc):
+    """Top-2·nb candidates over nb·V per batch entry: (scores [B, 2nb], flat indices beam·V + token).  On the GPU one
+    csrc/beam.hip launch (log_softmax normaliser + processors + beam score + top-k in one pass over the logits);
+    otherwise the torch composite of the same ops."""
+    min_length, ngram, forced_bos, forced_eos, max_length, eos = proc
+    if _fused_beam_ok(logits, nb):
+        from .. import _ext
+        ban = eos if (min_length is not None and cur < min_length and eos is not None) else -1
+        force = -1
+        if forced_bos is not None and cur == 1:
+            force = forced_bos
+        if forced_eos is not None and cur == max_length - 1:
+            force = forced_eos
+        top_s, top_i = _ext.native().beam_topk(logits.contiguous(), beam_scores.reshape(-1).float().contiguous(), seqs,
+                                               cur, ngram or 0, ban, force, nb, 2 * nb)
+        return top_s, top_i
+    logp = _apply_processors_device(torch.log_softmax(logits.float(), dim=-1), seqs, cur, min_length, ngram,
+                                    forced_bos, forced_eos, max_length, eos)
+    V = logp.shape[-1]
+    return (beam_scores.view(-1, 1) + logp).view(B, nb * V).topk(2 * nb, dim=1)
 
 
 def _apply_processors(logp, seqs, cur_len, cfg, min_length, no_repeat_ngram_size, forced_bos, forced_eos,
@@ -86,14 +117,8 @@ def _apply_processors(logp, seqs, cur_len, cfg, min_length, no_repeat_ngram_size
     V = logp.shape[-1]
     if min_length is not None and cur_len < min_length and eos is not None:
         logp[:, eos] = -float("inf")
-    if forced_bos is not None and cur_len == 1:
-        logp[:] = -float("inf")
-        logp[:, forced_bos] = 0.0
-    if forced_eos is not None and cur_len == max_length - 1:
-        logp[:] = -float("inf")
-        logp[:, forced_eos] = 0.0
     n = no_repeat_ngram_size or 0
-    if n > 0 and cur_len + 1 >= n:
+    if n > 0 and cur_len + 1 >= n:  # bans before the forced tokens (transformers' order: a forced token wins)
         rows = seqs.tolist()
         for b, row in enumerate(rows):
             prefix = tuple(row[cur_len - n + 1:cur_len]) if n > 1 else ()
@@ -103,10 +128,16 @@ def _apply_processors(logp, seqs, cur_len, cfg, min_length, no_repeat_ngram_size
                     banned.add(row[i + n - 1])
             if banned:
                 logp[b, [t for t in banned if t < V]] = -float("inf")
+    if forced_bos is not None and cur_len == 1:
+        logp[:] = -float("inf")
+        logp[:, forced_bos] = 0.0
+    if forced_eos is not None and cur_len == max_length - 1:
+        logp[:] = -float("inf")
+        logp[:, forced_eos] = 0.0
     return logp
 
 
-def _beam_search_device(model, seqs, enc, attention_mask, caches, cross, B, nb, max_length, process, eos, pad,
+def _beam_search_device(model, seqs, enc, attention_mask, caches, cross, B, nb, max_length, proc, eos, pad,
                         length_penalty, early_stopping, check_every):
     """Beam search with all bookkeeping on the device (transformers BeamSearchScorer semantics): top-2·nb candidates
     over nb·V, eos candidates ranked < nb scored ``sum_logprobs / len**length_penalty`` into a per-batch top-nb of
@@ -137,9 +168,9 @@ def _beam_search_device(model, seqs, enc, attention_mask, caches, cross, B, nb, 
     cur = 1
     while cur < max_length:
         h = model.decode(seqs[:, cur - 1:cur], enc, attention_mask, caches=caches, q_offset=cur - 1, cross_kv=cross)
-        logp = process(torch.log_softmax(model.lm_logits(h[:, -1]).float(), dim=-1), seqs, cur)
-        V = logp.shape[-1]
-        top_s, top_i = (beam_scores.view(-1, 1) + logp).view(B, nb * V).topk(2 * nb, dim=1)
+        logits = model.lm_logits(h[:, -1])
+        V = logits.shape[-1]
+        top_s, top_i = _beam_candidates(logits, beam_scores, seqs, cur, B, nb, proc)
         src = base + top_i // V
         tok = top_i % V
         is_eos = tok == eos if eos is not None else torch.zeros_like(tok, dtype=torch.bool)
@@ -249,7 +280,8 @@ def generate(model, input_ids, attention_mask=None, max_length: int | None = Non
             end = next((i + 2 for i, f in enumerate(flags) if f), cur)
             return seqs[:, :end]
         if os.environ.get("DLLM_GEN_HOST", "0") != "1":
-            return _beam_search_device(model, seqs, enc, attention_mask, caches, cross, B, nb, max_length, process,
+            proc = (min_length, no_repeat_ngram_size, forced_bos, forced_eos, max_length, eos)
+            return _beam_search_device(model, seqs, enc, attention_mask, caches, cross, B, nb, max_length, proc,
                                        eos, pad, length_penalty, early_stopping, check_every)
         # ---------------------------------------------------------------- beam search, host bookkeeping
         # (DLLM_GEN_HOST=1: the original per-step host loop, kept as the A/B oracle of the device version)
