@@ -1,7 +1,9 @@
 """Eval-generation throughput: ``generate(num_beams=2, max_length=128)`` over 818 SAMSum-test-shaped samples
-(ref/train-accelerator.py:239-249), device-side beam bookkeeping vs the per-step host loop (DLLM_GEN_HOST=1).
+(ref/train-accelerator.py:239-249).  Modes: ``fused`` = device-side beam bookkeeping with the one-kernel beam step
+(csrc/beam.hip), ``device`` = the same with the torch composite step (DLLM_GEN_FUSED_BEAM=0), ``host`` = the per-step
+host loop (DLLM_GEN_HOST=1).
 
-    python tools/eval_bench.py [--model t5-base] [--batch 64] [--src-len 512] [--n 818]
+    python tools/eval_bench.py [--model t5-base] [--batch 64] [--src-len 512] [--n 818] [--modes fused,device,host]
 Synthetic prompts (random ids, ragged attention masks) and random-init weights; prints one JSON line per mode.
 """
 import argparse
@@ -24,6 +26,7 @@ def main():
     ap.add_argument("--n", type=int, default=818)
     ap.add_argument("--beams", type=int, default=2)
     ap.add_argument("--max-length", type=int, default=128)
+    ap.add_argument("--modes", default="fused,device,host")
     a = ap.parse_args()
     torch.manual_seed(0)
     cfg = resolve_config(a.model)
@@ -32,8 +35,9 @@ def main():
     ids = torch.randint(3, cfg.vocab_size, (a.n, a.src_len), generator=g)
     lens = torch.randint(a.src_len // 4, a.src_len + 1, (a.n,), generator=g)
     am = (torch.arange(a.src_len)[None, :] < lens[:, None]).long()
-    for mode in ("device", "host"):
+    for mode in a.modes.split(","):
         os.environ["DLLM_GEN_HOST"] = "1" if mode == "host" else "0"
+        os.environ["DLLM_GEN_FUSED_BEAM"] = "1" if mode == "fused" else "0"
         m.generate(ids[:a.batch].cuda(), attention_mask=am[:a.batch].cuda(), max_length=8, num_beams=a.beams)
         torch.cuda.synchronize()
         t0 = time.perf_counter()

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-3 measurements: small-batch (reference micro-batches) graph vs eager, fp32 training, entry point in fp32,
-# and a kernel profile of the default bench.
+
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/r3b
@@ -23,10 +23,3 @@ timeout -k 10 600 python -u train-torchrun.py --model-ckpt t5-base --synthetic 2
   --max-target-length 128 --output-dir /tmp/ebench --batch-size 8 --grad-accum 2 --max-steps 6 --precision fp32 \
   --evaluation-steps 1000000 --max-eval-samples 4 > $O/torchrun_fp32.log 2>&1 || { tail -20 $O/torchrun_fp32.log; exit 1; }
 grep -h "train_runtime\|\"loss\"" $O/torchrun_fp32.log | tail -3
-echo "[r3b] profile b256"
-d=$O/prof
-mkdir -p $d
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $d -o run -- python bench.py --steps 3 --warmup 2 > $O/prof.log 2>&1 || { tail -5 $O/prof.log; exit 1; }
-db=$(find $d -name "*.db" | head -n 1); csv=$(find $d -name "*kernel_stats.csv" | head -n 1)
-python tools/prof_summary.py "${db:-$csv}" 5 > $O/prof_summary.txt && head -40 $O/prof_summary.txt
-[ -n "$db" ] && rm -f "$db"
