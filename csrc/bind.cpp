@@ -18,7 +18,8 @@ int dllm_norm_fwd(const void*, const void*, const void*, const void*, void*, voi
                   float, uint32_t, int, int, hipStream_t);
 int dllm_norm_bwd_grid(int);
 int dllm_norm_bwd(const void*, const void*, const void*, const void*, const float*, const float*, void*, void*,
-                  float*, float*, float*, float*, void*, void*, int, int, float, uint32_t, int, int, int, hipStream_t);
+                  float*, float*, float*, float*, void*, void*, float*, float*, int, int, float, uint32_t, int, int, int,
+                  hipStream_t);
 int dllm_act_fwd(const void*, void*, long, int, int, int, float, uint32_t, int, hipStream_t);
 int dllm_act_bwd(const void*, const void*, void*, long, int, int, int, float, uint32_t, int, hipStream_t);
 int dllm_dropout(const void*, void*, long, float, uint32_t, int, hipStream_t);
@@ -111,7 +112,7 @@ std::vector<Tensor> norm_fwd(const Tensor& x, const optional<Tensor>& resid, con
 std::vector<Tensor> norm_bwd(const optional<Tensor>& dout_o, const optional<Tensor>& ds, const Tensor& s,
                              const Tensor& w, const optional<Tensor>& b, const optional<Tensor>& mean,
                              const Tensor& rstd, double p, int64_t seed, int64_t kind, bool want_stream,
-                             const optional<Tensor>& dw_acc, const optional<Tensor>& db_acc) {
+                             const optional<Tensor>& dw_acc, const optional<Tensor>& db_acc, bool want_colsum) {
   check_gpu(s, "s");
   TORCH_CHECK(s.dim() == 2 && s.is_contiguous(), "s must be contiguous [N, d]");
   const int N = s.size(0), d = s.size(1);
@@ -144,16 +145,21 @@ std::vector<Tensor> norm_bwd(const optional<Tensor>& dout_o, const optional<Tens
   Tensor dw = acc ? Tensor() : at::zeros({d}, f32);
   Tensor db_part = has_b ? at::empty({G, d}, f32) : Tensor();
   Tensor db = (has_b && !acc) ? at::zeros({d}, f32) : Tensor();
+  // column sums of dx (the upstream linear layer's bias gradient), fp32 [d]
+  Tensor dxs_part = want_colsum ? at::empty({G, d}, f32) : Tensor();
+  Tensor dxs = want_colsum ? at::zeros({d}, f32) : Tensor();
   if (N > 0)
     check_rc(dllm_norm_bwd(dout.data_ptr(), dse.defined() ? dse.data_ptr() : nullptr, s.data_ptr(), w.data_ptr(),
                            kind == 1 ? mean->data_ptr<float>() : nullptr, rstd.data_ptr<float>(), dx.data_ptr(),
                            want_stream ? dstream.data_ptr() : nullptr, dw_part.data_ptr<float>(),
                            has_b ? db_part.data_ptr<float>() : nullptr, acc ? nullptr : dw.data_ptr<float>(),
                            (has_b && !acc) ? db.data_ptr<float>() : nullptr, acc ? dw_acc->data_ptr() : nullptr,
-                           (acc && has_b) ? db_acc->data_ptr() : nullptr, N, d, (float)p, (uint32_t)seed, (int)kind,
+                           (acc && has_b) ? db_acc->data_ptr() : nullptr,
+                           want_colsum ? dxs_part.data_ptr<float>() : nullptr,
+                           want_colsum ? dxs.data_ptr<float>() : nullptr, N, d, (float)p, (uint32_t)seed, (int)kind,
                            is_bf16(s), acc && dw_acc->scalar_type() == at::kFloat, stream()),
              "norm_bwd");
-  return {dx, dstream, dw, db};
+  return {dx, dstream, dw, db, dxs};
 }
 
 // ------------------------------------------------------------------------------------------- activations
@@ -867,7 +873,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("norm_fwd", &norm_fwd);
   m.def("norm_bwd", &norm_bwd, py::arg("dout"), py::arg("ds"), py::arg("s"), py::arg("w"), py::arg("b"),
         py::arg("mean"), py::arg("rstd"), py::arg("p"), py::arg("seed"), py::arg("kind"), py::arg("want_stream"),
-        py::arg("dw_acc") = py::none(), py::arg("db_acc") = py::none());
+        py::arg("dw_acc") = py::none(), py::arg("db_acc") = py::none(), py::arg("want_colsum") = false);
   m.def("act_fwd", &act_fwd);
   m.def("act_bwd", &act_bwd);
   m.def("dropout_fwd", &dropout_fwd);

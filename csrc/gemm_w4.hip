@@ -130,8 +130,10 @@ DLLM_DEVICE void mfma0(f32x4& c, const bf16x8v& b, const bf16x8v& a) {
   asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(c) : "v"(b), "v"(a));
 }
 
-// RS = fragment read schedule: 0 spreads the 16 next-sub-step reads over the 8 chunks (2 per chunk), 1 issues them
-// 4 per chunk in the first 4 chunks after they become legal (more MFMA cover for their latency)
+// RS bit 0 = fragment read schedule: 0 spreads the 16 next-sub-step reads over the 8 chunks (2 per chunk), 1 issues
+// them 4 per chunk in the first 4 chunks after they become legal (more MFMA cover for their latency).
+// RS bits 4..7 = ABLATIONS for timing studies only (results are garbage): 16 no k-loop DMAs, 32 no k-loop fragment
+// reads, 64 no k-loop wait + barrier, 128 no epilogue stores (tools/gemm_w4_bench.py --ablate)
 template <bool BKM, bool BIAS, bool ACC, int RS>
 __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -292,7 +294,8 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
       for (int i = 0; i < 8; ++i) {
         if (kt == 0) chunk0(fa0, fb0, i);
         else chunk(fa0, fb0, i);
-        if constexpr (RS == 0) {
+        if constexpr ((RS & 32) != 0) {
+        } else if constexpr ((RS & 1) == 0) {
           if (i < 4) {
             fb1[2 * i] = rd_b(b, 1, 2 * i);
             fb1[2 * i + 1] = rd_b(b, 1, 2 * i + 1);
@@ -316,18 +319,21 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
       // DMA k-tile g+2 into buffer b and read k-tile g+1's first half into fa0 / fb0, spread over the remaining 7 chunks
       chunk(fa1, fb1, 0);
       __builtin_amdgcn_sched_barrier(0);
-      if (kt == 0 && g > 0 && !ACC) asm volatile("s_waitcnt vmcnt(32) lgkmcnt(0)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
+      if constexpr ((RS & 64) == 0) {
+        if (kt == 0 && g > 0 && !ACC) asm volatile("s_waitcnt vmcnt(32) lgkmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+      }
       __builtin_amdgcn_sched_barrier(0);
       const Dma q = plan_next(ti, kt, b);
       sfor<1, 8>([&](auto I) {
         constexpr int i = decltype(I)::value;
         chunk(fa1, fb1, i);
         // DMA: instructions 0..7 of A then of B, spread over chunks 1..7 (2, 2, 2, 3, 2, 2, 3)
-        sfor<(i - 1) * 16 / 7, i * 16 / 7>([&](auto D) { dma(q, D); });
+        if constexpr ((RS & 16) == 0) sfor<(i - 1) * 16 / 7, i * 16 / 7>([&](auto D) { dma(q, D); });
         // fragments of k-tile g+1 (buffer b ^ 1), first half: B in chunks 1..4, A in chunks 5..7
-        if constexpr (RS == 0) {
+        if constexpr ((RS & 32) != 0) {
+        } else if constexpr ((RS & 1) == 0) {
           if (i <= 4) {
             fb0[2 * i - 2] = rd_b(b ^ 1, 0, 2 * i - 2);
             fb0[2 * i - 1] = rd_b(b ^ 1, 0, 2 * i - 1);
@@ -412,7 +418,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
             };
             o = u32x4{add2(o.x, c.x), add2(o.y, c.y), add2(o.z, c.z), add2(o.w, c.w)};
           }
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, o), srdC, off, 0, 0);
+          if constexpr ((RS & 128) == 0) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, o), srdC, off, 0, 0);
           // bound the live ranges
           if (j & 1) __builtin_amdgcn_sched_barrier(0);
         }
@@ -461,11 +467,23 @@ int launch_rs(const GemmW4Params& p, bool persist, hipStream_t st) {
   return 0;
 }
 
-// DLLM_W4_RS: fragment read schedule (kernel template RS), read per call so microbenchmarks can A/B it in one process
+// DLLM_W4_RS: fragment read schedule (kernel template RS), read per call so microbenchmarks can A/B it in one process;
+// the ablation values (bits 4..7) exist for the plain forward only
 template <bool BKM, bool BIAS, bool ACC>
 int launch(const GemmW4Params& p, bool persist, hipStream_t st) {
   const char* e = getenv("DLLM_W4_RS");
-  if (e && e[0] == '1') return launch_rs<BKM, BIAS, ACC, 1>(p, persist, st);
+  const int rs = e ? atoi(e) : 0;
+  if constexpr (!BKM && !BIAS && !ACC) {
+    switch (rs) {
+      case 16: return launch_rs<BKM, BIAS, ACC, 16>(p, persist, st);
+      case 32: return launch_rs<BKM, BIAS, ACC, 32>(p, persist, st);
+      case 64: return launch_rs<BKM, BIAS, ACC, 64>(p, persist, st);
+      case 128: return launch_rs<BKM, BIAS, ACC, 128>(p, persist, st);
+      case 112: return launch_rs<BKM, BIAS, ACC, 112>(p, persist, st);
+      default: break;
+    }
+  }
+  if (rs & 1) return launch_rs<BKM, BIAS, ACC, 1>(p, persist, st);
   return launch_rs<BKM, BIAS, ACC, 0>(p, persist, st);
 }
 

@@ -92,14 +92,16 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(const T* __restrict__ dou
                                                        const float* __restrict__ mean_in,
                                                        const float* __restrict__ rstd_in, T* __restrict__ dx,
                                                        T* __restrict__ dstream, float* __restrict__ dw_part,
-                                                       float* __restrict__ db_part, int N, int d, float p,
-                                                       uint32_t seed, uint32_t thr) {
+                                                       float* __restrict__ db_part, float* __restrict__ dxs_part,
+                                                       int N, int d, float p, uint32_t seed, uint32_t thr) {
   if (p > 0.f) seed = eff_seed(seed);
   extern __shared__ __attribute__((aligned(16))) float red[];  // [4][d]
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const bool drop = p > 0.f;
   const float dscale = drop ? 1.f / (1.f - p) : 1.f;
-  f32x4 adw[MAXV], adb[MAXV], wgt[MAXV];
+  // adx: column sums of the stored dx (dxs_part != nullptr) — the bias gradient of the linear layer whose output fed
+  // this norm's x (BART post-LN: out_proj / fc2), so that layer's backward needs no separate column-sum pass over dx
+  f32x4 adw[MAXV], adb[MAXV], adx[MAXV], wgt[MAXV];
   int cof[MAXV];
   float cm[MAXV];  // 1 for a column chunk inside the row, else 0
 #pragma unroll
@@ -108,7 +110,7 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(const T* __restrict__ dou
     cm[c] = col < d ? 1.f : 0.f;
     cof[c] = col < d ? col : 0;
     wgt[c] = Elem<T>::load4(w + cof[c]) * cm[c];
-    adw[c] = adb[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    adw[c] = adb[c] = adx[c] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
   constexpr int R = MAXV <= 4 ? 2 : 1;  // rows per iteration (registers: d = 2048 stays at one row)
   const int stride = gridDim.x * 4;
@@ -166,20 +168,22 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(const T* __restrict__ dou
           if (dstream != nullptr) Elem<T>::store4(dstream + base + col, dsv);
           if (drop) dropout4(dsv, seed, thr, (uint32_t)(base + col), dscale);
           Elem<T>::store4(dx + base + col, dsv);
+          if (dxs_part != nullptr) adx[c] += dsv;
         }
       }
     }
   }
-  // block-reduce the column partials of the 4 waves, one pass for dw, one for db
-  for (int pass = 0; pass < (db_part != nullptr ? 2 : 1); ++pass) {
+  // block-reduce the column partials of the 4 waves, one pass each for dw, db (if any), dx column sums (if asked)
+  for (int pass = 0; pass < 3; ++pass) {
+    if ((pass == 1 && db_part == nullptr) || (pass == 2 && dxs_part == nullptr)) continue;
     __syncthreads();
 #pragma unroll
     for (int c = 0; c < MAXV; ++c) {
       const int col = (c * 64 + lane) * 4;
-      if (col < d) *reinterpret_cast<f32x4*>(red + wv * d + col) = pass == 0 ? adw[c] : adb[c];
+      if (col < d) *reinterpret_cast<f32x4*>(red + wv * d + col) = pass == 0 ? adw[c] : (pass == 1 ? adb[c] : adx[c]);
     }
     __syncthreads();
-    float* dst = (pass == 0 ? dw_part : db_part) + (size_t)blockIdx.x * d;
+    float* dst = (pass == 0 ? dw_part : (pass == 1 ? db_part : dxs_part)) + (size_t)blockIdx.x * d;
     for (int col = threadIdx.x; col < d; col += 256) dst[col] = red[col] + red[d + col] + red[2 * d + col] + red[3 * d + col];
   }
 }
@@ -254,7 +258,8 @@ int launch_fwd(const void* x, const void* resid, const void* w, const void* b, v
 template <typename T, int KIND>
 int launch_bwd(const void* dout, const void* ds_extra, const void* s, const void* w, const float* mean,
                const float* rstd, void* dx, void* dstream, float* dw_part, float* db_part, float* dw, float* db,
-               void* dw_acc, void* db_acc, int N, int d, float p, uint32_t seed, int G, int acc_f32, hipStream_t st) {
+               void* dw_acc, void* db_acc, float* dxs_part, float* dxs, int N, int d, float p, uint32_t seed, int G,
+               int acc_f32, hipStream_t st) {
   const int chunks = (d + 255) / 256;
   dim3 grid(G), block(256);
   const size_t lds = (size_t)4 * d * sizeof(float);
@@ -264,11 +269,11 @@ int launch_bwd(const void* dout, const void* ds_extra, const void* s, const void
     if (ds_extra != nullptr)                                                                                      \
       hipLaunchKernelGGL((norm_bwd_kernel<T, KIND, MV, true>), grid, block, lds, st, (const T*)dout,              \
                          (const T*)ds_extra, (const T*)s, (const T*)w, mean, rstd, (T*)dx, (T*)dstream, dw_part,  \
-                         db_part, N, d, p, seed, thr);                                                            \
+                         db_part, dxs_part, N, d, p, seed, thr);                                                  \
     else                                                                                                          \
       hipLaunchKernelGGL((norm_bwd_kernel<T, KIND, MV, false>), grid, block, lds, st, (const T*)dout,             \
                          (const T*)ds_extra, (const T*)s, (const T*)w, mean, rstd, (T*)dx, (T*)dstream, dw_part,  \
-                         db_part, N, d, p, seed, thr);                                                            \
+                         db_part, dxs_part, N, d, p, seed, thr);                                                  \
   } while (0)
   if (chunks <= 1) L(1);
   else if (chunks <= 2) L(2);
@@ -278,6 +283,8 @@ int launch_bwd(const void* dout, const void* ds_extra, const void* s, const void
   else return -1;
 #undef L
   DLLM_CHECK_LAUNCH();
+  if (dxs_part != nullptr)  // dx column sums -> dxs (fp32, pre-zeroed)
+    hipLaunchKernelGGL(col_sum_acc_kernel<float>, dim3((d + 63) / 64), dim3(1024), 0, st, dxs_part, dxs, G, d);
   if (dw_acc != nullptr && acc_f32) {  // fp32 flat gradient buffer
     hipLaunchKernelGGL(col_sum_acc_kernel<float>, dim3((d + 63) / 64), dim3(1024), 0, st, dw_part, (float*)dw_acc, G,
                        d);
@@ -319,18 +326,13 @@ extern "C" int dllm_norm_bwd_grid(int N) {
 
 extern "C" int dllm_norm_bwd(const void* dout, const void* ds_extra, const void* s, const void* w, const float* mean,
                              const float* rstd, void* dx, void* dstream, float* dw_part, float* db_part, float* dw,
-                             float* db, void* dw_acc, void* db_acc, int N, int d, float p, uint32_t seed, int kind,
-                             int is_bf16, int acc_f32, hipStream_t st) {
+                             float* db, void* dw_acc, void* db_acc, float* dxs_part, float* dxs, int N, int d, float p,
+                             uint32_t seed, int kind, int is_bf16, int acc_f32, hipStream_t st) {
   if (d % 4 != 0) return -2;
   const int G = dllm_norm_bwd_grid(N);
-  if (is_bf16) {
-    return kind ? launch_bwd<uint16_t, 1>(dout, ds_extra, s, w, mean, rstd, dx, dstream, dw_part, db_part, dw, db, dw_acc, db_acc, N,
-                                          d, p, seed, G, acc_f32, st)
-                : launch_bwd<uint16_t, 0>(dout, ds_extra, s, w, mean, rstd, dx, dstream, dw_part, db_part, dw, db, dw_acc, db_acc, N,
-                                          d, p, seed, G, acc_f32, st);
-  }
-  return kind ? launch_bwd<float, 1>(dout, ds_extra, s, w, mean, rstd, dx, dstream, dw_part, db_part, dw, db, dw_acc, db_acc, N, d, p,
-                                     seed, G, acc_f32, st)
-              : launch_bwd<float, 0>(dout, ds_extra, s, w, mean, rstd, dx, dstream, dw_part, db_part, dw, db, dw_acc, db_acc, N, d, p,
-                                     seed, G, acc_f32, st);
+#define A dout, ds_extra, s, w, mean, rstd, dx, dstream, dw_part, db_part, dw, db, dw_acc, db_acc, dxs_part, dxs, N, d, p, \
+          seed, G, acc_f32, st
+  if (is_bf16) return kind ? launch_bwd<uint16_t, 1>(A) : launch_bwd<uint16_t, 0>(A);
+  return kind ? launch_bwd<float, 1>(A) : launch_bwd<float, 0>(A);
+#undef A
 }

@@ -10,6 +10,8 @@ LayerDrop (encoder/decoder_layerdrop, 0.0 in every public BART config) is not im
 """
 from __future__ import annotations
 
+import os
+
 import math
 
 import torch
@@ -26,6 +28,8 @@ from .blocks import run_block
 from .config import Seq2SeqConfig
 from .output import Seq2SeqLMOutput
 
+
+_NORM_BIAS_COLSUM = os.environ.get("DLLM_NORM_BIAS_COLSUM", "1") != "0"  # 0: separate column-sum pass (A/B)
 
 class BartAttention(nn.Module):
     def __init__(self, cfg: Seq2SeqConfig, cross: bool):
@@ -103,16 +107,17 @@ class BartLayer(nn.Module):
         # residual back from their input projection so its gradient is summed inside that projection's dgrad GEMM
         a, h = self.self_attn(h, mask=None if self.is_decoder else mask, causal=self.is_decoder, p=pa, cache=cache,
                               residual=True)
+        xb = _NORM_BIAS_COLSUM  # out_proj / fc2 bias gradients summed by the norm backward kernel (ops/norms.py)
         h = norms.add_dropout_layer_norm(h, a, self.self_attn_layer_norm.weight, self.self_attn_layer_norm.bias, eps,
-                                         p, rng.next_seed() if p > 0 else 0)
+                                         p, rng.next_seed() if p > 0 else 0, xb)
         if self.is_decoder:
             c, h = self.encoder_attn(h, kv_in=enc_out, mask=enc_mask, p=pa, kv=cross_kv, residual=True)
             h = norms.add_dropout_layer_norm(h, c, self.encoder_attn_layer_norm.weight,
                                              self.encoder_attn_layer_norm.bias, eps, p,
-                                             rng.next_seed() if p > 0 else 0)
+                                             rng.next_seed() if p > 0 else 0, xb)
         f, h = ffn_res(h, self.fc1, self.fc2, cfg.act, pact, rng.next_seed() if pact > 0 else 0)
         return norms.add_dropout_layer_norm(h, f, self.final_layer_norm.weight, self.final_layer_norm.bias, eps, p,
-                                            rng.next_seed() if p > 0 else 0)
+                                            rng.next_seed() if p > 0 else 0, xb)
 
 
 class BartLearnedPositionalEmbedding(nn.Embedding):

@@ -102,7 +102,7 @@ class _FusedFFNFn(torch.autograd.Function):
         with torch.no_grad():
             wgrad_accumulate(_gbuf(Wo), dy2, h)
             if Bo is not None:
-                bias_grad_accumulate(_gbuf(Bo), dy2)
+                bias_grad_accumulate(_gbuf(Bo), dy2, dy)
         _fire(Wo)
         if Bo is not None:
             _fire(Bo)

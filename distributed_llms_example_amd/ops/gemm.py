@@ -31,6 +31,7 @@ _W4_MODE = os.environ.get("DLLM_W4_GEMM", "auto")
 _W4 = _W4_MODE != "0"
 _W4_DGRAD_MAX_K = 1024
 w4_calls = 0  # projections that ran on csrc/gemm_w4.hip (tests assert the kernel really ran)
+colsum_handoffs = 0  # bias gradients taken from a norm backward's column sums (bias_grad_accumulate)
 
 
 def _w4_ok(a: torch.Tensor, b: torch.Tensor, kmajor: bool) -> bool:
@@ -94,8 +95,15 @@ def wgrad_accumulate(out: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, bet
 
 
 @torch.no_grad()
-def bias_grad_accumulate(out: torch.Tensor, dy2: torch.Tensor) -> torch.Tensor:
-    """``out += dy2.sum(0)`` (bias gradient of a linear layer, accumulated in place)."""
+def bias_grad_accumulate(out: torch.Tensor, dy2: torch.Tensor, dy: torch.Tensor | None = None) -> torch.Tensor:
+    """``out += dy2.sum(0)`` (bias gradient of a linear layer, accumulated in place).  ``dy``: the gradient tensor as
+    autograd delivered it; when its producer already summed it over tokens (ops/norms.py x_bias_grad: the BART
+    post-LN backward kernel) that fp32 column sum is added instead of re-reading dy."""
+    global colsum_handoffs
+    cs = getattr(dy, "_dllm_colsum", None) if dy is not None else None
+    if cs is not None and cs.numel() == out.numel():
+        colsum_handoffs += 1
+        return out.add_(cs.view_as(out).to(out.dtype))
     if _ext.use_native(dy2) and dy2.dtype == torch.bfloat16 and dy2.stride(-1) == 1 and dy2.shape[-1] % 2 == 0 \
             and dy2.stride(0) % 2 == 0 and out.is_contiguous():
         _ext.native().colsum_acc(dy2, out)

@@ -79,7 +79,7 @@ class _LinearAccumFn(torch.autograd.Function):
         with torch.no_grad():
             wgrad_accumulate(_gbuf(w), dy2, x2)
             if bias is not None:
-                bias_grad_accumulate(_gbuf(bias), dy2)
+                bias_grad_accumulate(_gbuf(bias), dy2, dy)
         _fire(w)
         if bias is not None:
             _fire(bias)

@@ -44,9 +44,10 @@ class _NormFn(torch.autograd.Function):
     """out = norm(s) with s = (resid +) dropout(x); returns (out, s)."""
 
     @staticmethod
-    def forward(ctx, x, resid, weight, bias, eps, p, seed, kind, params=None):
+    def forward(ctx, x, resid, weight, bias, eps, p, seed, kind, params=None, colsum=False):
         C = _ext.native()
         ctx.params = params
+        ctx.colsum = colsum
         for q in params or ():
             _use(q)
         shape = x.shape
@@ -68,14 +69,16 @@ class _NormFn(torch.autograd.Function):
         dout2 = dout.reshape(-1, d) if dout is not None else None
         ds2 = ds.reshape(-1, d) if ds is not None else None
         want_stream = has_resid and p > 0.0
-        dx, dstream, dw, db = C.norm_bwd(dout2, ds2, s, weight, bias, mean, rstd, float(p), int(seed), int(kind),
-                                         want_stream, *_acc_targets(ctx.params))
+        dx, dstream, dw, db, dxs = C.norm_bwd(dout2, ds2, s, weight, bias, mean, rstd, float(p), int(seed), int(kind),
+                                              want_stream, *_acc_targets(ctx.params), want_colsum=ctx.colsum)
         dx = dx.view(shape)
+        if ctx.colsum:  # handed to the producing linear layer's backward as its bias gradient (ops/gemm.py)
+            dx._dllm_colsum = dxs
         # d(resid) == d(s) (pre-dropout gradient); identical to dx when p == 0
         dres = None
         if has_resid:
             dres = dstream.view(shape) if want_stream else dx
-        return (dx, dres) + _param_grads(ctx.params, weight, bias, dw, db) + (None, None, None, None, None)
+        return (dx, dres) + _param_grads(ctx.params, weight, bias, dw, db) + (None, None, None, None, None, None)
 
 
 class _NormOnlyFn(torch.autograd.Function):
@@ -99,8 +102,8 @@ class _NormOnlyFn(torch.autograd.Function):
         C = _ext.native()
         x2, weight, bias, mean, rstd = ctx.saved_tensors
         kind, shape = ctx.cfg
-        dx, _, dw, db = C.norm_bwd(dout.reshape(-1, shape[-1]), None, x2, weight, bias, mean, rstd, 0.0, 0, int(kind),
-                                   False, *_acc_targets(ctx.params))
+        dx, _, dw, db, _ = C.norm_bwd(dout.reshape(-1, shape[-1]), None, x2, weight, bias, mean, rstd, 0.0, 0,
+                                      int(kind), False, *_acc_targets(ctx.params))
         return (dx.view(shape),) + _param_grads(ctx.params, weight, bias, dw, db) + (None, None, None)
 
 
@@ -121,7 +124,7 @@ def _param_grads(params, weight, bias, dw, db):
     return dw.to(weight.dtype), (db.to(bias.dtype) if db is not None else None)
 
 
-def _norm(x, resid, weight, bias, eps, p, seed, kind):
+def _norm(x, resid, weight, bias, eps, p, seed, kind, colsum=False):
     if _ext.use_native(x):
         params = None
         if torch.is_grad_enabled() and _fusable(weight) and _fusable(bias):
@@ -130,7 +133,7 @@ def _norm(x, resid, weight, bias, eps, p, seed, kind):
             bias = bias.detach() if bias is not None else None
         if resid is None and p == 0.0:
             return _NormOnlyFn.apply(x, weight, bias, eps, kind, params), x
-        return _NormFn.apply(x, resid, weight, bias, eps, p, seed, kind, params)
+        return _NormFn.apply(x, resid, weight, bias, eps, p, seed, kind, params, colsum and x.requires_grad)
     return _reference(x, resid, weight, bias, eps, p, seed, kind)
 
 
@@ -152,9 +155,11 @@ def add_dropout_rms_norm(resid, x, weight, eps, p, seed):
     return _norm(x, resid, weight, None, eps, p, seed, RMS)
 
 
-def add_dropout_layer_norm(resid, x, weight, bias, eps, p, seed):
-    """LN(resid + dropout(x)): BART post-norm residual block."""
-    return _norm(x, resid, weight, bias, eps, p, seed, LAYER)[0]
+def add_dropout_layer_norm(resid, x, weight, bias, eps, p, seed, x_bias_grad=False):
+    """LN(resid + dropout(x)): BART post-norm residual block.  ``x_bias_grad``: x is a biased linear layer's output
+    (out_proj / fc2); the backward kernel then also sums its gradient over tokens and hands that bias gradient to the
+    layer's backward with the gradient tensor (no separate column-sum pass, ops/gemm.py bias_grad_accumulate)."""
+    return _norm(x, resid, weight, bias, eps, p, seed, LAYER, x_bias_grad)[0]
 
 
 def dropout_layer_norm(x, weight, bias, eps, p, seed):

@@ -4,6 +4,11 @@ step at the bench batch (forward NT and input-gradient NN).  Rounds are interlea
 (cdna_hip_programming.md §5.4 rule 24); the median over rounds is reported, on random operands.
 
     python tools/gemm_w4_bench.py [--iters 10] [--rounds 3] [--batch 256] [--grp 4]
+    python tools/gemm_w4_bench.py --ablate --phases fwd --only "enc qkv"   # timing ablations of the w4 main loop
+
+--ablate times the forward kernel with parts of its k-loop removed (csrc/gemm_w4.hip RS bits 4..7; results are
+garbage, only the time counts): no DMAs, no fragment reads, no wait + barrier, no epilogue stores, and none of the
+first three (MFMAs alone).
 """
 import argparse
 import json
@@ -48,6 +53,7 @@ def main():
     ap.add_argument("--grp", type=int, default=4)
     ap.add_argument("--phases", default="fwd,dgrad")
     ap.add_argument("--only", default="")
+    ap.add_argument("--ablate", action="store_true")
     a = ap.parse_args()
     tunableop.enable(0)
     C = _ext.native()
@@ -75,11 +81,17 @@ def main():
             for k, fn in arms.items():
                 if k != "lib":
                     rec[f"{k}_relerr"] = float(f"{((fn().float() - ref).norm() / ref.norm()).item():.2e}")
+            rsv = {"w4rs1": "1"}
             arms["w4rs1"] = arms["w4"]  # same call, DLLM_W4_RS=1 (early fragment reads), set per arm below
+            if a.ablate and phase == "fwd":
+                for tag, v in (("nodma", "16"), ("noread", "32"), ("nobar", "64"), ("nostore", "128"),
+                               ("mfmaonly", "112")):
+                    arms["abl_" + tag] = arms["w4"]
+                    rsv["abl_" + tag] = v
             times = {k: [] for k in arms}
             for _ in range(a.rounds):
                 for k, fn in arms.items():
-                    os.environ["DLLM_W4_RS"] = "1" if k == "w4rs1" else "0"
+                    os.environ["DLLM_W4_RS"] = rsv.get(k, "0")
                     times[k].append(timeit(fn, a.iters))
             os.environ["DLLM_W4_RS"] = "0"
             for k, ts in times.items():

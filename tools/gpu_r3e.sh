@@ -1,0 +1,25 @@
+#!/bin/bash
+# Round-3: w4 main-loop ablations, then the per-model bench lines for the BASELINE.md comparator table.
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out/r3e
+mkdir -p $O
+echo "[r3e] w4 ablations"
+timeout -k 10 300 python -u tools/gemm_w4_bench.py --ablate --phases fwd --rounds 2 --only "enc" > $O/ablate.jsonl 2>&1 || { tail -5 $O/ablate.jsonl; exit 1; }
+grep '^{' $O/ablate.jsonl | python -c "
+import json,sys
+for l in sys.stdin:
+    r=json.loads(l); print(r['shape'], {k[:-3]: v for k, v in r.items() if k.endswith('_us')})"
+run() {  # tag, bench args...
+  local tag=$1; shift
+  echo "[r3e] $tag"
+  timeout -k 10 400 python -u bench.py "$@" > $O/$tag.log 2>&1 || { echo "[r3e] $tag failed rc=$?"; tail -8 $O/$tag.log; return 1; }
+  echo "$tag $(grep -h '"metric"' $O/$tag.log | tail -1 | cut -c100-200)"
+}
+run t5b_b32 --batch-per-gpu 32 --steps 10 --warmup 3 &&
+run t5b_b64 --batch-per-gpu 64 --steps 10 --warmup 3 &&
+run t5b_b128 --batch-per-gpu 128 --steps 10 --warmup 3 &&
+run bartl_b32 --model bart-large --batch-per-gpu 32 --steps 10 --warmup 3 &&
+run bartl_b256 --model bart-large --batch-per-gpu 256 --steps 6 --warmup 2 &&
+run t5l_b32 --model t5-large --batch-per-gpu 32 --steps 6 --warmup 2 &&
+run flanxl_b16 --model flan-t5-xl --batch-per-gpu 16 --steps 5 --warmup 2
