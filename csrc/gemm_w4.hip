@@ -472,7 +472,7 @@ int launch_rs(const GemmW4Params& p, bool persist, hipStream_t st) {
 template <bool BKM, bool BIAS, bool ACC>
 int launch(const GemmW4Params& p, bool persist, hipStream_t st) {
   const char* e = getenv("DLLM_W4_RS");
-  const int rs = e ? atoi(e) : 0;
+  const int rs = e ? atoi(e) : 1;  // default: early fragment reads (1-8 % faster on the routed dgrads)
   if constexpr (!BKM && !BIAS && !ACC) {
     switch (rs) {
       case 16: return launch_rs<BKM, BIAS, ACC, 16>(p, persist, st);
