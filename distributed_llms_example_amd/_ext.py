@@ -16,6 +16,27 @@ import torch
 
 _C = None
 _err: Exception | None = None
+_PKG = os.path.dirname(os.path.abspath(__file__))
+_CSRC = os.path.join(os.path.dirname(_PKG), "csrc")
+
+
+def stale_sources() -> list[str]:
+    """Native sources whose content differs from what the in-tree library was built from (tools/build_native.py
+    provenance record ``_C.build.json``); empty when they match or when there is no record / source tree to check."""
+    import glob
+    import hashlib
+    import json
+    rec_path = os.path.join(_PKG, "_C.build.json")
+    if not (os.path.exists(rec_path) and os.path.isdir(_CSRC)):
+        return []
+    with open(rec_path) as f:
+        built = json.load(f).get("sources", {})
+    cur = {}
+    for p in glob.glob(os.path.join(_CSRC, "*.hip")) + glob.glob(os.path.join(_CSRC, "*.cpp")) + \
+            glob.glob(os.path.join(_CSRC, "*.h")):
+        with open(p, "rb") as f:
+            cur[os.path.basename(p)] = hashlib.sha256(f.read()).hexdigest()
+    return sorted(k for k in set(built) | set(cur) if built.get(k) != cur.get(k))
 
 
 def _load():
@@ -30,6 +51,10 @@ def _load():
             spec.loader.exec_module(_C)
             sys.modules["distributed_llms_example_amd._C"] = _C
         else:
+            stale = stale_sources()
+            if stale:  # a library built from other sources than the tree's: never run it silently
+                raise ImportError(f"the in-tree _C was built from different sources ({', '.join(stale)}); rebuild "
+                                  "with `python tools/build_native.py`")
             _C = importlib.import_module("distributed_llms_example_amd._C")
     except Exception as e:  # pragma: no cover - depends on build state
         _C = None

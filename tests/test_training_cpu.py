@@ -329,3 +329,27 @@ def test_relayout_keeps_stacked_groups_adjacent():
         assert torch.equal(p.detach(), before[n]), n
     for grp in m._dllm_param_groups():
         assert _adjacent([p for p in grp]) is not None
+
+
+def test_native_build_provenance_detects_stale_sources(tmp_path, monkeypatch):
+    """tools/build_native.py records the sha256 of every native source in _C.build.json; the loader compares them with
+    the tree and refuses a library built from other sources (distributed_llms_example_amd/_ext.py stale_sources)."""
+    import json
+    import shutil
+    from distributed_llms_example_amd import _ext
+    pkg, csrc = tmp_path / "pkg", tmp_path / "csrc"
+    pkg.mkdir()
+    shutil.copytree(_ext._CSRC, csrc)
+    sys_path = __import__("sys").path
+    sys_path.insert(0, str(__import__("pathlib").Path(_ext._CSRC).parent / "tools"))
+    try:
+        import build_native
+    finally:
+        sys_path.pop(0)
+    monkeypatch.setattr(build_native, "CSRC", str(csrc))
+    (pkg / "_C.build.json").write_text(json.dumps({"sources": build_native.source_hashes()}))
+    monkeypatch.setattr(_ext, "_PKG", str(pkg))
+    monkeypatch.setattr(_ext, "_CSRC", str(csrc))
+    assert _ext.stale_sources() == []
+    (csrc / "norm.hip").write_text((csrc / "norm.hip").read_text() + "\n// edited\n")
+    assert _ext.stale_sources() == ["norm.hip"]

@@ -4,7 +4,10 @@ No hipify, no CUDA compatibility layer: every ``csrc/*.hip`` file is plain HIP c
 ``hipcc --offload-arch=gfx950`` into an object with C-ABI launchers; ``csrc/bind.cpp`` (torch +
 pybind11 glue, host-only) is compiled by the host C++ compiler with torch's headers; both are linked
 into one shared object next to the Python package so it travels with the repo snapshot.
-Incremental: an object is rebuilt only when its source or a header is newer.
+Incremental by content: an object is rebuilt when the hash of its source, the headers or its command line changed
+(``<obj>.sha256`` sidecars).  Every link writes the provenance record ``distributed_llms_example_amd/_C.build.json``
+(arch, hipcc version, sha256 of every source and of the .so, objects rebuilt); ``_ext`` compares it with the sources
+at import and refuses a stale library on the GPU.
 
     python tools/build_native.py [--force] [-j N]
 """
@@ -13,10 +16,13 @@ from __future__ import annotations
 import argparse
 import concurrent.futures as cf
 import glob
+import hashlib
+import json
 import os
 import subprocess
 import sys
 import sysconfig
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "csrc")
@@ -46,11 +52,39 @@ def so_path() -> str:
     return os.path.join(PKG, "_C" + sysconfig.get_config_var("EXT_SUFFIX"))
 
 
-def _newer(src_list, out) -> bool:
-    if not os.path.exists(out):
+def _sha(path: str) -> str:
+    with open(path, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
+def _stale(obj: str, key: str) -> bool:
+    """Rebuild decision by CONTENT: an object is current when its sidecar holds the hash of (source, every header,
+    command line) it was built from — not by file times, which a checkout or copy can reorder."""
+    side = obj + ".sha256"
+    if not (os.path.exists(obj) and os.path.exists(side)):
         return True
-    t = os.path.getmtime(out)
-    return any(os.path.getmtime(s) > t for s in src_list)
+    with open(side) as f:
+        return f.read().strip() != key
+
+
+def _key(src: str, headers, cmd) -> str:
+    h = hashlib.sha256()
+    for p in [src] + sorted(headers):
+        h.update(os.path.basename(p).encode())
+        h.update(_sha(p).encode())
+    h.update(" ".join(c for c in cmd if c not in ("-o",) and not c.endswith(".o")).encode())
+    return h.hexdigest()
+
+
+def source_hashes() -> dict:
+    """{file name: sha256} of every native source and header (the provenance record's and _ext's staleness check)."""
+    files = sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")) +
+                   glob.glob(os.path.join(CSRC, "*.h")))
+    return {os.path.basename(p): _sha(p) for p in files}
+
+
+def record_path() -> str:
+    return os.path.join(PKG, "_C.build.json")
 
 
 def _run(cmd):
@@ -71,36 +105,56 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = True) -> str:
     for src in hip_srcs:
         obj = os.path.join(BUILD, os.path.basename(src) + ".o")
         objs.append(obj)
-        if force or _newer([src] + headers, obj):
-            jobs_list.append([HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-ffp-contract=fast",
-                              "-munsafe-fp-atomics"] + EXTRA_FLAGS.get(os.path.basename(src), []) +
-                             ["-I", CSRC, "-c", src, "-o", obj])
+        cmd = ([HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-ffp-contract=fast",
+                "-munsafe-fp-atomics"] + EXTRA_FLAGS.get(os.path.basename(src), []) + ["-I", CSRC, "-c", src, "-o", obj])
+        key = _key(src, headers, cmd)
+        if force or _stale(obj, key):
+            jobs_list.append((cmd, obj, key))
     # host C++ (torch + pybind11 glue, native runtime pieces): every csrc/*.cpp
     for cpp_src in sorted(glob.glob(os.path.join(CSRC, "*.cpp"))):
         cpp_obj = os.path.join(BUILD, os.path.basename(cpp_src) + ".o")
         objs.append(cpp_obj)
-        if force or _newer([cpp_src] + headers, cpp_obj):
-            cmd = [CXX, "-O2", "-fPIC", "-std=c++17", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DUSE_ROCM=1",
-                   "-D__HIP_PLATFORM_AMD__=1", "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H",
-                   "-DUSE_C10D_GLOO", "-DUSE_C10D_NCCL", "-DUSE_DISTRIBUTED",
-                   "-Wno-deprecated-declarations", "-I", CSRC, "-I", py_inc]
-            for i in inc:
-                cmd += ["-I", i]
-            cmd += ["-c", cpp_src, "-o", cpp_obj]
-            jobs_list.append(cmd)
+        cmd = [CXX, "-O2", "-fPIC", "-std=c++17", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DUSE_ROCM=1",
+               "-D__HIP_PLATFORM_AMD__=1", "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H",
+               "-DUSE_C10D_GLOO", "-DUSE_C10D_NCCL", "-DUSE_DISTRIBUTED",
+               "-Wno-deprecated-declarations", "-I", CSRC, "-I", py_inc]
+        for i in inc:
+            cmd += ["-I", i]
+        cmd += ["-c", cpp_src, "-o", cpp_obj]
+        key = _key(cpp_src, headers, cmd)
+        if force or _stale(cpp_obj, key):
+            jobs_list.append((cmd, cpp_obj, key))
     if jobs_list:
+        def one(job):
+            cmd, obj, key = job
+            _run(cmd)
+            with open(obj + ".sha256", "w") as f:
+                f.write(key)
         with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
-            futs = [ex.submit(_run, c) for c in jobs_list]
+            futs = [ex.submit(one, j) for j in jobs_list]
             for f in futs:
                 f.result()
     out = so_path()
-    if force or jobs_list or _newer(objs, out):
+    srcs = source_hashes()
+    rec = None
+    if os.path.exists(record_path()):
+        with open(record_path()) as f:
+            rec = json.load(f)
+    fresh = (rec is not None and rec.get("sources") == srcs and rec.get("arch") == ARCH and os.path.exists(out)
+             and rec.get("so_sha256") == _sha(out))
+    if force or jobs_list or not fresh:
         link = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out] + objs + [
             f"-L{lib}", "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python", "-lc10_hip", "-ltorch_hip",
             "-L/opt/rocm/lib", "-lamdhip64", f"-Wl,-rpath,{lib}", "-Wl,-rpath,/opt/rocm/lib"]
         _run(link)
+        rec = {"arch": ARCH, "hipcc": _run([HIPCC, "--version"]).splitlines()[0:2], "sources": srcs,
+               "objects_rebuilt": [os.path.basename(j[1]) for j in jobs_list], "so": os.path.basename(out),
+               "so_sha256": _sha(out), "built_at": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime())}
+        with open(record_path(), "w") as f:
+            json.dump(rec, f, indent=1)
         if verbose:
-            print(f"[build_native] linked {os.path.relpath(out, ROOT)} ({len(hip_srcs)} HIP sources, arch {ARCH})")
+            print(f"[build_native] linked {os.path.relpath(out, ROOT)} ({len(hip_srcs)} HIP sources, arch {ARCH}; "
+                  f"{len(jobs_list)} objects rebuilt; provenance {os.path.relpath(record_path(), ROOT)})")
     elif verbose:
         print(f"[build_native] up to date: {os.path.relpath(out, ROOT)}")
     return out
