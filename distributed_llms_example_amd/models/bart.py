@@ -64,7 +64,10 @@ class BartAttention(nn.Module):
                 q = q.view(B, S, H, D)
             else:
                 q = self.q_proj(x).view(B, S, H, D)
-            o = attn_ops.attention_q_kv(q, kv if kv is not None else self.project_kv(kv_in), **kw)
+            kv = kv if kv is not None else self.project_kv(kv_in)
+            if kv.shape[0] != B:  # beam search: the nb hypotheses of a batch entry share its encoder K/V (read once)
+                q = q.reshape(kv.shape[0], (B // kv.shape[0]) * S, H, D)
+            o = attn_ops.attention_q_kv(q, kv, **kw)
         else:
             if residual:
                 qkv, res = linear_res(x, self.qkv_proj)

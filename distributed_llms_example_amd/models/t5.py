@@ -76,6 +76,8 @@ class T5Attention(nn.Module):
         if self.cross:
             q = self.q(x).view(B, S, H, D)
             kv = kv if kv is not None else self.project_kv(kv_in)
+            if kv.shape[0] != B:  # beam search: the nb hypotheses of a batch entry share its encoder K/V (read once)
+                q = q.reshape(kv.shape[0], (B // kv.shape[0]) * S, H, D)
             chunk = long_sequence_chunk(kv.shape[1], cross=True)
             if chunk is not None:  # long encoder output: key-chunked blocks merged by LSE
                 o = chunked_cross_attention(q, kv[:, :, 0], kv[:, :, 1], chunk=chunk, scale=1.0,

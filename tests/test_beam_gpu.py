@@ -69,3 +69,20 @@ def test_generation_fused_beam_step_matches_composite(monkeypatch):
                                min_length=5))
     assert _ext.native() is not None
     assert outs[0].shape == outs[1].shape and torch.equal(outs[0], outs[1]), (outs[0][:2], outs[1][:2])
+
+
+def test_generation_shared_cross_kv_matches_per_beam_copies(monkeypatch):
+    """Beam search with the encoder K/V projected once per batch entry (the nb hypotheses as query rows of one
+    cross-attention call) == per-hypothesis K/V copies (DLLM_GEN_SHARED_CROSS=0), on the GPU kernels."""
+    cfg = resolve_config("t5-base").replace(num_layers=2, num_decoder_layers=2, vocab_size=4096, d_model=512,
+                                            num_heads=8, d_kv=64, d_ff=1024)
+    torch.manual_seed(0)
+    m = build_model(cfg).cuda().to(torch.bfloat16).eval()
+    ids = torch.randint(3, cfg.vocab_size, (5, 60), device="cuda")
+    am = torch.ones_like(ids)
+    am[1, -17:] = 0
+    outs = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("DLLM_GEN_SHARED_CROSS", flag)
+        outs.append(m.generate(ids, attention_mask=am, max_length=20, num_beams=3))
+    assert outs[0].shape == outs[1].shape and torch.equal(outs[0], outs[1])

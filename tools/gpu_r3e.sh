@@ -35,4 +35,12 @@ run t5b_b64 --batch-per-gpu 64 --steps 10 --warmup 3 &&
 run t5b_b128 --batch-per-gpu 128 --steps 10 --warmup 3 &&
 run bartl_b256 --model bart-large --batch-per-gpu 256 --steps 6 --warmup 2 &&
 run t5l_b32 --model t5-large --batch-per-gpu 32 --steps 6 --warmup 2 &&
-run flanxl_b16 --model flan-t5-xl --batch-per-gpu 16 --steps 5 --warmup 2
+run flanxl_b16 --model flan-t5-xl --batch-per-gpu 16 --steps 5 --warmup 2 || true
+echo "[r3e] profile b8 (graph)"
+d=$O/prof8
+mkdir -p $d
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $d -o run -- python bench.py --batch-per-gpu 8 --steps 20 --warmup 3 --graph off > $O/prof8.log 2>&1 || { tail -5 $O/prof8.log; exit 1; }
+db=$(find $d -name "*.db" | head -n 1); csv=$(find $d -name "*kernel_stats.csv" | head -n 1)
+python tools/prof_summary.py "${db:-$csv}" 23 > $O/prof8_summary.txt && head -40 $O/prof8_summary.txt
+[ -n "$db" ] && rm -f "$db"
+exit 0
