@@ -132,6 +132,7 @@ DLLM_DEVICE void mfma0(f32x4& c, const bf16x8v& b, const bf16x8v& a) {
 
 // RS bit 0 = fragment read schedule: 0 spreads the 16 next-sub-step reads over the 8 chunks (2 per chunk), 1 issues
 // them 4 per chunk in the first 4 chunks after they become legal (more MFMA cover for their latency).
+// RS bit 1 = direct epilogue stores from the accumulator layout instead of the LDS-staged whole-row stores (A/B).
 // RS bits 4..7 = ABLATIONS for timing studies only (results are garbage): 16 no k-loop DMAs, 32 no k-loop fragment
 // reads, 64 no k-loop wait + barrier, 128 no epilogue stores (tools/gemm_w4_bench.py --ablate)
 template <bool BKM, bool BIAS, bool ACC, int RS>
@@ -366,8 +367,12 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
     // ---- epilogue.  acc[i][j][r] = C[m0 + wm*128 + 16 i + (l & 15)][n0 + wn*128 + 16 j + 4 (l >> 4) + r].
     // Row blocks 2ii / 2ii+1 packed to bf16 and exchanged with v_permlane16_swap (odd 16-lane rows of X <-> even rows
     // of Y): afterwards lane l holds 8 consecutive columns 16 j + 8 (qd >> 1) of row 32 ii + 16 (qd & 1) + (l & 15).
-    // Stores through a buffer descriptor over the tile's rows: rows past M fall out of its range, columns past N are
-    // pushed out per lane, so every wave issues exactly 32 stores (the vmcnt(32) above counts them).
+    // STAGE (default): each 32-row group goes through this wave's 8 KB LDS scratch (row-major, 16-B chunks XOR-swizzled
+    // by row: conflict-free both ways) and leaves as whole-row stores, 4 rows x 256 B per instruction = 8 full 128-B
+    // lines, instead of 32 rows x 32 B = 32 partial lines from the accumulator layout (the store-bound part of the
+    // kernel: tools/gemm_w4_bench.py --ablate).  Stores go through a buffer descriptor over the tile's rows: rows past
+    // M fall out of its range, columns past N are pushed out per lane, so every wave issues exactly 32 stores (the
+    // vmcnt(32) above counts them).
     {
       // descriptor inputs made provably wave-uniform (readfirstlane), or hipcc wraps every store in a waterfall loop
       const uint64_t cb = (uint64_t)(P.C + (long)m0 * P.ldc);
@@ -386,6 +391,16 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
           if (nb4 < P.N) bv[j] = Elem<uint16_t>::load4(P.bias + nb4);
         }
       }
+      auto add_c = [&](u32x4 o, uint32_t off) {  // ACC: o + C, in fp32, rounded once
+        const u32x4 c = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(srdC, off, 0, 0));
+        auto add2 = [](uint32_t u, uint32_t v) {
+          return pk2(bf2f((uint16_t)(u & 0xFFFFu)) + bf2f((uint16_t)(v & 0xFFFFu)),
+                     bf2f((uint16_t)(u >> 16)) + bf2f((uint16_t)(v >> 16)));
+        };
+        return u32x4{add2(o.x, c.x), add2(o.y, c.y), add2(o.z, c.z), add2(o.w, c.w)};
+      };
+      unsigned char* scr = smem + 2 * BUF + (uint32_t)w * 8192u;  // this wave's staging rows [32][256 B]
+      const int rowL = 16 * (qd & 1) + rl;                       // staging row written by this lane
 #pragma unroll
       for (int ii = 0; ii < 4; ++ii) {
 #pragma unroll
@@ -407,20 +422,33 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
             x1 = r1[0];
             y1 = r1[1];
           }
-          const int nl = nc + 16 * j;
-          const uint32_t off = n0 + nl < P.N ? (uint32_t)((mr + 32 * ii) * P.ldc + n0 + nl) * 2u : kOOB;
           u32x4 o = {x0, x1, y0, y1};
-          if constexpr (ACC) {
-            const u32x4 c = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(srdC, off, 0, 0));
-            auto add2 = [](uint32_t u, uint32_t v) {
-              return pk2(bf2f((uint16_t)(u & 0xFFFFu)) + bf2f((uint16_t)(v & 0xFFFFu)),
-                         bf2f((uint16_t)(u >> 16)) + bf2f((uint16_t)(v >> 16)));
-            };
-            o = u32x4{add2(o.x, c.x), add2(o.y, c.y), add2(o.z, c.z), add2(o.w, c.w)};
+          if constexpr ((RS & 2) == 0) {  // staged: chunk 2j + (qd >> 1) of staging row rowL, swizzled by the row
+            const int cj = 2 * j + (qd >> 1);
+            *reinterpret_cast<u32x4*>(scr + rowL * 256 + ((cj ^ (rowL & 15)) << 4)) = o;
+          } else {
+            const int nl = nc + 16 * j;
+            const uint32_t off = n0 + nl < P.N ? (uint32_t)((mr + 32 * ii) * P.ldc + n0 + nl) * 2u : kOOB;
+            if constexpr (ACC) o = add_c(o, off);
+            if constexpr ((RS & 128) == 0) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, o), srdC, off, 0, 0);
           }
-          if constexpr ((RS & 128) == 0) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, o), srdC, off, 0, 0);
           // bound the live ranges
           if (j & 1) __builtin_amdgcn_sched_barrier(0);
+        }
+        if constexpr ((RS & 2) == 0) {
+          // read back row-major (the same wave's DS instructions execute in order: no barrier, and the next group's
+          // writes cannot overtake these reads): store s covers staging rows 4s .. 4s+3, lane -> (row 4s + l/16,
+          // 16-B chunk l%16)
+#pragma unroll
+          for (int s2 = 0; s2 < 8; ++s2) {
+            const int r = 4 * s2 + (lane >> 4), c = lane & 15;
+            u32x4 o = *reinterpret_cast<const u32x4*>(scr + r * 256 + ((c ^ (r & 15)) << 4));
+            const int col = wn * 128 + 8 * c;
+            const uint32_t off = n0 + col < P.N ? (uint32_t)((wm * 128 + 32 * ii + r) * P.ldc + n0 + col) * 2u : kOOB;
+            if constexpr (ACC) o = add_c(o, off);
+            if constexpr ((RS & 128) == 0) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, o), srdC, off, 0, 0);
+          }
+          __builtin_amdgcn_sched_barrier(0);
         }
       }
     }
@@ -453,7 +481,7 @@ int num_cus() {
 // and at least 2 k-tiles per tile; otherwise one tile per workgroup
 template <bool BKM, bool BIAS, bool ACC, int RS>
 int launch_rs(const GemmW4Params& p, bool persist, hipStream_t st) {
-  constexpr size_t lds = 2 * 2 * 256 * BK * 2;  // 128 KB
+  constexpr size_t lds = 2 * 2 * 256 * BK * 2 + ((RS & 2) == 0 ? 4 * 8192 : 0);  // 128 KB (+ 32 KB output staging)
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)gemm_w4_kernel<BKM, BIAS, ACC, RS>,
@@ -483,8 +511,12 @@ int launch(const GemmW4Params& p, bool persist, hipStream_t st) {
       default: break;
     }
   }
-  if (rs & 1) return launch_rs<BKM, BIAS, ACC, 1>(p, persist, st);
-  return launch_rs<BKM, BIAS, ACC, 0>(p, persist, st);
+  switch (rs & 3) {  // bit 1: direct (unstaged) epilogue stores, for A/B
+    case 0: return launch_rs<BKM, BIAS, ACC, 0>(p, persist, st);
+    case 2: return launch_rs<BKM, BIAS, ACC, 2>(p, persist, st);
+    case 3: return launch_rs<BKM, BIAS, ACC, 3>(p, persist, st);
+    default: return launch_rs<BKM, BIAS, ACC, 1>(p, persist, st);
+  }
 }
 
 template <bool BKM>

@@ -81,8 +81,9 @@ def main():
             for k, fn in arms.items():
                 if k != "lib":
                     rec[f"{k}_relerr"] = float(f"{((fn().float() - ref).norm() / ref.norm()).item():.2e}")
-            rsv = {"w4rs1": "1"}
+            rsv = {"w4rs1": "1", "w4direct": "3"}
             arms["w4rs1"] = arms["w4"]  # same call, DLLM_W4_RS=1 (early fragment reads), set per arm below
+            arms["w4direct"] = arms["w4"]  # RS=3: early reads, unstaged epilogue stores
             if a.ablate and phase == "fwd":
                 for tag, v in (("nodma", "16"), ("noread", "32"), ("nobar", "64"), ("nostore", "128"),
                                ("mfmaonly", "112")):
