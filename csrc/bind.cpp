@@ -39,7 +39,8 @@ int dllm_attn_params_size();
 int dllm_attn_dropout_mask(AttnParams*, hipStream_t);
 int dllm_gemm_wgrad(const GemmWgradParams*, int, hipStream_t);
 int dllm_gemm_fused(const GemmFusedParams*, int, int, hipStream_t);
-int dllm_gemm_w4(const GemmW4Params*, int, int, hipStream_t);
+int dllm_gemm_w4(const GemmW4Params*, int, int, int, hipStream_t);
+int dllm_set_seed_step_gemm_w4(const uint32_t*);
 int dllm_colsum_rows();
 int dllm_ce_chunk_fwd(const void*, long, const int64_t*, const float*, float*, float*, float*, long, int, int, int, float,
                       long, int, int, int, hipStream_t);
@@ -700,8 +701,11 @@ bool gemm_w4_supported(const Tensor& a, const Tensor& b, bool b_kmajor) {
   return Kb == K && K > 0 && K % 64 == 0 && M > 0 && N > 0 && N % 8 == 0 && ranges && (M + 255) / 256 * ((N + 255) / 256) < INT_MAX;
 }
 
+// epi 0: plain; 1: ReLU + dropout(p, seed) writing the keep-and-positive bit mask (NT); 7: input gradient through
+// that mask (NN).  mask: int32 tensor of >= ceil(M/256) * ceil(N/256) * 2048 words (gemm_w4_mask_words).
 Tensor gemm_w4(const Tensor& a, const Tensor& b, bool b_kmajor, const optional<Tensor>& bias, const optional<Tensor>& out,
-               bool accumulate, int64_t grp, bool persist) {
+               bool accumulate, int64_t grp, bool persist, int64_t epi, double p, int64_t seed,
+               const optional<Tensor>& mask) {
   TORCH_CHECK(gemm_w4_supported(a, b, b_kmajor),
               "gemm_w4: need bf16 GPU a [M,K], b [N,K] (or [K,N] k-major), unit inner stride, 16-B aligned rows, K % 64 == 0, "
               "N % 8 == 0");
@@ -739,9 +743,25 @@ Tensor gemm_w4(const Tensor& a, const Tensor& b, bool b_kmajor, const optional<T
   P.tn = (int)((N + 255) / 256);
   P.grp = grp >= 0 ? (int)grp : 4;
   P.accumulate = accumulate ? 1 : 0;
-  check_rc(dllm_gemm_w4(&P, b_kmajor ? 1 : 0, persist ? 1 : 0, stream()), "gemm_w4");
+  if (epi != 0) {
+    TORCH_CHECK(mask.has_value() && mask->defined() && mask->is_cuda() && mask->device() == a.device() &&
+                    mask->scalar_type() == at::kInt && mask->is_contiguous() &&
+                    mask->numel() >= (int64_t)P.tm * P.tn * 2048 && reinterpret_cast<uintptr_t>(mask->data_ptr()) % 16 == 0,
+                "gemm_w4: epilogue mask must be a contiguous int32 GPU tensor of >= ceil(M/256)*ceil(N/256)*2048 words");
+    TORCH_CHECK(M * N < (1LL << 32), "gemm_w4: dropout element index must fit 32 bits");
+    TORCH_CHECK(p >= 0.0 && p < 1.0, "gemm_w4: dropout p in [0, 1)");
+    P.mask = reinterpret_cast<uint32_t*>(mask->data_ptr());
+    P.p = (float)p;
+    P.scale = p > 0.0 ? (float)(1.0 / (1.0 - p)) : 1.f;
+    P.seed = (uint32_t)seed;
+    const double t = p * 65536.0;  // csrc/common.h drop_threshold
+    P.thr = t >= 65535.0 ? 0xFFFFu : (uint32_t)t;
+  }
+  check_rc(dllm_gemm_w4(&P, b_kmajor ? 1 : 0, persist ? 1 : 0, (int)epi, stream()), "gemm_w4");
   return c;
 }
+
+int64_t gemm_w4_mask_words(int64_t M, int64_t N) { return ((M + 255) / 256) * ((N + 255) / 256) * 2048; }
 
 // Gated-GELU FFN (FLAN-T5 / T5 v1.1 "gated-gelu", tanh GELU) on the ping-pong kernel, csrc/gemm_fused.hip epi 8 / 9.
 // forward: x [M, d] . [wi_0; wi_1]^T ([2F, d], the stacked wi weight) -> h = dropout(gelu(x wi_0^T) * (x wi_1^T)) [M, F]
@@ -862,6 +882,7 @@ void set_seed_step(const optional<Tensor>& step) {
   check_rc(dllm_set_seed_step_act(p), "set_seed_step(act)");
   check_rc(dllm_set_seed_step_attn(p), "set_seed_step(attn)");
   check_rc(dllm_set_seed_step_gemm_fused(p), "set_seed_step(gemm_fused)");
+  check_rc(dllm_set_seed_step_gemm_w4(p), "set_seed_step(gemm_w4)");
 }
 
 namespace dllm {
@@ -910,7 +931,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_fused_variant", &gemm_fused_variant, "default kernel variant for reduction length K");
   m.def("gemm_w4", &gemm_w4, "out (+)= a . b (+ bias) on the one-wave-per-SIMD GEMM (csrc/gemm_w4.hip)", py::arg("a"),
         py::arg("b"), py::arg("b_kmajor"), py::arg("bias") = py::none(), py::arg("out") = py::none(),
-        py::arg("accumulate") = false, py::arg("grp") = -1, py::arg("persist") = true);
+        py::arg("accumulate") = false, py::arg("grp") = -1, py::arg("persist") = true, py::arg("epi") = 0,
+        py::arg("p") = 0.0, py::arg("seed") = 0, py::arg("mask") = py::none());
+  m.def("gemm_w4_mask_words", &gemm_w4_mask_words);
   m.def("gemm_w4_supported", &gemm_w4_supported);
   m.def("beam_topk", &beam_topk);
   m.def("colsum_acc", &colsum_acc, "out += x.sum(0) for a token-major bf16 x (bias gradients)");

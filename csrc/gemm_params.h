@@ -30,6 +30,12 @@ struct GemmW4Params {
   int tm, tn;      // ceil(M / 256), ceil(N / 256)
   int grp;         // tile order: groups of grp 256-row blocks, column-major inside a group; 0 = row-major
   int accumulate;  // 1: C += A . B (bf16 read-modify-write), 0: C = A . B
+  // epilogue (csrc/gemm_w4.hip W4_EPI_*): ReLU + dropout forward writing the keep-and-positive bit mask, or the input
+  // gradient through that mask.  mask: 8 words per thread per 256x256 tile (tile-major, thread-minor), bit 4 j + r of
+  // word i <-> accumulator acc[i][j][r]
+  uint32_t* mask;
+  float p, scale;  // dropout probability, 1 / (1 - p)
+  uint32_t seed, thr;
 };
 
 // csrc/gemm_fused.hip: C[M][N] = epi(A[M][K] . B), B = [N][K] (b_kmajor = 0) or [K][N] (b_kmajor = 1)

@@ -36,7 +36,14 @@
 
 using namespace dllm;
 
+DLLM_SEED_STEP_TU(gemm_w4)
+
 namespace {
+
+// epilogues: none; ReLU + dropout with the bit mask of kept positive outputs (forward, NT); the input gradient
+// through that mask, dU = dH * scale where the bit is set (backward, NN).  The mask is what the backward needs of
+// the forward: no re-read of H, no re-hash (T5 FFN, ops/ffn.py).
+enum { W4_EPI_NONE = 0, W4_EPI_RELU = 1, W4_EPI_DRELU_M = 7 };
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8v;
 typedef __attribute__((ext_vector_type(4))) short s16x4;
@@ -135,7 +142,7 @@ DLLM_DEVICE void mfma0(f32x4& c, const bf16x8v& b, const bf16x8v& a) {
 // RS bit 1 = direct epilogue stores from the accumulator layout instead of the LDS-staged whole-row stores (A/B).
 // RS bits 4..7 = ABLATIONS for timing studies only (results are garbage): 16 no k-loop DMAs, 32 no k-loop fragment
 // reads, 64 no k-loop wait + barrier, 128 no epilogue stores (tools/gemm_w4_bench.py --ablate)
-template <bool BKM, bool BIAS, bool ACC, int RS>
+template <bool BKM, bool BIAS, bool ACC, int RS, int EPI = W4_EPI_NONE>
 __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr uint32_t TB = 256 * BK * 2;  // one operand image: 32 KB
@@ -251,7 +258,23 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
     return dma_plan(cross ? sa1 : sa0, cross ? sb1 : sb0, cross ? kn - nk : min(kn, nk - 1), b);
   };
 
+  // ---- mask of a tile for the DRELU_M epilogue: this wave's 64 threads x 32 B by LDS-DMA into the first 2 KB of its
+  // output staging rows, issued when the tile starts; it lands under the k-loop (its waits retire it) and is read into
+  // registers before the staging rows are reused.
+  unsigned char* const scr = smem + 2 * BUF + (uint32_t)w * 8192u;  // this wave's staging rows [32][256 B]
+  const uint32_t scr_lds = lds_addr(smem) + 2 * BUF + (uint32_t)w * 8192u;
+  const i32x4 srd_mask = make_srd(P.mask, 0xFFFFFFF0u);
+  auto mask_dma = [&](int tm0, int tn0) {
+    if constexpr (EPI == W4_EPI_DRELU_M) {
+      const uint32_t base = (uint32_t)(((tm0 / 256) * P.tn + tn0 / 256) * 256 + tid) * 32u;
+      dma16<0>(srd_mask, base, 0u, scr_lds);
+      dma16<1024>(srd_mask, base + 16u, 0u, scr_lds);
+    }
+  };
+  const uint32_t seed = (EPI == W4_EPI_RELU && P.p > 0.f) ? eff_seed(P.seed) : P.seed;
+
   // ---- prologue: k-tiles 0 and 1 in flight, wait for k-tile 0, read its first half
+  mask_dma(m0, n0);
   {
     const Dma q0 = dma_plan(sa0, sb0, 0, 0), q1 = plan_next(0, -1, 1);
     sfor<0, 16>([&](auto D) { dma(q0, D); });
@@ -382,6 +405,18 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
           (int)__builtin_amdgcn_readfirstlane((uint32_t)(min(P.M - m0, 256) * P.ldc * 2)), 0x00020000);
       const int mr = wm * 128 + 16 * (qd & 1) + rl;  // tile-local row of ii = 0
       const int nc = wn * 128 + 8 * (qd >> 1);       // tile-local column of j = 0
+      uint32_t mw[8];  // mask words: bit 4 j + r of word i <-> acc[i][j][r]
+      if constexpr (EPI == W4_EPI_DRELU_M) {
+        // the tile's mask DMA is older than every DMA of the last k-tile: at most those 16 are still outstanding
+        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        const u32x4 lo = *reinterpret_cast<const u32x4*>(scr + 16 * lane);
+        const u32x4 hi = *reinterpret_cast<const u32x4*>(scr + 1024 + 16 * lane);
+        mw[0] = lo.x; mw[1] = lo.y; mw[2] = lo.z; mw[3] = lo.w;
+        mw[4] = hi.x; mw[5] = hi.y; mw[6] = hi.z; mw[7] = hi.w;
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) mw[i] = 0u;
+      }
       f32x4 bv[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -399,7 +434,6 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
         };
         return u32x4{add2(o.x, c.x), add2(o.y, c.y), add2(o.z, c.z), add2(o.w, c.w)};
       };
-      unsigned char* scr = smem + 2 * BUF + (uint32_t)w * 8192u;  // this wave's staging rows [32][256 B]
       const int rowL = 16 * (qd & 1) + rl;                       // staging row written by this lane
 #pragma unroll
       for (int ii = 0; ii < 4; ++ii) {
@@ -412,6 +446,30 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
           if constexpr (BIAS) {
             xv += bv[j];
             yv += bv[j];
+          }
+          if constexpr (EPI == W4_EPI_RELU) {
+            const uint32_t n4 = (uint32_t)(n0 + wn * 128 + 16 * j + 4 * qd);
+            const uint32_t ex = (uint32_t)(m0 + wm * 128 + 32 * ii + rl) * (uint32_t)P.N + n4;  // element of xv[0]
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              xv[r] = fmaxf(xv[r], 0.f);
+              yv[r] = fmaxf(yv[r], 0.f);
+            }
+            if (P.p > 0.f) {
+              dropout4(xv, seed, P.thr, ex, P.scale);
+              dropout4(yv, seed, P.thr, ex + 16u * (uint32_t)P.N, P.scale);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              mw[2 * ii] |= (xv[r] > 0.f ? 1u : 0u) << (4 * j + r);
+              mw[2 * ii + 1] |= (yv[r] > 0.f ? 1u : 0u) << (4 * j + r);
+            }
+          } else if constexpr (EPI == W4_EPI_DRELU_M) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              xv[r] = (mw[2 * ii] >> (4 * j + r)) & 1u ? xv[r] * P.scale : 0.f;
+              yv[r] = (mw[2 * ii + 1] >> (4 * j + r)) & 1u ? yv[r] * P.scale : 0.f;
+            }
           }
           uint32_t x0 = pk2(xv.x, xv.y), x1 = pk2(xv.z, xv.w), y0 = pk2(yv.x, yv.y), y1 = pk2(yv.z, yv.w);
           {
@@ -451,6 +509,11 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
           __builtin_amdgcn_sched_barrier(0);
         }
       }
+      if constexpr (EPI == W4_EPI_RELU) {  // this thread's 8 mask words of the tile
+        uint32_t* mp = P.mask + (size_t)(((m0 / 256) * P.tn + n0 / 256) * 256 + tid) * 8;
+        *reinterpret_cast<u32x4*>(mp) = u32x4{mw[0], mw[1], mw[2], mw[3]};
+        *reinterpret_cast<u32x4*>(mp + 4) = u32x4{mw[4], mw[5], mw[6], mw[7]};
+      }
     }
     __builtin_amdgcn_sched_barrier(0);
     // next tile becomes current
@@ -458,6 +521,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
     n0 = n1;
     sa0 = sa1;
     sb0 = sb1;
+    if (ti + 1 < ntw) mask_dma(m0, n0);  // the staging rows' reads above returned before their stores issued
     if (ti + 2 < ntw) {
       tile_mn(ti + 2, m1, n1);
       sa1 = srd_a(m1);
@@ -479,18 +543,19 @@ int num_cus() {
 
 // persist: one workgroup per CU (LDS and registers admit one) walking its tiles, when there are more tiles than CUs
 // and at least 2 k-tiles per tile; otherwise one tile per workgroup
-template <bool BKM, bool BIAS, bool ACC, int RS>
+template <bool BKM, bool BIAS, bool ACC, int RS, int EPI = W4_EPI_NONE>
 int launch_rs(const GemmW4Params& p, bool persist, hipStream_t st) {
+  static_assert(EPI == W4_EPI_NONE || (RS & 2) == 0, "epilogues use the staging rows");
   constexpr size_t lds = 2 * 2 * 256 * BK * 2 + ((RS & 2) == 0 ? 4 * 8192 : 0);  // 128 KB (+ 32 KB output staging)
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_w4_kernel<BKM, BIAS, ACC, RS>,
+    (void)hipFuncSetAttribute((const void*)gemm_w4_kernel<BKM, BIAS, ACC, RS, EPI>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
   const int T = p.tm * p.tn, cus = num_cus() / 8 * 8;
   const int grid = persist && p.K >= 2 * BK && cus >= 8 && T > cus ? cus : T;
-  hipLaunchKernelGGL((gemm_w4_kernel<BKM, BIAS, ACC, RS>), dim3(grid), dim3(NT), lds, st, p);
+  hipLaunchKernelGGL((gemm_w4_kernel<BKM, BIAS, ACC, RS, EPI>), dim3(grid), dim3(NT), lds, st, p);
   DLLM_CHECK_LAUNCH();
   return 0;
 }
@@ -527,8 +592,19 @@ int dispatch(const GemmW4Params& p, bool persist, hipStream_t st) {
 
 }  // namespace
 
-extern "C" int dllm_gemm_w4(const GemmW4Params* pp, int b_kmajor, int persist, hipStream_t st) {
+// epi: W4_EPI_NONE, W4_EPI_RELU (NT, optional bias, no accumulate), W4_EPI_DRELU_M (NN, no bias, no accumulate)
+extern "C" int dllm_gemm_w4(const GemmW4Params* pp, int b_kmajor, int persist, int epi, hipStream_t st) {
   const GemmW4Params& p = *pp;
   if (p.M <= 0 || p.N <= 0 || p.K <= 0 || p.K % BK || p.N % 8 || p.tm * 256 < p.M || p.tn * 256 < p.N) return -4;
+  if (epi == W4_EPI_RELU) {
+    if (b_kmajor || p.accumulate || p.mask == nullptr) return -5;
+    return p.bias ? launch_rs<false, true, false, 1, W4_EPI_RELU>(p, persist != 0, st)
+                  : launch_rs<false, false, false, 1, W4_EPI_RELU>(p, persist != 0, st);
+  }
+  if (epi == W4_EPI_DRELU_M) {
+    if (!b_kmajor || p.accumulate || p.bias || p.mask == nullptr) return -5;
+    return launch_rs<true, false, false, 1, W4_EPI_DRELU_M>(p, persist != 0, st);
+  }
+  if (epi != W4_EPI_NONE) return -5;
   return b_kmajor ? dispatch<true>(p, persist != 0, st) : dispatch<false>(p, persist != 0, st);
 }

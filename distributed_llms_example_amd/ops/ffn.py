@@ -46,6 +46,10 @@ EPILOGUES = {"relu": (1, 3), "gelu": (2, 4), "gelu_new": (5, 6), "gelu_fast": (5
 _VARIANT = int(os.environ.get("DLLM_GEMM_FUSED_VARIANT", "-1"))  # -1: picked by K in csrc/bind.cpp
 _RELU_MASK = os.environ.get("DLLM_RELU_MASK", "1") != "0"  # 0: the backward re-reads H (A/B runs)
 _COLSUM = os.environ.get("DLLM_FFN_BIAS_COLSUM", "1") != "0"  # 0: wi bias gradient by a separate column-sum pass
+# ReLU FFN (T5) on csrc/gemm_w4.hip: forward with the ReLU + dropout + bit-mask epilogue, backward input gradient through
+# the mask — instead of the 8-wave ping-pong kernel of csrc/gemm_fused.hip (0: ping-pong, A/B)
+_W4_FFN = os.environ.get("DLLM_W4_FFN", "1") != "0"
+w4_ffn_calls = 0
 fused_calls = 0  # number of FFN forwards that took the fused path (tests assert the kernel really ran)
 
 
@@ -66,6 +70,22 @@ class _FusedFFNFn(torch.autograd.Function):
         x2 = x.reshape(-1, shape[-1])
         efwd, _ = EPILOGUES[act]
         u = mask = None
+        if efwd == 1 and _W4_FFN and C.gemm_w4_supported(x2, wi, False) and \
+                (bi is None or (bi.dtype == torch.bfloat16 and bi.is_contiguous())):
+            global w4_ffn_calls
+            w4_ffn_calls += 1
+            mask = torch.empty(C.gemm_w4_mask_words(x2.shape[0], wi.shape[0]), device=x.device, dtype=torch.int32)
+            h = C.gemm_w4(x2, wi, False, bi, None, False, -1, True, 1, float(p), int(seed), mask)
+            y = linear_fwd(h, wo, bo)
+            ctx.set_materialize_grads(False)
+            ctx.save_for_backward(x2, h, None, mask)
+            ctx.params = params
+            for q in params:
+                _use(q)
+            ctx.cfg = (act, float(p), int(seed), shape)
+            ctx.w4 = True
+            return y.view(*shape[:-1], wo.shape[0]), x.view_as(x)
+        ctx.w4 = False
         if efwd != 1:  # GELU: the backward multiplies by the stored derivative
             u = torch.empty(x2.shape[0], wi.shape[0], device=x.device, dtype=x.dtype)
         elif _RELU_MASK and _pingpong(C, x2.shape[1]) and _pingpong(C, wo.shape[0]):  # ReLU: bits for the backward
@@ -95,7 +115,11 @@ class _FusedFFNFn(torch.autograd.Function):
         bsum = None
         if Bi is not None and ebwd in (4, 6) and _COLSUM and _pingpong(C, wo.shape[0]):
             bsum = torch.empty(dy2.shape[0] // 128, wo.shape[1], device=dy2.device, dtype=torch.float32)
-        if mask is not None:  # d-relu from the bit mask
+        if ctx.w4:  # d-relu from the w4 forward's bit mask
+            if not C.gemm_w4_supported(dy2, wo, True):
+                dy2 = dy2.contiguous()
+            du = C.gemm_w4(dy2, wo, True, None, None, False, -1, True, 7, p, seed, mask)
+        elif mask is not None:  # d-relu from the bit mask
             du = C.gemm_fused(dy2, wo, True, 7, None, None, None, p, seed, _VARIANT, mask)
         else:
             du = C.gemm_fused(dy2, wo, True, ebwd, None, h if ebwd == 3 else u, None, p, seed, _VARIANT, None, bsum)

@@ -84,3 +84,37 @@ def test_gemm_w4_rejects_bad_shapes():
     assert not C.gemm_w4_supported(a, w, False)
     with pytest.raises(RuntimeError):
         C.gemm_w4(a, w, False)
+
+
+@pytest.mark.parametrize("M,K,N", [(512, 128, 512), (1000, 768, 3072), (9000, 192, 2000), (300, 64, 264)])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+@pytest.mark.parametrize("bias", [False, True])
+def test_gemm_w4_relu_dropout_mask_roundtrip(M, K, N, p, bias):
+    """T5 FFN on w4 (ops/ffn.py): forward H = dropout(relu(X Wiᵀ + b)) with the counter-hash keep decision of element
+    m * N + n (ops/rng.py keep_from_index), writing the keep-and-positive bit mask; backward dU = (dY Wo) * mask / (1-p)
+    read from that mask.  Both vs fp32 torch."""
+    from distributed_llms_example_amd.ops.rng import keep_from_index
+    C = _ext.native()
+    torch.manual_seed(M + K + N)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    wi = (torch.randn(N, K, device=DEV) * K ** -0.5).to(torch.bfloat16)
+    bi = torch.randn(N, device=DEV).to(torch.bfloat16) if bias else None
+    seed = 1234
+    mask = torch.zeros(C.gemm_w4_mask_words(M, N), device=DEV, dtype=torch.int32)
+    h = C.gemm_w4(x, wi, False, bi, None, False, -1, True, 1, p, seed, mask)
+    u = x.float() @ wi.float().t() + (bi.float() if bias else 0.0)
+    keep = keep_from_index(seed, p, torch.arange(M * N, device=DEV, dtype=torch.int64)).view(M, N) if p > 0 else \
+        torch.ones(M, N, dtype=torch.bool, device=DEV)
+    ref = torch.relu(u) * keep / (1 - p)
+    assert _rel(h, ref) < 8e-3, _rel(h, ref)
+    # backward: dU = (dY Wo) through the mask, Wo = [K2, N] k-major operand of the dgrad
+    K2 = 256
+    dy = torch.randn(M, K2, device=DEV).to(torch.bfloat16)
+    wo = (torch.randn(K2, N, device=DEV) * K2 ** -0.5).to(torch.bfloat16)
+    du = C.gemm_w4(dy, wo, True, None, None, False, -1, True, 7, p, seed, mask)
+    live = (h.float() > 0)  # the mask's meaning: kept and positive
+    ref_du = (dy.float() @ wo.float()) * live / (1 - p)
+    assert _rel(du, ref_du) < 8e-3, _rel(du, ref_du)
+    # bits agree with H wherever H is clearly away from 0 (bf16 rounding of tiny positives aside)
+    far = h.float().abs() > 1e-2
+    assert torch.equal((du.float() != 0)[far], live[far] & ((dy.float() @ wo.float()) != 0)[far])
