@@ -47,8 +47,10 @@ _VARIANT = int(os.environ.get("DLLM_GEMM_FUSED_VARIANT", "-1"))  # -1: picked by
 _RELU_MASK = os.environ.get("DLLM_RELU_MASK", "1") != "0"  # 0: the backward re-reads H (A/B runs)
 _COLSUM = os.environ.get("DLLM_FFN_BIAS_COLSUM", "1") != "0"  # 0: wi bias gradient by a separate column-sum pass
 # ReLU FFN (T5) on csrc/gemm_w4.hip: forward with the ReLU + dropout + bit-mask epilogue, backward input gradient through
-# the mask — instead of the 8-wave ping-pong kernel of csrc/gemm_fused.hip (0: ping-pong, A/B)
-_W4_FFN = os.environ.get("DLLM_W4_FFN", "1") != "0"
+# the mask (DLLM_W4_FFN=1) instead of the 8-wave ping-pong kernel of csrc/gemm_fused.hip (default).  Measured 0.5 %
+# slower per t5-base step (profiles/r3_w4_ffn_ab.txt): w4's epilogue (the dropout hash of 64K elements per tile) runs
+# with the matrix cores idle, where the ping-pong kernel's second wave per SIMD keeps them busy.
+_W4_FFN = os.environ.get("DLLM_W4_FFN", "0") == "1"
 w4_ffn_calls = 0
 fused_calls = 0  # number of FFN forwards that took the fused path (tests assert the kernel really ran)
 
