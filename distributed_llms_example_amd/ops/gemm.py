@@ -24,9 +24,9 @@ from .. import _ext
 
 # Routing of the projection GEMMs (profiles/r3_gemm_w4_vs_hipblaslt.jsonl, t5-base / bart-large shapes):
 #   "auto" (default): csrc/gemm_w4.hip for input gradients whose reduction depth (the layer's output features) is
-#          <= 1024, or <= 2304 with >= 128K token rows — there it beats hipBLASLt's NN kernels by 1-9 % (o / wo / fc2
-#          and encoder QKV dgrads, the residual-accumulating ones included); forwards and deeper / smaller dgrads stay
-#          on hipBLASLt, which is 3-15 % faster there;
+#          <= 1024, <= 2304 with >= 128K token rows, or <= 3072 with >= 1024 output columns — there it beats
+#          hipBLASLt's NN kernels by 1-12 % (o / wo / fc2, encoder-QKV and BART-QKV dgrads, the residual-accumulating
+#          ones included); forwards and deeper dgrads stay on hipBLASLt, which is 1-10 % faster there;
 #   "1": every supported shape on gemm_w4 (A/B and tests), "0": none.
 _W4_MODE = os.environ.get("DLLM_W4_GEMM", "auto")
 _W4 = _W4_MODE != "0"
@@ -39,7 +39,8 @@ def _w4_ok(a: torch.Tensor, b: torch.Tensor, kmajor: bool) -> bool:
     if not _W4 or a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16 or not _ext.use_native(a):
         return False
     if _W4_MODE == "auto" and not (kmajor and (a.shape[-1] <= _W4_DGRAD_MAX_K
-                                               or (a.shape[-1] <= 2304 and a.shape[0] >= 131072))):
+                                               or (a.shape[-1] <= 2304 and a.shape[0] >= 131072)
+                                               or (a.shape[-1] <= 3072 and b.shape[-1] >= 1024))):
         return False
     return bool(_ext.native().gemm_w4_supported(a, b, kmajor))
 
