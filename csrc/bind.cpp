@@ -705,7 +705,7 @@ bool gemm_w4_supported(const Tensor& a, const Tensor& b, bool b_kmajor) {
 // that mask (NN).  mask: int32 tensor of >= ceil(M/256) * ceil(N/256) * 2048 words (gemm_w4_mask_words).
 Tensor gemm_w4(const Tensor& a, const Tensor& b, bool b_kmajor, const optional<Tensor>& bias, const optional<Tensor>& out,
                bool accumulate, int64_t grp, bool persist, int64_t epi, double p, int64_t seed,
-               const optional<Tensor>& mask) {
+               const optional<Tensor>& mask, bool mask_pp) {
   TORCH_CHECK(gemm_w4_supported(a, b, b_kmajor),
               "gemm_w4: need bf16 GPU a [M,K], b [N,K] (or [K,N] k-major), unit inner stride, 16-B aligned rows, K % 64 == 0, "
               "N % 8 == 0");
@@ -751,6 +751,7 @@ Tensor gemm_w4(const Tensor& a, const Tensor& b, bool b_kmajor, const optional<T
     TORCH_CHECK(M * N < (1LL << 32), "gemm_w4: dropout element index must fit 32 bits");
     TORCH_CHECK(p >= 0.0 && p < 1.0, "gemm_w4: dropout p in [0, 1)");
     P.mask = reinterpret_cast<uint32_t*>(mask->data_ptr());
+    P.mask_pp = mask_pp ? 1 : 0;
     P.p = (float)p;
     P.scale = p > 0.0 ? (float)(1.0 / (1.0 - p)) : 1.f;
     P.seed = (uint32_t)seed;
@@ -932,7 +933,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_w4", &gemm_w4, "out (+)= a . b (+ bias) on the one-wave-per-SIMD GEMM (csrc/gemm_w4.hip)", py::arg("a"),
         py::arg("b"), py::arg("b_kmajor"), py::arg("bias") = py::none(), py::arg("out") = py::none(),
         py::arg("accumulate") = false, py::arg("grp") = -1, py::arg("persist") = true, py::arg("epi") = 0,
-        py::arg("p") = 0.0, py::arg("seed") = 0, py::arg("mask") = py::none());
+        py::arg("p") = 0.0, py::arg("seed") = 0, py::arg("mask") = py::none(), py::arg("mask_pp") = false);
   m.def("gemm_w4_mask_words", &gemm_w4_mask_words);
   m.def("gemm_w4_supported", &gemm_w4_supported);
   m.def("beam_topk", &beam_topk);

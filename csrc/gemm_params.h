@@ -36,6 +36,7 @@ struct GemmW4Params {
   uint32_t* mask;
   float p, scale;  // dropout probability, 1 / (1 - p)
   uint32_t seed, thr;
+  int mask_pp;  // DRELU_M: the mask was written by csrc/gemm_fused.hip's ping-pong ReLU forward (its thread layout)
 };
 
 // csrc/gemm_fused.hip: C[M][N] = epi(A[M][K] . B), B = [N][K] (b_kmajor = 0) or [K][N] (b_kmajor = 1)

@@ -264,11 +264,17 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
   unsigned char* const scr = smem + 2 * BUF + (uint32_t)w * 8192u;  // this wave's staging rows [32][256 B]
   const uint32_t scr_lds = lds_addr(smem) + 2 * BUF + (uint32_t)w * 8192u;
   const i32x4 srd_mask = make_srd(P.mask, 0xFFFFFFF0u);
+  // mask_pp: the ping-pong forward's layout (8 waves of 128x64, 16 B per thread per tile, bit 16 i + 4 j + r of its
+  // acc[i][j][r]): this thread's elements of columns 16 j, j < 4 / >= 4, belong to ping-pong wave (wm, 2 wn) /
+  // (wm, 2 wn + 1), same lane, same i — their 16-B words are DMA'd instead of this kernel's own 32 B
+  const uint32_t pp_thread = (uint32_t)((wm * 4 + 2 * wn) * 64 + lane);
   auto mask_dma = [&](int tm0, int tn0) {
     if constexpr (EPI == W4_EPI_DRELU_M) {
-      const uint32_t base = (uint32_t)(((tm0 / 256) * P.tn + tn0 / 256) * 256 + tid) * 32u;
-      dma16<0>(srd_mask, base, 0u, scr_lds);
-      dma16<1024>(srd_mask, base + 16u, 0u, scr_lds);
+      const uint32_t tile = (uint32_t)((tm0 / 256) * P.tn + tn0 / 256);
+      const uint32_t a = P.mask_pp ? (tile * 512u + pp_thread) * 16u : (tile * 256u + (uint32_t)tid) * 32u;
+      const uint32_t b = P.mask_pp ? a + 64u * 16u : a + 16u;
+      dma16<0>(srd_mask, a, 0u, scr_lds);
+      dma16<1024>(srd_mask, b, 0u, scr_lds);
     }
   };
   const uint32_t seed = (EPI == W4_EPI_RELU && P.p > 0.f) ? eff_seed(P.seed) : P.seed;
@@ -411,8 +417,17 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
         asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
         const u32x4 lo = *reinterpret_cast<const u32x4*>(scr + 16 * lane);
         const u32x4 hi = *reinterpret_cast<const u32x4*>(scr + 1024 + 16 * lane);
-        mw[0] = lo.x; mw[1] = lo.y; mw[2] = lo.z; mw[3] = lo.w;
-        mw[4] = hi.x; mw[5] = hi.y; mw[6] = hi.z; mw[7] = hi.w;
+        if (P.mask_pp) {  // word i = [ping-pong (wm, 2wn) bits 16i..16i+15 | (wm, 2wn+1) bits 16i..16i+15]
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const uint32_t a = (i >> 1) == 0 ? lo.x : (i >> 1) == 1 ? lo.y : (i >> 1) == 2 ? lo.z : lo.w;
+            const uint32_t b = (i >> 1) == 0 ? hi.x : (i >> 1) == 1 ? hi.y : (i >> 1) == 2 ? hi.z : hi.w;
+            mw[i] = (i & 1) ? ((a >> 16) | (b & 0xFFFF0000u)) : ((a & 0xFFFFu) | (b << 16));
+          }
+        } else {
+          mw[0] = lo.x; mw[1] = lo.y; mw[2] = lo.z; mw[3] = lo.w;
+          mw[4] = hi.x; mw[5] = hi.y; mw[6] = hi.z; mw[7] = hi.w;
+        }
       } else {
 #pragma unroll
         for (int i = 0; i < 8; ++i) mw[i] = 0u;

@@ -51,6 +51,9 @@ _COLSUM = os.environ.get("DLLM_FFN_BIAS_COLSUM", "1") != "0"  # 0: wi bias gradi
 # slower per t5-base step (profiles/r3_w4_ffn_ab.txt): w4's epilogue (the dropout hash of 64K elements per tile) runs
 # with the matrix cores idle, where the ping-pong kernel's second wave per SIMD keeps them busy.
 _W4_FFN = os.environ.get("DLLM_W4_FFN", "0") == "1"
+# The ReLU backward (dU = dY Wo through the forward's bit mask) on csrc/gemm_w4.hip, reading the ping-pong forward's
+# mask layout (mask_pp): 17 % faster than the ping-pong backward kernel (profiles/r3_ffn_kernel_profile.txt)
+_W4_FFN_BWD = os.environ.get("DLLM_W4_FFN_BWD", "1") != "0"
 w4_ffn_calls = 0
 fused_calls = 0  # number of FFN forwards that took the fused path (tests assert the kernel really ran)
 
@@ -121,6 +124,8 @@ class _FusedFFNFn(torch.autograd.Function):
             if not C.gemm_w4_supported(dy2, wo, True):
                 dy2 = dy2.contiguous()
             du = C.gemm_w4(dy2, wo, True, None, None, False, -1, True, 7, p, seed, mask)
+        elif mask is not None and _W4_FFN_BWD and C.gemm_w4_supported(dy2, wo, True):  # d-relu, ping-pong mask
+            du = C.gemm_w4(dy2, wo, True, None, None, False, -1, True, 7, p, seed, mask, True)
         elif mask is not None:  # d-relu from the bit mask
             du = C.gemm_fused(dy2, wo, True, 7, None, None, None, p, seed, _VARIANT, mask)
         else:

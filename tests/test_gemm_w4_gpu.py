@@ -118,3 +118,25 @@ def test_gemm_w4_relu_dropout_mask_roundtrip(M, K, N, p, bias):
     # bits agree with H wherever H is clearly away from 0 (bf16 rounding of tiny positives aside)
     far = h.float().abs() > 1e-2
     assert torch.equal((du.float() != 0)[far], live[far] & ((dy.float() @ wo.float()) != 0)[far])
+
+
+@pytest.mark.parametrize("M,K,N", [(512, 256, 512), (2048, 768, 3072), (1280, 256, 1024)])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_gemm_w4_drelu_from_pingpong_mask(M, K, N, p):
+    """The ReLU backward on w4 reading the mask written by csrc/gemm_fused.hip's ping-pong ReLU forward (its thread
+    layout, mask_pp) == the ping-pong ReLU backward on the same mask (ops/ffn.py default backward)."""
+    C = _ext.native()
+    if C.gemm_fused_variant(K) not in (8, 9):
+        pytest.skip("ping-pong kernel not chosen for this K")
+    torch.manual_seed(M + N)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    wi = (torch.randn(N, K, device=DEV) * K ** -0.5).to(torch.bfloat16)
+    mask = torch.zeros(M * N // 32, device=DEV, dtype=torch.int32)
+    h = C.gemm_fused(x, wi, False, 1, None, None, None, p, 77, -1, mask)
+    dy = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    wo = (torch.randn(K, N, device=DEV) * K ** -0.5).to(torch.bfloat16)
+    ref = C.gemm_fused(dy, wo, True, 7, None, None, None, p, 77, -1, mask)
+    got = C.gemm_w4(dy, wo, True, None, None, False, -1, True, 7, p, 77, mask, True)
+    assert _rel(got, ref) < 1e-3, _rel(got, ref)
+    exact = (dy.float() @ wo.float()) * (h.float() > 0) / (1 - p)
+    assert _rel(got, exact) < 8e-3
