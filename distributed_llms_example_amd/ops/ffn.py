@@ -52,7 +52,7 @@ _COLSUM = os.environ.get("DLLM_FFN_BIAS_COLSUM", "1") != "0"  # 0: wi bias gradi
 # with the matrix cores idle, where the ping-pong kernel's second wave per SIMD keeps them busy.
 _W4_FFN = os.environ.get("DLLM_W4_FFN", "0") == "1"
 # The ReLU backward (dU = dY Wo through the forward's bit mask) on csrc/gemm_w4.hip, reading the ping-pong forward's
-# mask layout (mask_pp): 17 % faster than the ping-pong backward kernel (profiles/r3_ffn_kernel_profile.txt)
+# mask layout (mask_pp): 17 % faster than the ping-pong backward kernel (profiles/r3_ffn_kernel_profile.txt; whole step -0.9 %, profiles/r3_w4_ffn_bwd_ab.txt)
 _W4_FFN_BWD = os.environ.get("DLLM_W4_FFN_BWD", "1") != "0"
 w4_ffn_calls = 0
 fused_calls = 0  # number of FFN forwards that took the fused path (tests assert the kernel really ran)
