@@ -741,7 +741,7 @@ Tensor gemm_w4(const Tensor& a, const Tensor& b, bool b_kmajor, const optional<T
   P.K = (int)K;
   P.tm = (int)((M + 255) / 256);
   P.tn = (int)((N + 255) / 256);
-  P.grp = grp >= 0 ? (int)grp : 4;
+  P.grp = grp >= 0 ? (int)grp : 8;  // tile-group sweep: profiles/r3_gemm_w4_grp_sweep.txt
   P.accumulate = accumulate ? 1 : 0;
   if (epi != 0) {
     TORCH_CHECK(mask.has_value() && mask->defined() && mask->is_cuda() && mask->device() == a.device() &&

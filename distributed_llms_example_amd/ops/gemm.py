@@ -26,7 +26,8 @@ from .. import _ext
 #   "auto" (default): csrc/gemm_w4.hip for input gradients whose reduction depth (the layer's output features) is
 #          <= 1024, <= 2304 with >= 128K token rows, or <= 3072 with >= 1024 output columns — there it beats
 #          hipBLASLt's NN kernels by 1-12 % (o / wo / fc2, encoder-QKV and BART-QKV dgrads, the residual-accumulating
-#          ones included); forwards and deeper dgrads stay on hipBLASLt, which is 1-10 % faster there;
+#          ones included) and the short-K wide forwards (QKV, +1-3 %); the other forwards and the deeper dgrads stay on
+#          hipBLASLt, which is 1-17 % faster there (profiles/r3_gemm_w4_grp_sweep.txt);
 #   "1": every supported shape on gemm_w4 (A/B and tests), "0": none.
 _W4_MODE = os.environ.get("DLLM_W4_GEMM", "auto")
 _W4 = _W4_MODE != "0"
@@ -38,10 +39,14 @@ colsum_handoffs = 0  # bias gradients taken from a norm backward's column sums (
 def _w4_ok(a: torch.Tensor, b: torch.Tensor, kmajor: bool) -> bool:
     if not _W4 or a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16 or not _ext.use_native(a):
         return False
-    if _W4_MODE == "auto" and not (kmajor and (a.shape[-1] <= _W4_DGRAD_MAX_K
-                                               or (a.shape[-1] <= 2304 and a.shape[0] >= 131072)
-                                               or (a.shape[-1] <= 3072 and b.shape[-1] >= 1024))):
-        return False
+    if _W4_MODE == "auto":
+        K = a.shape[-1]
+        if kmajor:  # input gradients
+            ok = K <= _W4_DGRAD_MAX_K or (K <= 2304 and a.shape[0] >= 131072) or (K <= 3072 and b.shape[-1] >= 1024)
+        else:  # forwards: short-K, wide outputs (the QKV projections)
+            ok = K <= 1024 and 2048 <= b.shape[0] <= 4096 and a.shape[0] >= 131072
+        if not ok:
+            return False
     return bool(_ext.native().gemm_w4_supported(a, b, kmajor))
 
 
