@@ -23,13 +23,18 @@ import torch.nn.functional as F
 from .. import _ext
 
 # Routing of the projection GEMMs (profiles/r3_gemm_w4_vs_hipblaslt.jsonl, t5-base / bart-large shapes):
-#   "auto" (default): csrc/gemm_w4.hip for input gradients whose reduction depth (the layer's output features) is
+#   "auto": csrc/gemm_w4.hip for input gradients whose reduction depth (the layer's output features) is
 #          <= 1024, <= 2304 with >= 128K token rows, or <= 3072 with >= 1024 output columns — there it beats
 #          hipBLASLt's NN kernels by 1-12 % (o / wo / fc2, encoder-QKV and BART-QKV dgrads, the residual-accumulating
 #          ones included) and the short-K wide forwards (QKV, +1-3 %); the other forwards and the deeper dgrads stay on
 #          hipBLASLt, which is 1-17 % faster there (profiles/r3_gemm_w4_grp_sweep.txt);
-#   "1": every supported shape on gemm_w4 (A/B and tests), "0": none.
-_W4_MODE = os.environ.get("DLLM_W4_GEMM", "auto")
+#   "1": every supported shape on gemm_w4 (A/B and tests), "0" (default): none.
+# In-situ whole-step A/B (profiles/r3_w4_routing_ab.txt) overrules the microbenchmark: with every shape above routed
+# to w4 the t5-base / bart-large steps ran 0.8-1 % SLOWER than hipBLASLt-only, although each routed shape is faster in
+# isolation (operands there sit in the caches; in the step they come from HBM, and w4's one-k-tile prefetch depth is
+# the shallower).  The default is therefore hipBLASLt for the linear projections; csrc/gemm_w4.hip keeps the shapes it
+# wins in the step: the T5 FFN ReLU input gradient (ops/ffn.py, -0.9 % step time).
+_W4_MODE = os.environ.get("DLLM_W4_GEMM", "0")
 _W4 = _W4_MODE != "0"
 _W4_DGRAD_MAX_K = 1024
 w4_calls = 0  # projections that ran on csrc/gemm_w4.hip (tests assert the kernel really ran)
