@@ -219,3 +219,59 @@ extern "C" int dllm_beam_topk(const void* logits, long ld, int is_bf16, const fl
   BeamParams p{logits, ld, beam_scores, seqs, lds, cur, ngram, ban_tok, force_tok, nb, V, k_out, top_s, top_i};
   return is_bf16 ? launch<uint16_t>(p, B, st) : launch<float>(p, B, st);
 }
+
+// ---- beam reorder of every decoder layer's self-attention cache, in place (models/generation.py KVStore)
+// cache [LK = layers * 2][rows][max_len][hd] bf16, rows = batch * nb; row r takes the live prefix (positions < n) of
+// row src[r], which always lies in r's own group of nb rows (its batch entry).  One workgroup per (lk, group): a group
+// whose hypotheses all kept their own row is skipped (no bytes move); otherwise per position the group's source rows
+// are read into registers first and only the rows that change are written — an in-place permutation inside the group,
+// no second buffer, no copy of unchanged rows (vs a gather of every row into a temporary and a copy back).
+namespace {
+__global__ __launch_bounds__(256) void kv_reorder_kernel(uint16_t* __restrict__ cache, const int64_t* __restrict__ src,
+                                                         int rows, int nb, int max_len, int hd, int n) {
+  const int lk = blockIdx.y, g = blockIdx.x;
+  const int r0 = g * nb;
+  bool moved = false;
+  for (int j = 0; j < nb; ++j) moved |= src[r0 + j] != r0 + j;
+  if (!moved) return;  // uniform: every thread read the same indices
+  const int cpr = hd / 8;  // 16-B chunks per row
+  const long rowlen = (long)max_len * hd;
+  uint16_t* base = cache + ((long)lk * rows + r0) * rowlen;
+  const int per = cpr * nb;  // chunks of one position of the group
+  for (int p = 0; p < n; ++p) {
+    // each thread moves up to 2 chunks of this position (nb * hd / 8 <= 512, host-checked)
+    u32x4 v[2];
+    int dst_row[2], chunk[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int t = threadIdx.x + 256 * u;
+      dst_row[u] = -1;
+      if (t < per) {
+        const int j = t / cpr, c = t % cpr;
+        const int s = (int)src[r0 + j] - r0;
+        chunk[u] = c;
+        if (s != j) {
+          dst_row[u] = j;
+          v[u] = *reinterpret_cast<const u32x4*>(base + s * rowlen + (long)p * hd + 8 * c);
+        }
+      }
+    }
+    __syncthreads();  // every source chunk of this position is in registers before any row of the group changes
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+      if (dst_row[u] >= 0)
+        *reinterpret_cast<u32x4*>(base + dst_row[u] * rowlen + (long)p * hd + 8 * chunk[u]) = v[u];
+    __syncthreads();
+  }
+}
+}  // namespace
+
+extern "C" int dllm_kv_reorder(void* cache, const int64_t* src, int lk, int rows, int nb, int max_len, int hd, int n,
+                               hipStream_t st) {
+  if (lk <= 0 || rows <= 0 || nb <= 0 || rows % nb || hd % 8 || (long)nb * hd / 8 > 512 || n <= 0 || n > max_len)
+    return -4;
+  hipLaunchKernelGGL(kv_reorder_kernel, dim3(rows / nb, lk), dim3(256), 0, st, (uint16_t*)cache, src, rows, nb, max_len,
+                     hd, n);
+  DLLM_CHECK_LAUNCH();
+  return 0;
+}

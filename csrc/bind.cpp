@@ -49,6 +49,7 @@ int dllm_ce_chunk_bwd(const float*, void*, long, const int64_t*, const float*, c
 int dllm_embed_bwd(const int64_t*, const int64_t*, const void*, long, long, int, float*, void*, long, long, int,
                    hipStream_t);
 int dllm_colsum_acc(const void*, long, long, int, float*, void*, int, hipStream_t);
+int dllm_kv_reorder(void*, const int64_t*, int, int, int, int, int, int, hipStream_t);
 int dllm_beam_topk(const void*, long, int, const float*, const int64_t*, long, int, int, int, int, int, int, int, int,
                    float*, int64_t*, hipStream_t);
 }
@@ -686,6 +687,18 @@ std::vector<Tensor> beam_topk(const Tensor& logits, const Tensor& beam_scores, c
   return {top_s, top_i};
 }
 
+// In-place beam reorder of a [layers * 2, rows, max_len, hd] bf16 cache's live prefix (csrc/beam.hip kv_reorder).
+void kv_reorder(Tensor& cache, const Tensor& src, int64_t nb, int64_t n) {
+  TORCH_CHECK(cache.is_cuda() && cache.scalar_type() == at::kBFloat16 && cache.is_contiguous() && cache.dim() == 4,
+              "kv_reorder: cache must be a contiguous bf16 [layers*2, rows, max_len, hd] GPU tensor");
+  TORCH_CHECK(src.is_cuda() && src.scalar_type() == at::kLong && src.is_contiguous() && src.numel() == cache.size(1),
+              "kv_reorder: src must be an int64 [rows] GPU tensor");
+  if (n <= 0) return;
+  check_rc(dllm_kv_reorder(cache.data_ptr(), src.data_ptr<int64_t>(), (int)cache.size(0), (int)cache.size(1), (int)nb,
+                           (int)cache.size(2), (int)cache.size(3), (int)n, stream()),
+           "kv_reorder");
+}
+
 bool gemm_w4_supported(const Tensor& a, const Tensor& b, bool b_kmajor) {
   auto ok2 = [](const Tensor& t) {
     return t.is_cuda() && t.dim() == 2 && t.scalar_type() == at::kBFloat16 && t.stride(1) == 1 && t.stride(0) % 8 == 0 &&
@@ -937,6 +950,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_w4_mask_words", &gemm_w4_mask_words);
   m.def("gemm_w4_supported", &gemm_w4_supported);
   m.def("beam_topk", &beam_topk);
+  m.def("kv_reorder", &kv_reorder);
   m.def("colsum_acc", &colsum_acc, "out += x.sum(0) for a token-major bf16 x (bias gradients)");
   dllm::bind_reducer(m);
   m.attr("arch") = "gfx950";

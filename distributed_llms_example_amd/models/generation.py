@@ -24,25 +24,31 @@ from ..ops.attention import relative_bias_lut  # noqa: F401  (documented depende
 
 
 class KVStore:
-    """Self-attention K/V of EVERY decoder layer in one preallocated pair of buffers [layers, 2, rows, max_len, H, D].
+    """Self-attention K/V of EVERY decoder layer in one preallocated buffer [layers * 2, rows, max_len, H * D].
 
-    A beam reorder is then ONE gather of the live prefix of all layers from the current buffer into the other (then the
-    two swap roles): 1 launch per step instead of an index_select + copy-back per layer and tensor (48 launches and
-    twice the bytes for a 12-layer decoder)."""
+    A beam reorder is ONE in-place kernel over all layers on the GPU (csrc/beam.hip ``kv_reorder``): a batch entry
+    whose hypotheses all kept their own row moves no bytes, and otherwise only the rows that change are written (the
+    group's source rows are read first).  That replaces an index_select + copy-back per layer and tensor (48 launches
+    and two full passes over the live prefix for a 12-layer decoder)."""
 
-    def __init__(self, layers: int, batch: int, max_len: int, heads: int, dim: int, dtype, device):
-        shape = (layers, 2, batch, max_len, heads, dim)
-        self.buf = [torch.empty(shape, dtype=dtype, device=device), torch.empty(shape, dtype=dtype, device=device)]
-        self.cur = 0
+    def __init__(self, layers: int, batch: int, max_len: int, heads: int, dim: int, dtype, device, nb: int = 1):
+        self.buf = torch.empty(layers * 2, batch, max_len, heads * dim, dtype=dtype, device=device)
+        self.heads, self.dim, self.nb = heads, dim, nb
         self.len = 0
         self.layers = [KVCache(self, i) for i in range(layers)]
 
     def reorder(self, idx):
         n = self.len
-        if n:
-            src, dst = self.buf[self.cur], self.buf[1 - self.cur]
-            torch.index_select(src[:, :, :, :n], 2, idx, out=dst[:, :, :, :n])
-        self.cur = 1 - self.cur
+        if not n:
+            return
+        from .. import _ext
+        hd = self.heads * self.dim
+        if (self.buf.dtype == torch.bfloat16 and _ext.use_native(self.buf) and self.nb * hd // 8 <= 512
+                and hd % 8 == 0):
+            _ext.native().kv_reorder(self.buf, idx.contiguous(), self.nb, n)
+            return
+        live = self.buf[:, :, :n]
+        live.copy_(live.index_select(1, idx))
 
 
 class KVCache:
@@ -59,13 +65,15 @@ class KVCache:
     def append(self, k, v):
         st = self.store
         s = k.shape[1]
-        b = st.buf[st.cur][self.i]
-        b[0, :, st.len:st.len + s] = k
-        b[1, :, st.len:st.len + s] = v
-        if self.i == len(st.layers) - 1:  # the last layer of the step advances the shared length
-            st.len += s
-        n = st.len if self.i == len(st.layers) - 1 else st.len + s
-        return b[0, :, :n], b[1, :, :n]
+        last = self.i == len(st.layers) - 1
+        kb = st.buf[2 * self.i].view(-1, st.buf.shape[2], st.heads, st.dim)
+        vb = st.buf[2 * self.i + 1].view(-1, st.buf.shape[2], st.heads, st.dim)
+        kb[:, st.len:st.len + s] = k
+        vb[:, st.len:st.len + s] = v
+        n = st.len + s
+        if last:  # the last layer of the step advances the shared length
+            st.len = n
+        return kb[:, :n], vb[:, :n]
 
 
 def _head_geom(model):
@@ -274,7 +282,7 @@ def generate(model, input_ids, attention_mask=None, max_length: int | None = Non
         N = B * nb
         H, D = _head_geom(model)
         dtype = next(model.parameters()).dtype
-        store = KVStore(cfg.num_decoder_layers, N, max_length, H, D, dtype, dev)
+        store = KVStore(cfg.num_decoder_layers, N, max_length, H, D, dtype, dev, nb)
         caches = store.layers
         seqs = torch.full((N, max_length), pad, dtype=torch.long, device=dev)
         seqs[:, 0] = start

@@ -96,3 +96,21 @@ def test_generation_shared_cross_kv_runs(monkeypatch):
     am[1, -17:] = 0
     out = m.generate(ids, attention_mask=am, max_length=20, num_beams=3)
     assert out.shape[0] == 5 and out.shape[1] <= 20
+
+
+@pytest.mark.parametrize("nb", [1, 2, 4])
+def test_kv_reorder_in_place_matches_gather(nb):
+    """csrc/beam.hip kv_reorder (in place, only changed rows, groups that kept their rows skipped) == a gather of the
+    live prefix; positions past the live prefix untouched."""
+    torch.manual_seed(nb)
+    L2, B, T, hd, n = 6, 37, 40, 512, 23
+    rows = B * nb
+    cache = torch.randn(L2, rows, T, hd, device="cuda").to(torch.bfloat16)
+    src = torch.arange(rows, device="cuda")
+    g = torch.randint(0, nb, (B, nb), device="cuda") + torch.arange(B, device="cuda").view(B, 1) * nb
+    keep = torch.rand(B, device="cuda") < 0.3  # some batch entries keep every hypothesis in place
+    src = torch.where(keep.view(B, 1), src.view(B, nb), g).reshape(-1).contiguous()
+    ref = cache.clone()
+    ref[:, :, :n] = cache[:, :, :n].index_select(1, src)
+    _ext.native().kv_reorder(cache, src, nb, n)
+    assert torch.equal(cache, ref)
