@@ -110,8 +110,7 @@ __global__ __launch_bounds__(256) void beam_topk_kernel(BeamParams P) {
       tv[k] = -INFINITY;
       ti[k] = 0x7FFFFFFF;
     }
-    for (int c = tid; c < V; c += 256) {
-      const float v = ld1<T>(x, c);
+    auto visit = [&](float v, int c) {
       if (v > m) {
         s = s * expf(m - v) + 1.f;
         m = v;
@@ -119,7 +118,25 @@ __global__ __launch_bounds__(256) void beam_topk_kernel(BeamParams P) {
         s += expf(v - m);
       }
       if (!bans || !((bits[c >> 5] >> (c & 31)) & 1u)) insert<K>(tv, ti, v, c);
+    };
+    // 16-B loads (8 bf16 / 4 fp32 per lane) when the row is 16-B aligned; scalar otherwise and for the tail
+    constexpr int VW = sizeof(T) == 2 ? 8 : 4;
+    const bool vec = (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+    const int vend = vec ? V / VW * VW : 0;
+    for (int c0 = tid * VW; c0 < vend; c0 += 256 * VW) {
+      const u32x4 raw = *reinterpret_cast<const u32x4*>(x + c0);
+      if constexpr (sizeof(T) == 2) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          visit(bf2f((uint16_t)(raw[e] & 0xFFFFu)), c0 + 2 * e);
+          visit(bf2f((uint16_t)(raw[e] >> 16)), c0 + 2 * e + 1);
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) visit(__uint_as_float(raw[e]), c0 + e);
+      }
     }
+    for (int c = vend + tid; c < V; c += 256) visit(ld1<T>(x, c), c);
     // block max / sum-exp
     float M = m;
 #pragma unroll
