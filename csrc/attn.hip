@@ -45,58 +45,47 @@ DLLM_SEED_STEP_TU(attn)
 namespace {
 
 // attention dropout (ops/rng.py attention_keep_mask): per query row rh = mix32(seed, row); per key pair kp = key >> 1:
-// g = ((rh + kp * HG) & 0xFFFFFF) * C24, h = ((g ^ (g >> 15)) & 0xFFFFFF) * C24B (two v_mul_u32_u24: full rate, unlike
-// the quarter-rate v_mul_lo_u32); y = h ^ (h >> 16); the even key keeps iff (y & 0xFFFF) >= thr16, the odd key iff
-// (h >> 16) >= thr16.  The second round matters: g alone is linear in kp (a Weyl sequence times a constant), so at
-// p = 0.1 two odd keys two apart were NEVER both dropped and per-row drop counts had 1/8 of the binomial variance;
-// with the xorshift + multiply every lag-1/2/3/16 joint drop rate and the row-count variance match independent
-// Bernoulli draws (tests/test_training_cpu.py test_attention_dropout_hash_statistics).
+// g = (rh & 0xFFFFFF) * C24 + kp * HG (mod 2^32: a Weyl sequence along the row, so a kernel adds one constant per
+// pair to a per-tile base), h = ((g ^ (g >> 15)) & 0xFFFFFF) * C24B (full-rate v_mul_u32_u24), y = h ^ (h >> 16);
+// the even key keeps iff ((y & 0xFFFF) ^ 0x8000) >= thr16, the odd key iff ((y >> 16) ^ 0x8000) >= thr16.  The
+// xorshift + multiply round matters: g alone is linear in kp and leaves lag-2 drops anti-correlated; with it every
+// lag-1/2/3/16 joint drop rate and the row-count variance match independent Bernoulli draws
+// (tests/test_training_cpu.py test_attention_dropout_hash_statistics).  The top-bit flip makes the compare a signed
+// 16-bit one, which the kernels do on both keys of a pair at once (drop_mask2).
 constexpr uint32_t C24 = 0x9E3779u, C24B = 0x85EBCBu;
-DLLM_DEVICE uint32_t attn_pair_hash(uint32_t x) {
-  const uint32_t g = __umul24(x, C24);
-  return __umul24(g ^ (g >> 15), C24B);
+DLLM_DEVICE uint32_t pair_y(uint32_t g) {
+  const uint32_t h = __umul24(g ^ (g >> 15), C24B);
+  return h ^ (h >> 16);
+}
+// per-lane, per-tile start of the Weyl sequence: g of pair kp0 + j is gbase + j * HG
+DLLM_DEVICE uint32_t pair_gbase(uint32_t rh, uint32_t kp0) { return __umul24(rh, C24) + kp0 * HG; }
+// t2 = (thr16 - 0x8000) in both 16-bit halves.  Returns the pair's DROP mask: 0xFFFF in the half of each dropped key
+// (low half = even key, high half = odd key): saturating signed difference, then its sign spread over the half.
+DLLM_DEVICE uint32_t drop_mask2(uint32_t y, uint32_t t2) {
+  uint32_t d, m;
+  asm("v_pk_sub_i16 %0, %1, %2 clamp" : "=v"(d) : "v"(y), "s"(t2));
+  asm("v_pk_ashrrev_i16 %0, %1, %2" : "=v"(m) : "s"(0x000F000Fu), "v"(d));  // shift count per half (an inline 15
+                                                                            // would shift the high half by 0)
+  return m;
 }
 
-// Two key pairs (A, then B) of the forward's dropout: the four keep compares write SGPR-pair lane masks, then per key
-// one v_cndmask zeroes P and one v_addc_co_u32 shifts the keep bit into the word (word = 2 word + keep), odd key first
-// within a pair.  Compares and their consumers sit in ONE statement, each mask read >= 3 instructions after its
-// write (a VALU-written SGPR read as a lane mask needs wait states hipcc does not insert around inline asm).  The
-// compiler's select + or form of the same costs 4 instructions per pair more.
-DLLM_DEVICE void keep_pairs2(uint32_t& word, float& a_odd, float& a_even, float& b_odd, float& b_even, uint32_t ha,
-                             uint32_t ya, uint32_t hb, uint32_t yb, uint32_t thr_hi, uint32_t thr16) {
-  uint64_t m0, m1, m2, m3, co;
-  asm volatile(
-      "v_cmp_le_u32_e64 %[m0], %[thi], %[ha]\n\t"
-      "v_cmp_le_u32_e64 %[m1], %[t16], %[ya]\n\t"
-      "v_cmp_le_u32_e64 %[m2], %[thi], %[hb]\n\t"
-      "v_cmp_le_u32_e64 %[m3], %[t16], %[yb]\n\t"
-      "v_cndmask_b32_e64 %[ao], 0, %[ao], %[m0]\n\t"
-      "v_addc_co_u32_e64 %[w], %[co], %[w], %[w], %[m0]\n\t"
-      "v_cndmask_b32_e64 %[ae], 0, %[ae], %[m1]\n\t"
-      "v_addc_co_u32_e64 %[w], %[co], %[w], %[w], %[m1]\n\t"
-      "v_cndmask_b32_e64 %[bo], 0, %[bo], %[m2]\n\t"
-      "v_addc_co_u32_e64 %[w], %[co], %[w], %[w], %[m2]\n\t"
-      "v_cndmask_b32_e64 %[be], 0, %[be], %[m3]\n\t"
-      "v_addc_co_u32_e64 %[w], %[co], %[w], %[w], %[m3]"
-      : [ao] "+v"(a_odd), [ae] "+v"(a_even), [bo] "+v"(b_odd), [be] "+v"(b_even), [w] "+v"(word), [m0] "=&s"(m0),
-        [m1] "=&s"(m1), [m2] "=&s"(m2), [m3] "=&s"(m3), [co] "=&s"(co)
-      : [thi] "s"(thr_hi), [t16] "s"(thr16), [ha] "v"(ha), [ya] "v"(ya), [hb] "v"(hb), [yb] "v"(yb));
-}
+// Keep-word layout of one (row, 64-key tile, lane half) — shared by the forward and both backward kernels: the lane's
+// 16 key pairs are slots p = 0..15, pair slot p of accumulator register i of s0 (t = 0) or s1 (t = 1) being
+// p = 8 t + (i >> 1) (the key pair kbase + 32 t + crow(i & ~1, hh) .. + 1); the even key's bit is p, the odd key's 16 + p.
+DLLM_DEVICE constexpr int keep_bit(int t, int i) { return ((i & 1) << 4) + 8 * t + (i >> 1); }
+DLLM_DEVICE uint32_t pair_slot_kp(int p) { return (uint32_t)((p & 1) + 4 * ((p & 7) >> 1) + 16 * (p >> 3)); }
 
-// Dropout keep bits of one (row, 64-key tile, lane half): bit i <-> key kbase + crow(i, hh) (the forward's
-// s0[i]), bit 16 + i <-> key kbase + 32 + crow(i, hh) (s1[i]); one hash per adjacent key pair (ops/rng.py).
+// Dropout keep word of one (row, 64-key tile, lane half) in the keep_bit layout (ops/rng.py mirrors the decisions).
 DLLM_DEVICE uint32_t dropout_word(uint32_t rh, int kbase, int hh, uint32_t thr) {
-  const uint32_t base = rh + ((uint32_t)(kbase >> 1) + 2u * (uint32_t)hh) * HG;
-  uint32_t word = 0;
+  const uint32_t gbase = pair_gbase(rh, (uint32_t)(kbase >> 1) + 2u * (uint32_t)hh);
+  const uint32_t t2 = ((thr - 0x8000u) & 0xFFFFu) * 0x10001u;
+  uint32_t drop = 0;
 #pragma unroll
-  for (int i = 0; i < 16; i += 2) {
-    const uint32_t pair = (uint32_t)(((i & 3) >> 1) + 4 * (i >> 2));
-    const uint32_t h0 = attn_pair_hash(base + pair * HG), h1 = attn_pair_hash(base + (pair + 16u) * HG);  // keys + 32
-    const uint32_t y0 = h0 ^ (h0 >> 16), y1 = h1 ^ (h1 >> 16);
-    word |= ((y0 & 0xFFFFu) >= thr ? 1u << i : 0u) | ((h0 >> 16) >= thr ? 2u << i : 0u) |
-            ((y1 & 0xFFFFu) >= thr ? 0x10000u << i : 0u) | ((h1 >> 16) >= thr ? 0x20000u << i : 0u);
+  for (int p = 0; p < 16; ++p) {
+    const uint32_t m = drop_mask2(pair_y(gbase + pair_slot_kp(p) * HG), t2);
+    drop |= (m & ((1u << p) | (0x10000u << p)));
   }
-  return word;
+  return ~drop;
 }
 
 // ================================================================================== dropout bit planes
@@ -210,6 +199,7 @@ __global__ __launch_bounds__(256, FNB == 3 ? 2 : 3) void attn_fwd_kernel(AttnPar
   const long row_g = (long)(b * P.H + h) * P.Sq + qrow;
   const uint32_t rh = DROP ? mix32(eff_seed(P.seed), (uint32_t)row_g) : 0u;
   const float dscale = DROP ? 1.f / (1.f - P.p_drop) : 1.f;
+  const uint32_t t2drop = ((P.thr - 0x8000u) & 0xFFFFu) * 0x10001u;  // drop_mask2 threshold pair
 
   for (int t = w; t < ntiles; t += 4) {  // wave-per-tile: per-key mask + "tile has a masked key" flag
     const int j = t * FWD_BN + lane;
@@ -329,47 +319,42 @@ __global__ __launch_bounds__(256, FNB == 3 ? 2 : 3) void attn_fwd_kernel(AttnPar
     if (DROP && DROP_IN) {  // precomputed keep bits; the 1/(1-p) scale is applied once to O at the end
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        s0[i] = __uint_as_float(__float_as_uint(s0[i]) & (uint32_t)__builtin_amdgcn_sbfe((int)mword, i, 1));
-        s1[i] = __uint_as_float(__float_as_uint(s1[i]) & (uint32_t)__builtin_amdgcn_sbfe((int)mword, 16 + i, 1));
+        s0[i] = __uint_as_float(__float_as_uint(s0[i]) & (uint32_t)__builtin_amdgcn_sbfe((int)mword, keep_bit(0, i), 1));
+        s1[i] = __uint_as_float(__float_as_uint(s1[i]) & (uint32_t)__builtin_amdgcn_sbfe((int)mword, keep_bit(1, i), 1));
       }
-    } else if (DROP) {
-      // keep decisions -> P (the 1/(1-p) scale is applied once to O at the end) and one bit word per lane and
-      // tile for the backward kernels (bit i <-> s0[i], bit 16+i <-> s1[i]): they never re-hash.  Per key pair
-      // one add, two full-rate 24-bit multiplies and two shift-xors (attn_pair_hash); each compare's lane mask drives
-      // both the select that zeroes P and a carry-in add that shifts the bit into the word (s1[15] first, so it
-      // ends at bit 31).
-      const uint32_t base = rh + ((uint32_t)(kbase >> 1) + 2u * (uint32_t)hh) * HG;
-      const uint32_t thr_hi = P.thr << 16;
-      uint32_t word = 0;
+    }
+    // P as bf16 pairs: pk[2 t + half] holds registers 8 half .. 8 half + 7 of s_t; its dword j is one adjacent key pair,
+    // pair slot 4 (2 t + half) + j of the keep_bit layout
+    bf16x8v pk[4] = {pack8(s0, 0), pack8(s0, 8), pack8(s1, 0), pack8(s1, 8)};
+    if (DROP && !DROP_IN) {
+      // keep decisions applied to the packed pairs (the 1/(1-p) scale is applied once to O at the end) and recorded as
+      // one bit word per lane and tile for the backward kernels, which never re-hash.  Per key pair: one add (the
+      // Weyl step is a constant), two 24-bit multiplies, two shift-xors, the two-key signed compare (drop_mask2: 2),
+      // one bitwise op zeroing the dropped halves and one recording them — 10 VALU per two keys.
+      const uint32_t gbase = pair_gbase(rh, (uint32_t)(kbase >> 1) + 2u * (uint32_t)hh);
+      uint32_t drop = 0;
 #pragma unroll
-      for (int t = 1; t >= 0; --t) {
-        f32x16& sv = t == 0 ? s0 : s1;
+      for (int q = 0; q < 4; ++q) {
+        u32x4 v = __builtin_bit_cast(u32x4, pk[q]);
 #pragma unroll
-        for (int i = 14; i >= 0; i -= 4) {  // pairs (i, i + 1) then (i - 2, i - 1)
-          const uint32_t pa = (uint32_t)(((i & 3) >> 1) + 4 * (i >> 2) + 16 * t);  // (key - kbase - 4hh) / 2
-          const uint32_t pb = (uint32_t)((((i - 2) & 3) >> 1) + 4 * ((i - 2) >> 2) + 16 * t);
-          const uint32_t ha = attn_pair_hash(base + pa * HG), hb = attn_pair_hash(base + pb * HG);
-          const uint32_t ya = (ha ^ (ha >> 16)) & 0xFFFFu, yb = (hb ^ (hb >> 16)) & 0xFFFFu;
-          float ao = sv[i + 1], ae = sv[i], bo = sv[i - 1], be = sv[i - 2];
-          keep_pairs2(word, ao, ae, bo, be, ha, ya, hb, yb, thr_hi, P.thr);
-          sv[i + 1] = ao;
-          sv[i] = ae;
-          sv[i - 1] = bo;
-          sv[i - 2] = be;
+        for (int j = 0; j < 4; ++j) {
+          const int p = 4 * q + j;
+          const uint32_t m = drop_mask2(pair_y(gbase + pair_slot_kp(p) * HG), t2drop);
+          v[j] &= ~m;
+          drop |= m & ((1u << p) | (0x10000u << p));
         }
+        pk[q] = __builtin_bit_cast(bf16x8v, v);
       }
-      P.dmask[((long)bh * P.n_ktiles * 2 + 2 * kt + hh) * P.sq_pad + qrow] = word;
+      P.dmask[((long)bh * P.n_ktiles * 2 + 2 * kt + hh) * P.sq_pad + qrow] = ~drop;
     }
     // O^T += V^T P^T
-    const bf16x8v pa0 = pack8(s0, 0), pa1 = pack8(s0, 8), pb0 = pack8(s1, 0), pb1 = pack8(s1, 8);
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
       for (int sp = 0; sp < 2; ++sp) {
         const int kb0 = kb * 32 + 16 * sp + 4 * hh;
-        const bf16x8v pf = kb == 0 ? (sp == 0 ? pa0 : pa1) : (sp == 0 ? pb0 : pb1);
-        o0 = mfma32(ld_tr_operand(Vb, kb0, 0, r), pf, o0);
-        o1 = mfma32(ld_tr_operand(Vb, kb0, 1, r), pf, o1);
+        o0 = mfma32(ld_tr_operand(Vb, kb0, 0, r), pk[2 * kb + sp], o0);
+        o1 = mfma32(ld_tr_operand(Vb, kb0, 1, r), pk[2 * kb + sp], o1);
       }
     }
   };
@@ -539,7 +524,7 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dq_kernel(AttnParams P) {
     const unsigned long long m = __ballot(!ok);
     if (lane == 0) tflag[t] = m == 0ull ? 0 : (~m == 0ull ? 2 : 1);  // 2: every key masked -> tile skipped
   }
-  // dropout decisions: the bit words the forward stored (bit i <-> s0[i], bit 16+i <-> s1[i])
+  // dropout decisions: the bit words the forward stored (keep_bit layout: register i of key half kb -> keep_bit(kb, i))
   const uint32_t* mrow = DROP ? P.dmask + ((long)bh * P.n_ktiles * 2 + hh) * P.sq_pad + qrow : nullptr;
   const uint32_t dsbits = __float_as_uint(dscale);
   uint32_t mword = 0, mnext = 0;
@@ -606,7 +591,7 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dq_kernel(AttnParams P) {
         const float pr = fast_exp2(sv[i]);  // lse = +inf for rows >= Sq -> 0
         float kf = 1.f;
         if (DROP)  // sign-extended bit -> all-ones mask -> dscale or 0.0f
-          kf = __uint_as_float((uint32_t)__builtin_amdgcn_sbfe((int)mword, 16 * kb + i, 1) & dsbits);
+          kf = __uint_as_float((uint32_t)__builtin_amdgcn_sbfe((int)mword, keep_bit(kb, i), 1) & dsbits);
         sv[i] = pr * fmaf(pv[i], kf, -delta);
       }
       // dQ^T += K^T dS^T over this half's 32 keys
@@ -704,7 +689,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnParams P) {
   // this lane's dropout bit: the forward's lane (hh_f) and register (bit) that held (q, key)
   const int kl = key - k0, kc = kl & 31;
   const int mcol = (kl >> 6) * 2 + ((kc >> 2) & 1);
-  const int mbit = (kc & 3) + 4 * (kc >> 3) + 16 * ((kl >> 5) & 1);
+  const int mbit = keep_bit((kl >> 5) & 1, (kc & 3) + 4 * (kc >> 3));
   const float dscale = DROP ? 1.f / (1.f - P.p_drop) : 1.f;
   const uint32_t dsbits = __float_as_uint(dscale);
   int qt_begin = 0;
@@ -1000,7 +985,7 @@ __global__ __launch_bounds__(256, NB == 3 ? 2 : 3) void attn_bwd_dkdv2_kernel(At
   // this lane's dropout bit: the forward's lane (hh_f) and register (bit) that held (q, key)
   const int kl = key - k0, kc = kl & 31;
   const int mcol = (kl >> 6) * 2 + ((kc >> 2) & 1);
-  const int mbit = (kc & 3) + 4 * (kc >> 3) + 16 * ((kl >> 5) & 1);
+  const int mbit = keep_bit((kl >> 5) & 1, (kc & 3) + 4 * (kc >> 3));
   const float dscale = DROP ? 1.f / (1.f - P.p_drop) : 1.f;
   const uint32_t dsbits = __float_as_uint(dscale);
 

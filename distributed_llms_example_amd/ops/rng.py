@@ -55,21 +55,22 @@ _C24B = 0x85EBCB
 
 
 def attention_keep_mask(seed: int, p: float, B: int, H: int, Sq: int, Sk: int, device) -> torch.Tensor:
-    """Attention-probability mask [B, H, Sq, Sk] (mirrors csrc/attn.hip ``attn_pair_hash``).
+    """Attention-probability mask [B, H, Sq, Sk] (mirrors csrc/attn.hip ``pair_gbase`` / ``pair_y`` / ``drop_mask2``).
 
-    Per query row ``r = (b*H + h)*Sq + i``: ``rh = mix32(seed, r)`` (computed once per row in the
-    kernels); per key pair ``kp = j >> 1``: ``g = ((rh + kp*G) & 0xFFFFFF) * C24``,
-    ``h = ((g ^ (g >> 15)) & 0xFFFFFF) * C24B`` (mod 2^32 — two full-rate 24-bit multiplies per two keys inside the
-    attention kernels; ``g`` alone is linear in ``kp`` and leaves lag-2 drops anti-correlated), ``y = h ^ (h >> 16)``;
-    the even key keeps iff ``y & 0xFFFF >= threshold16(p)``, the odd key iff ``h >> 16 >= threshold16(p)``."""
+    Per query row ``r = (b*H + h)*Sq + i``: ``rh = mix32(seed, r)`` (computed once per row in the kernels); per key
+    pair ``kp = j >> 1``: ``g = (rh & 0xFFFFFF) * C24 + kp * G`` (mod 2^32: a Weyl sequence along the row, one add per
+    pair in the kernels), ``h = ((g ^ (g >> 15)) & 0xFFFFFF) * C24B`` (the xorshift + multiply round: ``g`` alone is
+    linear in ``kp`` and leaves lag-2 drops anti-correlated), ``y = h ^ (h >> 16)``; the even key keeps iff
+    ``(y & 0xFFFF) ^ 0x8000 >= threshold16(p)``, the odd key iff ``(y >> 16) ^ 0x8000 >= threshold16(p)`` (the
+    kernels compare both halves at once as signed 16-bit values)."""
     rows = torch.arange(B * H * Sq, device=device, dtype=torch.int64)
     rh = mix32(effective_seed(seed), rows).view(B, H, Sq, 1)
     j = torch.arange(Sk, device=device, dtype=torch.int64).view(1, 1, 1, Sk)
-    x = (rh + (j >> 1) * _G) & 0xFFFFFF
-    g = (x * _C24) & _MASK
+    g = ((rh & 0xFFFFFF) * _C24 + (j >> 1) * _G) & _MASK
     h = (((g ^ (g >> 15)) & 0xFFFFFF) * _C24B) & _MASK
-    half = torch.where((j & 1) == 1, h >> 16, (h ^ (h >> 16)) & 0xFFFF)
-    return half >= threshold16(p)
+    y = h ^ (h >> 16)
+    half = torch.where((j & 1) == 1, y >> 16, y & 0xFFFF)
+    return (half ^ 0x8000) >= threshold16(p)
 
 
 def mix_host(seed: int, idx: int) -> int:
