@@ -1222,9 +1222,16 @@ void launch_bwd_dkdv2_t(const AttnParams& p, int nblk, size_t lds, hipStream_t s
     return e != nullptr ? atoi(e) : 3;
   }();
   const size_t lds2 = lds - K2_STAGE;  // lds was sized for the 3-deep ring
-  // bias- and dropout-free variants only: they fit 168 VGPRs without spills (BART-large shapes: bwd -4..6 %, bench
-  // +0.8 %, profiles/r2_attn_dkdv_occ3.txt); the dropout variant spills and measured 2 % slower
-  if (occ == 3 && !HB && !DR && 3 * lds2 <= 160 * 1024) {
+  static const int occ_dr = [] {
+    const char* e = getenv("DLLM_ATTN_DKDV_OCC_DR");
+    return e != nullptr ? atoi(e) : 1;
+  }();
+  // bias- and dropout-free variants: they fit 168 VGPRs without spills (BART-large shapes: bwd -4..6 %, bench
+  // +0.8 %, profiles/r2_attn_dkdv_occ3.txt).  The dropout variant spills (7 VGPRs bias-free) and measured 2 % slower on
+  // self-attention, but short-query (Sq <= 256) bias-free calls — T5 cross-attention, two 64-row stages per key block,
+  // prologue-latency bound — gain from the third workgroup: step -0.5 % (profiles/r3_cross_dkdv_occ3_ab.txt);
+  // DLLM_ATTN_DKDV_OCC_DR=0 turns that off
+  if (occ == 3 && !HB && (!DR || (occ_dr == 1 && p.Sq <= 256)) && 3 * lds2 <= 160 * 1024) {
     hipLaunchKernelGGL((attn_bwd_dkdv2_kernel<HB, HK, CA, DR, 2>), dim3(nblk), dim3(256), lds2, st, p);
     return;
   }
