@@ -34,4 +34,8 @@ for k, d in acc.items():
     for c, v in sorted(d.items()): print("   %-24s %16.1f" % (c, v))
 EOF
 done
+
+# keep only the summaries (the rocpd databases can exceed the copy-back cap)
+for p in pmc1 pmc2; do f=$(find $O/$p -name "*.db" | head -n 1); [ -n "$f" ] && python tools/pmc_summary.py $f > $O/${p}_summary.txt; done
+find $O -name "*.db" -delete
 exit 0
