@@ -81,7 +81,13 @@ DLLM_DEVICE bf16x8v frag16(const uint16_t* T, int kk, int cb, int lane) {
 // same cycles per FLOP as 32x32x16, higher sustained clock on random data (MI355X_MICROARCH.md "DVFS give-back" 7)
 // PRE (16x16, BK = 64): both 32-deep k-steps' fragments are read before the first MFMA of a stage.  Not used:
 // with both operands on transposed reads it needs > 256 VGPRs and spills (2x slower, r1_gemm_wgrad_bench_v4).
-template <int BK, int NBUF, bool PRIO, int NI, int MF = 32, bool PRE = false>
+// PP (16x16, BK = 32, NBUF = 4): the two wave groups (wm = 0 / 1: one wave of each on every SIMD) run one stage apart —
+// group 1 passes one extra barrier first — so on each SIMD one wave is in its MFMA block while the other is at the start
+// of its stage (barrier, LDS reads, waits) instead of both stalling there together (cdna_hip_programming.md, the 256^2
+// template's staggered wave groups).  Every global barrier g: each wave first waits for its own DMA of stage g (stage g + 1
+// may stay in flight), then issues stage g + 2 into the buffer of stage g - 2, which group 0 finished before barrier
+// g - 1 and group 1 before barrier g; group 0 computes stage g, group 1 stage g - 1; barriers 0 .. nk for both.
+template <int BK, int NBUF, bool PRIO, int NI, int MF = 32, bool PRE = false, bool PP = false>
 __global__ __launch_bounds__((256 / (32 * NI)) * 2 * 64, 1) void gemm_wgrad_kernel(GemmWgradParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint16_t* lds = reinterpret_cast<uint16_t*>(smem);  // [NBUF][A tile | B tile], each [BK][256]
@@ -128,7 +134,7 @@ __global__ __launch_bounds__((256 / (32 * NI)) * 2 * 64, 1) void gemm_wgrad_kern
   };
 
 #pragma unroll
-  for (int p = 0; p < NBUF - 1; ++p)
+  for (int p = 0; p < (PP ? 2 : NBUF - 1); ++p)
     if (p < nk) issue(p, p);
 
   auto stage_sync = [&](int it) {
@@ -151,8 +157,7 @@ __global__ __launch_bounds__((256 / (32 * NI)) * 2 * 64, 1) void gemm_wgrad_kern
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int it = 0; it < nk; ++it) {
-      stage_sync(it);
+    auto stage_compute = [&](int it) __attribute__((always_inline)) {
       const uint16_t* As = lds + (it % NBUF) * 2 * TILE;
       const uint16_t* Bs = As + TILE;
       auto load_k = [&](int kk, bf16x8v (&a)[8], bf16x8v (&b)[4]) {
@@ -183,6 +188,23 @@ __global__ __launch_bounds__((256 / (32 * NI)) * 2 * 64, 1) void gemm_wgrad_kern
           load_k(32 * ks, a, b);
           mfma_block(a, b);
         }
+      }
+    };
+    if constexpr (PP) {
+      static_assert(BK == 32 && NBUF == 4, "staggered groups: one k-step per stage, 4-slot ring");
+      const int grp = __builtin_amdgcn_readfirstlane(wm);
+      for (int g = 0; g <= nk; ++g) {
+        if (g + 1 < nk) wait_vm<LPS>();  // stage g landed; stage g + 1 may stay in flight
+        else wait_vm<0>();
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if (g + 2 < nk) issue((g + 2) % NBUF, g + 2);
+        const int st = g - grp;
+        if (st >= 0 && st < nk) stage_compute(st);
+      }
+    } else {
+      for (int it = 0; it < nk; ++it) {
+        stage_sync(it);
+        stage_compute(it);
       }
     }
     // acc[i][j][0..3] = C[m0 + wm*128 + 16i + (lane & 15)][n0 + wn*64 + 16j + 4 (lane >> 4) + 0..3]
@@ -330,18 +352,18 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   }
 }
 
-template <int BK, int NBUF, bool PRIO = false, int NI = 2, int MF = 32, bool PRE = false>
+template <int BK, int NBUF, bool PRIO = false, int NI = 2, int MF = 32, bool PRE = false, bool PP = false>
 int launch_wgrad(const GemmWgradParams& p, hipStream_t st) {
   constexpr int threads = (256 / (32 * NI)) * 2 * 64;
   const size_t lds = (size_t)NBUF * 2 * BK * 256 * 2;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_wgrad_kernel<BK, NBUF, PRIO, NI, MF, PRE>,
+    (void)hipFuncSetAttribute((const void*)gemm_wgrad_kernel<BK, NBUF, PRIO, NI, MF, PRE, PP>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
   const int nblk = p.ntiles * p.splits;
-  hipLaunchKernelGGL((gemm_wgrad_kernel<BK, NBUF, PRIO, NI, MF, PRE>), dim3(nblk), dim3(threads), lds, st, p);
+  hipLaunchKernelGGL((gemm_wgrad_kernel<BK, NBUF, PRIO, NI, MF, PRE, PP>), dim3(nblk), dim3(threads), lds, st, p);
   DLLM_CHECK_LAUNCH();
   if (p.splits > 1) {
     const long n8 = (long)p.M * p.N / 8;
@@ -364,7 +386,7 @@ extern "C" int dllm_gemm_wgrad_bk() { return 64; }
 // variant: 0 = BK64 x 2 stages (128 KB LDS), 1 = BK32 x 4 stages (128 KB), 2 = BK32 x 3 stages (96 KB),
 // 3 / 4 = variants 0 / 1 with s_setprio raised around the MFMA block,
 // 5 / 6 = variants 0 / 1 with 4 waves of 128x128 (one wave per SIMD, accumulators in AGPRs),
-// 7 / 8 / 9 = variants 0 / 4 / 3 on v_mfma_f32_16x16x32_bf16
+// 7 / 8 / 9 = variants 0 / 4 / 3 on v_mfma_f32_16x16x32_bf16, 10 = variant 8 with staggered wave groups (PP)
 extern "C" int dllm_gemm_wgrad(const GemmWgradParams* pp, int variant, hipStream_t st) {
   const GemmWgradParams& p = *pp;
   if (p.M % 8 || p.M < 8 || p.N % BN || p.K <= 0 || p.splits < 1 || p.ntiles != ((p.M + BM - 1) / BM) * (p.N / BN))
@@ -381,6 +403,7 @@ extern "C" int dllm_gemm_wgrad(const GemmWgradParams* pp, int variant, hipStream
     case 7: return launch_wgrad<64, 2, false, 2, 16>(p, st);
     case 8: return launch_wgrad<32, 4, true, 2, 16>(p, st);
     case 9: return launch_wgrad<64, 2, true, 2, 16>(p, st);
+    case 10: return launch_wgrad<32, 4, true, 2, 16, false, true>(p, st);
     default: return launch_wgrad<64, 2>(p, st);
   }
 }
