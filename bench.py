@@ -53,10 +53,12 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--model", default="t5-base")
-    ap.add_argument("--batch-per-gpu", type=int, default=int(os.environ.get("DLLM_BENCH_BATCH", "256")),
-                    help="per-GPU micro-batch, sized for the 288 GB HBM (256: 95 GB, +1.9 %% samples/s over 128 in an "
-                         "interleaved A/B, profiles/r2_bench_batch_ab.txt; 128: +5.6 %% over 64).  The HF comparator "
-                         "was measured at 16/32/64/128 — it needs 262 GB at 128, so 128 is its largest batch")
+    ap.add_argument("--batch-per-gpu", type=int,
+                    default=int(os.environ["DLLM_BENCH_BATCH"]) if "DLLM_BENCH_BATCH" in os.environ else None,
+                    help="per-GPU micro-batch, sized for the 288 GB HBM.  Default: t5-base 512 (182 GB, +1.0 %% "
+                         "samples/s over 256 in an interleaved sweep, profiles/r3_bench_batch_sweep.txt; 256: +1.9 %% over "
+                         "128, profiles/r2_bench_batch_ab.txt), other models 256.  The HF comparator was measured at "
+                         "16/32/64/128 — it needs 262 GB at 128, so 128 is its largest batch")
     ap.add_argument("--src-len", type=int, default=1024)
     ap.add_argument("--tgt-len", type=int, default=128)
     ap.add_argument("--bucket-mb", type=float, default=None)
@@ -77,6 +79,8 @@ def parse():
     a = ap.parse_args()
     if a.comm_stress and "--batch-per-gpu" not in " ".join(sys.argv):
         a.batch_per_gpu = 8
+    if a.batch_per_gpu is None:
+        a.batch_per_gpu = 512 if a.model == "t5-base" else 256
     return a
 
 
