@@ -1096,21 +1096,29 @@ __global__ __launch_bounds__(256, NB == 3 ? 2 : 3) void attn_bwd_dkdv2_kernel(At
         else sat_acc_hi += t;
       } else if (HAS_BIAS) {
         // diagonal sums of the wave's 32x32 dS tile: rotate register i (row rho = crow(i, hh)) left by rho
-        // lanes so lane r receives element (rho, (r + rho) & 31) whose diagonal (col - row) is r or r - 32
-        float pos = 0.f, neg = 0.f;
+        // lanes so lane r receives element (rho, (r + rho) & 31) whose diagonal (col - row) is r or r - 32.
+        // The rotations go out in batches of 8 before any is consumed (one LDS round trip per batch: issued one by one,
+        // hipcc waited on each), the wrapped part is split off by one select per register (tot / neg), and the two sums
+        // leave by one LDS atomic per lane, no divergent branch: lanes 0-31 add diagonal r, lanes 32-63 diagonal r - 32.
+        const int rb = r + 4 * hh;  // r + rho = rb + crow(i, 0)
+        float tot = 0.f, neg = 0.f;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int rho = crow(i, hh);
-          const float v = __shfl(ds[i], ((r + rho) & 31) + 32 * hh, 64);
-          if (r + rho < 32) pos += v; else neg += v;
+        for (int i0 = 0; i0 < 16; i0 += 8) {
+          float v[8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) v[i] = __shfl(ds[i0 + i], ((rb + crow(i0 + i, 0)) & 31) + 32 * hh, 64);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            tot += v[i];
+            neg += rb + crow(i0 + i, 0) < 32 ? 0.f : v[i];
+          }
         }
-        pos += __shfl_xor(pos, 32, 64);
+        tot += __shfl_xor(tot, 32, 64);
         neg += __shfl_xor(neg, 32, 64);
-        if (hh == 0) {
-          const int li = w * 32 + r - q0 + P.Sq - 1;
-          atomicAdd(&dlut_s[li], pos);
-          if (li >= 32) atomicAdd(&dlut_s[li - 32], neg);
-        }
+        const int li = w * 32 + r - q0 + P.Sq - 1;
+        const int la = hh == 0 ? li : li - 32;
+        const float va = hh == 0 ? tot - neg : (li >= 32 ? neg : 0.f);
+        atomicAdd(&dlut_s[la < 0 ? 0 : la], va);  // la < 0: rows past Sq only (dS = 0)
       }
       const bf16x8v pf0 = pack8(pd, 0), pf1 = pack8(pd, 8), sf0 = pack8(ds, 0), sf1 = pack8(ds, 8);
 #pragma unroll

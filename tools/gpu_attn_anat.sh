@@ -7,15 +7,9 @@ mkdir -p $O
 for tag in sat nosat; do
   extra=""; [ $tag = nosat ] && extra="--nosat"
   d=$O/prof_$tag
-  timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $d -o run -- python tools/attn_anat.py $extra > $O/$tag.log 2>&1 || { tail -5 $O/$tag.log; exit 1; }
-  csv=$(find $d -name "*kernel_stats.csv" | head -n 1)
-  echo "== $tag"; python - "$csv" <<'EOF'
-import csv, sys
-rows = list(csv.DictReader(open(sys.argv[1])))
-for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"])):
-    if "attn" in r["Name"]:
-        print("%9.1f us avg  %4s calls  %s" % (float(r["AverageNs"]) / 1e3, r["Calls"], r["Name"][:110]))
-EOF
+  timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $d -o run -- python tools/attn_anat.py --cfg b1k1d1,b0k1d1,b1k1d0,b0k1d0,b1k0d0,b0k0d0 $extra > $O/$tag.log 2>&1 || { tail -5 $O/$tag.log; exit 1; }
+  db=$(find $d -name "*.db" | head -n 1)
+  echo "== $tag"; python tools/prof_summary.py "$db" 1 | grep attn_ | grep "avg" || true
 done
 echo "== pmc dkdv (b1k1d1)"
 timeout -s KILL 90 rocprofv3 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_INSTS_SALU -d $O/pmc1 -o run -- python tools/attn_anat.py --cfg b1k1d1,b0k0d0 --iters 3 > $O/pmc1.log 2>&1 || { tail -5 $O/pmc1.log; exit 1; }
