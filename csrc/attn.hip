@@ -1042,7 +1042,13 @@ __global__ __launch_bounds__(256, NB == 3 ? 2 : 3) void attn_bwd_dkdv2_kernel(At
         if (use_lut) {  // bias per (key - row) from the reversed LUT: immediate ds_read offsets per register
           const float* lrow_t = lut_r + (win - 1 - (key - q0 - 4 * hh + P.Sq - 1 - k0));
 #pragma unroll
-          for (int i = 0; i < 16; ++i) rt[i] += lrow_t[crow(i, 0)];
+          for (int i0 = 0; i0 < 16; i0 += 8) {  // 8 reads in flight per batch (hipcc otherwise waits on each in turn)
+            float lv[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) lv[i] = lrow_t[crow(i0 + i, 0)];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) rt[i0 + i] += lv[i];
+          }
         }
         if (block_masked) {  // padding / tail keys: -inf on the lane's whole column
 #pragma unroll
