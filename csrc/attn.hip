@@ -877,6 +877,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnParams P) {
 // and on the per-score lse / delta arithmetic half the time, profiles/r1_attn_pmc.txt).  Per score (saturated /
 // bias-free tile): P = exp2(fma(s, sl2, rt)), keep = sbfe & dscale bits, Pd = P keep, dS = P fma(dP, keep, -delta).
 constexpr int K2_QT = 64;
+#ifndef DKDV_OPERANDS_AHEAD
+#define DKDV_OPERANDS_AHEAD 1
+#endif
 constexpr int K2_NBUF = 3;
 constexpr int K2_STAGE = 2 * 64 * D * 2 + 1024 + 1024;  // Q, dO [64][64] bf16 + rowrec [4][64] f32 + keep [4][64] u32
 
@@ -1009,10 +1012,26 @@ __global__ __launch_bounds__(256, NB == 3 ? 2 : 3) void attn_bwd_dkdv2_kernel(At
     for (int u = 0; u < 2; ++u) {
       const int q0 = qt * K2_QT + 32 * u;
       f32x16 sacc = {}, dpacc = {};
+      if constexpr (NB == 3 && DKDV_OPERANDS_AHEAD) {
+        // all 8 operand rows in flight before the first MFMA (one LDS round trip; hipcc otherwise waits before each)
+        bf16x8v qa[4], da[4];
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        sacc = mfma32(as_frag(ld_row(Qb, 32 * u + r, 2 * s + hh)), kf[s], sacc);
-        dpacc = mfma32(as_frag(ld_row(dOb, 32 * u + r, 2 * s + hh)), vf[s], dpacc);
+        for (int s = 0; s < 4; ++s) {
+          qa[s] = as_frag(ld_row(Qb, 32 * u + r, 2 * s + hh));
+          da[s] = as_frag(ld_row(dOb, 32 * u + r, 2 * s + hh));
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          sacc = mfma32(qa[s], kf[s], sacc);
+          dpacc = mfma32(da[s], vf[s], dpacc);
+        }
+      } else {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          sacc = mfma32(as_frag(ld_row(Qb, 32 * u + r, 2 * s + hh)), kf[s], sacc);
+          dpacc = mfma32(as_frag(ld_row(dOb, 32 * u + r, 2 * s + hh)), vf[s], dpacc);
+        }
       }
       const int sat = !HAS_BIAS ? 0
                       : (kw0 + 31 - q0 + P.Sq - 1 <= P.sat_lo ? 1 : (kw0 - q0 - 31 + P.Sq - 1 >= P.sat_hi ? 2 : 0));
@@ -1127,14 +1146,36 @@ __global__ __launch_bounds__(256, NB == 3 ? 2 : 3) void attn_bwd_dkdv2_kernel(At
         atomicAdd(&dlut_s[la < 0 ? 0 : la], va);  // la < 0: rows past Sq only (dS = 0)
       }
       const bf16x8v pf0 = pack8(pd, 0), pf1 = pack8(pd, 8), sf0 = pack8(ds, 0), sf1 = pack8(ds, 8);
+      if constexpr (NB == 3 && DKDV_OPERANDS_AHEAD) {  // the 8 transposed operands (16 reads) in flight together
+        bf16x8v ot[2][2], qtr[2][2];
 #pragma unroll
-      for (int sp = 0; sp < 2; ++sp) {
-        const int c0 = 32 * u + 16 * sp + 4 * hh;
-        const bf16x8v pfv = sp == 0 ? pf0 : pf1, sfv = sp == 0 ? sf0 : sf1;
-        dv0 = mfma32(ld_tr_operand(dOb, c0, 0, r), pfv, dv0);
-        dv1 = mfma32(ld_tr_operand(dOb, c0, 1, r), pfv, dv1);
-        dk0 = mfma32(ld_tr_operand(Qb, c0, 0, r), sfv, dk0);
-        dk1 = mfma32(ld_tr_operand(Qb, c0, 1, r), sfv, dk1);
+        for (int sp = 0; sp < 2; ++sp) {
+          const int c0 = 32 * u + 16 * sp + 4 * hh;
+#pragma unroll
+          for (int t = 0; t < 2; ++t) {
+            ot[sp][t] = ld_tr_operand(dOb, c0, t, r);
+            qtr[sp][t] = ld_tr_operand(Qb, c0, t, r);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int sp = 0; sp < 2; ++sp) {
+          const bf16x8v pfv = sp == 0 ? pf0 : pf1, sfv = sp == 0 ? sf0 : sf1;
+          dv0 = mfma32(ot[sp][0], pfv, dv0);
+          dv1 = mfma32(ot[sp][1], pfv, dv1);
+          dk0 = mfma32(qtr[sp][0], sfv, dk0);
+          dk1 = mfma32(qtr[sp][1], sfv, dk1);
+        }
+      } else {
+#pragma unroll
+        for (int sp = 0; sp < 2; ++sp) {
+          const int c0 = 32 * u + 16 * sp + 4 * hh;
+          const bf16x8v pfv = sp == 0 ? pf0 : pf1, sfv = sp == 0 ? sf0 : sf1;
+          dv0 = mfma32(ld_tr_operand(dOb, c0, 0, r), pfv, dv0);
+          dv1 = mfma32(ld_tr_operand(dOb, c0, 1, r), pfv, dv1);
+          dk0 = mfma32(ld_tr_operand(Qb, c0, 0, r), sfv, dk0);
+          dk1 = mfma32(ld_tr_operand(Qb, c0, 1, r), sfv, dk1);
+        }
       }
     }
   };
