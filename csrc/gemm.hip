@@ -81,13 +81,18 @@ DLLM_DEVICE bf16x8v frag16(const uint16_t* T, int kk, int cb, int lane) {
 // same cycles per FLOP as 32x32x16, higher sustained clock on random data (MI355X_MICROARCH.md "DVFS give-back" 7)
 // PRE (16x16, BK = 64): both 32-deep k-steps' fragments are read before the first MFMA of a stage.  Not used:
 // with both operands on transposed reads it needs > 256 VGPRs and spills (2x slower, r1_gemm_wgrad_bench_v4).
-// PP (16x16, BK = 32, NBUF = 4): the two wave groups (wm = 0 / 1: one wave of each on every SIMD) run one stage apart —
+// PP = 2 (16x16, BK = 64, NBUF = 2): the barrier of stage s + 1 sits between the two 32-deep halves of stage s, so the
+// first fragments of stage s + 1 are read while the second half of stage s is on the matrix cores (the default
+// structure reads them after the barrier with every wave of the CU stalled on them).  Legal because the barrier only
+// needs stage s + 1 landed (its DMA is the one in flight) and every wave's reads of stage s done (lgkmcnt(0) before it:
+// the second half's fragments are in registers) before stage s + 2 refills stage s's slot.
+// PP = 1 (16x16, BK = 32, NBUF = 4): the two wave groups (wm = 0 / 1: one wave of each on every SIMD) run one stage apart —
 // group 1 passes one extra barrier first — so on each SIMD one wave is in its MFMA block while the other is at the start
 // of its stage (barrier, LDS reads, waits) instead of both stalling there together (cdna_hip_programming.md, the 256^2
 // template's staggered wave groups).  Every global barrier g: each wave first waits for its own DMA of stage g (stage g + 1
 // may stay in flight), then issues stage g + 2 into the buffer of stage g - 2, which group 0 finished before barrier
 // g - 1 and group 1 before barrier g; group 0 computes stage g, group 1 stage g - 1; barriers 0 .. nk for both.
-template <int BK, int NBUF, bool PRIO, int NI, int MF = 32, bool PRE = false, bool PP = false>
+template <int BK, int NBUF, bool PRIO, int NI, int MF = 32, bool PRE = false, int PP = 0>
 __global__ __launch_bounds__((256 / (32 * NI)) * 2 * 64, 1) void gemm_wgrad_kernel(GemmWgradParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint16_t* lds = reinterpret_cast<uint16_t*>(smem);  // [NBUF][A tile | B tile], each [BK][256]
@@ -134,7 +139,7 @@ __global__ __launch_bounds__((256 / (32 * NI)) * 2 * 64, 1) void gemm_wgrad_kern
   };
 
 #pragma unroll
-  for (int p = 0; p < (PP ? 2 : NBUF - 1); ++p)
+  for (int p = 0; p < (PP == 1 ? 2 : NBUF - 1); ++p)
     if (p < nk) issue(p, p);
 
   auto stage_sync = [&](int it) {
@@ -190,7 +195,51 @@ __global__ __launch_bounds__((256 / (32 * NI)) * 2 * 64, 1) void gemm_wgrad_kern
         }
       }
     };
-    if constexpr (PP) {
+    if constexpr (PP == 2) {
+      static_assert(BK == 64 && NBUF == 2, "cross-stage pipeline: two 32-deep halves per stage, 2-slot ring");
+      // fragments: A i = 0..3 and all of B of a stage's first half cross the barrier (32 VGPRs, what the register file
+      // holds beside the second half's 48); A i = 4..7 are read under the first 16 MFMAs
+      auto load_a = [&](int it, int kk, int i0, bf16x8v (&a)[8]) __attribute__((always_inline)) {
+        const uint16_t* As = lds + (it % NBUF) * 2 * TILE;
+#pragma unroll
+        for (int i = i0; i < i0 + 4; ++i) a[i] = frag16(As, kk, wm * 128 + 16 * i, lane);
+      };
+      auto load_b = [&](int it, int kk, bf16x8v (&b)[4]) __attribute__((always_inline)) {
+        const uint16_t* Bs = lds + (it % NBUF) * 2 * TILE + TILE;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b[j] = frag16(Bs, kk, wn * 64 + 16 * j, lane);
+      };
+      auto mfma_rows = [&](const bf16x8v (&a)[8], const bf16x8v (&b)[4], int i0, int i1) __attribute__((always_inline)) {
+        if (PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = i0; i < i1; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
+        if (PRIO) __builtin_amdgcn_s_setprio(0);
+      };
+      wait_vm<0>();  // stage 0 landed
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      if (nk > 1) issue(1, 1);
+      bf16x8v fa[8], fb[4], ga[8], gb[4];
+      load_a(0, 0, 0, fa);
+      load_b(0, 0, fb);
+      for (int it = 0; it < nk; ++it) {
+        load_a(it, 0, 4, fa);          // rest of the first half's A under its first 16 MFMAs
+        mfma_rows(fa, fb, 0, 4);
+        mfma_rows(fa, fb, 4, 8);
+        load_a(it, 32, 0, ga);         // second half (k 32..63) of stage it
+        load_a(it, 32, 4, ga);
+        load_b(it, 32, gb);
+        if (it + 1 < nk) {
+          wait_vm<0>();  // stage it + 1 landed (the only DMA in flight)
+          asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // all reads of stage it done
+          if (it + 2 < nk) issue(it % NBUF, it + 2);
+          load_a(it + 1, 0, 0, fa);
+          load_b(it + 1, 0, fb);
+        }
+        mfma_rows(ga, gb, 0, 8);
+      }
+    } else if constexpr (PP == 1) {
       static_assert(BK == 32 && NBUF == 4, "staggered groups: one k-step per stage, 4-slot ring");
       const int grp = __builtin_amdgcn_readfirstlane(wm);
       for (int g = 0; g <= nk; ++g) {
@@ -352,7 +401,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   }
 }
 
-template <int BK, int NBUF, bool PRIO = false, int NI = 2, int MF = 32, bool PRE = false, bool PP = false>
+template <int BK, int NBUF, bool PRIO = false, int NI = 2, int MF = 32, bool PRE = false, int PP = 0>
 int launch_wgrad(const GemmWgradParams& p, hipStream_t st) {
   constexpr int threads = (256 / (32 * NI)) * 2 * 64;
   const size_t lds = (size_t)NBUF * 2 * BK * 256 * 2;
@@ -386,7 +435,8 @@ extern "C" int dllm_gemm_wgrad_bk() { return 64; }
 // variant: 0 = BK64 x 2 stages (128 KB LDS), 1 = BK32 x 4 stages (128 KB), 2 = BK32 x 3 stages (96 KB),
 // 3 / 4 = variants 0 / 1 with s_setprio raised around the MFMA block,
 // 5 / 6 = variants 0 / 1 with 4 waves of 128x128 (one wave per SIMD, accumulators in AGPRs),
-// 7 / 8 / 9 = variants 0 / 4 / 3 on v_mfma_f32_16x16x32_bf16, 10 = variant 8 with staggered wave groups (PP)
+// 7 / 8 / 9 = variants 0 / 4 / 3 on v_mfma_f32_16x16x32_bf16, 10 = variant 8 with staggered wave groups (PP = 1),
+// 11 = variant 9 with the next stage's first fragments read across the barrier (PP = 2)
 extern "C" int dllm_gemm_wgrad(const GemmWgradParams* pp, int variant, hipStream_t st) {
   const GemmWgradParams& p = *pp;
   if (p.M % 8 || p.M < 8 || p.N % BN || p.K <= 0 || p.splits < 1 || p.ntiles != ((p.M + BM - 1) / BM) * (p.N / BN))
@@ -403,7 +453,8 @@ extern "C" int dllm_gemm_wgrad(const GemmWgradParams* pp, int variant, hipStream
     case 7: return launch_wgrad<64, 2, false, 2, 16>(p, st);
     case 8: return launch_wgrad<32, 4, true, 2, 16>(p, st);
     case 9: return launch_wgrad<64, 2, true, 2, 16>(p, st);
-    case 10: return launch_wgrad<32, 4, true, 2, 16, false, true>(p, st);
+    case 10: return launch_wgrad<32, 4, true, 2, 16, false, 1>(p, st);
+    case 11: return launch_wgrad<64, 2, true, 2, 16, false, 2>(p, st);
     default: return launch_wgrad<64, 2>(p, st);
   }
 }

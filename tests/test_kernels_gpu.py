@@ -235,7 +235,7 @@ def test_attention_packed_qkv_grad():
 
 
 # ------------------------------------------------------------------------------------ wgrad GEMM
-@pytest.mark.parametrize("variant", [0, 1, 2, 4, 7, 8, 9, 10])
+@pytest.mark.parametrize("variant", [0, 1, 2, 4, 7, 8, 9, 10, 11])
 @pytest.mark.parametrize("K,M,N,beta,lda_pad", [
     (4096, 768, 768, True, 0),      # t5-base o-proj shape class (many splits)
     (8192, 768, 3072, False, 0),    # wi wgrad, decoder token count
@@ -258,20 +258,22 @@ def test_gemm_wgrad(variant, K, M, N, beta, lda_pad):
     _close(c, ref, rtol=2e-2, atol=2e-2 * ref.abs().mean().item(), msg="wgrad")
 
 
+@pytest.mark.parametrize("variant,base", [(10, 8), (11, 9)])
 @pytest.mark.parametrize("K,M,N", [(8192, 768, 2304), (4096, 768, 768), (960, 512, 256), (64, 256, 256)])
-def test_gemm_wgrad_staggered_groups_bitwise(K, M, N):
-    """Variant 10 (wave groups one stage apart, csrc/gemm.hip PP) changes only the synchronisation of variant 8: every
-    output element sums the same products in the same order, so 12 repeated runs must equal variant 8 bit for bit (a
-    buffer read before its DMA landed, or refilled while still read, shows up as a mismatch)."""
+def test_gemm_wgrad_resynchronised_variants_bitwise(variant, base, K, M, N):
+    """Variants 10 (wave groups one stage apart, csrc/gemm.hip PP = 1) and 11 (next stage's first fragments read across
+    the barrier, PP = 2) change only the synchronisation of variants 8 / 9: every output element sums the same products
+    in the same order, so 12 repeated runs must equal the base variant bit for bit (a buffer read before its DMA landed,
+    or refilled while still read, shows up as a mismatch)."""
     torch.manual_seed(K + M)
     a = torch.randn(K, M, device=DEV, dtype=torch.bfloat16)
     b = torch.randn(K, N, device=DEV, dtype=torch.bfloat16)
     C = _ext.native()
     ref = torch.zeros(M, N, device=DEV, dtype=torch.float32)
-    C.gemm_wgrad(a, b, ref, False, 8, 0)
+    C.gemm_wgrad(a, b, ref, False, base, 0)
     for _ in range(12):
         c = torch.zeros(M, N, device=DEV, dtype=torch.float32)
-        C.gemm_wgrad(a, b, c, False, 10, 0)
+        C.gemm_wgrad(a, b, c, False, variant, 0)
         assert torch.equal(c, ref)
 
 
