@@ -18,7 +18,9 @@ Here the vocabulary is processed in chunks of ``Vc`` columns sized so a chunk of
 
 The price is one extra logits GEMM per step (the recompute); the gain is memory (no ``[N, V]`` tensor, no
 ``[N, V]`` gradient) and cache-resident CE passes.  Used when the full logits would exceed
-``DLLM_LMHEAD_FULL_MB`` (default 2048 MiB; ``0`` = always chunked, ``-1`` = never), or explicitly by callers.
+``DLLM_LMHEAD_FULL_MB`` (default 16384 MiB — sized for the 288 GB HBM: the t5-base bench at 512 samples per GPU keeps
+its 4 GiB of logits and runs 1.7 % faster than chunked, ``profiles/r3_lmhead_b512_ab.txt``; ``0`` = always chunked,
+``-1`` = never), or explicitly by callers.
 """
 from __future__ import annotations
 
@@ -58,7 +60,7 @@ def _chunks(V: int, vc: int):
 
 
 def use_chunked(N: int, V: int) -> bool:
-    lim = float(os.environ.get("DLLM_LMHEAD_FULL_MB", "2048"))
+    lim = float(os.environ.get("DLLM_LMHEAD_FULL_MB", "16384"))
     if lim < 0:
         return False
     return N * V * 2 > lim * 2**20
