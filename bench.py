@@ -10,6 +10,16 @@ weights with HF's initialisation (no network).  Weak scaling: fixed per-GPU micr
 
     python bench.py --gpus N --steps K --warmup W
 
+``--gpus N > 1`` without a launcher (no WORLD_SIZE in the environment) starts its own: the same command line under
+``python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1`` as a CHILD process (no exec,
+and before anything touches the GPU), forwards its exit code, and rank 0 of the child prints the JSON line.  The
+driver's ``torch.distributed.run ... bench.py --gpus N`` form runs the ranks directly.
+
+Every N runs the same step: forward + backward (+ GA micro-steps) and the optimizer replayed from HIP graphs
+(train/graph.py); for N > 1 the gradient all-reduce runs between the forward/backward graph and the optimizer graph
+as the reducer's frozen bucket schedule (``comm.schedule`` = "split-graph"), so the 1 -> N curve compares the same
+method at every N.  ``--graph off`` gives the eager, hook-overlapped reducer instead.
+
 Multi-GPU self-diagnosis (N > 1; every field is also produced on a gloo CPU rehearsal, DLLM_FORCE_CPU=1):
   * before timing, every rank's world size, RCCL version, bucket layout (bounds + segment sizes) and parameter count
     are all-gathered and compared: a mismatch aborts the run with the differing ranks named;
@@ -28,6 +38,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -71,9 +83,11 @@ def parse():
     ap.add_argument("--comm-stress", action="store_true",
                     help="small per-GPU batch (8 unless --batch-per-gpu is given): all-reduce ~ compute")
     ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
-                    help="capture the whole step (forward, backward, GA micro-steps, clip, AdamW) in one HIP graph and "
-                         "replay it (train/graph.py); auto: on for one GPU, off for N > 1 (the all-reduce is launched "
-                         "from autograd hooks)")
+                    help="replay the step (forward, backward, GA micro-steps, clip, AdamW) from HIP graphs "
+                         "(train/graph.py; N > 1: the bucketed all-reduce between the two graphs); auto: on whenever "
+                         "the ranks run on GPUs; off: eager steps with the hook-overlapped reducer")
+    ap.add_argument("--graph-comm", default=None, choices=["split", "capture"],
+                    help="N > 1 graph schedule (train/graph.py): split (default) or capture (RCCL inside the graph)")
     ap.add_argument("--dtype", default=None, choices=["bf16", "fp32"],
                     help="weights/activations dtype (default bf16; fp32 on a CPU rehearsal)")
     a = ap.parse_args()
@@ -82,6 +96,29 @@ def parse():
     if a.batch_per_gpu is None:
         a.batch_per_gpu = 512 if a.model == "t5-base" else 256
     return a
+
+
+def _free_port() -> int:
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def self_launch(gpus: int) -> int | None:
+    """``--gpus N > 1`` with no launcher around: run this same command line under torchrun as a child process (one
+    rank per GPU, rendezvous on 127.0.0.1) and return its exit code.  None when already launched (WORLD_SIZE set) or
+    N == 1.  Nothing here touches the GPU (counting devices does not initialise it)."""
+    if gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return None
+    if os.environ.get("DLLM_FORCE_CPU", "0") != "1" and os.environ.get("DLLM_DIST_BACKEND") != "gloo":
+        ndev = torch.cuda.device_count()
+        if ndev < gpus:
+            print(f"[bench] --gpus {gpus} but only {ndev} GPU(s) visible", file=sys.stderr)
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    print(f"[bench] self-launch: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return subprocess.run(cmd, env=dict(os.environ, DLLM_BENCH_SELF_LAUNCHED="1")).returncode
 
 
 def _rccl_version():
@@ -116,20 +153,41 @@ def check_rank_consistency(env, eng, model_name: str, batch: int):
     return {"status": "ok", "checked": sorted(mine), **{k: mine[k] for k in ("bucket_layout_sha", "n_buckets")}}
 
 
-def main():
-    a = parse()
+def comm_probe(env, eng, sizes_mb=(1.0, 32.0, 128.0), iters: int = 5) -> dict:
+    """In-run all-reduce bus bandwidth over the reducer's bucket sizes, fp32 and bf16 (GB/s, ring convention
+    2(N-1)/N x bytes / time, the slowest rank's time): what RCCL over xGMI delivers to THIS job's buckets."""
+    red = eng.reducer
+    n = env.world_size
+    dev = env.device if env.backend == "nccl" else torch.device("cpu")
+    if dev.type == "cpu":  # gloo rehearsal: the fields, not the numbers
+        sizes_mb = sizes_mb[:1]
+    sizes = sorted({round(x, 2) for x in list(sizes_mb) + red.bucket_sizes_mb()[:2]})
+    out = {}
+    for dt in (torch.float32, torch.bfloat16):
+        res = {}
+        for mb in sizes:
+            x = torch.ones(max(1, int(mb * 2**20) // (4 if dt == torch.float32 else 2)), dtype=dt, device=dev)
+            for _ in range(2):
+                dist.all_reduce(x)
+            _sync(dev)
+            dist.barrier()
+            t0 = time.perf_counter()
+            for _ in range(iters):
+                dist.all_reduce(x)
+            _sync(dev)
+            t = torch.tensor([(time.perf_counter() - t0) / iters], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            nbytes = x.numel() * x.element_size()
+            res[f"{mb:g}MiB"] = round(2 * (n - 1) / n * nbytes / t.item() / 1e9, 2)
+        out["fp32" if dt == torch.float32 else "bf16"] = res
+    return out
+
+
+def build(a, env):
     from distributed_llms_example_amd.models import build_model, resolve_config
     from distributed_llms_example_amd.ops.rng import manual_seed
-    from distributed_llms_example_amd.parallel.env import init_distributed
     from distributed_llms_example_amd.parallel.reducer import DEFAULT_BUCKET_MB
     from distributed_llms_example_amd.train.engine import TrainEngine
-    from distributed_llms_example_amd.utils.profiling import MI355X_BF16_DENSE_PEAK, seq2seq_train_flops
-
-    env = init_distributed()
-    n = env.world_size
-    if a.gpus != n:
-        raise SystemExit(f"[bench] --gpus {a.gpus} but WORLD_SIZE={n}: launch one rank per GPU "
-                         f"(python -m torch.distributed.run --nproc-per-node {a.gpus} bench.py --gpus {a.gpus})")
     torch.manual_seed(a.seed)
     manual_seed(a.seed * 1000 + env.rank)
     cfg = resolve_config(a.model)
@@ -143,6 +201,23 @@ def main():
     eng = TrainEngine(model, env, lr=5e-5, weight_decay=0.01, max_grad_norm=1.0, dtype=dtype,
                       bucket_mb=a.bucket_mb or DEFAULT_BUCKET_MB, overlap=not a.no_overlap)
     eng.train()
+    return cfg, eng, dtype_name
+
+
+def main():
+    a = parse()
+    rc = self_launch(a.gpus)
+    if rc is not None:
+        sys.exit(rc)
+    from distributed_llms_example_amd.parallel.env import init_distributed
+    from distributed_llms_example_amd.utils.profiling import MI355X_BF16_DENSE_PEAK, seq2seq_train_flops
+
+    env = init_distributed()
+    n = env.world_size
+    if a.gpus != n:
+        raise SystemExit(f"[bench] --gpus {a.gpus} but WORLD_SIZE={n}: launch one rank per GPU "
+                         f"(python -m torch.distributed.run --nproc-per-node {a.gpus} bench.py --gpus {a.gpus})")
+    cfg, eng, dtype_name = build(a, env)
     B, S, T, V = a.batch_per_gpu, a.src_len, a.tgt_len, cfg.vocab_size
     GA = max(1, a.grad_accum)
     g = torch.Generator(device="cpu").manual_seed(1000 + env.rank)
@@ -154,18 +229,28 @@ def main():
             "labels": torch.randint(2, V, (B, T), generator=g).to(env.device),
         })
 
-    use_graph = a.graph == "on" or (a.graph == "auto" and n == 1 and env.device.type == "cuda")
+    use_graph = a.graph == "on" or (a.graph == "auto" and env.device.type == "cuda")
     graphed = None
+    graph_error = None
     if use_graph:
         from distributed_llms_example_amd.train.graph import GraphedStep
         try:
-            graphed = GraphedStep(eng, batches[:GA], warmup=2)
-        except Exception as e:  # noqa: BLE001 - a capture problem must not cost the measurement: run eager
+            graphed = GraphedStep(eng, batches[:GA], warmup=2, comm=a.graph_comm)
+        except Exception as e:  # noqa: BLE001 - recorded in the JSON line; the step is then rebuilt from scratch
             if a.graph == "on":
                 raise
-            print(f"[bench] graph capture failed ({type(e).__name__}: {e}); eager steps", file=sys.stderr)
+            graph_error = f"{type(e).__name__}: {str(e)[:300]}"
+            print(f"[bench] graph capture failed ({graph_error}); rebuilding the engine, eager steps", file=sys.stderr)
             graphed = None
             torch.cuda.synchronize()
+            # the failed capture left the engine mid-state (warmup steps taken, step seeds on, host mirrors ahead of
+            # the device): start over with a fresh model, optimizer and seed stream
+            eng.disable_step_seeds()
+            if eng.reducer is not None:
+                eng.reducer.remove()
+            del eng
+            torch.cuda.empty_cache()
+            cfg, eng, dtype_name = build(a, env)
 
     def step(i):
         mbs = [batches[(i * GA + k) % len(batches)] for k in range(GA)]
@@ -197,9 +282,19 @@ def main():
         ex_t = torch.tensor([sum(ex) / max(1, len(ex)), max(ex, default=0.0)], dtype=torch.float64,
                             device=env.device if env.backend == "nccl" else "cpu")
         dist.all_reduce(ex_t, op=dist.ReduceOp.MAX)  # the slowest rank's exposure sets the step
-        comm = {"exposed_ms_per_step": round(ex_t[0].item(), 3), "exposed_ms_max": round(ex_t[1].item(), 3),
-                "timed_backwards": len(ex), "bucket_launch": eng.reducer.launch_summary(),
+        split = graphed is not None and graphed.comm == "split"
+        bl = eng.reducer.launch_summary()
+        if split:  # every bucket launches after backward, in bucket order (GradReducer.sync_buckets)
+            nb = len(eng.reducer.buckets)
+            bl = {"order": list(range(nb)), "ready_frac_at_launch": [1.0] * nb, "launched_before_backward_end": 0,
+                  "n_buckets": nb}
+        comm = {"schedule": ("split-graph" if split else "captured-graph" if graphed is not None else "eager-overlap"),
+                "exposed_ms_per_step": round(ex_t[0].item(), 3), "exposed_ms_max": round(ex_t[1].item(), 3),
+                "timed_backwards": len(ex), "bucket_launch": bl,
+                "buckets_launched_before_backward_end": bl["launched_before_backward_end"],
                 "bucket_mb": [round(x, 2) for x in eng.reducer.bucket_sizes_mb()[:4]],
+                "world_size_seen_by_pg": dist.get_world_size(), "backend": dist.get_backend(),
+                "rccl_version": _rccl_version() if env.backend == "nccl" else None,
                 "consistency": consistency}
     t = torch.tensor([dt], device=env.device if env.backend == "nccl" else "cpu", dtype=torch.float64)
     if n > 1:
@@ -209,6 +304,7 @@ def main():
     value = B * GA * n * a.steps / dt
     if comm is not None:
         comm["exposed_frac"] = round(comm["exposed_ms_per_step"] / ms, 4)
+        comm["busbw_gbps"] = comm_probe(env, eng)  # after the timed region: not part of the measurement
     # model FLOPs utilisation against the dense bf16 peak (2.5 PF per GPU; no 2:1-sparsity figure): analytic training
     # FLOPs of the step (GEMMs + attention + LM head, fwd + bwd = 3 x fwd; utils/profiling.py)
     step_flops = seq2seq_train_flops(cfg, B * GA, S, T)
@@ -245,11 +341,21 @@ def main():
                        "overlap": bool(eng.reducer.overlap) if eng.reducer else None,
                        "n_buckets": len(eng.reducer.buckets) if eng.reducer else None,
                        "comm_stress": bool(a.comm_stress), "hip_graph": graphed is not None,
+                       "graph_error": graph_error,
                        "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 2)
                        if env.device.type == "cuda" else None},
             "comm": comm,
         }), flush=True)
     if n > 1:
+        # orderly teardown: the native reducer holds the process group (and, on gloo, its worker threads): release it
+        # before the group is destroyed, so nothing is torn down from interpreter-exit destructors
+        _sync(env.device)
+        if eng.reducer is not None:
+            eng.reducer.remove()
+            eng.reducer.native = None
+        del eng, graphed
+        import gc
+        gc.collect()
         dist.barrier()
         dist.destroy_process_group()
 

@@ -3,11 +3,10 @@
 //
 // Works on the flat gradient buffer of parallel/flat.py: bucket b is the contiguous slice
 // [bounds[2b], bounds[2b+1]) of ONE buffer ("gradient as bucket view"), so a bucket's all-reduce runs in
-// place with no flatten/unflatten copies.  Readiness is tracked per flat segment:
-//   * post hooks on each parameter's AccumulateGrad node (registered here, in C++, like DDP) fire when
-//     autograd has accumulated that parameter's gradient;
-//   * parameters whose gradient is accumulated INSIDE a GEMM/norm kernel (ops/linear.py, ops/norms.py —
-//     AccumulateGrad never runs for them) call mark_ready() from Python.
+// place with no flatten/unflatten copies.  Readiness is tracked per flat segment: mark_ready(seg) is called once per
+// backward per segment — by FlatParams' post-accumulate hook for the few parameters autograd accumulates, and by the
+// fused op that accumulated the gradient inside its GEMM / norm kernel for the rest (ops/linear.py _fire,
+// ops/norms.py: AccumulateGrad never runs for them, so a C++ AccumulateGrad hook could not see them).
 // A bucket is launched the moment its last segment is ready, strictly in bucket order on every rank (RCCL
 // requires the same collective order everywhere), as an async all_reduce on the process group
 // (ProcessGroupNCCL = RCCL over xGMI on ROCm: the collective runs on RCCL's own stream while backward
@@ -16,8 +15,6 @@
 // synchronisation on the GPU path.  Averaging uses ReduceOp::AVG (RCCL) or SUM + one scale (gloo).
 #include <torch/extension.h>
 #include <torch/csrc/autograd/engine.h>
-#include <torch/csrc/autograd/functions/accumulate_grad.h>
-#include <torch/csrc/autograd/utils/lambda_post_hook.h>
 #include <torch/csrc/distributed/c10d/ProcessGroup.hpp>
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime_api.h>
@@ -64,22 +61,6 @@ class NativeReducer {
       counts_[b] += 1;
     }
     reset_state();
-  }
-
-  // Register C++ post hooks on the AccumulateGrad node of every parameter (index = flat segment index).
-  void attach_hooks(const std::vector<at::Tensor>& params) {
-    TORCH_CHECK(params.size() == seg_bucket_.size(), "one parameter per flat segment expected");
-    for (size_t i = 0; i < params.size(); ++i) {
-      auto acc = torch::autograd::impl::grad_accumulator(params[i]);
-      TORCH_CHECK(acc, "parameter ", i, " has no grad accumulator (requires_grad=False?)");
-      const int64_t seg = (int64_t)i;
-      acc->add_post_hook(std::make_unique<torch::autograd::utils::LambdaPostHook>(
-          [this, seg](const torch::autograd::variable_list& outputs, const torch::autograd::variable_list&) {
-            this->mark_ready(seg);
-            return outputs;
-          }));
-      grad_accs_.push_back(std::move(acc));
-    }
   }
 
   void mark_ready(int64_t seg) {
@@ -164,7 +145,7 @@ class NativeReducer {
   bool enabled() const { return enabled_; }
   int64_t num_buckets() const { return (int64_t)bounds_.size() / 2; }
   int64_t launched() const { return next_; }
-  void detach() { grad_accs_.clear(); }
+  void detach() {}
 
  private:
   void reset_state() {
@@ -203,7 +184,6 @@ class NativeReducer {
   bool callback_queued_ = false;
   int64_t next_ = 0;
   std::vector<c10::intrusive_ptr<c10d::Work>> works_;
-  std::vector<std::shared_ptr<torch::autograd::Node>> grad_accs_;
   std::mutex mu_;
 };
 
@@ -214,7 +194,6 @@ void bind_reducer(pybind11::module& m) {
                     bool, bool>(),
            py::arg("grad_buf"), py::arg("bounds"), py::arg("seg_bucket"), py::arg("process_group"),
            py::arg("average") = true, py::arg("use_avg_op") = true)
-      .def("attach_hooks", &NativeReducer::attach_hooks)
       .def("mark_ready", &NativeReducer::mark_ready)
       .def("finalize", &NativeReducer::finalize, py::call_guard<py::gil_scoped_release>())
       .def("sync_all", &NativeReducer::sync_all, py::call_guard<py::gil_scoped_release>())

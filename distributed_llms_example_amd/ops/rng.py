@@ -121,13 +121,20 @@ class StepSeed:
         self.t = torch.full((1,), start, dtype=torch.int32, device=device)
         self.host = start
         self.enabled = False
+        self._prev_site_mode = None
 
     def enable(self):
+        """Process-wide: the kernels' step pointer (every translation unit), the active-step registry read by the
+        reference ops, and the host seed stream's site mode.  ``disable()`` restores all three."""
         from .. import _ext
         if self.t.is_cuda and _ext.native() is not None:
             _ext.native().set_seed_step(self.t)
         self.enabled = True
         _active_step[0] = self
+        rng = default_rng()
+        if self._prev_site_mode is None:
+            self._prev_site_mode = rng.site_mode
+        rng.site_mode = True
 
     def disable(self):
         from .. import _ext
@@ -136,6 +143,9 @@ class StepSeed:
         self.enabled = False
         if _active_step[0] is self:
             _active_step[0] = None
+        if self._prev_site_mode is not None:
+            default_rng().site_mode = self._prev_site_mode
+            self._prev_site_mode = None
 
     def advance(self, n: int = 1):
         self.t.add_(n)

@@ -44,10 +44,13 @@ FIRST_BUCKET_MB = 1.0
 class GradReducer:
     def __init__(self, flat: FlatParams, group=None, bucket_mb: float = DEFAULT_BUCKET_MB,
                  first_bucket_mb: float = FIRST_BUCKET_MB, overlap: bool = True, average: bool = True,
-                 native: bool | None = None, rebuild: bool | None = None):
+                 native: bool | None = None, rebuild: bool | None = None, force: bool = False):
         self.flat = flat
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        # data parallel: more than one rank, or ``force`` (a 1-rank process group whose collectives really run: the
+        # GPU tests of the RCCL launch / graph-capture paths on a one-GPU box)
+        self.dp = self.world > 1 or (bool(force) and dist.is_initialized())
         self.backend = dist.get_backend(group) if dist.is_initialized() else "none"
         self.overlap = overlap
         self.average = average
@@ -60,7 +63,7 @@ class GradReducer:
         # is re-laid in the order gradients actually became ready, broadcast from rank 0 so every rank agrees
         if rebuild is None:
             rebuild = os.environ.get("DLLM_REBUILD_BUCKETS", "1") != "0"
-        self._rebuild_pending = bool(rebuild) and overlap and self.world > 1
+        self._rebuild_pending = bool(rebuild) and overlap and self.dp
         # per synchronised backward (diagnostics / tests): segment indices in readiness order, and (bucket, number of
         # segments ready at its launch) in launch order; the previous backward's logs are kept in *_last
         self.ready_log: list[int] = []
@@ -75,7 +78,7 @@ class GradReducer:
         self._hooks = []
         self.native = None
         self._build()
-        if self.world > 1 and overlap:
+        if self.dp and overlap:
             for p in flat.params:
                 # run by FlatParams' post-accumulate hook (autograd gradients) or by the fused op that accumulated
                 # the gradient in its kernel (ops/linear.py _fire), once per backward after the last contribution
@@ -115,7 +118,7 @@ class GradReducer:
         if self.native is not None:
             self.native.detach()
             self.native = None
-        if self.use_native and self.world > 1:
+        if self.use_native and self.dp:
             pg = self.group if self.group is not None else dist.distributed_c10d._get_default_group()
             bounds = [x for se in self.buckets for x in se]
             self.native = _ext.native().NativeReducer(flat.grad_buf, bounds, self.seg_bucket, pg, self.average,
@@ -186,7 +189,7 @@ class GradReducer:
 
     def finish(self):
         """End of backward: launch what is left (unused params) in order, wait on the GPU stream."""
-        if self.world <= 1:
+        if not self.dp:
             return
         ev = None
         if self.timing and self.flat.grad_buf.is_cuda:
@@ -225,9 +228,20 @@ class GradReducer:
             if self.native is not None:
                 self.native.set_enabled(prev)
 
+    def sync_buckets(self):
+        """Every bucket, in bucket order, as an async all-reduce; then the compute stream waits on them (no host sync
+        on RCCL).  The frozen launch schedule a graphed data-parallel step issues between its replays
+        (train/graph.py "split"): identical on every rank by construction (``layout_signature``)."""
+        if not self.dp:
+            return
+        if self.native is not None:
+            self.native.finalize()  # launches buckets next_..end (all of them: no hook has fired), waits, resets
+        else:
+            self.finish()
+
     def sync_now(self):
         """Non-overlapped path (train-task semantics): one coalesced all-reduce of all gradients."""
-        if self.world <= 1:
+        if not self.dp:
             return
         if self.native is not None:
             self.native.sync_all()
@@ -243,7 +257,7 @@ class GradReducer:
     def post_backward(self):
         """Call after a synchronised ``loss.backward()``: completes the reduction for the non-overlapped mode, rebuilds
         the buckets in ready order after the first one (maybe_rebuild) and rotates the readiness / launch logs."""
-        if self.world > 1 and not self.overlap and self.enabled:
+        if self.dp and not self.overlap and self.enabled:
             self.sync_now()
         if self.ready_log:
             if self.native is not None:  # leftovers launched by the native finalize
@@ -256,7 +270,7 @@ class GradReducer:
     def broadcast_params(self, module=None, src: int = 0):
         """DDP construction broadcast (distributed.py:864-870): one collective over the flat
         parameter buffer plus the module's buffers."""
-        if self.world <= 1:
+        if not self.dp:
             return
         dist.broadcast(self.flat.param_buf, src=src, group=self.group)
         if module is not None:

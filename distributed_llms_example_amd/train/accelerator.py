@@ -246,6 +246,31 @@ class Accelerator:
         m = model if isinstance(model, PreparedModel) else self._model
         return m.no_sync() if m is not None else contextlib.nullcontext()
 
+    def make_train_step(self, model, optimizer, graph: bool | None = None):
+        """The reference loop's per-batch body — ``outputs = model(**batch); accelerator.backward(outputs.loss);
+        optimizer.step(); optimizer.zero_grad()`` (ref/train-accelerator.py:219-228) — as one callable
+        ``step(batch) -> loss``, run by train/graph.py's StepRunner: replayed from a HIP graph once the batch shape
+        repeats (GPU, unless ``graph=False`` / ``DLLM_GRAPH=0``), eager otherwise.  Gradient accumulation keeps the
+        explicit loop (``accumulate`` / ``backward``); a clip requested with ``clip_grad_norm_`` before the first call is
+        part of every step."""
+        from .engine import TrainEngine
+        from .graph import StepRunner
+        m = model if isinstance(model, PreparedModel) else self._model
+        po = optimizer if isinstance(optimizer, PreparedOptimizer) else self._prepared_opts[-1]
+        if self.gradient_accumulation_steps != 1:
+            raise ValueError("make_train_step: one micro-batch per optimizer step (use accumulate() for GA)")
+        eng = TrainEngine.from_parts(m.module, self.env, m.flat, m.reducer, po.opt, max_grad_norm=po._clip)
+        runner = StepRunner(eng, enabled=graph)
+
+        def step(batch: dict) -> torch.Tensor:
+            self._step += 1
+            self.sync_gradients = True
+            losses, _ = runner([batch])
+            return losses[0]
+
+        step.runner = runner
+        return step
+
     def clip_grad_norm_(self, parameters=None, max_norm: float = 1.0):
         """Clipping is fused into the next optimizer step (norm over the flat gradient buffer)."""
         for o in self._optimizers():

@@ -16,6 +16,7 @@ import re
 import torch
 
 from ..models.hf_io import from_hf_state_dict, save_pretrained
+from ..ops import rng as _rng_mod
 from ..ops.rng import default_rng
 from ..parallel import collectives
 
@@ -38,6 +39,9 @@ def save_checkpoint(path: str, model, optimizer=None, scheduler=None, trainer_st
         if trainer_state is not None:
             trainer_state.save_to_json(os.path.join(path, "trainer_state.json"))
     rng = {"dropout": default_rng().state_dict(), "torch": torch.get_rng_state()}
+    st = _rng_mod._active_step[0]
+    if st is not None and st.enabled:  # graph-replayable dropout (ops/rng.py StepSeed): the device step counter
+        rng["step_seed"] = int(st.host)
     if torch.cuda.is_available():
         rng["cuda"] = torch.cuda.get_rng_state()
     torch.save(rng, os.path.join(path, f"rng_state_{rank}.pt"))
@@ -63,6 +67,8 @@ def load_checkpoint(path: str, model=None, optimizer=None, scheduler=None, rank:
     if os.path.exists(rp):
         rng = torch.load(rp, map_location="cpu", weights_only=True)
         default_rng().load_state_dict(rng["dropout"])
+        if "step_seed" in rng:
+            out["step_seed"] = int(rng["step_seed"])
         torch.set_rng_state(rng["torch"])
         if "cuda" in rng and torch.cuda.is_available():
             torch.cuda.set_rng_state(rng["cuda"])

@@ -44,12 +44,15 @@ class TrainEngine:
     def __init__(self, model: torch.nn.Module, env: DistEnv, *, lr: float = 5e-5, weight_decay: float = 0.0,
                  betas=(0.9, 0.999), eps: float = 1e-8, max_grad_norm: float | None = 1.0,
                  dtype: torch.dtype = torch.bfloat16, bucket_mb: float = DEFAULT_BUCKET_MB, overlap: bool = True,
-                 no_decay=default_no_decay, label_smoothing: float = 0.0, grad_dtype: torch.dtype | None = None):
+                 no_decay=default_no_decay, label_smoothing: float = 0.0, grad_dtype: torch.dtype | None = None,
+                 force_reducer: bool = False):
         self.env = env
         self.model = model.to(device=env.device, dtype=dtype)
         self.dtype = dtype
         self.flat = FlatParams(self.model, grad_dtype=grad_dtype or default_grad_dtype(dtype))
-        self.reducer = GradReducer(self.flat, bucket_mb=bucket_mb, overlap=overlap) if env.world_size > 1 else None
+        # force_reducer: a reducer (and its collectives) on a 1-rank process group — GPU tests of the RCCL paths
+        self.reducer = (GradReducer(self.flat, bucket_mb=bucket_mb, overlap=overlap, force=force_reducer)
+                        if env.world_size > 1 or force_reducer else None)
         if self.reducer is not None:
             self.reducer.broadcast_params(self.model)
         self.optimizer = FusedAdamW(self.flat, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay,
@@ -58,15 +61,37 @@ class TrainEngine:
         self.label_smoothing = label_smoothing
         self.step_seed: rng_mod.StepSeed | None = None
 
-    def enable_step_seeds(self) -> rng_mod.StepSeed:
+    @classmethod
+    def from_parts(cls, model: torch.nn.Module, env: DistEnv, flat: FlatParams, reducer: GradReducer | None,
+                   optimizer: FusedAdamW, max_grad_norm: float | None = None, label_smoothing: float = 0.0):
+        """An engine over state another front end already built (train/accelerator.py: the prepared model's flat
+        buffers and reducer, the prepared optimizer), so its loop can run the same step — and the same HIP-graph
+        step runner (train/graph.py) — as the Trainer."""
+        eng = cls.__new__(cls)
+        eng.env, eng.model, eng.dtype = env, model, flat.dtype
+        eng.flat, eng.reducer, eng.optimizer = flat, reducer, optimizer
+        eng.max_grad_norm, eng.label_smoothing = max_grad_norm, label_smoothing
+        eng.step_seed = None
+        return eng
+
+    def enable_step_seeds(self, start: int | None = None) -> rng_mod.StepSeed:
         """Dropout seeds that a captured HIP graph can replay (ops/rng.py StepSeed): from now on every micro-step
         advances a device counter the kernels mix into each site seed, and the host seed stream restarts per micro-step.
         Masks differ from the default mode's (another, equally uniform, stream), so enable it before training."""
         if self.step_seed is None:
             self.step_seed = rng_mod.StepSeed(self.env.device)
             self.step_seed.enable()
-            rng_mod.default_rng().site_mode = True
+        if start is not None:  # resumed run (train/checkpoint.py "step_seed")
+            self.step_seed.t.fill_(int(start))
+            self.step_seed.host = int(start)
         return self.step_seed
+
+    def disable_step_seeds(self) -> None:
+        """Back to the default dropout seed stream: the kernels' device step pointer, the active-step registry and the
+        host stream's site mode are all restored (StepSeed.disable), and forward_backward stops advancing it."""
+        if self.step_seed is not None:
+            self.step_seed.disable()
+            self.step_seed = None
 
     def no_sync(self):
         return self.reducer.no_sync() if self.reducer is not None else contextlib.nullcontext()

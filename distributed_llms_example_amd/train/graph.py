@@ -1,9 +1,24 @@
-"""Whole training step in one HIP graph (static shapes, one rank).
+"""Whole training step replayed from HIP graphs (static shapes), one rank or data parallel.
 
 A step of the flagship model launches ~1,000 kernels; at the reference's small micro-batches (batch 1-8 per GPU,
 ref/train-accelerator.py:169, ref/train-task.py:180, ref/train-torchrun.py:119,126) their host launch cost, not the
 GPU, sets the step time.  ``GraphedStep`` captures forward + backward (+ the gradient-accumulation micro-steps) + the
-global-norm clip + AdamW + zero_grad ONCE with ``torch.cuda.graph`` and then replays it: one host call per step.
+global-norm clip + AdamW + zero_grad with ``torch.cuda.graph`` and then replays it: one or two host calls per step.
+
+Data parallel (an engine with a gradient reducer, parallel/reducer.py) is graphed in one of two schedules
+(``comm``, default from ``DLLM_GRAPH_COMM``):
+
+* ``"split"`` (default): graph 1 = every micro-batch's forward + backward with the reducer disabled (gradients
+  accumulate locally, like ``no_sync``); then the gradient all-reduce is issued EAGERLY between the replays — the
+  reducer's launch schedule frozen to its bucket list (``GradReducer.sync_buckets``: the same buckets, in the same
+  order, on every rank, each an async RCCL all-reduce; the compute stream waits on them without a host sync);
+  graph 2 = clip + AdamW + zero_grad.  Nothing about RCCL is captured, so this is exactly the collective sequence
+  the eager engine runs; what it gives up is the overlap of the all-reduce with backward (≈1 % of a t5-base step
+  at per-GPU batch 512 over 8 GPUs, SURVEY.md §2.6 / bench.py ``comm``).
+* ``"capture"``: ONE graph for the whole step; the reducer's bucket all-reduces are launched from the autograd
+  hooks during capture, so RCCL's kernels are recorded into the graph at the point in backward where each bucket
+  became ready (overlap preserved).  This needs RCCL's graph-capture support and a process group that tolerates
+  capture (no async error handling); it is opt-in and covered by a 1-rank RCCL GPU test only.
 
 What makes the replay a real training step and not a re-run of the captured one:
 
@@ -11,79 +26,244 @@ What makes the replay a real training step and not a re-run of the captured one:
   inside the graph), and the host seed stream restarts every micro-step, so the seeds the graph baked in are the ones
   an eager step draws;
 * AdamW reads [lr, lr / bc1, 1 / sqrt(bc2)] from a device tensor computed inside the graph from a device step count
-  (ops/optim.py device_hyper), so the bias corrections advance; ``lr_fn(t)`` (device scalar -> device scalar) carries a
-  schedule, default the optimizer's lr;
+  (ops/optim.py device_hyper), so the bias corrections advance; the learning rate is a device scalar refreshed from
+  ``optimizer.param_groups[0]["lr"]`` before every replay (a scheduler or ``eng.step(lr=...)`` keeps working), or
+  ``lr_fn(t)`` (device scalar -> device scalar) computes it inside the graph;
 * inputs are copied into static buffers before each replay (same shapes required).
 
-Not covered (eager instead): more than one rank (the gradient all-reduce is launched from autograd hooks with host-side
-bucket bookkeeping), dynamic shapes, the Trainer's per-step host logic.  tests/test_graph_gpu.py checks graphed and
-eager steps give the same parameters.
+``use_graph=False`` runs the very same phase schedule eagerly (CPU / gloo tests of the schedule).
+
+:class:`StepRunner` is how the entry points use it (train/trainer.py, train/accelerator.py ``make_train_step``,
+train-task.py): the first steps of every new batch shape run eagerly (they are real training steps and warm up the
+lazy state a capture must not see), the next step with the same shapes is captured and replayed, and any step whose
+shapes differ (an epoch's last partial batch, dynamic padding) runs eagerly — the reference's max_length padding
+(ref/train-accelerator.py:114-133) makes every full batch the same shape.  tests/test_graph_gpu.py checks graphed and
+eager steps give the same parameters; tests/test_distributed_cpu.py checks the split schedule on 2 gloo ranks.
 """
 from __future__ import annotations
+
+import os
 
 import torch
 
 from ..ops import rng as rng_mod
 
+COMM_MODES = ("split", "capture")
+
 
 class GraphedStep:
-    def __init__(self, engine, batches: list[dict], warmup: int = 2, lr_fn=None):
-        if engine.reducer is not None:
-            raise ValueError("GraphedStep: one rank only (the reducer's collectives are launched from autograd hooks)")
-        if engine.env.device.type != "cuda":
-            raise ValueError("GraphedStep: GPU only")
+    def __init__(self, engine, batches: list[dict], warmup: int = 2, lr_fn=None, comm: str | None = None,
+                 use_graph: bool = True, num_items: bool = False, dp_ranks: int | None = None):
+        """``batches``: the step's micro-batches (passes), whose shapes the graph fixes; ``warmup`` eager steps on them
+        first (0: the caller already ran real steps of these shapes, StepRunner).  ``num_items``: the step's loss is
+        normalised by a global token count handed to every ``replay`` (engine.forward_backward ``num_items`` /
+        ``dp_ranks``, the Trainer's HF ``num_items_in_batch`` semantics); otherwise by the number of micro-batches."""
+        dev = engine.env.device
+        if use_graph and dev.type != "cuda":
+            raise ValueError("GraphedStep: GPU only (use_graph=False runs the same schedule eagerly)")
         self.eng = engine
+        self.red = engine.reducer
+        self.comm = (comm or os.environ.get("DLLM_GRAPH_COMM", "split")) if self.red is not None else None
+        if self.comm is not None and self.comm not in COMM_MODES:
+            raise ValueError(f"GraphedStep: comm must be one of {COMM_MODES}, got {self.comm!r}")
+        self.use_graph = use_graph
         self.ga = len(batches)
         self.static = [{k: v.clone() for k, v in b.items() if torch.is_tensor(v)} for b in batches]
         engine.enable_step_seeds()
         opt = engine.optimizer
-        dev = engine.env.device
         self.t = torch.full((), float(opt.step_count), dtype=torch.float32, device=dev)
+        self._t_host = opt.step_count  # what self.t holds (eager steps between replays move the optimizer's count)
+        self.num_items = torch.ones((), dtype=torch.int64, device=dev) if num_items else None
+        self.dp_ranks = dp_ranks
+        self.losses: list = []  # per-pass mean losses of the last step (static outputs of the graph)
         self.lr_fn = lr_fn
+        self._lr_host = float(opt.param_groups[0]["lr"])
+        self.lr_t = torch.full((), self._lr_host, dtype=torch.float32, device=dev)
         self.loss = None
+        self.norm = None
+        if not use_graph:
+            return
         # warmup on a side stream (lazy allocations, kernel attributes, GEMM solution lookups happen outside capture);
         # these are real training steps
-        s = torch.cuda.Stream(dev)
-        s.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.stream(s):
-            for _ in range(warmup):
-                self._body()
-        torch.cuda.current_stream(dev).wait_stream(s)
+        if warmup > 0:
+            s = torch.cuda.Stream(dev)
+            s.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(s):
+                for _ in range(warmup):
+                    self._eager_step()
+            torch.cuda.current_stream(dev).wait_stream(s)
         torch.cuda.synchronize(dev)
-        self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
-            self.loss = self._body()
-        self._host_after_replay_sync()  # the capture ran the Python side once but executed nothing
+        self.t.fill_(float(opt.step_count))
+        self._t_host = opt.step_count
+        torch.cuda.empty_cache()  # eager blocks cached by the warmup are not usable by the graph's private pool
+        if self.comm == "split":
+            self.g_fb = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.g_fb):
+                self.loss = self._fb(sync=False)
+            self.g_opt = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.g_opt):
+                self.norm = self._opt()
+        else:
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph):
+                self.loss = self._fb(sync=True)
+                self.norm = self._opt()
+        self._host_after_capture()  # the capture ran the Python side once but executed nothing
 
-    def _body(self):
+    # ------------------------------------------------------------------------------------------ phases
+    def _fb(self, sync: bool):
+        """Forward + backward of every micro-batch; ``sync``: the last one synchronises through the reducer hooks."""
         eng = self.eng
         total = None
+        self.losses = []
         for k, b in enumerate(self.static):
-            loss = eng.forward_backward(b, grad_accum=self.ga, sync=k == self.ga - 1)
+            loss = eng.forward_backward(b, grad_accum=self.ga, sync=sync and k == self.ga - 1,
+                                        num_items=self.num_items, dp_ranks=self.dp_ranks)
+            self.losses.append(loss)
             total = loss if total is None else total + loss
-        self.t.add_(1.0)
-        lr = self.lr_fn(self.t) if self.lr_fn is not None else eng.optimizer.param_groups[0]["lr"]
-        eng.step(hyper=eng.optimizer.device_hyper(self.t, lr))
         return total / self.ga
 
-    def _host_after_replay_sync(self):
+    def _comm(self):
+        """Split mode, between the replays: the frozen bucket schedule, eagerly (no host sync on RCCL; with the
+        reducer's timing on, its exposed-communication events bracket it)."""
+        self.red.sync_buckets()
+
+    def _opt(self):
+        eng = self.eng
+        self.t.add_(1.0)
+        lr = self.lr_fn(self.t) if self.lr_fn is not None else self.lr_t
+        return eng.step(hyper=eng.optimizer.device_hyper(self.t, lr))
+
+    def _eager_step(self):
+        """The step the graphs hold, run eagerly (warmup, and the use_graph=False schedule)."""
+        if self.comm == "split":
+            loss = self._fb(sync=False)
+            self._comm()
+        else:
+            loss = self._fb(sync=True)
+        norm = self._opt()
+        return loss, norm
+
+    def _host_after_capture(self):
         """Host mirrors of what a replay advances on the device (optimizer step count, dropout step counter) were
         advanced by the capture pass, which executed nothing: undo that."""
         eng = self.eng
         eng.optimizer.step_count -= 1
+        self._t_host = eng.optimizer.step_count
         eng.step_seed.host -= self.ga
 
-    def replay(self, batches: list[dict] | None = None) -> torch.Tensor:
+    # ------------------------------------------------------------------------------------------ API
+    def signature(self) -> tuple:
+        return batch_signature(self.static)
+
+    def replay(self, batches: list[dict] | None = None, num_items: torch.Tensor | None = None) -> torch.Tensor:
         """One training step on ``batches`` (copied into the static buffers; None: replay on the last ones).  Returns
-        the mean loss of the step's micro-batches (device scalar, valid until the next replay)."""
+        the mean loss of the step's micro-batches (device scalar, valid until the next replay; per pass: ``losses``)."""
         if batches is not None:
             if len(batches) != self.ga:
                 raise ValueError(f"GraphedStep: {self.ga} micro-batches per step, got {len(batches)}")
             for st, b in zip(self.static, batches):
                 for k, v in st.items():
                     v.copy_(b[k], non_blocking=True)
-        self.graph.replay()
-        self.eng.optimizer.step_count += 1
+        if self.num_items is not None:
+            if num_items is None:
+                raise ValueError("GraphedStep: built with num_items=True, replay needs the step's token count")
+            self.num_items.copy_(num_items, non_blocking=True)
+        opt = self.eng.optimizer
+        if opt.step_count != self._t_host:  # eager steps ran since the last replay: re-sync the bias corrections
+            self.t.fill_(float(opt.step_count))
+            self._t_host = opt.step_count
+        lr = float(self.eng.optimizer.param_groups[0]["lr"])
+        if lr != self._lr_host:
+            self.lr_t.fill_(lr)
+            self._lr_host = lr
+        if not self.use_graph:
+            self.loss, self.norm = self._eager_step()
+            return self.loss
+        if self.comm == "split":
+            self.g_fb.replay()
+            self._comm()
+            self.g_opt.replay()
+        else:
+            self.graph.replay()
+        opt.step_count += 1
+        self._t_host = opt.step_count
         self.eng.step_seed.host += self.ga
         rng_mod.default_rng().begin_micro_step()
         return self.loss
+
+
+def batch_signature(batches: list[dict]) -> tuple:
+    """What a captured graph fixes about a step's inputs: per pass, every tensor's name, shape and dtype."""
+    return tuple(tuple(sorted((k, tuple(v.shape), v.dtype) for k, v in b.items() if torch.is_tensor(v)))
+                 for b in batches)
+
+
+def graphs_enabled(device: torch.device) -> bool:
+    """Entry points replay their steps from HIP graphs on GPU unless ``DLLM_GRAPH=0``."""
+    return device.type == "cuda" and os.environ.get("DLLM_GRAPH", "1") != "0"
+
+
+class StepRunner:
+    """One optimizer step of an entry point's loop — forward + backward of the step's passes, gradient sync, clip +
+    AdamW — eager or replayed from a HIP graph (GraphedStep).
+
+    Per batch-shape signature: the first ``warmup`` steps run eagerly (real training steps; step seeds are on from
+    the first one, so eager and replayed steps draw dropout masks from one stream), the next one is captured and from
+    then on every step of that signature is a replay; steps of any other signature run eagerly.  ``enabled=False``
+    (CPU, ``DLLM_GRAPH=0``) is the plain eager step."""
+
+    def __init__(self, engine, enabled: bool | None = None, warmup: int = 2, num_items: bool = False,
+                 dp_ranks: int | None = None, comm: str | None = None):
+        self.eng = engine
+        self.enabled = graphs_enabled(engine.env.device) if enabled is None else bool(enabled)
+        self.warmup = max(1, int(warmup))
+        self.num_items = num_items
+        self.dp_ranks = dp_ranks
+        self.comm = comm
+        self.graph: GraphedStep | None = None
+        self.graph_error: str | None = None
+        self._sig = None
+        self._seen = 0
+        self.replays = 0
+        self.eager_steps = 0
+        if self.enabled:
+            engine.enable_step_seeds()
+
+    def __call__(self, passes: list[dict], num_items: torch.Tensor | None = None, lr: float | None = None):
+        """Run one step; returns (per-pass mean losses, pre-clip grad norm or None) as device tensors."""
+        eng = self.eng
+        if lr is not None:
+            eng.optimizer.param_groups[0]["lr"] = lr
+        if self.enabled:
+            sig = batch_signature(passes)
+            g = self.graph
+            if g is not None and sig == g.signature():
+                g.replay(passes, num_items=num_items)
+                self.replays += 1
+                return list(g.losses), g.norm
+            if g is None and self.graph_error is None:
+                self._seen = self._seen + 1 if sig == self._sig else 1
+                self._sig = sig
+                if self._seen > self.warmup:
+                    # a failed capture executed nothing on the device, but its host pass may have advanced the host
+                    # mirrors of device state: snapshot them
+                    rng = rng_mod.default_rng()
+                    snap = (eng.optimizer.step_count, eng.step_seed.host, rng.counter)
+                    try:
+                        self.graph = GraphedStep(eng, passes, warmup=0, comm=self.comm,
+                                                 num_items=num_items is not None, dp_ranks=self.dp_ranks)
+                    except Exception as e:  # noqa: BLE001 - capture unsupported here: stay eager, say why once
+                        eng.optimizer.step_count, eng.step_seed.host, rng.counter = snap
+                        self.graph_error = f"{type(e).__name__}: {str(e)[:300]}"
+                        from ..utils.logging import get_logger
+                        get_logger(__name__).warning(f"HIP graph capture failed, eager steps: {self.graph_error}")
+                        torch.cuda.synchronize()
+                    else:
+                        return self(passes, num_items=num_items)
+        self.eager_steps += 1
+        losses = []
+        for j, pb in enumerate(passes):
+            losses.append(eng.forward_backward(pb, grad_accum=len(passes), sync=j + 1 == len(passes),
+                                               num_items=num_items, dp_ranks=self.dp_ranks))
+        return losses, eng.step()

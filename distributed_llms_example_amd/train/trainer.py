@@ -36,6 +36,7 @@ from .callbacks import CallbackHandler, DefaultFlowCallback, TrainerControl, Tra
 from ..utils import faults
 from .checkpoint import latest_checkpoint, load_checkpoint, save_checkpoint
 from .engine import TrainEngine, default_no_decay, token_count
+from .graph import StepRunner, graphs_enabled
 from .schedule import LRScheduler
 
 logger = get_logger(__name__)
@@ -235,6 +236,7 @@ class Trainer:
         self.state.max_steps = max_steps
         self.state.num_train_epochs = epochs
         start_epoch, skip = 0, 0
+        step_seed_start = None
         resume = resume_from_checkpoint if resume_from_checkpoint is not None else args.resume_from_checkpoint
         if resume:
             path = latest_checkpoint(args.output_dir) if resume is True else resume
@@ -244,6 +246,7 @@ class Trainer:
                 self.state.global_step = ts.get("global_step", 0)
                 self.state.coalesce_cap = ts.get("coalesce_cap")
                 self.state.log_history = ts.get("log_history", [])
+                step_seed_start = info.get("step_seed")
                 start_epoch = self.state.global_step // steps_per_epoch
                 skip = (self.state.global_step % steps_per_epoch) * args.gradient_accumulation_steps
                 logger.info(f"resumed from {path} at step {self.state.global_step}")
@@ -261,6 +264,14 @@ class Trainer:
         if cap == -1 and self.state.coalesce_cap is not None:  # resumed: the original run's choice (same RNG stream)
             cap = self.state.coalesce_cap or None
         pad_id = getattr(getattr(self.model, "config", None), "pad_token_id", 0) or 0
+        # the optimizer step (passes + sync + clip + AdamW) replayed from HIP graphs once batch shapes repeat
+        # (train/graph.py StepRunner; the reference pads to max_length, so every full step has one shape); context
+        # parallelism keeps its eager ring-attention collectives
+        runner = StepRunner(eng, enabled=graphs_enabled(env.device) and self.cp_group is None, num_items=True,
+                            dp_ranks=self.dp_world)
+        if runner.enabled and step_seed_start is not None:
+            eng.enable_step_seeds(step_seed_start)
+        self.step_runner = runner
         if cap == -1:
             torch.cuda.synchronize()
             torch.cuda.reset_peak_memory_stats(env.device)
@@ -296,9 +307,9 @@ class Trainer:
                             cur = []
                         cur.append(b)
                     passes.append(cur)
-                for j, pb in enumerate(passes):
-                    loss = eng.forward_backward(self._merge(pb, pad_id), sync=j + 1 == len(passes),
-                                                num_items=num_items, dp_ranks=self.dp_world)
+                losses, last_norm = runner([self._merge(pb, pad_id) for pb in passes], num_items=num_items,
+                                           lr=self.scheduler.get_last_lr()[0])
+                for pb, loss in zip(passes, losses):
                     # logged loss: token-weighted mean (sum of token losses / tokens), the same number whether the
                     # micro-batches run one by one or merged into passes of different token counts
                     ntok = sum(token_count(b["labels"]) for b in pb).float()
@@ -309,7 +320,6 @@ class Trainer:
                     cap = self._auto_cap(mem_base, torch.cuda.max_memory_allocated(env.device),
                                          max(self._padded_tokens([b]) for b in group))
                     self.state.coalesce_cap = cap or 0
-                last_norm = eng.step(self.scheduler.get_last_lr()[0])
                 self.scheduler.step()
                 self.state.global_step += 1
                 if self.state.global_step in (warm_step, max_steps):  # steady-state clock: after the first steps,

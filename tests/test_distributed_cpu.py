@@ -339,3 +339,94 @@ def test_bench_multirank_diagnostics_on_gloo():
     bl = c["bucket_launch"]
     assert bl["n_buckets"] >= 2 and sorted(bl["order"]) == list(range(bl["n_buckets"]))
     assert bl["ready_frac_at_launch"][-1] == 1.0 and bl["launched_before_backward_end"] >= 1
+
+
+# ---------------------------------------------------------------- graphed data-parallel schedule (train/graph.py "split")
+def _split_schedule_case(rank, world, native=True, ga=2, steps=3):
+    """The split schedule the graphed DP step runs (local forward/backward of every micro-batch, then the frozen bucket
+    all-reduce, then clip + AdamW) — executed eagerly on gloo — against the hook-overlapped eager DP step."""
+    from distributed_llms_example_amd.models import build_model
+    from distributed_llms_example_amd.ops.rng import manual_seed
+    from distributed_llms_example_amd.parallel.env import DistEnv
+    from distributed_llms_example_amd.train.engine import TrainEngine
+    from distributed_llms_example_amd.train.graph import GraphedStep
+    os.environ["DLLM_NATIVE_REDUCER"] = "1" if native else "0"
+    env = DistEnv(rank=rank, world_size=world, backend="gloo", device=torch.device("cpu"))
+    g = torch.Generator().manual_seed(7 + rank)
+    data = [{"input_ids": torch.randint(3, 500, (2, 12), generator=g), "attention_mask": torch.ones(2, 12, dtype=torch.long),
+             "labels": torch.randint(3, 500, (2, 6), generator=g)} for _ in range(ga * steps)]
+
+    def engine():
+        torch.manual_seed(0)
+        manual_seed(5 + rank)
+        eng = TrainEngine(build_model("t5-tiny"), env, lr=1e-3, dtype=torch.float32, bucket_mb=0.05)
+        eng.train()  # dropout on: both arms draw the same step-seeded masks
+        return eng
+
+    eng_s = engine()
+    gs = GraphedStep(eng_s, data[:ga], use_graph=False)
+    assert gs.comm == "split"
+    ls = [float(gs.replay(data[ga * i:ga * (i + 1)])) for i in range(steps)]
+    launched = eng_s.reducer.native.launched() if eng_s.reducer.native is not None else None
+    p_split = eng_s.flat.to_canonical(eng_s.flat.param_buf).clone()
+    eng_s.disable_step_seeds()
+    eng_s.reducer.remove()
+
+    eng_e = engine()
+    eng_e.enable_step_seeds()
+    t = torch.zeros(())
+    le = []
+    for i in range(steps):
+        tot = 0.0
+        for k in range(ga):
+            tot += float(eng_e.forward_backward(data[ga * i + k], grad_accum=ga, sync=k == ga - 1))
+        t.add_(1.0)
+        eng_e.step(hyper=eng_e.optimizer.device_hyper(t, eng_e.optimizer.param_groups[0]["lr"]))
+        le.append(tot / ga)
+    p_eager = eng_e.flat.to_canonical(eng_e.flat.param_buf).clone()
+    eng_e.disable_step_seeds()
+    return ls, le, p_split, p_eager, launched, len(eng_s.reducer.buckets)
+
+
+@pytest.mark.parametrize("native", [False, pytest.param(True, marks=pytest.mark.skipif(
+    not _native_available(), reason="native extension not built"))])
+def test_split_graph_schedule_matches_eager_overlap(native):
+    out = run_ranks(functools.partial(_split_schedule_case, native=native))
+    for r in (0, 1):
+        ls, le, ps, pe, launched, nb = out[r]
+        assert nb >= 2
+        assert ls == pytest.approx(le, rel=1e-5, abs=1e-6), (ls, le)
+        ps, pe = torch.as_tensor(ps), torch.as_tensor(pe)
+        assert torch.allclose(ps, pe, rtol=1e-5, atol=1e-6), (ps - pe).abs().max()
+        if native:
+            assert launched == 0  # finalize resets the schedule after launching every bucket
+    assert torch.equal(torch.as_tensor(out[0][2]), torch.as_tensor(out[1][2]))  # ranks agree
+
+
+# ---------------------------------------------------------------- bench.py self-launch (the driver's `bench.py --gpus N`)
+@pytest.mark.parametrize("n", [2, 4])
+def test_bench_self_launches_ranks(n):
+    """``python bench.py --gpus N`` with no launcher: bench.py starts torchrun itself (child process) and rank 0 prints
+    one JSON line with the world size the process group saw, the in-run all-reduce bus bandwidth and the overlap."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                              "MASTER_PORT")}
+    env.update(DLLM_FORCE_CPU="1", OMP_NUM_THREADS="1")
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", str(n), "--model", "t5-tiny", "--steps", "2",
+           "--warmup", "2", "--batch-per-gpu", "2", "--src-len", "32", "--tgt-len", "8", "--bucket-mb", "0.1"]
+    r = subprocess.run(cmd, env=env, cwd=root, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=400)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{") and '"metric"' in l]
+    assert len(lines) == 1, r.stdout  # rank 0 only
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == n and d["config"]["world_size"] == n and d["config"]["parallelism"] == f"dp{n}"
+    assert d["config"]["hip_graph"] is False and d["config"]["graph_error"] is None  # CPU: eager schedule
+    c = d["comm"]
+    assert c["world_size_seen_by_pg"] == n and c["backend"] == "gloo" and c["schedule"] == "eager-overlap"
+    assert c["consistency"]["status"] == "ok" and c["buckets_launched_before_backward_end"] >= 1
+    for dt in ("fp32", "bf16"):
+        assert c["busbw_gbps"][dt] and all(v > 0 for v in c["busbw_gbps"][dt].values())
+    assert "self-launch" in r.stderr

@@ -79,6 +79,7 @@ class ModelTrainer:
             max_train_steps = min(max_train_steps, a.max_steps)
         lr_scheduler = get_scheduler("linear", optimizer, num_warmup_steps=1, num_training_steps=max_train_steps)
         metric = rouge.load("rouge")
+        train_step = acc.make_train_step(model, optimizer)
         self.logger.info(f"***** Running training ***** examples={len(train_ds)} epochs={a.num_epochs}")
         completed = 0
         t0 = time.perf_counter()
@@ -87,12 +88,10 @@ class ModelTrainer:
             model.train()
             train_dl.set_epoch(epoch)
             for batch in train_dl:
-                outputs = model(**batch)
-                loss = outputs.loss
-                acc.backward(loss)
-                optimizer.step()
+                # == outputs = model(**batch); acc.backward(outputs.loss); optimizer.step(); optimizer.zero_grad()
+                # (ref/train-accelerator.py:219-228), replayed from a HIP graph on GPU once the batch shape repeats
+                loss = train_step(batch)
                 lr_scheduler.step()
-                optimizer.zero_grad()
                 completed += 1
                 if completed == warm:
                     torch.cuda.synchronize() if acc.device.type == "cuda" else None

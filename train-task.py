@@ -59,6 +59,7 @@ def run(env, args):
     from distributed_llms_example_amd.train import rouge
     from distributed_llms_example_amd.utils import faults
     from distributed_llms_example_amd.train.engine import TrainEngine
+    from distributed_llms_example_amd.train.graph import StepRunner
     from distributed_llms_example_amd.train.schedule import LRScheduler
     from distributed_llms_example_amd.utils.gpu_report import gpu_report
     from distributed_llms_example_amd.utils.logging import dump_metrics, get_logger, setup_logging
@@ -97,15 +98,19 @@ def run(env, args):
     sched = LRScheduler(eng.optimizer, "linear", 1, max_steps)
     metric = rouge.load("rouge")
     dev = env.device
+    # forward + backward + gradient all-reduce + AdamW, replayed from HIP graphs once the batch shape repeats
+    # (train/graph.py StepRunner; eager on CPU, DLLM_GRAPH=0, or for a ragged last batch)
+    runner = StepRunner(eng)
     completed = 0
     for epoch in range(args.num_epochs):
         eng.train()
         loss_acc = torch.zeros((), device=dev)
         for batch in train_dl:
             batch = {k: v.to(dev, non_blocking=True) for k, v in batch.items()}
-            loss = eng.forward_backward(batch)  # all-reduce of the flat gradient buffer (average_gradients)
+            # all-reduce of the flat gradient buffer (average_gradients, ref/train-task.py:65-69,293) + AdamW
+            losses, _ = runner([batch], lr=sched.get_last_lr()[0])
+            loss = losses[0]
             loss_acc += loss
-            eng.step(sched.get_last_lr()[0])
             sched.step()
             completed += 1
             faults.maybe_inject(completed, env.rank)
