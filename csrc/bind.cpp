@@ -10,6 +10,7 @@
 #include <ATen/hip/HIPContext.h>
 #include <c10/hip/HIPStream.h>
 
+#include "attn_f32_params.h"
 #include "attn_params.h"
 #include "gemm_params.h"
 
@@ -37,6 +38,9 @@ int dllm_attn_fwd(AttnParams*, hipStream_t);
 int dllm_attn_bwd(AttnParams*, hipStream_t);
 int dllm_attn_params_size();
 int dllm_attn_dropout_mask(AttnParams*, hipStream_t);
+int dllm_attn_f32_fwd(AttnF32Params*, hipStream_t);
+int dllm_attn_f32_bwd(AttnF32Params*, hipStream_t);
+int dllm_set_seed_step_attn_f32(const uint32_t*);
 int dllm_gemm_wgrad(const GemmWgradParams*, int, hipStream_t);
 int dllm_gemm_fused(const GemmFusedParams*, int, int, hipStream_t);
 int dllm_gemm_w4(const GemmW4Params*, int, int, int, hipStream_t);
@@ -49,6 +53,8 @@ int dllm_ce_chunk_bwd(const float*, void*, long, const int64_t*, const float*, c
 int dllm_embed_bwd(const int64_t*, const int64_t*, const void*, long, long, int, float*, void*, long, long, int,
                    hipStream_t);
 int dllm_colsum_acc(const void*, long, long, int, float*, void*, int, hipStream_t);
+int dllm_ce_merge(const float*, int, long, const float*, const int64_t*, float*, float*, long, int, float, long,
+                  hipStream_t);
 int dllm_kv_reorder(void*, const int64_t*, int, int, int, int, int, int, hipStream_t);
 int dllm_beam_topk(const void*, long, int, const float*, const int64_t*, long, int, int, int, int, int, int, int, int,
                    float*, int64_t*, hipStream_t);
@@ -422,6 +428,113 @@ std::vector<Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, 
   return {o, lse, dmask};
 }
 
+// ------------------------------------------------------------------------------------------- fp32 attention
+// csrc/attn_f32.hip: the same op at the reference's precision (fp32 in, fp32 out, f32 MFMA).
+void check_bshd_f32(const Tensor& t, const char* n, int64_t B, int64_t S, int64_t H) {
+  check_gpu(t, n);
+  TORCH_CHECK(t.scalar_type() == at::kFloat, n, ": fp32 attention kernels take fp32");
+  TORCH_CHECK(t.dim() == 4 && t.size(0) == B && t.size(1) == S && t.size(2) == H && t.size(3) == 64, n,
+              ": expected [B, S, H, 64], got ", t.sizes());
+  TORCH_CHECK(t.stride(3) == 1, n, ": head dim must be contiguous");
+  TORCH_CHECK(t.stride(0) % 4 == 0 && t.stride(1) % 4 == 0 && t.stride(2) % 4 == 0, n,
+              ": strides must be multiples of 4 elements (16-B vector loads)");
+  check_aligned(t, 16, n);
+}
+
+void fill_f32(AttnF32Params& P, const Tensor& q, const Tensor& k, const Tensor& v, const optional<Tensor>& kpm,
+              const optional<Tensor>& lut, double scale, bool causal, double p, int64_t seed) {
+  const int64_t B = q.size(0), Sq = q.size(1), H = q.size(2), Sk = k.size(1);
+  check_bshd_f32(q, "q", B, Sq, H);
+  check_bshd_f32(k, "k", B, Sk, H);
+  check_bshd_f32(v, "v", B, Sk, H);
+  TORCH_CHECK(Sq > 0 && Sk > 0, "empty attention");
+  TORCH_CHECK(B * H <= 65535, "attention: B * H > 65535 unsupported (grid y)");
+  TORCH_CHECK(B * H * Sq < (int64_t)1 << 31 && (Sq + Sk) < (1 << 30), "attention too large");
+  TORCH_CHECK(p >= 0.0 && p < 1.0, "dropout p must be in [0, 1)");
+  P.q = q.data_ptr<float>();
+  P.k = k.data_ptr<float>();
+  P.v = v.data_ptr<float>();
+  P.q_sb = q.stride(0); P.q_ss = q.stride(1); P.q_sh = q.stride(2);
+  P.k_sb = k.stride(0); P.k_ss = k.stride(1); P.k_sh = k.stride(2);
+  P.v_sb = v.stride(0); P.v_ss = v.stride(1); P.v_sh = v.stride(2);
+  P.B = B; P.H = H; P.Sq = Sq; P.Sk = Sk;
+  P.scale = (float)scale;
+  P.causal = causal ? 1 : 0;
+  P.causal_off = Sk - Sq;
+  P.p_drop = (float)p;
+  P.seed = (uint32_t)seed;
+  P.thr = p > 0.0 ? (uint32_t)std::min(65535.0, p * 65536.0) : 0u;  // ops/rng.py threshold16
+  if (kpm.has_value() && kpm->defined()) {
+    TORCH_CHECK(kpm->scalar_type() == at::kByte && kpm->is_contiguous() && kpm->dim() == 2 && kpm->size(0) == B &&
+                    kpm->size(1) == Sk && kpm->is_cuda(),
+                "key_padding_mask must be uint8 [B, Sk] contiguous on GPU");
+    P.kpm = kpm->data_ptr<uint8_t>();
+  }
+  if (lut.has_value() && lut->defined()) {
+    TORCH_CHECK(lut->scalar_type() == at::kFloat && lut->is_contiguous() && lut->dim() == 2 && lut->size(0) == H &&
+                    lut->size(1) == Sq + Sk - 1 && lut->is_cuda(),
+                "bias_lut must be fp32 [H, Sq + Sk - 1] contiguous on GPU");
+    P.lut = lut->data_ptr<float>();
+  }
+}
+
+std::vector<Tensor> attn_f32_fwd(const Tensor& q, const Tensor& k, const Tensor& v, const optional<Tensor>& kpm,
+                                 const optional<Tensor>& lut, double scale, bool causal, double p, int64_t seed) {
+  AttnF32Params P{};
+  fill_f32(P, q, k, v, kpm, lut, scale, causal, p, seed);
+  auto o = at::empty({P.B, P.Sq, P.H, 64}, q.options());
+  auto lse = at::empty({P.B, P.H, P.Sq}, q.options());
+  P.o_out = o.data_ptr<float>();
+  P.o_sb = o.stride(0); P.o_ss = o.stride(1); P.o_sh = o.stride(2);
+  P.lse = lse.data_ptr<float>();
+  check_rc(dllm_attn_f32_fwd(&P, stream()), "attn_f32_fwd");
+  return {o, lse};
+}
+
+std::vector<Tensor> attn_f32_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor& v,
+                                 const Tensor& o, const Tensor& lse, const optional<Tensor>& kpm,
+                                 const optional<Tensor>& lut, double scale, bool causal, double p, int64_t seed,
+                                 bool need_dlut, const optional<Tensor>& dq_out, const optional<Tensor>& dk_out,
+                                 const optional<Tensor>& dv_out) {
+  AttnF32Params P{};
+  fill_f32(P, q, k, v, kpm, lut, scale, causal, p, seed);
+  check_bshd_f32(o, "o", P.B, P.Sq, P.H);
+  check_bshd_f32(dout, "dout", P.B, P.Sq, P.H);
+  TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.numel() == (int64_t)P.B * P.H * P.Sq && lse.is_contiguous() &&
+                  lse.is_cuda(),
+              "lse mismatch");
+  auto pick = [&](const optional<Tensor>& t, int64_t S, const char* n) {
+    if (t.has_value() && t->defined()) {
+      check_bshd_f32(*t, n, P.B, S, P.H);
+      return *t;
+    }
+    return at::empty({P.B, S, P.H, 64}, q.options());
+  };
+  Tensor dq = pick(dq_out, P.Sq, "dq_out");
+  Tensor dk = pick(dk_out, P.Sk, "dk_out");
+  Tensor dv = pick(dv_out, P.Sk, "dv_out");
+  auto delta = at::empty({P.B, P.H, P.Sq}, q.options());
+  Tensor dlut;
+  if (need_dlut && P.lut) {
+    dlut = at::zeros({P.H, P.Sq + P.Sk - 1}, q.options());
+    P.dlut = dlut.data_ptr<float>();
+  }
+  P.o = o.data_ptr<float>();
+  P.o_sb = o.stride(0); P.o_ss = o.stride(1); P.o_sh = o.stride(2);
+  P.dout = dout.data_ptr<float>();
+  P.do_sb = dout.stride(0); P.do_ss = dout.stride(1); P.do_sh = dout.stride(2);
+  P.lse = lse.data_ptr<float>();
+  P.delta = delta.data_ptr<float>();
+  P.dq = dq.data_ptr<float>();
+  P.dq_sb = dq.stride(0); P.dq_ss = dq.stride(1); P.dq_sh = dq.stride(2);
+  P.dk = dk.data_ptr<float>();
+  P.dk_sb = dk.stride(0); P.dk_ss = dk.stride(1); P.dk_sh = dk.stride(2);
+  P.dv = dv.data_ptr<float>();
+  P.dv_sb = dv.stride(0); P.dv_ss = dv.stride(1); P.dv_sh = dv.stride(2);
+  check_rc(dllm_attn_f32_bwd(&P, stream()), "attn_f32_bwd");
+  return {dq, dk, dv, dlut};
+}
+
 // dropout keep-bit planes of an attention call (generated ahead, e.g. on a side stream)
 Tensor attn_dropout_mask(int64_t B, int64_t H, int64_t Sq, int64_t Sk, double p, int64_t seed, const Tensor& like) {
   TORCH_CHECK(p > 0.0 && B > 0 && H > 0 && Sq > 0 && Sk > 0 && like.is_cuda(), "attn_dropout_mask: bad arguments");
@@ -699,6 +812,94 @@ void kv_reorder(Tensor& cache, const Tensor& src, int64_t nb, int64_t n) {
            "kv_reorder");
 }
 
+// ---- LM head + cross-entropy on the w4 GEMM's CE epilogues (csrc/gemm_w4.hip W4_EPI_CEF / W4_EPI_CEB)
+void check_lmhead_operands(const Tensor& h, const Tensor& w, const Tensor& labels, const optional<Tensor>& cbias,
+                           int64_t V) {
+  auto ok2 = [](const Tensor& t) {
+    return t.is_cuda() && t.dim() == 2 && t.scalar_type() == at::kBFloat16 && t.stride(1) == 1 && t.stride(0) % 8 == 0 &&
+           t.stride(0) >= t.size(1) && reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0 &&
+           256 * t.stride(0) * 2 < (1LL << 31);
+  };
+  TORCH_CHECK(ok2(h) && ok2(w), "lmhead: h [N, d] and w [n, d] must be bf16 GPU, unit inner stride, 16-B aligned rows");
+  TORCH_CHECK(h.size(1) == w.size(1) && h.size(1) % 64 == 0 && h.size(0) > 0 && w.size(0) > 0,
+              "lmhead: d must match and be a multiple of 64");
+  TORCH_CHECK(h.device() == w.device(), "lmhead: device mismatch");
+  TORCH_CHECK(labels.is_cuda() && labels.scalar_type() == at::kLong && labels.is_contiguous() &&
+                  labels.numel() == h.size(0),
+              "lmhead: labels must be a contiguous int64 [N] GPU tensor");
+  if (cbias.has_value() && cbias->defined())
+    TORCH_CHECK(cbias->is_cuda() && cbias->scalar_type() == at::kFloat && cbias->is_contiguous() &&
+                    cbias->numel() == V,
+                "lmhead: bias must be a contiguous fp32 [V] GPU tensor");
+}
+
+void fill_w4_tiles(GemmW4Params& P, int64_t M, int64_t N, int64_t K) {
+  TORCH_CHECK((M + 255) / 256 * ((N + 255) / 256) < INT_MAX && M < INT_MAX && N < INT_MAX, "gemm_w4: too large");
+  P.M = (int)M; P.N = (int)N; P.K = (int)K;
+  P.tm = (int)((M + 255) / 256);
+  P.tn = (int)((N + 255) / 256);
+  P.grp = 0;
+}
+
+// forward: loss_rows [N], lse [N] over the whole vocabulary w [V, d]; the logits are never written
+std::vector<Tensor> lmhead_ce_fwd(const Tensor& h, const Tensor& w, const Tensor& labels,
+                                  const optional<Tensor>& cbias, double eps, int64_t ignore) {
+  const int64_t V = w.size(0);
+  check_lmhead_operands(h, w, labels, cbias, V);
+  const int64_t N = h.size(0), K = h.size(1);
+  const int64_t np = (V + 127) / 128;
+  auto f32 = h.options().dtype(at::kFloat);
+  auto part = at::empty({N, np, 4}, f32);
+  auto xlab = at::zeros({N}, f32);
+  auto loss = at::empty({N}, f32);
+  auto lse = at::empty({N}, f32);
+  GemmW4Params P{};
+  P.A = reinterpret_cast<const uint16_t*>(h.data_ptr());
+  P.B = reinterpret_cast<const uint16_t*>(w.data_ptr());
+  P.lda = h.stride(0); P.ldb = w.stride(0); P.ldc = 0;
+  fill_w4_tiles(P, N, V, K);
+  P.labels = labels.data_ptr<int64_t>();
+  P.cbias = (cbias.has_value() && cbias->defined()) ? cbias->data_ptr<float>() : nullptr;
+  P.part = part.data_ptr<float>();
+  P.xlab = xlab.data_ptr<float>();
+  P.pstride = (int)np;
+  P.c0 = 0; P.V = (int)V; P.skip = 0; P.eps = (float)eps; P.ignore = ignore;
+  check_rc(dllm_gemm_w4(&P, 0, 1, 8, stream()), "lmhead_ce_fwd (gemm_w4 CEF)");
+  check_rc(dllm_ce_merge(P.part, (int)np, np, P.xlab, P.labels, loss.data_ptr<float>(), lse.data_ptr<float>(), N,
+                         (int)V, (float)eps, ignore, stream()),
+           "lmhead_ce_fwd (merge)");
+  return {loss, lse};
+}
+
+// backward of one vocabulary slice: out = dlogits of columns [c0, c0 + w_slice.size(0)) (bf16 [N, n], n % 8 == 0)
+void lmhead_ce_bwd_slice(const Tensor& h, const Tensor& w_slice, const Tensor& labels, const Tensor& lse,
+                         const Tensor& gscale, const optional<Tensor>& cbias, Tensor& out, int64_t c0, int64_t V,
+                         double eps, int64_t ignore, int64_t skip) {
+  check_lmhead_operands(h, w_slice, labels, cbias, V);
+  const int64_t N = h.size(0), K = h.size(1), n = w_slice.size(0);
+  TORCH_CHECK(n % 8 == 0 && c0 >= 0 && c0 + n <= V && skip >= 0 && skip < n, "lmhead_ce_bwd_slice: bad slice");
+  TORCH_CHECK(out.is_cuda() && out.device() == h.device() && out.scalar_type() == at::kBFloat16 && out.dim() == 2 &&
+                  out.size(0) == N && out.size(1) == n && out.stride(1) == 1 && out.stride(0) % 8 == 0 &&
+                  reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0 && 256 * out.stride(0) * 2 < (1LL << 31),
+              "lmhead_ce_bwd_slice: out must be a bf16 [N, n] GPU tensor, 16-B aligned rows");
+  TORCH_CHECK(lse.is_cuda() && lse.scalar_type() == at::kFloat && lse.is_contiguous() && lse.numel() == N,
+              "lmhead_ce_bwd_slice: lse must be fp32 [N]");
+  TORCH_CHECK(gscale.is_cuda() && gscale.scalar_type() == at::kFloat && gscale.numel() >= 1,
+              "lmhead_ce_bwd_slice: gscale must be a fp32 GPU scalar");
+  GemmW4Params P{};
+  P.A = reinterpret_cast<const uint16_t*>(h.data_ptr());
+  P.B = reinterpret_cast<const uint16_t*>(w_slice.data_ptr());
+  P.C = reinterpret_cast<uint16_t*>(out.data_ptr());
+  P.lda = h.stride(0); P.ldb = w_slice.stride(0); P.ldc = out.stride(0);
+  fill_w4_tiles(P, N, n, K);
+  P.labels = labels.data_ptr<int64_t>();
+  P.cbias = (cbias.has_value() && cbias->defined()) ? cbias->data_ptr<float>() : nullptr;
+  P.lse = lse.data_ptr<float>();
+  P.gscale = gscale.data_ptr<float>();
+  P.c0 = (int)c0; P.V = (int)V; P.skip = (int)skip; P.eps = (float)eps; P.ignore = ignore;
+  check_rc(dllm_gemm_w4(&P, 0, 1, 9, stream()), "lmhead_ce_bwd_slice (gemm_w4 CEB)");
+}
+
 bool gemm_w4_supported(const Tensor& a, const Tensor& b, bool b_kmajor) {
   auto ok2 = [](const Tensor& t) {
     return t.is_cuda() && t.dim() == 2 && t.scalar_type() == at::kBFloat16 && t.stride(1) == 1 && t.stride(0) % 8 == 0 &&
@@ -895,6 +1096,7 @@ void set_seed_step(const optional<Tensor>& step) {
   check_rc(dllm_set_seed_step_norm(p), "set_seed_step(norm)");
   check_rc(dllm_set_seed_step_act(p), "set_seed_step(act)");
   check_rc(dllm_set_seed_step_attn(p), "set_seed_step(attn)");
+  check_rc(dllm_set_seed_step_attn_f32(p), "set_seed_step(attn_f32)");
   check_rc(dllm_set_seed_step_gemm_fused(p), "set_seed_step(gemm_fused)");
   check_rc(dllm_set_seed_step_gemm_w4(p), "set_seed_step(gemm_w4)");
 }
@@ -932,6 +1134,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dv_out") = py::none(), py::arg("dmask") = py::none(), py::arg("sat_lo") = -1,
         py::arg("sat_hi") = -1);
   m.def("attn_params_size", []() { return dllm_attn_params_size(); });
+  m.def("attn_f32_fwd", &attn_f32_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("kpm"), py::arg("lut"),
+        py::arg("scale"), py::arg("causal"), py::arg("p"), py::arg("seed"));
+  m.def("attn_f32_bwd", &attn_f32_bwd, py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"),
+        py::arg("lse"), py::arg("kpm"), py::arg("lut"), py::arg("scale"), py::arg("causal"), py::arg("p"),
+        py::arg("seed"), py::arg("need_dlut"), py::arg("dq_out") = py::none(), py::arg("dk_out") = py::none(),
+        py::arg("dv_out") = py::none());
   m.def("gemm_wgrad", &gemm_wgrad, "c (+)= a^T b (token-major bf16 operands)", py::arg("a"), py::arg("b"), py::arg("c"),
         py::arg("beta") = true, py::arg("variant") = 0, py::arg("splits") = 0);
   m.def("gemm_wgrad_supported", &gemm_wgrad_supported);
@@ -948,6 +1156,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("accumulate") = false, py::arg("grp") = -1, py::arg("persist") = true, py::arg("epi") = 0,
         py::arg("p") = 0.0, py::arg("seed") = 0, py::arg("mask") = py::none(), py::arg("mask_pp") = false);
   m.def("gemm_w4_mask_words", &gemm_w4_mask_words);
+  m.def("lmhead_ce_fwd", &lmhead_ce_fwd, "LM-head GEMM + CE forward (gemm_w4 CE epilogue + row merge): (loss_rows, lse)");
+  m.def("lmhead_ce_bwd_slice", &lmhead_ce_bwd_slice, "dlogits of one vocabulary slice from the GEMM's CE epilogue");
   m.def("gemm_w4_supported", &gemm_w4_supported);
   m.def("beam_topk", &beam_topk);
   m.def("kv_reorder", &kv_reorder);

@@ -176,6 +176,38 @@ __global__ __launch_bounds__(256) void ce_chunk_bwd_kernel(const float* __restri
   }
 }
 
+// LM-head CE forward, fused path (ops/lm_head.py): merge the per-(row, 128-column) online-softmax partials the
+// W4_EPI_CEF GEMM epilogue wrote (csrc/gemm_w4.hip) into the row's lse and loss.  One wave per row.
+__global__ __launch_bounds__(256) void ce_merge_kernel(const f32x4* __restrict__ part, int np, long pstride,
+                                                       const float* __restrict__ xlab, const int64_t* __restrict__ labels,
+                                                       float* __restrict__ loss_out, float* __restrict__ lse_out, long N,
+                                                       int V, float eps, long ignore) {
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= N) return;
+  const f32x4* pr = part + row * pstride;
+  float m = -INFINITY, s = 0.f, sx = 0.f;
+  for (int c = lane; c < np; c += 64) {
+    const f32x4 v = pr[c];
+    const float nm = fmaxf(m, v.x);
+    if (nm != -INFINITY) {
+      s = (m == -INFINITY ? 0.f : s * __expf(m - nm)) + (v.x == -INFINITY ? 0.f : v.y * __expf(v.x - nm));
+      m = nm;
+    }
+    sx += v.z;
+  }
+  const float M = wave_max(m);
+  const float S = wave_sum(m == -INFINITY ? 0.f : s * __expf(m - M));
+  const float SX = wave_sum(sx);
+  if (lane == 0) {
+    const long y = labels[row];
+    const bool valid = y != ignore && y >= 0 && y < V;
+    const float lse = M + __logf(S);
+    loss_out[row] = valid ? lse - (1.f - eps) * xlab[row] - eps * SX / (float)V : 0.f;
+    lse_out[row] = lse;
+  }
+}
+
 }  // namespace
 
 extern "C" int dllm_ce_chunk_fwd(const void* logits, long ld, const int64_t* labels, const float* bias, float* state,
@@ -219,6 +251,15 @@ extern "C" int dllm_ce_bwd(const float* scale, const void* logits, const int64_t
   if (is_bf16) { if (vec) L(uint16_t, true); else L(uint16_t, false); }
   else { if (vec) L(float, true); else L(float, false); }
 #undef L
+  DLLM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dllm_ce_merge(const float* part, int np, long pstride, const float* xlab, const int64_t* labels,
+                             float* loss, float* lse, long N, int V, float eps, long ignore, hipStream_t st) {
+  if (N <= 0 || np <= 0 || pstride < np) return -2;
+  hipLaunchKernelGGL(ce_merge_kernel, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, st, (const f32x4*)part, np, pstride,
+                     xlab, labels, loss, lse, N, V, eps, ignore);
   DLLM_CHECK_LAUNCH();
   return 0;
 }

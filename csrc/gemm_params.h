@@ -37,6 +37,22 @@ struct GemmW4Params {
   float p, scale;  // dropout probability, 1 / (1 - p)
   uint32_t seed, thr;
   int mask_pp;  // DRELU_M: the mask was written by csrc/gemm_fused.hip's ping-pong ReLU forward (its thread layout)
+  // LM-head cross-entropy epilogues (NT: A = decoder hidden [M][K], B = a vocabulary slice of the tied embedding
+  // [N][K] = vocab columns [c0, c0 + N)):
+  //   W4_EPI_CEF  no C stores; per row and 128-column half tile the online-softmax partial {max, sum exp, sum x} ->
+  //               part[row * pstride + (n / 128)] (f32x4) and the label's logit -> xlab[row]
+  //   W4_EPI_CEB  C = dlogits = g * (exp(x - lse[row]) - eps / V - (1 - eps) [c0 + n == label])  (bf16)
+  // x = the fp32 accumulator (+ cbias[c0 + n]); columns n < skip (re-covered by a previous slice) and rows whose label
+  // is ignore / out of range contribute nothing
+  const int64_t* labels;
+  const float* cbias;   // [V] fp32 or null (BART final_logits_bias)
+  const float* lse;     // CEB: [M]
+  const float* gscale;  // CEB: device scalar g / count
+  float* part;          // CEF
+  float* xlab;          // CEF
+  int c0, V, skip, pstride;
+  float eps;
+  long ignore;
 };
 
 // csrc/gemm_fused.hip: C[M][N] = epi(A[M][K] . B), B = [N][K] (b_kmajor = 0) or [K][N] (b_kmajor = 1)

@@ -43,7 +43,8 @@ namespace {
 // epilogues: none; ReLU + dropout with the bit mask of kept positive outputs (forward, NT); the input gradient
 // through that mask, dU = dH * scale where the bit is set (backward, NN).  The mask is what the backward needs of
 // the forward: no re-read of H, no re-hash (T5 FFN, ops/ffn.py).
-enum { W4_EPI_NONE = 0, W4_EPI_RELU = 1, W4_EPI_DRELU_M = 7 };
+// LM-head cross-entropy (ops/lm_head.py): CEF = forward partials (no C), CEB = dlogits (gemm_params.h)
+enum { W4_EPI_NONE = 0, W4_EPI_RELU = 1, W4_EPI_DRELU_M = 7, W4_EPI_CEF = 8, W4_EPI_CEB = 9 };
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8v;
 typedef __attribute__((ext_vector_type(4))) short s16x4;
@@ -350,7 +351,8 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
       chunk(fa1, fb1, 0);
       __builtin_amdgcn_sched_barrier(0);
       if constexpr ((RS & 64) == 0) {
-        if (kt == 0 && g > 0 && !ACC) asm volatile("s_waitcnt vmcnt(32) lgkmcnt(0)" ::: "memory");
+        // after an epilogue its 32 C stores are the youngest VMEM ops (CEF stores fewer: drain everything)
+        if (kt == 0 && g > 0 && !ACC && EPI != W4_EPI_CEF) asm volatile("s_waitcnt vmcnt(32) lgkmcnt(0)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
       }
@@ -402,7 +404,61 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
     // kernel: tools/gemm_w4_bench.py --ablate).  Stores go through a buffer descriptor over the tile's rows: rows past
     // M fall out of its range, columns past N are pushed out per lane, so every wave issues exactly 32 stores (the
     // vmcnt(32) above counts them).
-    {
+    if constexpr (EPI == W4_EPI_CEF) {
+      // ---- LM-head CE forward: per row of the tile and per 128-column half (this wave's wn), the online-softmax
+      // partial {max, sum exp(x - max), sum x} of the valid vocabulary columns; the row's label logit from whichever
+      // lane holds that column.  The 4 lanes qd = 0..3 of a row hold its 4 x 8 columns: shuffles over lane >> 4.
+      const int nb = n0 + wn * 128 + 4 * qd;  // chunk-local column of acc[i][j][r]: nb + 16 j + r
+      float cb[8][4];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int n = nb + 16 * j + r;
+          cb[j][r] = (P.cbias != nullptr && n < P.N) ? P.cbias[P.c0 + n] : 0.f;
+        }
+      }
+      const int pcol = (n0 + wn * 128) >> 7;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int row = m0 + wm * 128 + 16 * i + rl;
+        const long yl = row < P.M ? P.labels[row] - (long)P.c0 - nb : -1;  // label column relative to this lane's
+        float xs[8][4];
+        float mx = -INFINITY;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          asm volatile("" : "+a"(acc[i][j]));
+          const f32x4 a = acc[i][j];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int n = nb + 16 * j + r;
+            const bool ok = n < P.N && n >= P.skip;
+            xs[j][r] = ok ? a[r] + cb[j][r] : -INFINITY;
+            mx = fmaxf(mx, xs[j][r]);
+          }
+        }
+        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        float se = 0.f, sx = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float x = xs[j][r];
+            se += x == -INFINITY ? 0.f : __expf(x - mx);
+            sx += x == -INFINITY ? 0.f : x;
+            if (yl == 16 * j + r && x != -INFINITY) P.xlab[row] = x;
+          }
+        }
+        se += __shfl_xor(se, 16, 64);
+        se += __shfl_xor(se, 32, 64);
+        sx += __shfl_xor(sx, 16, 64);
+        sx += __shfl_xor(sx, 32, 64);
+        if (qd == 0 && row < P.M)
+          *reinterpret_cast<f32x4*>(P.part + ((long)row * P.pstride + pcol) * 4) = f32x4{mx, se, sx, 0.f};
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else {
       // descriptor inputs made provably wave-uniform (readfirstlane), or hipcc wraps every store in a waterfall loop
       const uint64_t cb = (uint64_t)(P.C + (long)m0 * P.ldc);
       const uint32_t clo = __builtin_amdgcn_readfirstlane((uint32_t)cb), chi = __builtin_amdgcn_readfirstlane((uint32_t)(cb >> 32));
@@ -450,6 +506,22 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
         return u32x4{add2(o.x, c.x), add2(o.y, c.y), add2(o.z, c.z), add2(o.w, c.w)};
       };
       const int rowL = 16 * (qd & 1) + rl;                       // staging row written by this lane
+      // CEB: this lane's 8 rows (ii, half): lse, label column relative to the tile's column 0, row gradient scale
+      float ce_lse[8], ce_g[8];
+      int ce_y[8];
+      if constexpr (EPI == W4_EPI_CEB) {
+        const float gs = *P.gscale;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int row = m0 + wm * 128 + 32 * (q >> 1) + 16 * (q & 1) + rl;
+          const long y = row < P.M ? P.labels[row] : P.ignore;
+          const bool valid = row < P.M && y != P.ignore && y >= 0 && y < P.V;
+          ce_lse[q] = row < P.M ? P.lse[row] : 0.f;
+          ce_g[q] = valid ? gs : 0.f;
+          const long yt = y - (long)P.c0 - n0;
+          ce_y[q] = (yt >= 0 && yt < 256) ? (int)yt : -1;
+        }
+      }
 #pragma unroll
       for (int ii = 0; ii < 4; ++ii) {
 #pragma unroll
@@ -484,6 +556,21 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
             for (int r = 0; r < 4; ++r) {
               xv[r] = (mw[2 * ii] >> (4 * j + r)) & 1u ? xv[r] * P.scale : 0.f;
               yv[r] = (mw[2 * ii + 1] >> (4 * j + r)) & 1u ? yv[r] * P.scale : 0.f;
+            }
+          } else if constexpr (EPI == W4_EPI_CEB) {
+            // dlogits = g (softmax - (1 - eps) onehot - eps / V); xv: row q = 2 ii, yv: row q = 2 ii + 1
+            const float off = P.eps / (float)P.V, hit = 1.f - P.eps;
+            const int nt = wn * 128 + 16 * j + 4 * qd;  // tile column of r = 0
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int n = n0 + nt + r;
+              const bool ok = n < P.N && n >= P.skip;
+              const float b = (P.cbias != nullptr && n < P.N) ? P.cbias[P.c0 + n] : 0.f;
+              xv[r] = ok ? ce_g[2 * ii] * (__expf(xv[r] + b - ce_lse[2 * ii]) - off - (ce_y[2 * ii] == nt + r ? hit : 0.f))
+                         : 0.f;
+              yv[r] = ok ? ce_g[2 * ii + 1] *
+                               (__expf(yv[r] + b - ce_lse[2 * ii + 1]) - off - (ce_y[2 * ii + 1] == nt + r ? hit : 0.f))
+                         : 0.f;
             }
           }
           uint32_t x0 = pk2(xv.x, xv.y), x1 = pk2(xv.z, xv.w), y0 = pk2(yv.x, yv.y), y1 = pk2(yv.z, yv.w);
@@ -610,7 +697,10 @@ int dispatch(const GemmW4Params& p, bool persist, hipStream_t st) {
 // epi: W4_EPI_NONE, W4_EPI_RELU (NT, optional bias, no accumulate), W4_EPI_DRELU_M (NN, no bias, no accumulate)
 extern "C" int dllm_gemm_w4(const GemmW4Params* pp, int b_kmajor, int persist, int epi, hipStream_t st) {
   const GemmW4Params& p = *pp;
-  if (p.M <= 0 || p.N <= 0 || p.K <= 0 || p.K % BK || p.N % 8 || p.tm * 256 < p.M || p.tn * 256 < p.N) return -4;
+  // N % 8: 16-B C stores (CEF stores no C: any N)
+  if (p.M <= 0 || p.N <= 0 || p.K <= 0 || p.K % BK || (p.N % 8 && epi != W4_EPI_CEF) || p.tm * 256 < p.M ||
+      p.tn * 256 < p.N)
+    return -4;
   if (epi == W4_EPI_RELU) {
     if (b_kmajor || p.accumulate || p.mask == nullptr) return -5;
     return p.bias ? launch_rs<false, true, false, 1, W4_EPI_RELU>(p, persist != 0, st)
@@ -619,6 +709,15 @@ extern "C" int dllm_gemm_w4(const GemmW4Params* pp, int b_kmajor, int persist, i
   if (epi == W4_EPI_DRELU_M) {
     if (!b_kmajor || p.accumulate || p.bias || p.mask == nullptr) return -5;
     return launch_rs<true, false, false, 1, W4_EPI_DRELU_M>(p, persist != 0, st);
+  }
+  if (epi == W4_EPI_CEF || epi == W4_EPI_CEB) {
+    if (b_kmajor || p.accumulate || p.bias || p.labels == nullptr || p.skip < 0 || p.V <= 0) return -5;
+    if (epi == W4_EPI_CEF) {
+      if (p.part == nullptr || p.xlab == nullptr || p.pstride < (p.N + 127) / 128) return -5;
+      return launch_rs<false, false, false, 1, W4_EPI_CEF>(p, persist != 0, st);
+    }
+    if (p.lse == nullptr || p.gscale == nullptr) return -5;
+    return launch_rs<false, false, false, 1, W4_EPI_CEB>(p, persist != 0, st);
   }
   if (epi != W4_EPI_NONE) return -5;
   return b_kmajor ? dispatch<true>(p, persist != 0, st) : dispatch<false>(p, persist != 0, st);

@@ -22,7 +22,7 @@ from ..ops.ffn import ffn_res
 from ..ops.cross_entropy import cross_entropy
 from ..ops.embedding import embedding
 from ..ops.linear import Linear, linear, linear_res, stacked_linear
-from ..ops.lm_head import lm_head_loss, use_chunked
+from ..ops.lm_head import lm_head_loss, wants_lm_head_loss
 from ..ops.rng import default_rng
 from .blocks import run_block
 from .config import Seq2SeqConfig
@@ -275,8 +275,8 @@ class BartForConditionalGeneration(nn.Module):
             decoder_input_ids = self.shift_right(labels)
         dec = self.decode(decoder_input_ids, enc, attention_mask)
         loss = None
-        if labels is not None and not return_logits and use_chunked(labels.numel(), self.config.vocab_size):
-            # vocabulary-chunked LM head + CE with final_logits_bias (ops/lm_head.py)
+        if labels is not None and not return_logits and wants_lm_head_loss(dec, labels.numel(), self.config.vocab_size):
+            # LM head + CE with final_logits_bias, no materialised logits (ops/lm_head.py)
             loss = lm_head_loss(dec, self.output_embedding(), labels, bias=self.logits_bias(),
                                 label_smoothing=label_smoothing)
             return Seq2SeqLMOutput(loss=loss, logits=None, encoder_last_hidden_state=enc)

@@ -25,7 +25,7 @@ from ..ops.ffn import ffn, gated_ffn
 from ..ops.cross_entropy import cross_entropy
 from ..ops.embedding import embedding
 from ..ops.linear import Linear, linear, stacked_linear
-from ..ops.lm_head import lm_head_loss, use_chunked
+from ..ops.lm_head import lm_head_loss, wants_lm_head_loss
 from ..ops.rng import default_rng
 from .blocks import run_block
 from .config import Seq2SeqConfig
@@ -346,8 +346,8 @@ class T5ForConditionalGeneration(nn.Module):
         if decoder_input_ids is None:
             decoder_input_ids = self.shift_right(labels)
         dec = self.decode(decoder_input_ids, enc, attention_mask)
-        if labels is not None and not return_logits and use_chunked(labels.numel(), self.config.vocab_size):
-            # vocabulary-chunked LM head + CE: the [tokens, V] logits never exist (ops/lm_head.py)
+        if labels is not None and not return_logits and wants_lm_head_loss(dec, labels.numel(), self.config.vocab_size):
+            # LM head + CE without materialised logits: GEMM-epilogue CE or vocabulary chunks (ops/lm_head.py)
             scale = self.config.d_model ** -0.5 if self.config.scale_decoder_outputs else None
             loss = lm_head_loss(dec, self.output_embedding(), labels, scale=scale, label_smoothing=label_smoothing)
             return Seq2SeqLMOutput(loss=loss, logits=None, encoder_last_hidden_state=enc)

@@ -17,7 +17,8 @@ One op covers every attention variant the reference's models run (SURVEY.md §2.
 Layout: q ``[B, Sq, H, D]``, k/v ``[B, Sk, H, D]`` — the natural output of the fused QKV GEMM
 viewed without any transpose copy (only the last dim must be contiguous).  Output ``[B, Sq, H, D]``.
 
-Kernels: csrc/attn.hip (forward; backward = dQ kernel + dK/dV kernel, no atomics except the bias LUT).
+Kernels: csrc/attn.hip (bf16: forward; backward = dQ kernel + dK/dV kernel, no atomics except the bias LUT) and
+csrc/attn_f32.hip (fp32, the reference's own precision: the same op on the f32-input matrix cores, O(S) memory).
 """
 from __future__ import annotations
 
@@ -136,6 +137,12 @@ class _AttnFn(torch.autograd.Function):
     def forward(ctx, mode, a, b, c, lut, kpm, scale, causal, p, seed, pre=None):
         C = _ext.native()
         q, k, v = _split(mode, a, b, c)
+        if q.dtype == torch.float32:  # csrc/attn_f32.hip
+            o, lse = C.attn_f32_fwd(q, k, v, kpm, lut, float(scale), bool(causal), float(p), int(seed))
+            ctx.save_for_backward(a, b, c, o, lse, lut, kpm, None)
+            ctx.cfg = (mode, scale, causal, p, seed, lut is not None and lut.requires_grad, -1, -1)
+            ctx.grad_into = getattr(b, "_dllm_grad_into", None) if mode == "q_kv" else None
+            return o
         dmask_in = None
         if pre is not None:  # keep-bit planes generated ahead on the side stream (prefetch_dropout_mask)
             dmask_in, ev = pre
@@ -172,8 +179,12 @@ class _AttnFn(torch.autograd.Function):
             dq, dk, dv = da, db[:, :, 0], db[:, :, 1]
         else:
             dq = dk = dv = None
-        rq, rk, rv, dlut = C.attn_bwd(do.contiguous(), q, k, v, o, lse, kpm, lut, float(scale), bool(causal),
-                                      float(p), int(seed), bool(need_dlut), dq, dk, dv, dmask, sat_lo, sat_hi)
+        if q.dtype == torch.float32:
+            rq, rk, rv, dlut = C.attn_f32_bwd(do.contiguous(), q, k, v, o, lse, kpm, lut, float(scale), bool(causal),
+                                              float(p), int(seed), bool(need_dlut), dq, dk, dv)
+        else:
+            rq, rk, rv, dlut = C.attn_bwd(do.contiguous(), q, k, v, o, lse, kpm, lut, float(scale), bool(causal),
+                                          float(p), int(seed), bool(need_dlut), dq, dk, dv, dmask, sat_lo, sat_hi)
         if mode == "sep":
             da, db, dc = rq, rk, rv
         return None, da, db, dc, (dlut if need_dlut else None), None, None, None, None, None, None
@@ -186,12 +197,16 @@ def _prep_kpm(kpm):
 
 
 def _native(t) -> bool:
-    """The HIP flash kernels take bf16.  Other dtypes on the GPU — fp32 training, the reference's own precision
-    (ref/train-torchrun.py:115-128 sets neither bf16 nor fp16; Accelerate's default mixed_precision is 'no') — are
-    routed explicitly to the fp32 composite below (scores, bias, masks and dropout in fp32; the GEMMs run as fp32
-    library matmuls), which is the exact-math oracle the bf16 kernels are tested against.  Memory is O(S^2) per head
-    there, fine at the reference's fp32 batch sizes (1-6 per GPU)."""
-    return _ext.use_native(t) and t.dtype == torch.bfloat16
+    """bf16 -> csrc/attn.hip; fp32 — the reference's own precision (ref/train-torchrun.py:115-128 sets neither bf16
+    nor fp16; Accelerate's default mixed_precision is 'no') — -> csrc/attn_f32.hip (f32-input MFMA, exact f32
+    products).  Head dim 64 (every model this framework builds).  Anything else (CPU, other head dims) takes the
+    composite ``_reference`` below, the exact-math oracle the kernels are tested against.  ``DLLM_ATTN_F32=0`` sends
+    fp32 to the composite (A/B)."""
+    if not _ext.use_native(t) or t.shape[-1] != 64:
+        return False
+    if t.dtype == torch.bfloat16:
+        return True
+    return t.dtype == torch.float32 and os.environ.get("DLLM_ATTN_F32", "1") != "0"
 
 
 def attention(q, k, v, *, scale: float = 1.0, causal: bool = False, key_padding_mask=None, bias_lut=None,
@@ -219,7 +234,8 @@ def prefetch_dropout_mask(like: torch.Tensor, B: int, H: int, Sq: int, Sk: int, 
     """``DLLM_ATTN_MASK_STREAM=1``: generate the attention-dropout keep bits for an upcoming call on a side HIP
     stream, so the VALU-only mask kernel overlaps the (MFMA-bound) projection GEMM issued meanwhile on the
     compute stream.  Returns a handle for ``attention_qkv(pre=...)`` or None (mask hashed inside the forward)."""
-    if p <= 0.0 or os.environ.get("DLLM_ATTN_MASK_STREAM", "0") != "1" or not _native(like):
+    if (p <= 0.0 or os.environ.get("DLLM_ATTN_MASK_STREAM", "0") != "1" or not _native(like)
+            or like.dtype != torch.bfloat16):
         return None
     dev = like.device
     side = _SIDE.get(dev)

@@ -1,9 +1,16 @@
-"""Hand-written gfx950 GEMMs for every linear layer of a training step:
+"""GEMM routing for the linear layers of a training step.
 
-* projections, forward ``Y = X Wᵀ (+ b)`` and input gradient ``dX (+)= dY W`` (linear_fwd / linear_dgrad):
-  csrc/gemm_w4.hip, the one-wave-per-SIMD 256x256 kernel, on the shapes where it beats hipBLASLt (``_W4_MODE``
-  below; ``DLLM_W4_GEMM=1`` every supported shape, ``0`` none);
-* weight gradient ``dW (+)= dYᵀ X`` (wgrad_accumulate): csrc/gemm.hip.
+Who runs what (t5-base / bart-large training step, default settings):
+
+* weight gradients ``dW (+)= dYᵀ X`` (wgrad_accumulate): the hand-written csrc/gemm.hip kernel, accumulating straight
+  into the flat gradient buffer;
+* the FFN input GEMMs with their activation / dropout epilogues and the FFN backward through the activation
+  (ops/ffn.py): csrc/gemm_fused.hip and csrc/gemm_w4.hip;
+* the PLAIN projections — forward ``Y = X Wᵀ (+ b)`` and input gradient ``dX (+)= dY W`` of the attention q/k/v/o and
+  FFN output layers, and the LM head — go to the library (hipBLASLt through torch, with the TunableOp table in
+  configs/tunableop/): csrc/gemm_w4.hip ties it on these shapes in isolation and lost 0.8 % of the step in situ
+  (``_W4_MODE`` below, profiles/r3_w4_routing_ab.txt).  ``DLLM_W4_GEMM=1`` routes every supported shape to
+  csrc/gemm_w4.hip, ``auto`` the shapes it wins in isolation.
 
 Weight-gradient GEMM notes:
 
@@ -113,10 +120,14 @@ def bias_grad_accumulate(out: torch.Tensor, dy2: torch.Tensor, dy: torch.Tensor 
     autograd delivered it; when its producer already summed it over tokens (ops/norms.py x_bias_grad: the BART
     post-LN backward kernel) that fp32 column sum is added instead of re-reading dy."""
     global colsum_handoffs
-    cs = getattr(dy, "_dllm_colsum", None) if dy is not None else None
-    if cs is not None and cs.numel() == out.numel():
-        colsum_handoffs += 1
-        return out.add_(cs.view_as(out).to(out.dtype))
+    rec = getattr(dy, "_dllm_colsum", None) if dy is not None else None
+    if rec is not None:
+        cs, ver, shape, ptr = rec
+        # only while dy is still exactly the tensor the norm backward summed: same storage, shape and version (an
+        # in-place accumulation of another consumer's gradient bumps the version and the sum no longer describes dy)
+        if (cs.numel() == out.numel() and dy._version == ver and tuple(dy.shape) == shape and dy.data_ptr() == ptr):
+            colsum_handoffs += 1
+            return out.add_(cs.view_as(out).to(out.dtype))
     if _ext.use_native(dy2) and dy2.dtype == torch.bfloat16 and dy2.stride(-1) == 1 and dy2.shape[-1] % 2 == 0 \
             and dy2.stride(0) % 2 == 0 and out.is_contiguous():
         _ext.native().colsum_acc(dy2, out)

@@ -21,6 +21,15 @@ The price is one extra logits GEMM per step (the recompute); the gain is memory 
 ``DLLM_LMHEAD_FULL_MB`` (default 16384 MiB — sized for the 288 GB HBM: the t5-base bench at 512 samples per GPU keeps
 its 4 GiB of logits and runs 1.7 % faster than chunked, ``profiles/r3_lmhead_b512_ab.txt``; ``0`` = always chunked,
 ``-1`` = never), or explicitly by callers.
+
+GEMM-fused variant (``_LMHeadCEFusedFn``, ``DLLM_LMHEAD_FUSED=1``): the cross-entropy runs INSIDE the logits GEMM's
+epilogue (csrc/gemm_w4.hip W4_EPI_CEF / W4_EPI_CEB):
+
+* forward: ONE GEMM over the whole vocabulary whose epilogue reduces every row's 128-column half tile to an
+  online-softmax partial {max, Σexp, Σx} (+ the label's logit) straight from the fp32 accumulators — the logits are
+  never written, not even in bf16 — and csrc/ce.hip ``ce_merge`` folds the ``[N, V/128]`` partials into loss and lse;
+* backward: per vocabulary chunk the GEMM recomputes the logits and its epilogue writes ``g·(softmax - target)`` as
+  bf16 dlogits directly (no logits round trip, no separate CE pass), then the input- and weight-gradient GEMMs.
 """
 from __future__ import annotations
 
@@ -64,6 +73,14 @@ def use_chunked(N: int, V: int) -> bool:
     if lim < 0:
         return False
     return N * V * 2 > lim * 2**20
+
+
+def wants_lm_head_loss(hidden: torch.Tensor, N: int, V: int) -> bool:
+    """Whether a model's training loss goes through :func:`lm_head_loss` (no materialised logits): when the full
+    logits would be too large (use_chunked), or whenever the GEMM-fused CE applies (bf16 on the GPU)."""
+    if use_chunked(N, V):
+        return True
+    return (use_fused() and hidden.dtype == torch.bfloat16 and hidden.shape[-1] % 64 == 0 and _ext.use_native(hidden))
 
 
 def _reference(h, w, labels, bias, smoothing, ignore_index):
@@ -147,6 +164,63 @@ class _LMHeadCEFn(torch.autograd.Function):
         return dh.to(h.dtype), (dw.to(w.dtype) if dw is not None else None), None, None, None, None, None
 
 
+class _LMHeadCEFusedFn(torch.autograd.Function):
+    """LM head + CE with the CE inside the GEMM epilogues (module docstring, GEMM-fused variant)."""
+
+    @staticmethod
+    def forward(ctx, h, w, bias, labels, smoothing, ignore_index, params):
+        C = _ext.native()
+        bias32 = bias.float().reshape(-1).contiguous() if bias is not None else None
+        loss_rows, lse = C.lmhead_ce_fwd(h, w, labels, bias32, float(smoothing), int(ignore_index))
+        count = (labels != ignore_index).sum().clamp_min(1).to(torch.float32)
+        ctx.save_for_backward(h, w, labels, lse, count)
+        ctx.bias32 = bias32
+        ctx.cfg = (float(smoothing), int(ignore_index))
+        ctx.params = params
+        if params is not None:
+            _use(params[0])
+        return loss_rows.sum() / count
+
+    @staticmethod
+    def backward(ctx, g):
+        C = _ext.native()
+        h, w, labels, lse, count = ctx.saved_tensors
+        smoothing, ignore_index = ctx.cfg
+        N, d = h.shape
+        V = w.shape[0]
+        vc = _chunk_cols(N, V)
+        scale = (g.float() / count).reshape(1).contiguous()
+        p = ctx.params[0] if ctx.params is not None else None
+        gw = _gbuf(p) if p is not None else None
+        dw = torch.zeros_like(w, dtype=torch.float32) if (gw is None and ctx.needs_input_grad[1]) else None
+        dh = torch.zeros(N, d, dtype=torch.float32, device=h.device)
+        buf = torch.empty(N * min(vc + 8, V), dtype=h.dtype, device=h.device)
+        for c0, n, skip in _chunks(V, vc):
+            lg = buf[:N * n].view(N, n)
+            wc = w[c0:c0 + n]
+            C.lmhead_ce_bwd_slice(h, wc, labels, lse, scale, ctx.bias32, lg, c0, V, smoothing, ignore_index, skip)
+            _dh_accumulate(dh, lg, wc)
+            with torch.no_grad():
+                if gw is not None:
+                    wgrad_accumulate(gw[c0:c0 + n], lg, h)
+                elif dw is not None:
+                    dw[c0:c0 + n] += torch.mm(lg.t(), h)
+        if p is not None:
+            _fire(p)
+        return dh.to(h.dtype), (dw.to(w.dtype) if dw is not None else None), None, None, None, None, None
+
+
+def use_fused() -> bool:
+    return os.environ.get("DLLM_LMHEAD_FUSED", "1") != "0"
+
+
+def fused_ok(h: torch.Tensor, w: torch.Tensor) -> bool:
+    """Shapes the GEMM-epilogue CE handles (csrc/bind.cpp check_lmhead_operands): bf16, d % 64 == 0, 16-B rows."""
+    return (use_fused() and h.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and h.shape[-1] % 64 == 0
+            and w.stride(-1) == 1 and w.stride(0) % 8 == 0 and w.data_ptr() % 16 == 0 and h.data_ptr() % 16 == 0
+            and _ext.use_native(h))
+
+
 def lm_head_loss(hidden: torch.Tensor, weight: torch.Tensor, labels: torch.Tensor, *, scale: float | None = None,
                  bias: torch.Tensor | None = None, label_smoothing: float = 0.0, ignore_index: int = -100):
     """Mean (label-smoothed) CE of ``(hidden * scale) @ weightᵀ (+ bias)`` against ``labels`` over non-ignored rows,
@@ -163,4 +237,7 @@ def lm_head_loss(hidden: torch.Tensor, weight: torch.Tensor, labels: torch.Tenso
     if torch.is_grad_enabled() and _fusable(weight) and weight.requires_grad:
         params = (weight,)
         w = weight.detach()
-    return _LMHeadCEFn.apply(h.contiguous(), w, bias, lab.contiguous(), label_smoothing, ignore_index, params)
+    h = h.contiguous()
+    if fused_ok(h, w):
+        return _LMHeadCEFusedFn.apply(h, w, bias, lab.contiguous(), label_smoothing, ignore_index, params)
+    return _LMHeadCEFn.apply(h, w, bias, lab.contiguous(), label_smoothing, ignore_index, params)

@@ -73,7 +73,9 @@ class _NormFn(torch.autograd.Function):
                                               want_stream, *_acc_targets(ctx.params), want_colsum=ctx.colsum)
         dx = dx.view(shape)
         if ctx.colsum:  # handed to the producing linear layer's backward as its bias gradient (ops/gemm.py)
-            dx._dllm_colsum = dxs
+            # with the tensor's version: autograd may add a second consumer's gradient into dx in place, after which
+            # the column sum is stale (ops/gemm.py bias_grad_accumulate checks it)
+            dx._dllm_colsum = (dxs, dx._version, tuple(dx.shape), dx.data_ptr())
         # d(resid) == d(s) (pre-dropout gradient); identical to dx when p == 0
         dres = None
         if has_resid:

@@ -21,7 +21,11 @@ class TrainerState:
     best_metric: float | None = None
     total_flos: float = 0.0
     is_world_process_zero: bool = True
-    coalesce_cap: int | None = None  # samples per pass chosen for coalesced gradient accumulation (0 = off); resume reuses it
+    # coalesced gradient accumulation: the per-pass budget chosen (0 = off) and its unit; a resumed run reuses it.
+    # "padded_tokens" (samples x padded source + target length, Trainer._padded_tokens); checkpoints written before the
+    # unit was recorded hold a budget in samples (unit None)
+    coalesce_cap: int | None = None
+    coalesce_cap_unit: str | None = None
 
     def save_to_json(self, path):
         with open(path, "w") as f:
@@ -30,7 +34,9 @@ class TrainerState:
     @classmethod
     def load_from_json(cls, path):
         with open(path) as f:
-            return cls(**json.load(f))
+            d = json.load(f)
+        known = {f.name for f in dataclasses.fields(cls)}
+        return cls(**{k: v for k, v in d.items() if k in known})
 
 
 @dataclass

@@ -96,16 +96,22 @@ class GraphedStep:
         self.t.fill_(float(opt.step_count))
         self._t_host = opt.step_count
         torch.cuda.empty_cache()  # eager blocks cached by the warmup are not usable by the graph's private pool
+        # thread-local capture mode: only the capturing thread is barred from capture-unsafe HIP calls.  With the
+        # default ("global") an unrelated thread's call during capture invalidates it — ProcessGroupNCCL's watchdog
+        # thread polls the events of the warmup's all-reduces and aborts the process on that error (seen on a 1-rank
+        # RCCL group).  Backward kernels launched from autograd's device thread onto the capture stream are captured
+        # either way (capture is a property of the stream).
+        mode = "thread_local"
         if self.comm == "split":
             self.g_fb = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.g_fb):
+            with torch.cuda.graph(self.g_fb, capture_error_mode=mode):
                 self.loss = self._fb(sync=False)
             self.g_opt = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.g_opt):
+            with torch.cuda.graph(self.g_opt, capture_error_mode=mode):
                 self.norm = self._opt()
         else:
             self.graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.graph):
+            with torch.cuda.graph(self.graph, capture_error_mode=mode):
                 self.loss = self._fb(sync=True)
                 self.norm = self._opt()
         self._host_after_capture()  # the capture ran the Python side once but executed nothing

@@ -245,6 +245,7 @@ class Trainer:
                 ts = info.get("trainer_state", {})
                 self.state.global_step = ts.get("global_step", 0)
                 self.state.coalesce_cap = ts.get("coalesce_cap")
+                self.state.coalesce_cap_unit = ts.get("coalesce_cap_unit")
                 self.state.log_history = ts.get("log_history", [])
                 step_seed_start = info.get("step_seed")
                 start_epoch = self.state.global_step // steps_per_epoch
@@ -261,8 +262,13 @@ class Trainer:
         ga = args.gradient_accumulation_steps
         cap = self._coalesce_cap()
         cap_units = "micro" if cap is not None and cap > 0 else "tokens"
-        if cap == -1 and self.state.coalesce_cap is not None:  # resumed: the original run's choice (same RNG stream)
-            cap = self.state.coalesce_cap or None
+        if cap is not None and self.state.coalesce_cap is not None:  # resumed: the original run's budget, same unit
+            if self.state.coalesce_cap_unit == "padded_tokens":
+                cap, cap_units = (self.state.coalesce_cap or None), "tokens"
+            elif self.state.coalesce_cap:  # legacy checkpoint: a budget in samples, converted at the first group
+                cap, cap_units = self.state.coalesce_cap, "samples"
+            else:
+                cap = None
         pad_id = getattr(getattr(self.model, "config", None), "pad_token_id", 0) or 0
         # the optimizer step (passes + sync + clip + AdamW) replayed from HIP graphs once batch shapes repeat
         # (train/graph.py StepRunner; the reference pads to max_length, so every full step has one shape); context
@@ -297,8 +303,14 @@ class Trainer:
                     if self.cp_group is not None:  # every CP rank of a DP group counted the same batch
                         num_items = num_items // (self.env.world_size // self.dp_world)
                 passes = [[b] for b in group]
-                if cap is not None and cap > 0 and cap_units == "micro":  # explicit setting: k micro-batches
-                    cap, cap_units = cap * self._padded_tokens(group[:1]), "tokens"
+                if cap is not None and cap > 0 and cap_units in ("micro", "samples"):
+                    # explicit setting (k micro-batches) or a legacy sample budget -> padded tokens at this group's
+                    # lengths, recorded so that a resumed run groups its passes exactly like this one
+                    per = self._padded_tokens(group[:1])
+                    if cap_units == "samples":
+                        per = per // max(1, group[0]["labels"].shape[0])
+                    cap, cap_units = cap * per, "tokens"
+                    self.state.coalesce_cap, self.state.coalesce_cap_unit = cap, "padded_tokens"
                 if cap is not None and cap > 0:  # coalesced: consecutive micro-batches, <= cap padded tokens per pass
                     passes, cur = [], []
                     for b in group:
@@ -319,7 +331,7 @@ class Trainer:
                     torch.cuda.synchronize()
                     cap = self._auto_cap(mem_base, torch.cuda.max_memory_allocated(env.device),
                                          max(self._padded_tokens([b]) for b in group))
-                    self.state.coalesce_cap = cap or 0
+                    self.state.coalesce_cap, self.state.coalesce_cap_unit = cap or 0, "padded_tokens"
                 self.scheduler.step()
                 self.state.global_step += 1
                 if self.state.global_step in (warm_step, max_steps):  # steady-state clock: after the first steps,

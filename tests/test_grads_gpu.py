@@ -222,12 +222,16 @@ def test_global_token_normalisation_equals_full_batch_mean():
     assert _rel(alt.flat.grad_buf, ref_eng.flat.grad_buf) > 3 * _rel(g, ref_eng.flat.grad_buf)
 
 
+@pytest.mark.parametrize("fused", ["1", "0"])
 @pytest.mark.parametrize("bias,smooth,V", [(False, 0.0, 32128), (True, 0.1, 50265), (False, 0.1, 4000)])
-def test_lm_head_chunked_ce_matches_fp32(bias, smooth, V, monkeypatch):
-    """Vocab-chunked LM head + CE (ops/lm_head.py) vs F.cross_entropy on fp32 logits: loss, dh, dW (flat buffer)."""
+def test_lm_head_chunked_ce_matches_fp32(bias, smooth, V, fused, monkeypatch):
+    """LM head + CE without materialised logits (ops/lm_head.py) vs F.cross_entropy on fp32 logits: loss, dh, dW (flat
+    buffer).  fused=1: CE inside the GEMM epilogues (csrc/gemm_w4.hip CEF / CEB + csrc/ce.hip merge); 0: vocab chunks."""
+    from distributed_llms_example_amd.ops import lm_head as LH
     from distributed_llms_example_amd.ops.lm_head import lm_head_loss
     from distributed_llms_example_amd.parallel.flat import FlatParams
     monkeypatch.setenv("DLLM_LMHEAD_CHUNK_MB", "8")  # several chunks, ragged last one
+    monkeypatch.setenv("DLLM_LMHEAD_FUSED", fused)
     torch.manual_seed(0)
     N, d = 1000, 768
     emb = torch.nn.Embedding(V, d).cuda().to(torch.bfloat16)
@@ -238,8 +242,13 @@ def test_lm_head_chunked_ce_matches_fp32(bias, smooth, V, monkeypatch):
     labels = torch.randint(0, V, (N,), device=DEV)
     labels[::7] = -100
     b = (torch.randn(V, device=DEV) * 0.1) if bias else None
+    calls = []
+    if fused == "1":  # the GEMM-epilogue path must be the one that runs
+        real = LH._LMHeadCEFusedFn.apply
+        monkeypatch.setattr(LH._LMHeadCEFusedFn, "apply", lambda *a: (calls.append(1), real(*a))[1])
     loss = lm_head_loss(h, emb.weight, labels, scale=0.5, bias=b, label_smoothing=smooth)
     loss.backward()
+    assert calls == ([1] if fused == "1" else [])
     hr = h.detach().float().requires_grad_(True)
     wr = emb.weight.detach().float().requires_grad_(True)
     logits = (hr * 0.5) @ wr.t() + (b if bias else 0)
@@ -257,6 +266,7 @@ def test_t5_chunked_lm_head_matches_full(monkeypatch):
     sd = build_model(cfg).state_dict()
     b = _micro_batches(cfg, n=1, B=4)[0]
     res = []
+    monkeypatch.setenv("DLLM_LMHEAD_FUSED", "0")  # this test pins the vocab-chunked path against full logits
     for full_mb in ("-1", "0"):
         monkeypatch.setenv("DLLM_LMHEAD_FULL_MB", full_mb)
         eng = _engine(cfg, sd, torch.float32)
@@ -264,3 +274,22 @@ def test_t5_chunked_lm_head_matches_full(monkeypatch):
         res.append((float(loss), eng.flat.grad_buf.clone()))
     assert abs(res[0][0] - res[1][0]) < 1e-3 * res[0][0]
     assert _rel(res[1][1], res[0][1]) < 1e-2, _rel(res[1][1], res[0][1])
+
+
+def test_t5_fused_lm_head_matches_materialised_logits(monkeypatch):
+    """bf16 T5: the loss / flat gradient with the GEMM-epilogue CE == with materialised bf16 logits + the CE kernels
+    (fp32 logits inside the epilogue vs bf16-rounded ones: bf16-noise agreement)."""
+    cfg = _small_cfg()
+    torch.manual_seed(0)
+    sd = build_model(cfg).state_dict()
+    b = _micro_batches(cfg, n=1, B=4)[0]
+    monkeypatch.setenv("DLLM_LMHEAD_FULL_MB", "-1")
+    res = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("DLLM_LMHEAD_FUSED", fused)
+        eng = _engine(cfg, sd, torch.float32)
+        eng.train(False)
+        loss = eng.forward_backward(b)
+        res.append((float(loss), eng.flat.grad_buf.float().clone()))
+    assert abs(res[0][0] - res[1][0]) < 5e-3 * res[1][0], (res[0][0], res[1][0])
+    assert _rel(res[0][1], res[1][1]) < 3e-2, _rel(res[0][1], res[1][1])
