@@ -22,8 +22,8 @@ The price is one extra logits GEMM per step (the recompute); the gain is memory 
 its 4 GiB of logits and runs 1.7 % faster than chunked, ``profiles/r3_lmhead_b512_ab.txt``; ``0`` = always chunked,
 ``-1`` = never), or explicitly by callers.
 
-GEMM-fused variant (``_LMHeadCEFusedFn``, ``DLLM_LMHEAD_FUSED=1``): the cross-entropy runs INSIDE the logits GEMM's
-epilogue (csrc/gemm_w4.hip W4_EPI_CEF / W4_EPI_CEB):
+GEMM-fused variant (``_LMHeadCEFusedFn``, the no-materialised-logits path unless ``DLLM_LMHEAD_FUSED=0``; see
+``use_fused``): the cross-entropy runs INSIDE the logits GEMM's epilogue (csrc/gemm_w4.hip W4_EPI_CEF / W4_EPI_CEB):
 
 * forward: ONE GEMM over the whole vocabulary whose epilogue reduces every row's 128-column half tile to an
   online-softmax partial {max, Σexp, Σx} (+ the label's logit) straight from the fp32 accumulators — the logits are
@@ -77,10 +77,11 @@ def use_chunked(N: int, V: int) -> bool:
 
 def wants_lm_head_loss(hidden: torch.Tensor, N: int, V: int) -> bool:
     """Whether a model's training loss goes through :func:`lm_head_loss` (no materialised logits): when the full
-    logits would be too large (use_chunked), or whenever the GEMM-fused CE applies (bf16 on the GPU)."""
+    logits would exceed ``DLLM_LMHEAD_FULL_MB`` (use_chunked), or always with ``DLLM_LMHEAD_FUSED=1`` (bf16 GPU)."""
     if use_chunked(N, V):
         return True
-    return (use_fused() and hidden.dtype == torch.bfloat16 and hidden.shape[-1] % 64 == 0 and _ext.use_native(hidden))
+    return (os.environ.get("DLLM_LMHEAD_FUSED", "auto") == "1" and hidden.dtype == torch.bfloat16
+            and hidden.shape[-1] % 64 == 0 and _ext.use_native(hidden))
 
 
 def _reference(h, w, labels, bias, smoothing, ignore_index):
@@ -211,7 +212,12 @@ class _LMHeadCEFusedFn(torch.autograd.Function):
 
 
 def use_fused() -> bool:
-    return os.environ.get("DLLM_LMHEAD_FUSED", "1") != "0"
+    """The GEMM-epilogue CE (``_LMHeadCEFusedFn``) in place of the vocabulary-chunked path.  ``DLLM_LMHEAD_FUSED``:
+    ``auto`` (default) = whenever logits are not materialised (it beats the chunked path: no logits round trip, no CE
+    passes); ``1`` = also below the full-logits budget; ``0`` = never.  Below the budget the materialised-logits path
+    stays the default: it skips the backward's logits recompute and was 1.0 % faster per t5-base b=512 step
+    (profiles/r4_lmhead_fused_ab.txt)."""
+    return os.environ.get("DLLM_LMHEAD_FUSED", "auto") != "0"
 
 
 def fused_ok(h: torch.Tensor, w: torch.Tensor) -> bool:

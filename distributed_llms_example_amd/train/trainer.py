@@ -278,6 +278,7 @@ class Trainer:
         if runner.enabled and step_seed_start is not None:
             eng.enable_step_seeds(step_seed_start)
         self.step_runner = runner
+        self._batch_shape = None
         if cap == -1:
             torch.cuda.synchronize()
             torch.cuda.reset_peak_memory_stats(env.device)
@@ -296,6 +297,10 @@ class Trainer:
                 # one optimizer step = the next ga micro-batches (fewer at the end of the epoch), normalised by
                 # their global non-ignored target-token count (one int64 all-reduce per step)
                 group = [self._to_device(next(it), cp=True) for _ in range(min(ga, n_micro - done))]
+                if self._batch_shape is None:
+                    b0 = group[0]
+                    self._batch_shape = [int(b0["labels"].shape[0]), int(b0["input_ids"].shape[1]),
+                                         int(b0["labels"].shape[1])]
                 done += len(group)
                 num_items = sum(token_count(b["labels"]) for b in group)
                 if self.dp_world > 1:
@@ -387,6 +392,9 @@ class Trainer:
             per_step = args.per_device_train_batch_size * ga * self.dp_world
             dt = t_last - t_warm
             metrics["train_steady_samples_per_second"] = round(per_step * (self.state.global_step - warm_step) / dt, 3)
+        if self._batch_shape is not None:  # what the throughput was measured on: per-GPU micro-batch, padded lengths
+            metrics["batch_shape"] = self._batch_shape
+            metrics["hip_graph_replays"] = self.step_runner.replays
         self.log(metrics)
         self.handler.fire("on_train_end", args, self.state, self.control)
         return TrainOutput(self.state.global_step, train_loss, metrics)

@@ -283,7 +283,7 @@ def test_t5_fused_lm_head_matches_materialised_logits(monkeypatch):
     torch.manual_seed(0)
     sd = build_model(cfg).state_dict()
     b = _micro_batches(cfg, n=1, B=4)[0]
-    monkeypatch.setenv("DLLM_LMHEAD_FULL_MB", "-1")
+    monkeypatch.setenv("DLLM_LMHEAD_FULL_MB", "-1")  # never chunked: "1" forces the fused path, "0" full logits
     res = []
     for fused in ("1", "0"):
         monkeypatch.setenv("DLLM_LMHEAD_FUSED", fused)

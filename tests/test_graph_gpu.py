@@ -76,7 +76,8 @@ def _eager_reference(cfg, data, ga, steps, force_reducer=False):
         eng_e.step(hyper=eng_e.optimizer.device_hyper(t, eng_e.optimizer.param_groups[0]["lr"]))
         if i >= 2:
             losses_e.append(tot / ga)
-    pe = eng_e.flat.param_buf.float().clone()
+    # canonical layout: a synchronised eager backward re-lays the flat buffers in gradient-ready order (reducer rebuild)
+    pe = eng_e.flat.to_canonical(eng_e.flat.param_buf).float().clone()
     eng_e.disable_step_seeds()
     return losses_e, pe
 
@@ -89,7 +90,7 @@ def test_graphed_steps_match_eager(ga):
     data = _batches(cfg, ga * (steps + 2))
     gs = GraphedStep(eng_g, data[:ga], warmup=2)  # 2 warmup steps on data[:ga]
     losses_g = [float(gs.replay(data[ga * (2 + i):ga * (3 + i)])) for i in range(steps)]
-    pg = eng_g.flat.param_buf.float().clone()
+    pg = eng_g.flat.to_canonical(eng_g.flat.param_buf).float().clone()
     assert int(eng_g.step_seed.t.item()) == eng_g.step_seed.host == ga * (steps + 2)
     eng_g.disable_step_seeds()
 
@@ -144,7 +145,7 @@ def test_graphed_data_parallel_step_on_one_rank_rccl(comm):
         data = _batches(cfg, ga * (steps + 2))
         gs = GraphedStep(eng_g, data[:ga], warmup=2, comm=comm)
         losses_g = [float(gs.replay(data[ga * (2 + i):ga * (3 + i)])) for i in range(steps)]
-        pg = eng_g.flat.param_buf.float().clone()
+        pg = eng_g.flat.to_canonical(eng_g.flat.param_buf).float().clone()
         eng_g.disable_step_seeds()
         eng_g.reducer.remove()
         losses_e, pe = _eager_reference(cfg, data, ga, steps, force_reducer=True)

@@ -82,6 +82,7 @@ class ModelTrainer:
         train_step = acc.make_train_step(model, optimizer)
         self.logger.info(f"***** Running training ***** examples={len(train_ds)} epochs={a.num_epochs}")
         completed = 0
+        shape = None
         t0 = time.perf_counter()
         t_warm, warm = None, min(2, max(0, max_train_steps - 1))
         for epoch in range(a.num_epochs):
@@ -93,6 +94,7 @@ class ModelTrainer:
                 loss = train_step(batch)
                 lr_scheduler.step()
                 completed += 1
+                shape = [int(batch["input_ids"].shape[1]), int(batch["labels"].shape[1])]
                 if completed == warm:
                     torch.cuda.synchronize() if acc.device.type == "cuda" else None
                     t_warm = time.perf_counter()
@@ -104,7 +106,9 @@ class ModelTrainer:
             torch.cuda.synchronize() if acc.device.type == "cuda" else None
             t1 = time.perf_counter()
             per_step = a.batch_size * acc.num_processes
-            tp = {"train_samples_per_second": round(per_step * completed / (t1 - t0), 3), "epoch": epoch}
+            tp = {"train_samples_per_second": round(per_step * completed / (t1 - t0), 3), "epoch": epoch,
+                  "batch_shape": [a.batch_size] + (shape or []),  # per-GPU batch, padded source / target tokens
+                  "hip_graph_replays": train_step.runner.replays}
             if t_warm is not None and completed > warm:
                 tp["train_steady_samples_per_second"] = round(per_step * (completed - warm) / (t1 - t_warm), 3)
             self.dump(tp)
