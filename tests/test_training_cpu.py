@@ -353,3 +353,52 @@ def test_native_build_provenance_detects_stale_sources(tmp_path, monkeypatch):
     assert _ext.stale_sources() == []
     (csrc / "norm.hip").write_text((csrc / "norm.hip").read_text() + "\n// edited\n")
     assert _ext.stale_sources() == ["norm.hip"]
+
+
+def test_step_runner_schedule_matches_eager_steps(monkeypatch):
+    """train/graph.py StepRunner (what every entry point runs): eager warmup per batch shape, then capture + replays,
+    eager steps for other shapes — run here with the graph's eager schedule (GraphedStep use_graph=False), it must
+    give exactly the parameters of plain eager steps with the same dropout stream, and count replays correctly."""
+    import functools
+    from distributed_llms_example_amd.models import build_model
+    from distributed_llms_example_amd.ops.rng import manual_seed
+    from distributed_llms_example_amd.parallel.env import DistEnv
+    from distributed_llms_example_amd.train import graph as G
+    from distributed_llms_example_amd.train.engine import TrainEngine
+
+    env = DistEnv()
+    g = torch.Generator().manual_seed(1)
+
+    def batch(B, S=12, T=6):
+        return {"input_ids": torch.randint(3, 500, (B, S), generator=g),
+                "attention_mask": torch.ones(B, S, dtype=torch.long), "labels": torch.randint(3, 500, (B, T), generator=g)}
+
+    data = [batch(2) for _ in range(6)] + [batch(1)] + [batch(2)]  # a ragged batch between full ones
+
+    def engine():
+        torch.manual_seed(0)
+        manual_seed(5)
+        e = TrainEngine(build_model("t5-tiny"), env, lr=1e-3, dtype=torch.float32)
+        e.train()
+        return e
+
+    monkeypatch.setattr(G, "GraphedStep", functools.partial(G.GraphedStep, use_graph=False))
+    eng_r = engine()
+    runner = G.StepRunner(eng_r, enabled=True, warmup=2)
+    lr = [1e-3, 9e-4, 8e-4, 7e-4, 6e-4, 5e-4, 4e-4, 3e-4]
+    lr_run = [float(runner([b], lr=l)[0][0]) for b, l in zip(data, lr)]
+    assert runner.graph is not None and runner.graph_error is None
+    # shapes [2]: eager x2 (warmup), capture + replay, replays ...; the batch of 1 runs eagerly
+    assert runner.replays == 5 and runner.eager_steps == 3, (runner.replays, runner.eager_steps)
+    p_run = eng_r.flat.param_buf.clone()
+    eng_r.disable_step_seeds()
+
+    eng_e = engine()
+    eng_e.enable_step_seeds()
+    le = []
+    for b, l in zip(data, lr):
+        le.append(float(eng_e.forward_backward(b)))
+        eng_e.step(lr=l)
+    eng_e.disable_step_seeds()
+    assert lr_run == pytest.approx(le, rel=1e-6, abs=1e-7)
+    assert torch.allclose(p_run, eng_e.flat.param_buf, rtol=1e-5, atol=1e-7)
