@@ -15,7 +15,7 @@
 //   forward    grid (Sq/64, B*H), 4 waves x 16 query rows; per 64-key block: K (row-major) and V (transposed) staged in
 //              LDS, S^T = K Q^T (64 MFMAs / wave), online softmax + dropout in registers, O^T += V^T P^T (64 MFMAs).
 //   dQ         grid (Sq/64, B*H): S^T, dP^T = V dO^T, dS = P (dP_kept - delta), dQ^T += K^T dS^T; the bias gradient is
-//              summed per diagonal in LDS and added to dlut once per block (fp32 atomics).
+//              summed per diagonal of the block's dS tile in LDS and added to dlut once per block (fp32 atomics).
 //   dK / dV    grid (Sk/64, B*H), 4 waves x 16 keys: S = Q K^T, dP = dO V^T, dV += P_kept^T dO, dK += dS^T Q.
 #include "common.h"
 
@@ -246,7 +246,7 @@ __global__ __launch_bounds__(NT) void attn_f32_dq_kernel(AttnF32Params P) {
   __shared__ __attribute__((aligned(16))) float Kt[D * BKY];
   __shared__ __attribute__((aligned(16))) float Vs[BKY * D];
   __shared__ float Ls[2 * BKY];
-  __shared__ float Dl[2 * BKY];
+  __shared__ float Ds[BQ * (BKY + 1)];  // dS tile of the block, row stride 65: a diagonal walk is bank-conflict free
   __shared__ uint8_t Mk[BKY];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, c = lane & 15;
   const int bh = blockIdx.y, b = bh / P.H, h = bh % P.H;
@@ -288,7 +288,6 @@ __global__ __launch_bounds__(NT) void attn_f32_dq_kernel(AttnF32Params P) {
       idx = idx < 0 ? 0 : (idx >= L ? L - 1 : idx);
       Ls[tid] = P.lut[(long)h * L + idx];
     }
-    if (want_dlut && tid < 2 * BKY) Dl[tid] = 0.f;
     if (tid < BKY) Mk[tid] = key_ok(P, b, k0 + tid);
     __syncthreads();
     f32x4 st[4], dpt[4];
@@ -319,7 +318,7 @@ __global__ __launch_bounds__(NT) void attn_f32_dq_kernel(AttnF32Params P) {
         const float dpk = DROP ? (((kb4 >> i) & 1u) ? dpt[t][i] * dscale : 0.f) : dpt[t][i];
         const float ds = pr * (dpk - dlt);
         st[t][i] = ds;
-        if (want_dlut && row_ok && ds != 0.f) atomicAdd(&Dl[di], ds);
+        if (want_dlut) Ds[(16 * w + c) * (BKY + 1) + 16 * t + 4 * g + i] = ds;  // 0 for rows >= Sq (lse = inf)
       }
     }
 #pragma unroll
@@ -334,10 +333,15 @@ __global__ __launch_bounds__(NT) void attn_f32_dq_kernel(AttnF32Params P) {
       }
     }
     if (want_dlut) {
+      // bias gradient: per diagonal d = key - row + 63 of the 64x64 block, one thread walks its diagonal in the dS
+      // tile (LDS reads, no atomics) and adds the sum to dlut once
       __syncthreads();
       if (tid < 2 * BKY - 1) {
-        const float v = Dl[tid];
-        const long idx = (long)k0 - q0 - 63 + tid + P.Sq - 1;
+        const int d = tid;
+        const int r0 = d < 63 ? 63 - d : 0, r1 = d < 63 ? 63 : 126 - d;
+        float v = 0.f;
+        for (int r = r0; r <= r1; ++r) v += Ds[r * (BKY + 1) + r + d - 63];
+        const long idx = (long)k0 - q0 - 63 + d + P.Sq - 1;
         if (v != 0.f && idx >= 0 && idx < L) atomicAdd(&P.dlut[(long)h * L + idx], v);
       }
     }

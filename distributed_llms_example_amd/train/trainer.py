@@ -284,6 +284,7 @@ class Trainer:
             torch.cuda.reset_peak_memory_stats(env.device)
             mem_base = torch.cuda.memory_allocated(env.device)
         warm_step = self.state.global_step + min(2, max(0, max_steps - self.state.global_step - 1))
+        captured_at = None
         t_warm = t_last = None
         for epoch in range(start_epoch, epochs):
             loader, sampler = self._loader(self.train_dataset, args.per_device_train_batch_size, True, epoch)
@@ -339,6 +340,10 @@ class Trainer:
                     self.state.coalesce_cap, self.state.coalesce_cap_unit = cap or 0, "padded_tokens"
                 self.scheduler.step()
                 self.state.global_step += 1
+                if runner.replays and captured_at is None:  # the step that captured the HIP graph is warm-up too
+                    captured_at = self.state.global_step
+                    if captured_at < max_steps:
+                        warm_step = max(warm_step, captured_at)
                 if self.state.global_step in (warm_step, max_steps):  # steady-state clock: after the first steps,
                     if env.device.type == "cuda":                      # before the final eval / checkpoint
                         torch.cuda.synchronize()

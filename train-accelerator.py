@@ -95,6 +95,8 @@ class ModelTrainer:
                 lr_scheduler.step()
                 completed += 1
                 shape = [int(batch["input_ids"].shape[1]), int(batch["labels"].shape[1])]
+                if train_step.runner.replays == 1 and completed < max_train_steps:
+                    warm = completed  # the step that captured the HIP graph is warm-up too
                 if completed == warm:
                     torch.cuda.synchronize() if acc.device.type == "cuda" else None
                     t_warm = time.perf_counter()
