@@ -55,6 +55,8 @@ if ROOT not in sys.path:
 # BASELINE.md publishes no number, so vs_baseline compares against this comparator scaled linearly
 # with N (an upper bound for the reference's own scaling).
 HF_COMPARATOR_SAMPLES_PER_S_1GPU = {16: 107.4, 32: 132.0, 64: 150.7, 128: 155.3}
+# the same stack in fp32 (the reference's own precision: no AMP configured, ref/train-torchrun.py:115-128)
+HF_COMPARATOR_FP32_SAMPLES_PER_S_1GPU = {16: 76.7}
 # other BASELINE.json configs, same comparator tool (profiles/configs/hf_*.json): (model, per-GPU batch) -> samples/s
 HF_COMPARATOR_OTHER = {("bart-large", 32): 269.7, ("t5-large", 16): 46.6, ("flan-t5-xl", 8): 16.2}
 
@@ -312,8 +314,9 @@ def main():
     if a.model == "t5-base":
         metric = "samples/sec (whole node) T5-base summarization fine-tune at 1/2/4/8 MI355X"
         # the HF stack at the same per-GPU batch, or at its largest measured one below it (it does not fit above 128)
-        base_batch = max((bb for bb in HF_COMPARATOR_SAMPLES_PER_S_1GPU if bb <= B), default=None)
-        base = HF_COMPARATOR_SAMPLES_PER_S_1GPU.get(base_batch)
+        table = HF_COMPARATOR_FP32_SAMPLES_PER_S_1GPU if dtype_name == "fp32" else HF_COMPARATOR_SAMPLES_PER_S_1GPU
+        base_batch = max((bb for bb in table if bb <= B), default=None)
+        base = table.get(base_batch)
     elif (a.src_len, a.tgt_len) != (1024, 128):  # comparators were measured at the 1024/128 shapes only
         metric = f"samples/sec (whole node) {a.model} summarization fine-tune, {a.src_len}/{a.tgt_len} tokens"
         base, base_batch = None, None
@@ -328,9 +331,9 @@ def main():
             "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
             "mfu": round(mfu, 4), "tflops_per_gpu": round(step_flops / (ms * 1e-3) / n / 1e12, 1),
             "vs_baseline": round(value / (base * n), 3) if base and B >= 16 else None,
-            "baseline_note": f"HF transformers+torch stack measured on 1x MI355X at the same sequence shapes (its "
-                             f"per-GPU batch {base_batch}, samples/s compared per sample) x N (BASELINE.md publishes "
-                             f"no number)",
+            "baseline_note": f"HF transformers+torch stack ({dtype_name}) measured on 1x MI355X at the same sequence "
+                             f"shapes (its per-GPU batch {base_batch}, samples/s compared per sample) x N (BASELINE.md "
+                             f"publishes no number)",
             "dtype": dtype_name, "data": "synthetic (random token ids, random-init weights)",
             "config": {"model": a.model, "global_batch": B * GA * n, "per_gpu_batch": B, "grad_accum": GA, "seq_len": S,
                        "target_len": T, "parallelism": f"dp{n}", "grad_ckpt": bool(a.grad_ckpt),
