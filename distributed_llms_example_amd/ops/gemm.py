@@ -28,6 +28,7 @@ import torch
 import torch.nn.functional as F
 
 from .. import _ext
+from . import streams
 
 # Routing of the projection GEMMs (profiles/r3_gemm_w4_vs_hipblaslt.jsonl, t5-base / bart-large shapes):
 #   "auto": csrc/gemm_w4.hip for input gradients whose reduction depth (the layer's output features) is
@@ -98,8 +99,16 @@ def _native_ok(dy2: torch.Tensor, x2: torch.Tensor, out: torch.Tensor) -> bool:
 
 
 @torch.no_grad()
-def wgrad_accumulate(out: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, beta: bool = True) -> torch.Tensor:
-    """``out (+)= dy2ᵀ @ x2`` with dy2 = [T, M], x2 = [T, N], out = [M, N]."""
+def wgrad_accumulate(out: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, beta: bool = True,
+                     async_ok: bool = True) -> torch.Tensor:
+    """``out (+)= dy2ᵀ @ x2`` with dy2 = [T, M], x2 = [T, N], out = [M, N].  Inside an ops/streams.py scope (and with
+    ``async_ok``: no compute-stream kernel accumulates into ``out`` in the same backward) it runs on the side stream."""
+    if async_ok:
+        return streams.run(lambda: _wgrad(out, dy2, x2, beta), dy2, x2)
+    return _wgrad(out, dy2, x2, beta)
+
+
+def _wgrad(out, dy2, x2, beta):
     if _native_ok(dy2, x2, out):
         _ext.native().gemm_wgrad(dy2, x2, out, beta, _VARIANT, 0)
         return out
@@ -127,7 +136,11 @@ def bias_grad_accumulate(out: torch.Tensor, dy2: torch.Tensor, dy: torch.Tensor 
         # in-place accumulation of another consumer's gradient bumps the version and the sum no longer describes dy)
         if (cs.numel() == out.numel() and dy._version == ver and tuple(dy.shape) == shape and dy.data_ptr() == ptr):
             colsum_handoffs += 1
-            return out.add_(cs.view_as(out).to(out.dtype))
+            return streams.run(lambda: out.add_(cs.view_as(out).to(out.dtype)), cs)
+    return streams.run(lambda: _colsum(out, dy2), dy2)
+
+
+def _colsum(out, dy2):
     if _ext.use_native(dy2) and dy2.dtype == torch.bfloat16 and dy2.stride(-1) == 1 and dy2.shape[-1] % 2 == 0 \
             and dy2.stride(0) % 2 == 0 and out.is_contiguous():
         _ext.native().colsum_acc(dy2, out)

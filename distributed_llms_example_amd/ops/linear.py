@@ -47,6 +47,13 @@ def _use(p: torch.Tensor | None) -> None:
     p._dllm_fused_seen = True
 
 
+def _sole_writer(p: torch.Tensor) -> bool:
+    """True when this op is the only one that accumulates into ``p``'s gradient in this backward (one pending fused
+    contribution): its weight-gradient GEMM may then run on the side stream (ops/streams.py).  A tied weight (the
+    T5 / BART embedding shared with the LM head) also receives the embedding backward's kernel on the compute stream."""
+    return getattr(p, "_dllm_pending", 1) <= 1
+
+
 def _fire(p: torch.Tensor) -> None:
     """Backward: one fused contribution to ``p`` has been accumulated; run the post-accumulate hooks
     (gradient reducer) when it was the last one."""
@@ -77,7 +84,7 @@ class _LinearAccumFn(torch.autograd.Function):
         dy2 = dy.reshape(-1, dy.shape[-1])
         x2 = x.reshape(-1, x.shape[-1])
         with torch.no_grad():
-            wgrad_accumulate(_gbuf(w), dy2, x2)
+            wgrad_accumulate(_gbuf(w), dy2, x2, async_ok=_sole_writer(w))
             if bias is not None:
                 bias_grad_accumulate(_gbuf(bias), dy2, dy)
         _fire(w)
@@ -118,7 +125,7 @@ class _LinearResFn(torch.autograd.Function):
                     dx = dx + dres
         x2 = x.reshape(-1, x.shape[-1])
         with torch.no_grad():
-            wgrad_accumulate(_gbuf(w), dy2, x2)
+            wgrad_accumulate(_gbuf(w), dy2, x2, async_ok=_sole_writer(w))
             if bias is not None:
                 bias_grad_accumulate(_gbuf(bias), dy2)
         _fire(w)

@@ -1,0 +1,94 @@
+"""Weight-gradient GEMMs on a side HIP stream, overlapping the input-gradient chain of the backward pass.
+
+In backward every linear layer issues two independent GEMMs: the input gradient ``dX = dY W`` (the next layer's
+backward waits for it) and the weight gradient ``dW += dYᵀ X`` (nothing in the backward waits for it).  On one stream
+they serialise, and at the reference's small micro-batches (1-8 samples per GPU: a [1024 x 768] x [768 x 2304] GEMM is
+36 of the 256 CUs' worth of 256x256 tiles) each kernel leaves most of the chip idle.  Here the weight gradient (and the
+bias gradient) is launched on a side stream that forks from the compute stream at that point, so the chip runs it
+beside the following input-gradient / attention-backward kernels.
+
+Ordering and memory, without ``record_stream``:
+
+* fork: the side stream waits on the compute stream before each launch (dY, X and the gradient buffer are ready);
+* lag: after each launch the compute stream waits on the side work launched ``LAG`` launches earlier and only then
+  drops this module's references to that work's inputs, so the caching allocator never reuses a block the side
+  stream may still read, and at most ``LAG`` layers' inputs are held beyond their autograd lifetime;
+* join: the end of the backward (``scope`` exit, engine.forward_backward) joins the side stream into the compute stream,
+  before the gradient all-reduce and the optimizer read the gradients.
+
+All three are stream waits, so a HIP-graph capture records them as graph edges (train/graph.py).  Not used when a
+gradient reducer launches bucket all-reduces from the autograd hooks during the backward (those order themselves
+after the compute stream only), nor for gradients another compute-stream kernel also accumulates into (the tied
+embedding's LM-head slice: ops/lm_head.py keeps those synchronous).  ``DLLM_WGRAD_STREAM=0`` turns it off.
+"""
+from __future__ import annotations
+
+import collections
+import contextlib
+import os
+
+import torch
+
+LAG = max(1, int(os.environ.get("DLLM_WGRAD_STREAM_LAG", "2")))
+_on = [False]
+_side: dict = {}
+_used: set = set()  # devices whose side stream has work since the last join
+_pending: collections.deque = collections.deque()
+launches = 0  # side-stream launches since import (tests assert the path really ran)
+
+
+def default_enabled() -> bool:
+    return os.environ.get("DLLM_WGRAD_STREAM", "1") != "0"
+
+
+def _side_stream(dev: torch.device) -> torch.cuda.Stream:
+    s = _side.get(dev)
+    if s is None:
+        s = _side[dev] = torch.cuda.Stream(dev)
+    return s
+
+
+def run(fn, *refs):
+    """``fn()`` on the side stream when a scope is active and the tensors are on the GPU, else inline.  ``refs``: the
+    tensors ``fn`` reads (kept alive until the compute stream has waited for ``fn``)."""
+    global launches
+    if not _on[0] or not refs or not refs[0].is_cuda:
+        return fn()
+    dev = refs[0].device
+    cur = torch.cuda.current_stream(dev)
+    side = _side_stream(dev)
+    side.wait_stream(cur)
+    _used.add(dev)
+    with torch.cuda.stream(side):
+        r = fn()
+    ev = torch.cuda.Event()
+    ev.record(side)
+    _pending.append((ev, refs, dev))
+    launches += 1
+    while len(_pending) > LAG:
+        e, _, d = _pending.popleft()
+        torch.cuda.current_stream(d).wait_event(e)
+    return r
+
+
+def join() -> None:
+    """Compute stream waits for every side-stream launch since the last join; their inputs may be released.  Only
+    streams with new work are joined: in a graph capture, a wait on a side stream that never forked from the capture
+    stream would be a dependency on work outside the graph."""
+    for dev in _used:
+        torch.cuda.current_stream(dev).wait_stream(_side[dev])
+    _used.clear()
+    _pending.clear()
+
+
+@contextlib.contextmanager
+def scope(enabled: bool = True):
+    """Weight gradients of the backward run inside go to the side stream; joined on exit."""
+    prev = _on[0]
+    _on[0] = bool(enabled) and torch.cuda.is_available()
+    try:
+        yield
+    finally:
+        _on[0] = prev
+        if not prev:
+            join()

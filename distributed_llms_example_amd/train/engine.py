@@ -13,6 +13,7 @@ import os
 import torch
 
 from ..ops import rng as rng_mod
+from ..ops import streams
 from ..ops.optim import FusedAdamW
 from ..utils import profiling
 from ..parallel.env import DistEnv
@@ -124,7 +125,11 @@ class TrainEngine:
         if self.step_seed is not None:
             self.step_seed.advance()
             rng_mod.default_rng().begin_micro_step()
-        with ctx:
+        # weight gradients on a side stream (ops/streams.py) unless the reducer launches all-reduces from the hooks
+        # of this backward (those order themselves after the compute stream only)
+        hooks_reduce = self.reducer is not None and sync and self.reducer.overlap and self.reducer.dp
+        side = streams.scope(streams.default_enabled() and not hooks_reduce and self.env.device.type == "cuda")
+        with ctx, side:
             with profiling.range("forward"):
                 out = self.forward(batch)
                 loss = out.loss

@@ -293,3 +293,38 @@ def test_t5_fused_lm_head_matches_materialised_logits(monkeypatch):
         res.append((float(loss), eng.flat.grad_buf.float().clone()))
     assert abs(res[0][0] - res[1][0]) < 5e-3 * res[1][0], (res[0][0], res[1][0])
     assert _rel(res[0][1], res[1][1]) < 3e-2, _rel(res[0][1], res[1][1])
+
+
+@pytest.mark.parametrize("graphed", [False, True])
+def test_side_stream_wgrad_matches_single_stream(graphed, monkeypatch):
+    """Weight gradients on the side stream (ops/streams.py) == all on the compute stream: same flat gradient (the
+    kernels are deterministic and the accumulation order is unchanged), eager and inside a captured HIP graph; the side
+    path really ran."""
+    from distributed_llms_example_amd.ops import streams
+    cfg = _small_cfg().replace(dropout_rate=0.0)
+    torch.manual_seed(0)
+    sd = build_model(cfg).state_dict()
+    mbs = _micro_batches(cfg, n=2, B=2)
+    res = []
+    for on in ("1", "0"):
+        monkeypatch.setenv("DLLM_WGRAD_STREAM", on)
+        eng = _engine(cfg, sd, torch.float32)
+        eng.train(False)
+        n0 = streams.launches
+        if graphed:
+            from distributed_llms_example_amd.train.graph import GraphedStep
+            gs = GraphedStep(eng, mbs, warmup=1)
+            gs.replay(mbs)
+            eng.disable_step_seeds()
+            # the step ends with AdamW (reading every gradient) and zero_grad: the parameters after two optimizer steps
+            # (warmup + replay) carry the gradients; they must match the single-stream run bit for bit
+            res.append((float(gs.loss), eng.flat.param_buf.float().clone(), streams.launches - n0))
+        else:
+            for i, b in enumerate(mbs):
+                eng.forward_backward(b, grad_accum=len(mbs), sync=i + 1 == len(mbs))
+            torch.cuda.synchronize()
+            res.append((0.0, eng.flat.grad_buf.float().clone(), streams.launches - n0))
+    (l1, g1, n1), (l0, g0, n0) = res
+    assert n1 > 0 and n0 == 0, (n1, n0)
+    assert l1 == l0
+    assert torch.equal(g1, g0), _rel(g1, g0)
