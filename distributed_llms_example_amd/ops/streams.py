@@ -19,7 +19,8 @@ Ordering and memory, without ``record_stream``:
 All three are stream waits, so a HIP-graph capture records them as graph edges (train/graph.py).  Not used when a
 gradient reducer launches bucket all-reduces from the autograd hooks during the backward (those order themselves
 after the compute stream only), nor for gradients another compute-stream kernel also accumulates into (the tied
-embedding's LM-head slice: ops/lm_head.py keeps those synchronous).  ``DLLM_WGRAD_STREAM=0`` turns it off.
+embedding's LM-head slice: ops/lm_head.py keeps those synchronous).  Used for small micro-batches only
+(``default_enabled``).
 """
 from __future__ import annotations
 
@@ -37,8 +38,17 @@ _pending: collections.deque = collections.deque()
 launches = 0  # side-stream launches since import (tests assert the path really ran)
 
 
-def default_enabled() -> bool:
-    return os.environ.get("DLLM_WGRAD_STREAM", "1") != "0"
+def default_enabled(tokens: int | None = None) -> bool:
+    """``DLLM_WGRAD_STREAM``: ``auto`` (default) = on for micro-batches of at most ``DLLM_WGRAD_STREAM_MAX_TOKENS``
+    input tokens (default 32768), where single kernels leave the chip partly idle; off above, where two full-chip
+    GEMMs side by side only compete (t5-base, one MI355X, interleaved: batch 1 +9.8 %, batch 8 x GA 16 +4.2 %,
+    batch 512 -3.6 %, profiles/r4_wgrad_stream_ab.txt); ``1`` always; ``0`` never."""
+    mode = os.environ.get("DLLM_WGRAD_STREAM", "auto")
+    if mode == "0":
+        return False
+    if mode == "1" or tokens is None:
+        return True
+    return tokens <= int(os.environ.get("DLLM_WGRAD_STREAM_MAX_TOKENS", "32768"))
 
 
 def _side_stream(dev: torch.device) -> torch.cuda.Stream:

@@ -128,7 +128,9 @@ class TrainEngine:
         # weight gradients on a side stream (ops/streams.py) unless the reducer launches all-reduces from the hooks
         # of this backward (those order themselves after the compute stream only)
         hooks_reduce = self.reducer is not None and sync and self.reducer.overlap and self.reducer.dp
-        side = streams.scope(streams.default_enabled() and not hooks_reduce and self.env.device.type == "cuda")
+        ids = batch.get("input_ids")
+        side = streams.scope(streams.default_enabled(ids.numel() if ids is not None else None) and not hooks_reduce
+                             and self.env.device.type == "cuda")
         with ctx, side:
             with profiling.range("forward"):
                 out = self.forward(batch)

@@ -306,7 +306,7 @@ def test_side_stream_wgrad_matches_single_stream(graphed, monkeypatch):
     sd = build_model(cfg).state_dict()
     mbs = _micro_batches(cfg, n=2, B=2)
     res = []
-    for on in ("1", "0"):
+    for on in ("1", "0"):  # "1": forced on (the default "auto" enables it for small micro-batches only)
         monkeypatch.setenv("DLLM_WGRAD_STREAM", on)
         eng = _engine(cfg, sd, torch.float32)
         eng.train(False)
