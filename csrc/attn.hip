@@ -881,6 +881,12 @@ constexpr int K2_QT = 64;
 #define DKDV_OPERANDS_AHEAD 1
 #endif
 constexpr int K2_NBUF = 3;
+// timing ablations of the dK/dV kernel (A/B builds only, results are wrong; profiles/r4_dkdv_ablations.txt): 1 no
+// bias-gradient diagonal sums, 2 no LUT bias reads, 4 no stage barrier, 8 no dV/dK MFMAs, 16 no dropout keep bits,
+// 32 no row-term reads, 64 no exp
+#ifndef DKDV_ABLATE
+#define DKDV_ABLATE 0
+#endif
 constexpr int K2_STAGE = 2 * 64 * D * 2 + 1024 + 1024;  // Q, dO [64][64] bf16 + rowrec [4][64] f32 + keep [4][64] u32
 
 // NB = stage ring depth: 3 (two stages in flight, 2 workgroups per CU) or 2 (one in flight, a 168-VGPR budget so 3
@@ -1001,7 +1007,8 @@ __global__ __launch_bounds__(256, NB == 3 ? 2 : 3) void attn_bwd_dkdv2_kernel(At
     constexpr int SLOT = decltype(slot_c)::value;
     if (NB == 3 && qt + 1 < nqt) wait_vm<DPT>();
     else wait_vm<0>();
-    __syncthreads();  // stage qt landed for every wave; every wave is done with stage qt - 1 (the slot refilled next)
+    if constexpr ((DKDV_ABLATE & 4) == 0)
+      __syncthreads();  // stage qt landed for every wave; every wave is done with stage qt - 1 (the slot refilled next)
     if (qt + NB - 1 < nqt) issue((SLOT + NB - 1) % NB, qt + NB - 1);
     const unsigned char* stg = smem + SLOT * K2_STAGE;
     const uint16_t* Qb = reinterpret_cast<const uint16_t*>(stg);
@@ -1035,7 +1042,7 @@ __global__ __launch_bounds__(256, NB == 3 ? 2 : 3) void attn_bwd_dkdv2_kernel(At
       }
       const int sat = !HAS_BIAS ? 0
                       : (kw0 + 31 - q0 + P.Sq - 1 <= P.sat_lo ? 1 : (kw0 - q0 - 31 + P.Sq - 1 >= P.sat_hi ? 2 : 0));
-      const bool use_lut = HAS_BIAS && sat == 0;
+      const bool use_lut = HAS_BIAS && sat == 0 && (DKDV_ABLATE & 2) == 0;
       f32x16 pd, ds;
       if constexpr (NB == 3) {  // all 16 row terms read up front: their LDS latency hides under the MFMAs
         // rows 32u + crow(i, hh): four consecutive rows per 16-B read
@@ -1045,14 +1052,17 @@ __global__ __launch_bounds__(256, NB == 3 ? 2 : 3) void attn_bwd_dkdv2_kernel(At
         uint32_t mw[16];
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          const f32x4 a = *reinterpret_cast<const f32x4*>(rt_row + 8 * g);
-          const f32x4 c = *reinterpret_cast<const f32x4*>(nd_row + 8 * g);
+          f32x4 a = {0.f, -1.f, 0.5f, 0.25f}, c = a;
+          if constexpr ((DKDV_ABLATE & 32) == 0) {
+            a = *reinterpret_cast<const f32x4*>(rt_row + 8 * g);
+            c = *reinterpret_cast<const f32x4*>(nd_row + 8 * g);
+          }
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             rt[4 * g + e] = a[e];
             nd[4 * g + e] = c[e];
           }
-          if (DROP) {
+          if (DROP && (DKDV_ABLATE & 16) == 0) {
             const u32x4 v = *reinterpret_cast<const u32x4*>(mwd + mcol * 64 + 32 * u + 8 * g + 4 * hh);
 #pragma unroll
             for (int e = 0; e < 4; ++e) mw[4 * g + e] = v[e];
@@ -1076,10 +1086,11 @@ __global__ __launch_bounds__(256, NB == 3 ? 2 : 3) void attn_bwd_dkdv2_kernel(At
         const bool tile_causal = CAUSAL && (kw0 + 31 > q0 + P.causal_off);
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          float pr = fast_exp2(fmaf(sacc[i], sl2, rt[i]));  // rows >= Sq: rt = -inf -> 0
+          const float x = fmaf(sacc[i], sl2, rt[i]);
+          float pr = (DKDV_ABLATE & 64) ? x : fast_exp2(x);  // rows >= Sq: rt = -inf -> 0
           if (CAUSAL && tile_causal && key > q0 + crow(i, hh) + P.causal_off) pr = 0.f;
           float keepf = 1.f;
-          if (DROP) keepf = __uint_as_float((uint32_t)__builtin_amdgcn_sbfe((int)mw[i], mbit, 1) & dsbits);
+          if (DROP && (DKDV_ABLATE & 16) == 0) keepf = __uint_as_float((uint32_t)__builtin_amdgcn_sbfe((int)mw[i], mbit, 1) & dsbits);
           pd[i] = pr * keepf;
           ds[i] = pr * fmaf(dpacc[i], keepf, nd[i]);
         }
@@ -1119,7 +1130,7 @@ __global__ __launch_bounds__(256, NB == 3 ? 2 : 3) void attn_bwd_dkdv2_kernel(At
         for (int i = 0; i < 16; ++i) t += ds[i];
         if (sat == 1) sat_acc_lo += t;
         else sat_acc_hi += t;
-      } else if (HAS_BIAS) {
+      } else if (HAS_BIAS && (DKDV_ABLATE & 1) == 0) {
         // diagonal sums of the wave's 32x32 dS tile: rotate register i (row rho = crow(i, hh)) left by rho
         // lanes so lane r receives element (rho, (r + rho) & 31) whose diagonal (col - row) is r or r - 32.
         // The rotations go out in batches of 8 before any is consumed (one LDS round trip per batch: issued one by one,
@@ -1146,7 +1157,9 @@ __global__ __launch_bounds__(256, NB == 3 ? 2 : 3) void attn_bwd_dkdv2_kernel(At
         atomicAdd(&dlut_s[la < 0 ? 0 : la], va);  // la < 0: rows past Sq only (dS = 0)
       }
       const bf16x8v pf0 = pack8(pd, 0), pf1 = pack8(pd, 8), sf0 = pack8(ds, 0), sf1 = pack8(ds, 8);
-      if constexpr (NB == 3 && DKDV_OPERANDS_AHEAD) {  // the 8 transposed operands (16 reads) in flight together
+      if constexpr ((DKDV_ABLATE & 8) != 0) {
+        asm volatile("" ::"v"(pf0), "v"(pf1), "v"(sf0), "v"(sf1));
+      } else if constexpr (NB == 3 && DKDV_OPERANDS_AHEAD) {  // the 8 transposed operands (16 reads) in flight together
         bf16x8v ot[2][2], qtr[2][2];
 #pragma unroll
         for (int sp = 0; sp < 2; ++sp) {

@@ -623,6 +623,31 @@ bool gemm_wgrad_supported(const Tensor& a, const Tensor& b, const Tensor& c) {
          K < (1LL << 31) && M * N < (1LL << 31);
 }
 
+// K split count of the weight-gradient GEMM.  One 128-KB-LDS workgroup per CU, all workgroups equally long, so the
+// kernel runs ceil(T s / CUs) rounds of 1/s of a tile's K each: minimise that (the tail of the last round) plus the
+// split-K reduce pass (s fp32 slabs of the output; relative cost ~ 1.7 T s / K at ~1.1 PF/s and ~5 TB/s), fewest
+// splits on ties, at least 4 k-stages of 64 per split.  378 tiles (t5 LM head): 2 (3 full rounds instead of 1.48);
+// 216 (t5 cross-attention K/V of 12 layers): 13 (11 rounds, 99 % full, instead of one at 84 %);
+// 9 / 36 (768 x 768 / 768 x 3072 at 512K tokens): 28 / 7, one round; 27 (QKV): 28, three rounds.
+int wgrad_splits(int T, int K) {
+  static const int cus = [] {
+    const int n = at::cuda::getCurrentDeviceProperties()->multiProcessorCount;
+    return n > 0 ? n : 256;
+  }();
+  const int smax = std::max(1, std::min(K / 256, 64));
+  int best = 1;
+  double bestc = 1e30;
+  for (int s = 1; s <= smax; ++s) {
+    const double rounds = (double)((T * s + cus - 1) / cus);
+    const double c = rounds / s + (s > 1 ? 1.7 * T * s / K : 0.0);
+    if (c < bestc * (1.0 - 1e-6)) {
+      bestc = c;
+      best = s;
+    }
+  }
+  return best;
+}
+
 int64_t gemm_wgrad(const Tensor& a, const Tensor& b, Tensor& c, bool beta, int64_t variant, int64_t splits_req) {
   TORCH_CHECK(gemm_wgrad_supported(a, b, c),
               "gemm_wgrad: need bf16 GPU [K,M] x [K,N] -> bf16/fp32 [M,N], unit inner stride, 16-B aligned rows, K % 64 == 0, "
@@ -643,8 +668,7 @@ int64_t gemm_wgrad(const Tensor& a, const Tensor& b, Tensor& c, bool beta, int64
   P.tn = N / 256;
   P.ntiles = ((M + 255) / 256) * (N / 256);  // ragged last M tile (vocab-sized LM-head gradients)
   P.beta = beta ? 1 : 0;
-  // fill the 256 CUs once: split K until tiles x splits ~ 256, at least 4 k-stages of 64 per split
-  int splits = splits_req > 0 ? (int)splits_req : std::max(1, 256 / P.ntiles);
+  int splits = splits_req > 0 ? (int)splits_req : wgrad_splits(P.ntiles, K);
   splits = std::max(1, std::min(splits, K / 256));
   int kchunk = ((K + splits - 1) / splits + 63) / 64 * 64;
   splits = (K + kchunk - 1) / kchunk;

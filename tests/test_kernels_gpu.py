@@ -291,6 +291,21 @@ def test_gemm_wgrad_explicit_splits_match():
         assert _rel(o, ref) < 5e-3
 
 
+def test_gemm_wgrad_auto_splits_fill_the_last_round():
+    """378 output tiles (a t5 LM-head weight gradient: ragged vocab rows x 768) on 256 CUs: one tile per workgroup would
+    leave the second round half empty; the auto split count (csrc/bind.cpp wgrad_splits) takes 2 (3 full rounds)."""
+    torch.manual_seed(2)
+    K, M, N = 8192, 32128, 768
+    a = torch.randn(K, M, device=DEV, dtype=torch.bfloat16)
+    b = torch.randn(K, N, device=DEV, dtype=torch.bfloat16)
+    c = torch.zeros(M, N, device=DEV, dtype=torch.float32)
+    splits = _ext.native().gemm_wgrad(a, b, c, False, -1, 0)
+    if torch.cuda.get_device_properties(0).multi_processor_count == 256:
+        assert splits == 2
+    ref = a.float().t() @ b.float()
+    assert _rel(c, ref) < 5e-3, _rel(c, ref)
+
+
 def test_linear_wgrad_path_uses_native_gemm():
     from distributed_llms_example_amd.ops.gemm import _native_ok, wgrad_accumulate
     dy = torch.randn(1024, 768, device=DEV, dtype=torch.bfloat16)

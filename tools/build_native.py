@@ -37,6 +37,10 @@ CXX = os.environ.get("CXX", "g++")
 # costs more issue cycles than the scalar ops (MI355X_MICROARCH.md, per-instruction constants) and the compiler adds
 # v_mov shuffles to form the register pairs.
 EXTRA_FLAGS = {"attn.hip": ["-fno-slp-vectorize"]}
+# DLLM_HIPFLAGS_EXTRA: extra flags for every HIP source (A/B builds of a kernel variant, e.g. "-DDKDV_PIPE=0"); part
+# of the object key, so switching it back rebuilds the default objects
+_ENV_FLAGS = os.environ.get("DLLM_HIPFLAGS_EXTRA", "").split()
+_ENV_FLAGS_SRC = os.environ.get("DLLM_HIPFLAGS_EXTRA_SRC", "")  # only this source (default: every HIP source)
 
 
 def _torch_paths():
@@ -106,7 +110,9 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = True) -> str:
         obj = os.path.join(BUILD, os.path.basename(src) + ".o")
         objs.append(obj)
         cmd = ([HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-ffp-contract=fast",
-                "-munsafe-fp-atomics"] + EXTRA_FLAGS.get(os.path.basename(src), []) + ["-I", CSRC, "-c", src, "-o", obj])
+                "-munsafe-fp-atomics"] + EXTRA_FLAGS.get(os.path.basename(src), [])
+               + (_ENV_FLAGS if _ENV_FLAGS_SRC in ("", os.path.basename(src)) else [])
+               + ["-I", CSRC, "-c", src, "-o", obj])
         key = _key(src, headers, cmd)
         if force or _stale(obj, key):
             jobs_list.append((cmd, obj, key))
