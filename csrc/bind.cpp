@@ -634,6 +634,8 @@ int wgrad_splits(int T, int K) {
     const int n = at::cuda::getCurrentDeviceProperties()->multiProcessorCount;
     return n > 0 ? n : 256;
   }();
+  static const bool legacy = std::getenv("DLLM_WGRAD_SPLIT_LEGACY") != nullptr;  // A/B: fill the CUs once
+  if (legacy) return std::max(1, cus / T);
   const int smax = std::max(1, std::min(K / 256, 64));
   int best = 1;
   double bestc = 1e30;
