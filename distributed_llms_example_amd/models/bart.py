@@ -1,4 +1,5 @@
-"""BART (bart-large-cnn, the reference's default checkpoint: ref/valohai.yaml:10,36,65).
+"""BART (bart-large-cnn, the reference's default checkpoint: ref/valohai.yaml:10,36,65) and the other
+BART-family models ``AutoModelForSeq2SeqLM`` resolves to: mBART, Pegasus, Marian.
 
 Follows transformers' BartForConditionalGeneration (modeling_bart.py:835-958): learned positions
 with offset 2 (:74-98), ``layernorm_embedding`` + dropout after the embeddings (:507-549),
@@ -7,6 +8,13 @@ post-LN encoder/decoder layers (:280-308, :343-390), exact-erf GELU, attention s
 fused QKV / cross-KV projections (one GEMM each), ``LN(residual + dropout(x))`` as one kernel,
 flash attention with key-padding / causal masks, fused CE with the logits bias inside the kernel.
 LayerDrop (encoder/decoder_layerdrop, 0.0 in every public BART config) is not implemented.
+
+Family switches (models/config.py ``_FAMILY``; transformers modeling_mbart.py, modeling_pegasus.py,
+modeling_marian.py): pre-LN layers plus a final LayerNorm per stack (mBART, Pegasus) — there the residual update
+and the NEXT sub-layer's LayerNorm are one kernel returning both (as T5's RMSNorm blocks); no embedding LayerNorm
+(Pegasus, Marian); fixed sinusoidal positions without offset (Pegasus, Marian; sin in the first half of the
+features, cos in the second); SiLU FFN (Marian's ``swish``); mBART's decoder input starts from the label's last
+non-pad token (its language id).
 """
 from __future__ import annotations
 
@@ -18,7 +26,7 @@ import torch
 import torch.nn as nn
 
 from ..ops import activations, attention as attn_ops, norms
-from ..ops.ffn import ffn_res
+from ..ops.ffn import ffn, ffn_res
 from ..ops.cross_entropy import cross_entropy
 from ..ops.embedding import embedding
 from ..ops.linear import Linear, linear, linear_res, stacked_linear
@@ -122,6 +130,30 @@ class BartLayer(nn.Module):
         return norms.add_dropout_layer_norm(h, f, self.final_layer_norm.weight, self.final_layer_norm.bias, eps, p,
                                             rng.next_seed() if p > 0 else 0, xb)
 
+    def forward_pre(self, normed, h, next_norm, mask=None, enc_out=None, enc_mask=None, cache=None, cross_kv=None):
+        """Pre-LN layer (mBART / Pegasus) on (LN_self_attn(h), h) -> (next_norm(h'), h'): every residual update is
+        fused with the LayerNorm that follows it (the next sub-layer's, or ``next_norm``: the next layer's first
+        LayerNorm or the stack's final one)."""
+        cfg = self.cfg
+        tr = self.training
+        p = cfg.dropout_rate if tr else 0.0
+        pa = cfg.attention_dropout if tr else 0.0
+        pact = cfg.activation_dropout if tr else 0.0
+        eps = cfg.layer_norm_epsilon
+        rng = default_rng()
+        xb = _NORM_BIAS_COLSUM
+        a = self.self_attn(normed, mask=None if self.is_decoder else mask, causal=self.is_decoder, p=pa, cache=cache)
+        if self.is_decoder:
+            normed, h = norms.add_dropout_layer_norm_pre(h, a, self.encoder_attn_layer_norm.weight,
+                                                         self.encoder_attn_layer_norm.bias, eps, p,
+                                                         rng.next_seed() if p > 0 else 0, xb)
+            a = self.encoder_attn(normed, kv_in=enc_out, mask=enc_mask, p=pa, kv=cross_kv)
+        normed, h = norms.add_dropout_layer_norm_pre(h, a, self.final_layer_norm.weight, self.final_layer_norm.bias,
+                                                     eps, p, rng.next_seed() if p > 0 else 0, xb)
+        f = ffn(normed, self.fc1, self.fc2, cfg.act, pact, rng.next_seed() if pact > 0 else 0)
+        return norms.add_dropout_layer_norm_pre(h, f, next_norm.weight, next_norm.bias, eps, p,
+                                                rng.next_seed() if p > 0 else 0, xb)
+
 
 class BartLearnedPositionalEmbedding(nn.Embedding):
     offset = 2
@@ -130,16 +162,39 @@ class BartLearnedPositionalEmbedding(nn.Embedding):
         super().__init__(n + self.offset, d)
 
 
+class SinusoidalPositions(nn.Module):
+    """Fixed positions of Pegasus / Marian (modeling_pegasus.py PegasusSinusoidalPositionalEmbedding.create_weight):
+    feature j of position t is sin / cos of t / 10000^(2 floor(j/2) / d), the sines in the first half of the features
+    and the cosines in the second.  A persistent buffer named ``weight`` (the checkpoints carry it); never trained."""
+    offset = 0
+
+    def __init__(self, n, d):
+        super().__init__()
+        pos = torch.arange(n, dtype=torch.float64)[:, None]
+        j = torch.arange(d, dtype=torch.float64)[None, :]
+        enc = pos / torch.pow(10000.0, 2 * torch.div(j, 2, rounding_mode="floor") / d)
+        w = torch.empty(n, d, dtype=torch.float64)
+        half = d // 2 if d % 2 == 0 else d // 2 + 1
+        w[:, :half] = torch.sin(enc[:, 0::2])
+        w[:, half:] = torch.cos(enc[:, 1::2])
+        self.register_buffer("weight", w.float())
+
+
 class BartStack(nn.Module):
     def __init__(self, cfg, is_decoder, embed_tokens):
         super().__init__()
         self.cfg = cfg
         self.is_decoder = is_decoder
         self._embed = [embed_tokens]
-        self.embed_positions = BartLearnedPositionalEmbedding(cfg.max_position_embeddings, cfg.d_model)
+        pos_cls = SinusoidalPositions if cfg.position_embedding == "sinusoidal" else BartLearnedPositionalEmbedding
+        self.embed_positions = pos_cls(cfg.max_position_embeddings, cfg.d_model)
+        self._pos_offset = pos_cls.offset
         n = cfg.num_decoder_layers if is_decoder else cfg.num_layers
         self.layers = nn.ModuleList([BartLayer(cfg, is_decoder) for _ in range(n)])
-        self.layernorm_embedding = nn.LayerNorm(cfg.d_model)
+        if cfg.layernorm_embedding:
+            self.layernorm_embedding = nn.LayerNorm(cfg.d_model)
+        if cfg.normalize_before:  # pre-LN stacks end with a LayerNorm (modeling_mbart.py MBartEncoder.layer_norm)
+            self.layer_norm = nn.LayerNorm(cfg.d_model)
         self.embed_scale = math.sqrt(cfg.d_model) if cfg.scale_embedding else 1.0
 
     def cross_kv_linears(self):
@@ -159,12 +214,18 @@ class BartStack(nn.Module):
         x = embedding(input_ids, self._embed[0].weight, padding_idx=cfg.pad_token_id)
         if self.embed_scale != 1.0:
             x = x * self.embed_scale
-        pos = torch.arange(q_offset, q_offset + S, device=input_ids.device) + BartLearnedPositionalEmbedding.offset
-        x = x + embedding(pos, self.embed_positions.weight).unsqueeze(0)
-        h = norms.layer_norm(x, self.layernorm_embedding.weight, self.layernorm_embedding.bias, cfg.layer_norm_epsilon)
-        h = activations.dropout(h, p, default_rng().next_seed() if p > 0 else 0)
+        pos = torch.arange(q_offset, q_offset + S, device=input_ids.device) + self._pos_offset
+        pw = self.embed_positions.weight
+        x = x + (embedding(pos, pw) if pw.requires_grad else pw[pos].to(x.dtype)).unsqueeze(0)
+        if cfg.layernorm_embedding:
+            x = norms.layer_norm(x, self.layernorm_embedding.weight, self.layernorm_embedding.bias,
+                                 cfg.layer_norm_epsilon)
         if self.is_decoder and cross_kv is None and enc_out is not None:
             cross_kv = self.project_cross_kv(enc_out)
+        seed = default_rng().next_seed() if p > 0 else 0
+        if cfg.normalize_before:
+            return self._forward_pre(x, p, seed, attention_mask, enc_out, enc_mask, caches, cross_kv)
+        h = activations.dropout(x, p, seed)
         for i, layer in enumerate(self.layers):
             cache = caches[i] if caches is not None else None
             ckv = cross_kv[i] if cross_kv is not None else None
@@ -174,6 +235,25 @@ class BartStack(nn.Module):
 
             h = run_block(run, h, checkpoint=cfg.gradient_checkpointing and self.training and caches is None)
         return h
+
+    def _forward_pre(self, x, p, seed, attention_mask, enc_out, enc_mask, caches, cross_kv):
+        """Pre-LN stack: (LN_0(h), h) with h = dropout(embeddings), layer by layer, ending in (layer_norm(h), h)."""
+        cfg = self.cfg
+        layers = list(self.layers)
+        normed, h = norms.dropout_layer_norm_pre(x, layers[0].self_attn_layer_norm.weight,
+                                                 layers[0].self_attn_layer_norm.bias, cfg.layer_norm_epsilon, p, seed)
+        for i, layer in enumerate(layers):
+            nxt = layers[i + 1].self_attn_layer_norm if i + 1 < len(layers) else self.layer_norm
+            cache = caches[i] if caches is not None else None
+            ckv = cross_kv[i] if cross_kv is not None else None
+
+            def run(normed, h, layer=layer, nxt=nxt, cache=cache, ckv=ckv):
+                return layer.forward_pre(normed, h, nxt, mask=attention_mask, enc_out=enc_out, enc_mask=enc_mask,
+                                         cache=cache, cross_kv=ckv)
+
+            normed, h = run_block(run, normed, h, checkpoint=cfg.gradient_checkpointing and self.training and
+                                  caches is None)
+        return normed
 
 
 class BartModel(nn.Module):
@@ -185,6 +265,7 @@ class BartModel(nn.Module):
 
 
 class BartForConditionalGeneration(nn.Module):
+    """BART and the BART-family model types (``config.model_type`` bart / mbart / pegasus / marian)."""
     model_type = "bart"
 
     def __init__(self, cfg: Seq2SeqConfig):
@@ -214,11 +295,20 @@ class BartForConditionalGeneration(nn.Module):
         self.final_logits_bias.zero_()
 
     def shift_right(self, labels):
-        """shift_tokens_right (modeling_bart.py:58-71)"""
+        """shift_tokens_right (modeling_bart.py:58-71); mBART (modeling_mbart.py shift_tokens_right): the first
+        decoder input is the label row's last non-pad token (the target language id) instead of a fixed id."""
+        pad = self.config.pad_token_id
+        if self.config.shift_mode == "mbart":
+            prev = labels.masked_fill(labels == -100, pad)
+            last = (prev.ne(pad).sum(dim=1) - 1).clamp(min=0).unsqueeze(-1)
+            out = torch.empty_like(prev)
+            out[:, 1:] = prev[:, :-1]
+            out[:, 0] = prev.gather(1, last).squeeze(-1)
+            return out
         out = labels.new_zeros(labels.shape)
         out[:, 1:] = labels[:, :-1]
         out[:, 0] = self.config.decoder_start_token_id
-        out.masked_fill_(out == -100, self.config.pad_token_id)
+        out.masked_fill_(out == -100, pad)
         return out
 
     prepare_decoder_input_ids_from_labels = shift_right

@@ -19,7 +19,7 @@ from dataclasses import dataclass, field
 
 @dataclass
 class Seq2SeqConfig:
-    model_type: str = "t5"  # "t5" | "bart"
+    model_type: str = "t5"  # "t5" | "bart" | "mbart" | "pegasus" | "marian" (the last three: BART-family switches below)
     vocab_size: int = 32128
     d_model: int = 512
     d_kv: int = 64
@@ -46,6 +46,14 @@ class Seq2SeqConfig:
     max_position_embeddings: int = 1024
     scale_embedding: bool = False
     final_logits_bias: bool = False
+    # BART-family variants (transformers modeling_mbart.py / modeling_pegasus.py / modeling_marian.py):
+    # pre-LN layers with a final LayerNorm per stack (mBART, Pegasus) vs post-LN (BART, Marian); LayerNorm after
+    # the embeddings (BART, mBART); learned positions with offset 2 (BART, mBART) vs fixed sinusoidal (Pegasus,
+    # Marian); decoder start token = the last non-pad label token (mBART's language id) vs a fixed id
+    normalize_before: bool = False
+    layernorm_embedding: bool = True
+    position_embedding: str = "learned"  # "learned" | "sinusoidal"
+    shift_mode: str = "standard"  # "standard" | "mbart"
     # special tokens
     pad_token_id: int = 0
     eos_token_id: int = 1
@@ -70,6 +78,8 @@ class Seq2SeqConfig:
         a = self.feed_forward_proj.split("-")[-1]
         if self.feed_forward_proj == "gated-gelu":
             return "gelu_new"
+        if a == "swish":  # Marian's name for SiLU
+            return "silu"
         return a
 
     def replace(self, **kw) -> "Seq2SeqConfig":
@@ -106,9 +116,11 @@ class Seq2SeqConfig:
                 "tie_word_embeddings": self.tie_word_embeddings,
             }
         else:
+            arch = {"bart": "BartForConditionalGeneration", "mbart": "MBartForConditionalGeneration",
+                    "pegasus": "PegasusForConditionalGeneration", "marian": "MarianMTModel"}[self.model_type]
             d = {
-                "architectures": ["BartForConditionalGeneration"],
-                "model_type": "bart",
+                "architectures": [arch],
+                "model_type": self.model_type,
                 "vocab_size": self.vocab_size,
                 "d_model": self.d_model,
                 "encoder_layers": self.num_layers,
@@ -117,7 +129,7 @@ class Seq2SeqConfig:
                 "decoder_attention_heads": self.num_heads,
                 "encoder_ffn_dim": self.d_ff,
                 "decoder_ffn_dim": self.d_ff,
-                "activation_function": self.act,
+                "activation_function": self.feed_forward_proj,
                 "dropout": self.dropout_rate,
                 "attention_dropout": self.attention_dropout,
                 "activation_dropout": self.activation_dropout,
@@ -135,6 +147,9 @@ class Seq2SeqConfig:
                 "encoder_layerdrop": 0.0,
                 "decoder_layerdrop": 0.0,
             }
+            if self.model_type == "marian":
+                d["decoder_vocab_size"] = self.vocab_size
+                d["share_encoder_decoder_embeddings"] = True
         d["torch_dtype"] = "float32"
         return d
 
@@ -159,9 +174,10 @@ class Seq2SeqConfig:
                 pad_token_id=d.get("pad_token_id", 0), eos_token_id=_first(d.get("eos_token_id", 1)),
                 decoder_start_token_id=d.get("decoder_start_token_id", 0) or 0,
             )
-        if mt == "bart":
+        if mt in ("bart", "mbart", "pegasus", "marian"):
+            fam = _FAMILY[mt]
             return cls(
-                model_type="bart", vocab_size=d.get("vocab_size", 50265), d_model=d.get("d_model", 1024),
+                model_type=mt, vocab_size=d.get("vocab_size", 50265), d_model=d.get("d_model", 1024),
                 d_kv=d.get("d_model", 1024) // d.get("encoder_attention_heads", 16),
                 d_ff=d.get("encoder_ffn_dim", 4096), num_layers=d.get("encoder_layers", 12),
                 num_decoder_layers=d.get("decoder_layers", 12), num_heads=d.get("encoder_attention_heads", 16),
@@ -172,8 +188,11 @@ class Seq2SeqConfig:
                 scale_embedding=d.get("scale_embedding", False), final_logits_bias=True,
                 tie_word_embeddings=True, scale_decoder_outputs=False,
                 pad_token_id=d.get("pad_token_id", 1), eos_token_id=_first(d.get("eos_token_id", 2)),
-                bos_token_id=d.get("bos_token_id", 0), decoder_start_token_id=d.get("decoder_start_token_id", 2),
+                bos_token_id=d.get("bos_token_id", 0 if mt in ("bart", "mbart") else None),
+                decoder_start_token_id=d.get("decoder_start_token_id") if d.get("decoder_start_token_id") is not None
+                else (d.get("pad_token_id", 1) if mt != "bart" else 2),
                 forced_bos_token_id=d.get("forced_bos_token_id"), forced_eos_token_id=d.get("forced_eos_token_id", 2),
+                **fam,
             )
         raise ValueError(f"unsupported model_type {mt!r}")
 
@@ -201,6 +220,28 @@ class Seq2SeqConfig:
 
 def _first(x):
     return x[0] if isinstance(x, (list, tuple)) else x
+
+
+# structural switches of the BART-family model types (see the Seq2SeqConfig fields)
+_FAMILY = {
+    "bart": dict(normalize_before=False, layernorm_embedding=True, position_embedding="learned", shift_mode="standard"),
+    "mbart": dict(normalize_before=True, layernorm_embedding=True, position_embedding="learned", shift_mode="mbart"),
+    "pegasus": dict(normalize_before=True, layernorm_embedding=False, position_embedding="sinusoidal",
+                    shift_mode="standard"),
+    "marian": dict(normalize_before=False, layernorm_embedding=False, position_embedding="sinusoidal",
+                   shift_mode="standard"),
+}
+
+
+def _bartlike(mt, name, vocab, d_model, layers, heads, d_ff, act, max_pos, scale_emb, pad, eos, bos, start,
+              dropout=0.1, attn_dropout=0.0, act_dropout=0.0, forced_bos=None, forced_eos=None):
+    return Seq2SeqConfig(
+        model_type=mt, name=name, vocab_size=vocab, d_model=d_model, d_kv=d_model // heads, d_ff=d_ff,
+        num_layers=layers, num_decoder_layers=layers, num_heads=heads, feed_forward_proj=act, dropout_rate=dropout,
+        attention_dropout=attn_dropout, activation_dropout=act_dropout, layer_norm_epsilon=1e-5,
+        final_logits_bias=True, scale_decoder_outputs=False, max_position_embeddings=max_pos,
+        scale_embedding=scale_emb, pad_token_id=pad, eos_token_id=eos, bos_token_id=bos, decoder_start_token_id=start,
+        forced_bos_token_id=forced_bos, forced_eos_token_id=forced_eos, **_FAMILY[mt])
 
 
 def _t5(name, d_model, d_ff, layers, heads, ff="relu", tie=True, vocab=32128, d_kv=64):
@@ -236,12 +277,29 @@ PRESETS["bart-large-cnn"] = PRESETS["bart-large"].replace(
     name="bart-large-cnn", vocab_size=50264,
     generation={"min_length": 56, "max_length": 142, "length_penalty": 2.0, "no_repeat_ngram_size": 3,
                 "num_beams": 4, "early_stopping": True})
+# other AutoModelForSeq2SeqLM families on the BART implementation (models/bart.py; public config.json values)
+PRESETS["mbart-large-cc25"] = _bartlike("mbart", "mbart-large-cc25", 250027, 1024, 12, 16, 4096, "gelu", 1024, True,
+                                        pad=1, eos=2, bos=0, start=2, forced_eos=2)
+PRESETS["mbart-large-50"] = PRESETS["mbart-large-cc25"].replace(name="mbart-large-50", vocab_size=250054)
+PRESETS["pegasus-large"] = _bartlike("pegasus", "pegasus-large", 96103, 1024, 16, 16, 4096, "relu", 1024, True,
+                                     pad=0, eos=1, bos=None, start=0, attn_dropout=0.1, act_dropout=0.1, forced_eos=1)
+PRESETS["pegasus-xsum"] = PRESETS["pegasus-large"].replace(
+    name="pegasus-xsum", max_position_embeddings=512,
+    generation={"max_length": 64, "length_penalty": 0.6, "num_beams": 8})
+PRESETS["opus-mt-en-de"] = _bartlike("marian", "opus-mt-en-de", 58101, 512, 6, 8, 2048, "swish", 512, True,
+                                     pad=58100, eos=0, bos=None, start=58100, forced_eos=0)
 # tiny configs for CPU tests
 PRESETS["t5-tiny"] = _t5("t5-tiny", 64, 128, 2, 4, vocab=512, d_kv=16)
 PRESETS["t5-tiny-gated"] = _t5("t5-tiny-gated", 64, 96, 2, 4, ff="gated-gelu", tie=False, vocab=512, d_kv=16)
 PRESETS["bart-tiny"] = PRESETS["bart-base"].replace(name="bart-tiny", vocab_size=512, d_model=64, d_kv=16, d_ff=128,
                                                     num_layers=2, num_decoder_layers=2, num_heads=4,
                                                     max_position_embeddings=256)
+PRESETS["mbart-tiny"] = _bartlike("mbart", "mbart-tiny", 512, 64, 2, 4, 128, "gelu", 256, True, pad=1, eos=2, bos=0,
+                                  start=2, forced_eos=2)
+PRESETS["pegasus-tiny"] = _bartlike("pegasus", "pegasus-tiny", 512, 64, 2, 4, 128, "relu", 256, True, pad=0, eos=1,
+                                    bos=None, start=0, attn_dropout=0.1, act_dropout=0.1, forced_eos=1)
+PRESETS["marian-tiny"] = _bartlike("marian", "marian-tiny", 512, 64, 2, 4, 128, "swish", 256, True, pad=511, eos=0,
+                                   bos=None, start=511, forced_eos=0)
 
 
 def resolve_config(name_or_path: str) -> Seq2SeqConfig:

@@ -166,3 +166,15 @@ def add_dropout_layer_norm(resid, x, weight, bias, eps, p, seed, x_bias_grad=Fal
 
 def dropout_layer_norm(x, weight, bias, eps, p, seed):
     return _norm(x, None, weight, bias, eps, p, seed, LAYER)[0]
+
+
+def add_dropout_layer_norm_pre(resid, x, weight, bias, eps, p, seed, x_bias_grad=False):
+    """(LN(s), s) with s = resid + dropout(x): a pre-LN residual update fused with the next sub-layer's LayerNorm
+    (mBART / Pegasus layers, transformers modeling_mbart.py / modeling_pegasus.py).  ``x_bias_grad`` as in
+    ``add_dropout_layer_norm``."""
+    return _norm(x, resid, weight, bias, eps, p, seed, LAYER, x_bias_grad)
+
+
+def dropout_layer_norm_pre(x, weight, bias, eps, p, seed):
+    """(LN(s), s) with s = dropout(x): a pre-LN stack's embedding dropout fused with its first LayerNorm."""
+    return _norm(x, None, weight, bias, eps, p, seed, LAYER)

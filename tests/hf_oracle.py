@@ -11,12 +11,14 @@ def hf_model_for(model):
     d.pop("architectures", None)
     d.pop("torch_dtype", None)
     mt = d.pop("model_type")
-    if mt == "t5":
-        hcfg = transformers.T5Config(**d)
-        hf = transformers.T5ForConditionalGeneration(hcfg)
-    else:
-        hcfg = transformers.BartConfig(**d)
-        hf = transformers.BartForConditionalGeneration(hcfg)
+    classes = {"t5": (transformers.T5Config, transformers.T5ForConditionalGeneration),
+               "bart": (transformers.BartConfig, transformers.BartForConditionalGeneration),
+               "mbart": (transformers.MBartConfig, transformers.MBartForConditionalGeneration),
+               "pegasus": (transformers.PegasusConfig, transformers.PegasusForConditionalGeneration),
+               "marian": (transformers.MarianConfig, transformers.MarianMTModel)}
+    cfg_cls, model_cls = classes[mt]
+    hcfg = cfg_cls(**d)
+    hf = model_cls(hcfg)
     hcfg._attn_implementation = "eager"
     sd = to_hf_state_dict(model)
     missing, unexpected = hf.load_state_dict(sd, strict=False)

@@ -16,7 +16,7 @@ def _pair(name):
     return ours, hf
 
 
-@pytest.mark.parametrize("name", ["t5-tiny", "bart-tiny"])
+@pytest.mark.parametrize("name", ["t5-tiny", "bart-tiny", "mbart-tiny", "pegasus-tiny", "marian-tiny"])
 @pytest.mark.parametrize("beams", [1, 2, 3])
 def test_generate_matches_hf(name, beams):
     ours, hf = _pair(name)
@@ -29,7 +29,7 @@ def test_generate_matches_hf(name, beams):
               early_stopping=False)
     a = ours.generate(ids, attention_mask=am, **kw)
     extra = {}
-    if ours.config.model_type == "bart":
+    if ours.config.model_type != "t5":
         extra = dict(forced_bos_token_id=ours.config.forced_bos_token_id,
                      forced_eos_token_id=ours.config.forced_eos_token_id)
     b = hf.generate(ids, attention_mask=am, do_sample=False, **kw, **extra)

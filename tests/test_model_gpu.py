@@ -14,8 +14,11 @@ pytestmark = pytest.mark.gpu
 def _cfg(name):
     c = resolve_config(name)
     # small but kernel-shaped (head dim 64)
-    return c.replace(num_layers=2, num_decoder_layers=2, vocab_size=4096, d_model=512 if c.model_type == "t5" else 512,
-                     num_heads=8, d_kv=64, d_ff=1024)
+    c = c.replace(num_layers=2, num_decoder_layers=2, vocab_size=4096, d_model=512 if c.model_type == "t5" else 512,
+                  num_heads=8, d_kv=64, d_ff=1024)
+    if c.pad_token_id >= c.vocab_size:  # Marian's pad / decoder start id is its last vocabulary entry
+        c = c.replace(pad_token_id=c.vocab_size - 1, decoder_start_token_id=c.vocab_size - 1)
+    return c
 
 
 def _batch(cfg, B=4, S=200, T=40):
@@ -42,7 +45,8 @@ def _grad_report(m_test, m_ref):
 
 
 @pytest.mark.parametrize("name,layers", [("t5-base", 2), ("flan-t5-base", 2), ("bart-base", 2), ("t5-base", 4),
-                                         ("bart-base", 4)])
+                                         ("bart-base", 4), ("mbart-large-cc25", 2), ("pegasus-large", 2),
+                                         ("opus-mt-en-de", 2)])
 def test_native_bf16_matches_fp32_reference(name, layers):
     """The bf16 HIP-kernel path vs the fp32 torch reference on the same (bf16-representable) weights and dropout
     masks: loss within 1 %, and EVERY parameter's gradient (relative_attention_bias included) checked on its own — a
@@ -95,7 +99,7 @@ def test_native_bf16_matches_fp32_reference(name, layers):
     assert not bad, bad[:5]
 
 
-@pytest.mark.parametrize("name", ["t5-base", "bart-base"])
+@pytest.mark.parametrize("name", ["t5-base", "bart-base", "mbart-large-cc25", "opus-mt-en-de"])
 def test_fp32_training_on_gpu_matches_reference(name):
     """fp32 end to end on the GPU (the reference's own precision, ref/train-torchrun.py:115-128): attention and the LM
     head take the explicit fp32 composite (ops/attention.py _native), norms / CE / AdamW run their fp32 HIP kernels.

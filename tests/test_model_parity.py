@@ -18,7 +18,7 @@ def _batch(V, B=2, S=23, T=9, pad_tail=True, pad_id=0):
     return ids, am, labels
 
 
-@pytest.mark.parametrize("name", ["t5-tiny", "t5-tiny-gated", "bart-tiny"])
+@pytest.mark.parametrize("name", ["t5-tiny", "t5-tiny-gated", "bart-tiny", "mbart-tiny", "pegasus-tiny", "marian-tiny"])
 def test_forward_backward_matches_hf(name):
     torch.manual_seed(0)
     ours = build_model(name).eval()
@@ -74,3 +74,25 @@ def test_t5_bucket_lut_matches_hf_bias():
             ref = table[b].permute(2, 0, 1)
             rel = torch.arange(k)[None, :] - torch.arange(q)[:, None] + (q - 1)
             torch.testing.assert_close(lut[:, rel], ref)
+
+
+@pytest.mark.parametrize("name", ["pegasus-tiny", "marian-tiny"])
+def test_sinusoidal_positions_match_hf(name):
+    """The fixed position table is our own (models/bart.py SinusoidalPositions), not copied from the oracle: compare it
+    with a freshly built transformers model's."""
+    ours = build_model(name)
+    fresh = hf_model_for(ours)
+    import transformers
+    cls = type(fresh)
+    hf = cls(fresh.config)
+    for stack in ("encoder", "decoder"):
+        a = getattr(ours.model, stack).embed_positions.weight
+        b = getattr(hf.model, stack).embed_positions.weight
+        torch.testing.assert_close(a, b.to(a.dtype), atol=1e-6, rtol=0)
+
+
+def test_mbart_decoder_inputs_start_with_the_language_id():
+    from transformers.models.mbart.modeling_mbart import shift_tokens_right
+    ours = build_model("mbart-tiny")
+    labels = torch.tensor([[5, 6, 7, 2, 250], [8, 9, 2, 251, -100]])
+    torch.testing.assert_close(ours.shift_right(labels), shift_tokens_right(labels, ours.config.pad_token_id))
