@@ -259,6 +259,12 @@ PRESETS: dict[str, Seq2SeqConfig] = {
     "flan-t5-base": _t5("flan-t5-base", 768, 2048, 12, 12, ff="gated-gelu", tie=False),
     "flan-t5-large": _t5("flan-t5-large", 1024, 2816, 24, 16, ff="gated-gelu", tie=False),
     "flan-t5-xl": _t5("flan-t5-xl", 2048, 5120, 24, 32, ff="gated-gelu", tie=False),
+    # T5 v1.1 and mT5 (multilingual: 250K SentencePiece vocabulary): the FLAN-T5 architecture
+    "t5-v1_1-base": _t5("t5-v1_1-base", 768, 2048, 12, 12, ff="gated-gelu", tie=False),
+    "t5-v1_1-large": _t5("t5-v1_1-large", 1024, 2816, 24, 16, ff="gated-gelu", tie=False),
+    "mt5-small": _t5("mt5-small", 512, 1024, 8, 6, ff="gated-gelu", tie=False, vocab=250112),
+    "mt5-base": _t5("mt5-base", 768, 2048, 12, 12, ff="gated-gelu", tie=False, vocab=250112),
+    "mt5-large": _t5("mt5-large", 1024, 2816, 24, 16, ff="gated-gelu", tie=False, vocab=250112),
     "bart-base": Seq2SeqConfig(
         model_type="bart", name="bart-base", vocab_size=50265, d_model=768, d_kv=64, d_ff=3072, num_layers=6,
         num_decoder_layers=6, num_heads=12, feed_forward_proj="gelu", dropout_rate=0.1, attention_dropout=0.0,
