@@ -1,5 +1,5 @@
 """BART (bart-large-cnn, the reference's default checkpoint: ref/valohai.yaml:10,36,65) and the other
-BART-family models ``AutoModelForSeq2SeqLM`` resolves to: mBART, Pegasus, Marian.
+BART-family models ``AutoModelForSeq2SeqLM`` resolves to: mBART, Pegasus, Marian, M2M100 / NLLB.
 
 Follows transformers' BartForConditionalGeneration (modeling_bart.py:835-958): learned positions
 with offset 2 (:74-98), ``layernorm_embedding`` + dropout after the embeddings (:507-549),
@@ -12,9 +12,9 @@ LayerDrop (encoder/decoder_layerdrop, 0.0 in every public BART config) is not im
 Family switches (models/config.py ``_FAMILY``; transformers modeling_mbart.py, modeling_pegasus.py,
 modeling_marian.py): pre-LN layers plus a final LayerNorm per stack (mBART, Pegasus) — there the residual update
 and the NEXT sub-layer's LayerNorm are one kernel returning both (as T5's RMSNorm blocks); no embedding LayerNorm
-(Pegasus, Marian); fixed sinusoidal positions without offset (Pegasus, Marian; sin in the first half of the
-features, cos in the second); SiLU FFN (Marian's ``swish``); mBART's decoder input starts from the label's last
-non-pad token (its language id).
+(Pegasus, Marian, M2M100); fixed sinusoidal positions without offset (Pegasus, Marian; sin in the first half of the
+features, cos in the second) or padding-aware with offset 2 (M2M100 / NLLB); SiLU FFN (Marian's ``swish``); no
+``final_logits_bias`` (M2M100); mBART's decoder input starts from the label's last non-pad token (its language id).
 """
 from __future__ import annotations
 
@@ -162,6 +162,28 @@ class BartLearnedPositionalEmbedding(nn.Embedding):
         super().__init__(n + self.offset, d)
 
 
+class M2M100Positions(nn.Module):
+    """Fixed positions of M2M100 / NLLB (modeling_m2m_100.py M2M100SinusoidalPositionalEmbedding): the tensor2tensor
+    table [sin | cos] of t * 10000^(-i / (d/2 - 1)), row ``pad`` zero; a token's position is pad + 1 + (its index among
+    the row's non-pad tokens, past cache length included), a pad token's is ``pad``.  Not in the checkpoint."""
+
+    def __init__(self, n, d, pad):
+        super().__init__()
+        half = d // 2
+        freq = torch.exp(torch.arange(half, dtype=torch.float32) * -(math.log(10000.0) / (half - 1)))
+        ang = torch.arange(n + 2, dtype=torch.float32)[:, None] * freq[None, :]
+        w = torch.cat([torch.sin(ang), torch.cos(ang)], dim=1)
+        if d % 2 == 1:
+            w = torch.cat([w, torch.zeros(n + 2, 1)], dim=1)
+        w[pad] = 0.0
+        self.pad = pad
+        self.register_buffer("weight", w, persistent=False)
+
+    def positions(self, input_ids, past: int):
+        keep = input_ids.ne(self.pad).long()
+        return (torch.cumsum(keep, dim=1) + past) * keep + self.pad
+
+
 class SinusoidalPositions(nn.Module):
     """Fixed positions of Pegasus / Marian (modeling_pegasus.py PegasusSinusoidalPositionalEmbedding.create_weight):
     feature j of position t is sin / cos of t / 10000^(2 floor(j/2) / d), the sines in the first half of the features
@@ -186,9 +208,13 @@ class BartStack(nn.Module):
         self.cfg = cfg
         self.is_decoder = is_decoder
         self._embed = [embed_tokens]
-        pos_cls = SinusoidalPositions if cfg.position_embedding == "sinusoidal" else BartLearnedPositionalEmbedding
-        self.embed_positions = pos_cls(cfg.max_position_embeddings, cfg.d_model)
-        self._pos_offset = pos_cls.offset
+        if cfg.position_embedding == "sinusoidal_m2m":
+            self.embed_positions = M2M100Positions(cfg.max_position_embeddings, cfg.d_model, cfg.pad_token_id)
+            self._pos_offset = None
+        else:
+            pos_cls = SinusoidalPositions if cfg.position_embedding == "sinusoidal" else BartLearnedPositionalEmbedding
+            self.embed_positions = pos_cls(cfg.max_position_embeddings, cfg.d_model)
+            self._pos_offset = pos_cls.offset
         n = cfg.num_decoder_layers if is_decoder else cfg.num_layers
         self.layers = nn.ModuleList([BartLayer(cfg, is_decoder) for _ in range(n)])
         if cfg.layernorm_embedding:
@@ -214,9 +240,12 @@ class BartStack(nn.Module):
         x = embedding(input_ids, self._embed[0].weight, padding_idx=cfg.pad_token_id)
         if self.embed_scale != 1.0:
             x = x * self.embed_scale
-        pos = torch.arange(q_offset, q_offset + S, device=input_ids.device) + self._pos_offset
         pw = self.embed_positions.weight
-        x = x + (embedding(pos, pw) if pw.requires_grad else pw[pos].to(x.dtype)).unsqueeze(0)
+        if self._pos_offset is None:  # padding-aware positions, one row per sequence
+            x = x + pw[self.embed_positions.positions(input_ids, q_offset)].to(x.dtype)
+        else:
+            pos = torch.arange(q_offset, q_offset + S, device=input_ids.device) + self._pos_offset
+            x = x + (embedding(pos, pw) if pw.requires_grad else pw[pos].to(x.dtype)).unsqueeze(0)
         if cfg.layernorm_embedding:
             x = norms.layer_norm(x, self.layernorm_embedding.weight, self.layernorm_embedding.bias,
                                  cfg.layer_norm_epsilon)
@@ -272,7 +301,10 @@ class BartForConditionalGeneration(nn.Module):
         super().__init__()
         self.config = cfg
         self.model = BartModel(cfg)
-        self.register_buffer("final_logits_bias", torch.zeros(1, cfg.vocab_size))
+        if cfg.final_logits_bias:  # BART / mBART / Pegasus / Marian; M2M100 has none
+            self.register_buffer("final_logits_bias", torch.zeros(1, cfg.vocab_size))
+        else:
+            self.final_logits_bias = None
         self.reset_parameters()
 
     @torch.no_grad()
@@ -292,7 +324,8 @@ class BartForConditionalGeneration(nn.Module):
             elif isinstance(m, nn.LayerNorm):
                 m.weight.fill_(1.0)
                 m.bias.zero_()
-        self.final_logits_bias.zero_()
+        if self.final_logits_bias is not None:
+            self.final_logits_bias.zero_()
 
     def shift_right(self, labels):
         """shift_tokens_right (modeling_bart.py:58-71); mBART (modeling_mbart.py shift_tokens_right): the first
@@ -324,10 +357,11 @@ class BartForConditionalGeneration(nn.Module):
         return self.model.shared.weight
 
     def logits_bias(self):
-        return self.final_logits_bias.view(-1)
+        return self.final_logits_bias.view(-1) if self.final_logits_bias is not None else None
 
     def lm_logits(self, hidden):
-        return linear(hidden, self.output_embedding()) + self.final_logits_bias.to(hidden.dtype)
+        logits = linear(hidden, self.output_embedding())
+        return logits + self.final_logits_bias.to(hidden.dtype) if self.final_logits_bias is not None else logits
 
     def cross_attention_modules(self):
         return [layer.encoder_attn for layer in self.model.decoder.layers]

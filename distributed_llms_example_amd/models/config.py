@@ -19,7 +19,7 @@ from dataclasses import dataclass, field
 
 @dataclass
 class Seq2SeqConfig:
-    model_type: str = "t5"  # "t5" | "bart" | "mbart" | "pegasus" | "marian" (the last three: BART-family switches below)
+    model_type: str = "t5"  # "t5" | "bart" | "mbart" | "pegasus" | "marian" | "m2m_100" (BART family: switches below)
     vocab_size: int = 32128
     d_model: int = 512
     d_kv: int = 64
@@ -52,7 +52,7 @@ class Seq2SeqConfig:
     # Marian); decoder start token = the last non-pad label token (mBART's language id) vs a fixed id
     normalize_before: bool = False
     layernorm_embedding: bool = True
-    position_embedding: str = "learned"  # "learned" | "sinusoidal"
+    position_embedding: str = "learned"  # "learned" | "sinusoidal" | "sinusoidal_m2m" (padding-aware, offset 2)
     shift_mode: str = "standard"  # "standard" | "mbart"
     # special tokens
     pad_token_id: int = 0
@@ -117,7 +117,8 @@ class Seq2SeqConfig:
             }
         else:
             arch = {"bart": "BartForConditionalGeneration", "mbart": "MBartForConditionalGeneration",
-                    "pegasus": "PegasusForConditionalGeneration", "marian": "MarianMTModel"}[self.model_type]
+                    "pegasus": "PegasusForConditionalGeneration", "marian": "MarianMTModel",
+                    "m2m_100": "M2M100ForConditionalGeneration"}[self.model_type]
             d = {
                 "architectures": [arch],
                 "model_type": self.model_type,
@@ -174,8 +175,8 @@ class Seq2SeqConfig:
                 pad_token_id=d.get("pad_token_id", 0), eos_token_id=_first(d.get("eos_token_id", 1)),
                 decoder_start_token_id=d.get("decoder_start_token_id", 0) or 0,
             )
-        if mt in ("bart", "mbart", "pegasus", "marian"):
-            fam = _FAMILY[mt]
+        if mt in _FAMILY:
+            fam = {"final_logits_bias": True, **_FAMILY[mt]}
             return cls(
                 model_type=mt, vocab_size=d.get("vocab_size", 50265), d_model=d.get("d_model", 1024),
                 d_kv=d.get("d_model", 1024) // d.get("encoder_attention_heads", 16),
@@ -185,7 +186,7 @@ class Seq2SeqConfig:
                 attention_dropout=d.get("attention_dropout", 0.0),
                 activation_dropout=d.get("activation_dropout", 0.0), layer_norm_epsilon=1e-5,
                 init_std=d.get("init_std", 0.02), max_position_embeddings=d.get("max_position_embeddings", 1024),
-                scale_embedding=d.get("scale_embedding", False), final_logits_bias=True,
+                scale_embedding=d.get("scale_embedding", False),
                 tie_word_embeddings=True, scale_decoder_outputs=False,
                 pad_token_id=d.get("pad_token_id", 1), eos_token_id=_first(d.get("eos_token_id", 2)),
                 bos_token_id=d.get("bos_token_id", 0 if mt in ("bart", "mbart") else None),
@@ -230,6 +231,9 @@ _FAMILY = {
                     shift_mode="standard"),
     "marian": dict(normalize_before=False, layernorm_embedding=False, position_embedding="sinusoidal",
                    shift_mode="standard"),
+    # M2M100 / NLLB: pre-LN, padding-aware sinusoidal positions (modeling_m2m_100.py), no final_logits_bias
+    "m2m_100": dict(normalize_before=True, layernorm_embedding=False, position_embedding="sinusoidal_m2m",
+                    shift_mode="standard", final_logits_bias=False),
 }
 
 
@@ -239,9 +243,9 @@ def _bartlike(mt, name, vocab, d_model, layers, heads, d_ff, act, max_pos, scale
         model_type=mt, name=name, vocab_size=vocab, d_model=d_model, d_kv=d_model // heads, d_ff=d_ff,
         num_layers=layers, num_decoder_layers=layers, num_heads=heads, feed_forward_proj=act, dropout_rate=dropout,
         attention_dropout=attn_dropout, activation_dropout=act_dropout, layer_norm_epsilon=1e-5,
-        final_logits_bias=True, scale_decoder_outputs=False, max_position_embeddings=max_pos,
+        scale_decoder_outputs=False, max_position_embeddings=max_pos,
         scale_embedding=scale_emb, pad_token_id=pad, eos_token_id=eos, bos_token_id=bos, decoder_start_token_id=start,
-        forced_bos_token_id=forced_bos, forced_eos_token_id=forced_eos, **_FAMILY[mt])
+        forced_bos_token_id=forced_bos, forced_eos_token_id=forced_eos, **{"final_logits_bias": True, **_FAMILY[mt]})
 
 
 def _t5(name, d_model, d_ff, layers, heads, ff="relu", tie=True, vocab=32128, d_kv=64):
@@ -294,6 +298,9 @@ PRESETS["pegasus-xsum"] = PRESETS["pegasus-large"].replace(
     generation={"max_length": 64, "length_penalty": 0.6, "num_beams": 8})
 PRESETS["opus-mt-en-de"] = _bartlike("marian", "opus-mt-en-de", 58101, 512, 6, 8, 2048, "swish", 512, True,
                                      pad=58100, eos=0, bos=None, start=58100, forced_eos=0)
+PRESETS["m2m100_418m"] = _bartlike("m2m_100", "m2m100_418m", 128112, 1024, 12, 16, 4096, "relu", 1024, True,
+                                   pad=1, eos=2, bos=0, start=2, attn_dropout=0.1, forced_eos=2)
+PRESETS["nllb-200-distilled-600m"] = PRESETS["m2m100_418m"].replace(name="nllb-200-distilled-600m", vocab_size=256206)
 # tiny configs for CPU tests
 PRESETS["t5-tiny"] = _t5("t5-tiny", 64, 128, 2, 4, vocab=512, d_kv=16)
 PRESETS["t5-tiny-gated"] = _t5("t5-tiny-gated", 64, 96, 2, 4, ff="gated-gelu", tie=False, vocab=512, d_kv=16)
@@ -304,6 +311,8 @@ PRESETS["mbart-tiny"] = _bartlike("mbart", "mbart-tiny", 512, 64, 2, 4, 128, "ge
                                   start=2, forced_eos=2)
 PRESETS["pegasus-tiny"] = _bartlike("pegasus", "pegasus-tiny", 512, 64, 2, 4, 128, "relu", 256, True, pad=0, eos=1,
                                     bos=None, start=0, attn_dropout=0.1, act_dropout=0.1, forced_eos=1)
+PRESETS["m2m100-tiny"] = _bartlike("m2m_100", "m2m100-tiny", 512, 64, 2, 4, 128, "relu", 256, True, pad=1, eos=2,
+                                   bos=0, start=2, attn_dropout=0.1, forced_eos=2)
 PRESETS["marian-tiny"] = _bartlike("marian", "marian-tiny", 512, 64, 2, 4, 128, "swish", 256, True, pad=511, eos=0,
                                    bos=None, start=511, forced_eos=0)
 

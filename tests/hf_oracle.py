@@ -15,7 +15,8 @@ def hf_model_for(model):
                "bart": (transformers.BartConfig, transformers.BartForConditionalGeneration),
                "mbart": (transformers.MBartConfig, transformers.MBartForConditionalGeneration),
                "pegasus": (transformers.PegasusConfig, transformers.PegasusForConditionalGeneration),
-               "marian": (transformers.MarianConfig, transformers.MarianMTModel)}
+               "marian": (transformers.MarianConfig, transformers.MarianMTModel),
+               "m2m_100": (transformers.M2M100Config, transformers.M2M100ForConditionalGeneration)}
     cfg_cls, model_cls = classes[mt]
     hcfg = cfg_cls(**d)
     hf = model_cls(hcfg)

@@ -46,7 +46,7 @@ def _grad_report(m_test, m_ref):
 
 @pytest.mark.parametrize("name,layers", [("t5-base", 2), ("flan-t5-base", 2), ("bart-base", 2), ("t5-base", 4),
                                          ("bart-base", 4), ("mbart-large-cc25", 2), ("pegasus-large", 2),
-                                         ("opus-mt-en-de", 2)])
+                                         ("opus-mt-en-de", 2), ("m2m100_418m", 2)])
 def test_native_bf16_matches_fp32_reference(name, layers):
     """The bf16 HIP-kernel path vs the fp32 torch reference on the same (bf16-representable) weights and dropout
     masks: loss within 1 %, and EVERY parameter's gradient (relative_attention_bias included) checked on its own — a
