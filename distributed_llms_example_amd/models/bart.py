@@ -1,5 +1,5 @@
 """BART (bart-large-cnn, the reference's default checkpoint: ref/valohai.yaml:10,36,65) and the other
-BART-family models ``AutoModelForSeq2SeqLM`` resolves to: mBART, Pegasus, Marian, M2M100 / NLLB.
+BART-family models ``AutoModelForSeq2SeqLM`` resolves to: mBART, Pegasus, Marian, M2M100 / NLLB, PLBart, Blenderbot.
 
 Follows transformers' BartForConditionalGeneration (modeling_bart.py:835-958): learned positions
 with offset 2 (:74-98), ``layernorm_embedding`` + dropout after the embeddings (:507-549),
@@ -14,7 +14,8 @@ modeling_marian.py): pre-LN layers plus a final LayerNorm per stack (mBART, Pega
 and the NEXT sub-layer's LayerNorm are one kernel returning both (as T5's RMSNorm blocks); no embedding LayerNorm
 (Pegasus, Marian, M2M100); fixed sinusoidal positions without offset (Pegasus, Marian; sin in the first half of the
 features, cos in the second) or padding-aware with offset 2 (M2M100 / NLLB); SiLU FFN (Marian's ``swish``); no
-``final_logits_bias`` (M2M100); mBART's decoder input starts from the label's last non-pad token (its language id).
+``final_logits_bias`` (M2M100); learned positions without the offset 2 (Blenderbot); mBART's and PLBart's decoder
+input starts from the label's last non-pad token (the language id).
 """
 from __future__ import annotations
 
@@ -162,6 +163,11 @@ class BartLearnedPositionalEmbedding(nn.Embedding):
         super().__init__(n + self.offset, d)
 
 
+class LearnedPositionalEmbedding0(BartLearnedPositionalEmbedding):
+    """Blenderbot's learned positions: no offset (modeling_blenderbot.py BlenderbotLearnedPositionalEmbedding)."""
+    offset = 0
+
+
 class M2M100Positions(nn.Module):
     """Fixed positions of M2M100 / NLLB (modeling_m2m_100.py M2M100SinusoidalPositionalEmbedding): the tensor2tensor
     table [sin | cos] of t * 10000^(-i / (d/2 - 1)), row ``pad`` zero; a token's position is pad + 1 + (its index among
@@ -212,7 +218,8 @@ class BartStack(nn.Module):
             self.embed_positions = M2M100Positions(cfg.max_position_embeddings, cfg.d_model, cfg.pad_token_id)
             self._pos_offset = None
         else:
-            pos_cls = SinusoidalPositions if cfg.position_embedding == "sinusoidal" else BartLearnedPositionalEmbedding
+            pos_cls = {"sinusoidal": SinusoidalPositions, "learned0": LearnedPositionalEmbedding0}.get(
+                cfg.position_embedding, BartLearnedPositionalEmbedding)
             self.embed_positions = pos_cls(cfg.max_position_embeddings, cfg.d_model)
             self._pos_offset = pos_cls.offset
         n = cfg.num_decoder_layers if is_decoder else cfg.num_layers

@@ -19,7 +19,7 @@ from dataclasses import dataclass, field
 
 @dataclass
 class Seq2SeqConfig:
-    model_type: str = "t5"  # "t5" | "bart" | "mbart" | "pegasus" | "marian" | "m2m_100" (BART family: switches below)
+    model_type: str = "t5"  # "t5" | BART family: "bart" | "mbart" | "pegasus" | "marian" | "m2m_100" | "plbart" | "blenderbot"
     vocab_size: int = 32128
     d_model: int = 512
     d_kv: int = 64
@@ -52,7 +52,7 @@ class Seq2SeqConfig:
     # Marian); decoder start token = the last non-pad label token (mBART's language id) vs a fixed id
     normalize_before: bool = False
     layernorm_embedding: bool = True
-    position_embedding: str = "learned"  # "learned" | "sinusoidal" | "sinusoidal_m2m" (padding-aware, offset 2)
+    position_embedding: str = "learned"  # "learned" (offset 2) | "learned0" | "sinusoidal" | "sinusoidal_m2m"
     shift_mode: str = "standard"  # "standard" | "mbart"
     # special tokens
     pad_token_id: int = 0
@@ -118,7 +118,8 @@ class Seq2SeqConfig:
         else:
             arch = {"bart": "BartForConditionalGeneration", "mbart": "MBartForConditionalGeneration",
                     "pegasus": "PegasusForConditionalGeneration", "marian": "MarianMTModel",
-                    "m2m_100": "M2M100ForConditionalGeneration"}[self.model_type]
+                    "m2m_100": "M2M100ForConditionalGeneration", "plbart": "PLBartForConditionalGeneration",
+                    "blenderbot": "BlenderbotForConditionalGeneration"}[self.model_type]
             d = {
                 "architectures": [arch],
                 "model_type": self.model_type,
@@ -231,6 +232,11 @@ _FAMILY = {
                     shift_mode="standard"),
     "marian": dict(normalize_before=False, layernorm_embedding=False, position_embedding="sinusoidal",
                    shift_mode="standard"),
+    # PLBart: BART layers with mBART's language-id decoder start (modeling_plbart.py)
+    "plbart": dict(normalize_before=False, layernorm_embedding=True, position_embedding="learned", shift_mode="mbart"),
+    # Blenderbot: pre-LN, learned positions without offset, no embedding LayerNorm (modeling_blenderbot.py)
+    "blenderbot": dict(normalize_before=True, layernorm_embedding=False, position_embedding="learned0",
+                       shift_mode="standard"),
     # M2M100 / NLLB: pre-LN, padding-aware sinusoidal positions (modeling_m2m_100.py), no final_logits_bias
     "m2m_100": dict(normalize_before=True, layernorm_embedding=False, position_embedding="sinusoidal_m2m",
                     shift_mode="standard", final_logits_bias=False),
@@ -238,10 +244,10 @@ _FAMILY = {
 
 
 def _bartlike(mt, name, vocab, d_model, layers, heads, d_ff, act, max_pos, scale_emb, pad, eos, bos, start,
-              dropout=0.1, attn_dropout=0.0, act_dropout=0.0, forced_bos=None, forced_eos=None):
+              dropout=0.1, attn_dropout=0.0, act_dropout=0.0, forced_bos=None, forced_eos=None, dec_layers=None):
     return Seq2SeqConfig(
         model_type=mt, name=name, vocab_size=vocab, d_model=d_model, d_kv=d_model // heads, d_ff=d_ff,
-        num_layers=layers, num_decoder_layers=layers, num_heads=heads, feed_forward_proj=act, dropout_rate=dropout,
+        num_layers=layers, num_decoder_layers=dec_layers or layers, num_heads=heads, feed_forward_proj=act, dropout_rate=dropout,
         attention_dropout=attn_dropout, activation_dropout=act_dropout, layer_norm_epsilon=1e-5,
         scale_decoder_outputs=False, max_position_embeddings=max_pos,
         scale_embedding=scale_emb, pad_token_id=pad, eos_token_id=eos, bos_token_id=bos, decoder_start_token_id=start,
@@ -300,6 +306,11 @@ PRESETS["opus-mt-en-de"] = _bartlike("marian", "opus-mt-en-de", 58101, 512, 6, 8
                                      pad=58100, eos=0, bos=None, start=58100, forced_eos=0)
 PRESETS["m2m100_418m"] = _bartlike("m2m_100", "m2m100_418m", 128112, 1024, 12, 16, 4096, "relu", 1024, True,
                                    pad=1, eos=2, bos=0, start=2, attn_dropout=0.1, forced_eos=2)
+PRESETS["plbart-base"] = _bartlike("plbart", "plbart-base", 50005, 768, 6, 12, 3072, "gelu", 1024, True, pad=1, eos=2,
+                                   bos=0, start=2, forced_eos=2)
+PRESETS["blenderbot-400m-distill"] = _bartlike("blenderbot", "blenderbot-400m-distill", 8008, 1280, 2, 32, 5120,
+                                               "gelu", 128, True, pad=0, eos=2, bos=1, start=1, forced_eos=2,
+                                               dec_layers=12)
 PRESETS["nllb-200-distilled-600m"] = PRESETS["m2m100_418m"].replace(name="nllb-200-distilled-600m", vocab_size=256206)
 # tiny configs for CPU tests
 PRESETS["t5-tiny"] = _t5("t5-tiny", 64, 128, 2, 4, vocab=512, d_kv=16)
@@ -313,6 +324,10 @@ PRESETS["pegasus-tiny"] = _bartlike("pegasus", "pegasus-tiny", 512, 64, 2, 4, 12
                                     bos=None, start=0, attn_dropout=0.1, act_dropout=0.1, forced_eos=1)
 PRESETS["m2m100-tiny"] = _bartlike("m2m_100", "m2m100-tiny", 512, 64, 2, 4, 128, "relu", 256, True, pad=1, eos=2,
                                    bos=0, start=2, attn_dropout=0.1, forced_eos=2)
+PRESETS["plbart-tiny"] = _bartlike("plbart", "plbart-tiny", 512, 64, 2, 4, 128, "gelu", 256, True, pad=1, eos=2, bos=0,
+                                   start=2, forced_eos=2)
+PRESETS["blenderbot-tiny"] = _bartlike("blenderbot", "blenderbot-tiny", 512, 64, 1, 4, 128, "gelu", 256, True, pad=0,
+                                       eos=2, bos=1, start=1, forced_eos=2, dec_layers=2)
 PRESETS["marian-tiny"] = _bartlike("marian", "marian-tiny", 512, 64, 2, 4, 128, "swish", 256, True, pad=511, eos=0,
                                    bos=None, start=511, forced_eos=0)
 

@@ -16,7 +16,9 @@ def hf_model_for(model):
                "mbart": (transformers.MBartConfig, transformers.MBartForConditionalGeneration),
                "pegasus": (transformers.PegasusConfig, transformers.PegasusForConditionalGeneration),
                "marian": (transformers.MarianConfig, transformers.MarianMTModel),
-               "m2m_100": (transformers.M2M100Config, transformers.M2M100ForConditionalGeneration)}
+               "m2m_100": (transformers.M2M100Config, transformers.M2M100ForConditionalGeneration),
+               "plbart": (transformers.PLBartConfig, transformers.PLBartForConditionalGeneration),
+               "blenderbot": (transformers.BlenderbotConfig, transformers.BlenderbotForConditionalGeneration)}
     cfg_cls, model_cls = classes[mt]
     hcfg = cfg_cls(**d)
     hf = model_cls(hcfg)

@@ -59,7 +59,7 @@ def test_fused_adamw_reference_matches_torch_with_clip():
 
 def test_checkpoint_loads_in_transformers(tmp_path):
     import transformers
-    for name in ("t5-tiny", "bart-tiny", "mbart-tiny", "pegasus-tiny", "marian-tiny", "m2m100-tiny"):
+    for name in ("t5-tiny", "bart-tiny", "mbart-tiny", "pegasus-tiny", "marian-tiny", "m2m100-tiny", "plbart-tiny", "blenderbot-tiny"):
         m = build_model(name).eval()
         d = tmp_path / name
         save_pretrained(m, str(d))
