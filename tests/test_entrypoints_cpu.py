@@ -41,8 +41,9 @@ def _json_lines(out):
 COMMON = ["--synthetic", "32", "--max-source-length", "40", "--max-target-length", "10", "--gen-max-length", "8"]
 
 
-def test_train_torchrun_single_process(tmp_path):
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "train-torchrun.py"), "--model-ckpt", "t5-tiny",
+@pytest.mark.parametrize("model", ["t5-tiny", "mbart-tiny", "pegasus-tiny"])
+def test_train_torchrun_single_process(tmp_path, model):
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "train-torchrun.py"), "--model-ckpt", model,
                         "--output-dir", "out", "--batch-size", "4", "--grad-accum", "2", "--evaluation-steps", "2",
                         "--warmup-steps", "1", *COMMON], env=_env(tmp_path), capture_output=True, text=True,
                        timeout=300)
