@@ -1270,14 +1270,10 @@ void launch_fwd_t(const AttnParams& p, int nblk, size_t lds, hipStream_t st) {
 }
 template <bool HB, bool HK, bool CA, bool DR>
 void launch_bwd_dq_t(const AttnParams& p, int nblk, size_t lds, hipStream_t st) {
-  static const int occ_env = [] {
+  static const int occ = [] {
     const char* e = getenv("DLLM_ATTN_DQ_OCC");
-    return e != nullptr ? atoi(e) : 0;
+    return e != nullptr ? atoi(e) : 2;  // 3 measured equal (profiles/r2_ab_attn_dq_halves.txt)
   }();
-  // 2 per CU by default (3 measured equal on large grids, profiles/r2_ab_attn_dq_halves.txt); 3 where it saves a
-  // whole round of a small grid (batch 8 at 1024 tokens: 768 blocks = 1 round at 3 per CU instead of 1.5 at 2)
-  const int cus = 256, r2 = (nblk + 2 * cus - 1) / (2 * cus), r3 = (nblk + 3 * cus - 1) / (3 * cus);
-  const int occ = occ_env != 0 ? occ_env : (r2 <= 2 && r3 < r2 ? 3 : 2);
   if (occ == 3 && !CA && 3 * lds <= 160 * 1024)  // the causal variant spills at 168 VGPRs
     hipLaunchKernelGGL((attn_bwd_dq_kernel<HB, HK, CA, DR, 3>), dim3(nblk), dim3(256), lds, st, p);
   else
