@@ -135,8 +135,10 @@ def test_fp32_training_on_gpu_matches_reference(name):
     assert ((p1 - p0).norm() / p0.norm()).item() < 1e-5
 
 
-def test_generate_on_gpu():
-    cfg = _cfg("bart-base")
+@pytest.mark.parametrize("name", ["bart-base", "mbart-large-cc25", "pegasus-large", "opus-mt-en-de", "m2m100_418m",
+                                  "blenderbot-400m-distill"])
+def test_generate_on_gpu(name):
+    cfg = _cfg(name)
     m = build_model(cfg).cuda().to(torch.bfloat16).eval()
     ids = torch.randint(3, cfg.vocab_size, (3, 50), device="cuda")
     out = m.generate(ids, attention_mask=torch.ones_like(ids), max_length=12, num_beams=2)
