@@ -20,6 +20,9 @@ from dataclasses import dataclass, field
 @dataclass
 class Seq2SeqConfig:
     model_type: str = "t5"  # "t5" | BART family: "bart" | "mbart" | "pegasus" | "marian" | "m2m_100" | "plbart" | "blenderbot"
+    # T5 implementation variants: "t5" / "mt5" (same layers), "umt5" (every self-attention layer owns its
+    # relative-position bias table: modeling_umt5.py UMT5LayerSelfAttention, has_relative_attention_bias=True)
+    t5_flavor: str = "t5"
     vocab_size: int = 32128
     d_model: int = 512
     d_kv: int = 64
@@ -74,6 +77,10 @@ class Seq2SeqConfig:
         return self.feed_forward_proj.startswith("gated")
 
     @property
+    def per_layer_position_bias(self) -> bool:
+        return self.model_type == "t5" and self.t5_flavor == "umt5"
+
+    @property
     def act(self) -> str:
         a = self.feed_forward_proj.split("-")[-1]
         if self.feed_forward_proj == "gated-gelu":
@@ -94,8 +101,9 @@ class Seq2SeqConfig:
     def to_hf_dict(self) -> dict:
         if self.model_type == "t5":
             d = {
-                "architectures": ["T5ForConditionalGeneration"],
-                "model_type": "t5",
+                "architectures": [{"t5": "T5ForConditionalGeneration", "mt5": "MT5ForConditionalGeneration",
+                                   "umt5": "UMT5ForConditionalGeneration"}[self.t5_flavor]],
+                "model_type": self.t5_flavor,
                 "vocab_size": self.vocab_size,
                 "d_model": self.d_model,
                 "d_kv": self.d_kv,
@@ -158,12 +166,12 @@ class Seq2SeqConfig:
     @classmethod
     def from_hf_dict(cls, d: dict) -> "Seq2SeqConfig":
         mt = d.get("model_type", "t5")
-        if mt in ("t5", "mt5"):
+        if mt in ("t5", "mt5", "umt5"):
             ff = d.get("feed_forward_proj", "relu")
             nl = d.get("num_layers", 6)
             tie = d.get("tie_word_embeddings", True)
             return cls(
-                model_type="t5", vocab_size=d.get("vocab_size", 32128), d_model=d.get("d_model", 512),
+                model_type="t5", t5_flavor=mt, vocab_size=d.get("vocab_size", 32128), d_model=d.get("d_model", 512),
                 d_kv=d.get("d_kv", 64), d_ff=d.get("d_ff", 2048), num_layers=nl,
                 num_decoder_layers=d.get("num_decoder_layers") or nl, num_heads=d.get("num_heads", 8),
                 relative_attention_num_buckets=d.get("relative_attention_num_buckets", 32),
@@ -254,8 +262,9 @@ def _bartlike(mt, name, vocab, d_model, layers, heads, d_ff, act, max_pos, scale
         forced_bos_token_id=forced_bos, forced_eos_token_id=forced_eos, **{"final_logits_bias": True, **_FAMILY[mt]})
 
 
-def _t5(name, d_model, d_ff, layers, heads, ff="relu", tie=True, vocab=32128, d_kv=64):
-    return Seq2SeqConfig(model_type="t5", name=name, vocab_size=vocab, d_model=d_model, d_kv=d_kv, d_ff=d_ff,
+def _t5(name, d_model, d_ff, layers, heads, ff="relu", tie=True, vocab=32128, d_kv=64, flavor="t5"):
+    return Seq2SeqConfig(model_type="t5", t5_flavor=flavor, name=name, vocab_size=vocab, d_model=d_model, d_kv=d_kv,
+                         d_ff=d_ff,
                          num_layers=layers, num_decoder_layers=layers, num_heads=heads, feed_forward_proj=ff,
                          tie_word_embeddings=tie, scale_decoder_outputs=tie)
 
@@ -272,9 +281,13 @@ PRESETS: dict[str, Seq2SeqConfig] = {
     # T5 v1.1 and mT5 (multilingual: 250K SentencePiece vocabulary): the FLAN-T5 architecture
     "t5-v1_1-base": _t5("t5-v1_1-base", 768, 2048, 12, 12, ff="gated-gelu", tie=False),
     "t5-v1_1-large": _t5("t5-v1_1-large", 1024, 2816, 24, 16, ff="gated-gelu", tie=False),
-    "mt5-small": _t5("mt5-small", 512, 1024, 8, 6, ff="gated-gelu", tie=False, vocab=250112),
-    "mt5-base": _t5("mt5-base", 768, 2048, 12, 12, ff="gated-gelu", tie=False, vocab=250112),
-    "mt5-large": _t5("mt5-large", 1024, 2816, 24, 16, ff="gated-gelu", tie=False, vocab=250112),
+    "mt5-small": _t5("mt5-small", 512, 1024, 8, 6, ff="gated-gelu", tie=False, vocab=250112, flavor="mt5"),
+    "mt5-base": _t5("mt5-base", 768, 2048, 12, 12, ff="gated-gelu", tie=False, vocab=250112, flavor="mt5"),
+    "mt5-large": _t5("mt5-large", 1024, 2816, 24, 16, ff="gated-gelu", tie=False, vocab=250112, flavor="mt5"),
+    # UMT5: the mT5 architecture with a relative-position bias table in every self-attention layer
+    "umt5-small": _t5("umt5-small", 512, 1024, 8, 6, ff="gated-gelu", tie=False, vocab=256384, flavor="umt5"),
+    "umt5-base": _t5("umt5-base", 768, 2048, 12, 12, ff="gated-gelu", tie=False, vocab=256384, flavor="umt5"),
+    "umt5-xl": _t5("umt5-xl", 2048, 5120, 24, 32, ff="gated-gelu", tie=False, vocab=256384, flavor="umt5"),
     "bart-base": Seq2SeqConfig(
         model_type="bart", name="bart-base", vocab_size=50265, d_model=768, d_kv=64, d_ff=3072, num_layers=6,
         num_decoder_layers=6, num_heads=12, feed_forward_proj="gelu", dropout_rate=0.1, attention_dropout=0.0,
@@ -315,6 +328,7 @@ PRESETS["nllb-200-distilled-600m"] = PRESETS["m2m100_418m"].replace(name="nllb-2
 # tiny configs for CPU tests
 PRESETS["t5-tiny"] = _t5("t5-tiny", 64, 128, 2, 4, vocab=512, d_kv=16)
 PRESETS["t5-tiny-gated"] = _t5("t5-tiny-gated", 64, 96, 2, 4, ff="gated-gelu", tie=False, vocab=512, d_kv=16)
+PRESETS["umt5-tiny"] = _t5("umt5-tiny", 64, 96, 2, 4, ff="gated-gelu", tie=True, vocab=512, d_kv=16, flavor="umt5")
 PRESETS["bart-tiny"] = PRESETS["bart-base"].replace(name="bart-tiny", vocab_size=512, d_model=64, d_kv=16, d_ff=128,
                                                     num_layers=2, num_decoder_layers=2, num_heads=4,
                                                     max_position_embeddings=256)

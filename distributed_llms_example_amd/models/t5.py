@@ -9,7 +9,8 @@ reference fine-tunes through ``AutoModelForSeq2SeqLM``), restructured for MI355X
 * every residual update ``h + dropout(sublayer)`` is fused with the NEXT sub-layer's RMSNorm
   (ops/norms.py), so the residual stream is read/written once per sub-layer;
 * the relative-position bias is a per-head LUT (ops/attention.py) — layer 0 owns the bucket table
-  and every layer reuses it (modeling_t5.py:739-740), as in HF;
+  and every layer reuses it (modeling_t5.py:739-740), as in HF; UMT5 (``t5_flavor="umt5"``) gives every
+  self-attention layer its own table (modeling_umt5.py UMT5LayerSelfAttention), one LUT per layer;
 * LM head + cross-entropy: logits in bf16, CE fused (ops/cross_entropy.py), the
   ``d_model**-0.5`` tied-embedding scale (modeling_t5.py:1044-1045) applied to the decoder output.
 """
@@ -169,7 +170,8 @@ class T5Stack(nn.Module):
         self.is_decoder = is_decoder
         self._embed = [embed_tokens]  # shared; not registered twice
         n = cfg.num_decoder_layers if is_decoder else cfg.num_layers
-        self.block = nn.ModuleList([T5Block(cfg, has_bias=(i == 0), is_decoder=is_decoder) for i in range(n)])
+        self.block = nn.ModuleList([T5Block(cfg, has_bias=(i == 0 or cfg.per_layer_position_bias), is_decoder=is_decoder)
+                                    for i in range(n)])
         self.final_layer_norm = T5LayerNorm(cfg.d_model, cfg.layer_norm_epsilon)
 
     def cross_kv_linears(self):
@@ -192,12 +194,14 @@ class T5Stack(nn.Module):
         k_len = S + q_offset
         cp = getattr(self, "_cp_group", False)
         chunk = long_sequence_chunk(S, rows=B * cfg.num_heads) if not self.is_decoder and caches is None else None
-        if (cp is not False or chunk is not None) and not self.is_decoder:
-            lut = _CPBias(cp, self.block[0].layer[0].SelfAttention.relative_attention_bias.weight,
-                          chunk=chunk if cp is False else None)
-        else:
-            lut = self.block[0].layer[0].SelfAttention.bias_lut(S, k_len, q_offset=q_offset)
         blocks = list(self.block)
+        # T5 / mT5: layer 0's table serves every layer; UMT5: each layer's own table
+        owners = blocks if cfg.per_layer_position_bias else blocks[:1]
+        if (cp is not False or chunk is not None) and not self.is_decoder:
+            luts = [_CPBias(cp, b.layer[0].SelfAttention.relative_attention_bias.weight,
+                            chunk=chunk if cp is False else None) for b in owners]
+        else:
+            luts = [b.layer[0].SelfAttention.bias_lut(S, k_len, q_offset=q_offset) for b in owners]
         # h = dropout(embeddings); normed = block0 self-attn norm(h)
         normed, h = norms.dropout_rms_norm(x, blocks[0].layer[0].layer_norm.weight, eps, p,
                                            rng.next_seed() if p > 0 else 0)
@@ -207,8 +211,9 @@ class T5Stack(nn.Module):
             nxt = blocks[i + 1].layer[0].layer_norm.weight if i + 1 < len(blocks) else self.final_layer_norm.weight
             ckv = cross_kv[i] if cross_kv is not None else None
             cache = caches[i] if caches is not None else None
+            lut = luts[i if len(luts) > 1 else 0]
 
-            def run(normed, h, blk=blk, nxt=nxt, ckv=ckv, cache=cache):
+            def run(normed, h, blk=blk, nxt=nxt, ckv=ckv, cache=cache, lut=lut):
                 return self._block(blk, nxt, normed, h, attention_mask, lut, enc_out, enc_mask, ckv, cache, p, pa, eps)
 
             normed, h = run_block(run, normed, h, checkpoint=cfg.gradient_checkpointing and self.training and

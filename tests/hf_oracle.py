@@ -12,6 +12,8 @@ def hf_model_for(model):
     d.pop("torch_dtype", None)
     mt = d.pop("model_type")
     classes = {"t5": (transformers.T5Config, transformers.T5ForConditionalGeneration),
+               "mt5": (transformers.MT5Config, transformers.MT5ForConditionalGeneration),
+               "umt5": (transformers.UMT5Config, transformers.UMT5ForConditionalGeneration),
                "bart": (transformers.BartConfig, transformers.BartForConditionalGeneration),
                "mbart": (transformers.MBartConfig, transformers.MBartForConditionalGeneration),
                "pegasus": (transformers.PegasusConfig, transformers.PegasusForConditionalGeneration),
@@ -20,9 +22,10 @@ def hf_model_for(model):
                "plbart": (transformers.PLBartConfig, transformers.PLBartForConditionalGeneration),
                "blenderbot": (transformers.BlenderbotConfig, transformers.BlenderbotForConditionalGeneration)}
     cfg_cls, model_cls = classes[mt]
-    hcfg = cfg_cls(**d)
+    # eager attention everywhere (the stacks' sub-configs included): transformers' SDPA path for UMT5 drops the
+    # position bias and the decoder's causal mask
+    hcfg = cfg_cls(**d, attn_implementation="eager")
     hf = model_cls(hcfg)
-    hcfg._attn_implementation = "eager"
     sd = to_hf_state_dict(model)
     missing, unexpected = hf.load_state_dict(sd, strict=False)
     allowed = {"encoder.embed_tokens.weight", "decoder.embed_tokens.weight", "lm_head.weight",

@@ -97,11 +97,11 @@ def test_merge_and_block_math_single_process():
     torch.testing.assert_close(om2, o1, atol=1e-6, rtol=1e-6)
 
 
-def _t5_cp_case(rank, world):
+def _t5_cp_case(rank, world, name="t5-tiny"):
     from distributed_llms_example_amd.models import build_model
     from distributed_llms_example_amd.parallel.context import shard_sequence
     torch.manual_seed(0)
-    model = build_model("t5-tiny").eval()
+    model = build_model(name).eval()
     model.enable_context_parallel(None)
     g = torch.Generator().manual_seed(5)
     ids = torch.randint(3, 500, (3, 16), generator=g)
@@ -118,12 +118,13 @@ def _t5_cp_case(rank, world):
     return out.loss.detach(), grads
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_t5_context_parallel_matches_single_process(world):
+@pytest.mark.parametrize("world,name", [(2, "t5-tiny"), (4, "t5-tiny"), (2, "umt5-tiny")])
+def test_t5_context_parallel_matches_single_process(world, name):
+    import functools
     from distributed_llms_example_amd.models import build_model
-    out = run_ranks(_t5_cp_case, world=world)
+    out = run_ranks(functools.partial(_t5_cp_case, name=name), world=world)
     torch.manual_seed(0)
-    model = build_model("t5-tiny").eval()
+    model = build_model(name).eval()
     g = torch.Generator().manual_seed(5)
     ids = torch.randint(3, 500, (3, 16), generator=g)
     mask = torch.ones(3, 16, dtype=torch.long)
@@ -150,11 +151,12 @@ def test_chunked_attention_matches_full():
         torch.testing.assert_close(x.grad, y, atol=5e-5, rtol=1e-4)
 
 
-def test_t5_long_sequence_chunked_encoder(monkeypatch):
+@pytest.mark.parametrize("name", ["t5-tiny", "umt5-tiny"])
+def test_t5_long_sequence_chunked_encoder(monkeypatch, name):
     """Above DLLM_ATTN_CHUNK_MIN tokens the T5 encoder runs chunked attention: same loss and gradients."""
     from distributed_llms_example_amd.models import build_model
     torch.manual_seed(0)
-    model = build_model("t5-tiny").eval()
+    model = build_model(name).eval()
     g = torch.Generator().manual_seed(5)
     ids = torch.randint(3, 500, (2, 24), generator=g)
     mask = torch.ones(2, 24, dtype=torch.long)

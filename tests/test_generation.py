@@ -16,7 +16,7 @@ def _pair(name):
     return ours, hf
 
 
-@pytest.mark.parametrize("name", ["t5-tiny", "bart-tiny", "mbart-tiny", "pegasus-tiny", "marian-tiny", "m2m100-tiny", "plbart-tiny", "blenderbot-tiny"])
+@pytest.mark.parametrize("name", ["t5-tiny", "umt5-tiny", "bart-tiny", "mbart-tiny", "pegasus-tiny", "marian-tiny", "m2m100-tiny", "plbart-tiny", "blenderbot-tiny"])
 @pytest.mark.parametrize("beams", [1, 2, 3])
 def test_generate_matches_hf(name, beams):
     ours, hf = _pair(name)

@@ -46,7 +46,7 @@ def _grad_report(m_test, m_ref):
 
 @pytest.mark.parametrize("name,layers", [("t5-base", 2), ("flan-t5-base", 2), ("bart-base", 2), ("t5-base", 4),
                                          ("bart-base", 4), ("mbart-large-cc25", 2), ("pegasus-large", 2),
-                                         ("opus-mt-en-de", 2), ("m2m100_418m", 2)])
+                                         ("opus-mt-en-de", 2), ("m2m100_418m", 2), ("umt5-base", 2)])
 def test_native_bf16_matches_fp32_reference(name, layers):
     """The bf16 HIP-kernel path vs the fp32 torch reference on the same (bf16-representable) weights and dropout
     masks: loss within 1 %, and EVERY parameter's gradient (relative_attention_bias included) checked on its own — a
@@ -87,7 +87,8 @@ def test_native_bf16_matches_fp32_reference(name, layers):
     floor = {n: (rel, cos) for rel, cos, n in _grad_report(t16, m32)}
     names = {n for _, _, n in rep}
     if cfg.model_type == "t5":
-        assert any("relative_attention_bias" in n for n in names)
+        nb = sum("relative_attention_bias" in n for n in names)
+        assert nb == (2 * layers if cfg.per_layer_position_bias else 2), nb
     bad = []
     for rel, cos, n in rep:
         frel, fcos = floor[n]
@@ -136,7 +137,7 @@ def test_fp32_training_on_gpu_matches_reference(name):
 
 
 @pytest.mark.parametrize("name", ["bart-base", "mbart-large-cc25", "pegasus-large", "opus-mt-en-de", "m2m100_418m",
-                                  "blenderbot-400m-distill"])
+                                  "blenderbot-400m-distill", "umt5-base"])
 def test_generate_on_gpu(name):
     cfg = _cfg(name)
     m = build_model(cfg).cuda().to(torch.bfloat16).eval()

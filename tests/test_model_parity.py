@@ -18,7 +18,7 @@ def _batch(V, B=2, S=23, T=9, pad_tail=True, pad_id=0):
     return ids, am, labels
 
 
-@pytest.mark.parametrize("name", ["t5-tiny", "t5-tiny-gated", "bart-tiny", "mbart-tiny", "pegasus-tiny", "marian-tiny", "m2m100-tiny", "plbart-tiny", "blenderbot-tiny"])
+@pytest.mark.parametrize("name", ["t5-tiny", "t5-tiny-gated", "umt5-tiny", "bart-tiny", "mbart-tiny", "pegasus-tiny", "marian-tiny", "m2m100-tiny", "plbart-tiny", "blenderbot-tiny"])
 def test_forward_backward_matches_hf(name):
     torch.manual_seed(0)
     ours = build_model(name).eval()

@@ -59,11 +59,13 @@ def test_fused_adamw_reference_matches_torch_with_clip():
 
 def test_checkpoint_loads_in_transformers(tmp_path):
     import transformers
-    for name in ("t5-tiny", "bart-tiny", "mbart-tiny", "pegasus-tiny", "marian-tiny", "m2m100-tiny", "plbart-tiny", "blenderbot-tiny"):
+    for name in ("t5-tiny", "umt5-tiny", "bart-tiny", "mbart-tiny", "pegasus-tiny", "marian-tiny", "m2m100-tiny",
+                 "plbart-tiny", "blenderbot-tiny"):
         m = build_model(name).eval()
         d = tmp_path / name
         save_pretrained(m, str(d))
-        hf = transformers.AutoModelForSeq2SeqLM.from_pretrained(str(d)).eval()
+        # eager: transformers' SDPA path for UMT5 drops the position bias (tests/hf_oracle.py)
+        hf = transformers.AutoModelForSeq2SeqLM.from_pretrained(str(d), attn_implementation="eager").eval()
         ids = torch.randint(3, 500, (2, 11))
         lab = torch.randint(3, 500, (2, 6))
         a = m(input_ids=ids, labels=lab).loss
@@ -72,7 +74,7 @@ def test_checkpoint_loads_in_transformers(tmp_path):
         m2 = from_pretrained(str(d)).eval()
         assert float(m2(input_ids=ids, labels=lab).loss) == pytest.approx(float(a), rel=1e-6)
         meta = json.load(open(d / "config.json"))
-        assert meta["model_type"] == m.config.model_type
+        assert meta["model_type"] == (m.config.t5_flavor if m.config.model_type == "t5" else m.config.model_type)
 
 
 def test_trainer_resume_is_exact(tmp_path):
