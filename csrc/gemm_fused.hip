@@ -845,9 +845,10 @@ int num_cus() {
 }
 
 // persist: one workgroup per CU when there are >= 2 tiles per CU and >= 2 k-tiles per tile, for the store-only
-// epilogues (none / ReLU / ReLU backward from the bit mask, whose only load is an LDS-DMA unit).  The others load (aux) or store twice (GELU pre-activation): their first load waits in order
-// behind the next tile's queued DMA units and the persistent form measured 7-17 % SLOWER there
-// (profiles/r1_gemm_experiments.md), so they keep one tile per workgroup.
+// epilogues (none / ReLU / GELU forward / ReLU backward from the bit mask, whose only load is an LDS-DMA unit).  The
+// GELU backward loads its aux tile in the epilogue: that first load waits in order behind the next tile's queued DMA
+// units and the persistent form measured 7-17 % SLOWER (profiles/r1_gemm_experiments.md), so it keeps one tile per
+// workgroup.
 template <int EPI, bool BKM>
 int launch_pp(const GemmFusedParams& p, bool persist, hipStream_t st) {
   const size_t lds = (size_t)2 * 2 * 64 * 256 * 2 + (EPI == EPI_DRELU_M ? 2 * 8192 : 0);
@@ -858,8 +859,15 @@ int launch_pp(const GemmFusedParams& p, bool persist, hipStream_t st) {
     const char* e = std::getenv("DLLM_GEGLU_BWD_PERSIST");
     return !(e && e[0] == '0');
   }();
+  // the GELU forward (two stores, no loads) is persistent too: +0.9 % on the bart-large b=256 step in round 4, after the
+  // DMA-descriptor and vmcnt changes since round 1 (profiles/r4_gelu_persist_ab.txt); DLLM_PP_PERSIST_GELU=0 turns it off
+  static const bool gelu_persist = [] {
+    const char* e = std::getenv("DLLM_PP_PERSIST_GELU");
+    return !(e && e[0] == '0');
+  }();
   const bool light = EPI == EPI_NONE || EPI == EPI_RELU || EPI == EPI_DRELU_M || EPI == EPI_GEGLU ||
-                     (EPI == EPI_DGEGLU && dgeglu_persist);
+                     (EPI == EPI_DGEGLU && dgeglu_persist) ||
+                     ((EPI == EPI_GELU || EPI == EPI_GELU_TANH) && gelu_persist);
   if (light && persist && cus >= 8 && T >= 2 * cus && p.K >= 128) {
     static bool attr = false;
     if (!attr) {

@@ -9,6 +9,8 @@
 // Dropout keep-decision for element row*d + col: common.h dropout4 / ops/rng.py keep_mask.
 #include "common.h"
 
+#include <cstdlib>
+
 using namespace dllm;
 
 DLLM_SEED_STEP_TU(norm)
@@ -319,9 +321,19 @@ extern "C" int dllm_norm_fwd(const void* x, const void* resid, const void* w, co
 }
 
 // Number of partial rows the caller must allocate for dw_part/db_part.
+// DLLM_NORM_BWD_G: cap on the workgroups (default 512 = 2 per CU; each wave then walks N / 2048 rows, two at a time)
+static int norm_bwd_cap() {
+  static const int cap = [] {
+    const char* e = getenv("DLLM_NORM_BWD_G");
+    const int v = e != nullptr ? atoi(e) : 0;
+    return v > 0 ? v : 512;
+  }();
+  return cap;
+}
+
 extern "C" int dllm_norm_bwd_grid(int N) {
-  int g = (N + 3) / 4;
-  return g < 512 ? g : 512;
+  const int g = (N + 3) / 4, cap = norm_bwd_cap();
+  return g < cap ? g : cap;
 }
 
 extern "C" int dllm_norm_bwd(const void* dout, const void* ds_extra, const void* s, const void* w, const float* mean,
