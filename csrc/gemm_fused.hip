@@ -859,8 +859,8 @@ int launch_pp(const GemmFusedParams& p, bool persist, hipStream_t st) {
     const char* e = std::getenv("DLLM_GEGLU_BWD_PERSIST");
     return !(e && e[0] == '0');
   }();
-  // the GELU forward (two stores, no loads) is persistent too: +0.9 % on the bart-large b=256 step in round 4, after the
-  // DMA-descriptor and vmcnt changes since round 1 (profiles/r4_gelu_persist_ab.txt); DLLM_PP_PERSIST_GELU=0 turns it off
+  // the GELU forward (two stores, no loads) is persistent too: +0.9 % on the bart-large b=256 step in round 4
+  // (profiles/r4_gelu_persist_ab.txt); DLLM_PP_PERSIST_GELU=0 turns it off
   static const bool gelu_persist = [] {
     const char* e = std::getenv("DLLM_PP_PERSIST_GELU");
     return !(e && e[0] == '0');
