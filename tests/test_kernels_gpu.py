@@ -466,6 +466,27 @@ def test_gemm_pp_persistent(K, kmajor):
         _close(du, ref, 2e-2, 2e-2, "pp persistent bwd")
 
 
+@pytest.mark.parametrize("act,p", [("gelu", 0.1), ("gelu", 0.0), ("gelu_new", 0.1)])
+def test_gemm_pp_persistent_gelu(act, p):
+    """GELU forward (bias + dropout, two stores: H and the scaled derivative) on the persistent ping-pong kernel: 528
+    tiles over the CUs, so every workgroup runs an epilogue inside the DMA stream of its next tile."""
+    from distributed_llms_example_amd.ops.rng import keep_mask
+    torch.manual_seed(6)
+    M, K, N = 8448, 1024, 4096
+    C = _ext.native()
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) * K ** -0.5).to(torch.bfloat16)
+    b = (0.5 * torch.randn(N, device=DEV)).to(torch.bfloat16)
+    aux = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    h = C.gemm_fused(x, w, False, _EPI_FWD[act], b, None, aux, p, 31, 9)
+    u = x.float() @ w.float().t() + b.float()
+    ref = activations._act_ref(u, act)
+    if p > 0:
+        ref = ref * keep_mask(31, p, ref.shape, ref.device).float() / (1.0 - p)
+    _close(h, ref, 2e-2, 2e-2, "pp persistent gelu fwd")
+    assert _rel(aux, _act_grad(u, act, 31, p)) < 1e-2, _rel(aux, _act_grad(u, act, 31, p))
+
+
 @pytest.mark.parametrize("variant", [8, 9])
 @pytest.mark.parametrize("M,d,F_", [(768, 512, 1024), (8448, 768, 4096)])
 def test_gemm_relu_bit_mask(variant, M, d, F_):
