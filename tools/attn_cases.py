@@ -1,5 +1,6 @@
 """Fwd + bwd of one attention configuration, repeated (for rocprofv3 --kernel-trace --stats per-kernel times):
-    python tools/attn_cases.py B H S bias kpm p scale [iters]"""
+    python tools/attn_cases.py B H S bias kpm p scale [iters]
+ATTN_SQ=n: n queries against the S keys (cross-attention; no bias)."""
 import os
 import sys
 
@@ -16,7 +17,9 @@ def main():
     iters = int(sys.argv[8]) if len(sys.argv) > 8 else 5
     D = 64
     torch.manual_seed(0)
-    q, k, v = (torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16, requires_grad=True) for _ in range(3))
+    Sq = int(os.environ.get("ATTN_SQ", S))
+    q = torch.randn(B, Sq, H, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    k, v = (torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16, requires_grad=True) for _ in range(2))
     tab = torch.randn(32, H, device="cuda", requires_grad=True) if bias else None
     mask = torch.ones(B, S, dtype=torch.bool, device="cuda") if kpm else None
     g = None
