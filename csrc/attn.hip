@@ -1233,6 +1233,192 @@ __global__ __launch_bounds__(256, NB == 3 ? 2 : 3) void attn_bwd_dkdv2_kernel(At
   }
 }
 
+// ================================================================================== backward: dK, dV, short queries
+// Cross-attention (T5 / BART decoder queries against the encoder keys: Sq <= 128, no bias, no causal mask).  The whole
+// query side of one (b, h) — Q, dO and the per-row terms, two 64-row stages — stays in LDS while one workgroup walks MB
+// consecutive key blocks of 128, loading block j + 1's K / V fragments, key flags and dropout keep words while block
+// j computes.  attn_bwd_dkdv2_kernel starts one workgroup per key block instead, each re-staging the query side and
+// waiting on its own K / V loads before two short stages: prologue-latency bound at this shape.  Per score: the
+// bias-free body of attn_bwd_dkdv2_kernel (P = exp2(fma(s, sl2, rt)), Pd = P keep, dS = P fma(dP, keep, -delta)).
+template <bool HAS_KPM, bool DROP, int MB>
+__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_sq_kernel(AttnParams P) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  // [2 stages of K2_STAGE: Q | dO | row terms (1 KB) | unused], keep words [2 parities][2 stages][1 KB], key mask [128]
+  const uint32_t* keepb = reinterpret_cast<const uint32_t*>(smem + 2 * K2_STAGE);
+  float* kmask = reinterpret_cast<float*>(smem + 2 * K2_STAGE + 4096);
+
+  const int tid = threadIdx.x, w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, r = lane & 31,
+            hh = lane >> 5;
+  const int ngrp = (P.n_tiles + MB - 1) / MB;
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int grp = logical % ngrp;
+  const int bh = logical / ngrp;
+  const int h = bh % P.H, b = bh / P.H;
+  const int kb_begin = grp * MB;
+  const int kb_end = min(kb_begin + MB, P.n_tiles);
+  const float sl2 = P.scale * LOG2E;
+  const int nqt = (P.Sq + K2_QT - 1) / K2_QT;  // 1 or 2: the launcher takes this kernel for Sq <= 128 only
+  const uint32_t st_lds = lds_addr(smem);
+
+  // query side, once: Q / dO pieces and the row terms of every stage (the DMA pieces of attn_bwd_dkdv2_kernel)
+  {
+    const uint16_t* qbase_p = P.q + b * P.q_sb + h * P.q_sh;
+    const uint16_t* dbase_p = P.dout + b * P.do_sb + h * P.do_sh;
+    const uint32_t qss2 = (uint32_t)P.q_ss * 2u, dss2 = (uint32_t)P.do_ss * 2u;
+    const float* rec_src = P.rowrec + (long)bh * (P.sq_pad >> 6) * 256 + w * 64 + lane;
+    for (int qt = 0; qt < nqt; ++qt) {
+      const uint32_t base = st_lds + (uint32_t)(qt * K2_STAGE);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int drow = 8 * (2 * w + i) + (lane >> 3);
+        const uint32_t dc16 = (uint32_t)(((lane & 7) ^ swz(drow)) * 16);
+        const uint32_t qq = (uint32_t)min(qt * K2_QT + drow, P.Sq - 1);
+        const uint32_t dst = base + (uint32_t)((2 * w + i) * 1024);
+        bld16(qbase_p, __umul24(qq, qss2) + dc16, __builtin_amdgcn_readfirstlane(dst));
+        bld16(dbase_p, __umul24(qq, dss2) + dc16, __builtin_amdgcn_readfirstlane(dst + TILE64 * 2));
+      }
+      glds4(rec_src + (long)qt * 256, __builtin_amdgcn_readfirstlane(base + 4 * TILE64 + w * 256));
+    }
+  }
+  // this lane's key inside a block and its dropout bit (the forward's lane half and register that held (q, key))
+  const int kl = w * 32 + r, kc = kl & 31;
+  const int mcol = (kl >> 6) * 2 + ((kc >> 2) & 1);
+  const int mbit = keep_bit((kl >> 5) & 1, (kc & 3) + 4 * (kc >> 3));
+  const uint32_t dsbits = __float_as_uint(DROP ? 1.f / (1.f - P.p_drop) : 1.f);
+
+  // per key block: wave w's keep-word column (64-key tile 2 kb + w / 2, lane half w & 1) for every stage
+  auto issue_keep = [&](int kb, int par) __attribute__((always_inline)) {
+    if constexpr (DROP) {
+      const int ktf = min(2 * kb + (w >> 1), P.n_ktiles - 1);
+      const uint32_t* src = P.dmask + (((long)bh * P.n_ktiles + ktf) * 2 + (w & 1)) * P.sq_pad + lane;
+      for (int qt = 0; qt < nqt; ++qt)
+        glds4(src + qt * K2_QT,
+              __builtin_amdgcn_readfirstlane(st_lds + 2 * K2_STAGE + (uint32_t)((par * 2 + qt) * 1024 + w * 256)));
+    }
+  };
+  auto load_kv = [&](int kb, bf16x8v(&kf)[4], bf16x8v(&vf)[4]) __attribute__((always_inline)) {
+    const int key = kb * BWD_BK + kl;
+    const bool kvalid = key < P.Sk;
+    const uint16_t* kp = P.k + b * P.k_sb + (long)key * P.k_ss + h * P.k_sh;
+    const uint16_t* vp = P.v + b * P.v_sb + (long)key * P.v_ss + h * P.v_sh;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      u16x8 a = {0, 0, 0, 0, 0, 0, 0, 0}, c = a;
+      if (kvalid) {
+        a = *reinterpret_cast<const u16x8*>(kp + 16 * s + 8 * hh);
+        c = *reinterpret_cast<const u16x8*>(vp + 16 * s + 8 * hh);
+      }
+      kf[s] = as_frag(a);
+      vf[s] = as_frag(c);
+    }
+  };
+  auto key_flag = [&](int kb) __attribute__((always_inline)) {
+    const int kk = kb * BWD_BK + tid;
+    bool ok = tid < BWD_BK && kk < P.Sk;
+    if (HAS_KPM && ok) ok = P.kpm[(long)b * P.Sk + kk] != 0;
+    return ok;
+  };
+
+  // Each block: key flags -> mask, prefetch of the next block, stages, then ONE drain (wait_vm<0>: the prefetch and the
+  // previous block's dK / dV stores, both issued a whole block earlier) and barrier before this block's stores — the
+  // barrier also retires every wave's reads of the key mask and keep slot the next block's writes reuse.  Waiting on
+  // everything (not a counted vmcnt) keeps it correct when a wave skips loads or stores for keys past Sk.
+  bf16x8v kf[4], vf[4], kfn[4], vfn[4];
+  issue_keep(kb_begin, 0);
+  load_kv(kb_begin, kf, vf);
+  bool key_ok = key_flag(kb_begin);
+  wait_vm<0>();
+  __syncthreads();
+  for (int kb = kb_begin; kb < kb_end; ++kb) {
+    const int par = (kb - kb_begin) & 1;
+    const int key = kb * BWD_BK + kl;
+    if (tid < BWD_BK) kmask[tid] = key_ok ? 0.f : -INFINITY;
+    const bool block_live = !HAS_KPM || __syncthreads_or(key_ok ? 1 : 0);
+    const bool block_masked = __syncthreads_or((tid < BWD_BK && !key_ok) ? 1 : 0);
+    const float km = block_masked ? kmask[kl] : 0.f;
+    const bool more = kb + 1 < kb_end;
+    if (more) {  // next block's inputs, in flight during this block's stages
+      issue_keep(kb + 1, par ^ 1);
+      load_kv(kb + 1, kfn, vfn);
+      key_ok = key_flag(kb + 1);
+    }
+    f32x16 dv0 = {}, dv1 = {}, dk0 = {}, dk1 = {};
+    if (block_live) {
+      for (int qt = 0; qt < nqt; ++qt) {
+        const unsigned char* stg = smem + qt * K2_STAGE;
+        const uint16_t* Qb = reinterpret_cast<const uint16_t*>(stg);
+        const uint16_t* dOb = Qb + TILE64;
+        const float* rec = reinterpret_cast<const float*>(stg + 4 * TILE64);
+        const uint32_t* mwd = keepb + (par * 2 + qt) * 256;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          f32x16 sacc = {}, dpacc = {};
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            sacc = mfma32(as_frag(ld_row(Qb, 32 * u + r, 2 * s + hh)), kf[s], sacc);
+            dpacc = mfma32(as_frag(ld_row(dOb, 32 * u + r, 2 * s + hh)), vf[s], dpacc);
+          }
+          // row terms of rows 32 u + crow(i, hh): the bias-free -lse at 128.., -delta at 192..
+          const float* rt_row = rec + 128 + 32 * u + 4 * hh;
+          const float* nd_row = rec + 192 + 32 * u + 4 * hh;
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const f32x4 rt4 = *reinterpret_cast<const f32x4*>(rt_row + 8 * g);
+            const f32x4 nd4 = *reinterpret_cast<const f32x4*>(nd_row + 8 * g);
+            u32x4 mw4 = {0u, 0u, 0u, 0u};
+            if (DROP) mw4 = *reinterpret_cast<const u32x4*>(mwd + mcol * 64 + 32 * u + 8 * g + 4 * hh);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int i = 4 * g + e;
+              const float pr = fast_exp2(fmaf(sacc[i], sl2, rt4[e] + km));  // rows >= Sq: rt = -inf -> 0
+              float keepf = 1.f;
+              if (DROP) keepf = __uint_as_float((uint32_t)__builtin_amdgcn_sbfe((int)mw4[e], mbit, 1) & dsbits);
+              sacc[i] = pr * keepf;
+              dpacc[i] = pr * fmaf(dpacc[i], keepf, nd4[e]);
+            }
+          }
+          const bf16x8v pf0 = pack8(sacc, 0), pf1 = pack8(sacc, 8), sf0 = pack8(dpacc, 0), sf1 = pack8(dpacc, 8);
+#pragma unroll
+          for (int sp = 0; sp < 2; ++sp) {
+            const int c0 = 32 * u + 16 * sp + 4 * hh;
+            const bf16x8v pfv = sp == 0 ? pf0 : pf1, sfv = sp == 0 ? sf0 : sf1;
+            dv0 = mfma32(ld_tr_operand(dOb, c0, 0, r), pfv, dv0);
+            dv1 = mfma32(ld_tr_operand(dOb, c0, 1, r), pfv, dv1);
+            dk0 = mfma32(ld_tr_operand(Qb, c0, 0, r), sfv, dk0);
+            dk1 = mfma32(ld_tr_operand(Qb, c0, 1, r), sfv, dk1);
+          }
+        }
+      }
+    }
+    wait_vm<0>();
+    __syncthreads();
+    if (key < P.Sk) {
+      uint16_t* dkp = P.dk + b * P.dk_sb + (long)key * P.dk_ss + h * P.dk_sh;
+      uint16_t* dvp = P.dv + b * P.dv_sb + (long)key * P.dv_ss + h * P.dv_sh;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const f32x16& ak = t == 0 ? dk0 : dk1;
+        const f32x16& av = t == 0 ? dv0 : dv1;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          u16x4 pk = {f2bf(ak[4 * g] * P.scale), f2bf(ak[4 * g + 1] * P.scale), f2bf(ak[4 * g + 2] * P.scale),
+                      f2bf(ak[4 * g + 3] * P.scale)};
+          u16x4 pv = {f2bf(av[4 * g]), f2bf(av[4 * g + 1]), f2bf(av[4 * g + 2]), f2bf(av[4 * g + 3])};
+          *reinterpret_cast<u16x4*>(dkp + 32 * t + 8 * g + 4 * hh) = pk;
+          *reinterpret_cast<u16x4*>(dvp + 32 * t + 8 * g + 4 * hh) = pv;
+        }
+      }
+    }
+    if (more) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        kf[s] = kfn[s];
+        vf[s] = vfn[s];
+      }
+    }
+  }
+}
+
 #define DISPATCH4(FN, hb, hk, ca, dr, ...)                                              \
   do {                                                                                  \
     if (hb) {                                                                           \
@@ -1312,6 +1498,14 @@ void launch_bwd_dkdv2_t(const AttnParams& p, int nblk, size_t lds, hipStream_t s
   hipLaunchKernelGGL((attn_bwd_dkdv2_kernel<HB, HK, CA, DR, 3>), dim3(nblk), dim3(256), lds, st, p);
 }
 
+template <bool HK, bool DR>
+void launch_bwd_dkdv_sq_t(const AttnParams& p, int mb, size_t lds, hipStream_t st) {
+  const long ng = (p.n_tiles + mb - 1) / mb;
+  const dim3 grid((unsigned)(ng * p.H * p.B));
+  if (mb >= 8) hipLaunchKernelGGL((attn_bwd_dkdv_sq_kernel<HK, DR, 8>), grid, dim3(256), lds, st, p);
+  else if (mb >= 4) hipLaunchKernelGGL((attn_bwd_dkdv_sq_kernel<HK, DR, 4>), grid, dim3(256), lds, st, p);
+  else hipLaunchKernelGGL((attn_bwd_dkdv_sq_kernel<HK, DR, 2>), grid, dim3(256), lds, st, p);
+}
 
 }  // namespace
 
@@ -1360,6 +1554,39 @@ extern "C" int dllm_attn_bwd(AttnParams* pp, hipStream_t st) {
   // 2) dK, dV (+ bias-LUT gradient): key blocks
   p.n_tiles = (p.Sk + BWD_BK - 1) / BWD_BK;
   nblk = (long)p.n_tiles * p.H * p.B;
+  // short-query cross-attention (Sq <= 128, no bias, not causal): one workgroup walks MB key blocks with the query
+  // side resident (attn_bwd_dkdv_sq_kernel) — the largest MB in {8, 4, 2} (capped by DLLM_ATTN_DKDV_SQ_MB, default 4;
+  // 0 / 1 = off) that still launches two workgroups per CU; small batches keep one workgroup per key block (dkdv2).
+  // In the t5-base b=512 step: 15.34 -> 13.50 ms/step (MB 8: 14.10), profiles/r4_dkdv_sq_ab.txt
+  static const int sq_cap = [] {
+    const char* e = getenv("DLLM_ATTN_DKDV_SQ_MB");
+    return e != nullptr ? atoi(e) : 4;
+  }();
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    return n > 0 ? n : 256;
+  }();
+  // DLLM_ATTN_DKDV_SQ_FORCE=1 (read per call; tests): the largest allowed MB whatever the launch size
+  const char* force_e = getenv("DLLM_ATTN_DKDV_SQ_FORCE");
+  const bool force = force_e != nullptr && force_e[0] == '1';
+  int mb = 0;
+  for (int m = 8; m >= 2; m /= 2)
+    if (m <= sq_cap && mb == 0 && (force || (long)((p.n_tiles + m - 1) / m) * p.H * p.B >= 2L * cus)) mb = m;
+  if (p.rowrec != nullptr && p.lut == nullptr && !p.causal && p.Sq <= 2 * K2_QT && mb > 1 && p.n_tiles >= 2) {
+    const size_t lds_sq = (size_t)2 * K2_STAGE + 4096 + BWD_BK * 4;
+    if ((long)((p.n_tiles + mb - 1) / mb) * p.H * p.B > 0x7fffffff) return -4;
+    if (p.kpm != nullptr) {
+      if (p.p_drop > 0.f) launch_bwd_dkdv_sq_t<true, true>(p, mb, lds_sq, st);
+      else launch_bwd_dkdv_sq_t<true, false>(p, mb, lds_sq, st);
+    } else {
+      if (p.p_drop > 0.f) launch_bwd_dkdv_sq_t<false, true>(p, mb, lds_sq, st);
+      else launch_bwd_dkdv_sq_t<false, false>(p, mb, lds_sq, st);
+    }
+    DLLM_CHECK_LAUNCH();
+    return 0;
+  }
   if (p.rowrec != nullptr) {  // v2: 64-row stages through an LDS-DMA ring (per-row terms from the dQ kernel)
     lds = (size_t)K2_NBUF * K2_STAGE + BWD_BK * 4;
     if (p.lut) lds += (size_t)(2 * (p.Sq + BWD_BK) + K2_QT) * 4;

@@ -173,11 +173,16 @@ ATTN_CASES = [
     (2, 12, 1024, 1024, True, True, False, 0.1, 1.0),  # t5-base encoder shape
     (2, 3, 300, 600, True, "heavy", False, 0.1, 1.0),  # short dialogue padded to max length: skipped key tiles
     (2, 2, 64, 600, False, "heavy", False, 0.1, 0.125),  # same for cross-attention
+    (3, 4, 128, 1000, False, True, False, 0.1, 1.0),   # T5 cross-attention: short-query dK/dV kernel, ragged last block
+    (2, 3, 100, 520, False, False, False, 0.1, 0.125),  # same without key padding
 ]
 
 
 @pytest.mark.parametrize("B,H,Sq,Sk,bias,kpm,causal,p,scale", ATTN_CASES)
-def test_attention(B, H, Sq, Sk, bias, kpm, causal, p, scale):
+def test_attention(B, H, Sq, Sk, bias, kpm, causal, p, scale, monkeypatch):
+    # short-query cross-attention: the dK/dV kernel that walks several key blocks per workgroup, which the launcher
+    # otherwise keeps for launches that still fill the chip (csrc/attn.hip attn_bwd_dkdv_sq_kernel)
+    monkeypatch.setenv("DLLM_ATTN_DKDV_SQ_FORCE", "1")
     torch.manual_seed(Sq * 7 + Sk)
     D = 64
     q = torch.randn(B, Sq, H, D, device=DEV).to(torch.bfloat16)
