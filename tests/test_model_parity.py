@@ -96,3 +96,29 @@ def test_mbart_decoder_inputs_start_with_the_language_id():
     ours = build_model("mbart-tiny")
     labels = torch.tensor([[5, 6, 7, 2, 250], [8, 9, 2, 251, -100]])
     torch.testing.assert_close(ours.shift_right(labels), shift_tokens_right(labels, ours.config.pad_token_id))
+
+
+def test_every_preset_round_trips_through_config_json():
+    """Every preset survives to_hf_dict -> from_hf_dict with the same architecture switches, and transformers' own
+    config class for its model type accepts the dict (AutoConfig.for_model)."""
+    import transformers
+    from distributed_llms_example_amd.models import PRESETS, Seq2SeqConfig
+    keys = ("model_type", "t5_flavor", "vocab_size", "d_model", "d_kv", "d_ff", "num_layers", "num_decoder_layers",
+            "num_heads", "feed_forward_proj", "tie_word_embeddings", "scale_decoder_outputs", "normalize_before",
+            "layernorm_embedding", "position_embedding", "shift_mode", "final_logits_bias", "scale_embedding",
+            "max_position_embeddings", "pad_token_id", "eos_token_id", "decoder_start_token_id", "per_layer_position_bias")
+    for name, cfg in PRESETS.items():
+        d = cfg.to_hf_dict()
+        back = Seq2SeqConfig.from_hf_dict(d)
+        for k in keys:
+            a, b = getattr(cfg, k), getattr(back, k)
+            if cfg.model_type == "t5" and k in ("normalize_before", "layernorm_embedding", "position_embedding",
+                                                 "shift_mode", "final_logits_bias", "scale_embedding",
+                                                 "max_position_embeddings"):
+                continue  # BART-family switches: not part of a T5 config.json
+            assert a == b, (name, k, a, b)
+        hf = dict(d)
+        hf.pop("architectures")
+        hf.pop("torch_dtype")
+        hcfg = transformers.AutoConfig.for_model(hf.pop("model_type"), **hf)
+        assert hcfg.vocab_size == cfg.vocab_size and hcfg.d_model == cfg.d_model, name
