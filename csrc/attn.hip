@@ -1556,7 +1556,8 @@ extern "C" int dllm_attn_bwd(AttnParams* pp, hipStream_t st) {
   nblk = (long)p.n_tiles * p.H * p.B;
   // short-query cross-attention (Sq <= 128, no bias, not causal): one workgroup walks MB key blocks with the query
   // side resident (attn_bwd_dkdv_sq_kernel) — the largest MB in {8, 4, 2} (capped by DLLM_ATTN_DKDV_SQ_MB, default 4;
-  // 0 / 1 = off) that still launches two workgroups per CU; small batches keep one workgroup per key block (dkdv2).
+  // 0 / 1 = off) that still launches 6 workgroups per CU (3 rounds at 2 per CU); smaller launches keep one workgroup
+  // per key block (dkdv2).  Batch sweep at the T5 cross shape: dkdv2 wins at batch 8 / 16, MB 2 at 32, MB 4 from 64.
   // In the t5-base b=512 step: 15.34 -> 13.50 ms/step (MB 8: 14.10), profiles/r4_dkdv_sq_ab.txt
   static const int sq_cap = [] {
     const char* e = getenv("DLLM_ATTN_DKDV_SQ_MB");
@@ -1573,7 +1574,7 @@ extern "C" int dllm_attn_bwd(AttnParams* pp, hipStream_t st) {
   const bool force = force_e != nullptr && force_e[0] == '1';
   int mb = 0;
   for (int m = 8; m >= 2; m /= 2)
-    if (m <= sq_cap && mb == 0 && (force || (long)((p.n_tiles + m - 1) / m) * p.H * p.B >= 2L * cus)) mb = m;
+    if (m <= sq_cap && mb == 0 && (force || (long)((p.n_tiles + m - 1) / m) * p.H * p.B >= 6L * cus)) mb = m;
   if (p.rowrec != nullptr && p.lut == nullptr && !p.causal && p.Sq <= 2 * K2_QT && mb > 1 && p.n_tiles >= 2) {
     const size_t lds_sq = (size_t)2 * K2_STAGE + 4096 + BWD_BK * 4;
     if ((long)((p.n_tiles + mb - 1) / mb) * p.H * p.B > 0x7fffffff) return -4;
