@@ -887,6 +887,9 @@ constexpr int K2_NBUF = 3;
 #ifndef DKDV_ABLATE
 #define DKDV_ABLATE 0
 #endif
+#ifndef DKDV_SQ_STAGE
+#define DKDV_SQ_STAGE 1
+#endif
 constexpr int K2_STAGE = 2 * 64 * D * 2 + 1024 + 1024;  // Q, dO [64][64] bf16 + rowrec [4][64] f32 + keep [4][64] u32
 
 // NB = stage ring depth: 3 (two stages in flight, 2 workgroups per CU) or 2 (one in flight, a 168-VGPR budget so 3
@@ -1243,7 +1246,8 @@ __global__ __launch_bounds__(256, NB == 3 ? 2 : 3) void attn_bwd_dkdv2_kernel(At
 template <bool HAS_KPM, bool DROP, int MB>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_sq_kernel(AttnParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  // [2 stages of K2_STAGE: Q | dO | row terms (1 KB) | unused], keep words [2 parities][2 stages][1 KB], key mask [128]
+  // [2 stages of K2_STAGE: Q | dO | row terms (1 KB) | unused], keep words [2 parities][2 stages][1 KB], key mask [128],
+  // (DKDV_SQ_STAGE) per-wave 8 KB store staging
   const uint32_t* keepb = reinterpret_cast<const uint32_t*>(smem + 2 * K2_STAGE);
   float* kmask = reinterpret_cast<float*>(smem + 2 * K2_STAGE + 4096);
 
@@ -1392,6 +1396,40 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_sq_kernel(AttnParams P) 
     }
     wait_vm<0>();
     __syncthreads();
+#if DKDV_SQ_STAGE
+    {
+      // the wave's 32 x 64 dK and dV tiles through its LDS scratch (16-B chunks XOR-swizzled by row), then whole
+      // 128-B key rows: 8 full-line stores per wave instead of 16 stores of 16 B into 32 lines each
+      unsigned char* scr = smem + 2 * K2_STAGE + 4096 + BWD_BK * 4 + w * 8192;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const f32x16& ak = t == 0 ? dk0 : dk1;
+        const f32x16& av = t == 0 ? dv0 : dv1;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          u16x4 pk = {f2bf(ak[4 * g] * P.scale), f2bf(ak[4 * g + 1] * P.scale), f2bf(ak[4 * g + 2] * P.scale),
+                      f2bf(ak[4 * g + 3] * P.scale)};
+          u16x4 pv = {f2bf(av[4 * g]), f2bf(av[4 * g + 1]), f2bf(av[4 * g + 2]), f2bf(av[4 * g + 3])};
+          const int off = r * 128 + (((4 * t + g) ^ (r & 7)) << 4) + 8 * hh;
+          *reinterpret_cast<u16x4*>(scr + off) = pk;
+          *reinterpret_cast<u16x4*>(scr + 4096 + off) = pv;
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // other lanes of this wave read what these wrote
+#pragma unroll
+      for (int st = 0; st < 4; ++st) {
+        const int row = 8 * st + (lane >> 3), ch = lane & 7;
+        const int off = row * 128 + ((ch ^ (row & 7)) << 4);
+        const u16x8 vk = *reinterpret_cast<const u16x8*>(scr + off);
+        const u16x8 vv = *reinterpret_cast<const u16x8*>(scr + 4096 + off);
+        const int ks = kb * BWD_BK + w * 32 + row;
+        if (ks < P.Sk) {
+          *reinterpret_cast<u16x8*>(P.dk + b * P.dk_sb + (long)ks * P.dk_ss + h * P.dk_sh + 8 * ch) = vk;
+          *reinterpret_cast<u16x8*>(P.dv + b * P.dv_sb + (long)ks * P.dv_ss + h * P.dv_sh + 8 * ch) = vv;
+        }
+      }
+    }
+#else
     if (key < P.Sk) {
       uint16_t* dkp = P.dk + b * P.dk_sb + (long)key * P.dk_ss + h * P.dk_sh;
       uint16_t* dvp = P.dv + b * P.dv_sb + (long)key * P.dv_ss + h * P.dv_sh;
@@ -1409,6 +1447,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_sq_kernel(AttnParams P) 
         }
       }
     }
+#endif
     if (more) {
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
@@ -1498,13 +1537,24 @@ void launch_bwd_dkdv2_t(const AttnParams& p, int nblk, size_t lds, hipStream_t s
   hipLaunchKernelGGL((attn_bwd_dkdv2_kernel<HB, HK, CA, DR, 3>), dim3(nblk), dim3(256), lds, st, p);
 }
 
+template <bool HK, bool DR, int MB>
+void launch_bwd_dkdv_sq_mb(const AttnParams& p, dim3 grid, size_t lds, hipStream_t st) {
+  static bool attr = false;  // the staged epilogue puts the dynamic LDS above the 64 KB default
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)attn_bwd_dkdv_sq_kernel<HK, DR, MB>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = true;
+  }
+  hipLaunchKernelGGL((attn_bwd_dkdv_sq_kernel<HK, DR, MB>), grid, dim3(256), lds, st, p);
+}
+
 template <bool HK, bool DR>
 void launch_bwd_dkdv_sq_t(const AttnParams& p, int mb, size_t lds, hipStream_t st) {
   const long ng = (p.n_tiles + mb - 1) / mb;
   const dim3 grid((unsigned)(ng * p.H * p.B));
-  if (mb >= 8) hipLaunchKernelGGL((attn_bwd_dkdv_sq_kernel<HK, DR, 8>), grid, dim3(256), lds, st, p);
-  else if (mb >= 4) hipLaunchKernelGGL((attn_bwd_dkdv_sq_kernel<HK, DR, 4>), grid, dim3(256), lds, st, p);
-  else hipLaunchKernelGGL((attn_bwd_dkdv_sq_kernel<HK, DR, 2>), grid, dim3(256), lds, st, p);
+  if (mb >= 8) launch_bwd_dkdv_sq_mb<HK, DR, 8>(p, grid, lds, st);
+  else if (mb >= 4) launch_bwd_dkdv_sq_mb<HK, DR, 4>(p, grid, lds, st);
+  else launch_bwd_dkdv_sq_mb<HK, DR, 2>(p, grid, lds, st);
 }
 
 }  // namespace
@@ -1576,7 +1626,7 @@ extern "C" int dllm_attn_bwd(AttnParams* pp, hipStream_t st) {
   for (int m = 8; m >= 2; m /= 2)
     if (m <= sq_cap && mb == 0 && (force || (long)((p.n_tiles + m - 1) / m) * p.H * p.B >= 6L * cus)) mb = m;
   if (p.rowrec != nullptr && p.lut == nullptr && !p.causal && p.Sq <= 2 * K2_QT && mb > 1 && p.n_tiles >= 2) {
-    const size_t lds_sq = (size_t)2 * K2_STAGE + 4096 + BWD_BK * 4;
+    const size_t lds_sq = (size_t)2 * K2_STAGE + 4096 + BWD_BK * 4 + (DKDV_SQ_STAGE ? 4 * 8192 : 0);
     if ((long)((p.n_tiles + mb - 1) / mb) * p.H * p.B > 0x7fffffff) return -4;
     if (p.kpm != nullptr) {
       if (p.p_drop > 0.f) launch_bwd_dkdv_sq_t<true, true>(p, mb, lds_sq, st);
