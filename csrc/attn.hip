@@ -42,6 +42,14 @@ using namespace dllm;
 
 DLLM_SEED_STEP_TU(attn)
 
+// output tiles staged through LDS and stored as whole rows (store_rows_staged): forward O, dQ (A/B: -D..._STAGE=0)
+#ifndef FWD_STAGE
+#define FWD_STAGE 1
+#endif
+#ifndef DQ_STAGE
+#define DQ_STAGE 1
+#endif
+
 namespace {
 
 // attention dropout (ops/rng.py attention_keep_mask): per query row rh = mix32(seed, row); per key pair kp = key >> 1:
@@ -86,6 +94,31 @@ DLLM_DEVICE uint32_t dropout_word(uint32_t rh, int kbase, int hh, uint32_t thr) 
     drop |= (m & ((1u << p) | (0x10000u << p)));
   }
   return ~drop;
+}
+
+// One wave's 32 rows x 64 bf16 output tile in the MFMA accumulator layout (lane (r, hh) holds columns 32 t + 8 g + 4 hh
+// .. + 3 of row r in a_t[4 g .. 4 g + 3]; times `mul`) through the wave's 4 KB LDS scratch (16-B chunks XOR-swizzled by
+// row), stored as whole 128-B rows: 4 full-line stores instead of 8 per-lane 8-B stores touching 32 lines each.  Row rr
+// goes to base + rr * row_stride (elements) for rr < nrows.  The caller has made the scratch free (barrier).
+DLLM_DEVICE void store_rows_staged(unsigned char* scr, const f32x16& a0, const f32x16& a1, float mul, int r, int hh,
+                                   int lane, uint16_t* base, long row_stride, int nrows) {
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const f32x16& a = t == 0 ? a0 : a1;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const u16x4 pk = {f2bf(a[4 * g] * mul), f2bf(a[4 * g + 1] * mul), f2bf(a[4 * g + 2] * mul),
+                        f2bf(a[4 * g + 3] * mul)};
+      *reinterpret_cast<u16x4*>(scr + r * 128 + (((4 * t + g) ^ (r & 7)) << 4) + 8 * hh) = pk;
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // other lanes of this wave read what these wrote
+#pragma unroll
+  for (int st = 0; st < 4; ++st) {
+    const int row = 8 * st + (lane >> 3), ch = lane & 7;
+    const u16x8 v = *reinterpret_cast<const u16x8*>(scr + row * 128 + ((ch ^ (row & 7)) << 4));
+    if (row < nrows) *reinterpret_cast<u16x8*>(base + (long)row * row_stride + 8 * ch) = v;
+  }
 }
 
 // ================================================================================== dropout bit planes
@@ -391,7 +424,14 @@ __global__ __launch_bounds__(256, FNB == 3 ? 2 : 3) void attn_fwd_kernel(AttnPar
 
   const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
   const float inv = l_tot > 0.f ? dscale / l_tot : 0.f;  // dropout's 1/(1-p) folded in
+#if FWD_STAGE
+  // every wave is done with the K/V ring (the last tile's DMAs were waited for): its first 16 KB stage the O tiles
+  __syncthreads();
+  store_rows_staged(smem + w * 4096, o0, o1, inv, r, hh, lane, P.o_out + b * P.o_sb + (long)qw0 * P.o_ss + h * P.o_sh,
+                    P.o_ss, P.Sq - qw0);
+#endif
   if (qvalid) {
+#if !FWD_STAGE
     uint16_t* op = P.o_out + b * P.o_sb + (long)qrow * P.o_ss + h * P.o_sh;
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
@@ -403,6 +443,7 @@ __global__ __launch_bounds__(256, FNB == 3 ? 2 : 3) void attn_fwd_kernel(AttnPar
         *reinterpret_cast<u16x4*>(op + 32 * t + 8 * g + 4 * hh) = pk;
       }
     }
+#endif
     if (hh == 0) {
       const float m_use = m_run == -INFINITY ? 0.f : m_run;
       P.lse[row_g] = l_tot > 0.f ? m_use + log2f(l_tot) : INFINITY;  // log2 units
@@ -608,6 +649,12 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dq_kernel(AttnParams P) {
     step(kt, std::integral_constant<int, 0>{});
     if (kt + 1 < ntiles) step(kt + 1, std::integral_constant<int, 1>{});
   }
+#if DQ_STAGE
+  // every wave is done with the K/V buffers (the last tile's DMAs were waited for): they stage the dQ tiles
+  __syncthreads();
+  store_rows_staged(smem + w * 4096, dq0, dq1, P.scale, r, hh, lane,
+                    P.dq + b * P.dq_sb + (long)qw0 * P.dq_ss + h * P.dq_sh, P.dq_ss, P.Sq - qw0);
+#else
   if (qvalid) {
     uint16_t* dqp = P.dq + b * P.dq_sb + (long)qrow * P.dq_ss + h * P.dq_sh;
 #pragma unroll
@@ -621,6 +668,7 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dq_kernel(AttnParams P) {
       }
     }
   }
+#endif
 }
 
 // ================================================================================== backward: dK, dV
@@ -889,6 +937,9 @@ constexpr int K2_NBUF = 3;
 #endif
 #ifndef DKDV_SQ_STAGE
 #define DKDV_SQ_STAGE 1
+#endif
+#ifndef DKDV2_STAGE
+#define DKDV2_STAGE 1
 #endif
 constexpr int K2_STAGE = 2 * 64 * D * 2 + 1024 + 1024;  // Q, dO [64][64] bf16 + rowrec [4][64] f32 + keep [4][64] u32
 
@@ -1203,6 +1254,42 @@ __global__ __launch_bounds__(256, NB == 3 ? 2 : 3) void attn_bwd_dkdv2_kernel(At
     }
   }
 
+#if DKDV2_STAGE
+  {
+    // every wave is done with the stage ring (its last stage drained the DMAs): reuse it to stage the wave's 32 x 64 dK
+    // and dV tiles (16-B chunks XOR-swizzled by row) and store whole 128-B key rows, 8 full-line stores per wave
+    // instead of 16 per-lane stores touching 32 lines each (as attn_bwd_dkdv_sq_kernel)
+    __syncthreads();
+    unsigned char* scr = smem + w * 8192;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const f32x16& ak = t == 0 ? dk0 : dk1;
+      const f32x16& av = t == 0 ? dv0 : dv1;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        u16x4 pk = {f2bf(ak[4 * g] * P.scale), f2bf(ak[4 * g + 1] * P.scale), f2bf(ak[4 * g + 2] * P.scale),
+                    f2bf(ak[4 * g + 3] * P.scale)};
+        u16x4 pv = {f2bf(av[4 * g]), f2bf(av[4 * g + 1]), f2bf(av[4 * g + 2]), f2bf(av[4 * g + 3])};
+        const int off = r * 128 + (((4 * t + g) ^ (r & 7)) << 4) + 8 * hh;
+        *reinterpret_cast<u16x4*>(scr + off) = pk;
+        *reinterpret_cast<u16x4*>(scr + 4096 + off) = pv;
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // other lanes of this wave read what these wrote
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+      const int row = 8 * st + (lane >> 3), ch = lane & 7;
+      const int off = row * 128 + ((ch ^ (row & 7)) << 4);
+      const u16x8 vk = *reinterpret_cast<const u16x8*>(scr + off);
+      const u16x8 vv = *reinterpret_cast<const u16x8*>(scr + 4096 + off);
+      const int ks = kw0 + row;
+      if (ks < P.Sk) {
+        *reinterpret_cast<u16x8*>(P.dk + b * P.dk_sb + (long)ks * P.dk_ss + h * P.dk_sh + 8 * ch) = vk;
+        *reinterpret_cast<u16x8*>(P.dv + b * P.dv_sb + (long)ks * P.dv_ss + h * P.dv_sh + 8 * ch) = vv;
+      }
+    }
+  }
+#else
   if (kvalid) {
     uint16_t* dkp = P.dk + b * P.dk_sb + (long)key * P.dk_ss + h * P.dk_sh;
     uint16_t* dvp = P.dv + b * P.dv_sb + (long)key * P.dv_ss + h * P.dv_sh;
@@ -1220,6 +1307,7 @@ __global__ __launch_bounds__(256, NB == 3 ? 2 : 3) void attn_bwd_dkdv2_kernel(At
       }
     }
   }
+#endif
   if (HAS_BIAS) {
     __syncthreads();
     float* grow = P.dlut + (long)h * L;
