@@ -198,6 +198,43 @@ DLLM_DEVICE f32x4 epilogue4(const GemmFusedParams& P, uint32_t seed, int m, int 
   return v;
 }
 
+// Forward activation of epilogue4 without its stores (the ping-pong kernel's LDS-staged epilogue stores whole rows):
+// returns act(v) with dropout, and in dg the GELU forwards' second output
+template <int EPI>
+DLLM_DEVICE f32x4 act4(const GemmFusedParams& P, uint32_t seed, int m, int n, f32x4 v, f32x4& dg) {
+  const bool drop = P.p > 0.f;
+  const uint32_t e = (uint32_t)m * (uint32_t)P.N + (uint32_t)n;
+  if (EPI == EPI_RELU) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = fmaxf(v[k], 0.f);
+    if (drop) dropout4(v, seed, P.thr, e, P.scale);
+  } else if (EPI == EPI_GELU || EPI == EPI_GELU_TANH) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float g, d;
+      if (EPI == EPI_GELU) gelu_pair(v[k], g, d);
+      else gelu_tanh_pair(v[k], g, d);
+      v[k] = g;
+      dg[k] = d;
+    }
+    if (drop) {
+      bool k0, k1, k2, k3;
+      keep_two(seed, P.thr, e, k0, k1);
+      keep_two(seed, P.thr, e + 2u, k2, k3);
+      const float s0 = k0 ? P.scale : 0.f, s1 = k1 ? P.scale : 0.f, s2 = k2 ? P.scale : 0.f, s3 = k3 ? P.scale : 0.f;
+      v = v * f32x4{s0, s1, s2, s3};
+      dg = dg * f32x4{s0, s1, s2, s3};
+    }
+  }
+  return v;
+}
+
+// PP_STAGE: the ping-pong kernel's GELU forward epilogues (two outputs) go through a 4 KB per-wave LDS scratch after
+// the operand ring and leave as whole 128-B rows (A/B: -DPP_STAGE=0)
+#ifndef PP_STAGE
+#define PP_STAGE 1
+#endif
+
 // MF = 32: v_mfma_f32_32x32x16_bf16, 4x2 accumulator tiles of 32x32 per wave;
 // MF = 16: v_mfma_f32_16x16x32_bf16, 8x4 tiles of 16x16 (same cycles per FLOP; on random data the chip holds a
 // higher clock on this shape, MI355X_MICROARCH.md "DVFS give-back" item 7) — both built, the faster picked by
@@ -424,7 +461,12 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(GemmFusedParams P) {
   uint16_t* lds = reinterpret_cast<uint16_t*>(smem);  // [2][A image | B image], [256][64] each
   using RI = RowImg<64>;
   constexpr int TILE = 64 * 256;
-  constexpr int NST = (EPI == EPI_GELU || EPI == EPI_GELU_TANH || EPI == EPI_DGEGLU) ? 64 : EPI == EPI_GEGLU ? 48 : 32;
+  // staged store-only epilogues: 2 whole-row stores per 16-row block and output (32 instead of 64).  GELU forwards only
+  // (two outputs): bart-large +0.45 %; the ReLU forward measured 1 % slower staged (profiles/r4_gemm_pp_stage_ab.txt)
+  constexpr bool STAGED = PP_STAGE && (EPI == EPI_GELU || EPI == EPI_GELU_TANH);
+  constexpr int NST = STAGED ? ((EPI == EPI_GELU || EPI == EPI_GELU_TANH) ? 32 : 16)
+                             : (EPI == EPI_GELU || EPI == EPI_GELU_TANH || EPI == EPI_DGEGLU) ? 64
+                             : EPI == EPI_GEGLU ? 48 : 32;
   // gated forward (EPI_GEGLU, NT only): B = the stacked [wi_0; wi_1] weight [2F][K]; tile column block nb covers hidden
   // units f0 = 128 nb .. f0 + 127: image rows 0-127 are wi_0 rows f0.., rows 128-255 wi_1 rows f0.. (two DMA sources),
   // and each wave reads its fragments so that accumulator columns j = 0, 2 are gate and j = 1, 3 the matching up
@@ -757,6 +799,42 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(GemmFusedParams P) {
           for (int r = 0; r < 4; ++r) v[r] = (mw[i >> 1] >> ((i & 1) * 16 + 4 * j + r)) & 1u ? v[r] * P.scale : 0.f;
           store4(P.C + (long)(mrow + 16 * i) * P.ldc + ncol + 16 * j, v);
         }
+    } else if constexpr (STAGED) {
+      // per 16-row block: the wave's 16 x 64 outputs (and the GELU derivative) into its 4 KB scratch after the operand
+      // ring (16-B chunks XOR-swizzled by row), then 2 whole-row stores per output: 8 full 128-B lines each
+      unsigned char* scr = smem + 4 * TILE * 2 + w * 4096;
+      constexpr bool TWO = EPI == EPI_GELU || EPI == EPI_GELU_TANH;
+      u32x4 bits = {0u, 0u, 0u, 0u};
+      const int rho = ln & 15, q = ln >> 4;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          f32x4 dg = {0.f, 0.f, 0.f, 0.f};
+          const f32x4 v = act4<EPI>(P, seed, mrow + 16 * i, ncol + 16 * j, acc[i][j] + bv[j], dg);
+          if (EPI == EPI_RELU) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) bits[i >> 1] |= (v[r] != 0.f ? 1u : 0u) << ((i & 1) * 16 + 4 * j + r);
+          }
+          const int off = rho * 128 + (((2 * j + (q >> 1)) ^ (rho & 7)) << 4) + 8 * (q & 1);
+          *reinterpret_cast<u16x4*>(scr + off) = u16x4{f2bf(v.x), f2bf(v.y), f2bf(v.z), f2bf(v.w)};
+          if (TWO) *reinterpret_cast<u16x4*>(scr + 2048 + off) = u16x4{f2bf(dg.x), f2bf(dg.y), f2bf(dg.z), f2bf(dg.w)};
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // other lanes of this wave read what these wrote
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+          const int row = 8 * st + (ln >> 3), ch = ln & 7;
+          const int off = row * 128 + ((ch ^ (row & 7)) << 4);
+          const long m = tm0 + wm * 128 + 16 * i + row;
+          const int n = tn0 + wn * 64 + 8 * ch;
+          *reinterpret_cast<u16x8*>(P.C + m * P.ldc + n) = *reinterpret_cast<const u16x8*>(scr + off);
+          if (TWO) *reinterpret_cast<u16x8*>(P.aux_out + m * P.ldaux + n) = *reinterpret_cast<const u16x8*>(scr + 2048 + off);
+        }
+        // the next block's scratch writes must not overtake these reads (in-order LDS per wave; the barrier keeps
+        // the compiler from moving them)
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (EPI == EPI_RELU && P.mask) *reinterpret_cast<u32x4*>(P.mask + mask_word(tm0, tn0) + tid * 4) = bits;
     } else {
       u32x4 bits = {0u, 0u, 0u, 0u};
       // GELU backward: column sums of the stored dU over the wave's 128 rows — the fc1 bias gradient — from registers
@@ -851,7 +929,8 @@ int num_cus() {
 // workgroup.
 template <int EPI, bool BKM>
 int launch_pp(const GemmFusedParams& p, bool persist, hipStream_t st) {
-  const size_t lds = (size_t)2 * 2 * 64 * 256 * 2 + (EPI == EPI_DRELU_M ? 2 * 8192 : 0);
+  constexpr bool staged = PP_STAGE && (EPI == EPI_GELU || EPI == EPI_GELU_TANH);
+  const size_t lds = (size_t)2 * 2 * 64 * 256 * 2 + (EPI == EPI_DRELU_M ? 2 * 8192 : 0) + (staged ? 8 * 4096 : 0);
   const int T = p.tm * p.tn, cus = num_cus() / 8 * 8;
   // the gated forward is store-only too; its backward (two aux loads per accumulator block) measured 6-10 % faster
   // persistent as well (profiles/r2_geglu_bench.jsonl); DLLM_GEGLU_BWD_PERSIST=0 keeps one tile per workgroup
