@@ -234,6 +234,9 @@ DLLM_DEVICE f32x4 act4(const GemmFusedParams& P, uint32_t seed, int m, int n, f3
 #ifndef PP_STAGE
 #define PP_STAGE 1
 #endif
+#ifndef PP_STAGE_BWD
+#define PP_STAGE_BWD 1
+#endif
 
 // MF = 32: v_mfma_f32_32x32x16_bf16, 4x2 accumulator tiles of 32x32 per wave;
 // MF = 16: v_mfma_f32_16x16x32_bf16, 8x4 tiles of 16x16 (same cycles per FLOP; on random data the chip holds a
@@ -464,6 +467,8 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(GemmFusedParams P) {
   // staged store-only epilogues: 2 whole-row stores per 16-row block and output (32 instead of 64).  GELU forwards only
   // (two outputs): bart-large +0.45 %; the ReLU forward measured 1 % slower staged (profiles/r4_gemm_pp_stage_ab.txt)
   constexpr bool STAGED = PP_STAGE && (EPI == EPI_GELU || EPI == EPI_GELU_TANH);
+  // GELU backward (one tile per workgroup): derivative loads and dU stores as whole rows through the same scratch
+  constexpr bool STAGED_BWD = PP_STAGE_BWD && (EPI == EPI_DGELU || EPI == EPI_DGELU_TANH);
   constexpr int NST = STAGED ? ((EPI == EPI_GELU || EPI == EPI_GELU_TANH) ? 32 : 16)
                              : (EPI == EPI_GELU || EPI == EPI_GELU_TANH || EPI == EPI_DGEGLU) ? 64
                              : EPI == EPI_GEGLU ? 48 : 32;
@@ -841,6 +846,53 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(GemmFusedParams P) {
       // (otherwise a separate pass re-reads all of dU, [tokens, d_ff] bf16)
       constexpr bool CS = EPI == EPI_DGELU || EPI == EPI_DGELU_TANH;
       f32x4 cs[4] = {};
+      if constexpr (STAGED_BWD) {
+        // GELU backward: per 16-row block the saved derivative rows come in as whole 128-B rows (prefetched one block
+        // ahead) through the wave's 4 KB scratch, each lane multiplies its accumulator layout in place there, and dU
+        // leaves as whole rows: 2 + 2 full-line accesses per block instead of 4 + 4 partial ones
+        unsigned char* scr = smem + 4 * TILE * 2 + w * 4096;
+        const int rho = ln & 15, q = ln >> 4, lrow = ln >> 3, lch = ln & 7;
+        auto ldaux = [&](int i, u16x8(&a)[2]) __attribute__((always_inline)) {
+#pragma unroll
+          for (int st = 0; st < 2; ++st) {
+            const long m = tm0 + wm * 128 + 16 * i + 8 * st + lrow;
+            a[st] = *reinterpret_cast<const u16x8*>(P.aux + m * P.ldaux + tn0 + wn * 64 + 8 * lch);
+          }
+        };
+        u16x8 cur[2], nxt[2];
+        ldaux(0, cur);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          if (i + 1 < 8) ldaux(i + 1, nxt);
+#pragma unroll
+          for (int st = 0; st < 2; ++st) {
+            const int row = 8 * st + lrow;
+            *reinterpret_cast<u16x8*>(scr + row * 128 + ((lch ^ (row & 7)) << 4)) = cur[st];
+          }
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // other lanes of this wave read what these wrote
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int off = rho * 128 + (((2 * j + (q >> 1)) ^ (rho & 7)) << 4) + 8 * (q & 1);
+            const u16x4 a4 = *reinterpret_cast<const u16x4*>(scr + off);
+            const f32x4 v = (acc[i][j] + bv[j]) * f32x4{bf2f(a4.x), bf2f(a4.y), bf2f(a4.z), bf2f(a4.w)};
+            cs[j] += v;
+            *reinterpret_cast<u16x4*>(scr + off) = u16x4{f2bf(v.x), f2bf(v.y), f2bf(v.z), f2bf(v.w)};
+          }
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+          for (int st = 0; st < 2; ++st) {
+            const int row = 8 * st + lrow;
+            const long m = tm0 + wm * 128 + 16 * i + row;
+            *reinterpret_cast<u16x8*>(P.C + m * P.ldc + tn0 + wn * 64 + 8 * lch) =
+                *reinterpret_cast<const u16x8*>(scr + row * 128 + ((lch ^ (row & 7)) << 4));
+          }
+          __builtin_amdgcn_sched_barrier(0);  // the next block's scratch writes stay after these reads
+          if (i + 1 < 8) {
+            cur[0] = nxt[0];
+            cur[1] = nxt[1];
+          }
+        }
+      } else {
 #pragma unroll
       for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -852,6 +904,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(GemmFusedParams P) {
           }
           if constexpr (CS) cs[j] += v;
         }
+      }
       if (EPI == EPI_RELU && P.mask) *reinterpret_cast<u32x4*>(P.mask + mask_word(tm0, tn0) + tid * 4) = bits;
       if constexpr (CS) {
         if (P.colsum) {  // the 16 lanes of a lane group hold the same 16 columns on 16 different rows
@@ -929,7 +982,8 @@ int num_cus() {
 // workgroup.
 template <int EPI, bool BKM>
 int launch_pp(const GemmFusedParams& p, bool persist, hipStream_t st) {
-  constexpr bool staged = PP_STAGE && (EPI == EPI_GELU || EPI == EPI_GELU_TANH);
+  constexpr bool staged = (PP_STAGE && (EPI == EPI_GELU || EPI == EPI_GELU_TANH)) ||
+                          (PP_STAGE_BWD && (EPI == EPI_DGELU || EPI == EPI_DGELU_TANH));
   const size_t lds = (size_t)2 * 2 * 64 * 256 * 2 + (EPI == EPI_DRELU_M ? 2 * 8192 : 0) + (staged ? 8 * 4096 : 0);
   const int T = p.tm * p.tn, cus = num_cus() / 8 * 8;
   // the gated forward is store-only too; its backward (two aux loads per accumulator block) measured 6-10 % faster
