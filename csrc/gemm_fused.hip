@@ -469,9 +469,13 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(GemmFusedParams P) {
   constexpr bool STAGED = PP_STAGE && (EPI == EPI_GELU || EPI == EPI_GELU_TANH);
   // GELU backward (one tile per workgroup): derivative loads and dU stores as whole rows through the same scratch
   constexpr bool STAGED_BWD = PP_STAGE_BWD && (EPI == EPI_DGELU || EPI == EPI_DGELU_TANH);
+  // gated backward (persistent): G1 / G2 rows in and both output halves out as whole rows through the scratch
+  constexpr bool STAGED_DGEGLU = PP_STAGE_BWD && EPI == EPI_DGEGLU;
+  // (the staged gated backward's loads are consumed before its last stores: 32 stores stay queued)
   constexpr int NST = STAGED ? ((EPI == EPI_GELU || EPI == EPI_GELU_TANH) ? 32 : 16)
-                             : (EPI == EPI_GELU || EPI == EPI_GELU_TANH || EPI == EPI_DGEGLU) ? 64
-                             : EPI == EPI_GEGLU ? 48 : 32;
+                      : STAGED_DGEGLU ? 32
+                      : (EPI == EPI_GELU || EPI == EPI_GELU_TANH || EPI == EPI_DGEGLU) ? 64
+                      : EPI == EPI_GEGLU ? 48 : 32;
   // gated forward (EPI_GEGLU, NT only): B = the stacked [wi_0; wi_1] weight [2F][K]; tile column block nb covers hidden
   // units f0 = 128 nb .. f0 + 127: image rows 0-127 are wi_0 rows f0.., rows 128-255 wi_1 rows f0.. (two DMA sources),
   // and each wave reads its fragments so that accumulator columns j = 0, 2 are gate and j = 1, 3 the matching up
@@ -846,7 +850,61 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(GemmFusedParams P) {
       // (otherwise a separate pass re-reads all of dU, [tokens, d_ff] bf16)
       constexpr bool CS = EPI == EPI_DGELU || EPI == EPI_DGELU_TANH;
       f32x4 cs[4] = {};
-      if constexpr (STAGED_BWD) {
+      if constexpr (STAGED_DGEGLU) {
+        // per 16-row block: G1 / G2 rows in as whole 128-B rows (one block ahead) to the wave's scratch (G1 at 0, G2 at
+        // 2 KB), dH * G1 / dH * G2 formed in place in the accumulator layout, both [M][2F] halves out as whole rows
+        unsigned char* scr = smem + 4 * TILE * 2 + w * 4096;
+        const int rho = ln & 15, q = ln >> 4, lrow = ln >> 3, lch = ln & 7;
+        auto ldg = [&](int i, u16x8(&a)[4]) __attribute__((always_inline)) {
+#pragma unroll
+          for (int st = 0; st < 2; ++st) {
+            const long m = tm0 + wm * 128 + 16 * i + 8 * st + lrow;
+            const long o = m * P.ldaux + tn0 + wn * 64 + 8 * lch;
+            a[st] = *reinterpret_cast<const u16x8*>(P.aux + o);
+            a[2 + st] = *reinterpret_cast<const u16x8*>(P.aux2 + o);
+          }
+        };
+        u16x8 cur[4], nxt[4];
+        ldg(0, cur);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          if (i + 1 < 8) ldg(i + 1, nxt);
+#pragma unroll
+          for (int st = 0; st < 2; ++st) {
+            const int row = 8 * st + lrow;
+            const int off = row * 128 + ((lch ^ (row & 7)) << 4);
+            *reinterpret_cast<u16x8*>(scr + off) = cur[st];
+            *reinterpret_cast<u16x8*>(scr + 2048 + off) = cur[2 + st];
+          }
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // other lanes of this wave read what these wrote
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int off = rho * 128 + (((2 * j + (q >> 1)) ^ (rho & 7)) << 4) + 8 * (q & 1);
+            const u16x4 a1 = *reinterpret_cast<const u16x4*>(scr + off);
+            const u16x4 a2 = *reinterpret_cast<const u16x4*>(scr + 2048 + off);
+            const f32x4 v = acc[i][j] + bv[j];
+            const f32x4 v1 = v * f32x4{bf2f(a1.x), bf2f(a1.y), bf2f(a1.z), bf2f(a1.w)};
+            const f32x4 v2 = v * f32x4{bf2f(a2.x), bf2f(a2.y), bf2f(a2.z), bf2f(a2.w)};
+            *reinterpret_cast<u16x4*>(scr + off) = u16x4{f2bf(v1.x), f2bf(v1.y), f2bf(v1.z), f2bf(v1.w)};
+            *reinterpret_cast<u16x4*>(scr + 2048 + off) = u16x4{f2bf(v2.x), f2bf(v2.y), f2bf(v2.z), f2bf(v2.w)};
+          }
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+          for (int st = 0; st < 2; ++st) {
+            const int row = 8 * st + lrow;
+            const int off = row * 128 + ((lch ^ (row & 7)) << 4);
+            const long m = tm0 + wm * 128 + 16 * i + row;
+            uint16_t* cp = P.C + m * P.ldc + tn0 + wn * 64 + 8 * lch;
+            *reinterpret_cast<u16x8*>(cp) = *reinterpret_cast<const u16x8*>(scr + off);
+            *reinterpret_cast<u16x8*>(cp + P.N) = *reinterpret_cast<const u16x8*>(scr + 2048 + off);
+          }
+          __builtin_amdgcn_sched_barrier(0);  // the next block's scratch writes stay after these reads
+          if (i + 1 < 8) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) cur[e] = nxt[e];
+          }
+        }
+      } else if constexpr (STAGED_BWD) {
         // GELU backward: per 16-row block the saved derivative rows come in as whole 128-B rows (prefetched one block
         // ahead) through the wave's 4 KB scratch, each lane multiplies its accumulator layout in place there, and dU
         // leaves as whole rows: 2 + 2 full-line accesses per block instead of 4 + 4 partial ones
@@ -983,7 +1041,7 @@ int num_cus() {
 template <int EPI, bool BKM>
 int launch_pp(const GemmFusedParams& p, bool persist, hipStream_t st) {
   constexpr bool staged = (PP_STAGE && (EPI == EPI_GELU || EPI == EPI_GELU_TANH)) ||
-                          (PP_STAGE_BWD && (EPI == EPI_DGELU || EPI == EPI_DGELU_TANH));
+                          (PP_STAGE_BWD && (EPI == EPI_DGELU || EPI == EPI_DGELU_TANH || EPI == EPI_DGEGLU));
   const size_t lds = (size_t)2 * 2 * 64 * 256 * 2 + (EPI == EPI_DRELU_M ? 2 * 8192 : 0) + (staged ? 8 * 4096 : 0);
   const int T = p.tm * p.tn, cus = num_cus() / 8 * 8;
   // the gated forward is store-only too; its backward (two aux loads per accumulator block) measured 6-10 % faster
