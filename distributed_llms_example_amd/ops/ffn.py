@@ -212,11 +212,13 @@ class _FusedGatedFFNFn(torch.autograd.Function):
 gated_calls = 0  # number of gated FFN forwards that took the fused path
 # Where the fused gated GEMMs win (tools/geglu_bench.py, profiles/r2_geglu_bench.jsonl, flan-t5 A/Bs in
 # profiles/r2_geglu_ab.txt): they need >= 2 output tiles per CU to run persistent (epilogue stores / loads under the
-# next tile's MFMAs), so tokens x d_ff >= _GATED_MIN_MF; and with a long reduction (d_model >= 1024) hipBLASLt's
-# GEMM outruns the ping-pong kernel by more than the two activation passes cost (flan-t5-large -3 %, flan-t5-xl
-# encoder -10 % in the model), so d_model <= _GATED_MAX_D.  flan-t5-base at b=64: +0.6 % samples/s.
+# next tile's MFMAs), so tokens x d_ff >= _GATED_MIN_MF; and with the longest reduction (d_model 2048) hipBLASLt's
+# GEMM outruns the ping-pong kernel by as much as the two activation passes cost, so d_model <= _GATED_MAX_D.  Round 2
+# had flan-t5-large 3 % slower fused; since the gated backward's epilogue loads and stores whole rows through LDS
+# (round 4, profiles/r4_gemm_pp_stage_ab.txt) flan-t5-large b=32 is 2.1 % faster fused and flan-t5-xl equal, so the
+# bound moved from 768 to 1024.  flan-t5-base at b=128: 875 samples/s.
 _GATED_MIN_MF = int(os.environ.get("DLLM_GATED_MIN_MF", str(2 * 256 * 256 * 256)))
-_GATED_MAX_D = int(os.environ.get("DLLM_GATED_MAX_D", "768"))
+_GATED_MAX_D = int(os.environ.get("DLLM_GATED_MAX_D", "1024"))
 
 
 def gated_ffn(x: torch.Tensor, lin_in, lin_out, act: str, p: float = 0.0, seed: int = 0) -> torch.Tensor:
