@@ -454,7 +454,8 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
         se += __shfl_xor(se, 32, 64);
         sx += __shfl_xor(sx, 16, 64);
         sx += __shfl_xor(sx, 32, 64);
-        if (qd == 0 && row < P.M)
+        // a 128-column half lying wholly past N has no partial slot (pcol == pstride would be the next row's slot 0)
+        if (qd == 0 && row < P.M && pcol < P.pstride)
           *reinterpret_cast<f32x4*>(P.part + ((long)row * P.pstride + pcol) * 4) = f32x4{mx, se, sx, 0.f};
         __builtin_amdgcn_sched_barrier(0);
       }

@@ -195,6 +195,7 @@ class SinusoidalPositions(nn.Module):
     feature j of position t is sin / cos of t / 10000^(2 floor(j/2) / d), the sines in the first half of the features
     and the cosines in the second.  A persistent buffer named ``weight`` (the checkpoints carry it); never trained."""
     offset = 0
+    derived_table = True  # models/hf_io.py: may be absent from a checkpoint (transformers' Marian does not save it)
 
     def __init__(self, n, d):
         super().__init__()

@@ -93,7 +93,11 @@ def from_hf_state_dict(model, sd: dict[str, torch.Tensor], strict: bool = True):
                 new[name] = sd[name]
             elif name.endswith("shared.weight") and "model.shared.weight" not in sd and "lm_head.weight" in sd:
                 new[name] = sd["lm_head.weight"]
-    missing = [k for k in own if k not in new]
+    # fixed sinusoidal position tables are a function of (max_position_embeddings, d_model): transformers' Marian drops
+    # them on save (_keys_to_ignore_on_save) and our module already holds the exact table, so their absence is not an
+    # error (Pegasus checkpoints do carry them and they are loaded like any other key)
+    derived = {n + ".weight" for n, m in model.named_modules() if getattr(m, "derived_table", False)}
+    missing = [k for k in own if k not in new and k not in derived]
     if strict and missing:
         raise KeyError(f"missing keys in checkpoint: {missing[:8]}{'...' if len(missing) > 8 else ''}")
     with torch.no_grad():

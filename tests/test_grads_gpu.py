@@ -259,6 +259,34 @@ def test_lm_head_chunked_ce_matches_fp32(bias, smooth, V, fused, monkeypatch):
     assert _rel(flat.grad_view(0), wr.grad) < 1e-2, _rel(flat.grad_view(0), wr.grad)
 
 
+@pytest.mark.parametrize("V", [32128, 50265, 4000, 128112])
+def test_lm_head_fused_lse_exact(V):
+    """The GEMM-epilogue CE forward's per-row lse / loss vs fp32 logsumexp on the same bf16 operands, at fp32-rounding
+    tolerance.  ceil(V / 128) odd (T5 32128, BART 50265, M2M100 128112) is the case where a tile's second 128-column
+    half lies wholly past V: its partial must not be written (it would land in the next row's first slot and drop
+    vocabulary columns 0..127 from that row).  Columns 0..127 carry most of the mass here, so a dropped slot moves lse
+    by O(1); near-uniform logits would hide it (4e-4 relative)."""
+    C = _ext.native()
+    torch.manual_seed(1)
+    N, d = 777, 256
+    h = (torch.randn(N, d, device=DEV) * 0.5).to(torch.bfloat16)
+    w = (torch.randn(V, d, device=DEV) * 0.1).to(torch.bfloat16)
+    bias = torch.zeros(V, device=DEV)
+    bias[:128] = 4.0
+    labels = torch.randint(0, V, (N,), device=DEV)
+    labels[::5] = -100
+    labels[1::5] = 3
+    ref = torch.logsumexp(h.float() @ w.float().t() + bias, dim=1)
+    for _ in range(3):
+        loss_rows, lse = C.lmhead_ce_fwd(h, w, labels, bias, 0.0, -100)
+        torch.cuda.synchronize()
+        assert (lse - ref).abs().max().item() < 2e-4 * ref.abs().max().item(), (lse - ref).abs().max().item()
+        lg = h.float() @ w.float().t() + bias
+        valid = labels != -100
+        ref_loss = torch.nn.functional.cross_entropy(lg[valid], labels[valid], reduction="none")
+        assert (loss_rows[valid] - ref_loss).abs().max().item() < 1e-3, (loss_rows[valid] - ref_loss).abs().max().item()
+
+
 def test_t5_chunked_lm_head_matches_full(monkeypatch):
     """The T5 model's loss / flat gradient with the chunked LM head == with materialised logits."""
     cfg = _small_cfg()

@@ -91,6 +91,21 @@ def test_sinusoidal_positions_match_hf(name):
         torch.testing.assert_close(a, b.to(a.dtype), atol=1e-6, rtol=0)
 
 
+@pytest.mark.parametrize("name", ["pegasus-tiny", "marian-tiny"])
+def test_from_pretrained_reads_transformers_save_pretrained(name, tmp_path):
+    """A directory written by transformers' own save_pretrained loads through from_pretrained (Marian drops the fixed
+    position tables on save; Pegasus keeps them) and gives the same parameters and logits."""
+    from distributed_llms_example_amd.models import from_pretrained
+    ours = build_model(name)
+    hf = hf_model_for(ours)
+    hf.save_pretrained(str(tmp_path), safe_serialization=True)
+    back = from_pretrained(str(tmp_path))
+    a, b = ours.state_dict(), back.state_dict()
+    assert a.keys() == b.keys()
+    for k in a:
+        torch.testing.assert_close(a[k], b[k], atol=0, rtol=0, msg=k)
+
+
 def test_mbart_decoder_inputs_start_with_the_language_id():
     from transformers.models.mbart.modeling_mbart import shift_tokens_right
     ours = build_model("mbart-tiny")
