@@ -1,7 +1,7 @@
 #!/bin/bash
 # TunableOp re-tune of the hipBLASLt GEMMs at the bench default (b=512 since late round 3: encoder GEMMs with 524288 rows
 # and the full-logits LM head are not in the shipped table).  Writes gpurun_out/tune/merged.csv; the A/B against the
-# previous table is tools/gpu_tune_ab.sh.  A heartbeat line every 50 s keeps the (otherwise silent) tuning run alive.
+# previous table is tools/tunableop_ab.sh.  A heartbeat line every 50 s keeps the (otherwise silent) tuning run alive.
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/tune
