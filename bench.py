@@ -16,9 +16,12 @@ and before anything touches the GPU), forwards its exit code, and rank 0 of the 
 driver's ``torch.distributed.run ... bench.py --gpus N`` form runs the ranks directly.
 
 Every N runs the same step: forward + backward (+ GA micro-steps) and the optimizer replayed from HIP graphs
-(train/graph.py); for N > 1 the gradient all-reduce runs between the forward/backward graph and the optimizer graph
-as the reducer's frozen bucket schedule (``comm.schedule`` = "split-graph"), so the 1 -> N curve compares the same
-method at every N.  ``--graph off`` gives the eager, hook-overlapped reducer instead.
+(train/graph.py).  For N > 1 the backward graph is a chain of segments cut at the reducer's bucket boundaries and
+each bucket's async RCCL all-reduce is launched between the segment replays, overlapping the rest of the backward
+(``comm.schedule`` = "overlap-graph"; ``--no-overlap``: every bucket after the backward, "split-graph").  ``--graph
+off`` gives the eager, hook-overlapped reducer.  ``--bucket-mb auto`` (default for N > 1) picks the bucket size from an
+all-reduce probe on the job's process group (``comm.bucket_choice``); ``--grad-reduce-dtype bf16`` puts bf16 on the
+wire (fp32 accumulation kept).
 
 Multi-GPU self-diagnosis (N > 1; every field is also produced on a gloo CPU rehearsal, DLLM_FORCE_CPU=1):
   * before timing, every rank's world size, RCCL version, bucket layout (bounds + segment sizes) and parameter count
@@ -75,8 +78,12 @@ def parse():
                          "16/32/64/128 — it needs 262 GB at 128, so 128 is its largest batch")
     ap.add_argument("--src-len", type=int, default=1024)
     ap.add_argument("--tgt-len", type=int, default=128)
-    ap.add_argument("--bucket-mb", type=float, default=None)
-    ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--bucket-mb", default="auto",
+                    help="all-reduce bucket MiB, or auto (probe over 32-256 MiB on the job's process group; N > 1)")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="all-reduce every bucket after the backward (graph: split schedule; eager: one coalesced call)")
+    ap.add_argument("--grad-reduce-dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="dtype of the gradient all-reduce on the wire (fp32 accumulation either way)")
     ap.add_argument("--dropout", type=float, default=None, help="override model dropout (default: config 0.1)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--grad-ckpt", action="store_true", help="activation checkpointing per block")
@@ -88,11 +95,13 @@ def parse():
                     help="replay the step (forward, backward, GA micro-steps, clip, AdamW) from HIP graphs "
                          "(train/graph.py; N > 1: the bucketed all-reduce between the two graphs); auto: on whenever "
                          "the ranks run on GPUs; off: eager steps with the hook-overlapped reducer")
-    ap.add_argument("--graph-comm", default=None, choices=["split", "capture"],
-                    help="N > 1 graph schedule (train/graph.py): split (default) or capture (RCCL inside the graph)")
+    ap.add_argument("--graph-comm", default=None, choices=["overlap", "split", "capture"],
+                    help="N > 1 graph schedule (train/graph.py): overlap (default: segmented backward graph, buckets "
+                         "launched between the segments), split (after backward) or capture (RCCL inside the graph)")
     ap.add_argument("--dtype", default=None, choices=["bf16", "fp32"],
                     help="weights/activations dtype (default bf16; fp32 on a CPU rehearsal)")
     a = ap.parse_args()
+    a.bucket_mb = "auto" if str(a.bucket_mb).lower() == "auto" else float(a.bucket_mb)
     if a.comm_stress and "--batch-per-gpu" not in " ".join(sys.argv):
         a.batch_per_gpu = 8
     if a.batch_per_gpu is None:
@@ -200,8 +209,11 @@ def build(a, env):
     model = build_model(cfg)
     dtype_name = a.dtype or ("bf16" if env.device.type == "cuda" else "fp32")
     dtype = torch.bfloat16 if dtype_name == "bf16" else torch.float32
+    bucket_mb = a.bucket_mb
+    if bucket_mb == "auto" and (env.world_size == 1 or env.backend != "nccl"):
+        bucket_mb = DEFAULT_BUCKET_MB  # nothing to probe (1 rank) / a gloo rehearsal: the fixed default
     eng = TrainEngine(model, env, lr=5e-5, weight_decay=0.01, max_grad_norm=1.0, dtype=dtype,
-                      bucket_mb=a.bucket_mb or DEFAULT_BUCKET_MB, overlap=not a.no_overlap)
+                      bucket_mb=bucket_mb, overlap=not a.no_overlap, grad_reduce_dtype=a.grad_reduce_dtype)
     eng.train()
     return cfg, eng, dtype_name
 
@@ -239,11 +251,23 @@ def main():
         try:
             graphed = GraphedStep(eng, batches[:GA], warmup=2, comm=a.graph_comm)
         except Exception as e:  # noqa: BLE001 - recorded in the JSON line; the step is then rebuilt from scratch
-            if a.graph == "on":
+            if a.graph == "on" and n == 1:
                 raise
             graph_error = f"{type(e).__name__}: {str(e)[:300]}"
-            print(f"[bench] graph capture failed ({graph_error}); rebuilding the engine, eager steps", file=sys.stderr)
             graphed = None
+        if n > 1:
+            # every rank must take the same path (graphed collective schedule vs eager hooks): agree on the capture
+            # outcome before anything else runs a collective; one failed rank sends every rank to the rebuilt eager step
+            ok = torch.tensor([0 if graphed is None else 1], dtype=torch.int32,
+                              device=env.device if env.backend == "nccl" else "cpu")
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            if ok.item() == 0 and graphed is not None:
+                graph_error = "capture failed on another rank"
+                graphed = None
+            if graphed is None and a.graph == "on":
+                raise SystemExit(f"[bench] rank {env.rank}: HIP-graph capture failed ({graph_error}) with --graph on")
+        if graphed is None:
+            print(f"[bench] graph capture failed ({graph_error}); rebuilding the engine, eager steps", file=sys.stderr)
             torch.cuda.synchronize()
             # the failed capture left the engine mid-state (warmup steps taken, step seeds on, host mirrors ahead of
             # the device): start over with a fresh model, optimizer and seed stream
@@ -284,13 +308,21 @@ def main():
         ex_t = torch.tensor([sum(ex) / max(1, len(ex)), max(ex, default=0.0)], dtype=torch.float64,
                             device=env.device if env.backend == "nccl" else "cpu")
         dist.all_reduce(ex_t, op=dist.ReduceOp.MAX)  # the slowest rank's exposure sets the step
-        split = graphed is not None and graphed.comm == "split"
+        gcomm = graphed.comm if graphed is not None else None
         bl = eng.reducer.launch_summary()
-        if split:  # every bucket launches after backward, in bucket order (GradReducer.sync_buckets)
-            nb = len(eng.reducer.buckets)
+        nb = len(eng.reducer.buckets)
+        if gcomm == "split":  # every bucket launches after backward, in bucket order (GradReducer.sync_buckets)
             bl = {"order": list(range(nb)), "ready_frac_at_launch": [1.0] * nb, "launched_before_backward_end": 0,
                   "n_buckets": nb}
-        comm = {"schedule": ("split-graph" if split else "captured-graph" if graphed is not None else "eager-overlap"),
+        elif gcomm == "overlap":  # the segmented replay: buckets launched between backward segments, then the tail
+            sch = graphed.schedule()
+            bl = {"order": list(range(nb)), "segments": sch["segments"], "tail_buckets": sch["tail_buckets"],
+                  "launched_before_backward_end": sch["buckets_launched_before_backward_end"], "n_buckets": nb}
+        comm = {"schedule": {"split": "split-graph", "overlap": "overlap-graph", "capture": "captured-graph",
+                             None: "eager-overlap" if eng.reducer.overlap else "eager-post-backward"}[gcomm],
+                "overlap_frac": round(bl["launched_before_backward_end"] / max(1, nb), 3),
+                "grad_reduce_dtype": a.grad_reduce_dtype,
+                "bucket_choice": eng.reducer.bucket_choice,
                 "exposed_ms_per_step": round(ex_t[0].item(), 3), "exposed_ms_max": round(ex_t[1].item(), 3),
                 "timed_backwards": len(ex), "bucket_launch": bl,
                 "buckets_launched_before_backward_end": bl["launched_before_backward_end"],

@@ -13,6 +13,10 @@
 // keeps computing).  The first hook of a backward queues finalize() on the autograd engine; finalize
 // launches leftovers (unused parameters) and makes the compute stream wait on the RCCL work — no host
 // synchronisation on the GPU path.  Averaging uses ReduceOp::AVG (RCCL) or SUM + one scale (gloo).
+// Compress-for-wire (set_wire_buffer, --grad-reduce-dtype bf16): a launch casts the fp32 bucket into its slice of a
+// persistent bf16 shadow on the compute stream and all-reduces that; finalize widens it back after the wait.
+// launch_upto(n) is the replay side of a segmented HIP-graph step (train/graph.py "overlap"): the buckets whose
+// readiness the capture cut the backward graph at are launched between the graph segments, in bucket order.
 #include <torch/extension.h>
 #include <torch/csrc/autograd/engine.h>
 #include <torch/csrc/distributed/c10d/ProcessGroup.hpp>
@@ -21,6 +25,7 @@
 
 #include <dlfcn.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -98,7 +103,13 @@ class NativeReducer {
     }
     const auto h0 = std::chrono::steady_clock::now();
     while (next_ < nb) launch_locked(next_++);
-    for (auto& w : works_) w->wait();
+    for (auto& bw : works_) {
+      bw.second->wait();
+      if (wire_.defined()) {
+        const int64_t s = bounds_[2 * bw.first], e = bounds_[2 * bw.first + 1];
+        grad_buf_.narrow(0, s, e - s).copy_(wire_.narrow(0, s, e - s));
+      }
+    }
     works_.clear();
     if (timed && e0) {
       (void)hipEventRecord(e1, st);
@@ -112,11 +123,28 @@ class NativeReducer {
 
   // train-task path: one coalesced all-reduce of the whole buffer, no hooks involved
   void sync_all() {
-    std::vector<at::Tensor> ts{grad_buf_};
+    if (wire_.defined()) wire_.copy_(grad_buf_);
+    std::vector<at::Tensor> ts{wire_.defined() ? wire_ : grad_buf_};
     c10d::AllreduceOptions opts;
     opts.reduceOp = use_avg_op_ && average_ ? c10d::ReduceOp::AVG : c10d::ReduceOp::SUM;
     pg_->allreduce(ts, opts)->wait();
+    if (wire_.defined()) grad_buf_.copy_(wire_);
     if (average_ && !use_avg_op_) grad_buf_.div_(pg_->getSize());
+  }
+
+  void set_wire_buffer(at::Tensor w) {
+    std::lock_guard<std::mutex> g(mu_);
+    TORCH_CHECK(w.dim() == 1 && w.is_contiguous() && w.numel() == grad_buf_.numel() &&
+                    w.device() == grad_buf_.device(),
+                "wire buffer must be a contiguous 1-D tensor shaped like the gradient buffer");
+    wire_ = std::move(w);
+  }
+
+  // launch buckets [launched, n) in order (no readiness check: the caller's schedule guarantees the gradients)
+  void launch_upto(int64_t n) {
+    std::lock_guard<std::mutex> g(mu_);
+    n = std::min<int64_t>(n, num_buckets());
+    while (next_ < n) launch_locked(next_++);
   }
 
   void set_enabled(bool e) {
@@ -161,10 +189,16 @@ class NativeReducer {
     std::snprintf(msg, sizeof msg, "allreduce bucket %ld (%.1f MiB)", (long)b,
                   (double)(e - s) * grad_buf_.element_size() / 1048576.0);
     roctx_mark(msg);
-    std::vector<at::Tensor> ts{grad_buf_.narrow(0, s, e - s)};
+    at::Tensor view = grad_buf_.narrow(0, s, e - s);
+    if (wire_.defined()) {
+      at::Tensor w = wire_.narrow(0, s, e - s);
+      w.copy_(view);  // compute stream: the all-reduce's stream waits on it
+      view = w;
+    }
+    std::vector<at::Tensor> ts{view};
     c10d::AllreduceOptions opts;
     opts.reduceOp = use_avg_op_ && average_ ? c10d::ReduceOp::AVG : c10d::ReduceOp::SUM;
-    works_.push_back(pg_->allreduce(ts, opts));
+    works_.emplace_back(b, pg_->allreduce(ts, opts));
   }
 
   void launch_ready_locked() {
@@ -173,6 +207,7 @@ class NativeReducer {
   }
 
   at::Tensor grad_buf_;
+  at::Tensor wire_;  // compress-for-wire shadow (undefined: all-reduce the buckets in place)
   std::vector<int64_t> bounds_, seg_bucket_, counts_, pending_;
   std::vector<bool> ready_;
   c10::intrusive_ptr<c10d::ProcessGroup> pg_;
@@ -183,7 +218,7 @@ class NativeReducer {
   std::vector<double> host_ms_;
   bool callback_queued_ = false;
   int64_t next_ = 0;
-  std::vector<c10::intrusive_ptr<c10d::Work>> works_;
+  std::vector<std::pair<int64_t, c10::intrusive_ptr<c10d::Work>>> works_;
   std::mutex mu_;
 };
 
@@ -197,6 +232,8 @@ void bind_reducer(pybind11::module& m) {
       .def("mark_ready", &NativeReducer::mark_ready)
       .def("finalize", &NativeReducer::finalize, py::call_guard<py::gil_scoped_release>())
       .def("sync_all", &NativeReducer::sync_all, py::call_guard<py::gil_scoped_release>())
+      .def("set_wire_buffer", &NativeReducer::set_wire_buffer)
+      .def("launch_upto", &NativeReducer::launch_upto, py::call_guard<py::gil_scoped_release>())
       .def("set_enabled", &NativeReducer::set_enabled)
       .def("set_timing", &NativeReducer::set_timing)
       .def("take_exposed_ms", &NativeReducer::take_exposed_ms, py::call_guard<py::gil_scoped_release>())

@@ -16,6 +16,11 @@ from .models.config import resolve_config
 from .platform import valohai
 
 
+def bucket_mb_arg(v: str):
+    """``--bucket-mb``: a size in MiB or ``auto``."""
+    return "auto" if str(v).lower() == "auto" else float(v)
+
+
 def base_parser(description: str, defaults: dict | None = None) -> argparse.ArgumentParser:
     d = {"batch_size": 1, "num_epochs": 1, "warmup_steps": 500, "evaluation_steps": 500}
     d.update(defaults or {})
@@ -39,8 +44,15 @@ def base_parser(description: str, defaults: dict | None = None) -> argparse.Argu
                         "first step's measured activation memory allows in 60%% of HBM), N (max samples per pass), 0 off")
     g.add_argument("--learning-rate", type=float, default=5e-5)
     g.add_argument("--max-steps", type=int, default=-1)
-    g.add_argument("--bucket-mb", type=float, default=None, help="gradient all-reduce bucket size (MiB)")
-    g.add_argument("--no-overlap", action="store_true", help="all-reduce after backward instead of overlapping")
+    g.add_argument("--bucket-mb", type=bucket_mb_arg, default=None,
+                   help="gradient all-reduce bucket size in MiB, or 'auto' (probe RCCL's bus bandwidth over 32-256 MiB "
+                        "on the job's process group and take the smallest size within 5%% of the best; default 128)")
+    g.add_argument("--no-overlap", action="store_true",
+                   help="all-reduce after backward instead of overlapping (HIP-graph steps: the post-backward "
+                        "'split' schedule)")
+    g.add_argument("--grad-reduce-dtype", choices=["fp32", "bf16"], default="fp32",
+                   help="dtype of the gradient all-reduce on the wire: bf16 halves the xGMI bytes; gradients are still "
+                        "accumulated in fp32 and widened back after each bucket's all-reduce")
     g.add_argument("--eval-batch-size", type=int, default=None)
     g.add_argument("--max-eval-samples", type=int, default=None)
     g.add_argument("--gen-max-length", type=int, default=128)

@@ -15,7 +15,13 @@ Replaces torch DDP's C++ Reducer that the reference reaches through HF Trainer /
   per bucket, not link bandwidth, dominates small buckets); the first bucket stays small (1 MiB,
   DDP's ``_DEFAULT_FIRST_BUCKET_BYTES``) so communication starts early in backward;
 * ``no_sync()`` for gradient accumulation (HF Trainer trainer.py:1750-1757);
-* ``overlap=False`` → one coalesced all-reduce after backward (train-task semantics, same math).
+* ``overlap=False`` → one coalesced all-reduce after backward (train-task semantics, same math);
+* ``wire_dtype=torch.bfloat16`` (``--grad-reduce-dtype bf16``) → compress for the wire only: gradients accumulate in
+  the fp32 flat buffer, each bucket is cast to a persistent bf16 shadow on the compute stream at launch, all-reduced
+  in bf16 (half the bytes over xGMI) and widened back into the fp32 bucket once its all-reduce has been waited for;
+* segmented HIP-graph capture (train/graph.py "overlap"): ``begin_capture_cuts`` counts readiness without launching
+  anything and calls back when the next bucket(s) in order became ready, so the backward graph is cut there and the
+  replay launches those buckets between the segments (``launch_upto``).
 
 Two engines implement the same bucket/launch policy: the native one (csrc/reducer.cpp,
 ``NativeReducer``: bucket state machine and c10d ``ProcessGroup::allreduce`` launches in C++ — the
@@ -39,12 +45,58 @@ from .flat import FlatParams
 
 DEFAULT_BUCKET_MB = 128.0
 FIRST_BUCKET_MB = 1.0
+BUCKET_MB_CANDIDATES = (32.0, 64.0, 128.0, 256.0)
+
+
+def wire_dtype_of(name: str | None) -> torch.dtype | None:
+    """``--grad-reduce-dtype``: None / "fp32" -> all-reduce the fp32 buckets as they are, "bf16" -> compress-for-wire."""
+    if name in (None, "", "fp32", "float32", "none"):
+        return None
+    if name in ("bf16", "bfloat16"):
+        return torch.bfloat16
+    raise ValueError(f"grad reduce dtype must be fp32 or bf16, got {name!r}")
+
+
+def choose_bucket_mb(device: torch.device, total_mb: float, group=None, wire_dtype: torch.dtype | None = None,
+                     candidates=BUCKET_MB_CANDIDATES, iters: int = 3, tolerance: float = 0.95) -> dict:
+    """Bucket size from an in-run all-reduce probe on the job's own process group (every rank runs it: collective).
+
+    For each candidate size (capped by the gradient buffer) the slowest rank's time of an all-reduce of that many
+    bytes (in the wire dtype) is measured; the bus bandwidth 2(N-1)/N x bytes / time is what RCCL over xGMI delivers
+    at that size.  Chosen: the SMALLEST candidate within ``tolerance`` of the best bandwidth — large enough that the
+    per-collective latency is amortised, no larger, so the first bucket launches early in backward and the exposed
+    tail (the last bucket, launched when backward ends) stays short.  Returns {"bucket_mb", "busbw_gbps": {...}}."""
+    n = dist.get_world_size(group)
+    esz_wire = 2 if wire_dtype == torch.bfloat16 else 4
+    cands = sorted({float(c) for c in candidates if c <= max(total_mb, min(candidates))})
+    table = {}
+    for mb in cands:
+        x = torch.ones(max(1, int(mb * 2**20) // 4 * 4 // esz_wire), device=device,
+                       dtype=torch.bfloat16 if wire_dtype == torch.bfloat16 else torch.float32)
+        dist.all_reduce(x, group=group)
+        if device.type == "cuda":
+            torch.cuda.synchronize(device)
+        dist.barrier(group=group)
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            dist.all_reduce(x, group=group)
+        if device.type == "cuda":
+            torch.cuda.synchronize(device)
+        t = torch.tensor([(time.perf_counter() - t0) / iters], dtype=torch.float64,
+                         device=device if device.type == "cuda" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+        table[mb] = 2 * (n - 1) / n * x.numel() * x.element_size() / t.item() / 1e9
+    best = max(table.values())
+    pick = min(mb for mb, bw in table.items() if bw >= tolerance * best)
+    return {"bucket_mb": pick, "busbw_gbps": {f"{mb:g}": round(bw, 2) for mb, bw in table.items()},
+            "rule": f"smallest within {tolerance:g} of the best bus bandwidth"}
 
 
 class GradReducer:
-    def __init__(self, flat: FlatParams, group=None, bucket_mb: float = DEFAULT_BUCKET_MB,
+    def __init__(self, flat: FlatParams, group=None, bucket_mb: float | str | None = DEFAULT_BUCKET_MB,
                  first_bucket_mb: float = FIRST_BUCKET_MB, overlap: bool = True, average: bool = True,
-                 native: bool | None = None, rebuild: bool | None = None, force: bool = False):
+                 native: bool | None = None, rebuild: bool | None = None, force: bool = False,
+                 wire_dtype: torch.dtype | None = None):
         self.flat = flat
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -54,8 +106,25 @@ class GradReducer:
         self.backend = dist.get_backend(group) if dist.is_initialized() else "none"
         self.overlap = overlap
         self.average = average
+        if wire_dtype is not None and wire_dtype == flat.grad_buf.dtype:
+            wire_dtype = None  # the buckets are already in that dtype
+        if wire_dtype not in (None, torch.bfloat16):
+            raise ValueError(f"wire dtype must be None or bfloat16, got {wire_dtype}")
+        self.wire_dtype = wire_dtype
+        # persistent bf16 shadow of the gradient buffer (compress-for-wire): bucket b's all-reduce runs on its slice
+        self.wire_buf = (torch.empty(flat.grad_buf.numel(), dtype=wire_dtype, device=flat.grad_buf.device)
+                         if wire_dtype is not None and self.dp else None)
+        self._cut_fn = None  # segmented graph capture (begin_capture_cuts)
         self.enabled = True
-        self.bucket_mb, self.first_bucket_mb = bucket_mb, first_bucket_mb
+        self.bucket_choice = None
+        if bucket_mb in ("auto", None):
+            bucket_mb = DEFAULT_BUCKET_MB
+            if self.world > 1:  # probe on the job's own process group (every rank constructs its reducer together)
+                total = flat.grad_buf.numel() * flat.grad_buf.element_size() / 2**20
+                dev = flat.grad_buf.device if self.backend == "nccl" else torch.device("cpu")
+                self.bucket_choice = choose_bucket_mb(dev, total, group=group, wire_dtype=wire_dtype)
+                bucket_mb = self.bucket_choice["bucket_mb"]
+        self.bucket_mb, self.first_bucket_mb = float(bucket_mb), first_bucket_mb
         if native is None:
             native = os.environ.get("DLLM_NATIVE_REDUCER", "1") != "0" and _ext.native() is not None
         self.use_native = bool(native)
@@ -123,6 +192,8 @@ class GradReducer:
             bounds = [x for se in self.buckets for x in se]
             self.native = _ext.native().NativeReducer(flat.grad_buf, bounds, self.seg_bucket, pg, self.average,
                                                       self.backend == "nccl")
+            if self.wire_buf is not None:
+                self.native.set_wire_buffer(self.wire_buf)
 
     # --------------------------------------------------------------------------------- hooks
     def _on_ready(self, p):
@@ -130,6 +201,18 @@ class GradReducer:
             return
         i = self._seg_of[id(p)]
         self.ready_log.append(i)
+        if self._cut_fn is not None:  # segmented capture: count, never launch (nothing may run inside the capture)
+            b = self.seg_bucket[i]
+            self._pending[b] -= 1
+            if self._pending[b] == 0:
+                self._ready[b] = True
+            first = self._next
+            while self._next < len(self.buckets) and self._ready[self._next]:
+                self._next += 1
+            if self._next > first:
+                self.launch_log.extend((b, len(self.ready_log)) for b in range(first, self._next))
+                self._cut_fn(list(range(first, self._next)))
+            return
         if self.native is not None:
             before = self.native.launched()
             self.native.mark_ready(i)
@@ -174,6 +257,9 @@ class GradReducer:
     def _launch(self, b: int):
         s, e = self.buckets[b]
         view = self.flat.grad_buf[s:e]
+        if self.wire_buf is not None:  # compress for the wire (widened back in finish)
+            self.wire_buf[s:e].copy_(view)
+            view = self.wire_buf[s:e]
         profiling.mark(f"allreduce bucket {b} ({(e - s) * view.element_size() / 2**20:.1f} MiB)")
         if self.average and self.backend == "nccl":
             w = dist.all_reduce(view, op=dist.ReduceOp.AVG, group=self.group, async_op=True)
@@ -199,8 +285,11 @@ class GradReducer:
         while self._next < len(self.buckets):
             self._launch(self._next)
             self._next += 1
-        for _, w in self._works:
+        for b, w in self._works:
             w.wait()
+            if self.wire_buf is not None:
+                s, e = self.buckets[b]
+                self.flat.grad_buf[s:e].copy_(self.wire_buf[s:e])
         if ev is not None:
             ev[1].record()
             self._events.append(ev)
@@ -228,6 +317,35 @@ class GradReducer:
             if self.native is not None:
                 self.native.set_enabled(prev)
 
+    def begin_capture_cuts(self, cut_fn):
+        """Segmented graph capture of a synchronised backward (train/graph.py "overlap"): readiness is counted as
+        usual but nothing is launched; ``cut_fn(buckets)`` is called (on the autograd thread) each time the next
+        bucket(s) in bucket order became ready — the point where the capture cuts the backward graph and the replay
+        launches them.  ``end_capture_cuts`` returns the buckets left for after the backward."""
+        self._pending = list(self._counts)
+        self._ready = [False] * len(self.buckets)
+        self._next = 0
+        self._cut_fn = cut_fn
+
+    def end_capture_cuts(self) -> list[int]:
+        rest = list(range(self._next, len(self.buckets)))
+        self._cut_fn = None
+        self._pending = list(self._counts)
+        self._ready = [False] * len(self.buckets)
+        self._next = 0
+        return rest
+
+    def launch_upto(self, n: int):
+        """Launch buckets [launched, n) in order (async all-reduce; replay of a segmented graph step)."""
+        if not self.dp:
+            return
+        if self.native is not None:
+            self.native.launch_upto(n)
+            return
+        while self._next < min(n, len(self.buckets)):
+            self._launch(self._next)
+            self._next += 1
+
     def sync_buckets(self):
         """Every bucket, in bucket order, as an async all-reduce; then the compute stream waits on them (no host sync
         on RCCL).  The frozen launch schedule a graphed data-parallel step issues between its replays
@@ -247,6 +365,15 @@ class GradReducer:
             self.native.sync_all()
             return
         g = self.flat.grad_buf
+        if self.wire_buf is not None:
+            w = self.wire_buf
+            w.copy_(g)
+            dist.all_reduce(w, op=dist.ReduceOp.AVG if (self.average and self.backend == "nccl") else dist.ReduceOp.SUM,
+                            group=self.group)
+            g.copy_(w)
+            if self.average and self.backend != "nccl":
+                g.div_(self.world)
+            return
         if self.average and self.backend == "nccl":
             dist.all_reduce(g, op=dist.ReduceOp.AVG, group=self.group)
         else:

@@ -29,7 +29,7 @@ from ..ops.optim import FusedAdamW
 from ..parallel import collectives
 from ..parallel.env import init_distributed
 from ..parallel.flat import FlatParams
-from ..parallel.reducer import DEFAULT_BUCKET_MB, GradReducer
+from ..parallel.reducer import DEFAULT_BUCKET_MB, GradReducer, wire_dtype_of
 from ..parallel.sampler import ShardedBatchSampler
 from .engine import default_grad_dtype
 from .schedule import LRScheduler
@@ -110,8 +110,8 @@ class PreparedOptimizer:
 
 class Accelerator:
     def __init__(self, mixed_precision: str | None = None, gradient_accumulation_steps: int = 1,
-                 bucket_mb: float = DEFAULT_BUCKET_MB, overlap_comm: bool = True, cpu: bool = False, seed: int = 0,
-                 even_batches: bool = True):
+                 bucket_mb: float | str = DEFAULT_BUCKET_MB, overlap_comm: bool = True, cpu: bool = False, seed: int = 0,
+                 even_batches: bool = True, grad_reduce_dtype: str | None = None):
         self.env = init_distributed(cpu=cpu if cpu else None)
         self.device = self.env.device
         if mixed_precision is None:
@@ -121,6 +121,7 @@ class Accelerator:
         self.gradient_accumulation_steps = gradient_accumulation_steps
         self.bucket_mb = bucket_mb
         self.overlap_comm = overlap_comm
+        self.grad_reduce_dtype = grad_reduce_dtype
         self.seed = seed
         self.even_batches = even_batches
         self.sync_gradients = True
@@ -192,7 +193,8 @@ class Accelerator:
         flat = FlatParams(model, grad_dtype=default_grad_dtype(self.dtype))  # fp32 gradients (train/engine.py)
         reducer = None
         if self.env.world_size > 1:
-            reducer = GradReducer(flat, bucket_mb=self.bucket_mb, overlap=self.overlap_comm)
+            reducer = GradReducer(flat, bucket_mb=self.bucket_mb, overlap=self.overlap_comm,
+                                  wire_dtype=wire_dtype_of(self.grad_reduce_dtype))
             reducer.broadcast_params(model)
         self._model = PreparedModel(model, flat, reducer)
         return self._model
@@ -251,18 +253,23 @@ class Accelerator:
         optimizer.step(); optimizer.zero_grad()`` (ref/train-accelerator.py:219-228) — as one callable
         ``step(batch) -> loss``, run by train/graph.py's StepRunner: replayed from a HIP graph once the batch shape
         repeats (GPU, unless ``graph=False`` / ``DLLM_GRAPH=0``), eager otherwise.  Gradient accumulation keeps the
-        explicit loop (``accumulate`` / ``backward``); a clip requested with ``clip_grad_norm_`` before the first call is
-        part of every step."""
+        explicit loop (``accumulate`` / ``backward``).  ``clip_grad_norm_`` keeps its eager meaning: it applies to the
+        next step only (call it every iteration to clip every step); a captured graph holds the clip it was captured
+        with, so a step whose clip differs drops the graph and the runner captures again (StepRunner.invalidate)."""
         from .engine import TrainEngine
         from .graph import StepRunner
         m = model if isinstance(model, PreparedModel) else self._model
         po = optimizer if isinstance(optimizer, PreparedOptimizer) else self._prepared_opts[-1]
         if self.gradient_accumulation_steps != 1:
             raise ValueError("make_train_step: one micro-batch per optimizer step (use accumulate() for GA)")
-        eng = TrainEngine.from_parts(m.module, self.env, m.flat, m.reducer, po.opt, max_grad_norm=po._clip)
+        eng = TrainEngine.from_parts(m.module, self.env, m.flat, m.reducer, po.opt, max_grad_norm=None)
         runner = StepRunner(eng, enabled=graph)
 
         def step(batch: dict) -> torch.Tensor:
+            clip, po._clip = po._clip, None  # requested for this step only (eager PreparedOptimizer.step semantics)
+            if clip != eng.max_grad_norm:
+                eng.max_grad_norm = clip
+                runner.invalidate()
             self._step += 1
             self.sync_gradients = True
             losses, _ = runner([batch])

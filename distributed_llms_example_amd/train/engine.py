@@ -18,7 +18,7 @@ from ..ops.optim import FusedAdamW
 from ..utils import profiling
 from ..parallel.env import DistEnv
 from ..parallel.flat import FlatParams
-from ..parallel.reducer import DEFAULT_BUCKET_MB, GradReducer
+from ..parallel.reducer import DEFAULT_BUCKET_MB, GradReducer, wire_dtype_of
 
 # transformers Trainer.get_decay_parameter_names: no decay for biases and norm weights (trainer.py:1305-1315)
 def default_no_decay(name: str) -> bool:
@@ -44,15 +44,19 @@ def token_count(labels: torch.Tensor, ignore_index: int = -100) -> torch.Tensor:
 class TrainEngine:
     def __init__(self, model: torch.nn.Module, env: DistEnv, *, lr: float = 5e-5, weight_decay: float = 0.0,
                  betas=(0.9, 0.999), eps: float = 1e-8, max_grad_norm: float | None = 1.0,
-                 dtype: torch.dtype = torch.bfloat16, bucket_mb: float = DEFAULT_BUCKET_MB, overlap: bool = True,
+                 dtype: torch.dtype = torch.bfloat16, bucket_mb: float | str = DEFAULT_BUCKET_MB, overlap: bool = True,
                  no_decay=default_no_decay, label_smoothing: float = 0.0, grad_dtype: torch.dtype | None = None,
-                 force_reducer: bool = False):
+                 force_reducer: bool = False, grad_reduce_dtype: str | None = None):
+        """``bucket_mb``: MiB per all-reduce bucket, or "auto" (parallel/reducer.py choose_bucket_mb: probed on the
+        job's process group, recorded in ``reducer.bucket_choice``).  ``grad_reduce_dtype``: "bf16" compresses each bucket
+        for the wire only (fp32 accumulation kept), None / "fp32" reduces the gradient buffer as it is."""
         self.env = env
         self.model = model.to(device=env.device, dtype=dtype)
         self.dtype = dtype
         self.flat = FlatParams(self.model, grad_dtype=grad_dtype or default_grad_dtype(dtype))
         # force_reducer: a reducer (and its collectives) on a 1-rank process group — GPU tests of the RCCL paths
-        self.reducer = (GradReducer(self.flat, bucket_mb=bucket_mb, overlap=overlap, force=force_reducer)
+        self.reducer = (GradReducer(self.flat, bucket_mb=bucket_mb, overlap=overlap, force=force_reducer,
+                                    wire_dtype=wire_dtype_of(grad_reduce_dtype))
                         if env.world_size > 1 or force_reducer else None)
         if self.reducer is not None:
             self.reducer.broadcast_params(self.model)

@@ -5,10 +5,20 @@ ref/train-accelerator.py:169, ref/train-task.py:180, ref/train-torchrun.py:119,1
 GPU, sets the step time.  ``GraphedStep`` captures forward + backward (+ the gradient-accumulation micro-steps) + the
 global-norm clip + AdamW + zero_grad with ``torch.cuda.graph`` and then replays it: one or two host calls per step.
 
-Data parallel (an engine with a gradient reducer, parallel/reducer.py) is graphed in one of two schedules
-(``comm``, default from ``DLLM_GRAPH_COMM``):
+Data parallel (an engine with a gradient reducer, parallel/reducer.py) is graphed in one of three schedules
+(``comm``; default ``DLLM_GRAPH_COMM``, else "overlap" when the reducer overlaps, "split" with ``--no-overlap``):
 
-* ``"split"`` (default): graph 1 = every micro-batch's forward + backward with the reducer disabled (gradients
+* ``"overlap"`` (default): the forward + backward is captured as a CHAIN of graph segments cut at the reducer's bucket
+  boundaries.  During the capture of the synchronised pass the reducer counts gradient readiness exactly as in an
+  eager step but launches nothing (``GradReducer.begin_capture_cuts``); each time the next bucket(s) in bucket order
+  become ready, the capture ends the current segment and begins the next one (same stream, same memory pool, relaxed
+  capture mode: the cut runs on autograd's device thread).  A replay runs segment k, launches the buckets that became
+  ready at the end of segment k as async RCCL all-reduces (their stream waits on the compute stream, so they run
+  beside segment k+1), ..., then the compute stream waits on every bucket and the optimizer graph runs.  Same
+  collective sequence as the eager engine, the overlap of the eager engine, and nothing of RCCL inside a graph.
+  The bucket layout is the one rebuilt in gradient-ready order by the eager warm-up steps (rank 0's, broadcast), so
+  every rank cuts at the same buckets; one host call per segment (≈8 at t5-base).
+* ``"split"``: graph 1 = every micro-batch's forward + backward with the reducer disabled (gradients
   accumulate locally, like ``no_sync``); then the gradient all-reduce is issued EAGERLY between the replays — the
   reducer's launch schedule frozen to its bucket list (``GradReducer.sync_buckets``: the same buckets, in the same
   order, on every rank, each an async RCCL all-reduce; the compute stream waits on them without a host sync);
@@ -48,7 +58,7 @@ import torch
 
 from ..ops import rng as rng_mod
 
-COMM_MODES = ("split", "capture")
+COMM_MODES = ("overlap", "split", "capture")
 
 
 class GraphedStep:
@@ -63,7 +73,10 @@ class GraphedStep:
             raise ValueError("GraphedStep: GPU only (use_graph=False runs the same schedule eagerly)")
         self.eng = engine
         self.red = engine.reducer
-        self.comm = (comm or os.environ.get("DLLM_GRAPH_COMM", "split")) if self.red is not None else None
+        default = "overlap" if (self.red is not None and self.red.overlap and self.red.dp) else "split"
+        self.comm = (comm or os.environ.get("DLLM_GRAPH_COMM", default)) if self.red is not None else None
+        if self.comm == "overlap" and not (self.red.overlap and self.red.dp):
+            self.comm = "split"  # no readiness hooks (--no-overlap) or nothing to reduce: post-backward buckets
         if self.comm is not None and self.comm not in COMM_MODES:
             raise ValueError(f"GraphedStep: comm must be one of {COMM_MODES}, got {self.comm!r}")
         self.use_graph = use_graph
@@ -102,7 +115,9 @@ class GraphedStep:
         # RCCL group).  Backward kernels launched from autograd's device thread onto the capture stream are captured
         # either way (capture is a property of the stream).
         mode = "thread_local"
-        if self.comm == "split":
+        if self.comm == "overlap":
+            self._capture_overlap()
+        elif self.comm == "split":
             self.g_fb = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.g_fb, capture_error_mode=mode):
                 self.loss = self._fb(sync=False)
@@ -115,6 +130,59 @@ class GraphedStep:
                 self.loss = self._fb(sync=True)
                 self.norm = self._opt()
         self._host_after_capture()  # the capture ran the Python side once but executed nothing
+
+    def _capture_overlap(self):
+        """Segmented capture of forward + backward (module docstring, "overlap"), then the optimizer graph, all in one
+        private memory pool (the graphs are replayed in the order they were captured)."""
+        dev = self.eng.env.device
+        red = self.red
+        if red._rebuild_pending:
+            raise RuntimeError("GraphedStep(overlap): the bucket layout must be rebuilt by an eager synchronised step "
+                               "before capture (warmup >= 1 or a StepRunner eager step)")
+        self._tick = torch.zeros(1, device=dev)  # one tiny kernel per cut: no segment is ever an empty graph
+        self._pool = torch.cuda.graph_pool_handle()
+        self._cap_stream = torch.cuda.Stream(dev)
+        self.segments: list = []  # (graph, launch buckets up to this index after it, or None)
+        import gc
+        gc.collect()
+        self._cap_stream.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(self._cap_stream):
+            self._seg = torch.cuda.CUDAGraph()
+            self._seg.capture_begin(pool=self._pool, capture_error_mode="relaxed")
+            red.begin_capture_cuts(self._cut)
+            try:
+                self.loss = self._fb(sync=True)
+            finally:
+                self.tail_buckets = red.end_capture_cuts()
+                self._seg.capture_end()
+            self.segments.append((self._seg, None))
+            self._seg = None
+            self.g_opt = torch.cuda.CUDAGraph()
+            self.g_opt.capture_begin(pool=self._pool, capture_error_mode="relaxed")
+            self.norm = self._opt()
+            self.g_opt.capture_end()
+        torch.cuda.current_stream(dev).wait_stream(self._cap_stream)
+
+    def schedule(self) -> dict:
+        """The data-parallel launch schedule a replay runs (bench.py ``comm``): for "overlap", the buckets launched
+        between backward segments (before the backward ends) and the tail launched after it."""
+        if self.comm != "overlap" or not self.use_graph:
+            return {"schedule": self.comm}
+        ups = [u for _, u in self.segments if u is not None]
+        return {"schedule": "overlap", "segments": len(self.segments), "buckets_launched_before_backward_end":
+                max(ups, default=0), "tail_buckets": list(self.tail_buckets), "n_buckets": len(self.red.buckets)}
+
+    def _cut(self, buckets: list[int]):
+        """Reducer callback during the segmented capture (autograd thread): buckets ``buckets`` just became ready —
+        end the current segment here; the replay launches them after it."""
+        from ..ops import streams
+        with torch.cuda.stream(self._cap_stream):
+            streams.join()  # side-stream gradient work (if any) belongs to this segment
+            self._tick.add_(1.0)
+            self._seg.capture_end()
+            self.segments.append((self._seg, buckets[-1] + 1))
+            self._seg = torch.cuda.CUDAGraph()
+            self._seg.capture_begin(pool=self._pool, capture_error_mode="relaxed")
 
     # ------------------------------------------------------------------------------------------ phases
     def _fb(self, sync: bool):
@@ -141,7 +209,18 @@ class GraphedStep:
         return eng.step(hyper=eng.optimizer.device_hyper(self.t, lr))
 
     def _eager_step(self):
-        """The step the graphs hold, run eagerly (warmup, and the use_graph=False schedule)."""
+        """The step the graphs hold, run eagerly (warmup, and the use_graph=False schedule).  "overlap": the eager
+        hook-launched reducer for the warm-up steps (they rebuild the buckets in ready order); with use_graph=False the
+        segmented schedule itself — readiness counted in capture-cut mode, each cut launching its buckets at once."""
+        if self.comm == "overlap" and not self.use_graph and not self.red._rebuild_pending:
+            red = self.red
+            red.begin_capture_cuts(lambda bs: red.launch_upto(bs[-1] + 1))
+            try:
+                loss = self._fb(sync=True)
+            finally:
+                red.end_capture_cuts()
+            red.sync_buckets()
+            return loss, self._opt()
         if self.comm == "split":
             loss = self._fb(sync=False)
             self._comm()
@@ -186,7 +265,14 @@ class GraphedStep:
         if not self.use_graph:
             self.loss, self.norm = self._eager_step()
             return self.loss
-        if self.comm == "split":
+        if self.comm == "overlap":
+            for g, upto in self.segments:
+                g.replay()
+                if upto is not None:
+                    self.red.launch_upto(upto)
+            self.red.sync_buckets()  # the tail buckets; the compute stream waits on every bucket (no host sync)
+            self.g_opt.replay()
+        elif self.comm == "split":
             self.g_fb.replay()
             self._comm()
             self.g_opt.replay()
@@ -235,6 +321,15 @@ class StepRunner:
         self.eager_steps = 0
         if self.enabled:
             engine.enable_step_seeds()
+
+    def invalidate(self):
+        """Something a captured graph baked in changed (e.g. the clip norm): drop the graph; the next steps of the
+        signature run eagerly again and are re-captured after ``warmup`` of them."""
+        if self.graph is not None:
+            torch.cuda.synchronize()
+        self.graph = None
+        self._sig = None
+        self._seen = 0
 
     def __call__(self, passes: list[dict], num_items: torch.Tensor | None = None, lr: float | None = None):
         """Run one step; returns (per-pass mean losses, pre-clip grad norm or None) as device tensors."""

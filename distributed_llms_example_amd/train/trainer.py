@@ -72,9 +72,10 @@ class TrainingArguments:
     dataloader_num_workers: int = 0
     dataloader_drop_last: bool = False
     ddp_find_unused_parameters: bool | None = None
-    ddp_bucket_cap_mb: float | None = None
+    ddp_bucket_cap_mb: float | str | None = None  # MiB, or "auto" (parallel/reducer.py choose_bucket_mb)
     ddp_timeout: int = 1800
     overlap_comm: bool = True
+    grad_reduce_dtype: str = "fp32"  # "bf16": compress each gradient bucket for the wire (fp32 accumulation kept)
     context_parallel_size: int = 1  # shard the encoder sequence over groups of this many consecutive ranks
     resume_from_checkpoint: str | None = None
     nan_guard: bool = True  # raise when the (logged, already synchronised) mean loss is NaN/Inf
@@ -130,6 +131,7 @@ class Trainer:
                                   betas=(args.adam_beta1, args.adam_beta2), eps=args.adam_epsilon,
                                   max_grad_norm=args.max_grad_norm, dtype=self.dtype,
                                   bucket_mb=args.ddp_bucket_cap_mb or DEFAULT_BUCKET_MB, overlap=args.overlap_comm,
+                                  grad_reduce_dtype=args.grad_reduce_dtype,
                                   no_decay=default_no_decay, label_smoothing=args.label_smoothing_factor)
         self.model = self.engine.model
         self.train_dataset = train_dataset

@@ -342,9 +342,11 @@ def test_bench_multirank_diagnostics_on_gloo():
 
 
 # ---------------------------------------------------------------- graphed data-parallel schedule (train/graph.py "split")
-def _split_schedule_case(rank, world, native=True, ga=2, steps=3):
-    """The split schedule the graphed DP step runs (local forward/backward of every micro-batch, then the frozen bucket
-    all-reduce, then clip + AdamW) — executed eagerly on gloo — against the hook-overlapped eager DP step."""
+def _split_schedule_case(rank, world, native=True, ga=2, steps=3, comm="split", wire=None):
+    """The schedules the graphed DP step runs — executed eagerly on gloo — against the hook-overlapped eager DP step.
+    "split": local forward/backward of every micro-batch, then the frozen bucket all-reduce, then clip + AdamW;
+    "overlap": the segmented schedule (readiness counted in capture-cut mode, each cut's buckets launched at the cut,
+    the tail after the backward)."""
     from distributed_llms_example_amd.models import build_model
     from distributed_llms_example_amd.ops.rng import manual_seed
     from distributed_llms_example_amd.parallel.env import DistEnv
@@ -359,15 +361,17 @@ def _split_schedule_case(rank, world, native=True, ga=2, steps=3):
     def engine():
         torch.manual_seed(0)
         manual_seed(5 + rank)
-        eng = TrainEngine(build_model("t5-tiny"), env, lr=1e-3, dtype=torch.float32, bucket_mb=0.05)
+        eng = TrainEngine(build_model("t5-tiny"), env, lr=1e-3, dtype=torch.float32, bucket_mb=0.05,
+                          grad_reduce_dtype=wire)
         eng.train()  # dropout on: both arms draw the same step-seeded masks
         return eng
 
     eng_s = engine()
-    gs = GraphedStep(eng_s, data[:ga], use_graph=False)
-    assert gs.comm == "split"
+    gs = GraphedStep(eng_s, data[:ga], use_graph=False, comm=comm)
+    assert gs.comm == comm
     ls = [float(gs.replay(data[ga * i:ga * (i + 1)])) for i in range(steps)]
     launched = eng_s.reducer.native.launched() if eng_s.reducer.native is not None else None
+    summary = eng_s.reducer.launch_summary()
     p_split = eng_s.flat.to_canonical(eng_s.flat.param_buf).clone()
     eng_s.disable_step_seeds()
     eng_s.reducer.remove()
@@ -385,22 +389,83 @@ def _split_schedule_case(rank, world, native=True, ga=2, steps=3):
         le.append(tot / ga)
     p_eager = eng_e.flat.to_canonical(eng_e.flat.param_buf).clone()
     eng_e.disable_step_seeds()
-    return ls, le, p_split, p_eager, launched, len(eng_s.reducer.buckets)
+    return ls, le, p_split, p_eager, launched, len(eng_s.reducer.buckets), summary
 
 
+@pytest.mark.parametrize("comm", ["split", "overlap"])
 @pytest.mark.parametrize("native", [False, pytest.param(True, marks=pytest.mark.skipif(
     not _native_available(), reason="native extension not built"))])
-def test_split_graph_schedule_matches_eager_overlap(native):
-    out = run_ranks(functools.partial(_split_schedule_case, native=native))
+def test_split_graph_schedule_matches_eager_overlap(native, comm):
+    out = run_ranks(functools.partial(_split_schedule_case, native=native, comm=comm))
     for r in (0, 1):
-        ls, le, ps, pe, launched, nb = out[r]
+        ls, le, ps, pe, launched, nb, summary = out[r]
         assert nb >= 2
         assert ls == pytest.approx(le, rel=1e-5, abs=1e-6), (ls, le)
         ps, pe = torch.as_tensor(ps), torch.as_tensor(pe)
         assert torch.allclose(ps, pe, rtol=1e-5, atol=1e-6), (ps - pe).abs().max()
         if native:
             assert launched == 0  # finalize resets the schedule after launching every bucket
+        if comm == "overlap":  # the segmented schedule launches every bucket but the tail before backward ends
+            assert summary["launched_before_backward_end"] >= nb - 1, summary
     assert torch.equal(torch.as_tensor(out[0][2]), torch.as_tensor(out[1][2]))  # ranks agree
+
+
+def _wire_case(rank, world, native, wire):
+    from distributed_llms_example_amd.models import build_model
+    from distributed_llms_example_amd.parallel.env import DistEnv
+    from distributed_llms_example_amd.train.engine import TrainEngine
+    os.environ["DLLM_NATIVE_REDUCER"] = "1" if native else "0"
+    torch.manual_seed(0)
+    env = DistEnv(rank=rank, world_size=world, backend="gloo", device=torch.device("cpu"))
+    eng = TrainEngine(build_model("t5-tiny"), env, lr=1e-3, dtype=torch.float32, bucket_mb=0.05, grad_reduce_dtype=wire)
+    eng.train(False)
+    g = torch.Generator().manual_seed(7 + rank)
+    b = {"input_ids": torch.randint(3, 500, (4, 10), generator=g), "attention_mask": torch.ones(4, 10, dtype=torch.long),
+         "labels": torch.randint(3, 500, (4, 5), generator=g)}
+    out = []
+    for _ in range(2):  # the second backward runs on the rebuilt (ready-order) buckets
+        eng.optimizer.zero_grad()
+        eng.forward_backward(b)
+        out.append(eng.flat.to_canonical(eng.flat.grad_buf).clone())
+    eng.flat.grad_buf.zero_()
+    eng.forward_backward(b, sync=False)  # this rank's local gradient (no all-reduce)
+    out.append(eng.flat.to_canonical(eng.flat.grad_buf).clone())
+    if wire == "bf16":
+        assert eng.reducer.wire_buf is not None and eng.reducer.wire_buf.dtype == torch.bfloat16
+    return out
+
+
+@pytest.mark.parametrize("native", [False, pytest.param(True, marks=pytest.mark.skipif(
+    not _native_available(), reason="native extension not built"))])
+def test_bf16_wire_all_reduce_error_is_bounded(native):
+    """--grad-reduce-dtype bf16: fp32 accumulation, bf16 on the wire.  The averaged gradient differs from the fp32-wire
+    one by bf16 rounding of the summands and of the sum: |err| <= 2^-8 (|g0| + |g1|) + 2^-8 |g| per element (x2 slack),
+    is not zero (the wire really was bf16), and every rank holds the same result."""
+    fp = run_ranks(functools.partial(_wire_case, native=native, wire="fp32"))
+    bf = run_ranks(functools.partial(_wire_case, native=native, wire="bf16"))
+    loc0, loc1 = torch.as_tensor(fp[0][2]), torch.as_tensor(fp[1][2])
+    for step in (0, 1):
+        gf, gb = torch.as_tensor(fp[0][step]), torch.as_tensor(bf[0][step])
+        torch.testing.assert_close(gf, (loc0 + loc1) / 2, atol=1e-6, rtol=1e-5)
+        err = (gb - gf).abs()
+        bound = 2 * (2 ** -8 * (loc0.abs() + loc1.abs()) / 2 + 2 ** -8 * gf.abs()) + 1e-12
+        assert err.max() > 0
+        assert bool((err <= bound).all()), (err - bound).max()
+        assert torch.equal(torch.as_tensor(bf[0][step]), torch.as_tensor(bf[1][step]))  # ranks agree
+
+
+def _bucket_probe_case(rank, world):
+    from distributed_llms_example_amd.parallel.reducer import choose_bucket_mb
+    return choose_bucket_mb(torch.device("cpu"), total_mb=3.0, candidates=(0.25, 0.5, 1.0, 2.0, 8.0), iters=2)
+
+
+def test_bucket_size_probe_agrees_across_ranks():
+    """--bucket-mb auto: every rank measures the same all-reduces (slowest rank's time) and so picks the same size,
+    one of the candidates that fit the gradient buffer."""
+    out = run_ranks(_bucket_probe_case)
+    a, b = out[0], out[1]
+    assert a["bucket_mb"] == b["bucket_mb"] and a["bucket_mb"] in (0.25, 0.5, 1.0, 2.0)
+    assert set(a["busbw_gbps"]) == {"0.25", "0.5", "1", "2"} and all(v > 0 for v in a["busbw_gbps"].values())
 
 
 # ---------------------------------------------------------------- bench.py self-launch (the driver's `bench.py --gpus N`)

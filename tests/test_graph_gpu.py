@@ -132,11 +132,12 @@ def test_graph_follows_param_group_lr():
     assert not torch.equal(p1, p2)
 
 
-@pytest.mark.parametrize("comm", ["split", "capture"])
+@pytest.mark.parametrize("comm", ["overlap", "split", "capture"])
 def test_graphed_data_parallel_step_on_one_rank_rccl(comm):
-    """A reducer on a real 1-rank RCCL group: the split schedule (eager bucket all-reduces between the forward/backward
-    graph and the optimizer graph) and the captured schedule (RCCL all-reduces inside the graph) both give the eager
-    data-parallel step's parameters."""
+    """A reducer on a real 1-rank RCCL group: the overlap schedule (backward graph cut at the bucket boundaries, each
+    bucket's all-reduce launched between the segment replays), the split schedule (eager bucket all-reduces between
+    the forward/backward graph and the optimizer graph) and the captured schedule (RCCL all-reduces inside the graph)
+    all give the eager data-parallel step's parameters."""
     from distributed_llms_example_amd.train.graph import GraphedStep
     ga, steps = 2, 3
     with _one_rank_rccl():
@@ -144,6 +145,10 @@ def test_graphed_data_parallel_step_on_one_rank_rccl(comm):
         assert eng_g.reducer is not None and eng_g.reducer.dp and len(eng_g.reducer.buckets) >= 2
         data = _batches(cfg, ga * (steps + 2))
         gs = GraphedStep(eng_g, data[:ga], warmup=2, comm=comm)
+        if comm == "overlap":
+            sch = gs.schedule()
+            nb = len(eng_g.reducer.buckets)
+            assert sch["segments"] >= 2 and sch["buckets_launched_before_backward_end"] >= nb - 1, sch
         losses_g = [float(gs.replay(data[ga * (2 + i):ga * (3 + i)])) for i in range(steps)]
         pg = eng_g.flat.to_canonical(eng_g.flat.param_buf).float().clone()
         eng_g.disable_step_seeds()

@@ -404,3 +404,37 @@ def test_step_runner_schedule_matches_eager_steps(monkeypatch):
     eng_e.disable_step_seeds()
     assert lr_run == pytest.approx(le, rel=1e-6, abs=1e-7)
     assert torch.allclose(p_run, eng_e.flat.param_buf, rtol=1e-5, atol=1e-7)
+
+
+def test_accelerator_train_step_clip_applies_to_the_next_step_only():
+    """make_train_step keeps the eager meaning of clip_grad_norm_: a clip requested before a step applies
+    to that step only, exactly like the explicit loop backward + PreparedOptimizer.step."""
+    from distributed_llms_example_amd.models import build_model
+    from distributed_llms_example_amd.train.accelerator import Accelerator
+
+    g = torch.Generator().manual_seed(3)
+    batches = [{"input_ids": torch.randint(3, 500, (2, 12), generator=g), "attention_mask": torch.ones(2, 12, dtype=torch.long),
+                "labels": torch.randint(3, 500, (2, 6), generator=g)} for _ in range(3)]
+    clips = [0.01, None, 0.02]
+
+    def run(fused_step: bool):
+        acc = Accelerator(cpu=True)
+        torch.manual_seed(0)
+        model = build_model("t5-tiny")
+        opt = torch.optim.AdamW(model.parameters(), lr=1e-2, weight_decay=0.0)
+        model, opt = acc.prepare(model, opt)
+        model.train(False)
+        step = acc.make_train_step(model, opt) if fused_step else None
+        for b, c in zip(batches, clips):
+            if c is not None:
+                acc.clip_grad_norm_(model.parameters(), c)
+            if fused_step:
+                step(b)
+            else:
+                acc.backward(model(**b).loss)
+                opt.step()
+                opt.zero_grad()
+        return torch.cat([p.detach().reshape(-1).float() for p in model.parameters()])
+
+    a, b = run(True), run(False)
+    torch.testing.assert_close(a, b, rtol=0, atol=0)

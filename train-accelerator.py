@@ -41,7 +41,8 @@ class ModelTrainer:
         self.args = args
         mp = None if args.precision is None else ("bf16" if args.precision == "bf16" else "no")
         self.accelerator = Accelerator(mixed_precision=mp, bucket_mb=args.bucket_mb or 128.0,
-                                       overlap_comm=not args.no_overlap, seed=args.seed)
+                                       overlap_comm=not args.no_overlap, seed=args.seed,
+                                       grad_reduce_dtype=args.grad_reduce_dtype)
         self.device = self.accelerator.device
         setup_logging(self.accelerator.is_local_main_process)
         self.logger = get_logger("train-accelerator")

@@ -82,7 +82,8 @@ def run(env, args):
     dtype = torch.bfloat16 if (args.precision or ("bf16" if env.device.type == "cuda" else "fp32")) == "bf16" \
         else torch.float32
     eng = TrainEngine(model, env, lr=args.learning_rate, weight_decay=0.0, max_grad_norm=None, dtype=dtype,
-                      bucket_mb=args.bucket_mb or 128.0, overlap=not args.no_overlap, no_decay=None)
+                      bucket_mb=args.bucket_mb or 128.0, overlap=not args.no_overlap, no_decay=None,
+                      grad_reduce_dtype=args.grad_reduce_dtype)
     collator = DataCollatorForSeq2Seq.for_model(cfg, pad_to_multiple_of=8)
     # partition_dataset (ref/train-task.py:176-191)
     world = env.world_size

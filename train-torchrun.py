@@ -59,7 +59,7 @@ def run(args):
         save_steps=args.save_steps or 1e6, gradient_accumulation_steps=args.grad_accum or 16, ddp_find_unused_parameters=False,
         learning_rate=args.learning_rate, max_steps=args.max_steps, seed=args.seed,
         bf16=None if args.precision is None else args.precision == "bf16",
-        ddp_bucket_cap_mb=args.bucket_mb, overlap_comm=not args.no_overlap,
+        ddp_bucket_cap_mb=args.bucket_mb, overlap_comm=not args.no_overlap, grad_reduce_dtype=args.grad_reduce_dtype,
         context_parallel_size=args.context_parallel,
         coalesce_grad_accum=getattr(args, "coalesce_grad_accum", "auto"))
     trainer = Trainer(model=model, args=targs, tokenizer=tok, data_collator=DataCollatorForSeq2Seq.for_model(cfg),
