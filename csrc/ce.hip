@@ -10,34 +10,86 @@ using namespace dllm;
 
 namespace {
 
-template <typename T, bool VEC>
+// Rows of any length V: row r starts at logits + r * V, 16-B aligned only when V is a multiple of 16 / sizeof(T)
+// (BART's V = 50265 is odd).  Each row is walked as a scalar head up to the first 16-B boundary, 16-B vectors (8 bf16
+// or 4 fp32 per thread and step: one global_load_dwordx4), and a scalar tail — every row at the vector rate whatever
+// its alignment (an odd V with element-wise loads ran at 1.5-2.3 TB/s on bart-large 1024/1024, r5 profile).
+template <typename T>
+DLLM_DEVICE int row_head(const T* p, int V) {
+  const int mis = (int)(reinterpret_cast<uintptr_t>(p) & 15);
+  return min(V, ((16 - mis) & 15) / (int)sizeof(T));
+}
+
+template <typename T>
+struct Vec16 {
+  static constexpr int N = 16 / (int)sizeof(T);
+  DLLM_DEVICE static void load(const T* p, float (&v)[16 / sizeof(T)]) {
+    if constexpr (sizeof(T) == 2) {
+      const u16x8 u = *reinterpret_cast<const u16x8*>(p);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = bf2f(u[k]);
+    } else {
+      const f32x4 u = *reinterpret_cast<const f32x4*>(p);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = u[k];
+    }
+  }
+  DLLM_DEVICE static void store(T* p, const float (&v)[16 / sizeof(T)]) {
+    if constexpr (sizeof(T) == 2) {
+      u16x8 u;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) u[k] = f2bf(v[k]);
+      *reinterpret_cast<u16x8*>(p) = u;
+    } else {
+      *reinterpret_cast<f32x4*>(p) = f32x4{v[0], v[1], v[2], v[3]};
+    }
+  }
+};
+
+template <typename T>
 __global__ __launch_bounds__(256) void ce_fwd_kernel(const T* __restrict__ logits, const int64_t* __restrict__ labels,
                                                      const float* __restrict__ bias, float* __restrict__ loss_out,
                                                      float* __restrict__ lse_out, int V, float eps, long ignore) {
   __shared__ float red[4];
+  constexpr int E = Vec16<T>::N;
   const long row = blockIdx.x;
   const T* x = logits + row * (long)V;
   float m = -INFINITY, s = 0.f, sx = 0.f;
-  if (VEC) {
-    for (int c = threadIdx.x * 4; c < V; c += 256 * 4) {
-      f32x4 v = Elem<T>::load4(x + c);
-      if (bias != nullptr) v += *reinterpret_cast<const f32x4*>(bias + c);
-      const float lm = fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w));
-      const float nm = fmaxf(m, lm);
-      s = s * __expf(m - nm) + __expf(v.x - nm) + __expf(v.y - nm) + __expf(v.z - nm) + __expf(v.w - nm);
+  auto add1 = [&](float v) {
+    const float nm = fmaxf(m, v);
+    if (nm != -INFINITY) {
+      s = (m == -INFINITY ? 0.f : s * __expf(m - nm)) + __expf(v - nm);
       m = nm;
-      sx += v.x + v.y + v.z + v.w;
     }
-  } else {
-    for (int c = threadIdx.x; c < V; c += 256) {
-      float v = Elem<T>::load(x + c);
-      if (bias != nullptr) v += bias[c];
-      const float nm = fmaxf(m, v);
-      s = s * __expf(m - nm) + __expf(v - nm);
+    sx += v;
+  };
+  const int head = row_head(x, V);
+  const int nvec = (V - head) / E;
+  const int body_end = head + nvec * E;
+  if ((int)threadIdx.x < head) add1(Elem<T>::load(x + threadIdx.x) + (bias != nullptr ? bias[threadIdx.x] : 0.f));
+  for (int c = head + (int)threadIdx.x * E; c < body_end; c += 256 * E) {
+    float v[E];
+    Vec16<T>::load(x + c, v);
+    if (bias != nullptr) {
+#pragma unroll
+      for (int k = 0; k < E; ++k) v[k] += bias[c + k];
+    }
+    float lm = v[0];
+#pragma unroll
+    for (int k = 1; k < E; ++k) lm = fmaxf(lm, v[k]);
+    const float nm = fmaxf(m, lm);
+    if (nm != -INFINITY) {
+      float e = 0.f;
+#pragma unroll
+      for (int k = 0; k < E; ++k) e += __expf(v[k] - nm);
+      s = (m == -INFINITY ? 0.f : s * __expf(m - nm)) + e;
       m = nm;
-      sx += v;
     }
+#pragma unroll
+    for (int k = 0; k < E; ++k) sx += v[k];
   }
+  for (int c = body_end + (int)threadIdx.x; c < V; c += 256)
+    add1(Elem<T>::load(x + c) + (bias != nullptr ? bias[c] : 0.f));
   const float M = block_max<256>(m, red);
   const float scaled = (m == -INFINITY) ? 0.f : s * __expf(m - M);
   const float S = block_sum<256>(scaled, red);
@@ -56,11 +108,12 @@ __global__ __launch_bounds__(256) void ce_fwd_kernel(const T* __restrict__ logit
   }
 }
 
-template <typename T, bool VEC>
+template <typename T>
 __global__ __launch_bounds__(256) void ce_bwd_kernel(const float* __restrict__ scale, const T* __restrict__ logits,
                                                      const int64_t* __restrict__ labels,
                                                      const float* __restrict__ lse_in, const float* __restrict__ bias,
                                                      T* __restrict__ dlogits, int V, float eps, long ignore) {
+  constexpr int E = Vec16<T>::N;
   const long row = blockIdx.x;
   const T* x = logits + row * (long)V;
   T* dx = dlogits + row * (long)V;
@@ -70,22 +123,29 @@ __global__ __launch_bounds__(256) void ce_bwd_kernel(const float* __restrict__ s
   const float lse = lse_in[row];
   const float off = eps / (float)V;
   const float hit = 1.f - eps;
-  if (VEC) {
-    for (int c = threadIdx.x * 4; c < V; c += 256 * 4) {
-      f32x4 v = Elem<T>::load4(x + c);
-      if (bias != nullptr) v += *reinterpret_cast<const f32x4*>(bias + c);
-      f32x4 r;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) r[k] = g * (__expf(v[k] - lse) - off - ((c + k) == y ? hit : 0.f));
-      Elem<T>::store4(dx + c, r);
-    }
-  } else {
-    for (int c = threadIdx.x; c < V; c += 256) {
-      float v = Elem<T>::load(x + c);
-      if (bias != nullptr) v += bias[c];
-      Elem<T>::store(dx + c, g * (__expf(v - lse) - off - (c == y ? hit : 0.f)));
-    }
+  auto one = [&](int c) {
+    const float v = Elem<T>::load(x + c) + (bias != nullptr ? bias[c] : 0.f);
+    Elem<T>::store(dx + c, g * (__expf(v - lse) - off - (c == y ? hit : 0.f)));
+  };
+  // vector body only when input and output rows share their 16-B phase (in place, or equally aligned buffers)
+  if (((reinterpret_cast<uintptr_t>(x) ^ reinterpret_cast<uintptr_t>(dx)) & 15) != 0) {
+    for (int c = threadIdx.x; c < V; c += 256) one(c);
+    return;
   }
+  const int head = row_head(x, V);
+  const int body_end = head + ((V - head) / E) * E;
+  if ((int)threadIdx.x < head) one(threadIdx.x);
+  for (int c = head + (int)threadIdx.x * E; c < body_end; c += 256 * E) {
+    float v[E];
+    Vec16<T>::load(x + c, v);
+#pragma unroll
+    for (int k = 0; k < E; ++k) {
+      const float b = bias != nullptr ? bias[c + k] : 0.f;
+      v[k] = g * (__expf(v[k] + b - lse) - off - ((c + k) == y ? hit : 0.f));
+    }
+    Vec16<T>::store(dx + c, v);
+  }
+  for (int c = body_end + (int)threadIdx.x; c < V; c += 256) one(c);
 }
 
 // bias[c0 + c .. + 3]: one 16-B load when that address is 16-B aligned, else four scalar loads (the ragged vocab tail
@@ -232,12 +292,12 @@ extern "C" int dllm_ce_chunk_bwd(const float* scale, void* logits, long ld, cons
 
 extern "C" int dllm_ce_fwd(const void* logits, const int64_t* labels, const float* bias, float* loss, float* lse,
                            long N, int V, float eps, long ignore, int is_bf16, hipStream_t st) {
-  const bool vec = (V % 4) == 0;
   dim3 g(N), b(256);
-#define L(T, VE) hipLaunchKernelGGL((ce_fwd_kernel<T, VE>), g, b, 0, st, (const T*)logits, labels, bias, loss, lse, V, eps, ignore)
-  if (is_bf16) { if (vec) L(uint16_t, true); else L(uint16_t, false); }
-  else { if (vec) L(float, true); else L(float, false); }
-#undef L
+  if (is_bf16)
+    hipLaunchKernelGGL((ce_fwd_kernel<uint16_t>), g, b, 0, st, (const uint16_t*)logits, labels, bias, loss, lse, V, eps,
+                       ignore);
+  else
+    hipLaunchKernelGGL((ce_fwd_kernel<float>), g, b, 0, st, (const float*)logits, labels, bias, loss, lse, V, eps, ignore);
   DLLM_CHECK_LAUNCH();
   return 0;
 }
@@ -245,12 +305,13 @@ extern "C" int dllm_ce_fwd(const void* logits, const int64_t* labels, const floa
 extern "C" int dllm_ce_bwd(const float* scale, const void* logits, const int64_t* labels, const float* lse,
                            const float* bias, void* dlogits, long N, int V, float eps, long ignore, int is_bf16,
                            hipStream_t st) {
-  const bool vec = (V % 4) == 0;
   dim3 g(N), b(256);
-#define L(T, VE) hipLaunchKernelGGL((ce_bwd_kernel<T, VE>), g, b, 0, st, scale, (const T*)logits, labels, lse, bias, (T*)dlogits, V, eps, ignore)
-  if (is_bf16) { if (vec) L(uint16_t, true); else L(uint16_t, false); }
-  else { if (vec) L(float, true); else L(float, false); }
-#undef L
+  if (is_bf16)
+    hipLaunchKernelGGL((ce_bwd_kernel<uint16_t>), g, b, 0, st, scale, (const uint16_t*)logits, labels, lse, bias,
+                       (uint16_t*)dlogits, V, eps, ignore);
+  else
+    hipLaunchKernelGGL((ce_bwd_kernel<float>), g, b, 0, st, scale, (const float*)logits, labels, lse, bias,
+                       (float*)dlogits, V, eps, ignore);
   DLLM_CHECK_LAUNCH();
   return 0;
 }

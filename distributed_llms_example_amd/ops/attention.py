@@ -29,6 +29,7 @@ import os
 import torch
 
 from .. import _ext
+from . import streams
 from .rng import attention_keep_mask
 
 # --------------------------------------------------------------------------- T5 relative bias
@@ -187,6 +188,7 @@ class _AttnFn(torch.autograd.Function):
                                           float(p), int(seed), bool(need_dlut), dq, dk, dv, dmask, sat_lo, sat_hi)
         if mode == "sep":
             da, db, dc = rq, rk, rv
+        streams.pair_join()  # side-stream weight gradients paired with these VALU-bound kernels (ops/streams.py)
         return None, da, db, dc, (dlut if need_dlut else None), None, None, None, None, None, None
 
 

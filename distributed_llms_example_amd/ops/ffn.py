@@ -38,6 +38,7 @@ import torch.nn.functional as F
 
 from .. import _ext
 from .activations import act_dropout
+from . import streams
 from .gemm import bias_grad_accumulate, linear_dgrad, linear_fwd, wgrad_accumulate
 from .linear import _RES_GEMM, _fire, _fusable, _gbuf, _use
 
@@ -131,9 +132,9 @@ class _FusedFFNFn(torch.autograd.Function):
         else:
             du = C.gemm_fused(dy2, wo, True, ebwd, None, h if ebwd == 3 else u, None, p, seed, _VARIANT, None, bsum)
         with torch.no_grad():
-            wgrad_accumulate(_gbuf(Wo), dy2, h)
+            wgrad_accumulate(_gbuf(Wo), dy2, h, async_ok=streams.site_ok(Wo))
             if Bo is not None:
-                bias_grad_accumulate(_gbuf(Bo), dy2, dy)
+                bias_grad_accumulate(_gbuf(Bo), dy2, dy, async_ok=streams.site_ok(Bo))
         _fire(Wo)
         if Bo is not None:
             _fire(Bo)
@@ -146,12 +147,12 @@ class _FusedFFNFn(torch.autograd.Function):
                 if dres is not None:
                     dx = dx + dres.reshape(dx.shape)
         with torch.no_grad():
-            wgrad_accumulate(_gbuf(Wi), du, x2)
+            wgrad_accumulate(_gbuf(Wi), du, x2, async_ok=streams.site_ok(Wi))
             if bsum is not None:
                 gb = _gbuf(Bi)
                 gb.add_(bsum.sum(0).to(gb.dtype))
             elif Bi is not None:
-                bias_grad_accumulate(_gbuf(Bi), du)
+                bias_grad_accumulate(_gbuf(Bi), du, async_ok=streams.site_ok(Bi))
         _fire(Wi)
         if Bi is not None:
             _fire(Bi)
@@ -200,11 +201,11 @@ class _FusedGatedFFNFn(torch.autograd.Function):
             dy2 = dy2.contiguous()
         du = C.gemm_dgeglu(dy2, Wo.detach(), g1, g2)
         with torch.no_grad():
-            wgrad_accumulate(_gbuf(Wo), dy2, h)
+            wgrad_accumulate(_gbuf(Wo), dy2, h, async_ok=streams.site_ok(Wo))
         _fire(Wo)
         dx = linear_dgrad(du, Wi.detach()) if ctx.needs_input_grad[0] else None
         with torch.no_grad():
-            wgrad_accumulate(_gbuf(Wi), du, x2)
+            wgrad_accumulate(_gbuf(Wi), du, x2, async_ok=streams.site_ok(Wi))
         _fire(Wi)
         return (None if dx is None else dx.view(ctx.shape)), None, None, None, None, None
 

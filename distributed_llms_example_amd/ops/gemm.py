@@ -124,7 +124,8 @@ def _wgrad(out, dy2, x2, beta):
 
 
 @torch.no_grad()
-def bias_grad_accumulate(out: torch.Tensor, dy2: torch.Tensor, dy: torch.Tensor | None = None) -> torch.Tensor:
+def bias_grad_accumulate(out: torch.Tensor, dy2: torch.Tensor, dy: torch.Tensor | None = None,
+                         async_ok: bool = True) -> torch.Tensor:
     """``out += dy2.sum(0)`` (bias gradient of a linear layer, accumulated in place).  ``dy``: the gradient tensor as
     autograd delivered it; when its producer already summed it over tokens (ops/norms.py x_bias_grad: the BART
     post-LN backward kernel) that fp32 column sum is added instead of re-reading dy."""
@@ -136,7 +137,11 @@ def bias_grad_accumulate(out: torch.Tensor, dy2: torch.Tensor, dy: torch.Tensor 
         # in-place accumulation of another consumer's gradient bumps the version and the sum no longer describes dy)
         if (cs.numel() == out.numel() and dy._version == ver and tuple(dy.shape) == shape and dy.data_ptr() == ptr):
             colsum_handoffs += 1
+            if not async_ok:
+                return out.add_(cs.view_as(out).to(out.dtype))
             return streams.run(lambda: out.add_(cs.view_as(out).to(out.dtype)), cs)
+    if not async_ok:
+        return _colsum(out, dy2)
     return streams.run(lambda: _colsum(out, dy2), dy2)
 
 

@@ -20,6 +20,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from . import streams
 from .gemm import bias_grad_accumulate, linear_dgrad, linear_fwd, wgrad_accumulate
 
 
@@ -84,9 +85,9 @@ class _LinearAccumFn(torch.autograd.Function):
         dy2 = dy.reshape(-1, dy.shape[-1])
         x2 = x.reshape(-1, x.shape[-1])
         with torch.no_grad():
-            wgrad_accumulate(_gbuf(w), dy2, x2, async_ok=_sole_writer(w))
+            wgrad_accumulate(_gbuf(w), dy2, x2, async_ok=_sole_writer(w) and streams.site_ok(w))
             if bias is not None:
-                bias_grad_accumulate(_gbuf(bias), dy2, dy)
+                bias_grad_accumulate(_gbuf(bias), dy2, dy, async_ok=streams.site_ok(bias))
         _fire(w)
         if bias is not None:
             _fire(bias)
@@ -125,9 +126,9 @@ class _LinearResFn(torch.autograd.Function):
                     dx = dx + dres
         x2 = x.reshape(-1, x.shape[-1])
         with torch.no_grad():
-            wgrad_accumulate(_gbuf(w), dy2, x2, async_ok=_sole_writer(w))
+            wgrad_accumulate(_gbuf(w), dy2, x2, async_ok=_sole_writer(w) and streams.site_ok(w))
             if bias is not None:
-                bias_grad_accumulate(_gbuf(bias), dy2)
+                bias_grad_accumulate(_gbuf(bias), dy2, async_ok=streams.site_ok(bias))
         _fire(w)
         if bias is not None:
             _fire(bias)

@@ -15,6 +15,7 @@ from __future__ import annotations
 import torch
 
 from .. import _ext
+from . import streams
 from .linear import _fire, _fusable, _gbuf, _use
 from .rng import keep_mask
 
@@ -80,6 +81,7 @@ class _NormFn(torch.autograd.Function):
         dres = None
         if has_resid:
             dres = dstream.view(shape) if want_stream else dx
+        streams.pair_join()  # side-stream weight gradients paired with this memory-bound kernel (ops/streams.py)
         return (dx, dres) + _param_grads(ctx.params, weight, bias, dw, db) + (None, None, None, None, None, None)
 
 
@@ -106,6 +108,7 @@ class _NormOnlyFn(torch.autograd.Function):
         kind, shape = ctx.cfg
         dx, _, dw, db, _ = C.norm_bwd(dout.reshape(-1, shape[-1]), None, x2, weight, bias, mean, rstd, 0.0, 0,
                                       int(kind), False, *_acc_targets(ctx.params))
+        streams.pair_join()
         return (dx.view(shape),) + _param_grads(ctx.params, weight, bias, dw, db) + (None, None, None)
 
 

@@ -16,7 +16,14 @@ Ordering and memory, without ``record_stream``:
 * join: the end of the backward (``scope`` exit, engine.forward_backward) joins the side stream into the compute stream,
   before the gradient all-reduce and the optimizer read the gradients.
 
-All three are stream waits, so a HIP-graph capture records them as graph edges (train/graph.py).  Not used when a
+All three are stream waits, so a HIP-graph capture records them as graph edges (train/graph.py).
+
+Paired mode (``DLLM_WGRAD_STREAM_SITES=qkv,wi,...``, the layer roles of the parameters: the name of the module that
+owns the weight, e.g. T5 ``qkv`` / ``o`` / ``wi`` / ``wo``, BART ``qkv_proj`` / ``out_proj`` / ``fc1`` / ``fc2``): only
+those layers' weight gradients go to the side stream, at any micro-batch size, and instead of the lagged joins the
+compute stream joins at the end of the NEXT memory- or VALU-bound backward op (``pair_join``: the norm backward,
+the attention backward) — so a weight-gradient GEMM (MFMA-bound) runs beside a kernel that leaves the matrix cores
+idle, never beside another GEMM (the all-sites mode's loss at large batch).  Not used when a
 gradient reducer launches bucket all-reduces from the autograd hooks during the backward (those order themselves
 after the compute stream only), nor for gradients another compute-stream kernel also accumulates into (the tied
 embedding's LM-head slice: ops/lm_head.py keeps those synchronous).  Used for small micro-batches only
@@ -31,6 +38,8 @@ import os
 import torch
 
 LAG = max(1, int(os.environ.get("DLLM_WGRAD_STREAM_LAG", "2")))
+_SITES_ENV = os.environ.get("DLLM_WGRAD_STREAM_SITES")
+SITES = frozenset(s for s in (_SITES_ENV or "").split(",") if s) if _SITES_ENV is not None else None
 _on = [False]
 _side: dict = {}
 _used: set = set()  # devices whose side stream has work since the last join
@@ -46,6 +55,8 @@ def default_enabled(tokens: int | None = None) -> bool:
     mode = os.environ.get("DLLM_WGRAD_STREAM", "auto")
     if mode == "0":
         return False
+    if SITES is not None:
+        return bool(SITES)
     if mode == "1" or tokens is None:
         return True
     return tokens <= int(os.environ.get("DLLM_WGRAD_STREAM_MAX_TOKENS", "32768"))
@@ -56,6 +67,26 @@ def _side_stream(dev: torch.device) -> torch.cuda.Stream:
     if s is None:
         s = _side[dev] = torch.cuda.Stream(dev)
     return s
+
+
+def site_ok(p) -> bool:
+    """May the weight gradient of parameter ``p`` go to the side stream?  All of them, unless paired mode names the
+    layer roles (``_dllm_role``: tools set it from the parameter names, train/engine.py tag_roles)."""
+    return SITES is None or getattr(p, "_dllm_role", None) in SITES
+
+
+def pair_join() -> None:
+    """Paired mode: the end of a backward op that side-stream weight gradients were paired with."""
+    if SITES is not None and _used:
+        join()
+
+
+def tag_roles(module: torch.nn.Module) -> None:
+    """``_dllm_role`` of every weight / bias: the name of the module owning it (``qkv``, ``wi``, ``fc1`` ...)."""
+    for name, p in module.named_parameters():
+        parts = name.split(".")
+        if len(parts) >= 2:
+            p._dllm_role = parts[-2]
 
 
 def run(fn, *refs):
@@ -75,7 +106,7 @@ def run(fn, *refs):
     ev.record(side)
     _pending.append((ev, refs, dev))
     launches += 1
-    while len(_pending) > LAG:
+    while SITES is None and len(_pending) > LAG:
         e, _, d = _pending.popleft()
         torch.cuda.current_stream(d).wait_event(e)
     return r

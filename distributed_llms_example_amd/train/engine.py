@@ -54,6 +54,7 @@ class TrainEngine:
         self.model = model.to(device=env.device, dtype=dtype)
         self.dtype = dtype
         self.flat = FlatParams(self.model, grad_dtype=grad_dtype or default_grad_dtype(dtype))
+        streams.tag_roles(self.model)  # layer roles for the paired side-stream policy (ops/streams.py)
         # force_reducer: a reducer (and its collectives) on a 1-rank process group — GPU tests of the RCCL paths
         self.reducer = (GradReducer(self.flat, bucket_mb=bucket_mb, overlap=overlap, force=force_reducer,
                                     wire_dtype=wire_dtype_of(grad_reduce_dtype))

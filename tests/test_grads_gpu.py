@@ -324,11 +324,14 @@ def test_t5_fused_lm_head_matches_materialised_logits(monkeypatch):
 
 
 @pytest.mark.parametrize("graphed", [False, True])
-def test_side_stream_wgrad_matches_single_stream(graphed, monkeypatch):
+@pytest.mark.parametrize("sites", [None, "qkv,wi,o"])
+def test_side_stream_wgrad_matches_single_stream(graphed, sites, monkeypatch):
     """Weight gradients on the side stream (ops/streams.py) == all on the compute stream: same flat gradient (the
     kernels are deterministic and the accumulation order is unchanged), eager and inside a captured HIP graph; the side
-    path really ran."""
+    path really ran.  ``sites``: the paired mode (only those layers' weight gradients, joined at the next norm /
+    attention backward)."""
     from distributed_llms_example_amd.ops import streams
+    monkeypatch.setattr(streams, "SITES", frozenset(sites.split(",")) if sites else None)
     cfg = _small_cfg().replace(dropout_rate=0.0)
     torch.manual_seed(0)
     sd = build_model(cfg).state_dict()

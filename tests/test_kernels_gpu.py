@@ -95,12 +95,16 @@ def test_dropout_standalone():
     _close(x.grad, keep_mask(99, 0.25, x.shape, x.device).float() / 0.75, 1e-2, 1e-2)
 
 
-@pytest.mark.parametrize("V", [32128, 50264, 50265, 1000])
+@pytest.mark.parametrize("V,dtype", [(32128, torch.bfloat16), (50264, torch.bfloat16), (50265, torch.bfloat16),
+                                     (1000, torch.bfloat16), (7, torch.bfloat16), (50265, torch.float32),
+                                     (1001, torch.float32)])
 @pytest.mark.parametrize("smooth,bias", [(0.0, False), (0.1, False), (0.0, True)])
-def test_cross_entropy(V, smooth, bias):
+def test_cross_entropy(V, dtype, smooth, bias):
+    """Every row alignment: odd V puts row r at an odd element offset (scalar head up to the 16-B boundary, vector
+    body, scalar tail); V = 7 is all head."""
     torch.manual_seed(V)
     N = 300
-    logits = (3 * torch.randn(N, V, device=DEV)).to(torch.bfloat16).requires_grad_(True)
+    logits = (3 * torch.randn(N, V, device=DEV)).to(dtype).requires_grad_(True)
     labels = torch.randint(0, V, (N,), device=DEV)
     labels[::7] = -100
     bvec = (0.5 * torch.randn(V, device=DEV)) if bias else None

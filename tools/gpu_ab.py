@@ -11,8 +11,10 @@ Steps, each under its own time limit; the session stops at the first failure (a 
 
 * ``--tests``: ``pytest -m gpu`` over the given selection (one process);
 * ``--bench`` x ``--reps``, interleaved over the arms: ``--arms name=path.so,...`` swaps the in-tree ``_C`` (the
-  loader's ``DLLM_NATIVE_SO``), ``--env-arms name=K=V;K2=V2,...`` sets environment variables; one JSON bench line per
-  run goes to ``<tag>/bench.jsonl`` with the arm name added;
+  loader's ``DLLM_NATIVE_SO``), ``--env-arms name=K=V;K2=V2,...`` sets environment variables, ``--tree-arms
+  name=dir,...`` runs another checkout's bench.py with its own package and library (e.g. the round-start tree built
+  under ab/, tools/regression_gate.sh); one JSON bench line per run goes to ``<tag>/bench.jsonl`` with the arm name
+  added, and a per-config table of median samples/s per arm (delta vs the first arm) closes the session;
 * ``--prof``: ``rocprofv3 --kernel-trace --stats`` over ``bench.py <args>`` (first arm), summarised by
   tools/prof_summary.py (kernel families) and tools/trace_shapes.py (per-dispatch shapes) into ``<tag>/``;
 * ``--cmd``: any extra command (e.g. a microbenchmark), output to ``<tag>/cmd.log``.
@@ -33,29 +35,36 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _run(cmd: list[str], log: str, limit: int, env: dict | None = None) -> int:
+def _run(cmd: list[str], log: str, limit: int, env: dict | None = None, cwd: str = ROOT) -> int:
     """One GPU step under its own limit (timeout -k 10), output to ``log``; progress line on stdout."""
     t0 = time.time()
     with open(log, "w") as f:
         rc = subprocess.run(["timeout", "-k", "10", str(limit)] + cmd, stdout=f, stderr=subprocess.STDOUT,
-                            env=env, cwd=ROOT).returncode
+                            env=env, cwd=cwd).returncode
     print(f"[gpu_ab] rc={rc} {time.time() - t0:7.1f}s  {' '.join(cmd)[:160]}", flush=True)
     return rc
 
 
-def _arms(a) -> list[tuple[str, dict]]:
+def _arms(a) -> list[tuple[str, dict, str]]:
+    """(name, environment additions, working tree) per arm."""
     arms = []
+    for spec in filter(None, (a.tree_arms or "").split(",")):
+        name, path = spec.split("=", 1)
+        tree = path if os.path.isabs(path) else os.path.join(ROOT, path)
+        if not os.path.exists(os.path.join(tree, "bench.py")):
+            raise SystemExit(f"[gpu_ab] tree arm {name}: no bench.py under {tree}")
+        arms.append((name, {}, tree))
     for spec in filter(None, (a.arms or "").split(",")):
         name, path = spec.split("=", 1)
         hits = glob.glob(os.path.join(ROOT, path)) if not os.path.isabs(path) else glob.glob(path)
         if not hits:
             raise SystemExit(f"[gpu_ab] arm {name}: no file matches {path}")
-        arms.append((name, {"DLLM_NATIVE_SO": hits[0]}))
+        arms.append((name, {"DLLM_NATIVE_SO": hits[0]}, ROOT))
     for spec in filter(None, (a.env_arms or "").split(",")):
         name, kvs = spec.split("=", 1)
         env = dict(kv.split("=", 1) for kv in filter(None, kvs.split(";")))
-        arms.append((name, env))
-    return arms or [("default", {})]
+        arms.append((name, env, ROOT))
+    return arms or [("default", {}, ROOT)]
 
 
 def main() -> int:
@@ -67,6 +76,7 @@ def main() -> int:
     ap.add_argument("--bench-limit", type=int, default=420)
     ap.add_argument("--arms", default=None, help="name=path.so,... (in-tree _C swapped per run)")
     ap.add_argument("--env-arms", default=None, help="name=K=V;K2=V2,... environment arms")
+    ap.add_argument("--tree-arms", default=None, help="name=dir,... arms that run another checkout's bench.py")
     ap.add_argument("--reps", type=int, default=1)
     ap.add_argument("--prof", action="append", default=[], help="bench.py arguments for a rocprofv3 kernel trace")
     ap.add_argument("--prof-limit", type=int, default=420)
@@ -94,12 +104,13 @@ def main() -> int:
             return rc
 
     lines = open(os.path.join(out, "bench.jsonl"), "a")
+    results: dict = {}
     for rep in range(a.reps):
         for bi, bargs in enumerate(a.bench):
-            for name, env in arms:
+            for name, env, tree in arms:
                 log = os.path.join(out, f"bench_{bi}_{name}_{rep}.log")
                 rc = _run([sys.executable, "-u", "bench.py"] + shlex.split(bargs), log, a.bench_limit,
-                          env=dict(base_env, **env))
+                          env=dict(base_env, **env), cwd=tree)
                 if rc != 0:
                     print("\n".join(open(log).read().splitlines()[-20:]), flush=True)
                     return rc
@@ -109,15 +120,20 @@ def main() -> int:
                     d.update({"arm": name, "rep": rep, "bench_args": bargs})
                     lines.write(json.dumps(d) + "\n")
                     lines.flush()
+                    results.setdefault(bi, {}).setdefault(name, []).append(d["value"])
                     print(f"[gpu_ab] {name:>10s} rep {rep} cfg {bi}: {d['value']:9.2f} {d['unit']}  "
                           f"{d['ms_per_step']:9.3f} ms/step", flush=True)
+
+    if results:
+        _table(results, a.bench, [n for n, _, _ in arms], os.path.join(out, "bench_table.txt"))
 
     for pi, pargs in enumerate(a.prof):
         d = os.path.join(out, f"prof{pi}")
         os.makedirs(d, exist_ok=True)
-        name, env = arms[0]
+        name, env, tree = arms[0]
         rc = _run(["rocprofv3", "--kernel-trace", "--stats", "-d", d, "-o", "run", "--", sys.executable, "bench.py"]
-                  + shlex.split(pargs), os.path.join(out, f"prof{pi}.log"), a.prof_limit, env=dict(base_env, **env))
+                  + shlex.split(pargs), os.path.join(out, f"prof{pi}.log"), a.prof_limit, env=dict(base_env, **env),
+                  cwd=tree)
         if rc != 0:
             print("\n".join(open(os.path.join(out, f"prof{pi}.log")).read().splitlines()[-20:]), flush=True)
             return rc
@@ -133,6 +149,28 @@ def main() -> int:
             for p in dbs:
                 os.remove(p)
     return 0
+
+
+def _table(results: dict, benches: list[str], names: list[str], path: str) -> None:
+    """Median samples/s per (config, arm), and each arm's delta against the first arm."""
+    import statistics
+    rows = [f"{'config':<70s} " + " ".join(f"{n:>16s}" for n in names)]
+    for bi, bargs in enumerate(benches):
+        med = {n: statistics.median(v) for n, v in results.get(bi, {}).items()}
+        base = med.get(names[0])
+        cells = []
+        for n in names:
+            if n not in med:
+                cells.append(f"{'-':>16s}")
+            elif n == names[0] or not base:
+                cells.append(f"{med[n]:>16.2f}")
+            else:
+                cells.append(f"{med[n]:>8.2f} {100 * (med[n] / base - 1):+6.2f}%")
+        rows.append(f"{bargs[:70]:<70s} " + " ".join(cells))
+    txt = "\n".join(rows)
+    with open(path, "w") as f:
+        f.write(txt + "\n")
+    print(txt, flush=True)
 
 
 def _prof_steps(args: str) -> int:

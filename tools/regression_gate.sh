@@ -1,0 +1,21 @@
+#!/bin/bash
+# No-regression gate across BASELINE.json's configs: every config below, interleaved between the
+# round-start tree (arm "base": a checkout of the round's first commit with its own library, built under ab/) and the
+# current tree (arm "cur"), REPS rounds, medians per arm and the delta in gpurun_out/<tag>/bench_table.txt.
+# A config more than 1 % below base is a finding to fix.
+#
+#   git worktree add ab/r4base <round-start commit> && (cd ab/r4base && python tools/build_native.py)
+#   gpurun --timeout 1200 -- bash tools/regression_gate.sh gate [REPS]
+set -o pipefail
+TAG=${1:-gate}
+REPS=${2:-2}
+BASE=${GATE_BASE:-ab/r4base}
+exec_args=(
+  --tag "$TAG" --tree-arms "base=$BASE,cur=." --reps "$REPS" --bench-limit 480
+  --bench "--steps 10 --warmup 3"
+  --bench "--model bart-large --batch-per-gpu 256 --steps 6 --warmup 2"
+  --bench "--model t5-large --batch-per-gpu 32 --steps 6 --warmup 2"
+  --bench "--model flan-t5-xl --batch-per-gpu 16 --steps 5 --warmup 2"
+  --bench "--dtype fp32 --batch-per-gpu 16 --steps 6 --warmup 2"
+)
+python tools/gpu_ab.py "${exec_args[@]}"
