@@ -34,12 +34,13 @@ from __future__ import annotations
 import collections
 import contextlib
 import os
+import re
 
 import torch
 
 LAG = max(1, int(os.environ.get("DLLM_WGRAD_STREAM_LAG", "2")))
 _SITES_ENV = os.environ.get("DLLM_WGRAD_STREAM_SITES")
-SITES = frozenset(s for s in (_SITES_ENV or "").split(",") if s) if _SITES_ENV is not None else None
+SITES = frozenset(s for s in re.split(r"[,+]", _SITES_ENV or "") if s) if _SITES_ENV is not None else None
 _on = [False]
 _side: dict = {}
 _used: set = set()  # devices whose side stream has work since the last join
