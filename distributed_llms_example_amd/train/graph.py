@@ -293,7 +293,14 @@ def batch_signature(batches: list[dict]) -> tuple:
 
 def graphs_enabled(device: torch.device) -> bool:
     """Entry points replay their steps from HIP graphs on GPU unless ``DLLM_GRAPH=0``."""
-    return device.type == "cuda" and os.environ.get("DLLM_GRAPH", "1") != "0"
+    return device.type == "cuda" and os.environ.get("DLLM_GRAPH", "auto") != "0"
+
+
+def graph_policy() -> str:
+    """``DLLM_GRAPH``: ``auto`` (default) = capture, then keep the graph only if its replays are not slower than the
+    eager steps of the same shape (StepRunner's timed probe); ``1`` = always replay; ``0`` = never capture."""
+    v = os.environ.get("DLLM_GRAPH", "auto")
+    return {"0": "off", "1": "on"}.get(v, "auto")
 
 
 class StepRunner:
@@ -303,7 +310,16 @@ class StepRunner:
     Per batch-shape signature: the first ``warmup`` steps run eagerly (real training steps; step seeds are on from
     the first one, so eager and replayed steps draw dropout masks from one stream), the next one is captured and from
     then on every step of that signature is a replay; steps of any other signature run eagerly.  ``enabled=False``
-    (CPU, ``DLLM_GRAPH=0``) is the plain eager step."""
+    (CPU, ``DLLM_GRAPH=0``) is the plain eager step.
+
+    Policy ``auto`` (default, graph_policy): the last eager warm-up steps and the first ``PROBE`` replays of a signature
+    are timed with device events (no host synchronisation until the decision); if the replays' median is slower than
+    the eager steps' median by more than ``GRAPH_TOL``, the graph is dropped and the signature stays eager (at large
+    micro-batches launch overhead is nil and a replay can lose to the eager stream; at small ones the graph wins by
+    tens of percent).  The outcome is ``decision`` (logged by the entry points)."""
+
+    PROBE = 3
+    GRAPH_TOL = 0.003
 
     def __init__(self, engine, enabled: bool | None = None, warmup: int = 2, num_items: bool = False,
                  dp_ranks: int | None = None, comm: str | None = None):
@@ -319,6 +335,12 @@ class StepRunner:
         self._seen = 0
         self.replays = 0
         self.eager_steps = 0
+        # the timed probe needs device events: on the CPU schedule (tests) an enabled runner always replays
+        self.policy = ("off" if not self.enabled else graph_policy() if engine.env.device.type == "cuda" else "on")
+        self.decision: dict | None = None  # auto policy: {"graph": bool, "eager_ms": .., "replay_ms": ..}
+        self._eager_t: list = []   # (start, end) events of this signature's eager steps
+        self._replay_t: list = []  # ... and of its first replays
+        self._eager_sigs: set = set()  # signatures the probe sent back to eager steps
         if self.enabled:
             engine.enable_step_seeds()
 
@@ -336,14 +358,25 @@ class StepRunner:
         eng = self.eng
         if lr is not None:
             eng.optimizer.param_groups[0]["lr"] = lr
+        timed = None
         if self.enabled:
             sig = batch_signature(passes)
             g = self.graph
             if g is not None and sig == g.signature():
+                probing = self.policy == "auto" and self.decision is None
+                if probing and len(self._replay_t) >= self.PROBE:
+                    self._decide()
+                    if self.graph is None:
+                        return self(passes, num_items=num_items)
+                    probing = False
+                ev = self._events() if probing else None
                 g.replay(passes, num_items=num_items)
+                if ev is not None:
+                    ev[1].record()
+                    self._replay_t.append(ev)
                 self.replays += 1
                 return list(g.losses), g.norm
-            if g is None and self.graph_error is None:
+            if g is None and self.graph_error is None and sig not in self._eager_sigs:
                 self._seen = self._seen + 1 if sig == self._sig else 1
                 self._sig = sig
                 if self._seen > self.warmup:
@@ -362,9 +395,37 @@ class StepRunner:
                         torch.cuda.synchronize()
                     else:
                         return self(passes, num_items=num_items)
+            # the eager steps of the signature that will be captured are the probe's baseline (not the first one: it
+            # carries the lazy initialisation)
+            if self.policy == "auto" and self.decision is None and sig == self._sig and self._seen >= 2:
+                timed = self._events()
         self.eager_steps += 1
         losses = []
         for j, pb in enumerate(passes):
             losses.append(eng.forward_backward(pb, grad_accum=len(passes), sync=j + 1 == len(passes),
                                                num_items=num_items, dp_ranks=self.dp_ranks))
-        return losses, eng.step()
+        norm = eng.step()
+        if timed is not None:
+            timed[1].record()
+            self._eager_t.append(timed)
+        return losses, norm
+
+    @staticmethod
+    def _events():
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        return e0, e1
+
+    def _decide(self):
+        """Auto policy: keep the graph iff its replays are not slower than the eager steps (medians)."""
+        import statistics
+        self._replay_t[-1][1].synchronize()
+        med = lambda evs: statistics.median(a.elapsed_time(b) for a, b in evs)  # noqa: E731
+        eager = med(self._eager_t[-2:]) if self._eager_t else float("inf")
+        replay = med(self._replay_t)
+        keep = replay <= eager * (1.0 + self.GRAPH_TOL)
+        self.decision = {"graph": keep, "eager_ms": round(eager, 3), "replay_ms": round(replay, 3)}
+        if not keep:
+            self._eager_sigs.add(self.graph.signature())
+            self.graph = None
+        self._eager_t, self._replay_t = [], []

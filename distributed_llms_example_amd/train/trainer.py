@@ -402,6 +402,8 @@ class Trainer:
         if self._batch_shape is not None:  # what the throughput was measured on: per-GPU micro-batch, padded lengths
             metrics["batch_shape"] = self._batch_shape
             metrics["hip_graph_replays"] = self.step_runner.replays
+            if self.step_runner.decision is not None:  # auto policy's probe: graph kept iff not slower than eager
+                metrics["hip_graph_decision"] = self.step_runner.decision
         self.log(metrics)
         self.handler.fire("on_train_end", args, self.state, self.control)
         return TrainOutput(self.state.global_step, train_loss, metrics)

@@ -156,3 +156,38 @@ def test_graphed_data_parallel_step_on_one_rank_rccl(comm):
         losses_e, pe = _eager_reference(cfg, data, ga, steps, force_reducer=True)
     assert losses_g == pytest.approx(losses_e, rel=1e-3), (losses_g, losses_e)
     assert ((pg - pe).norm() / pe.norm()).item() < 1e-3
+
+
+@pytest.mark.parametrize("tol,keep", [(10.0, True), (-0.99, False)])
+def test_step_runner_auto_policy(tol, keep, monkeypatch):
+    """DLLM_GRAPH=auto (the entry points' default): eager warm-up steps and the first replays are timed; the graph is
+    kept only if its replays are not slower than the eager steps.  Forced both ways through the tolerance, the runner
+    must record the decision, keep replaying or fall back to eager steps, and give the same parameters as eager steps
+    with the same dropout stream either way."""
+    from distributed_llms_example_amd.train.graph import StepRunner
+    monkeypatch.setenv("DLLM_GRAPH", "auto")
+    monkeypatch.setattr(StepRunner, "GRAPH_TOL", tol)
+    steps = 8
+    cfg, eng = _setup()
+    data = _batches(cfg, steps)
+    runner = StepRunner(eng, enabled=True, warmup=2)
+    assert runner.policy == "auto"
+    for b in data:
+        runner([b])
+    torch.cuda.synchronize()
+    assert runner.decision is not None and runner.decision["graph"] is keep, runner.decision
+    assert runner.decision["eager_ms"] > 0 and runner.decision["replay_ms"] > 0
+    # capture step + probe replays, then either replays to the end or eager steps
+    assert runner.replays == (steps - 2 if keep else StepRunner.PROBE)
+    p_auto = eng.flat.to_canonical(eng.flat.param_buf).float().clone()
+    eng.disable_step_seeds()
+    cfg, ref = _setup()
+    ref.enable_step_seeds()
+    t = torch.zeros((), device="cuda")
+    for b in data:
+        ref.forward_backward(b)
+        t.add_(1.0)
+        ref.step(hyper=ref.optimizer.device_hyper(t, ref.optimizer.param_groups[0]["lr"]))
+    p_ref = ref.flat.to_canonical(ref.flat.param_buf).float()
+    ref.disable_step_seeds()
+    assert ((p_auto - p_ref).norm() / p_ref.norm()).item() < 1e-3

@@ -112,6 +112,8 @@ class ModelTrainer:
             tp = {"train_samples_per_second": round(per_step * completed / (t1 - t0), 3), "epoch": epoch,
                   "batch_shape": [a.batch_size] + (shape or []),  # per-GPU batch, padded source / target tokens
                   "hip_graph_replays": train_step.runner.replays}
+            if train_step.runner.decision is not None:
+                tp["hip_graph_decision"] = train_step.runner.decision
             if t_warm is not None and completed > warm:
                 tp["train_steady_samples_per_second"] = round(per_step * (completed - warm) / (t1 - t_warm), 3)
             self.dump(tp)
