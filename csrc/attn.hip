@@ -100,8 +100,35 @@ DLLM_DEVICE uint32_t dropout_word(uint32_t rh, int kbase, int hh, uint32_t thr) 
 // .. + 3 of row r in a_t[4 g .. 4 g + 3]; times `mul`) through the wave's 4 KB LDS scratch (16-B chunks XOR-swizzled by
 // row), stored as whole 128-B rows: 4 full-line stores instead of 8 per-lane 8-B stores touching 32 lines each.  Row rr
 // goes to base + rr * row_stride (elements) for rr < nrows.  The caller has made the scratch free (barrier).
+//
+// Bias-gradient column sums (AttnParams csq / csk / csv): the staged rows are summed per column on their way to the row
+// stores.  Lane (row group lane >> 3, 16-B chunk ch) adds the 8 bf16 values of each of its valid rows (the stored,
+// rounded values: what a separate column reduction of dQ / dK / dV would read), cs_wave folds the 8 row groups with xor
+// shuffles and writes the wave's 64 sums to `red` (LDS); after a barrier one thread per column adds the 4 waves' sums in
+// a fixed order (deterministic) and stores one partial row of the [B * blocks][cols] fp32 buffer the host reduces.
+DLLM_DEVICE void cs_add(float (&acc)[8], const u16x8& v) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) acc[e] += bf2f(v[e]);
+}
+
+DLLM_DEVICE void cs_wave(float (&acc)[8], int lane, float* red) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    float s = acc[e];
+    s += __shfl_xor(s, 8, 64);
+    s += __shfl_xor(s, 16, 64);
+    s += __shfl_xor(s, 32, 64);
+    acc[e] = s;
+  }
+  if (lane < 8) {
+    *reinterpret_cast<float4*>(red + 8 * lane) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    *reinterpret_cast<float4*>(red + 8 * lane + 4) = make_float4(acc[4], acc[5], acc[6], acc[7]);
+  }
+}
+
+// `red` != nullptr: also the tile's column sums over its rows < nrows into red[0, 64) (cs_wave)
 DLLM_DEVICE void store_rows_staged(unsigned char* scr, const f32x16& a0, const f32x16& a1, float mul, int r, int hh,
-                                   int lane, uint16_t* base, long row_stride, int nrows) {
+                                   int lane, uint16_t* base, long row_stride, int nrows, float* red = nullptr) {
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
     const f32x16& a = t == 0 ? a0 : a1;
@@ -113,12 +140,17 @@ DLLM_DEVICE void store_rows_staged(unsigned char* scr, const f32x16& a0, const f
     }
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // other lanes of this wave read what these wrote
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int st = 0; st < 4; ++st) {
     const int row = 8 * st + (lane >> 3), ch = lane & 7;
     const u16x8 v = *reinterpret_cast<const u16x8*>(scr + row * 128 + ((ch ^ (row & 7)) << 4));
-    if (row < nrows) *reinterpret_cast<u16x8*>(base + (long)row * row_stride + 8 * ch) = v;
+    if (row < nrows) {
+      *reinterpret_cast<u16x8*>(base + (long)row * row_stride + 8 * ch) = v;
+      if (red != nullptr) cs_add(acc, v);
+    }
   }
+  if (red != nullptr) cs_wave(acc, lane, red);
 }
 
 // ================================================================================== dropout bit planes
@@ -652,8 +684,17 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dq_kernel(AttnParams P) {
 #if DQ_STAGE
   // every wave is done with the K/V buffers (the last tile's DMAs were waited for): they stage the dQ tiles
   __syncthreads();
+  // column sums: the 4 waves' 64 sums at smem + 16 KB (past the 4 staging tiles, still inside the K/V buffers)
+  float* red = P.csq != nullptr ? reinterpret_cast<float*>(smem + 4 * 4096) : nullptr;
   store_rows_staged(smem + w * 4096, dq0, dq1, P.scale, r, hh, lane,
-                    P.dq + b * P.dq_sb + (long)qw0 * P.dq_ss + h * P.dq_sh, P.dq_ss, P.Sq - qw0);
+                    P.dq + b * P.dq_sb + (long)qw0 * P.dq_ss + h * P.dq_sh, P.dq_ss, P.Sq - qw0,
+                    red != nullptr ? red + w * 64 : nullptr);
+  if (P.csq != nullptr) {
+    __syncthreads();
+    if (tid < 64)
+      P.csq[(long)(b * P.n_tiles + qt) * P.csq_ld + h * 64 + tid] = red[tid] + red[64 + tid] + red[128 + tid] +
+                                                                     red[192 + tid];
+  }
 #else
   if (qvalid) {
     uint16_t* dqp = P.dq + b * P.dq_sb + (long)qrow * P.dq_ss + h * P.dq_sh;
@@ -1276,6 +1317,7 @@ __global__ __launch_bounds__(256, NB == 3 ? 2 : 3) void attn_bwd_dkdv2_kernel(At
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // other lanes of this wave read what these wrote
+    float ak[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, av[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int st = 0; st < 4; ++st) {
       const int row = 8 * st + (lane >> 3), ch = lane & 7;
@@ -1286,6 +1328,24 @@ __global__ __launch_bounds__(256, NB == 3 ? 2 : 3) void attn_bwd_dkdv2_kernel(At
       if (ks < P.Sk) {
         *reinterpret_cast<u16x8*>(P.dk + b * P.dk_sb + (long)ks * P.dk_ss + h * P.dk_sh + 8 * ch) = vk;
         *reinterpret_cast<u16x8*>(P.dv + b * P.dv_sb + (long)ks * P.dv_ss + h * P.dv_sh + 8 * ch) = vv;
+        if (P.csk != nullptr) {
+          cs_add(ak, vk);
+          cs_add(av, vv);
+        }
+      }
+    }
+    if (P.csk != nullptr) {
+      // column sums (cs_wave): [wave][dK 64 | dV 64] at smem + 32 KB, past the 4 waves' 8 KB staging areas and
+      // inside the drained stage ring (NB * K2_STAGE >= 36 KB)
+      float* red = reinterpret_cast<float*>(smem + 4 * 8192);
+      cs_wave(ak, lane, red + w * 128);
+      cs_wave(av, lane, red + w * 128 + 64);
+      __syncthreads();
+      if (tid < 128) {
+        const int c = tid & 63, which = tid >> 6;
+        const float s = red[which * 64 + c] + red[128 + which * 64 + c] + red[256 + which * 64 + c] +
+                        red[384 + which * 64 + c];
+        (which == 0 ? P.csk : P.csv)[(long)(b * P.n_tiles + kblk) * P.cskv_ld + h * 64 + c] = s;
       }
     }
   }
@@ -1504,6 +1564,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_sq_kernel(AttnParams P) 
         }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // other lanes of this wave read what these wrote
+      float ak[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, av[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int st = 0; st < 4; ++st) {
         const int row = 8 * st + (lane >> 3), ch = lane & 7;
@@ -1514,6 +1575,24 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_sq_kernel(AttnParams P) 
         if (ks < P.Sk) {
           *reinterpret_cast<u16x8*>(P.dk + b * P.dk_sb + (long)ks * P.dk_ss + h * P.dk_sh + 8 * ch) = vk;
           *reinterpret_cast<u16x8*>(P.dv + b * P.dv_sb + (long)ks * P.dv_ss + h * P.dv_sh + 8 * ch) = vv;
+          if (P.csk != nullptr) {
+            cs_add(ak, vk);
+            cs_add(av, vv);
+          }
+        }
+      }
+      if (P.csk != nullptr) {
+        // column sums (cs_wave): [wave][dK 64 | dV 64] in the 2 KB past the staging areas (lds_sq); the next key
+        // block's writes come after its own barrier above
+        float* red = reinterpret_cast<float*>(smem + 2 * K2_STAGE + 4096 + BWD_BK * 4 + 4 * 8192);
+        cs_wave(ak, lane, red + w * 128);
+        cs_wave(av, lane, red + w * 128 + 64);
+        __syncthreads();
+        if (tid < 128) {
+          const int c = tid & 63, which = tid >> 6;
+          const float s = red[which * 64 + c] + red[128 + which * 64 + c] + red[256 + which * 64 + c] +
+                          red[384 + which * 64 + c];
+          (which == 0 ? P.csk : P.csv)[(long)(b * P.n_tiles + kb) * P.cskv_ld + h * 64 + c] = s;
         }
       }
     }
@@ -1681,6 +1760,10 @@ extern "C" int dllm_attn_bwd(AttnParams* pp, hipStream_t st) {
   p.n_ktiles = (p.Sk + FWD_BN - 1) / FWD_BN;
   p.sq_pad = p.n_tiles * FWD_BM;
   if (p.p_drop > 0.f && p.dmask == nullptr) return -5;
+  // column sums need the staged stores of all three kernels (and the v2 / short-query dK/dV kernels)
+  if ((p.csq != nullptr || p.csk != nullptr) && (!DQ_STAGE || !DKDV2_STAGE || !DKDV_SQ_STAGE || p.rowrec == nullptr))
+    return -7;
+  if ((p.csk == nullptr) != (p.csv == nullptr)) return -7;
   long nblk = (long)p.n_tiles * p.H * p.B;
   // 2 K/V buffers + per-key mask + tile flags + bias LUT window
   size_t lds = (size_t)4 * TILE64 * 2 + (size_t)p.n_ktiles * (FWD_BN + 1) * 4;
@@ -1714,7 +1797,7 @@ extern "C" int dllm_attn_bwd(AttnParams* pp, hipStream_t st) {
   for (int m = 8; m >= 2; m /= 2)
     if (m <= sq_cap && mb == 0 && (force || (long)((p.n_tiles + m - 1) / m) * p.H * p.B >= 6L * cus)) mb = m;
   if (p.rowrec != nullptr && p.lut == nullptr && !p.causal && p.Sq <= 2 * K2_QT && mb > 1 && p.n_tiles >= 2) {
-    const size_t lds_sq = (size_t)2 * K2_STAGE + 4096 + BWD_BK * 4 + (DKDV_SQ_STAGE ? 4 * 8192 : 0);
+    const size_t lds_sq = (size_t)2 * K2_STAGE + 4096 + BWD_BK * 4 + (DKDV_SQ_STAGE ? 4 * 8192 + 2048 : 0);
     if ((long)((p.n_tiles + mb - 1) / mb) * p.H * p.B > 0x7fffffff) return -4;
     if (p.kpm != nullptr) {
       if (p.p_drop > 0.f) launch_bwd_dkdv_sq_t<true, true>(p, mb, lds_sq, st);

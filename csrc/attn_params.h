@@ -45,4 +45,11 @@ struct AttnParams {
   // lut[L-1] (no diagonal shear).  Disabled: sat_lo = INT_MIN / 2, sat_hi = INT_MAX / 2.
   int sat_lo;
   int sat_hi;
+  // bwd, optional: per-block column sums of dQ / dK / dV (the bias gradients of the projections that produced q / k /
+  // v).  Row b * ceil(S / 128) + block (S = Sq for csq, Sk for csk / csv), columns h * 64 + d, row strides csq_ld /
+  // cskv_ld floats; the host sums the rows (ops/attention.py).  nullptr: not wanted.
+  float* csq;
+  float* csk;
+  float* csv;
+  long csq_ld, cskv_ld;
 };

@@ -553,7 +553,8 @@ std::vector<Tensor> attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& 
                              double scale, bool causal, double p, int64_t seed, bool need_dlut,
                              const optional<Tensor>& dq_out, const optional<Tensor>& dk_out,
                              const optional<Tensor>& dv_out, const optional<Tensor>& dmask, int64_t sat_lo,
-                             int64_t sat_hi) {
+                             int64_t sat_hi, const optional<Tensor>& csq, const optional<Tensor>& csk,
+                             const optional<Tensor>& csv) {
   AttnParams P{};
   fill_qkv(P, q, k, v, kpm, lut, scale, causal, p, seed);
   set_sat(P, sat_lo, sat_hi);
@@ -600,6 +601,22 @@ std::vector<Tensor> attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& 
   P.dv = reinterpret_cast<uint16_t*>(dv.data_ptr());
   P.dv_sb = dv.stride(0); P.dv_ss = dv.stride(1); P.dv_sh = dv.stride(2);
   P.dlut = dlut.defined() ? dlut.data_ptr<float>() : nullptr;
+  // optional per-block column sums ([B * ceil(S / 128)][H * 64] fp32 views, unit column stride; dK / dV share a row
+  // stride): the bias gradients of the q / k / v projections, summed over blocks by the caller
+  auto cs = [&](const optional<Tensor>& t, int64_t S, const char* n, long* ld) -> float* {
+    if (!t.has_value() || !t->defined()) return nullptr;
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->dim() == 2 && t->size(0) == P.B * ((S + 127) / 128) &&
+                    t->size(1) == (int64_t)P.H * 64 && t->stride(1) == 1 && t->stride(0) >= t->size(1),
+                n, ": expected fp32 [B * ceil(S / 128), H * 64] with unit column stride");
+    *ld = t->stride(0);
+    return t->data_ptr<float>();
+  };
+  long ldk = 0, ldv = 0;
+  P.csq = cs(csq, P.Sq, "csq", &P.csq_ld);
+  P.csk = cs(csk, P.Sk, "csk", &ldk);
+  P.csv = cs(csv, P.Sk, "csv", &ldv);
+  TORCH_CHECK((P.csk == nullptr) == (P.csv == nullptr) && ldk == ldv, "csk / csv: both or neither, one row stride");
+  P.cskv_ld = ldk;
   check_rc(dllm_attn_bwd(&P, stream()), "attn_bwd");
   return {dq, dk, dv, need_dlut ? dlut : Tensor()};
 }
@@ -1158,7 +1175,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("lse"), py::arg("kpm"), py::arg("lut"), py::arg("scale"), py::arg("causal"), py::arg("p"),
         py::arg("seed"), py::arg("need_dlut"), py::arg("dq_out") = py::none(), py::arg("dk_out") = py::none(),
         py::arg("dv_out") = py::none(), py::arg("dmask") = py::none(), py::arg("sat_lo") = -1,
-        py::arg("sat_hi") = -1);
+        py::arg("sat_hi") = -1, py::arg("csq") = py::none(), py::arg("csk") = py::none(),
+        py::arg("csv") = py::none());
   m.def("attn_params_size", []() { return dllm_attn_params_size(); });
   m.def("attn_f32_fwd", &attn_f32_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("kpm"), py::arg("lut"),
         py::arg("scale"), py::arg("causal"), py::arg("p"), py::arg("seed"));

@@ -30,6 +30,7 @@ import torch
 
 from .. import _ext
 from . import streams
+from .gemm import colsum_record
 from .rng import attention_keep_mask
 
 # --------------------------------------------------------------------------- T5 relative bias
@@ -157,6 +158,9 @@ class _AttnFn(torch.autograd.Function):
                                    sat_lo if fsat else -1, sat_hi if fsat else -1)
         ctx.save_for_backward(a, b, c, o, lse, lut, kpm, dmask)
         ctx.cfg = (mode, scale, causal, p, seed, lut is not None and lut.requires_grad, sat_lo, sat_hi)
+        # packed inputs straight from a biased projection (ops/linear.py marks its output): the backward kernels also
+        # sum dQ / dK / dV over tokens for that projection's bias gradient (colsum_record)
+        ctx.cs = (BIAS_COLSUM and mode != "sep" and _bias_out(a), BIAS_COLSUM and mode == "q_kv" and _bias_out(b))
         # ops/linear.py stacked_linear: the packed kv is a slice of a multi-layer projection and its
         # gradient has a home in the stacked gradient buffer — write dK/dV there directly
         ctx.grad_into = getattr(b, "_dllm_grad_into", None) if mode == "q_kv" else None
@@ -180,16 +184,53 @@ class _AttnFn(torch.autograd.Function):
             dq, dk, dv = da, db[:, :, 0], db[:, :, 1]
         else:
             dq = dk = dv = None
+        part = pq = pkv = None
+        csq = csk = csv = None
+        if q.dtype != torch.float32 and (ctx.cs[0] or ctx.cs[1]):
+            B, Sq, H = q.shape[0], q.shape[1], q.shape[2]
+            HD, nq, nk = H * 64, B * ((Sq + 127) // 128), B * ((k.shape[1] + 127) // 128)
+            f32 = dict(device=q.device, dtype=torch.float32)
+            if mode == "qkv":  # one [blocks, 3 H D] buffer: the q | k | v thirds of the fused bias
+                part = torch.empty(nq, 3 * HD, **f32)
+                csq, csk, csv = part[:, :HD], part[:, HD:2 * HD], part[:, 2 * HD:]
+            else:
+                if ctx.cs[0]:
+                    pq = csq = torch.empty(nq, HD, **f32)
+                if ctx.cs[1]:
+                    pkv = torch.empty(nk, 2 * HD, **f32)
+                    csk, csv = pkv[:, :HD], pkv[:, HD:]
         if q.dtype == torch.float32:
             rq, rk, rv, dlut = C.attn_f32_bwd(do.contiguous(), q, k, v, o, lse, kpm, lut, float(scale), bool(causal),
                                               float(p), int(seed), bool(need_dlut), dq, dk, dv)
         else:
             rq, rk, rv, dlut = C.attn_bwd(do.contiguous(), q, k, v, o, lse, kpm, lut, float(scale), bool(causal),
-                                          float(p), int(seed), bool(need_dlut), dq, dk, dv, dmask, sat_lo, sat_hi)
+                                          float(p), int(seed), bool(need_dlut), dq, dk, dv, dmask, sat_lo, sat_hi,
+                                          csq, csk, csv)
+        if part is not None:
+            colsum_record(da, part.sum(0))
+        if pq is not None:
+            colsum_record(da, pq.sum(0))
+        if pkv is not None:
+            colsum_record(db, pkv.sum(0))
         if mode == "sep":
             da, db, dc = rq, rk, rv
         streams.pair_join()  # side-stream weight gradients paired with these VALU-bound kernels (ops/streams.py)
         return None, da, db, dc, (dlut if need_dlut else None), None, None, None, None, None, None
+
+
+# 0: the projections' bias gradients from a separate column reduction of dQKV (A/B; tests flip the module attribute)
+BIAS_COLSUM = os.environ.get("DLLM_ATTN_BIAS_COLSUM", "1") != "0"
+
+
+def _bias_out(t) -> bool:
+    """t (or the tensor it is a full view of) is a biased projection's output (ops/linear.py ``_dllm_bias_out``)."""
+    if t is None:
+        return False
+    if getattr(t, "_dllm_bias_out", False):
+        return True
+    src = t._base
+    return (src is not None and getattr(src, "_dllm_bias_out", False) and src.data_ptr() == t.data_ptr()
+            and src.numel() == t.numel())
 
 
 def _prep_kpm(kpm):

@@ -127,22 +127,43 @@ def _wgrad(out, dy2, x2, beta):
 def bias_grad_accumulate(out: torch.Tensor, dy2: torch.Tensor, dy: torch.Tensor | None = None,
                          async_ok: bool = True) -> torch.Tensor:
     """``out += dy2.sum(0)`` (bias gradient of a linear layer, accumulated in place).  ``dy``: the gradient tensor as
-    autograd delivered it; when its producer already summed it over tokens (ops/norms.py x_bias_grad: the BART
-    post-LN backward kernel) that fp32 column sum is added instead of re-reading dy."""
+    autograd delivered it; when its producer already summed it over tokens (:func:`colsum_record`: the BART post-LN
+    backward kernel, the attention backward kernels) that fp32 column sum is added instead of re-reading dy."""
     global colsum_handoffs
-    rec = getattr(dy, "_dllm_colsum", None) if dy is not None else None
-    if rec is not None:
-        cs, ver, shape, ptr = rec
-        # only while dy is still exactly the tensor the norm backward summed: same storage, shape and version (an
-        # in-place accumulation of another consumer's gradient bumps the version and the sum no longer describes dy)
-        if (cs.numel() == out.numel() and dy._version == ver and tuple(dy.shape) == shape and dy.data_ptr() == ptr):
-            colsum_handoffs += 1
-            if not async_ok:
-                return out.add_(cs.view_as(out).to(out.dtype))
-            return streams.run(lambda: out.add_(cs.view_as(out).to(out.dtype)), cs)
+    cs = colsum_of(dy, out.numel())
+    if cs is not None:
+        colsum_handoffs += 1
+        if not async_ok:
+            return out.add_(cs.view_as(out).to(out.dtype))
+        return streams.run(lambda: out.add_(cs.view_as(out).to(out.dtype)), cs)
     if not async_ok:
         return _colsum(out, dy2)
     return streams.run(lambda: _colsum(out, dy2), dy2)
+
+
+def colsum_record(t: torch.Tensor, cs: torch.Tensor) -> None:
+    """Attach ``cs`` = fp32 ``t.reshape(-1, n).sum(0)``, computed by t's producer on the way (the BART post-LN backward
+    kernel, ops/norms.py; the attention backward kernels' dQ / dK / dV epilogues, ops/attention.py), for the bias
+    gradient of the linear layer that consumes t's gradient (:func:`bias_grad_accumulate`)."""
+    t._dllm_colsum = (cs, t._version, t.numel(), t.data_ptr())
+
+
+def colsum_of(dy: torch.Tensor | None, n: int) -> torch.Tensor | None:
+    """The column sum recorded on ``dy`` — or on its base, when autograd delivers a full view of the producer's tensor
+    (the [B, S, 3, H, D] attention gradient as the projection's [B, S, 3 d]) — if it still describes dy: same storage,
+    element count and version (an in-place accumulation of another consumer's gradient bumps the version and the sum
+    no longer describes dy); ``n`` = the bias length.  None otherwise."""
+    if dy is None:
+        return None
+    rec = getattr(dy, "_dllm_colsum", None)
+    if rec is None and dy._base is not None:
+        rec = getattr(dy._base, "_dllm_colsum", None)
+    if rec is None:
+        return None
+    cs, ver, numel, ptr = rec
+    if cs.numel() == n and dy._version == ver and dy.numel() == numel and dy.data_ptr() == ptr:
+        return cs
+    return None
 
 
 def _colsum(out, dy2):

@@ -21,7 +21,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import streams
-from .gemm import bias_grad_accumulate, linear_dgrad, linear_fwd, wgrad_accumulate
+from . import gemm
+from .gemm import bias_grad_accumulate, colsum_of, linear_dgrad, linear_fwd, wgrad_accumulate
 
 
 def _gbuf(p: torch.Tensor | None) -> torch.Tensor | None:
@@ -128,7 +129,7 @@ class _LinearResFn(torch.autograd.Function):
         with torch.no_grad():
             wgrad_accumulate(_gbuf(w), dy2, x2, async_ok=_sole_writer(w) and streams.site_ok(w))
             if bias is not None:
-                bias_grad_accumulate(_gbuf(bias), dy2, async_ok=streams.site_ok(bias))
+                bias_grad_accumulate(_gbuf(bias), dy2, dy, async_ok=streams.site_ok(bias))
         _fire(w)
         if bias is not None:
             _fire(bias)
@@ -143,8 +144,22 @@ def linear_res(x: torch.Tensor, mod) -> tuple[torch.Tensor, torch.Tensor]:
     residual's gradient is accumulated by this linear's input-gradient GEMM (``_LinearResFn``)."""
     w, b = mod.weight, mod.bias
     if _RES_GEMM and torch.is_grad_enabled() and x.requires_grad and _fusable(w) and _fusable(b):
-        return _LinearResFn.apply(x, w.detach(), None if b is None else b.detach(), (w, b))
+        y, res = _LinearResFn.apply(x, w.detach(), None if b is None else b.detach(), (w, b))
+        _mark_bias_out(y, b is not None)
+        return y, res
     return mod(x), x
+
+
+def _mark_bias_out(y: torch.Tensor, on: bool) -> None:
+    """Mark a biased projection's output: a consumer that sums dY over tokens on the way (ops/attention.py) hands that
+    sum to the bias gradient (ops/gemm.py colsum_record).  Also on the tensor y is a full view of (the GEMM's 2-D
+    result): views of y, like the attention's [B, S, 3, H, D], point at that root, not at y."""
+    if not on:
+        return
+    y._dllm_bias_out = True
+    base = y._base
+    if base is not None and base.data_ptr() == y.data_ptr() and base.numel() == y.numel():
+        base._dllm_bias_out = True
 
 
 def _fusable(p: torch.Tensor | None) -> bool:
@@ -154,7 +169,9 @@ def _fusable(p: torch.Tensor | None) -> bool:
 def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Tensor:
     """Functional ``F.linear`` with the weight gradient accumulated by the GEMM (e.g. a tied LM head)."""
     if torch.is_grad_enabled() and _fusable(weight) and _fusable(bias):
-        return _LinearAccumFn.apply(x, weight.detach(), None if bias is None else bias.detach(), (weight, bias))
+        y = _LinearAccumFn.apply(x, weight.detach(), None if bias is None else bias.detach(), (weight, bias))
+        _mark_bias_out(y, bias is not None)
+        return y
     return F.linear(x, weight, bias)
 
 
@@ -195,6 +212,7 @@ class _StackedFn(torch.autograd.Function):
         for l in range(len(ws)):
             o = y[..., l * n:(l + 1) * n].view(shape)
             o._dllm_grad_into = gbuf[..., l * n:(l + 1) * n].view(shape)  # consumers may write dY_l here
+            o._dllm_bias_out = b is not None  # ... and record its column sum there (colsum_record)
             outs.append(o)
         ctx.save_for_backward(x)
         ctx.W, ctx.gbuf, ctx.params, ctx.n = W, gbuf, (ws, bs), n
@@ -228,7 +246,12 @@ class _StackedFn(torch.autograd.Function):
                     _gbuf(w).add_(dW[l * n:(l + 1) * n])
             if bs[0] is not None:
                 gb = _adjacent([_gbuf(bb) for bb in bs])
-                if gb is not None:
+                # every layer's consumer summed its dY_l over tokens (ops/attention.py): n-column adds, no G2 pass
+                cs = [colsum_of(g, n) for g in grads]
+                if gb is not None and all(c is not None for c in cs):
+                    gemm.colsum_handoffs += len(cs)
+                    gb.add_(torch.cat(cs).view_as(gb).to(gb.dtype))
+                elif gb is not None:
                     bias_grad_accumulate(gb, G2)
                 else:
                     db = G2.sum(0)

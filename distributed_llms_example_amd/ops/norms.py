@@ -16,6 +16,7 @@ import torch
 
 from .. import _ext
 from . import streams
+from .gemm import colsum_record
 from .linear import _fire, _fusable, _gbuf, _use
 from .rng import keep_mask
 
@@ -76,7 +77,7 @@ class _NormFn(torch.autograd.Function):
         if ctx.colsum:  # handed to the producing linear layer's backward as its bias gradient (ops/gemm.py)
             # with the tensor's version: autograd may add a second consumer's gradient into dx in place, after which
             # the column sum is stale (ops/gemm.py bias_grad_accumulate checks it)
-            dx._dllm_colsum = (dxs, dx._version, tuple(dx.shape), dx.data_ptr())
+            colsum_record(dx, dxs)
         # d(resid) == d(s) (pre-dropout gradient); identical to dx when p == 0
         dres = None
         if has_resid:
