@@ -42,6 +42,7 @@ int dllm_attn_f32_fwd(AttnF32Params*, hipStream_t);
 int dllm_attn_f32_bwd(AttnF32Params*, hipStream_t);
 int dllm_set_seed_step_attn_f32(const uint32_t*);
 int dllm_gemm_wgrad(const GemmWgradParams*, int, hipStream_t);
+int dllm_wgrad_reduce(const GemmWgradParams*, hipStream_t);
 int dllm_gemm_fused(const GemmFusedParams*, int, int, hipStream_t);
 int dllm_gemm_w4(const GemmW4Params*, int, int, int, hipStream_t);
 int dllm_set_seed_step_gemm_w4(const uint32_t*);
@@ -667,6 +668,8 @@ int wgrad_splits(int T, int K) {
   return best;
 }
 
+constexpr int64_t kWgradW4 = 12;  // gemm_wgrad variant: csrc/gemm_w4.hip's weight-gradient mode
+
 int64_t gemm_wgrad(const Tensor& a, const Tensor& b, Tensor& c, bool beta, int64_t variant, int64_t splits_req) {
   TORCH_CHECK(gemm_wgrad_supported(a, b, c),
               "gemm_wgrad: need bf16 GPU [K,M] x [K,N] -> bf16/fp32 [M,N], unit inner stride, 16-B aligned rows, K % 64 == 0, "
@@ -690,6 +693,19 @@ int64_t gemm_wgrad(const Tensor& a, const Tensor& b, Tensor& c, bool beta, int64
   int splits = splits_req > 0 ? (int)splits_req : wgrad_splits(P.ntiles, K);
   splits = std::max(1, std::min(splits, K / 256));
   int kchunk = ((K + splits - 1) / splits + 63) / 64 * 64;
+  // default (variant < 0): the w4 weight-gradient mode — +1.2 % t5-base b=512, +1.5 % bart-large b=256 steps, equal at
+  // b=8 (profiles/r5_wgrad_w4_ab.txt); kernel-level 2-8 % faster than variant 9 on every T5 / BART shape
+  if (variant < 0) variant = kWgradW4;
+  if (variant == kWgradW4) {
+    // the w4 kernel addresses a split's k-rows through one 32-bit buffer-descriptor range: more splits when a wide
+    // operand (e.g. the decoder's stacked cross-attention K/V gradient, 24576 columns) would overflow it
+    const long ld = std::max(P.lda, P.ldb), wd = std::max(M, N);
+    while (kchunk > 64 && ((long)(kchunk - 1) * ld + wd) * 2 >= 0xFFFFFFFFL) {
+      ++splits;
+      kchunk = ((K + splits - 1) / splits + 63) / 64 * 64;
+    }
+    if (((long)(kchunk - 1) * ld + wd) * 2 >= 0xFFFFFFFFL) variant = 9;  // even 64-row splits overflow: csrc/gemm.hip
+  }
   splits = (K + kchunk - 1) / kchunk;
   P.kchunk = kchunk;
   P.splits = splits;
@@ -697,6 +713,30 @@ int64_t gemm_wgrad(const Tensor& a, const Tensor& b, Tensor& c, bool beta, int64
   if (splits > 1) {
     ws = at::empty({(int64_t)splits * M * N}, a.options().dtype(at::kFloat));
     P.ws = ws.data_ptr<float>();
+  }
+  if (variant == kWgradW4) {
+    // csrc/gemm_w4.hip weight-gradient mode: one wave per SIMD, both operands k-major, fp32 split slabs
+    GemmW4Params Q{};
+    Q.A = P.A;
+    Q.B = P.B;
+    Q.lda = P.lda;
+    Q.ldb = P.ldb;
+    Q.ldc = P.ldc;
+    Q.M = M;
+    Q.N = N;
+    Q.K = K;
+    Q.tm = (M + 255) / 256;
+    Q.tn = N / 256;
+    Q.grp = 8;
+    Q.ws = P.ws;
+    Q.Cw = P.C;
+    Q.splits = splits;
+    Q.kchunk = kchunk;
+    Q.c_f32 = P.c_f32;
+    Q.beta = P.beta;
+    check_rc(dllm_gemm_w4(&Q, 1, 0, 10, stream()), "gemm_wgrad (w4)");
+    if (splits > 1) check_rc(dllm_wgrad_reduce(&P, stream()), "gemm_wgrad (w4) split-K reduce");
+    return splits;
   }
   check_rc(dllm_gemm_wgrad(&P, (int)variant, stream()), "gemm_wgrad");
   return splits;

@@ -432,6 +432,22 @@ int launch_wgrad(const GemmWgradParams& p, hipStream_t st) {
 
 extern "C" int dllm_gemm_wgrad_bk() { return 64; }
 
+// the split-K pass alone: C (+)= sum of p.splits fp32 slabs p.ws (the w4 weight-gradient kernel's, csrc/gemm_w4.hip)
+extern "C" int dllm_wgrad_reduce(const GemmWgradParams* pp, hipStream_t st) {
+  const GemmWgradParams& p = *pp;
+  if (p.splits < 2 || p.ws == nullptr || p.N % 8 || p.M <= 0) return -4;
+  const long n8 = (long)p.M * p.N / 8;
+  const int blocks = (int)std::min<long>((n8 + 255) / 256, 2048);
+  if (p.c_f32)
+    hipLaunchKernelGGL(splitk_reduce_kernel<float>, dim3(blocks), dim3(256), 0, st, p.ws, (float*)p.C, p.ldc, p.M, p.N,
+                       p.splits, p.beta);
+  else
+    hipLaunchKernelGGL(splitk_reduce_kernel<uint16_t>, dim3(blocks), dim3(256), 0, st, p.ws, (uint16_t*)p.C, p.ldc,
+                       p.M, p.N, p.splits, p.beta);
+  DLLM_CHECK_LAUNCH();
+  return 0;
+}
+
 // variant: 0 = BK64 x 2 stages (128 KB LDS), 1 = BK32 x 4 stages (128 KB), 2 = BK32 x 3 stages (96 KB),
 // 3 / 4 = variants 0 / 1 with s_setprio raised around the MFMA block,
 // 5 / 6 = variants 0 / 1 with 4 waves of 128x128 (one wave per SIMD, accumulators in AGPRs),

@@ -53,6 +53,11 @@ struct GemmW4Params {
   int c0, V, skip, pstride;
   float eps;
   long ignore;
+  // weight-gradient epilogue (W4_EPI_WG): A = [K][M] k-major too; K split in `splits` chunks of `kchunk` rows; fp32
+  // slabs ws[splits][M][N] (splits > 1), else Cw (fp32 if c_f32, else bf16; += when beta) with row stride ldc
+  float* ws;
+  void* Cw;
+  int splits, kchunk, c_f32, beta;
 };
 
 // csrc/gemm_fused.hip: C[M][N] = epi(A[M][K] . B), B = [N][K] (b_kmajor = 0) or [K][N] (b_kmajor = 1)

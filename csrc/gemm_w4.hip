@@ -29,6 +29,7 @@
 // * bijective XCD remap of the 1-D grid, tiles grouped grp x (32 / grp) per XCD for L2 reuse of A and B.
 #include "common.h"
 
+#include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 
@@ -44,7 +45,11 @@ namespace {
 // through that mask, dU = dH * scale where the bit is set (backward, NN).  The mask is what the backward needs of
 // the forward: no re-read of H, no re-hash (T5 FFN, ops/ffn.py).
 // LM-head cross-entropy (ops/lm_head.py): CEF = forward partials (no C), CEB = dlogits (gemm_params.h)
-enum { W4_EPI_NONE = 0, W4_EPI_RELU = 1, W4_EPI_DRELU_M = 7, W4_EPI_CEF = 8, W4_EPI_CEB = 9 };
+// Weight gradient (WG, "TN"): C[M][N] (+)= A^T B with BOTH operands token-major (A = dY [K][M], B = X [K][N]): the A
+// image is k-major like the NN B operand (transposed fragment reads), K is split over workgroups (tile index = split x
+// output tile, one tile per workgroup) and each split stores its fp32 product to a slab of ws (reduced into C by
+// csrc/gemm.hip's split-K pass), or — one split — accumulates straight into the fp32 / bf16 C.
+enum { W4_EPI_NONE = 0, W4_EPI_RELU = 1, W4_EPI_DRELU_M = 7, W4_EPI_CEF = 8, W4_EPI_CEB = 9, W4_EPI_WG = 10 };
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8v;
 typedef __attribute__((ext_vector_type(4))) short s16x4;
@@ -149,23 +154,27 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
   constexpr uint32_t TB = 256 * BK * 2;  // one operand image: 32 KB
   constexpr uint32_t BUF = 2 * TB;       // [A | B] of one k-tile: 64 KB; two buffers
 
+  constexpr bool AKM = EPI == W4_EPI_WG;  // A k-major too (weight gradient)
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = w >> 1, wn = w & 1;
-  const int nk = P.K / BK;
 
   // ---- tiles of this workgroup.  Blocks are dealt round-robin over the 8 XCDs (b % 8 share one), so XCD x takes a
   // contiguous range of virtual tiles and its slot-th workgroup walks vbase + slot, + nwx, ... (grid == #tiles: one
   // tile each, the bijective XCD remap); virtual tile -> (row block, column block) in groups of grp row blocks,
   // column-major inside a group, so the 32 tiles an XCD runs at once share A and B panels in its L2.
-  const int T = P.tm * P.tn, G = gridDim.x, bid = blockIdx.x, xcd = bid % 8, slot = bid / 8;
+  // (WG: virtual tile = split * tm * tn + output tile, so an XCD's contiguous range shares the splits' k-ranges)
+  const int Tmn = P.tm * P.tn, T = AKM ? Tmn * P.splits : Tmn, G = gridDim.x, bid = blockIdx.x, xcd = bid % 8,
+            slot = bid / 8;
   const int nwx = G / 8 + (xcd < G % 8 ? 1 : 0);
   const int ntx = T / 8 + (xcd < T % 8 ? 1 : 0);
   const int vbase = xcd * (T / 8) + min(xcd, T % 8) + slot;
   const int ntw = slot < ntx ? (ntx - slot + nwx - 1) / nwx : 0;
   if (ntw == 0) return;
-  auto tile_mn = [&](int i, int& m0, int& n0) {
-    const int vt = vbase + i * nwx;
+  auto tile_mn = [&](int i, int& m0, int& n0, int& ks) {
+    int vt = vbase + i * nwx;
+    ks = AKM ? vt / Tmn : 0;
+    vt -= ks * Tmn;
     int mb = vt / P.tn, nb = vt % P.tn;
     if (P.grp > 0) {
       const int gs = P.grp * P.tn, g = vt / gs, r = vt % gs;
@@ -176,9 +185,17 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
     m0 = mb * 256;
     n0 = nb * 256;
   };
-  auto srd_a = [&](int m0) { return make_srd(P.A + (long)m0 * P.lda, (uint32_t)(min(P.M - m0, 256) * P.lda * 2)); };
-  auto srd_b = [&](int n0) {
-    return BKM ? make_srd(P.B + n0, (uint32_t)(((long)(P.K - 1) * P.ldb + P.N - n0) * 2))
+  // k-rows of split ks (WG) / all of K
+  auto krows = [&](int ks) { return AKM ? min(P.kchunk, P.K - ks * P.kchunk) : P.K; };
+  // k-major descriptors span the split's k-rows of the view (column overrun: see the DMA offsets below)
+  auto srd_a = [&](int m0, int ks) {
+    return AKM ? make_srd(P.A + (long)ks * P.kchunk * P.lda + m0,
+                          (uint32_t)(((long)(krows(ks) - 1) * P.lda + P.M - m0) * 2))
+               : make_srd(P.A + (long)m0 * P.lda, (uint32_t)(min(P.M - m0, 256) * P.lda * 2));
+  };
+  auto srd_b = [&](int n0, int ks) {
+    return BKM ? make_srd(P.B + (long)(AKM ? ks * P.kchunk : 0) * P.ldb + n0,
+                          (uint32_t)(((long)(krows(ks) - 1) * P.ldb + P.N - n0) * 2))
                : make_srd(P.B + (long)n0 * P.ldb, (uint32_t)(min(P.N - n0, 256) * P.ldb * 2));
   };
 
@@ -194,9 +211,10 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
     const int q = w * 8 + i;
     const int r = 8 * q + (lane >> 3);
     const int c = (lane & 7) ^ ((r >> 1) & 7);
-    va[i] = (uint32_t)(r * P.lda + c * 8) * 2u;
+    const int kr = 2 * q + (lane >> 5);
+    if (AKM) va[i] = (uint32_t)(kr * P.lda + ((lane & 31) ^ gsw(kr)) * 8) * 2u;
+    else va[i] = (uint32_t)(r * P.lda + c * 8) * 2u;
     if (BKM) {
-      const int kr = 2 * q + (lane >> 5);
       vb[i] = (uint32_t)(kr * P.ldb + ((lane & 31) ^ gsw(kr)) * 8) * 2u;
     } else {
       vb[i] = (uint32_t)(r * P.ldb + c * 8) * 2u;
@@ -211,14 +229,19 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
   };
   auto dma_plan = [&](const i32x4& sa, const i32x4& sb, int kk, int b) {
     Dma r;
-    r.sa = sa;
-    r.soa = (uint32_t)kk * (BK * 2);
+    if constexpr (AKM) {
+      r.sa = srd_advance(sa, (uint32_t)kk * (uint32_t)(BK * P.lda * 2));
+      r.soa = 0;
+    } else {
+      r.sa = sa;
+      r.soa = (uint32_t)kk * (BK * 2);
+    }
     if constexpr (BKM) {
       r.sb = srd_advance(sb, (uint32_t)kk * (uint32_t)(BK * P.ldb * 2));
       r.sob = 0;
     } else {
       r.sb = sb;
-      r.sob = r.soa;
+      r.sob = (uint32_t)kk * (BK * 2);
     }
     r.ldsb = lds0 + (uint32_t)b * BUF;
     return r;
@@ -236,7 +259,10 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
   const int asw = (int)((arow >> 1) & 7), bsw = (int)((brow >> 1) & 7);
   const uint32_t aoff[2] = {arow * 128u + (uint32_t)((qd ^ asw) << 4), arow * 128u + (uint32_t)(((qd + 4) ^ asw) << 4)};
   const uint32_t boff[2] = {brow * 128u + (uint32_t)((qd ^ bsw) << 4), brow * 128u + (uint32_t)(((qd + 4) ^ bsw) << 4)};
-  auto rd_a = [&](int b, int h, int i) { return lds_ld<bf16x8v>(smem, (uint32_t)b * BUF + aoff[h] + (uint32_t)i * 2048u); };
+  auto rd_a = [&](int b, int h, int i) {
+    if constexpr (AKM) return frag_km16(smem, (uint32_t)b * BUF, 32 * h, wm * 128 + 16 * i, lane);
+    else return lds_ld<bf16x8v>(smem, (uint32_t)b * BUF + aoff[h] + (uint32_t)i * 2048u);
+  };
   auto rd_b = [&](int b, int h, int j) {
     if constexpr (BKM) return frag_km16(smem, (uint32_t)b * BUF + TB, 32 * h, wn * 128 + 16 * j, lane);
     else return lds_ld<bf16x8v>(smem, (uint32_t)b * BUF + TB + boff[h] + (uint32_t)j * 2048u);
@@ -248,10 +274,12 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
   // ---- current / next tile.  The DMA stream runs on across tile boundaries: the last two k-tiles of a tile prefetch
   // the first two of the next, which land while the wave rows run the epilogue.  Persistent mode needs nk >= 2
   // (host-checked); with one tile per workgroup the prefetch past the end is clamped to the last k-tile.
-  int m0, n0, m1 = 0, n1 = 0;
-  tile_mn(0, m0, n0);
-  if (ntw > 1) tile_mn(1, m1, n1);
-  i32x4 sa0 = srd_a(m0), sb0 = srd_b(n0), sa1 = srd_a(m1), sb1 = srd_b(n1);
+  int m0, n0, ks0, m1 = 0, n1 = 0, ks1 = 0;
+  tile_mn(0, m0, n0, ks0);
+  if (ntw > 1) tile_mn(1, m1, n1, ks1);
+  // k-tiles per tile: all of K, or (WG, one tile per workgroup) this split's
+  const int nk = krows(ks0) / BK;
+  i32x4 sa0 = srd_a(m0, ks0), sb0 = srd_b(n0, ks0), sa1 = srd_a(m1, ks1), sb1 = srd_b(n1, ks1);
   // DMA plan for k-tile kt + 2 of tile i (tile-local numbering; >= nk means the next tile) into buffer b
   auto plan_next = [&](int i, int kt, int b) {
     const int kn = kt + 2;
@@ -352,7 +380,8 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
       __builtin_amdgcn_sched_barrier(0);
       if constexpr ((RS & 64) == 0) {
         // after an epilogue its 32 C stores are the youngest VMEM ops (CEF stores fewer: drain everything)
-        if (kt == 0 && g > 0 && !ACC && EPI != W4_EPI_CEF) asm volatile("s_waitcnt vmcnt(32) lgkmcnt(0)" ::: "memory");
+        if (kt == 0 && g > 0 && !ACC && EPI != W4_EPI_CEF && EPI != W4_EPI_WG)
+          asm volatile("s_waitcnt vmcnt(32) lgkmcnt(0)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
       }
@@ -404,7 +433,37 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
     // kernel: tools/gemm_w4_bench.py --ablate).  Stores go through a buffer descriptor over the tile's rows: rows past
     // M fall out of its range, columns past N are pushed out per lane, so every wave issues exactly 32 stores (the
     // vmcnt(32) above counts them).
-    if constexpr (EPI == W4_EPI_CEF) {
+    if constexpr (EPI == W4_EPI_WG) {
+      // ---- weight gradient: acc[i][j] = 4 fp32 of row m0 + wm*128 + 16 i + (l & 15), columns n0 + wn*128 + 16 j +
+      // 4 qd .. + 3 (N % 256 == 0: no column edge) -> this split's slab of ws, or C (one split)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int row = m0 + wm * 128 + 16 * i + rl;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          asm volatile("" : "+a"(acc[i][j]));
+          f32x4 v = acc[i][j];
+          const int col = n0 + wn * 128 + 16 * j + 4 * qd;
+          if (row < P.M) {
+            if (P.splits > 1) {
+              *reinterpret_cast<f32x4*>(P.ws + ((long)ks0 * P.M + row) * P.N + col) = v;
+            } else if (P.c_f32) {
+              float* cp = reinterpret_cast<float*>(P.Cw) + (long)row * P.ldc + col;
+              if (P.beta) v += *reinterpret_cast<const f32x4*>(cp);
+              *reinterpret_cast<f32x4*>(cp) = v;
+            } else {
+              uint16_t* cp = reinterpret_cast<uint16_t*>(P.Cw) + (long)row * P.ldc + col;
+              if (P.beta) {
+                const u16x4 c = *reinterpret_cast<const u16x4*>(cp);
+                v += f32x4{bf2f(c[0]), bf2f(c[1]), bf2f(c[2]), bf2f(c[3])};
+              }
+              *reinterpret_cast<u16x4*>(cp) = u16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+            }
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else if constexpr (EPI == W4_EPI_CEF) {
       // ---- LM-head CE forward: per row of the tile and per 128-column half (this wave's wn), the online-softmax
       // partial {max, sum exp(x - max), sum x} of the valid vocabulary columns; the row's label logit from whichever
       // lane holds that column.  The 4 lanes qd = 0..3 of a row hold its 4 x 8 columns: shuffles over lane >> 4.
@@ -622,13 +681,14 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
     // next tile becomes current
     m0 = m1;
     n0 = n1;
+    ks0 = ks1;
     sa0 = sa1;
     sb0 = sb1;
     if (ti + 1 < ntw) mask_dma(m0, n0);  // the staging rows' reads above returned before their stores issued
     if (ti + 2 < ntw) {
-      tile_mn(ti + 2, m1, n1);
-      sa1 = srd_a(m1);
-      sb1 = srd_b(n1);
+      tile_mn(ti + 2, m1, n1, ks1);
+      sa1 = srd_a(m1, ks1);
+      sb1 = srd_b(n1, ks1);
     }
   } while (++ti < ntw);
   wait_vm<0>();  // clamped prefetches of the last tile may still be landing in LDS
@@ -656,8 +716,8 @@ int launch_rs(const GemmW4Params& p, bool persist, hipStream_t st) {
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
-  const int T = p.tm * p.tn, cus = num_cus() / 8 * 8;
-  const int grid = persist && p.K >= 2 * BK && cus >= 8 && T > cus ? cus : T;
+  const int T = p.tm * p.tn * (EPI == W4_EPI_WG ? p.splits : 1), cus = num_cus() / 8 * 8;
+  const int grid = EPI != W4_EPI_WG && persist && p.K >= 2 * BK && cus >= 8 && T > cus ? cus : T;
   hipLaunchKernelGGL((gemm_w4_kernel<BKM, BIAS, ACC, RS, EPI>), dim3(grid), dim3(NT), lds, st, p);
   DLLM_CHECK_LAUNCH();
   return 0;
@@ -719,6 +779,17 @@ extern "C" int dllm_gemm_w4(const GemmW4Params* pp, int b_kmajor, int persist, i
     }
     if (p.lse == nullptr || p.gscale == nullptr) return -5;
     return launch_rs<false, false, false, 1, W4_EPI_CEB>(p, persist != 0, st);
+  }
+  if (epi == W4_EPI_WG) {
+    // both operands k-major, one tile per workgroup; ws holds `splits` [M][N] fp32 slabs (splits > 1) or C is written
+    if (!b_kmajor || p.accumulate || p.bias || p.N % 256 || p.splits < 1 || p.kchunk < BK || p.kchunk % BK ||
+        (long)p.kchunk * p.splits < p.K || (long)p.kchunk * (p.splits - 1) >= p.K || (p.splits > 1 && p.ws == nullptr) ||
+        (p.splits == 1 && p.Cw == nullptr) || (long)p.tm * p.tn * p.splits > 0x7fffffffL)
+      return -5;
+    // every split's k-major descriptors (k-rows x leading dimension) must fit their 32-bit byte range
+    const long span = ((long)(p.kchunk - 1) * std::max(p.lda, p.ldb) + std::max(p.M, p.N)) * 2;
+    if (span >= 0xFFFFFFFFL) return -6;
+    return launch_rs<true, false, false, 1, W4_EPI_WG>(p, false, st);
   }
   if (epi != W4_EPI_NONE) return -5;
   return b_kmajor ? dispatch<true>(p, persist != 0, st) : dispatch<false>(p, persist != 0, st);

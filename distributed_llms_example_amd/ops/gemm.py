@@ -2,8 +2,9 @@
 
 Who runs what (t5-base / bart-large training step, default settings):
 
-* weight gradients ``dW (+)= dYᵀ X`` (wgrad_accumulate): the hand-written csrc/gemm.hip kernel, accumulating straight
-  into the flat gradient buffer;
+* weight gradients ``dW (+)= dYᵀ X`` (wgrad_accumulate): csrc/gemm_w4.hip's weight-gradient mode (both operands
+  token-major, K split over workgroups, fp32 split slabs summed into the flat gradient buffer by csrc/gemm.hip's
+  split-K pass; round 5, 2-8 % faster than the csrc/gemm.hip kernel it replaced);
 * the FFN input GEMMs with their activation / dropout epilogues and the FFN backward through the activation
   (ops/ffn.py): csrc/gemm_fused.hip and csrc/gemm_w4.hip;
 * the PLAIN projections — forward ``Y = X Wᵀ (+ b)`` and input gradient ``dX (+)= dY W`` of the attention q/k/v/o and
@@ -89,7 +90,8 @@ def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = N
         return out
     return torch.matmul(dy, w)
 
-_VARIANT = int(os.environ.get("DLLM_WGRAD_VARIANT", "-1"))  # -1: pick by K (csrc/gemm.hip)
+# -1: csrc/gemm_w4.hip's weight-gradient mode (csrc/bind.cpp kWgradW4 = 12); 0..11: the csrc/gemm.hip variants (A/B)
+_VARIANT = int(os.environ.get("DLLM_WGRAD_VARIANT", "-1"))
 
 
 def _native_ok(dy2: torch.Tensor, x2: torch.Tensor, out: torch.Tensor) -> bool:

@@ -29,7 +29,7 @@ def _rel(a, b):
     (4096, 768, 768, True, 0),         # t5-base o-proj class
     (2048, 264, 256, True, 3),         # two M tiles, the second 8 rows tall
 ])
-@pytest.mark.parametrize("variant", [0, 9])
+@pytest.mark.parametrize("variant", [0, 9, 12])  # 12: csrc/gemm_w4.hip weight-gradient mode
 def test_gemm_wgrad_fp32_out_ragged_m(K, M, N, beta, splits, variant):
     torch.manual_seed(0)
     a = torch.randn(K, M, device=DEV, dtype=torch.bfloat16)
@@ -43,7 +43,8 @@ def test_gemm_wgrad_fp32_out_ragged_m(K, M, N, beta, splits, variant):
     assert _rel(c, ref) < 1e-5, _rel(c, ref)
 
 
-def test_gemm_wgrad_ragged_m_bf16_out_and_no_overrun():
+@pytest.mark.parametrize("variant,splits", [(9, 0), (12, 0), (12, 1)])
+def test_gemm_wgrad_ragged_m_bf16_out_and_no_overrun(variant, splits):
     """bf16 output, ragged M: rows past M are never written (guard row below the output stays intact)."""
     torch.manual_seed(1)
     K, M, N = 2048, 520, 256
@@ -51,10 +52,31 @@ def test_gemm_wgrad_ragged_m_bf16_out_and_no_overrun():
     b = torch.randn(K, N, device=DEV, dtype=torch.bfloat16)
     big = torch.full((M + 8, N), 7.0, device=DEV, dtype=torch.bfloat16)
     c = big[:M]
-    _ext.native().gemm_wgrad(a, b, c, False, 9, 0)
+    _ext.native().gemm_wgrad(a, b, c, False, variant, splits)
     ref = a.float().t() @ b.float()
     assert _rel(c, ref) < 5e-3
     assert bool((big[M:] == 7.0).all())
+
+
+@pytest.mark.parametrize("splits", [0, 1, 5])
+def test_gemm_wgrad_w4_strided_operands(splits):
+    """w4 weight-gradient mode on strided [K, M] / [K, N] views whose gaps hold NaN: the k-major images' column overrun
+    (past M in the last row tile) reads the gap, which may only reach output rows >= M — never stored; fp32 and bf16
+    accumulate (beta) agree with the fp64 product."""
+    torch.manual_seed(2)
+    K, M, N = 3072, 520, 512
+    af = torch.full((K, M + 72), float("nan"), device=DEV, dtype=torch.bfloat16)
+    bf = torch.full((K, N + 64), float("nan"), device=DEV, dtype=torch.bfloat16)
+    a, b = af[:, :M], bf[:, :N]
+    a.copy_(torch.randn(K, M, device=DEV))
+    b.copy_(torch.randn(K, N, device=DEV))
+    ref = a.double().t() @ b.double()
+    C = _ext.native()
+    for dt, tol in ((torch.float32, 1e-5), (torch.bfloat16, 5e-3)):
+        c0 = torch.randn(M, N, device=DEV).to(dt)
+        c = c0.clone()
+        C.gemm_wgrad(a, b, c, True, 12, splits)
+        assert _rel(c, ref + c0.double()) < tol, (dt, _rel(c, ref + c0.double()))
 
 
 @pytest.mark.parametrize("out_dtype", [torch.float32, torch.bfloat16])
@@ -400,3 +422,19 @@ def test_bart_attention_bias_colsum_matches_column_reduction(sq_force, monkeypat
             off = (gb.data_ptr() - eng.flat.grad_buf.data_ptr()) // gb.element_size()
             mask[off:off + gb.numel()] = False
     assert torch.equal(g1[mask], g0[mask])
+
+
+def test_gemm_wgrad_w4_wide_leading_dim():
+    """A [K, M] view of a 40000-column buffer with one split requested: its k-rows span > 4 GB, past one buffer
+    descriptor's 32-bit range — the binding raises the split count until each split's span fits (csrc/bind.cpp)."""
+    torch.manual_seed(3)
+    K, M, N, LD = 65536, 256, 256, 40000
+    af = torch.empty(K, LD, device=DEV, dtype=torch.bfloat16)
+    a = af[:, :M]
+    a.copy_(torch.randn(K, M, device=DEV))
+    b = torch.randn(K, N, device=DEV, dtype=torch.bfloat16)
+    c = torch.zeros(M, N, device=DEV, dtype=torch.float32)
+    splits = _ext.native().gemm_wgrad(a, b, c, True, 12, 1)
+    assert splits >= 2, splits
+    ref = a.double().t() @ b.double()
+    assert _rel(c, ref) < 1e-5, _rel(c, ref)

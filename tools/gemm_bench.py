@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--variants", default="0,4,9")
     ap.add_argument("--shapes", default=None, help="K:M:N,... (default: the T5/BART training set)")
     ap.add_argument("--no-torch", action="store_true")
+    ap.add_argument("--c-f32", action="store_true", help="fp32 output (the fp32 flat gradient buffer)")
     a = ap.parse_args()
     tunableop.enable(0)
     C = _ext.native()
@@ -41,7 +42,7 @@ def main():
     for K, M, N in shapes:
         dy = torch.randn(K, M, device="cuda", dtype=torch.bfloat16)
         x = torch.randn(K, N, device="cuda", dtype=torch.bfloat16)
-        g = torch.zeros(M, N, device="cuda", dtype=torch.bfloat16)
+        g = torch.zeros(M, N, device="cuda", dtype=torch.float32 if a.c_f32 else torch.bfloat16)
         fl = 2.0 * K * M * N
         rec = {"K": K, "M": M, "N": N}
         if not a.no_torch:
