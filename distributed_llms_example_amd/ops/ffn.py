@@ -38,7 +38,7 @@ import torch.nn.functional as F
 
 from .. import _ext
 from .activations import act_dropout
-from . import streams
+from . import gemm, streams
 from .gemm import bias_grad_accumulate, linear_dgrad, linear_fwd, wgrad_accumulate
 from .linear import _RES_GEMM, _fire, _fusable, _gbuf, _use
 
@@ -141,7 +141,9 @@ class _FusedFFNFn(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:  # post-LN residual (ffn_res): its gradient accumulated by this GEMM (beta = 1)
             if dres is not None and dres.is_contiguous() and dres.dtype == du.dtype and dres.shape == shape:
-                dx = linear_dgrad(du, Wi.detach(), out=dres.view(-1, shape[-1]))
+                # a deferred weight gradient still reads dres (ops/gemm.py WgradDefer): accumulate into a copy
+                acc = dres.clone() if gemm.holds(dres) else dres
+                dx = linear_dgrad(du, Wi.detach(), out=acc.view(-1, shape[-1]))
             else:
                 dx = linear_dgrad(du, Wi.detach())
                 if dres is not None:

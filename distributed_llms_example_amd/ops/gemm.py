@@ -23,6 +23,7 @@ multiples of 64, CPU tensors) go to
 """
 from __future__ import annotations
 
+import contextlib
 import os
 
 import torch
@@ -100,11 +101,100 @@ def _native_ok(dy2: torch.Tensor, x2: torch.Tensor, out: torch.Tensor) -> bool:
     return bool(_ext.native().gemm_wgrad_supported(dy2, x2, out))
 
 
+class WgradDefer:
+    """Weight gradients of a gradient-accumulation window deferred to its last micro-batch.
+
+    With small micro-batches (the reference's train-torchrun default is batch 1 x GA 16, ref/train-torchrun.py:119,126)
+    each weight-gradient GEMM reduces over a few thousand tokens: split over all CUs for occupancy, its fp32 split
+    slabs and their reduction cost as much as the product (profiles/r5_t5base_b8_ga16_summary.txt: wgrad + split-K
+    pass 31 % of the step).  Deferred, every no_sync micro-batch only keeps its (dY, X) operand pairs alive and the
+    last micro-batch runs ONE GEMM per weight over the concatenated tokens of the whole window — the same sum, at the
+    efficiency of a large batch.  Readiness for the gradient reducer is unchanged: a weight's gradient is complete in
+    the last micro-batch's backward, where its hook fires (bucket overlap as before).  The kept operands cost what the
+    activations of one coalesced batch would; ``mem_cap`` bytes allocated ends a window's deferral early (flush)."""
+
+    def __init__(self, mem_cap: int | None = None):
+        self.segs: dict = {}  # (ptr, shape, stride, dtype) of the gradient view -> [out, beta, [(dy2, x2, v), ...]]
+        self.held: set = set()  # storages of kept dY operands: nothing may write into them (holds())
+        self.final = False
+        self.active = True
+        self.mem_cap = mem_cap
+        self.deferred = 0  # operand pairs kept (tests)
+        self.merged = 0    # GEMMs that ran over a concatenated window
+
+    @staticmethod
+    def key(out):
+        return (out.data_ptr(), tuple(out.shape), tuple(out.stride()), out.dtype)
+
+    @staticmethod
+    def operands(parts):
+        """The window's concatenated (dY, X); a kept dY changed in place since (its version moved) fails loudly."""
+        for dy2, _, v in parts:
+            if dy2._version != v:
+                raise RuntimeError("deferred weight-gradient operand modified in place (a writer must check holds())")
+        return torch.cat([p[0] for p in parts]), torch.cat([p[1] for p in parts])
+
+    @torch.no_grad()
+    def flush(self) -> None:
+        """Every pending window now (compute stream): the end of the last micro-batch's backward, or the memory cap."""
+        segs, self.segs = self.segs, {}
+        self.held = set()
+        for out, beta, parts in segs.values():
+            self.merged += 1
+            _wgrad(out, *self.operands(parts), beta)
+
+
+_defer: list = [None]
+
+
+def holds(t: torch.Tensor | None) -> bool:
+    """``t`` shares storage with a kept (deferred) dY operand: a caller about to write into t in place (a dgrad GEMM
+    accumulating into the residual gradient, ops/linear.py / ops/ffn.py) must write elsewhere instead."""
+    d = _defer[0]
+    return bool(t is not None and d is not None and d.held and t.untyped_storage().data_ptr() in d.held)
+
+
+@contextlib.contextmanager
+def defer_wgrads(d: WgradDefer | None, final: bool):
+    """Weight gradients inside go to ``d`` (no_sync micro-batches: kept; ``final``: merged with what was kept)."""
+    prev = _defer[0]
+    _defer[0] = d if d is not None and d.active else None
+    if d is not None:
+        d.final = final
+    try:
+        yield
+    finally:
+        _defer[0] = prev
+
+
 @torch.no_grad()
 def wgrad_accumulate(out: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, beta: bool = True,
-                     async_ok: bool = True) -> torch.Tensor:
+                     async_ok: bool = True, defer: bool = True) -> torch.Tensor:
     """``out (+)= dy2ᵀ @ x2`` with dy2 = [T, M], x2 = [T, N], out = [M, N].  Inside an ops/streams.py scope (and with
-    ``async_ok``: no compute-stream kernel accumulates into ``out`` in the same backward) it runs on the side stream."""
+    ``async_ok``: no compute-stream kernel accumulates into ``out`` in the same backward) it runs on the side stream.
+    Inside :func:`defer_wgrads` the product joins the window's deferred GEMM (:class:`WgradDefer`) — unless ``defer``
+    is False: the caller reuses dy2's memory afterwards (the LM head's vocabulary-chunk scratch)."""
+    d = _defer[0] if defer else None
+    if d is not None:
+        k = WgradDefer.key(out)
+        ent = d.segs.pop(k, None) if (d.final or not beta) else d.segs.get(k)
+        if not beta:
+            ent = None  # overwritten: what was kept no longer counts
+        if not d.final:
+            if ent is None:
+                d.segs[k] = ent = [out, beta, []]
+            ent[2].append((dy2, x2, dy2._version))
+            d.held.add(dy2.untyped_storage().data_ptr())
+            d.deferred += 1
+            return out
+        if ent is not None:
+            parts = ent[2] + [(dy2, x2, dy2._version)]
+            beta = ent[1]
+            d.merged += 1
+            fn = lambda: _wgrad(out, *WgradDefer.operands(parts), beta)  # noqa: E731
+            if async_ok:
+                return streams.run(fn, *[t for p in parts for t in p[:2]])
+            return fn()
     if async_ok:
         return streams.run(lambda: _wgrad(out, dy2, x2, beta), dy2, x2)
     return _wgrad(out, dy2, x2, beta)

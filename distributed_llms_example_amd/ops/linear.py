@@ -119,8 +119,9 @@ class _LinearResFn(torch.autograd.Function):
         dy2 = dy.reshape(-1, dy.shape[-1])
         dx = None
         if ctx.needs_input_grad[0]:
-            if (dres is not None and dres.is_contiguous() and dres.dtype == dy.dtype and dres.shape == x.shape):
-                dx = linear_dgrad(dy, w.detach(), out=dres)
+            if dres is not None and dres.is_contiguous() and dres.dtype == dy.dtype and dres.shape == x.shape:
+                # a deferred weight gradient still reads dres (ops/gemm.py WgradDefer): accumulate into a copy
+                dx = linear_dgrad(dy, w.detach(), out=dres.clone() if gemm.holds(dres) else dres)
             else:
                 dx = linear_dgrad(dy, w.detach())
                 if dres is not None:

@@ -157,7 +157,7 @@ class _LMHeadCEFn(torch.autograd.Function):
             _dh_accumulate(dh, lg, wc)
             with torch.no_grad():
                 if gw is not None:
-                    wgrad_accumulate(gw[c0:c0 + n], lg, h, async_ok=False)  # tied: embed bwd adds too
+                    wgrad_accumulate(gw[c0:c0 + n], lg, h, async_ok=False, defer=False)  # tied: embed bwd adds too
                 elif dw is not None:
                     dw[c0:c0 + n] += torch.mm(lg.t(), h)
         if p is not None:
@@ -203,7 +203,7 @@ class _LMHeadCEFusedFn(torch.autograd.Function):
             _dh_accumulate(dh, lg, wc)
             with torch.no_grad():
                 if gw is not None:
-                    wgrad_accumulate(gw[c0:c0 + n], lg, h, async_ok=False)  # tied: embed bwd adds too
+                    wgrad_accumulate(gw[c0:c0 + n], lg, h, async_ok=False, defer=False)  # tied: embed bwd adds too
                 elif dw is not None:
                     dw[c0:c0 + n] += torch.mm(lg.t(), h)
         if p is not None:

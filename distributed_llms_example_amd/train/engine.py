@@ -12,6 +12,7 @@ import os
 
 import torch
 
+from ..ops import gemm
 from ..ops import rng as rng_mod
 from ..ops import streams
 from ..ops.optim import FusedAdamW
@@ -66,6 +67,30 @@ class TrainEngine:
         self.max_grad_norm = max_grad_norm
         self.label_smoothing = label_smoothing
         self.step_seed: rng_mod.StepSeed | None = None
+        self._init_defer()
+
+    # micro-batches of at most this many input tokens defer their weight gradients to the window's last one
+    DEFER_MAX_TOKENS = 16384
+
+    def _init_defer(self):
+        """Deferred weight gradients for gradient accumulation (ops/gemm.py WgradDefer): ``DLLM_DEFER_WGRAD`` = auto
+        (micro-batches of <= DEFER_MAX_TOKENS input tokens on the GPU), 1 (always), 0 (never).  Kept operands end the
+        window's deferral early past 60 % of the device memory."""
+        cap = None
+        if self.env.device.type == "cuda":
+            cap = int(0.6 * torch.cuda.get_device_properties(self.env.device).total_memory)
+        self.wgrad_defer = gemm.WgradDefer(mem_cap=cap)
+        self._defer_mode = os.environ.get("DLLM_DEFER_WGRAD", "auto").lower()
+        self._ga_k = 0
+
+    def _defer_for(self, batch: dict, grad_accum: int) -> gemm.WgradDefer | None:
+        if grad_accum <= 1 or self._defer_mode in ("0", "off", "false"):
+            return None
+        if self._defer_mode == "auto":
+            ids = batch.get("input_ids")
+            if self.env.device.type != "cuda" or ids is None or ids.numel() > self.DEFER_MAX_TOKENS:
+                return None
+        return self.wgrad_defer
 
     @classmethod
     def from_parts(cls, model: torch.nn.Module, env: DistEnv, flat: FlatParams, reducer: GradReducer | None,
@@ -78,6 +103,7 @@ class TrainEngine:
         eng.flat, eng.reducer, eng.optimizer = flat, reducer, optimizer
         eng.max_grad_norm, eng.label_smoothing = max_grad_norm, label_smoothing
         eng.step_seed = None
+        eng._init_defer()
         return eng
 
     def enable_step_seeds(self, start: int | None = None) -> rng_mod.StepSeed:
@@ -136,7 +162,14 @@ class TrainEngine:
         ids = batch.get("input_ids")
         side = streams.scope(streams.default_enabled(ids.numel() if ids is not None else None) and not hooks_reduce
                              and self.env.device.type == "cuda")
-        with ctx, side:
+        # the accumulation window ends at the synchronising micro-batch, or after grad_accum of them (a graph's split
+        # schedule runs every micro-batch unsynchronised and reduces after the last)
+        self._ga_k += 1
+        last = sync or self._ga_k >= grad_accum
+        if last:
+            self._ga_k = 0
+        dfr = self._defer_for(batch, grad_accum)
+        with ctx, side, gemm.defer_wgrads(dfr, final=last):
             with profiling.range("forward"):
                 out = self.forward(batch)
                 loss = out.loss
@@ -147,6 +180,15 @@ class TrainEngine:
                     (loss * scale).backward()
                 else:
                     (loss / grad_accum if grad_accum > 1 else loss).backward()
+        if last:
+            # weights the last micro-batch did not touch (or all of them, when its size turned deferral off), before
+            # the reducer's post-backward launches their buckets
+            if self.wgrad_defer.segs:
+                self.wgrad_defer.flush()
+            self.wgrad_defer.active = True
+        elif dfr is not None and dfr.mem_cap is not None and torch.cuda.memory_allocated(self.env.device) > dfr.mem_cap:
+            dfr.flush()
+            dfr.active = False  # the rest of this window runs undeferred
         if sync and self.reducer is not None:
             with profiling.range("allreduce(post_backward)"):
                 self.reducer.post_backward()
@@ -157,6 +199,10 @@ class TrainEngine:
         [lr, lr / bc1, 1 / sqrt(bc2)] (graph mode, ops/optim.py device_hyper)."""
         if lr is not None:
             self.optimizer.param_groups[0]["lr"] = lr
+        if self.wgrad_defer.segs:  # a window left open (fewer micro-batches than its grad_accum)
+            self.wgrad_defer.flush()
+        self.wgrad_defer.active = True
+        self._ga_k = 0
         with profiling.range("optimizer(clip+adamw)"):
             norm = self.optimizer.step(self.max_grad_norm, hyper=hyper)
             self.optimizer.zero_grad()

@@ -438,3 +438,29 @@ def test_gemm_wgrad_w4_wide_leading_dim():
     assert splits >= 2, splits
     ref = a.double().t() @ b.double()
     assert _rel(c, ref) < 1e-5, _rel(c, ref)
+
+
+@pytest.mark.parametrize("model", ["t5", "bart"])
+def test_deferred_weight_gradients_gpu(model, monkeypatch):
+    """bf16 on the GPU, side streams on: GA 4 with the weight gradients deferred to the window's last micro-batch (one
+    w4 weight-gradient GEMM over the concatenated tokens) == per-micro-batch GEMMs, up to fp32 summation order."""
+    cfg = _small_cfg()
+    if model == "bart":
+        cfg = resolve_config("bart-large").replace(num_layers=2, num_decoder_layers=2, vocab_size=4096, d_model=512,
+                                                   num_heads=8, d_ff=1024, dropout_rate=0.0, attention_dropout=0.0)
+    torch.manual_seed(0)
+    sd = build_model(cfg).state_dict()
+    mbs = _micro_batches(cfg, n=4, B=2)
+    res = []
+    for mode in ("1", "0"):
+        monkeypatch.setenv("DLLM_DEFER_WGRAD", mode)
+        monkeypatch.setenv("DLLM_WGRAD_STREAM", "1")
+        eng = _engine(cfg, sd, torch.float32)
+        eng.train(False)
+        for i, b in enumerate(mbs):
+            eng.forward_backward(b, grad_accum=4, sync=i == 3)
+        torch.cuda.synchronize()
+        res.append((eng.flat.grad_buf.float().clone(), eng.wgrad_defer.merged))
+    (g1, m1), (g0, m0) = res
+    assert m1 > 0 and m0 == 0
+    assert _rel(g1, g0) < 1e-5, _rel(g1, g0)

@@ -438,3 +438,36 @@ def test_accelerator_train_step_clip_applies_to_the_next_step_only():
 
     a, b = run(True), run(False)
     torch.testing.assert_close(a, b, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("model", ["t5-tiny", "bart-tiny"])
+def test_deferred_weight_gradients_match_per_micro_batch(model, monkeypatch):
+    """Gradient accumulation with the weight gradients deferred to the window's last micro-batch (ops/gemm.py
+    WgradDefer: one GEMM over the concatenated tokens) == one GEMM per micro-batch; the deferral really ran; the last
+    window (here shorter than grad_accum) is flushed by step()."""
+    from distributed_llms_example_amd.parallel.env import init_distributed
+    from distributed_llms_example_amd.train.engine import TrainEngine
+    env = init_distributed(cpu=True)
+    g = torch.Generator().manual_seed(1)
+    mbs = [{"input_ids": torch.randint(3, 500, (2, 12), generator=g), "attention_mask": torch.ones(2, 12, dtype=torch.long),
+            "labels": torch.randint(3, 500, (2, 6), generator=g)} for _ in range(4)]
+    torch.manual_seed(0)
+    sd = build_model(model).state_dict()
+    res = []
+    for mode in ("1", "0"):
+        monkeypatch.setenv("DLLM_DEFER_WGRAD", mode)
+        m = build_model(model)
+        m.load_state_dict(sd)
+        e = TrainEngine(m, env, dtype=torch.float32).train(False)
+        for i, b in enumerate(mbs):
+            e.forward_backward(b, grad_accum=4, sync=i == 3)
+        res.append((e.flat.grad_buf.clone(), e.wgrad_defer.deferred, e.wgrad_defer.merged))
+        # an open window: two micro-batches of a grad_accum=4 window, then the optimizer step flushes them
+        for b in mbs[:2]:
+            e.forward_backward(b, grad_accum=4, sync=False)
+        assert (len(e.wgrad_defer.segs) > 0) == (mode == "1")
+        e.step()
+        assert not e.wgrad_defer.segs
+    (g1, d1, m1), (g0, d0, m0) = res
+    assert d1 > 0 and m1 > 0 and d0 == 0 and m0 == 0, (d1, m1, d0, m0)
+    torch.testing.assert_close(g1, g0, atol=1e-6, rtol=1e-4)
