@@ -742,6 +742,73 @@ int64_t gemm_wgrad(const Tensor& a, const Tensor& b, Tensor& c, bool beta, int64
   return splits;
 }
 
+// c[M][N] (+)= sum_i a_i^T b_i over the deferred micro-batches of a gradient-accumulation window (ops/gemm.py
+// WgradDefer): equal-shaped token-major segments a_i = [rows][M], b_i = [rows][N] (up to W4_MAX_SEGS), read in place
+// by the w4 weight-gradient mode — each segment cut into seg_chunks splits, split-K slabs as gemm_wgrad.  Returns the
+// split count.
+int64_t gemm_wgrad_segs(const std::vector<Tensor>& as, const std::vector<Tensor>& bs, Tensor& c, bool beta) {
+  const int nseg = (int)as.size();
+  TORCH_CHECK(nseg >= 1 && nseg <= W4_MAX_SEGS && (int)bs.size() == nseg, "gemm_wgrad_segs: 1..", W4_MAX_SEGS,
+              " (a, b) segment pairs");
+  for (int i = 0; i < nseg; ++i) {
+    TORCH_CHECK(gemm_wgrad_supported(as[i], bs[i], c), "gemm_wgrad_segs: segment ", i, " unsupported");
+    TORCH_CHECK(as[i].sizes() == as[0].sizes() && bs[i].sizes() == bs[0].sizes() &&
+                    as[i].stride(0) == as[0].stride(0) && bs[i].stride(0) == bs[0].stride(0) &&
+                    as[i].device() == c.device() && bs[i].device() == c.device(),
+                "gemm_wgrad_segs: segments must share shapes, leading dimensions and device");
+  }
+  const int rows = as[0].size(0), M = as[0].size(1), N = bs[0].size(1);
+  GemmW4Params Q{};
+  Q.lda = as[0].stride(0);
+  Q.ldb = bs[0].stride(0);
+  Q.ldc = c.stride(0);
+  Q.M = M;
+  Q.N = N;
+  Q.K = rows * nseg;
+  Q.tm = (M + 255) / 256;
+  Q.tn = N / 256;
+  Q.grp = 8;
+  for (int i = 0; i < nseg; ++i) {
+    Q.segA[i] = reinterpret_cast<const uint16_t*>(as[i].data_ptr());
+    Q.segB[i] = reinterpret_cast<const uint16_t*>(bs[i].data_ptr());
+  }
+  // the split count gemm_wgrad would pick for the window's whole K, spread over the segments
+  const int want = wgrad_splits(Q.tm * Q.tn, Q.K);
+  int chunks = std::max(1, std::min((want + nseg / 2) / nseg, rows / 64));
+  int kchunk = ((rows + chunks - 1) / chunks + 63) / 64 * 64;
+  const long ld = std::max(Q.lda, Q.ldb), wd = std::max(M, N);
+  while (kchunk > 64 && ((long)(kchunk - 1) * ld + wd) * 2 >= 0xFFFFFFFFL) kchunk -= 64;
+  TORCH_CHECK(((long)(kchunk - 1) * ld + wd) * 2 < 0xFFFFFFFFL, "gemm_wgrad_segs: leading dimension too large");
+  chunks = (rows + kchunk - 1) / kchunk;
+  Q.nseg = nseg;
+  Q.seg_rows = rows;
+  Q.seg_chunks = chunks;
+  Q.kchunk = kchunk;
+  Q.splits = nseg * chunks;
+  Q.c_f32 = c.scalar_type() == at::kFloat ? 1 : 0;
+  Q.beta = beta ? 1 : 0;
+  Q.Cw = c.data_ptr();
+  Tensor ws;
+  if (Q.splits > 1) {
+    ws = at::empty({(int64_t)Q.splits * M * N}, as[0].options().dtype(at::kFloat));
+    Q.ws = ws.data_ptr<float>();
+  }
+  check_rc(dllm_gemm_w4(&Q, 1, 0, 10, stream()), "gemm_wgrad_segs (w4)");
+  if (Q.splits > 1) {
+    GemmWgradParams P{};
+    P.ws = Q.ws;
+    P.C = c.data_ptr();
+    P.ldc = Q.ldc;
+    P.M = M;
+    P.N = N;
+    P.splits = Q.splits;
+    P.beta = Q.beta;
+    P.c_f32 = Q.c_f32;
+    check_rc(dllm_wgrad_reduce(&P, stream()), "gemm_wgrad_segs split-K reduce");
+  }
+  return Q.splits;
+}
+
 // c[M][N] = epi(a[M][K] . b) with b = [N][K] (nn.Linear weight, b_kmajor = false) or [K][N] (b_kmajor = true).
 // epi (csrc/gemm_fused.hip): 0 none, 1 relu, 2 gelu-erf, 3 d-relu, 4 d-gelu-erf, 5 gelu-tanh, 6 d-gelu-tanh.
 // Forward activations apply dropout(p, seed) on the output element index m * N + n (ops/rng.py); the GELU
@@ -1224,6 +1291,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("lse"), py::arg("kpm"), py::arg("lut"), py::arg("scale"), py::arg("causal"), py::arg("p"),
         py::arg("seed"), py::arg("need_dlut"), py::arg("dq_out") = py::none(), py::arg("dk_out") = py::none(),
         py::arg("dv_out") = py::none());
+  m.def("gemm_wgrad_segs", &gemm_wgrad_segs, "c (+)= sum_i a_i^T b_i (deferred micro-batch segments, w4)",
+        py::arg("a"), py::arg("b"), py::arg("c"), py::arg("beta") = true);
   m.def("gemm_wgrad", &gemm_wgrad, "c (+)= a^T b (token-major bf16 operands)", py::arg("a"), py::arg("b"), py::arg("c"),
         py::arg("beta") = true, py::arg("variant") = 0, py::arg("splits") = 0);
   m.def("gemm_wgrad_supported", &gemm_wgrad_supported);

@@ -17,6 +17,8 @@ struct GemmWgradParams {
   int c_f32;  // C is fp32 (fp32 gradient accumulation across micro-batches), else bf16
 };
 
+#define W4_MAX_SEGS 32
+
 // csrc/gemm_w4.hip: C[M][N] (+)= A[M][K] . B (+ bias), B = [N][K] (b_kmajor = 0) or [K][N] (b_kmajor = 1).
 // Ragged M and N (loads past the edge return 0 through the buffer descriptor's range check, stores are masked);
 // K % 64 == 0.
@@ -58,6 +60,12 @@ struct GemmW4Params {
   float* ws;
   void* Cw;
   int splits, kchunk, c_f32, beta;
+  // ... over the deferred micro-batches of a gradient-accumulation window (nseg > 0, ops/gemm.py WgradDefer): split ks
+  // reads segment ks / seg_chunks (A = segA[], B = segB[], seg_rows k-rows each, leading dimensions lda / ldb), k-rows
+  // [(ks % seg_chunks) kchunk, + kchunk); A / B / K unused.  No concatenated copy of the window's operands.
+  const uint16_t* segA[W4_MAX_SEGS];
+  const uint16_t* segB[W4_MAX_SEGS];
+  int nseg, seg_rows, seg_chunks;
 };
 
 // csrc/gemm_fused.hip: C[M][N] = epi(A[M][K] . B), B = [N][K] (b_kmajor = 0) or [K][N] (b_kmajor = 1)

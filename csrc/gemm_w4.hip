@@ -185,17 +185,27 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
     m0 = mb * 256;
     n0 = nb * 256;
   };
-  // k-rows of split ks (WG) / all of K
-  auto krows = [&](int ks) { return AKM ? min(P.kchunk, P.K - ks * P.kchunk) : P.K; };
+  // k-rows of split ks (WG: of K, or of its deferred segment) / all of K; first k-row of the split's operands
+  auto krows = [&](int ks) {
+    if (!AKM) return P.K;
+    return P.nseg > 0 ? min(P.kchunk, P.seg_rows - (ks % P.seg_chunks) * P.kchunk) : min(P.kchunk, P.K - ks * P.kchunk);
+  };
+  auto a_at = [&](int ks) {
+    return P.nseg > 0 ? P.segA[ks / P.seg_chunks] + (long)(ks % P.seg_chunks) * P.kchunk * P.lda
+                      : P.A + (long)ks * P.kchunk * P.lda;
+  };
+  auto b_at = [&](int ks) {
+    if (!AKM) return P.B;
+    return P.nseg > 0 ? P.segB[ks / P.seg_chunks] + (long)(ks % P.seg_chunks) * P.kchunk * P.ldb
+                      : P.B + (long)ks * P.kchunk * P.ldb;
+  };
   // k-major descriptors span the split's k-rows of the view (column overrun: see the DMA offsets below)
   auto srd_a = [&](int m0, int ks) {
-    return AKM ? make_srd(P.A + (long)ks * P.kchunk * P.lda + m0,
-                          (uint32_t)(((long)(krows(ks) - 1) * P.lda + P.M - m0) * 2))
+    return AKM ? make_srd(a_at(ks) + m0, (uint32_t)(((long)(krows(ks) - 1) * P.lda + P.M - m0) * 2))
                : make_srd(P.A + (long)m0 * P.lda, (uint32_t)(min(P.M - m0, 256) * P.lda * 2));
   };
   auto srd_b = [&](int n0, int ks) {
-    return BKM ? make_srd(P.B + (long)(AKM ? ks * P.kchunk : 0) * P.ldb + n0,
-                          (uint32_t)(((long)(krows(ks) - 1) * P.ldb + P.N - n0) * 2))
+    return BKM ? make_srd(b_at(ks) + n0, (uint32_t)(((long)(krows(ks) - 1) * P.ldb + P.N - n0) * 2))
                : make_srd(P.B + (long)n0 * P.ldb, (uint32_t)(min(P.N - n0, 256) * P.ldb * 2));
   };
 
@@ -783,9 +793,18 @@ extern "C" int dllm_gemm_w4(const GemmW4Params* pp, int b_kmajor, int persist, i
   if (epi == W4_EPI_WG) {
     // both operands k-major, one tile per workgroup; ws holds `splits` [M][N] fp32 slabs (splits > 1) or C is written
     if (!b_kmajor || p.accumulate || p.bias || p.N % 256 || p.splits < 1 || p.kchunk < BK || p.kchunk % BK ||
-        (long)p.kchunk * p.splits < p.K || (long)p.kchunk * (p.splits - 1) >= p.K || (p.splits > 1 && p.ws == nullptr) ||
-        (p.splits == 1 && p.Cw == nullptr) || (long)p.tm * p.tn * p.splits > 0x7fffffffL)
+        (p.splits > 1 && p.ws == nullptr) || (p.splits == 1 && p.Cw == nullptr) ||
+        (long)p.tm * p.tn * p.splits > 0x7fffffffL)
       return -5;
+    if (p.nseg > 0) {  // deferred segments: seg_chunks splits of kchunk rows cover each segment exactly
+      if (p.nseg > W4_MAX_SEGS || p.seg_chunks < 1 || p.splits != p.nseg * p.seg_chunks || p.seg_rows % BK ||
+          (long)p.kchunk * p.seg_chunks < p.seg_rows || (long)p.kchunk * (p.seg_chunks - 1) >= p.seg_rows)
+        return -5;
+      for (int i = 0; i < p.nseg; ++i)
+        if (p.segA[i] == nullptr || p.segB[i] == nullptr) return -5;
+    } else if ((long)p.kchunk * p.splits < p.K || (long)p.kchunk * (p.splits - 1) >= p.K) {
+      return -5;
+    }
     // every split's k-major descriptors (k-rows x leading dimension) must fit their 32-bit byte range
     const long span = ((long)(p.kchunk - 1) * std::max(p.lda, p.ldb) + std::max(p.M, p.N)) * 2;
     if (span >= 0xFFFFFFFFL) return -6;

@@ -127,12 +127,23 @@ class WgradDefer:
         return (out.data_ptr(), tuple(out.shape), tuple(out.stride()), out.dtype)
 
     @staticmethod
-    def operands(parts):
-        """The window's concatenated (dY, X); a kept dY changed in place since (its version moved) fails loudly."""
+    def run(out, parts, beta):
+        """``out (+)= Σ dY_iᵀ X_i`` over the window: the w4 weight-gradient kernel reading every kept segment in place
+        (csrc/bind.cpp gemm_wgrad_segs; equal-shaped segments, 32 per launch), else one GEMM over the concatenated
+        operands.  A kept dY changed in place since it was kept (its version moved) fails loudly."""
         for dy2, _, v in parts:
             if dy2._version != v:
                 raise RuntimeError("deferred weight-gradient operand modified in place (a writer must check holds())")
-        return torch.cat([p[0] for p in parts]), torch.cat([p[1] for p in parts])
+        dys, xs = [p[0] for p in parts], [p[1] for p in parts]
+        d0, x0 = dys[0], xs[0]
+        if (_VARIANT in (-1, 12) and _native_ok(d0, x0, out)
+                and all(d.shape == d0.shape and d.stride() == d0.stride() for d in dys)
+                and all(x.shape == x0.shape and x.stride() == x0.stride() for x in xs)):
+            C = _ext.native()
+            for g in range(0, len(dys), 32):
+                C.gemm_wgrad_segs(dys[g:g + 32], xs[g:g + 32], out, beta or g > 0)
+            return out
+        return _wgrad(out, torch.cat(dys), torch.cat(xs), beta)
 
     @torch.no_grad()
     def flush(self) -> None:
@@ -141,7 +152,7 @@ class WgradDefer:
         self.held = set()
         for out, beta, parts in segs.values():
             self.merged += 1
-            _wgrad(out, *self.operands(parts), beta)
+            self.run(out, parts, beta)
 
 
 _defer: list = [None]
@@ -191,7 +202,7 @@ def wgrad_accumulate(out: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, bet
             parts = ent[2] + [(dy2, x2, dy2._version)]
             beta = ent[1]
             d.merged += 1
-            fn = lambda: _wgrad(out, *WgradDefer.operands(parts), beta)  # noqa: E731
+            fn = lambda: WgradDefer.run(out, parts, beta)  # noqa: E731
             if async_ok:
                 return streams.run(fn, *[t for p in parts for t in p[:2]])
             return fn()

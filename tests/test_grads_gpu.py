@@ -464,3 +464,20 @@ def test_deferred_weight_gradients_gpu(model, monkeypatch):
     (g1, m1), (g0, m0) = res
     assert m1 > 0 and m0 == 0
     assert _rel(g1, g0) < 1e-5, _rel(g1, g0)
+
+
+@pytest.mark.parametrize("nseg,rows,M,N", [(5, 1024, 520, 512), (16, 192, 768, 768), (32, 64, 256, 256)])
+def test_gemm_wgrad_segs_matches_fp64(nseg, rows, M, N):
+    """The w4 weight-gradient mode over deferred micro-batch segments read in place (csrc/bind.cpp gemm_wgrad_segs):
+    Σ_i a_iᵀ b_i + C for fp32 / bf16 C, ragged M, strided segments."""
+    torch.manual_seed(4)
+    af = torch.randn(nseg, rows, M + 8, device=DEV, dtype=torch.bfloat16)
+    bs = [torch.randn(rows, N, device=DEV, dtype=torch.bfloat16) for _ in range(nseg)]
+    as_ = [af[i, :, :M] for i in range(nseg)]
+    ref = sum(a.double().t() @ b.double() for a, b in zip(as_, bs))
+    C = _ext.native()
+    for dt, tol in ((torch.float32, 1e-5), (torch.bfloat16, 5e-3)):
+        c0 = torch.randn(M, N, device=DEV).to(dt)
+        c = c0.clone()
+        C.gemm_wgrad_segs(as_, bs, c, True)
+        assert _rel(c, ref + c0.double()) < tol, (dt, _rel(c, ref + c0.double()))
