@@ -54,6 +54,7 @@ int dllm_ce_chunk_bwd(const float*, void*, long, const int64_t*, const float*, c
 int dllm_embed_bwd(const int64_t*, const int64_t*, const void*, long, long, int, float*, void*, long, long, int,
                    hipStream_t);
 int dllm_colsum_acc(const void*, long, long, int, float*, void*, int, hipStream_t);
+int dllm_colsum_partials_acc(const float*, void*, int, int, int, hipStream_t);
 int dllm_ce_merge(const float*, int, long, const float*, const int64_t*, float*, float*, long, int, float, long,
                   hipStream_t);
 int dllm_kv_reorder(void*, const int64_t*, int, int, int, int, int, int, hipStream_t);
@@ -156,7 +157,7 @@ std::vector<Tensor> norm_bwd(const optional<Tensor>& dout_o, const optional<Tens
   Tensor db = (has_b && !acc) ? at::zeros({d}, f32) : Tensor();
   // column sums of dx (the upstream linear layer's bias gradient), fp32 [d]
   Tensor dxs_part = want_colsum ? at::empty({G, d}, f32) : Tensor();
-  Tensor dxs = want_colsum ? at::zeros({d}, f32) : Tensor();
+  // the dx column sums stay per-block partials: the consuming bias gradient reduces them (ops/gemm.py, one kernel)
   if (N > 0)
     check_rc(dllm_norm_bwd(dout.data_ptr(), dse.defined() ? dse.data_ptr() : nullptr, s.data_ptr(), w.data_ptr(),
                            kind == 1 ? mean->data_ptr<float>() : nullptr, rstd.data_ptr<float>(), dx.data_ptr(),
@@ -165,10 +166,10 @@ std::vector<Tensor> norm_bwd(const optional<Tensor>& dout_o, const optional<Tens
                            (has_b && !acc) ? db.data_ptr<float>() : nullptr, acc ? dw_acc->data_ptr() : nullptr,
                            (acc && has_b) ? db_acc->data_ptr() : nullptr,
                            want_colsum ? dxs_part.data_ptr<float>() : nullptr,
-                           want_colsum ? dxs.data_ptr<float>() : nullptr, N, d, (float)p, (uint32_t)seed, (int)kind,
+                           nullptr, N, d, (float)p, (uint32_t)seed, (int)kind,
                            is_bf16(s), acc && dw_acc->scalar_type() == at::kFloat, stream()),
              "norm_bwd");
-  return {dx, dstream, dw, db, dxs};
+  return {dx, dstream, dw, db, dxs_part};
 }
 
 // ------------------------------------------------------------------------------------------- activations
@@ -1194,6 +1195,17 @@ Tensor gemm_dgeglu(const Tensor& dy, const Tensor& wo, const Tensor& g1, const T
 }
 
 // out (+)= column sums of x ([T, N] bf16, unit inner stride): bias gradients accumulated in place
+void colsum_partials_acc(const Tensor& part, Tensor& out) {
+  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.dim() == 2 && part.is_contiguous() &&
+                  out.is_cuda() && out.is_contiguous() && out.numel() == part.size(1) &&
+                  (out.scalar_type() == at::kFloat || out.scalar_type() == at::kBFloat16),
+              "colsum_partials_acc: part fp32 [G, d] contiguous, out fp32/bf16 [d] contiguous");
+  TORCH_CHECK(part.size(0) < INT_MAX && part.size(1) < INT_MAX, "colsum_partials_acc: too large");
+  check_rc(dllm_colsum_partials_acc(part.data_ptr<float>(), out.data_ptr(), out.scalar_type() == at::kBFloat16 ? 1 : 0,
+                                    (int)part.size(0), (int)part.size(1), stream()),
+           "colsum_partials_acc");
+}
+
 void colsum_acc(const Tensor& x, Tensor& out) {
   check_gpu(x, "x");
   TORCH_CHECK(x.dim() == 2 && x.scalar_type() == at::kBFloat16 && x.stride(1) == 1 && x.stride(0) % 2 == 0 &&
@@ -1314,6 +1326,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_w4_supported", &gemm_w4_supported);
   m.def("beam_topk", &beam_topk);
   m.def("kv_reorder", &kv_reorder);
+  m.def("colsum_partials_acc", &colsum_partials_acc, "out += part.sum(0) for fp32 partial column sums [G, d]");
   m.def("colsum_acc", &colsum_acc, "out += x.sum(0) for a token-major bf16 x (bias gradients)");
   dllm::bind_reducer(m);
   m.attr("arch") = "gfx950";

@@ -285,7 +285,7 @@ int launch_bwd(const void* dout, const void* ds_extra, const void* s, const void
   else return -1;
 #undef L
   DLLM_CHECK_LAUNCH();
-  if (dxs_part != nullptr)  // dx column sums -> dxs (fp32, pre-zeroed)
+  if (dxs_part != nullptr && dxs != nullptr)  // dx column sums -> dxs (fp32, pre-zeroed); else the caller reduces
     hipLaunchKernelGGL(col_sum_acc_kernel<float>, dim3((d + 63) / 64), dim3(1024), 0, st, dxs_part, dxs, G, d);
   if (dw_acc != nullptr && acc_f32) {  // fp32 flat gradient buffer
     hipLaunchKernelGGL(col_sum_acc_kernel<float>, dim3((d + 63) / 64), dim3(1024), 0, st, dw_part, (float*)dw_acc, G,
@@ -329,6 +329,17 @@ static int norm_bwd_cap() {
     return v > 0 ? v : 512;
   }();
   return cap;
+}
+
+// out[col] (+)= sum of the G rows of part [G][d] (fp32 partial column sums handed to a bias gradient, ops/gemm.py)
+extern "C" int dllm_colsum_partials_acc(const float* part, void* out, int out_is_bf16, int G, int d, hipStream_t st) {
+  if (G <= 0 || d <= 0) return -4;
+  if (out_is_bf16)
+    hipLaunchKernelGGL(col_sum_acc_kernel<uint16_t>, dim3((d + 63) / 64), dim3(1024), 0, st, part, (uint16_t*)out, G, d);
+  else
+    hipLaunchKernelGGL(col_sum_acc_kernel<float>, dim3((d + 63) / 64), dim3(1024), 0, st, part, (float*)out, G, d);
+  DLLM_CHECK_LAUNCH();
+  return 0;
 }
 
 extern "C" int dllm_norm_bwd_grid(int N) {

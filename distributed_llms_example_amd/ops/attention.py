@@ -206,12 +206,12 @@ class _AttnFn(torch.autograd.Function):
             rq, rk, rv, dlut = C.attn_bwd(do.contiguous(), q, k, v, o, lse, kpm, lut, float(scale), bool(causal),
                                           float(p), int(seed), bool(need_dlut), dq, dk, dv, dmask, sat_lo, sat_hi,
                                           csq, csk, csv)
-        if part is not None:
-            colsum_record(da, part.sum(0))
+        if part is not None:  # per-block partials, reduced by the consumer into the bias gradient (ops/gemm.py)
+            colsum_record(da, part)
         if pq is not None:
-            colsum_record(da, pq.sum(0))
+            colsum_record(da, pq)
         if pkv is not None:
-            colsum_record(db, pkv.sum(0))
+            colsum_record(db, pkv)
         if mode == "sep":
             da, db, dc = rq, rk, rv
         streams.pair_join()  # side-stream weight gradients paired with these VALU-bound kernels (ops/streams.py)

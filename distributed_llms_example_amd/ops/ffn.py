@@ -151,8 +151,7 @@ class _FusedFFNFn(torch.autograd.Function):
         with torch.no_grad():
             wgrad_accumulate(_gbuf(Wi), du, x2, async_ok=streams.site_ok(Wi))
             if bsum is not None:
-                gb = _gbuf(Bi)
-                gb.add_(bsum.sum(0).to(gb.dtype))
+                gemm.colsum_partials_acc(_gbuf(Bi), bsum)  # the GELU backward GEMM's per-128-row partials
             elif Bi is not None:
                 bias_grad_accumulate(_gbuf(Bi), du, async_ok=streams.site_ok(Bi))
         _fire(Wi)

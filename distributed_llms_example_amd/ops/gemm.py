@@ -237,18 +237,29 @@ def bias_grad_accumulate(out: torch.Tensor, dy2: torch.Tensor, dy: torch.Tensor 
     if cs is not None:
         colsum_handoffs += 1
         if not async_ok:
-            return out.add_(cs.view_as(out).to(out.dtype))
-        return streams.run(lambda: out.add_(cs.view_as(out).to(out.dtype)), cs)
+            return colsum_partials_acc(out, cs)
+        return streams.run(lambda: colsum_partials_acc(out, cs), cs)
     if not async_ok:
         return _colsum(out, dy2)
     return streams.run(lambda: _colsum(out, dy2), dy2)
 
 
 def colsum_record(t: torch.Tensor, cs: torch.Tensor) -> None:
-    """Attach ``cs`` = fp32 ``t.reshape(-1, n).sum(0)``, computed by t's producer on the way (the BART post-LN backward
-    kernel, ops/norms.py; the attention backward kernels' dQ / dK / dV epilogues, ops/attention.py), for the bias
-    gradient of the linear layer that consumes t's gradient (:func:`bias_grad_accumulate`)."""
+    """Attach ``cs`` = fp32 partial column sums [G, n] of ``t.reshape(-1, n)`` (rows summing to its column sum),
+    computed by t's producer on the way (the BART post-LN backward kernel, ops/norms.py; the attention backward kernels'
+    dQ / dK / dV epilogues, ops/attention.py), for the bias gradient of the linear layer that consumes t's gradient
+    (:func:`bias_grad_accumulate`: one reduce-and-accumulate kernel)."""
     t._dllm_colsum = (cs, t._version, t.numel(), t.data_ptr())
+
+
+def colsum_partials_acc(out: torch.Tensor, part: torch.Tensor) -> torch.Tensor:
+    """``out += part.sum(0)`` (fp32 partials [G, n] into an fp32 / bf16 [n] gradient): csrc/norm.hip's column
+    reduction straight into the flat gradient buffer."""
+    part = part.reshape(-1, out.numel())
+    if part.is_cuda and out.is_contiguous() and part.is_contiguous() and out.dtype in (torch.float32, torch.bfloat16):
+        _ext.native().colsum_partials_acc(part, out.view(-1))
+        return out
+    return out.add_(part.sum(0).view_as(out).to(out.dtype))
 
 
 def colsum_of(dy: torch.Tensor | None, n: int) -> torch.Tensor | None:
@@ -264,7 +275,7 @@ def colsum_of(dy: torch.Tensor | None, n: int) -> torch.Tensor | None:
     if rec is None:
         return None
     cs, ver, numel, ptr = rec
-    if cs.numel() == n and dy._version == ver and dy.numel() == numel and dy.data_ptr() == ptr:
+    if cs.shape[-1] == n and dy._version == ver and dy.numel() == numel and dy.data_ptr() == ptr:
         return cs
     return None
 

@@ -251,7 +251,8 @@ class _StackedFn(torch.autograd.Function):
                 cs = [colsum_of(g, n) for g in grads]
                 if gb is not None and all(c is not None for c in cs):
                     gemm.colsum_handoffs += len(cs)
-                    gb.add_(torch.cat(cs).view_as(gb).to(gb.dtype))
+                    for l, c in enumerate(cs):
+                        gemm.colsum_partials_acc(gb[l * n:(l + 1) * n], c)
                 elif gb is not None:
                     bias_grad_accumulate(gb, G2)
                 else:
