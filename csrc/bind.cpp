@@ -1070,7 +1070,8 @@ bool gemm_w4_supported(const Tensor& a, const Tensor& b, bool b_kmajor) {
 // that mask (NN).  mask: int32 tensor of >= ceil(M/256) * ceil(N/256) * 2048 words (gemm_w4_mask_words).
 Tensor gemm_w4(const Tensor& a, const Tensor& b, bool b_kmajor, const optional<Tensor>& bias, const optional<Tensor>& out,
                bool accumulate, int64_t grp, bool persist, int64_t epi, double p, int64_t seed,
-               const optional<Tensor>& mask, bool mask_pp) {
+               const optional<Tensor>& mask, bool mask_pp, const optional<Tensor>& aux,
+               const optional<Tensor>& aux_out, const optional<Tensor>& colsum) {
   TORCH_CHECK(gemm_w4_supported(a, b, b_kmajor),
               "gemm_w4: need bf16 GPU a [M,K], b [N,K] (or [K,N] k-major), unit inner stride, 16-B aligned rows, K % 64 == 0, "
               "N % 8 == 0");
@@ -1108,7 +1109,34 @@ Tensor gemm_w4(const Tensor& a, const Tensor& b, bool b_kmajor, const optional<T
   P.tn = (int)((N + 255) / 256);
   P.grp = grp >= 0 ? (int)grp : 8;  // tile-group sweep: profiles/r3_gemm_w4_grp_sweep.txt
   P.accumulate = accumulate ? 1 : 0;
-  if (epi != 0) {
+  if (epi == 11 || epi == 12) {
+    // GELU FFN (csrc/gemm_w4.hip W4_EPI_GELU / W4_EPI_DGELU): bf16 [M, N] derivative out (forward) / in (backward),
+    // and the backward's fp32 [M / 128, N] dU column partials
+    const optional<Tensor>& x = epi == 11 ? aux_out : aux;
+    TORCH_CHECK(x.has_value() && x->defined() && x->is_cuda() && x->device() == a.device() &&
+                    x->scalar_type() == at::kBFloat16 && x->dim() == 2 && x->size(0) == M && x->size(1) == N &&
+                    x->stride(1) == 1 && x->stride(0) % 8 == 0 && reinterpret_cast<uintptr_t>(x->data_ptr()) % 16 == 0 &&
+                    256 * x->stride(0) * 2 < (1LL << 31),
+                "gemm_w4: GELU epilogues need a bf16 [M, N] aux tensor with 16-B aligned rows");
+    TORCH_CHECK(M * N < (1LL << 32), "gemm_w4: dropout element index must fit 32 bits");
+    TORCH_CHECK(p >= 0.0 && p < 1.0, "gemm_w4: dropout p in [0, 1)");
+    P.ldaux = x->stride(0);
+    if (epi == 11) {
+      P.aux_out = reinterpret_cast<uint16_t*>(x->data_ptr());
+    } else {
+      P.aux = reinterpret_cast<const uint16_t*>(x->data_ptr());
+      TORCH_CHECK(colsum.has_value() && colsum->defined() && colsum->is_cuda() &&
+                      colsum->scalar_type() == at::kFloat && colsum->is_contiguous() && M % 128 == 0 &&
+                      colsum->numel() == (M / 128) * N && reinterpret_cast<uintptr_t>(colsum->data_ptr()) % 16 == 0,
+                  "gemm_w4: GELU backward needs an fp32 contiguous [M / 128, N] colsum tensor (M % 128 == 0)");
+      P.colsum = colsum->data_ptr<float>();
+    }
+    P.p = (float)p;
+    P.scale = p > 0.0 ? (float)(1.0 / (1.0 - p)) : 1.f;
+    P.seed = (uint32_t)seed;
+    const double t = p * 65536.0;  // csrc/common.h drop_threshold
+    P.thr = t >= 65535.0 ? 0xFFFFu : (uint32_t)t;
+  } else if (epi != 0) {
     TORCH_CHECK(mask.has_value() && mask->defined() && mask->is_cuda() && mask->device() == a.device() &&
                     mask->scalar_type() == at::kInt && mask->is_contiguous() &&
                     mask->numel() >= (int64_t)P.tm * P.tn * 2048 && reinterpret_cast<uintptr_t>(mask->data_ptr()) % 16 == 0,
@@ -1319,7 +1347,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_w4", &gemm_w4, "out (+)= a . b (+ bias) on the one-wave-per-SIMD GEMM (csrc/gemm_w4.hip)", py::arg("a"),
         py::arg("b"), py::arg("b_kmajor"), py::arg("bias") = py::none(), py::arg("out") = py::none(),
         py::arg("accumulate") = false, py::arg("grp") = -1, py::arg("persist") = true, py::arg("epi") = 0,
-        py::arg("p") = 0.0, py::arg("seed") = 0, py::arg("mask") = py::none(), py::arg("mask_pp") = false);
+        py::arg("p") = 0.0, py::arg("seed") = 0, py::arg("mask") = py::none(), py::arg("mask_pp") = false,
+        py::arg("aux") = py::none(), py::arg("aux_out") = py::none(), py::arg("colsum") = py::none());
   m.def("gemm_w4_mask_words", &gemm_w4_mask_words);
   m.def("lmhead_ce_fwd", &lmhead_ce_fwd, "LM-head GEMM + CE forward (gemm_w4 CE epilogue + row merge): (loss_rows, lse)");
   m.def("lmhead_ce_bwd_slice", &lmhead_ce_bwd_slice, "dlogits of one vocabulary slice from the GEMM's CE epilogue");

@@ -63,6 +63,12 @@ struct GemmW4Params {
   // ... over the deferred micro-batches of a gradient-accumulation window (nseg > 0, ops/gemm.py WgradDefer): split ks
   // reads segment ks / seg_chunks (A = segA[], B = segB[], seg_rows k-rows each, leading dimensions lda / ldb), k-rows
   // [(ks % seg_chunks) kchunk, + kchunk); A / B / K unused.  No concatenated copy of the window's operands.
+  // GELU epilogues: forward (NT + bias) writes C = s gelu(u) and aux_out = s gelu'(u) (s = dropout keep / (1 - p));
+  // backward (NN) C = dU = (A . B) * aux and per-128-row column sums of dU -> colsum [M / 128][N] (fc1 bias gradient)
+  uint16_t* aux_out;
+  const uint16_t* aux;
+  long ldaux;
+  float* colsum;
   const uint16_t* segA[W4_MAX_SEGS];
   const uint16_t* segB[W4_MAX_SEGS];
   int nseg, seg_rows, seg_chunks;

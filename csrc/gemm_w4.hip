@@ -33,6 +33,7 @@
 #include <cstdlib>
 #include <type_traits>
 
+#include "gelu.h"
 #include "gemm_params.h"
 
 using namespace dllm;
@@ -49,10 +50,14 @@ namespace {
 // image is k-major like the NN B operand (transposed fragment reads), K is split over workgroups (tile index = split x
 // output tile, one tile per workgroup) and each split stores its fp32 product to a slab of ws (reduced into C by
 // csrc/gemm.hip's split-K pass), or — one split — accumulates straight into the fp32 / bf16 C.
-enum { W4_EPI_NONE = 0, W4_EPI_RELU = 1, W4_EPI_DRELU_M = 7, W4_EPI_CEF = 8, W4_EPI_CEB = 9, W4_EPI_WG = 10 };
+// GELU (erf) FFN: forward NT + bias writing h and its dropout-scaled derivative (two outputs, as csrc/gemm_fused.hip's
+// epilogue 2), backward NN multiplying by that derivative and summing dU per 128 rows (csrc/gemm_fused.hip epilogue 4)
+enum { W4_EPI_NONE = 0, W4_EPI_RELU = 1, W4_EPI_DRELU_M = 7, W4_EPI_CEF = 8, W4_EPI_CEB = 9, W4_EPI_WG = 10,
+       W4_EPI_GELU = 11, W4_EPI_DGELU = 12 };
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8v;
 typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((ext_vector_type(2))) uint32_t u32x2;
 
 constexpr int NT = 256, BK = 64;
 constexpr uint32_t kOOB = 0x80000000u;  // a buffer offset past every descriptor's range: the load returns 0
@@ -316,7 +321,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
       dma16<1024>(srd_mask, b, 0u, scr_lds);
     }
   };
-  const uint32_t seed = (EPI == W4_EPI_RELU && P.p > 0.f) ? eff_seed(P.seed) : P.seed;
+  const uint32_t seed = ((EPI == W4_EPI_RELU || EPI == W4_EPI_GELU) && P.p > 0.f) ? eff_seed(P.seed) : P.seed;
 
   // ---- prologue: k-tiles 0 and 1 in flight, wait for k-tile 0, read its first half
   mask_dma(m0, n0);
@@ -390,7 +395,8 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
       __builtin_amdgcn_sched_barrier(0);
       if constexpr ((RS & 64) == 0) {
         // after an epilogue its 32 C stores are the youngest VMEM ops (CEF stores fewer: drain everything)
-        if (kt == 0 && g > 0 && !ACC && EPI != W4_EPI_CEF && EPI != W4_EPI_WG)
+        if (kt == 0 && g > 0 && !ACC && EPI != W4_EPI_CEF && EPI != W4_EPI_WG && EPI != W4_EPI_GELU &&
+            EPI != W4_EPI_DGELU)
           asm volatile("s_waitcnt vmcnt(32) lgkmcnt(0)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
@@ -535,6 +541,19 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
       const __amdgpu_buffer_rsrc_t srdC = __builtin_amdgcn_make_buffer_rsrc(
           (void*)(((uint64_t)chi << 32) | clo), (short)0,
           (int)__builtin_amdgcn_readfirstlane((uint32_t)(min(P.M - m0, 256) * P.ldc * 2)), 0x00020000);
+      // GELU: the second output (forward) / the saved derivative (backward), rows m0 .. m0 + 255 of [M][ldaux]
+      __amdgpu_buffer_rsrc_t srdX = srdC;
+      if constexpr (EPI == W4_EPI_GELU || EPI == W4_EPI_DGELU) {
+        const uint64_t xb = EPI == W4_EPI_GELU ? (uint64_t)(P.aux_out + (long)m0 * P.ldaux)
+                                               : (uint64_t)(P.aux + (long)m0 * P.ldaux);
+        const uint32_t xlo = __builtin_amdgcn_readfirstlane((uint32_t)xb), xhi = __builtin_amdgcn_readfirstlane((uint32_t)(xb >> 32));
+        srdX = __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)xhi << 32) | xlo), (short)0,
+                                                 (int)__builtin_amdgcn_readfirstlane((uint32_t)(min(P.M - m0, 256) * P.ldaux * 2)),
+                                                 0x00020000);
+      }
+      f32x4 csum[8];  // DGELU: this lane's column sums (columns 16 j + 4 qd + r) over its rows of the wave's 128
+#pragma unroll
+      for (int j = 0; j < 8; ++j) csum[j] = f32x4{0.f, 0.f, 0.f, 0.f};
       const int mr = wm * 128 + 16 * (qd & 1) + rl;  // tile-local row of ii = 0
       const int nc = wn * 128 + 8 * (qd >> 1);       // tile-local column of j = 0
       uint32_t mw[8];  // mask words: bit 4 j + r of word i <-> acc[i][j][r]
@@ -558,15 +577,20 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) mw[i] = 0u;
       }
-      f32x4 bv[8];
+      // bias kept as packed bf16 (16 registers instead of 32 fp32), widened where added
+      u32x2 bv[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        bv[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        bv[j] = u32x2{0u, 0u};
         if constexpr (BIAS) {
           const int nb4 = n0 + wn * 128 + 16 * j + 4 * qd;
-          if (nb4 < P.N) bv[j] = Elem<uint16_t>::load4(P.bias + nb4);
+          if (nb4 < P.N) bv[j] = *reinterpret_cast<const u32x2*>(P.bias + nb4);
         }
       }
+      auto bias4 = [&](int j) {
+        return f32x4{bf2f((uint16_t)(bv[j].x & 0xFFFFu)), bf2f((uint16_t)(bv[j].x >> 16)),
+                     bf2f((uint16_t)(bv[j].y & 0xFFFFu)), bf2f((uint16_t)(bv[j].y >> 16))};
+      };
       auto add_c = [&](u32x4 o, uint32_t off) {  // ACC: o + C, in fp32, rounded once
         const u32x4 c = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(srdC, off, 0, 0));
         auto add2 = [](uint32_t u, uint32_t v) {
@@ -594,6 +618,19 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
       }
 #pragma unroll
       for (int ii = 0; ii < 4; ++ii) {
+        u32x4 gp[8];  // GELU forward: the packed derivative output of this row group (staged after h)
+        u32x2 ga[8][2];  // GELU backward: the saved derivative at this lane's accumulator positions (rows ii, ii + 16)
+        if constexpr (EPI == W4_EPI_DGELU) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int col = n0 + wn * 128 + 16 * j + 4 * qd;
+            const int row = wm * 128 + 32 * ii + rl;  // tile-local
+            const uint32_t o0 = col < P.N ? (uint32_t)(row * P.ldaux + col) * 2u : kOOB;
+            const uint32_t o1 = col < P.N ? (uint32_t)((row + 16) * P.ldaux + col) * 2u : kOOB;
+            ga[j][0] = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(srdX, o0, 0, 0));
+            ga[j][1] = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(srdX, o1, 0, 0));
+          }
+        }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           // opaque re-definition in place: the AGPR -> VGPR copies cannot be hoisted above this point (otherwise all 256
@@ -601,8 +638,9 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
           asm volatile("" : "+a"(acc[2 * ii][j]), "+a"(acc[2 * ii + 1][j]));
           f32x4 xv = acc[2 * ii][j], yv = acc[2 * ii + 1][j];
           if constexpr (BIAS) {
-            xv += bv[j];
-            yv += bv[j];
+            const f32x4 b4 = bias4(j);
+            xv += b4;
+            yv += b4;
           }
           if constexpr (EPI == W4_EPI_RELU) {
             const uint32_t n4 = (uint32_t)(n0 + wn * 128 + 16 * j + 4 * qd);
@@ -627,6 +665,48 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
               xv[r] = (mw[2 * ii] >> (4 * j + r)) & 1u ? xv[r] * P.scale : 0.f;
               yv[r] = (mw[2 * ii + 1] >> (4 * j + r)) & 1u ? yv[r] * P.scale : 0.f;
             }
+          } else if constexpr (EPI == W4_EPI_GELU) {
+            // h = s gelu(u), G = s gelu'(u), s = keep / (1 - p) with the keep bits of the [M][N] element index
+            f32x4 gx, gy;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              float g, d;
+              dllm_gelu::gelu_pair(xv[r], g, d);
+              xv[r] = g;
+              gx[r] = d;
+              dllm_gelu::gelu_pair(yv[r], g, d);
+              yv[r] = g;
+              gy[r] = d;
+            }
+            if (P.p > 0.f) {
+              const uint32_t n4 = (uint32_t)(n0 + wn * 128 + 16 * j + 4 * qd);
+              const uint32_t ex = (uint32_t)(m0 + wm * 128 + 32 * ii + rl) * (uint32_t)P.N + n4;
+              const uint32_t ey = ex + 16u * (uint32_t)P.N;
+              bool k0, k1, k2, k3;
+              keep_two(seed, P.thr, ex, k0, k1);
+              keep_two(seed, P.thr, ex + 2u, k2, k3);
+              const f32x4 sx = {k0 ? P.scale : 0.f, k1 ? P.scale : 0.f, k2 ? P.scale : 0.f, k3 ? P.scale : 0.f};
+              keep_two(seed, P.thr, ey, k0, k1);
+              keep_two(seed, P.thr, ey + 2u, k2, k3);
+              const f32x4 sy = {k0 ? P.scale : 0.f, k1 ? P.scale : 0.f, k2 ? P.scale : 0.f, k3 ? P.scale : 0.f};
+              xv *= sx;
+              gx *= sx;
+              yv *= sy;
+              gy *= sy;
+            }
+            uint32_t g0 = pk2(gx.x, gx.y), g1 = pk2(gx.z, gx.w), h0 = pk2(gy.x, gy.y), h1 = pk2(gy.z, gy.w);
+            const auto r0 = __builtin_amdgcn_permlane16_swap(g0, h0, false, false);
+            const auto r1 = __builtin_amdgcn_permlane16_swap(g1, h1, false, false);
+            gp[j] = u32x4{r0[0], r1[0], r0[1], r1[1]};
+          } else if constexpr (EPI == W4_EPI_DGELU) {
+            // dU = dH * G (fp32, rounded once); column sums of dU for the bias gradient
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const uint32_t wx = ga[j][0][r >> 1], wy = ga[j][1][r >> 1];
+              xv[r] *= bf2f((uint16_t)((r & 1) ? (wx >> 16) : (wx & 0xFFFFu)));
+              yv[r] *= bf2f((uint16_t)((r & 1) ? (wy >> 16) : (wy & 0xFFFFu)));
+            }
+            csum[j] += xv + yv;
           } else if constexpr (EPI == W4_EPI_CEB) {
             // dlogits = g (softmax - (1 - eps) onehot - eps / V); xv: row q = 2 ii, yv: row q = 2 ii + 1
             const float off = P.eps / (float)P.V, hit = 1.f - P.eps;
@@ -679,6 +759,46 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
             if constexpr ((RS & 128) == 0) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, o), srdC, off, 0, 0);
           }
           __builtin_amdgcn_sched_barrier(0);
+          if constexpr (EPI == W4_EPI_GELU) {
+            // the derivative output of the same 32 rows through the same scratch (this wave's DS ops run in order)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              const int cj = 2 * j + (qd >> 1);
+              *reinterpret_cast<u32x4*>(scr + rowL * 256 + ((cj ^ (rowL & 15)) << 4)) = gp[j];
+            }
+#pragma unroll
+            for (int s2 = 0; s2 < 8; ++s2) {
+              const int r = 4 * s2 + (lane >> 4), c = lane & 15;
+              const u32x4 o = *reinterpret_cast<const u32x4*>(scr + r * 256 + ((c ^ (r & 15)) << 4));
+              const int col = wn * 128 + 8 * c;
+              const uint32_t off =
+                  n0 + col < P.N ? (uint32_t)((wm * 128 + 32 * ii + r) * P.ldaux + n0 + col) * 2u : kOOB;
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, o), srdX, off, 0, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+      }
+      if constexpr (EPI == W4_EPI_DGELU) {
+        // the 16 lanes rl = 0..15 of a quarter qd hold the same columns on 16 rows: fold them, lane rl = 0 stores the
+        // wave's 128-row partial row (m0 / 128 + wm) of colsum
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float v = csum[j][r];
+            v += __shfl_xor(v, 1, 64);
+            v += __shfl_xor(v, 2, 64);
+            v += __shfl_xor(v, 4, 64);
+            v += __shfl_xor(v, 8, 64);
+            csum[j][r] = v;
+          }
+        }
+        if (rl == 0) {
+          float* cp = P.colsum + (long)(m0 / 128 + wm) * P.N + n0 + wn * 128 + 4 * qd;
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (n0 + wn * 128 + 16 * j + 4 * qd < P.N) *reinterpret_cast<f32x4*>(cp + 16 * j) = csum[j];
         }
       }
       if constexpr (EPI == W4_EPI_RELU) {  // this thread's 8 mask words of the tile
@@ -780,6 +900,17 @@ extern "C" int dllm_gemm_w4(const GemmW4Params* pp, int b_kmajor, int persist, i
   if (epi == W4_EPI_DRELU_M) {
     if (!b_kmajor || p.accumulate || p.bias || p.mask == nullptr) return -5;
     return launch_rs<true, false, false, 1, W4_EPI_DRELU_M>(p, persist != 0, st);
+  }
+  if (epi == W4_EPI_GELU) {  // NT, bias, two outputs; persistent (store-only epilogue)
+    if (b_kmajor || p.accumulate || p.aux_out == nullptr || p.ldaux < p.N || p.ldaux % 8 || p.N % 8) return -5;
+    return p.bias ? launch_rs<false, true, false, 1, W4_EPI_GELU>(p, persist != 0, st)
+                  : launch_rs<false, false, false, 1, W4_EPI_GELU>(p, persist != 0, st);
+  }
+  if (epi == W4_EPI_DGELU) {  // NN; its derivative loads would queue behind a persistent tile's prefetch: one tile each
+    if (!b_kmajor || p.accumulate || p.bias || p.aux == nullptr || p.colsum == nullptr || p.ldaux < p.N ||
+        p.ldaux % 4 || p.M % 128 || p.N % 4)
+      return -5;
+    return launch_rs<true, false, false, 1, W4_EPI_DGELU>(p, false, st);
   }
   if (epi == W4_EPI_CEF || epi == W4_EPI_CEB) {
     if (b_kmajor || p.accumulate || p.bias || p.labels == nullptr || p.skip < 0 || p.V <= 0) return -5;

@@ -55,7 +55,14 @@ _W4_FFN = os.environ.get("DLLM_W4_FFN", "0") == "1"
 # The ReLU backward (dU = dY Wo through the forward's bit mask) on csrc/gemm_w4.hip, reading the ping-pong forward's
 # mask layout (mask_pp): 17 % faster than the ping-pong backward kernel (profiles/r3_ffn_kernel_profile.txt; whole step -0.9 %, profiles/r3_w4_ffn_bwd_ab.txt)
 _W4_FFN_BWD = os.environ.get("DLLM_W4_FFN_BWD", "1") != "0"
+# GELU (erf) FFN (BART) on csrc/gemm_w4.hip's GELU epilogues (forward: h and the dropout-scaled derivative; backward:
+# dU = dH * derivative with the wi bias column partials) instead of the ping-pong kernel's epilogues 2 / 4 (DLLM_W4_GELU=1).
+# Off by default: at the BART fc1 shape both kernels are bound by the forward's two [tokens, d_ff] bf16 outputs
+# (w4 GELU forward 2660 us vs 1835 us without the epilogue; ping-pong 2552 us; backward equal), and the bart-large step
+# ran 0.25-0.43 % slower with it (profiles/r5_w4_gelu_ab.txt)
+_W4_GELU = os.environ.get("DLLM_W4_GELU", "0") == "1"
 w4_ffn_calls = 0
+w4_gelu_calls = 0
 fused_calls = 0  # number of FFN forwards that took the fused path (tests assert the kernel really ran)
 
 
@@ -94,7 +101,20 @@ class _FusedFFNFn(torch.autograd.Function):
         ctx.w4 = False
         if efwd != 1:  # GELU: the backward multiplies by the stored derivative
             u = torch.empty(x2.shape[0], wi.shape[0], device=x.device, dtype=x.dtype)
-        elif _RELU_MASK and _pingpong(C, x2.shape[1]) and _pingpong(C, wo.shape[0]):  # ReLU: bits for the backward
+        if efwd == 2 and _W4_GELU and C.gemm_w4_supported(x2, wi, False) and \
+                (bi is None or (bi.dtype == torch.bfloat16 and bi.is_contiguous())):
+            global w4_gelu_calls
+            w4_gelu_calls += 1
+            h = C.gemm_w4(x2, wi, False, bi, None, False, -1, True, 11, float(p), int(seed), None, False, None, u)
+            y = linear_fwd(h, wo, bo)
+            ctx.set_materialize_grads(False)
+            ctx.save_for_backward(x2, h, u, None)
+            ctx.params = params
+            for q in params:
+                _use(q)
+            ctx.cfg = (act, float(p), int(seed), shape)
+            return y.view(*shape[:-1], wo.shape[0]), x.view_as(x)
+        if efwd == 1 and _RELU_MASK and _pingpong(C, x2.shape[1]) and _pingpong(C, wo.shape[0]):  # ReLU: mask bits
             mask = torch.empty(x2.shape[0] * wi.shape[0] // 32, device=x.device, dtype=torch.int32)
         h = C.gemm_fused(x2, wi, False, efwd, bi, None, u, float(p), int(seed), _VARIANT, mask)
         y = linear_fwd(h, wo, bo)
@@ -119,9 +139,14 @@ class _FusedFFNFn(torch.autograd.Function):
             dy2 = dy2.contiguous()
         # GELU: the wi bias gradient comes out of the same GEMM's epilogue as per-128-row column sums of dU
         bsum = None
-        if Bi is not None and ebwd in (4, 6) and _COLSUM and _pingpong(C, wo.shape[0]):
+        w4g = ebwd == 4 and _W4_GELU and dy2.shape[0] % 128 == 0 and C.gemm_w4_supported(dy2, wo, True)
+        if Bi is not None and ebwd in (4, 6) and _COLSUM and (w4g or _pingpong(C, wo.shape[0])):
             bsum = torch.empty(dy2.shape[0] // 128, wo.shape[1], device=dy2.device, dtype=torch.float32)
-        if ctx.w4:  # d-relu from the w4 forward's bit mask
+        if w4g:  # dU = dH * (stored derivative) + per-128-row column partials, on the w4 kernel
+            cs = bsum if bsum is not None else torch.empty(dy2.shape[0] // 128, wo.shape[1], device=dy2.device,
+                                                           dtype=torch.float32)
+            du = C.gemm_w4(dy2, wo, True, None, None, False, -1, False, 12, 0.0, 0, None, False, u, None, cs)
+        elif ctx.w4:  # d-relu from the w4 forward's bit mask
             if not C.gemm_w4_supported(dy2, wo, True):
                 dy2 = dy2.contiguous()
             du = C.gemm_w4(dy2, wo, True, None, None, False, -1, True, 7, p, seed, mask)

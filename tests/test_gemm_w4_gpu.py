@@ -140,3 +140,52 @@ def test_gemm_w4_drelu_from_pingpong_mask(M, K, N, p):
     assert _rel(got, ref) < 1e-3, _rel(got, ref)
     exact = (dy.float() @ wo.float()) * (h.float() > 0) / (1 - p)
     assert _rel(got, exact) < 8e-3
+
+
+def _gelu_pair_ref(u):
+    """fp32 GELU (erf) and its derivative."""
+    cdf = 0.5 * (1.0 + torch.erf(u * 0.7071067811865476))
+    return u * cdf, cdf + u * 0.3989422804014327 * torch.exp(-0.5 * u * u)
+
+
+@pytest.mark.parametrize("M,K,N,p,bias", [(8448, 1024, 4096, 0.0, True), (8448, 1024, 4096, 0.1, True),
+                                          (1000, 256, 520, 0.0, False), (300, 128, 264, 0.1, True)])
+def test_gemm_w4_gelu_forward(M, K, N, p, bias):
+    """W4_EPI_GELU: h = s gelu(x wᵀ + b) and aux = s gelu'(.) (s = dropout keep / (1 - p)) vs the fp32 composite with
+    the same keep bits; persistent (528 tiles) and ragged shapes; equal to the ping-pong kernel's epilogue 2 where
+    that kernel runs (M % 256 == 0, N % 256 == 0)."""
+    from distributed_llms_example_amd.ops.rng import keep_mask
+    C = _ext.native()
+    torch.manual_seed(M + N)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) * K ** -0.5).to(torch.bfloat16)
+    b = (0.5 * torch.randn(N, device=DEV)).to(torch.bfloat16) if bias else None
+    aux = torch.full((M, N), float("nan"), device=DEV, dtype=torch.bfloat16)
+    h = C.gemm_w4(x, w, False, b, None, False, -1, True, 11, p, 31, None, False, None, aux)
+    u = x.float() @ w.float().t() + (b.float() if bias else 0.0)
+    g, dg = _gelu_pair_ref(u)
+    if p > 0:
+        keep = keep_mask(31, p, (M, N), x.device).float() / (1.0 - p)
+        g, dg = g * keep, dg * keep
+    assert _rel(h, g) < 1e-2, _rel(h, g)
+    assert _rel(aux, dg) < 1e-2, _rel(aux, dg)
+    if M % 256 == 0 and N % 256 == 0 and bias:
+        aux_pp = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        h_pp = C.gemm_fused(x, w, False, 2, b, None, aux_pp, p, 31, 9)
+        assert _rel(h, h_pp) < 2e-3 and _rel(aux, aux_pp) < 2e-3, (_rel(h, h_pp), _rel(aux, aux_pp))
+
+
+@pytest.mark.parametrize("M,d,F_", [(8448, 1024, 4096), (768, 512, 1024), (384, 256, 520)])
+def test_gemm_w4_gelu_backward_colsum(M, d, F_):
+    """W4_EPI_DGELU: dU = (dY · wo) * aux with per-128-row column sums of dU (the fc1 bias gradient) vs fp32."""
+    C = _ext.native()
+    torch.manual_seed(M + F_)
+    dy = torch.randn(M, d, device=DEV).to(torch.bfloat16)
+    wo = (torch.randn(d, F_, device=DEV) * d ** -0.5).to(torch.bfloat16)
+    aux = torch.rand(M, F_, device=DEV).to(torch.bfloat16)
+    part = torch.full((M // 128, F_), float("nan"), device=DEV)
+    du = C.gemm_w4(dy, wo, True, None, None, False, -1, False, 12, 0.0, 0, None, False, aux, None, part)
+    ref = (dy.float() @ wo.float()) * aux.float()
+    assert _rel(du, ref) < 1e-2, _rel(du, ref)
+    ref_part = ref.view(M // 128, 128, F_).sum(1)
+    assert _rel(part, ref_part) < 1e-2, _rel(part, ref_part)
