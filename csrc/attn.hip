@@ -485,7 +485,9 @@ __global__ __launch_bounds__(256, FNB == 3 ? 2 : 3) void attn_fwd_kernel(AttnPar
 
 // ================================================================================== backward: dQ
 // OCC = workgroups per CU the register budget is cut for (2: 256 VGPRs, 3: 168)
-template <bool HAS_BIAS, bool HAS_KPM, bool CAUSAL, bool DROP, int OCC>
+// CS: also the dQ column sums (AttnParams csq; instantiated for the bias-free kernels only, so the T5 variants compile
+// without any of that code)
+template <bool HAS_BIAS, bool HAS_KPM, bool CAUSAL, bool DROP, int OCC, bool CS = false>
 __global__ __launch_bounds__(256, OCC) void attn_bwd_dq_kernel(AttnParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint16_t* KV = reinterpret_cast<uint16_t*>(smem);            // [2][K | V]
@@ -685,11 +687,11 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dq_kernel(AttnParams P) {
   // every wave is done with the K/V buffers (the last tile's DMAs were waited for): they stage the dQ tiles
   __syncthreads();
   // column sums: the 4 waves' 64 sums at smem + 16 KB (past the 4 staging tiles, still inside the K/V buffers)
-  float* red = P.csq != nullptr ? reinterpret_cast<float*>(smem + 4 * 4096) : nullptr;
+  float* red = CS ? reinterpret_cast<float*>(smem + 4 * 4096) : nullptr;
   store_rows_staged(smem + w * 4096, dq0, dq1, P.scale, r, hh, lane,
                     P.dq + b * P.dq_sb + (long)qw0 * P.dq_ss + h * P.dq_sh, P.dq_ss, P.Sq - qw0,
-                    red != nullptr ? red + w * 64 : nullptr);
-  if (P.csq != nullptr) {
+                    CS ? red + w * 64 : nullptr);
+  if constexpr (CS) {
     __syncthreads();
     if (tid < 64)
       P.csq[(long)(b * P.n_tiles + qt) * P.csq_ld + h * 64 + tid] = red[tid] + red[64 + tid] + red[128 + tid] +
@@ -986,7 +988,7 @@ constexpr int K2_STAGE = 2 * 64 * D * 2 + 1024 + 1024;  // Q, dO [64][64] bf16 +
 
 // NB = stage ring depth: 3 (two stages in flight, 2 workgroups per CU) or 2 (one in flight, a 168-VGPR budget so 3
 // workgroups share a CU; taken for the bias-free variants, which fit it)
-template <bool HAS_BIAS, bool HAS_KPM, bool CAUSAL, bool DROP, int NB>
+template <bool HAS_BIAS, bool HAS_KPM, bool CAUSAL, bool DROP, int NB, bool CS = false>
 __global__ __launch_bounds__(256, NB == 3 ? 2 : 3) void attn_bwd_dkdv2_kernel(AttnParams P) {
   static_assert(NB == 2 || NB == 3, "stage ring depth");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1328,13 +1330,13 @@ __global__ __launch_bounds__(256, NB == 3 ? 2 : 3) void attn_bwd_dkdv2_kernel(At
       if (ks < P.Sk) {
         *reinterpret_cast<u16x8*>(P.dk + b * P.dk_sb + (long)ks * P.dk_ss + h * P.dk_sh + 8 * ch) = vk;
         *reinterpret_cast<u16x8*>(P.dv + b * P.dv_sb + (long)ks * P.dv_ss + h * P.dv_sh + 8 * ch) = vv;
-        if (P.csk != nullptr) {
+        if constexpr (CS) {
           cs_add(ak, vk);
           cs_add(av, vv);
         }
       }
     }
-    if (P.csk != nullptr) {
+    if constexpr (CS) {
       // column sums (cs_wave): [wave][dK 64 | dV 64] at smem + 32 KB, past the 4 waves' 8 KB staging areas and
       // inside the drained stage ring (NB * K2_STAGE >= 36 KB)
       float* red = reinterpret_cast<float*>(smem + 4 * 8192);
@@ -1391,7 +1393,7 @@ __global__ __launch_bounds__(256, NB == 3 ? 2 : 3) void attn_bwd_dkdv2_kernel(At
 // j computes.  attn_bwd_dkdv2_kernel starts one workgroup per key block instead, each re-staging the query side and
 // waiting on its own K / V loads before two short stages: prologue-latency bound at this shape.  Per score: the
 // bias-free body of attn_bwd_dkdv2_kernel (P = exp2(fma(s, sl2, rt)), Pd = P keep, dS = P fma(dP, keep, -delta)).
-template <bool HAS_KPM, bool DROP, int MB>
+template <bool HAS_KPM, bool DROP, int MB, bool CS = false>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_sq_kernel(AttnParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   // [2 stages of K2_STAGE: Q | dO | row terms (1 KB) | unused], keep words [2 parities][2 stages][1 KB], key mask [128],
@@ -1575,13 +1577,13 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_sq_kernel(AttnParams P) 
         if (ks < P.Sk) {
           *reinterpret_cast<u16x8*>(P.dk + b * P.dk_sb + (long)ks * P.dk_ss + h * P.dk_sh + 8 * ch) = vk;
           *reinterpret_cast<u16x8*>(P.dv + b * P.dv_sb + (long)ks * P.dv_ss + h * P.dv_sh + 8 * ch) = vv;
-          if (P.csk != nullptr) {
+          if constexpr (CS) {
             cs_add(ak, vk);
             cs_add(av, vv);
           }
         }
       }
-      if (P.csk != nullptr) {
+      if constexpr (CS) {
         // column sums (cs_wave): [wave][dK 64 | dV 64] in the 2 KB past the staging areas (lds_sq); the next key
         // block's writes come after its own barrier above
         float* red = reinterpret_cast<float*>(smem + 2 * K2_STAGE + 4096 + BWD_BK * 4 + 4 * 8192);
@@ -1666,6 +1668,12 @@ void launch_bwd_dq_t(const AttnParams& p, int nblk, size_t lds, hipStream_t st) 
     const char* e = getenv("DLLM_ATTN_DQ_OCC");
     return e != nullptr ? atoi(e) : 2;  // 3 measured equal (profiles/r2_ab_attn_dq_halves.txt)
   }();
+  if constexpr (!HB) {
+    if (p.csq != nullptr) {  // column sums for the q-projection bias (BART)
+      hipLaunchKernelGGL((attn_bwd_dq_kernel<HB, HK, CA, DR, 2, true>), dim3(nblk), dim3(256), lds, st, p);
+      return;
+    }
+  }
   if (occ == 3 && !CA && 3 * lds <= 160 * 1024)  // the causal variant spills at 168 VGPRs
     hipLaunchKernelGGL((attn_bwd_dq_kernel<HB, HK, CA, DR, 3>), dim3(nblk), dim3(256), lds, st, p);
   else
@@ -1692,8 +1700,20 @@ void launch_bwd_dkdv2_t(const AttnParams& p, int nblk, size_t lds, hipStream_t s
   // prologue-latency bound — gain from the third workgroup: step -0.5 % (profiles/r3_cross_dkdv_occ3_ab.txt);
   // DLLM_ATTN_DKDV_OCC_DR=0 turns that off
   if (occ == 3 && !HB && (!DR || (occ_dr == 1 && p.Sq <= 256)) && 3 * lds2 <= 160 * 1024) {
+    if constexpr (!HB) {
+      if (p.csk != nullptr) {  // column sums for the k / v projection biases (BART)
+        hipLaunchKernelGGL((attn_bwd_dkdv2_kernel<HB, HK, CA, DR, 2, true>), dim3(nblk), dim3(256), lds2, st, p);
+        return;
+      }
+    }
     hipLaunchKernelGGL((attn_bwd_dkdv2_kernel<HB, HK, CA, DR, 2>), dim3(nblk), dim3(256), lds2, st, p);
     return;
+  }
+  if constexpr (!HB) {
+    if (p.csk != nullptr) {
+      hipLaunchKernelGGL((attn_bwd_dkdv2_kernel<HB, HK, CA, DR, 3, true>), dim3(nblk), dim3(256), lds, st, p);
+      return;
+    }
   }
   static size_t attr = 64 * 1024;  // dynamic LDS above 64 KB (long sequences with bias) must be opted into
   if (lds > attr) {
@@ -1704,15 +1724,21 @@ void launch_bwd_dkdv2_t(const AttnParams& p, int nblk, size_t lds, hipStream_t s
   hipLaunchKernelGGL((attn_bwd_dkdv2_kernel<HB, HK, CA, DR, 3>), dim3(nblk), dim3(256), lds, st, p);
 }
 
-template <bool HK, bool DR, int MB>
-void launch_bwd_dkdv_sq_mb(const AttnParams& p, dim3 grid, size_t lds, hipStream_t st) {
+template <bool HK, bool DR, int MB, bool CS>
+void launch_bwd_dkdv_sq_cs(const AttnParams& p, dim3 grid, size_t lds, hipStream_t st) {
   static bool attr = false;  // the staged epilogue puts the dynamic LDS above the 64 KB default
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)attn_bwd_dkdv_sq_kernel<HK, DR, MB>,
+    (void)hipFuncSetAttribute((const void*)attn_bwd_dkdv_sq_kernel<HK, DR, MB, CS>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
-  hipLaunchKernelGGL((attn_bwd_dkdv_sq_kernel<HK, DR, MB>), grid, dim3(256), lds, st, p);
+  hipLaunchKernelGGL((attn_bwd_dkdv_sq_kernel<HK, DR, MB, CS>), grid, dim3(256), lds, st, p);
+}
+
+template <bool HK, bool DR, int MB>
+void launch_bwd_dkdv_sq_mb(const AttnParams& p, dim3 grid, size_t lds, hipStream_t st) {
+  if (p.csk != nullptr) launch_bwd_dkdv_sq_cs<HK, DR, MB, true>(p, grid, lds, st);
+  else launch_bwd_dkdv_sq_cs<HK, DR, MB, false>(p, grid, lds, st);
 }
 
 template <bool HK, bool DR>
