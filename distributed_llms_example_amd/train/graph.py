@@ -303,6 +303,17 @@ def graph_policy() -> str:
     return {"0": "off", "1": "on"}.get(v, "auto")
 
 
+def _all_ranks(flag: bool, eng) -> bool:
+    """``flag`` AND-ed over the ranks of the default process group (itself when there is none)."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() <= 1:
+        return bool(flag)
+    dev = eng.env.device if dist.get_backend() == "nccl" else torch.device("cpu")
+    t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(t.item())
+
+
 class StepRunner:
     """One optimizer step of an entry point's loop — forward + backward of the step's passes, gradient sync, clip +
     AdamW — eager or replayed from a HIP graph (GraphedStep).
@@ -384,12 +395,20 @@ class StepRunner:
                     # mirrors of device state: snapshot them
                     rng = rng_mod.default_rng()
                     snap = (eng.optimizer.step_count, eng.step_seed.host, rng.counter)
+                    err = None
                     try:
                         self.graph = GraphedStep(eng, passes, warmup=0, comm=self.comm,
                                                  num_items=num_items is not None, dp_ranks=self.dp_ranks)
                     except Exception as e:  # noqa: BLE001 - capture unsupported here: stay eager, say why once
+                        err = f"{type(e).__name__}: {str(e)[:300]}"
+                    # every data-parallel rank must take the same schedule (graph replays vs eager steps issue their
+                    # collectives differently): a capture failure anywhere sends all ranks back to eager steps
+                    if not _all_ranks(err is None, eng):
+                        err = err or "HIP graph capture failed on another rank"
+                    if err is not None:
+                        self.graph = None
                         eng.optimizer.step_count, eng.step_seed.host, rng.counter = snap
-                        self.graph_error = f"{type(e).__name__}: {str(e)[:300]}"
+                        self.graph_error = err
                         from ..utils.logging import get_logger
                         get_logger(__name__).warning(f"HIP graph capture failed, eager steps: {self.graph_error}")
                         torch.cuda.synchronize()
@@ -423,7 +442,8 @@ class StepRunner:
         med = lambda evs: statistics.median(a.elapsed_time(b) for a, b in evs)  # noqa: E731
         eager = med(self._eager_t[-2:]) if self._eager_t else float("inf")
         replay = med(self._replay_t)
-        keep = replay <= eager * (1.0 + self.GRAPH_TOL)
+        # one decision for all data-parallel ranks (their schedules must match): graphs only if every rank keeps them
+        keep = _all_ranks(replay <= eager * (1.0 + self.GRAPH_TOL), self.eng)
         self.decision = {"graph": keep, "eager_ms": round(eager, 3), "replay_ms": round(replay, 3)}
         if not keep:
             self._eager_sigs.add(self.graph.signature())

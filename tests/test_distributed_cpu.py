@@ -468,6 +468,20 @@ def test_bucket_size_probe_agrees_across_ranks():
     assert set(a["busbw_gbps"]) == {"0.25", "0.5", "1", "2"} and all(v > 0 for v in a["busbw_gbps"].values())
 
 
+def _all_ranks_case(rank, world):
+    from types import SimpleNamespace
+    from distributed_llms_example_amd.train.graph import _all_ranks
+    eng = SimpleNamespace(env=SimpleNamespace(device=torch.device("cpu")))
+    return [_all_ranks(True, eng), _all_ranks(rank == 0, eng), _all_ranks(rank == 1, eng)]
+
+
+def test_graph_decisions_agree_across_ranks():
+    """StepRunner's capture outcome and auto-policy decision are AND-ed over the data-parallel ranks (train/graph.py
+    _all_ranks): one rank failing / preferring eager sends every rank to eager, so their collective schedules match."""
+    out = run_ranks(_all_ranks_case)
+    assert out[0] == out[1] == [True, False, False]
+
+
 # ---------------------------------------------------------------- bench.py self-launch (the driver's `bench.py --gpus N`)
 @pytest.mark.parametrize("n", [2, 4])
 def test_bench_self_launches_ranks(n):
