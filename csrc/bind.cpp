@@ -122,7 +122,8 @@ std::vector<Tensor> norm_fwd(const Tensor& x, const optional<Tensor>& resid, con
 std::vector<Tensor> norm_bwd(const optional<Tensor>& dout_o, const optional<Tensor>& ds, const Tensor& s,
                              const Tensor& w, const optional<Tensor>& b, const optional<Tensor>& mean,
                              const Tensor& rstd, double p, int64_t seed, int64_t kind, bool want_stream,
-                             const optional<Tensor>& dw_acc, const optional<Tensor>& db_acc, bool want_colsum) {
+                             const optional<Tensor>& dw_acc, const optional<Tensor>& db_acc, bool want_colsum,
+                             bool partials_only) {
   check_gpu(s, "s");
   TORCH_CHECK(s.dim() == 2 && s.is_contiguous(), "s must be contiguous [N, d]");
   const int N = s.size(0), d = s.size(1);
@@ -142,7 +143,8 @@ std::vector<Tensor> norm_bwd(const optional<Tensor>& dout_o, const optional<Tens
   auto dw_part = at::empty({G, d}, f32);
   const bool has_b = b.has_value() && b->defined();
   // dw_acc / db_acc: accumulate the parameter gradients in place (param dtype, contiguous, d elements)
-  const bool acc = dw_acc.has_value() && dw_acc->defined();
+  // partials_only: no reduction at all — dw / db come back as the fp32 per-block partials [G, d] (deferred windows)
+  const bool acc = !partials_only && dw_acc.has_value() && dw_acc->defined();
   if (acc) {
     // the flat gradient buffer: param dtype or fp32 (FlatParams grad_dtype)
     TORCH_CHECK(dw_acc->numel() == d && dw_acc->is_contiguous() &&
@@ -152,9 +154,9 @@ std::vector<Tensor> norm_bwd(const optional<Tensor>& dout_o, const optional<Tens
                            db_acc->is_contiguous() && db_acc->scalar_type() == dw_acc->scalar_type()),
                 "db_acc mismatch");
   }
-  Tensor dw = acc ? Tensor() : at::zeros({d}, f32);
+  Tensor dw = (acc || partials_only) ? Tensor() : at::zeros({d}, f32);
   Tensor db_part = has_b ? at::empty({G, d}, f32) : Tensor();
-  Tensor db = (has_b && !acc) ? at::zeros({d}, f32) : Tensor();
+  Tensor db = (has_b && !acc && !partials_only) ? at::zeros({d}, f32) : Tensor();
   // column sums of dx (the upstream linear layer's bias gradient), fp32 [d]
   Tensor dxs_part = want_colsum ? at::empty({G, d}, f32) : Tensor();
   // the dx column sums stay per-block partials: the consuming bias gradient reduces them (ops/gemm.py, one kernel)
@@ -162,13 +164,14 @@ std::vector<Tensor> norm_bwd(const optional<Tensor>& dout_o, const optional<Tens
     check_rc(dllm_norm_bwd(dout.data_ptr(), dse.defined() ? dse.data_ptr() : nullptr, s.data_ptr(), w.data_ptr(),
                            kind == 1 ? mean->data_ptr<float>() : nullptr, rstd.data_ptr<float>(), dx.data_ptr(),
                            want_stream ? dstream.data_ptr() : nullptr, dw_part.data_ptr<float>(),
-                           has_b ? db_part.data_ptr<float>() : nullptr, acc ? nullptr : dw.data_ptr<float>(),
-                           (has_b && !acc) ? db.data_ptr<float>() : nullptr, acc ? dw_acc->data_ptr() : nullptr,
+                           has_b ? db_part.data_ptr<float>() : nullptr, dw.defined() ? dw.data_ptr<float>() : nullptr,
+                           db.defined() ? db.data_ptr<float>() : nullptr, acc ? dw_acc->data_ptr() : nullptr,
                            (acc && has_b) ? db_acc->data_ptr() : nullptr,
                            want_colsum ? dxs_part.data_ptr<float>() : nullptr,
                            nullptr, N, d, (float)p, (uint32_t)seed, (int)kind,
                            is_bf16(s), acc && dw_acc->scalar_type() == at::kFloat, stream()),
              "norm_bwd");
+  if (partials_only) return {dx, dstream, dw_part, db_part, dxs_part};
   return {dx, dstream, dw, db, dxs_part};
 }
 
@@ -1300,7 +1303,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("norm_fwd", &norm_fwd);
   m.def("norm_bwd", &norm_bwd, py::arg("dout"), py::arg("ds"), py::arg("s"), py::arg("w"), py::arg("b"),
         py::arg("mean"), py::arg("rstd"), py::arg("p"), py::arg("seed"), py::arg("kind"), py::arg("want_stream"),
-        py::arg("dw_acc") = py::none(), py::arg("db_acc") = py::none(), py::arg("want_colsum") = false);
+        py::arg("dw_acc") = py::none(), py::arg("db_acc") = py::none(), py::arg("want_colsum") = false,
+        py::arg("partials_only") = false);
   m.def("act_fwd", &act_fwd);
   m.def("act_bwd", &act_bwd);
   m.def("dropout_fwd", &dropout_fwd);

@@ -297,11 +297,11 @@ int launch_bwd(const void* dout, const void* ds_extra, const void* s, const void
     hipLaunchKernelGGL(col_sum_acc_kernel<T>, dim3((d + 63) / 64), dim3(1024), 0, st, dw_part, (T*)dw_acc, G, d);
     if (db_part != nullptr)
       hipLaunchKernelGGL(col_sum_acc_kernel<T>, dim3((d + 63) / 64), dim3(1024), 0, st, db_part, (T*)db_acc, G, d);
-  } else {
+  } else if (dw != nullptr) {
     const dim3 cg((d + 63) / 64, kColChunks);
     hipLaunchKernelGGL(col_sum_kernel, cg, dim3(256), 0, st, dw_part, dw, G, d);
     if (db_part != nullptr) hipLaunchKernelGGL(col_sum_kernel, cg, dim3(256), 0, st, db_part, db, G, d);
-  }
+  }  // neither: the caller keeps the per-block partials (a deferred gradient-accumulation window, ops/gemm.py)
   DLLM_CHECK_LAUNCH();
   return 0;
 }

@@ -116,6 +116,8 @@ class WgradDefer:
     def __init__(self, mem_cap: int | None = None):
         self.segs: dict = {}  # (ptr, shape, stride, dtype) of the gradient view -> [out, beta, [(dy2, x2, v), ...]]
         self.held: set = set()  # storages of kept dY operands: nothing may write into them (holds())
+        # per-block column partials of norm weight / bias gradients (ops/norms.py): reduced once per window
+        self.psegs: dict = {}  # key of the gradient view -> [out, [part [G, d], ...]]
         self.final = False
         self.active = True
         self.mem_cap = mem_cap
@@ -149,13 +151,33 @@ class WgradDefer:
     def flush(self) -> None:
         """Every pending window now (compute stream): the end of the last micro-batch's backward, or the memory cap."""
         segs, self.segs = self.segs, {}
+        psegs, self.psegs = self.psegs, {}
         self.held = set()
         for out, beta, parts in segs.values():
             self.merged += 1
             self.run(out, parts, beta)
+        for out, parts in psegs.values():
+            self.merged += 1
+            colsum_partials_acc(out, torch.cat(parts) if len(parts) > 1 else parts[0])
+
+    def partials(self, out: torch.Tensor, part: torch.Tensor | None = None) -> list | None:
+        """A norm backward's per-block partials of ``out``'s gradient: kept (no_sync micro-batch; returns None), or —
+        in the window's last micro-batch — the kept ones for the caller to reduce with its own (returns the list)."""
+        k = self.key(out)
+        if not self.final:
+            self.psegs.setdefault(k, [out, []])[1].append(part)
+            self.deferred += 1
+            return None
+        ent = self.psegs.pop(k, None)
+        return ent[1] if ent is not None else []
 
 
 _defer: list = [None]
+
+
+def deferring() -> WgradDefer | None:
+    """The active deferral window (:func:`defer_wgrads`), if any."""
+    return _defer[0]
 
 
 def holds(t: torch.Tensor | None) -> bool:

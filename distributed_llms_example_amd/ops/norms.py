@@ -16,7 +16,8 @@ import torch
 
 from .. import _ext
 from . import streams
-from .gemm import colsum_record
+from . import gemm
+from .gemm import colsum_partials_acc, colsum_record
 from .linear import _fire, _fusable, _gbuf, _use
 from .rng import keep_mask
 
@@ -71,8 +72,13 @@ class _NormFn(torch.autograd.Function):
         dout2 = dout.reshape(-1, d) if dout is not None else None
         ds2 = ds.reshape(-1, d) if ds is not None else None
         want_stream = has_resid and p > 0.0
+        dfr = gemm.deferring() if ctx.params is not None else None
         dx, dstream, dw, db, dxs = C.norm_bwd(dout2, ds2, s, weight, bias, mean, rstd, float(p), int(seed), int(kind),
-                                              want_stream, *_acc_targets(ctx.params), want_colsum=ctx.colsum)
+                                              want_stream, *_acc_targets(ctx.params), want_colsum=ctx.colsum,
+                                              partials_only=dfr is not None)
+        if dfr is not None:  # deferred window: the weight / bias gradient partials are reduced once per window
+            _defer_partials(dfr, ctx.params, dw, db)
+            dw = db = None
         dx = dx.view(shape)
         if ctx.colsum:  # handed to the producing linear layer's backward as its bias gradient (ops/gemm.py)
             # with the tensor's version: autograd may add a second consumer's gradient into dx in place, after which
@@ -111,6 +117,18 @@ class _NormOnlyFn(torch.autograd.Function):
                                       int(kind), False, *_acc_targets(ctx.params))
         streams.pair_join()
         return (dx.view(shape),) + _param_grads(ctx.params, weight, bias, dw, db) + (None, None, None)
+
+
+def _defer_partials(dfr, params, dw_part, db_part):
+    """Keep this micro-batch's [G, d] partials (no_sync) or reduce them with the kept ones into the flat gradient (the
+    window's last micro-batch): one reduction per parameter per window instead of one per micro-batch."""
+    for prm, part in ((params[0], dw_part), (params[1], db_part)):
+        if prm is None or part is None:
+            continue
+        out = _gbuf(prm)
+        kept = dfr.partials(out, part)
+        if kept is not None:
+            colsum_partials_acc(out, torch.cat(kept + [part]) if kept else part)
 
 
 def _acc_targets(params):
