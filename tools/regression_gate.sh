@@ -18,4 +18,13 @@ exec_args=(
   --bench "--model flan-t5-xl --batch-per-gpu 16 --steps 5 --warmup 2"
   --bench "--dtype fp32 --batch-per-gpu 16 --steps 6 --warmup 2"
 )
+# GATE_SMALL=1: also the reference's small micro-batch / long-target shapes (train-torchrun: batch 1 x GA 16, BART
+# 1024 / 1024)
+if [ "${GATE_SMALL:-0}" = 1 ]; then
+  exec_args+=(
+    --bench "--model bart-large --src-len 1024 --tgt-len 1024 --batch-per-gpu 64 --steps 5 --warmup 2"
+    --bench "--batch-per-gpu 8 --grad-accum 16 --steps 6 --warmup 2"
+    --bench "--batch-per-gpu 1 --grad-accum 16 --steps 6 --warmup 2"
+  )
+fi
 python tools/gpu_ab.py "${exec_args[@]}"
