@@ -759,6 +759,10 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
             if constexpr ((RS & 128) == 0) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, o), srdC, off, 0, 0);
           }
           __builtin_amdgcn_sched_barrier(0);
+          if constexpr (EPI == W4_EPI_RELU) {  // this row group's 2 of the thread's 8 mask words of the tile
+            uint32_t* mp = P.mask + (size_t)(((m0 / 256) * P.tn + n0 / 256) * 256 + tid) * 8;
+            *reinterpret_cast<u32x2*>(mp + 2 * ii) = u32x2{mw[2 * ii], mw[2 * ii + 1]};
+          }
           if constexpr (EPI == W4_EPI_GELU) {
             // the derivative output of the same 32 rows through the same scratch (this wave's DS ops run in order)
 #pragma unroll
@@ -801,11 +805,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
             if (n0 + wn * 128 + 16 * j + 4 * qd < P.N) *reinterpret_cast<f32x4*>(cp + 16 * j) = csum[j];
         }
       }
-      if constexpr (EPI == W4_EPI_RELU) {  // this thread's 8 mask words of the tile
-        uint32_t* mp = P.mask + (size_t)(((m0 / 256) * P.tn + n0 / 256) * 256 + tid) * 8;
-        *reinterpret_cast<u32x4*>(mp) = u32x4{mw[0], mw[1], mw[2], mw[3]};
-        *reinterpret_cast<u32x4*>(mp + 4) = u32x4{mw[4], mw[5], mw[6], mw[7]};
-      }
+
     }
     __builtin_amdgcn_sched_barrier(0);
     // next tile becomes current
