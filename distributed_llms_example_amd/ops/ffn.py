@@ -47,11 +47,12 @@ EPILOGUES = {"relu": (1, 3), "gelu": (2, 4), "gelu_new": (5, 6), "gelu_fast": (5
 _VARIANT = int(os.environ.get("DLLM_GEMM_FUSED_VARIANT", "-1"))  # -1: picked by K in csrc/bind.cpp
 _RELU_MASK = os.environ.get("DLLM_RELU_MASK", "1") != "0"  # 0: the backward re-reads H (A/B runs)
 _COLSUM = os.environ.get("DLLM_FFN_BIAS_COLSUM", "1") != "0"  # 0: wi bias gradient by a separate column-sum pass
-# ReLU FFN (T5) on csrc/gemm_w4.hip: forward with the ReLU + dropout + bit-mask epilogue, backward input gradient through
-# the mask (DLLM_W4_FFN=1) instead of the 8-wave ping-pong kernel of csrc/gemm_fused.hip (default).  Measured 0.5 %
-# slower per t5-base step (profiles/r3_w4_ffn_ab.txt): w4's epilogue (the dropout hash of 64K elements per tile) runs
-# with the matrix cores idle, where the ping-pong kernel's second wave per SIMD keeps them busy.
-_W4_FFN = os.environ.get("DLLM_W4_FFN", "0") == "1"
+# ReLU FFN (T5) on csrc/gemm_w4.hip (default since round 5): forward with the ReLU + dropout + bit-mask epilogue, backward
+# input gradient through that mask, instead of the 8-wave ping-pong kernel of csrc/gemm_fused.hip (DLLM_W4_FFN=0).  In
+# round 3 it measured 0.5 % slower (profiles/r3_w4_ffn_ab.txt): its epilogue spilled 53 VGPRs because all 8 mask words
+# of a tile stayed live through it.  Stored per row group (round 5) the bias-free variant is spill-free: forward 2.74 vs
+# 2.90 ms at the t5-base encoder shape, step +0.24 % / +0.50 % on two boxes (profiles/r5_w4_relu_ffn_ab.txt).
+_W4_FFN = os.environ.get("DLLM_W4_FFN", "1") != "0"
 # The ReLU backward (dU = dY Wo through the forward's bit mask) on csrc/gemm_w4.hip, reading the ping-pong forward's
 # mask layout (mask_pp): 17 % faster than the ping-pong backward kernel (profiles/r3_ffn_kernel_profile.txt; whole step -0.9 %, profiles/r3_w4_ffn_bwd_ab.txt)
 _W4_FFN_BWD = os.environ.get("DLLM_W4_FFN_BWD", "1") != "0"
