@@ -1787,7 +1787,9 @@ extern "C" int dllm_attn_bwd(AttnParams* pp, hipStream_t st) {
   p.sq_pad = p.n_tiles * FWD_BM;
   if (p.p_drop > 0.f && p.dmask == nullptr) return -5;
   // column sums need the staged stores of all three kernels (and the v2 / short-query dK/dV kernels)
-  if ((p.csq != nullptr || p.csk != nullptr) && (!DQ_STAGE || !DKDV2_STAGE || !DKDV_SQ_STAGE || p.rowrec == nullptr))
+  // (the column-sum variants are instantiated for the bias-LUT-free kernels only)
+  if ((p.csq != nullptr || p.csk != nullptr) &&
+      (!DQ_STAGE || !DKDV2_STAGE || !DKDV_SQ_STAGE || p.rowrec == nullptr || p.lut != nullptr))
     return -7;
   if ((p.csk == nullptr) != (p.csv == nullptr)) return -7;
   long nblk = (long)p.n_tiles * p.H * p.B;

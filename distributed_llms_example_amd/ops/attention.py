@@ -160,7 +160,9 @@ class _AttnFn(torch.autograd.Function):
         ctx.cfg = (mode, scale, causal, p, seed, lut is not None and lut.requires_grad, sat_lo, sat_hi)
         # packed inputs straight from a biased projection (ops/linear.py marks its output): the backward kernels also
         # sum dQ / dK / dV over tokens for that projection's bias gradient (colsum_record)
-        ctx.cs = (BIAS_COLSUM and mode != "sep" and _bias_out(a), BIAS_COLSUM and mode == "q_kv" and _bias_out(b))
+        # (bias-LUT-free calls only: the kernels' column-sum variants exist for those, csrc/attn.hip)
+        cs_ok = BIAS_COLSUM and lut is None
+        ctx.cs = (cs_ok and mode != "sep" and _bias_out(a), cs_ok and mode == "q_kv" and _bias_out(b))
         # ops/linear.py stacked_linear: the packed kv is a slice of a multi-layer projection and its
         # gradient has a home in the stacked gradient buffer — write dK/dV there directly
         ctx.grad_into = getattr(b, "_dllm_grad_into", None) if mode == "q_kv" else None
