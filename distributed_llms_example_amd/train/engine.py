@@ -82,9 +82,12 @@ class TrainEngine:
         self.wgrad_defer = gemm.WgradDefer(mem_cap=cap)
         self._defer_mode = os.environ.get("DLLM_DEFER_WGRAD", "auto").lower()
         self._ga_k = 0
+        # callers that measure one micro-batch's activation memory (train/trainer.py coalescing) switch deferral off for
+        # that step: the kept operands of the whole window would count as one micro-batch's activations
+        self.defer_enabled = True
 
     def _defer_for(self, batch: dict, grad_accum: int) -> gemm.WgradDefer | None:
-        if grad_accum <= 1 or self._defer_mode in ("0", "off", "false"):
+        if grad_accum <= 1 or not self.defer_enabled or self._defer_mode in ("0", "off", "false"):
             return None
         if self._defer_mode == "auto":
             ids = batch.get("input_ids")

@@ -285,6 +285,9 @@ class Trainer:
             torch.cuda.synchronize()
             torch.cuda.reset_peak_memory_stats(env.device)
             mem_base = torch.cuda.memory_allocated(env.device)
+            # the measured step runs micro-batch by micro-batch WITHOUT deferred weight gradients (ops/gemm.py
+            # WgradDefer), whose kept operands would otherwise count as one micro-batch's activations
+            eng.defer_enabled = False
         warm_step = self.state.global_step + min(2, max(0, max_steps - self.state.global_step - 1))
         captured_at = None
         t_warm = t_last = None
@@ -340,6 +343,7 @@ class Trainer:
                     cap = self._auto_cap(mem_base, torch.cuda.max_memory_allocated(env.device),
                                          max(self._padded_tokens([b]) for b in group))
                     self.state.coalesce_cap, self.state.coalesce_cap_unit = cap or 0, "padded_tokens"
+                    eng.defer_enabled = True
                 self.scheduler.step()
                 self.state.global_step += 1
                 if runner.replays and captured_at is None:  # the step that captured the HIP graph is warm-up too
