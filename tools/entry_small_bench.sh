@@ -16,3 +16,8 @@ run torchrun_b1_ga16 train-torchrun.py $common --batch-size 1 --grad-accum 16 --
 run torchrun_b8_ga16 train-torchrun.py $common --batch-size 8 --grad-accum 16 --max-steps 16 \
   --evaluation-steps 1000000 --max-eval-samples 8
 run accelerator_b1 train-accelerator.py $common --batch-size 1 --max-steps 200 --max-eval-samples 8 --gen-max-length 16
+# the reference's default training step itself: bart-large-cnn, 1024 source / 1024 target, batch 1 x GA 16
+# (ref/valohai.yaml:10, ref/train-torchrun.py:99,102,119,126)
+bart="--model-ckpt bart-large-cnn --synthetic 2048 --max-source-length 1024 --max-target-length 1024 --output-dir /tmp/esb2"
+run torchrun_bart_cnn_b1_ga16 train-torchrun.py $bart --batch-size 1 --grad-accum 16 --max-steps 16 \
+  --evaluation-steps 1000000 --max-eval-samples 8
