@@ -618,7 +618,6 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
       }
 #pragma unroll
       for (int ii = 0; ii < 4; ++ii) {
-        u32x4 gp[8];  // GELU forward: the packed derivative output of this row group (staged after h)
         u32x2 ga[8][2];  // GELU backward: the saved derivative at this lane's accumulator positions (rows ii, ii + 16)
         if constexpr (EPI == W4_EPI_DGELU) {
 #pragma unroll
@@ -697,7 +696,12 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
             uint32_t g0 = pk2(gx.x, gx.y), g1 = pk2(gx.z, gx.w), h0 = pk2(gy.x, gy.y), h1 = pk2(gy.z, gy.w);
             const auto r0 = __builtin_amdgcn_permlane16_swap(g0, h0, false, false);
             const auto r1 = __builtin_amdgcn_permlane16_swap(g1, h1, false, false);
-            gp[j] = u32x4{r0[0], r1[0], r0[1], r1[1]};
+            // the derivative leaves directly from the swapped layout (16 B per lane, 8 consecutive columns of one
+            // row): keeping all 8 for a second staging pass spilled the epilogue
+            const int nl = nc + 16 * j;
+            const uint32_t goff = n0 + nl < P.N ? (uint32_t)((mr + 32 * ii) * P.ldaux + n0 + nl) * 2u : kOOB;
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, u32x4{r0[0], r1[0], r0[1], r1[1]}), srdX,
+                                                   goff, 0, 0);
           } else if constexpr (EPI == W4_EPI_DGELU) {
             // dU = dH * G (fp32, rounded once); column sums of dU for the bias gradient
 #pragma unroll
@@ -762,24 +766,6 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
           if constexpr (EPI == W4_EPI_RELU) {  // this row group's 2 of the thread's 8 mask words of the tile
             uint32_t* mp = P.mask + (size_t)(((m0 / 256) * P.tn + n0 / 256) * 256 + tid) * 8;
             *reinterpret_cast<u32x2*>(mp + 2 * ii) = u32x2{mw[2 * ii], mw[2 * ii + 1]};
-          }
-          if constexpr (EPI == W4_EPI_GELU) {
-            // the derivative output of the same 32 rows through the same scratch (this wave's DS ops run in order)
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-              const int cj = 2 * j + (qd >> 1);
-              *reinterpret_cast<u32x4*>(scr + rowL * 256 + ((cj ^ (rowL & 15)) << 4)) = gp[j];
-            }
-#pragma unroll
-            for (int s2 = 0; s2 < 8; ++s2) {
-              const int r = 4 * s2 + (lane >> 4), c = lane & 15;
-              const u32x4 o = *reinterpret_cast<const u32x4*>(scr + r * 256 + ((c ^ (r & 15)) << 4));
-              const int col = wn * 128 + 8 * c;
-              const uint32_t off =
-                  n0 + col < P.N ? (uint32_t)((wm * 128 + 32 * ii + r) * P.ldaux + n0 + col) * 2u : kOOB;
-              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, o), srdX, off, 0, 0);
-            }
-            __builtin_amdgcn_sched_barrier(0);
           }
         }
       }
