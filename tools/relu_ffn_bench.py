@@ -47,6 +47,8 @@ def main():
         "pp_relu_drop_fwd": lambda: C.gemm_fused(x, wi, False, 1, None, None, None, 0.1, 1, -1, mask_pp),
         "w4_relu_drop_fwd": lambda: C.gemm_w4(x, wi, False, None, None, False, -1, True, 1, 0.1, 1, mask_w4),
         "w4_relu_nodrop_fwd": lambda: C.gemm_w4(x, wi, False, None, None, False, -1, True, 1, 0.0, 1, mask_w4),
+        "w4_relu_drop_fwd_np": lambda: C.gemm_w4(x, wi, False, None, None, False, -1, False, 1, 0.1, 1, mask_w4),
+        "w4_plain_fwd_np": lambda: C.gemm_w4(x, wi, False, None, None, False, -1, False),
         "w4_plain_fwd": lambda: C.gemm_w4(x, wi, False),
         "lib_fwd": lambda: torch.nn.functional.linear(x, wi),
         "w4_drelu_bwd": lambda: C.gemm_w4(dy, wo, True, None, None, False, -1, True, 7, 0.1, 1, mask_pp, True),
