@@ -145,6 +145,29 @@ def _sync(dev):
         torch.cuda.synchronize()
 
 
+def _torch_profile(step, path: str, top: int = 60) -> None:
+    """One extra (untimed) eager step under torch.profiler: device time per (kernel, Python call site), so the small
+    ATen kernels in a rocprofv3 summary can be traced to the op that launched them.  Env DLLM_TORCH_PROFILE=<file>."""
+    from torch.profiler import ProfilerActivity, profile
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
+        step(0)
+        torch.cuda.synchronize()
+    rows = prof.key_averages(group_by_stack_n=6).table(sort_by="self_cuda_time_total", row_limit=top,
+                                                       max_name_column_width=70)
+    # ATen ops with their Python call sites (the rows above group by stack but do not print it)
+    sites = []
+    for e in prof.key_averages(group_by_stack_n=6):
+        if e.key.startswith("aten::") and e.self_device_time_total > 0 and e.stack:
+            sites.append((e.self_device_time_total, e.count, e.key, " <- ".join(e.stack[:6])))
+    sites.sort(reverse=True)
+    os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
+    with open(path, "w") as f:
+        f.write(rows)
+        f.write("\n# ATen ops by call site: self device us, calls, op, stack\n")
+        for us, n, k, st in sites[:top]:
+            f.write(f"{us:10.1f} {n:6d} {k:28s} {st}\n")
+
+
 def check_rank_consistency(env, eng, model_name: str, batch: int):
     """All-gather what every rank must agree on (RCCL matches collectives by order and size: a mismatch deadlocks or
     silently mixes gradients) and fail loudly, naming the ranks, when anything differs."""
@@ -301,6 +324,8 @@ def main():
     env.barrier()
     _sync(env.device)
     dt = time.perf_counter() - t0
+    if os.environ.get("DLLM_TORCH_PROFILE") and env.rank == 0 and graphed is None:
+        _torch_profile(step, os.environ["DLLM_TORCH_PROFILE"])  # after timing: attributes kernels to call sites
     comm = None
     if eng.reducer is not None:
         eng.reducer.set_timing(False)

@@ -20,7 +20,8 @@ def enable(device_index: int = 0, arch: str = "gfx950") -> str | None:
     mode = os.environ.get("DLLM_TUNABLEOP", "1")
     if mode == "0" or "PYTORCH_TUNABLEOP_ENABLED" in os.environ:
         return None
-    src = os.path.join(ROOT, "configs", "tunableop", f"{arch}.csv")
+    # DLLM_TUNABLEOP_TABLE: another table (A/B of a re-tuned table against the shipped one)
+    src = os.environ.get("DLLM_TUNABLEOP_TABLE") or os.path.join(ROOT, "configs", "tunableop", f"{arch}.csv")
     if not os.path.exists(src):
         return None
     d = os.environ.get("DLLM_TUNABLEOP_DIR") or tempfile.mkdtemp(prefix="dllm_tunableop_")

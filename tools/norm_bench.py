@@ -2,6 +2,7 @@
 
     python tools/norm_bench.py            # one process per DLLM_NORM_BWD_G value (the cap is read once per process)
     python tools/norm_bench.py --one      # this process's setting only
+    python tools/norm_bench.py --rows 4096,1024 --partials   # micro-batch shapes of a deferred GA window
 
 Bytes counted: forward reads x + resid, writes out + s; backward reads dout + ds_extra + s, writes dx + dstream.
 """
@@ -15,7 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def one(rows_list, d, reps):
+def one(rows_list, d, reps, partials=False):
     import torch
     from distributed_llms_example_amd import _ext
     C = _ext.native()
@@ -29,8 +30,9 @@ def one(rows_list, d, reps):
         dse = torch.randn(N, d, device="cuda", generator=g).bfloat16()
         fwd = lambda: C.norm_fwd(x, r, w, None, 1e-6, 0.1, 7, 0, True)
         o, s, mean, rstd = fwd()
-        bwd = lambda: C.norm_bwd(dout, dse, s, w, None, mean, rstd, 0.1, 7, 0, True, None, None)
-        res = {"N": N, "d": d, "G": int(os.environ.get("DLLM_NORM_BWD_G", "512"))}
+        bwd = lambda: C.norm_bwd(dout, dse, s, w, None, mean, rstd, 0.1, 7, 0, True, None, None,
+                                 partials_only=partials)
+        res = {"N": N, "d": d, "G": int(os.environ.get("DLLM_NORM_BWD_G", "512")), "partials_only": partials}
         for name, fn, nbytes in (("fwd", fwd, 4 * N * d * 2), ("bwd", bwd, 5 * N * d * 2)):
             for _ in range(3):
                 fn()
@@ -56,15 +58,16 @@ def main():
     ap.add_argument("--d", type=int, default=768)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--grids", default="256,512,1024,2048")
+    ap.add_argument("--partials", action="store_true", help="backward keeps the per-block dw partials (deferred GA)")
     a = ap.parse_args()
     rows = [int(v) for v in a.rows.split(",")]
     if a.one:
-        one(rows, a.d, a.reps)
+        one(rows, a.d, a.reps, a.partials)
         return
     for gv in a.grids.split(","):
         env = dict(os.environ, DLLM_NORM_BWD_G=gv)
         r = subprocess.run([sys.executable, __file__, "--one", "--rows", a.rows, "--d", str(a.d), "--reps",
-                            str(a.reps)], env=env)
+                            str(a.reps)] + (["--partials"] if a.partials else []), env=env)
         if r.returncode != 0:
             sys.exit(r.returncode)
 

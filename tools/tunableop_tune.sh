@@ -4,7 +4,7 @@
 # previous table is tools/tunableop_ab.sh.  A heartbeat line every 50 s keeps the (otherwise silent) tuning run alive.
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/tune
+O=${TUNE_OUT:-gpurun_out/tune}
 mkdir -p $O
 ( while sleep 50; do echo "[tune] alive: $(grep -vc '^Validator' $O/tunableop_results0.csv 2>/dev/null) solutions"; done ) &
 HB=$!
