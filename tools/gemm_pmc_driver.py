@@ -3,7 +3,8 @@ hipBLASLt (torch, shipped TunableOp table), a few launches each.
 
     python tools/gemm_pmc_driver.py [M K N variant]      (default: t5-base encoder QKV at b=128, ping-pong variant 9)
 
-variant "w4": the one-wave-per-SIMD kernel (csrc/gemm_w4.hip), "w4nn": the same with a k-major B (input gradient).
+variant "w4": the one-wave-per-SIMD kernel (csrc/gemm_w4.hip), "w4nn": the same with a k-major B (input gradient),
+"wg": its weight-gradient mode (c [N, K] fp32 += dy[M, N]^T x[M, K], both operands k-major, split-K), the same FLOPs.
 """
 import os
 import sys
@@ -23,8 +24,12 @@ C = _ext.native()
 x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
 w = (torch.randn(N, K, device="cuda") * K ** -0.5).to(torch.bfloat16)
 wt = w.t().contiguous()
+dy = torch.randn(M, N, device="cuda").to(torch.bfloat16) if V == "wg" else None
+c = torch.zeros(N, K, device="cuda") if V == "wg" else None
 for _ in range(5):
-    if V == "w4":
+    if V == "wg":
+        C.gemm_wgrad(dy, x, c, True, -1, 0)
+    elif V == "w4":
         C.gemm_w4(x, w, False)
         F.linear(x, w)
     elif V == "w4nn":  # x [M, K] . wt [K, N]
