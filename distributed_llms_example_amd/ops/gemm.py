@@ -38,7 +38,8 @@ from . import streams
 #          hipBLASLt's NN kernels by 1-12 % (o / wo / fc2, encoder-QKV and BART-QKV dgrads, the residual-accumulating
 #          ones included) and the short-K wide forwards (QKV, +1-3 %); the other forwards and the deeper dgrads stay on
 #          hipBLASLt, which is 1-17 % faster there (profiles/r3_gemm_w4_grp_sweep.txt);
-#   "1": every supported shape on gemm_w4 (A/B and tests), "0" (default): none.
+#   "dgrad": the input-gradient shapes of "auto" only; "1": every supported shape on gemm_w4 (A/B and tests);
+#   "0" (default): none.
 # In-situ whole-step A/B (profiles/r3_w4_routing_ab.txt) overrules the microbenchmark: with every shape above routed
 # to w4 the t5-base / bart-large steps ran 0.8-1 % SLOWER than hipBLASLt-only, although each routed shape is faster in
 # isolation (operands there sit in the caches; in the step they come from HBM, and w4's one-k-tile prefetch depth is
@@ -54,8 +55,10 @@ colsum_handoffs = 0  # bias gradients taken from a norm backward's column sums (
 def _w4_ok(a: torch.Tensor, b: torch.Tensor, kmajor: bool) -> bool:
     if not _W4 or a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16 or not _ext.use_native(a):
         return False
-    if _W4_MODE == "auto":
+    if _W4_MODE in ("auto", "dgrad"):
         K = a.shape[-1]
+        if _W4_MODE == "dgrad" and not kmajor:  # "dgrad": the input-gradient half of "auto" only
+            return False
         if kmajor:  # input gradients
             ok = K <= _W4_DGRAD_MAX_K or (K <= 2304 and a.shape[0] >= 131072) or (K <= 3072 and b.shape[-1] >= 1024)
         else:  # forwards: short-K, wide outputs (the QKV projections)
