@@ -7,11 +7,12 @@ Who runs what (t5-base / bart-large training step, default settings):
   split-K pass; round 5, 2-8 % faster than the csrc/gemm.hip kernel it replaced);
 * the FFN input GEMMs with their activation / dropout epilogues and the FFN backward through the activation
   (ops/ffn.py): csrc/gemm_fused.hip and csrc/gemm_w4.hip;
-* the PLAIN projections — forward ``Y = X Wᵀ (+ b)`` and input gradient ``dX (+)= dY W`` of the attention q/k/v/o and
-  FFN output layers, and the LM head — go to the library (hipBLASLt through torch, with the TunableOp table in
-  configs/tunableop/): csrc/gemm_w4.hip ties it on these shapes in isolation and lost 0.8 % of the step in situ
-  (``_W4_MODE`` below, profiles/r3_w4_routing_ab.txt).  ``DLLM_W4_GEMM=1`` routes every supported shape to
-  csrc/gemm_w4.hip, ``auto`` the shapes it wins in isolation.
+* the PLAIN projections — forward ``Y = X Wᵀ (+ b)`` of the attention q/k/v/o and FFN output layers, and the LM
+  head — go to the library (hipBLASLt through torch, with the TunableOp table in configs/tunableop/): csrc/gemm_w4.hip
+  ties it on these shapes in isolation and lost 0.8 % of the step in situ (``_W4_MODE`` below,
+  profiles/r3_w4_routing_ab.txt).  Their input gradients ``dX (+)= dY W`` run on csrc/gemm_w4.hip where that measured
+  faster in the step (layers at most 768 features wide: t5-base), on hipBLASLt otherwise.  ``DLLM_W4_GEMM=1`` routes
+  every supported shape to csrc/gemm_w4.hip, ``auto`` the shapes it wins in isolation, ``0`` none.
 
 Weight-gradient GEMM notes:
 
@@ -39,15 +40,20 @@ from . import streams
 #          ones included) and the short-K wide forwards (QKV, +1-3 %); the other forwards and the deeper dgrads stay on
 #          hipBLASLt, which is 1-17 % faster there (profiles/r3_gemm_w4_grp_sweep.txt);
 #   "dgrad": the input-gradient shapes of "auto" only; "1": every supported shape on gemm_w4 (A/B and tests);
-#   "0" (default): none.
+#   "dgrad768" (default): the "dgrad" shapes whose output (the layer's input features) is at most 768 wide;
+#   "0": none (hipBLASLt for every plain projection).
 # In-situ whole-step A/B (profiles/r3_w4_routing_ab.txt) overrules the microbenchmark: with every shape above routed
 # to w4 the t5-base / bart-large steps ran 0.8-1 % SLOWER than hipBLASLt-only, although each routed shape is faster in
 # isolation (operands there sit in the caches; in the step they come from HBM, and w4's one-k-tile prefetch depth is
-# the shallower).  The default is therefore hipBLASLt for the linear projections; csrc/gemm_w4.hip keeps the shapes it
-# wins in the step: the T5 FFN ReLU input gradient (ops/ffn.py, -0.9 % step time).
-_W4_MODE = os.environ.get("DLLM_W4_GEMM", "0")
+# the shallower).  The forwards therefore stay on hipBLASLt.  The input gradients measured in situ split by width:
+# d_model 768 (t5-base's o / q / qkv input gradients) +0.33 % and +0.23 % on two leases, 4 of 4 interleaved pairs ahead
+# on the second (profiles/r5_w4route_dgrad_ab.txt, r5_w4_dgrad768_ab.txt); d_model 1024 (t5-large, bart-large) -0.45 to
+# -0.86 %: "dgrad768" routes the first and leaves the second on hipBLASLt.  csrc/gemm_w4.hip also runs the T5 FFN ReLU
+# forward and input gradient (ops/ffn.py).
+_W4_MODE = os.environ.get("DLLM_W4_GEMM", "dgrad768")
 _W4 = _W4_MODE != "0"
 _W4_DGRAD_MAX_K = 1024
+_W4_NARROW_MAX_OUT = 768
 w4_calls = 0  # projections that ran on csrc/gemm_w4.hip (tests assert the kernel really ran)
 colsum_handoffs = 0  # bias gradients taken from a norm backward's column sums (bias_grad_accumulate)
 
@@ -55,9 +61,11 @@ colsum_handoffs = 0  # bias gradients taken from a norm backward's column sums (
 def _w4_ok(a: torch.Tensor, b: torch.Tensor, kmajor: bool) -> bool:
     if not _W4 or a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16 or not _ext.use_native(a):
         return False
-    if _W4_MODE in ("auto", "dgrad"):
+    if _W4_MODE in ("auto", "dgrad", "dgrad768"):
         K = a.shape[-1]
-        if _W4_MODE == "dgrad" and not kmajor:  # "dgrad": the input-gradient half of "auto" only
+        if _W4_MODE != "auto" and not kmajor:  # "dgrad", "dgrad768": the input-gradient half of "auto" only
+            return False
+        if _W4_MODE == "dgrad768" and b.shape[-1] > _W4_NARROW_MAX_OUT:
             return False
         if kmajor:  # input gradients
             ok = K <= _W4_DGRAD_MAX_K or (K <= 2304 and a.shape[0] >= 131072) or (K <= 3072 and b.shape[-1] >= 1024)

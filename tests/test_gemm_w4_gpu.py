@@ -189,3 +189,26 @@ def test_gemm_w4_gelu_backward_colsum(M, d, F_):
     assert _rel(du, ref) < 1e-2, _rel(du, ref)
     ref_part = ref.view(M // 128, 128, F_).sum(1)
     assert _rel(part, ref_part) < 1e-2, _rel(part, ref_part)
+
+
+@pytest.mark.parametrize("N_out,K_in,routed", [(768, 768, True), (2304, 768, True), (1024, 1024, False),
+                                               (3072, 1024, False)])
+def test_default_dgrad_routing(N_out, K_in, routed):
+    """Default DLLM_W4_GEMM=dgrad768 (ops/gemm.py): a projection's input gradient dX = dY W runs on gemm_w4 when the
+    layer is at most 768 features wide (t5-base's o / qkv; 2304-deep only with >= 128K token rows), on hipBLASLt for
+    wider layers (t5-large / bart-large), and the forward always on hipBLASLt; either way it matches fp32."""
+    from distributed_llms_example_amd.ops import gemm
+    if gemm._W4_MODE != "dgrad768":
+        pytest.skip(f"DLLM_W4_GEMM={gemm._W4_MODE} set in the environment")
+    M = 131072 if N_out > 1024 else 4096
+    torch.manual_seed(N_out + K_in)
+    dy = torch.randn(M, N_out, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N_out, K_in, device=DEV) * N_out ** -0.5).to(torch.bfloat16)
+    before = gemm.w4_calls
+    got = gemm.linear_dgrad(dy, w)
+    assert (gemm.w4_calls - before == 1) == routed
+    assert _rel(got, dy.float() @ w.float()) < 8e-3
+    x = torch.randn(M, K_in, device=DEV).to(torch.bfloat16)
+    before = gemm.w4_calls
+    gemm.linear_fwd(x, w)
+    assert gemm.w4_calls == before  # forwards stay on hipBLASLt
