@@ -11,8 +11,9 @@ Who runs what (t5-base / bart-large training step, default settings):
   head — go to the library (hipBLASLt through torch, with the TunableOp table in configs/tunableop/): csrc/gemm_w4.hip
   ties it on these shapes in isolation and lost 0.8 % of the step in situ (``_W4_MODE`` below,
   profiles/r3_w4_routing_ab.txt).  Their input gradients ``dX (+)= dY W`` run on csrc/gemm_w4.hip where that measured
-  faster in the step (layers at most 768 features wide: t5-base), on hipBLASLt otherwise.  ``DLLM_W4_GEMM=1`` routes
-  every supported shape to csrc/gemm_w4.hip, ``auto`` the shapes it wins in isolation, ``0`` none.
+  faster in the step (layers at most 768 features wide, >= 64K token rows: t5-base at large batch), on hipBLASLt
+  otherwise.  ``DLLM_W4_GEMM=1`` routes every supported shape to csrc/gemm_w4.hip, ``auto`` the shapes it wins in
+  isolation, ``0`` none.
 
 Weight-gradient GEMM notes:
 
@@ -40,7 +41,7 @@ from . import streams
 #          ones included) and the short-K wide forwards (QKV, +1-3 %); the other forwards and the deeper dgrads stay on
 #          hipBLASLt, which is 1-17 % faster there (profiles/r3_gemm_w4_grp_sweep.txt);
 #   "dgrad": the input-gradient shapes of "auto" only; "1": every supported shape on gemm_w4 (A/B and tests);
-#   "dgrad768" (default): the "dgrad" shapes whose output (the layer's input features) is at most 768 wide;
+#   "dgrad768" (default): the "dgrad" shapes whose output (the layer's input features) is at most 768 wide, >= 64K rows;
 #   "0": none (hipBLASLt for every plain projection).
 # In-situ whole-step A/B (profiles/r3_w4_routing_ab.txt) overrules the microbenchmark: with every shape above routed
 # to w4 the t5-base / bart-large steps ran 0.8-1 % SLOWER than hipBLASLt-only, although each routed shape is faster in
@@ -48,12 +49,14 @@ from . import streams
 # the shallower).  The forwards therefore stay on hipBLASLt.  The input gradients measured in situ split by width:
 # d_model 768 (t5-base's o / q / qkv input gradients) +0.33 % and +0.23 % on two leases, 4 of 4 interleaved pairs ahead
 # on the second (profiles/r5_w4route_dgrad_ab.txt, r5_w4_dgrad768_ab.txt); d_model 1024 (t5-large, bart-large) -0.45 to
-# -0.86 %: "dgrad768" routes the first and leaves the second on hipBLASLt.  csrc/gemm_w4.hip also runs the T5 FFN ReLU
-# forward and input gradient (ops/ffn.py).
+# -0.86 %: "dgrad768" routes the first and leaves the second on hipBLASLt, and only with >= 64K token rows: at the
+# micro-batch shapes (t5-base b=8 / b=1 x GA16, 8K / 1K rows) w4 cost 2.9 / 6.3 % of the step (r5_w4_dgrad768_ab.txt).
+# csrc/gemm_w4.hip also runs the T5 FFN ReLU forward and input gradient (ops/ffn.py).
 _W4_MODE = os.environ.get("DLLM_W4_GEMM", "dgrad768")
 _W4 = _W4_MODE != "0"
 _W4_DGRAD_MAX_K = 1024
 _W4_NARROW_MAX_OUT = 768
+_W4_NARROW_MIN_ROWS = 65536  # fewer token rows (micro-batches of 8 / 1): hipBLASLt, 2.9 / 6.3 % faster in the step
 w4_calls = 0  # projections that ran on csrc/gemm_w4.hip (tests assert the kernel really ran)
 colsum_handoffs = 0  # bias gradients taken from a norm backward's column sums (bias_grad_accumulate)
 
@@ -65,7 +68,7 @@ def _w4_ok(a: torch.Tensor, b: torch.Tensor, kmajor: bool) -> bool:
         K = a.shape[-1]
         if _W4_MODE != "auto" and not kmajor:  # "dgrad", "dgrad768": the input-gradient half of "auto" only
             return False
-        if _W4_MODE == "dgrad768" and b.shape[-1] > _W4_NARROW_MAX_OUT:
+        if _W4_MODE == "dgrad768" and (b.shape[-1] > _W4_NARROW_MAX_OUT or a.shape[0] < _W4_NARROW_MIN_ROWS):
             return False
         if kmajor:  # input gradients
             ok = K <= _W4_DGRAD_MAX_K or (K <= 2304 and a.shape[0] >= 131072) or (K <= 3072 and b.shape[-1] >= 1024)

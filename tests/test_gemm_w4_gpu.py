@@ -191,16 +191,17 @@ def test_gemm_w4_gelu_backward_colsum(M, d, F_):
     assert _rel(part, ref_part) < 1e-2, _rel(part, ref_part)
 
 
-@pytest.mark.parametrize("N_out,K_in,routed", [(768, 768, True), (2304, 768, True), (1024, 1024, False),
-                                               (3072, 1024, False)])
-def test_default_dgrad_routing(N_out, K_in, routed):
+@pytest.mark.parametrize("N_out,K_in,M,routed", [(768, 768, 65536, True), (2304, 768, 131072, True),
+                                                 (768, 768, 8192, False), (1024, 1024, 65536, False),
+                                                 (3072, 1024, 131072, False)])
+def test_default_dgrad_routing(N_out, K_in, M, routed):
     """Default DLLM_W4_GEMM=dgrad768 (ops/gemm.py): a projection's input gradient dX = dY W runs on gemm_w4 when the
-    layer is at most 768 features wide (t5-base's o / qkv; 2304-deep only with >= 128K token rows), on hipBLASLt for
-    wider layers (t5-large / bart-large), and the forward always on hipBLASLt; either way it matches fp32."""
+    layer is at most 768 features wide and has >= 64K token rows (t5-base's o / qkv at large batch; 2304-deep only with
+    >= 128K rows), on hipBLASLt for wider layers (t5-large / bart-large) and micro-batches, and the forward always on
+    hipBLASLt; either way it matches fp32."""
     from distributed_llms_example_amd.ops import gemm
     if gemm._W4_MODE != "dgrad768":
         pytest.skip(f"DLLM_W4_GEMM={gemm._W4_MODE} set in the environment")
-    M = 131072 if N_out > 1024 else 4096
     torch.manual_seed(N_out + K_in)
     dy = torch.randn(M, N_out, device=DEV).to(torch.bfloat16)
     w = (torch.randn(N_out, K_in, device=DEV) * N_out ** -0.5).to(torch.bfloat16)
