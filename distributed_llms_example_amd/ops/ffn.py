@@ -53,6 +53,10 @@ _COLSUM = os.environ.get("DLLM_FFN_BIAS_COLSUM", "1") != "0"  # 0: wi bias gradi
 # of a tile stayed live through it.  Stored per row group (round 5) the bias-free variant is spill-free: forward 2.74 vs
 # 2.90 ms at the t5-base encoder shape, step +0.24 % / +0.50 % on two boxes (profiles/r5_w4_relu_ffn_ab.txt).
 _W4_FFN = os.environ.get("DLLM_W4_FFN", "1") != "0"
+# ... from this many token rows up; below it the ping-pong forward (its bit mask feeds the same w4 backward) measured
+# +0.35 % / +0.26 % at t5-base b=8 / b=1 x GA16 (8K / 1K encoder rows: too few 256 x 256 tiles for w4's one workgroup
+# per CU, profiles/r5_ffn_small_rows_ab.txt)
+_W4_FFN_MIN_ROWS = int(os.environ.get("DLLM_W4_FFN_MIN_ROWS", "65536"))
 # The ReLU backward (dU = dY Wo through the forward's bit mask) on csrc/gemm_w4.hip, reading the ping-pong forward's
 # mask layout (mask_pp): 17 % faster than the ping-pong backward kernel (profiles/r3_ffn_kernel_profile.txt; whole step -0.9 %, profiles/r3_w4_ffn_bwd_ab.txt)
 _W4_FFN_BWD = os.environ.get("DLLM_W4_FFN_BWD", "1") != "0"
@@ -76,6 +80,13 @@ def _enabled() -> bool:
     return os.environ.get("DLLM_FUSED_FFN", "1") != "0"
 
 
+# FFNs with fewer token rows than this run unfused (library GEMMs + the activation / dropout kernel): at 1024 rows and
+# below (t5-base b=1 x GA16 encoder and decoder, b=8 decoder) the fused kernels' 256 x 256 tiles leave most CUs idle and
+# hipBLASLt's tuned small-shape kernels win: +1.9 % (b=8 x GA16), +2.2 % (b=1 x GA16) over fusing them
+# (profiles/r5_ffn_small_rows_ab.txt; unfusing the 8K-row encoder FFNs of b=8 as well lost 1.6 %)
+_FUSED_MIN_ROWS = int(os.environ.get("DLLM_FUSED_FFN_MIN_ROWS", "1025"))
+
+
 class _FusedFFNFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, wi, bi, wo, bo, act, p, seed, params):
@@ -84,7 +95,7 @@ class _FusedFFNFn(torch.autograd.Function):
         x2 = x.reshape(-1, shape[-1])
         efwd, _ = EPILOGUES[act]
         u = mask = None
-        if efwd == 1 and _W4_FFN and C.gemm_w4_supported(x2, wi, False) and \
+        if efwd == 1 and _W4_FFN and x2.shape[0] >= _W4_FFN_MIN_ROWS and C.gemm_w4_supported(x2, wi, False) and \
                 (bi is None or (bi.dtype == torch.bfloat16 and bi.is_contiguous())):
             global w4_ffn_calls
             w4_ffn_calls += 1
@@ -283,7 +294,7 @@ def ffn_res(x: torch.Tensor, lin_in, lin_out, act: str, p: float = 0.0, seed: in
             and torch.is_grad_enabled()
             and all(_fusable(t) for t in (lin_in.weight, lin_in.bias, lin_out.weight, lin_out.bias))):
         x2 = x.reshape(-1, x.shape[-1])
-        if _fusable_shapes(x2, lin_in.weight, lin_out.weight):
+        if x2.shape[0] >= _FUSED_MIN_ROWS and _fusable_shapes(x2, lin_in.weight, lin_out.weight):
             fused_calls += 1
             bi, bo = lin_in.bias, lin_out.bias
             y, res = _FusedFFNFn.apply(x, lin_in.weight.detach(), None if bi is None else bi.detach(),

@@ -164,7 +164,7 @@ def test_engine_steps_reduce_loss_on_gpu():
     assert _ext.native() is not None
 
 
-@pytest.mark.parametrize("name", ["t5-base", "bart-base", "flan-t5-base"])
+@pytest.mark.parametrize("name", ["t5-base", "t5-base:w4", "bart-base", "flan-t5-base"])
 def test_fused_ffn_matches_unfused_in_engine(name, monkeypatch):
     """TrainEngine (FlatParams: the FFN runs as GEMMs with activation/dropout epilogues, ops/ffn.py) vs the same
     step with DLLM_FUSED_FFN=0 (library GEMMs + activation kernels): same loss, same dropout masks, and the fused
@@ -175,11 +175,15 @@ def test_fused_ffn_matches_unfused_in_engine(name, monkeypatch):
     from distributed_llms_example_amd.parallel.env import init_distributed
     from distributed_llms_example_amd.train.engine import TrainEngine
     env = init_distributed()
+    w4 = name.endswith(":w4")  # the T5 ReLU FFN forward on csrc/gemm_w4.hip (default only from 64K token rows up)
+    name = name.split(":")[0]
+    monkeypatch.setattr(ffn_mod, "_W4_FFN_MIN_ROWS", 0 if w4 else 1 << 62)
     cfg = _cfg(name)
     monkeypatch.setattr(ffn_mod, "_GATED_MIN_MF", 0)  # small shapes: force the fused gated path as well
     monkeypatch.setattr(ffn_mod, "_GATED_MAX_D", 1 << 30)
     torch.manual_seed(0)
     sd = {k: v.to(torch.bfloat16).float() for k, v in build_model(cfg).state_dict().items()}
+    w4_before = ffn_mod.w4_ffn_calls
     b = _batch(cfg, B=4, S=256, T=64)  # 1024 / 256 tokens: the fused kernel's shapes
     m = build_model(cfg)
     m.load_state_dict(sd)
@@ -205,12 +209,32 @@ def test_fused_ffn_matches_unfused_in_engine(name, monkeypatch):
         res.append((float(loss), eng.flat.grad_buf.float().clone(), used))
     (l0, g0, n0), (l1, g1, n1) = res
     assert n0 == 0 and n1 == cfg.num_layers + cfg.num_decoder_layers, (n0, n1)
+    assert (ffn_mod.w4_ffn_calls - w4_before == n1) if w4 else (ffn_mod.w4_ffn_calls == w4_before)
     assert abs(l0 - l1) < 1e-2 * abs(l0) and abs(l1 - l_ref) < 1e-2 * abs(l_ref), (l0, l1, l_ref)
     e0, e1 = ((g0 - g_ref).norm() / g_ref.norm()).item(), ((g1 - g_ref).norm() / g_ref.norm()).item()
     print(f"[fused-ffn {name}] rel err vs fp32 reference: unfused {e0:.4f}, fused {e1:.4f}")
     assert e1 < max(1.5 * e0, 1e-2), (e0, e1)
     cos = torch.nn.functional.cosine_similarity(g0, g1, dim=0).item()
     assert cos > 0.995, cos
+
+
+def test_small_ffn_runs_unfused_by_default(monkeypatch):
+    """Production default (ops/ffn.py _FUSED_MIN_ROWS = 1025): in the engine, FFNs of <= 1024 token rows run unfused
+    (library GEMMs + activation kernel) and larger ones on the fused kernels.  Encoder 4 x 512 = 2048 rows, decoder
+    4 x 64 = 256 rows: one fused FFN per encoder layer, none in the decoder; the step stays finite."""
+    from distributed_llms_example_amd.ops import ffn as ffn_mod
+    from distributed_llms_example_amd.parallel.env import init_distributed
+    from distributed_llms_example_amd.train.engine import TrainEngine
+    monkeypatch.setattr(ffn_mod, "_FUSED_MIN_ROWS", 1025)
+    env = init_distributed()
+    cfg = _cfg("t5-base")
+    torch.manual_seed(0)
+    eng = TrainEngine(build_model(cfg), env, lr=1e-4, dtype=torch.bfloat16)
+    eng.train()
+    before = ffn_mod.fused_calls
+    loss = float(eng.forward_backward(_batch(cfg, B=4, S=512, T=64)))
+    assert ffn_mod.fused_calls - before == cfg.num_layers, ffn_mod.fused_calls - before
+    assert loss == loss and torch.isfinite(eng.flat.grad_buf.float()).all()
 
 
 def test_bart_residual_grad_in_dgrad_gemm(monkeypatch):
