@@ -56,7 +56,8 @@ _W4_MODE = os.environ.get("DLLM_W4_GEMM", "dgrad768")
 _W4 = _W4_MODE != "0"
 _W4_DGRAD_MAX_K = 1024
 _W4_NARROW_MAX_OUT = 768
-_W4_NARROW_MIN_ROWS = 65536  # fewer token rows (micro-batches of 8 / 1): hipBLASLt, 2.9 / 6.3 % faster in the step
+# fewer token rows (micro-batches of 8 / 1): hipBLASLt, 2.9 / 6.3 % faster in the step
+_W4_NARROW_MIN_ROWS = int(os.environ.get("DLLM_W4_DGRAD_MIN_ROWS", "65536"))
 w4_calls = 0  # projections that ran on csrc/gemm_w4.hip (tests assert the kernel really ran)
 colsum_handoffs = 0  # bias gradients taken from a norm backward's column sums (bias_grad_accumulate)
 
