@@ -162,6 +162,10 @@ class WgradDefer:
             return out
         return _wgrad(out, torch.cat(dys), torch.cat(xs), beta)
 
+    def pending(self) -> bool:
+        """Kept weight-gradient operands or norm partials that no GEMM / reduction has consumed yet."""
+        return bool(self.segs or self.psegs)
+
     @torch.no_grad()
     def flush(self) -> None:
         """Every pending window now (compute stream): the end of the last micro-batch's backward, or the memory cap."""

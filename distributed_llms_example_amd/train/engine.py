@@ -172,6 +172,11 @@ class TrainEngine:
         if last:
             self._ga_k = 0
         dfr = self._defer_for(batch, grad_accum)
+        if dfr is None and last and self.wgrad_defer.active and self.wgrad_defer.pending():
+            # a last micro-batch that does not defer itself (too many tokens) still closes the window the earlier ones
+            # opened: its weight-gradient GEMMs merge the kept segments in the backward, before the hooks that launch
+            # the overlapped bucket all-reduces fire (a flush after backward() would add them after the reduction)
+            dfr = self.wgrad_defer
         with ctx, side, gemm.defer_wgrads(dfr, final=last):
             with profiling.range("forward"):
                 out = self.forward(batch)
@@ -184,9 +189,8 @@ class TrainEngine:
                 else:
                     (loss / grad_accum if grad_accum > 1 else loss).backward()
         if last:
-            # weights the last micro-batch did not touch (or all of them, when its size turned deferral off), before
-            # the reducer's post-backward launches their buckets
-            if self.wgrad_defer.segs:
+            # weights the last micro-batch did not touch, before the reducer's post-backward launches their buckets
+            if self.wgrad_defer.pending():
                 self.wgrad_defer.flush()
             self.wgrad_defer.active = True
         elif dfr is not None and dfr.mem_cap is not None and torch.cuda.memory_allocated(self.env.device) > dfr.mem_cap:
@@ -202,7 +206,7 @@ class TrainEngine:
         [lr, lr / bc1, 1 / sqrt(bc2)] (graph mode, ops/optim.py device_hyper)."""
         if lr is not None:
             self.optimizer.param_groups[0]["lr"] = lr
-        if self.wgrad_defer.segs:  # a window left open (fewer micro-batches than its grad_accum)
+        if self.wgrad_defer.pending():  # a window left open (fewer micro-batches than its grad_accum)
             self.wgrad_defer.flush()
         self.wgrad_defer.active = True
         self._ga_k = 0

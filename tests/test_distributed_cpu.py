@@ -509,3 +509,40 @@ def test_bench_self_launches_ranks(n):
     for dt in ("fp32", "bf16"):
         assert c["busbw_gbps"][dt] and all(v > 0 for v in c["busbw_gbps"][dt].values())
     assert "self-launch" in r.stderr
+
+
+# ---------------------------------------------------------------- deferred weight gradients under the overlap reducer
+def _defer_last_big_case(rank, world, native=True, defer=True):
+    """GA 3 on 2 gloo ranks with the hook-overlapped reducer: micro-batches 0-1 defer their weight gradients, the last
+    one is larger and does not (engine._defer_for returns None for it, as the "auto" mode does past DEFER_MAX_TOKENS).
+    The window must still close INSIDE the last backward (before the hooks launch the bucket all-reduces), so the
+    replicas' gradients equal the undeferred run's and each other."""
+    from distributed_llms_example_amd.models import build_model
+    from distributed_llms_example_amd.parallel.env import DistEnv
+    from distributed_llms_example_amd.train.engine import TrainEngine
+    os.environ["DLLM_NATIVE_REDUCER"] = "1" if native else "0"
+    env = DistEnv(rank=rank, world_size=world, backend="gloo", device=torch.device("cpu"))
+    torch.manual_seed(0)
+    eng = TrainEngine(build_model("t5-tiny"), env, lr=1e-3, dtype=torch.float32, bucket_mb=0.05, overlap=True)
+    eng.train(False)
+    small = 2 * 12
+    eng._defer_for = lambda batch, ga: (eng.wgrad_defer if defer and batch["input_ids"].numel() <= small else None)
+    g = torch.Generator().manual_seed(11 + rank)
+    shapes = [(2, 12), (2, 12), (4, 16)]
+    for i, (b, s) in enumerate(shapes):
+        ids = torch.randint(3, 500, (b, s), generator=g)
+        eng.forward_backward({"input_ids": ids, "attention_mask": torch.ones_like(ids),
+                              "labels": torch.randint(3, 500, (b, 6), generator=g)}, grad_accum=3, sync=i == 2)
+    assert not eng.wgrad_defer.pending()
+    return eng.flat.to_canonical(eng.flat.grad_buf).clone(), eng.wgrad_defer.deferred, eng.wgrad_defer.merged
+
+
+@pytest.mark.parametrize("native", [False, pytest.param(True, marks=pytest.mark.skipif(
+    not _native_available(), reason="native extension not built"))])
+def test_deferred_window_closed_by_undeferred_last_micro_batch(native):
+    d = run_ranks(functools.partial(_defer_last_big_case, native=native, defer=True))
+    u = run_ranks(functools.partial(_defer_last_big_case, native=native, defer=False))
+    g0, dd, dm = d[0]
+    assert dd > 0 and dm > 0, (dd, dm)  # the deferral ran, and the last backward merged it
+    torch.testing.assert_close(torch.as_tensor(g0), torch.as_tensor(d[1][0]))  # replicas agree
+    torch.testing.assert_close(torch.as_tensor(g0), torch.as_tensor(u[0][0]), atol=1e-6, rtol=1e-5)
