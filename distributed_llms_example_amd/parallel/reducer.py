@@ -137,6 +137,7 @@ class GradReducer:
         # segments ready at its launch) in launch order; the previous backward's logs are kept in *_last
         self.ready_log: list[int] = []
         self.launch_log: list[tuple[int, int]] = []
+        self.launches = 0  # Python engine: all-reduces actually launched (tests of the eager segmented schedule)
         self.ready_log_last: list[int] = []
         self.launch_log_last: list[tuple[int, int]] = []
         self.rebuilt = False
@@ -182,6 +183,7 @@ class GradReducer:
         self._pending = list(counts)
         self._ready = [False] * len(self.buckets)
         self._next = 0
+        self._cut_next = 0
         self._works = []
         self._callback_queued = False
         if self.native is not None:
@@ -206,12 +208,18 @@ class GradReducer:
             self._pending[b] -= 1
             if self._pending[b] == 0:
                 self._ready[b] = True
-            first = self._next
-            while self._next < len(self.buckets) and self._ready[self._next]:
-                self._next += 1
-            if self._next > first:
-                self.launch_log.extend((b, len(self.ready_log)) for b in range(first, self._next))
-                self._cut_fn(list(range(first, self._next)))
+            # the cut cursor is not the launch cursor: a cut callback may launch right away (eager segmented schedule,
+            # launch_upto) and that must find its buckets still unlaunched
+            first = self._cut_next
+            while self._cut_next < len(self.buckets) and self._ready[self._cut_next]:
+                self._cut_next += 1
+            if self._cut_next > first:
+                cut = list(range(first, self._cut_next))
+                n0 = self._launched_count()
+                self._cut_fn(cut)
+                # logged here unless the Python engine's _launch logged the launches the callback just made
+                if self.native is not None or self._launched_count() == n0:
+                    self.launch_log.extend((b, len(self.ready_log)) for b in cut)
             return
         if self.native is not None:
             before = self.native.launched()
@@ -254,6 +262,9 @@ class GradReducer:
         self.rebuilt = True
         return True
 
+    def _launched_count(self) -> int:
+        return self.native.launched() if self.native is not None else self.launches
+
     def _launch(self, b: int):
         s, e = self.buckets[b]
         view = self.flat.grad_buf[s:e]
@@ -266,6 +277,7 @@ class GradReducer:
         else:
             w = dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         self._works.append((b, w))
+        self.launches += 1
         self.launch_log.append((b, len(self.ready_log)))
 
     def _launch_ready(self):
@@ -325,14 +337,16 @@ class GradReducer:
         self._pending = list(self._counts)
         self._ready = [False] * len(self.buckets)
         self._next = 0
+        self._cut_next = 0
         self._cut_fn = cut_fn
 
     def end_capture_cuts(self) -> list[int]:
-        rest = list(range(self._next, len(self.buckets)))
+        """Buckets no cut covered: launched after the backward."""
+        rest = list(range(self._cut_next, len(self.buckets)))
         self._cut_fn = None
         self._pending = list(self._counts)
         self._ready = [False] * len(self.buckets)
-        self._next = 0
+        self._cut_next = 0
         return rest
 
     def launch_upto(self, n: int):

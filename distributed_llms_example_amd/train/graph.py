@@ -303,6 +303,26 @@ def graph_policy() -> str:
     return {"0": "off", "1": "on"}.get(v, "auto")
 
 
+def _sig_key(sig) -> int:
+    """A process-independent 62-bit key of a batch signature (Python's hash() of strings is salted per process)."""
+    import hashlib
+    return int.from_bytes(hashlib.sha256(repr(sig).encode()).digest()[:8], "little") >> 2
+
+
+def _ranks_agree(sig, eng) -> bool:
+    """Every rank of the default process group runs a step of signature ``sig`` (one tiny all-reduce; itself when
+    there is no group).  The runner's capture and probe decisions issue collectives of their own, so they may only be
+    taken on steps all ranks share."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() <= 1:
+        return True
+    dev = eng.env.device if dist.get_backend() == "nccl" else torch.device("cpu")
+    k = _sig_key(sig)
+    t = torch.tensor([k, -k], dtype=torch.int64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return int(t[0].item()) == -int(t[1].item())
+
+
 def _all_ranks(flag: bool, eng) -> bool:
     """``flag`` AND-ed over the ranks of the default process group (itself when there is none)."""
     import torch.distributed as dist
@@ -348,6 +368,8 @@ class StepRunner:
         self.eager_steps = 0
         # the timed probe needs device events: on the CPU schedule (tests) an enabled runner always replays
         self.policy = ("off" if not self.enabled else graph_policy() if engine.env.device.type == "cuda" else "on")
+        if self.policy == "auto":  # the probe's eager baseline: PROBE timed eager steps after the untimed first one
+            self.warmup = max(self.warmup, 1 + self.PROBE)
         self.decision: dict | None = None  # auto policy: {"graph": bool, "eager_ms": .., "replay_ms": ..}
         self._eager_t: list = []   # (start, end) events of this signature's eager steps
         self._replay_t: list = []  # ... and of its first replays
@@ -373,6 +395,12 @@ class StepRunner:
         if self.enabled:
             sig = batch_signature(passes)
             g = self.graph
+            # while the runner may still capture or probe, its decisions run collectives: take them only on steps whose
+            # signature every rank shares (a disagreeing step runs eagerly and counts for nothing)
+            unsettled = (g is None and self.graph_error is None and sig not in self._eager_sigs) or (
+                g is not None and self.policy == "auto" and self.decision is None)
+            if unsettled and not _ranks_agree(sig, eng):
+                return self._eager(passes, num_items, None)
             if g is not None and sig == g.signature():
                 probing = self.policy == "auto" and self.decision is None
                 if probing and len(self._replay_t) >= self.PROBE:
@@ -418,6 +446,10 @@ class StepRunner:
             # carries the lazy initialisation)
             if self.policy == "auto" and self.decision is None and sig == self._sig and self._seen >= 2:
                 timed = self._events()
+        return self._eager(passes, num_items, timed)
+
+    def _eager(self, passes, num_items, timed):
+        eng = self.eng
         self.eager_steps += 1
         losses = []
         for j, pb in enumerate(passes):
@@ -440,7 +472,7 @@ class StepRunner:
         import statistics
         self._replay_t[-1][1].synchronize()
         med = lambda evs: statistics.median(a.elapsed_time(b) for a, b in evs)  # noqa: E731
-        eager = med(self._eager_t[-2:]) if self._eager_t else float("inf")
+        eager = med(self._eager_t[-self.PROBE:]) if self._eager_t else float("inf")
         replay = med(self._replay_t)
         # one decision for all data-parallel ranks (their schedules must match): graphs only if every rank keeps them
         keep = _all_ranks(replay <= eager * (1.0 + self.GRAPH_TOL), self.eng)

@@ -372,6 +372,10 @@ def _split_schedule_case(rank, world, native=True, ga=2, steps=3, comm="split", 
     ls = [float(gs.replay(data[ga * i:ga * (i + 1)])) for i in range(steps)]
     launched = eng_s.reducer.native.launched() if eng_s.reducer.native is not None else None
     summary = eng_s.reducer.launch_summary()
+    # every bucket launched exactly once per step, and logged once (Python engine: launches counted at _launch)
+    summary["log_len"] = len(eng_s.reducer.launch_log_last)
+    summary["py_launches"] = eng_s.reducer.launches if eng_s.reducer.native is None else None
+    summary["steps"] = steps
     p_split = eng_s.flat.to_canonical(eng_s.flat.param_buf).clone()
     eng_s.disable_step_seeds()
     eng_s.reducer.remove()
@@ -407,6 +411,9 @@ def test_split_graph_schedule_matches_eager_overlap(native, comm):
             assert launched == 0  # finalize resets the schedule after launching every bucket
         if comm == "overlap":  # the segmented schedule launches every bucket but the tail before backward ends
             assert summary["launched_before_backward_end"] >= nb - 1, summary
+            assert summary["log_len"] == nb, summary
+        if summary["py_launches"] is not None:
+            assert summary["py_launches"] == nb * summary["steps"], summary
     assert torch.equal(torch.as_tensor(out[0][2]), torch.as_tensor(out[1][2]))  # ranks agree
 
 
@@ -480,6 +487,43 @@ def test_graph_decisions_agree_across_ranks():
     _all_ranks): one rank failing / preferring eager sends every rank to eager, so their collective schedules match."""
     out = run_ranks(_all_ranks_case)
     assert out[0] == out[1] == [True, False, False]
+
+
+def _runner_sig_case(rank, world):
+    """StepRunner on 2 gloo ranks whose batch shapes disagree on one step near the capture point (rank 1 gets a
+    ragged batch): the step must run eagerly on both ranks and count for neither, so both capture on the same step and
+    their collectives stay matched (a rank-local capture decision would pair its agreement all-reduce with the other
+    rank's gradient buckets)."""
+    import functools
+    from distributed_llms_example_amd.models import build_model
+    from distributed_llms_example_amd.ops.rng import manual_seed
+    from distributed_llms_example_amd.parallel.env import DistEnv
+    from distributed_llms_example_amd.train import graph as G
+    from distributed_llms_example_amd.train.engine import TrainEngine
+    G.GraphedStep = functools.partial(G.GraphedStep, use_graph=False)
+    env = DistEnv(rank=rank, world_size=world, backend="gloo", device=torch.device("cpu"))
+    g = torch.Generator().manual_seed(3 + rank)
+
+    def batch(B, S=12, T=6):
+        return {"input_ids": torch.randint(3, 500, (B, S), generator=g),
+                "attention_mask": torch.ones(B, S, dtype=torch.long), "labels": torch.randint(3, 500, (B, T), generator=g)}
+
+    data = [batch(1 if (rank == 1 and i == 2) else 2) for i in range(6)]
+    torch.manual_seed(0)
+    manual_seed(5)
+    eng = TrainEngine(build_model("t5-tiny"), env, lr=1e-3, dtype=torch.float32, bucket_mb=0.05)
+    eng.train(False)
+    runner = G.StepRunner(eng, enabled=True, warmup=2)
+    for b in data:
+        runner([b])
+    return runner.replays, runner.eager_steps, eng.flat.to_canonical(eng.flat.param_buf).clone()
+
+
+def test_step_runner_waits_for_rank_agreement():
+    out = run_ranks(_runner_sig_case)
+    (r0, e0, p0), (r1, e1, p1) = out[0], out[1]
+    assert (r0, e0) == (r1, e1) == (3, 3), (out[0][:2], out[1][:2])  # steps 0, 1, 2 (disagreeing) eager; 3 capture; 4, 5
+    torch.testing.assert_close(torch.as_tensor(p0), torch.as_tensor(p1))
 
 
 # ---------------------------------------------------------------- bench.py self-launch (the driver's `bench.py --gpus N`)

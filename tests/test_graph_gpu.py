@@ -178,7 +178,8 @@ def test_step_runner_auto_policy(tol, keep, monkeypatch):
     assert runner.decision is not None and runner.decision["graph"] is keep, runner.decision
     assert runner.decision["eager_ms"] > 0 and runner.decision["replay_ms"] > 0
     # capture step + probe replays, then either replays to the end or eager steps
-    assert runner.replays == (steps - 2 if keep else StepRunner.PROBE)
+    assert runner.warmup == 1 + StepRunner.PROBE  # auto: PROBE timed eager steps after the untimed first one
+    assert runner.replays == (steps - runner.warmup if keep else StepRunner.PROBE)
     p_auto = eng.flat.to_canonical(eng.flat.param_buf).float().clone()
     eng.disable_step_seeds()
     cfg, ref = _setup()
