@@ -44,9 +44,9 @@ def base_parser(description: str, defaults: dict | None = None) -> argparse.Argu
                         "first step's measured activation memory allows in 60%% of HBM), N (max samples per pass), 0 off")
     g.add_argument("--learning-rate", type=float, default=5e-5)
     g.add_argument("--max-steps", type=int, default=-1)
-    g.add_argument("--bucket-mb", type=bucket_mb_arg, default=None,
-                   help="gradient all-reduce bucket size in MiB, or 'auto' (probe RCCL's bus bandwidth over 32-256 MiB "
-                        "on the job's process group and take the smallest size within 5%% of the best; default 128)")
+    g.add_argument("--bucket-mb", type=bucket_mb_arg, default="auto",
+                   help="gradient all-reduce bucket size in MiB, or 'auto' (default: probe RCCL's bus bandwidth over "
+                        "32-256 MiB on the job's process group and take the smallest size within 5%% of the best)")
     g.add_argument("--no-overlap", action="store_true",
                    help="all-reduce after backward instead of overlapping (HIP-graph steps: the post-backward "
                         "'split' schedule)")

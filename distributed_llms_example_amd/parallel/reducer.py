@@ -58,11 +58,13 @@ def wire_dtype_of(name: str | None) -> torch.dtype | None:
 
 
 def choose_bucket_mb(device: torch.device, total_mb: float, group=None, wire_dtype: torch.dtype | None = None,
-                     candidates=BUCKET_MB_CANDIDATES, iters: int = 3, tolerance: float = 0.95) -> dict:
+                     candidates=BUCKET_MB_CANDIDATES, iters: int = 10, tolerance: float = 0.95,
+                     warmup: int = 3) -> dict:
     """Bucket size from an in-run all-reduce probe on the job's own process group (every rank runs it: collective).
 
-    For each candidate size (capped by the gradient buffer) the slowest rank's time of an all-reduce of that many
-    bytes (in the wire dtype) is measured; the bus bandwidth 2(N-1)/N x bytes / time is what RCCL over xGMI delivers
+    For each candidate size (capped by the gradient buffer) the slowest rank's time of ``iters`` all-reduces of that
+    many bytes (in the wire dtype), after ``warmup`` untimed ones (a cold RCCL communicator sets up its channels on the
+    first calls), is measured; the bus bandwidth 2(N-1)/N x bytes / time is what RCCL over xGMI delivers
     at that size.  Chosen: the SMALLEST candidate within ``tolerance`` of the best bandwidth — large enough that the
     per-collective latency is amortised, no larger, so the first bucket launches early in backward and the exposed
     tail (the last bucket, launched when backward ends) stays short.  Returns {"bucket_mb", "busbw_gbps": {...}}."""
@@ -73,7 +75,8 @@ def choose_bucket_mb(device: torch.device, total_mb: float, group=None, wire_dty
     for mb in cands:
         x = torch.ones(max(1, int(mb * 2**20) // 4 * 4 // esz_wire), device=device,
                        dtype=torch.bfloat16 if wire_dtype == torch.bfloat16 else torch.float32)
-        dist.all_reduce(x, group=group)
+        for _ in range(max(1, warmup)):
+            dist.all_reduce(x, group=group)
         if device.type == "cuda":
             torch.cuda.synchronize(device)
         dist.barrier(group=group)
@@ -89,7 +92,7 @@ def choose_bucket_mb(device: torch.device, total_mb: float, group=None, wire_dty
     best = max(table.values())
     pick = min(mb for mb, bw in table.items() if bw >= tolerance * best)
     return {"bucket_mb": pick, "busbw_gbps": {f"{mb:g}": round(bw, 2) for mb, bw in table.items()},
-            "rule": f"smallest within {tolerance:g} of the best bus bandwidth"}
+            "rule": f"smallest within {tolerance:g} of the best bus bandwidth", "iters": iters, "warmup": warmup}
 
 
 class GradReducer:
@@ -435,6 +438,15 @@ class GradReducer:
             out.append(e0.elapsed_time(e1))
         self._events.clear()
         return out
+
+    def describe(self) -> dict:
+        """The communication design this job runs (the entry points log it as their first JSON line): bucket size and
+        how it was chosen, bucket count, overlap, wire dtype, engine."""
+        return {"world_size": self.world, "backend": self.backend, "bucket_mb": self.bucket_mb,
+                "bucket_choice": self.bucket_choice if self.bucket_choice is not None else "fixed",
+                "n_buckets": len(self.buckets), "overlap": self.overlap,
+                "wire_dtype": "bf16" if self.wire_dtype == torch.bfloat16 else str(self.flat.grad_buf.dtype).split(".")[-1],
+                "engine": "native" if self.native is not None else "python"}
 
     def layout_signature(self) -> list[int]:
         """Bucket bounds + segment sizes: must be identical on every rank (RCCL matches collectives by order and

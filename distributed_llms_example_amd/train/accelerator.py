@@ -29,7 +29,7 @@ from ..ops.optim import FusedAdamW
 from ..parallel import collectives
 from ..parallel.env import init_distributed
 from ..parallel.flat import FlatParams
-from ..parallel.reducer import DEFAULT_BUCKET_MB, GradReducer, wire_dtype_of
+from ..parallel.reducer import GradReducer, wire_dtype_of
 from ..parallel.sampler import ShardedBatchSampler
 from .engine import default_grad_dtype
 from .schedule import LRScheduler
@@ -110,7 +110,7 @@ class PreparedOptimizer:
 
 class Accelerator:
     def __init__(self, mixed_precision: str | None = None, gradient_accumulation_steps: int = 1,
-                 bucket_mb: float | str = DEFAULT_BUCKET_MB, overlap_comm: bool = True, cpu: bool = False, seed: int = 0,
+                 bucket_mb: float | str = "auto", overlap_comm: bool = True, cpu: bool = False, seed: int = 0,
                  even_batches: bool = True, grad_reduce_dtype: str | None = None):
         self.env = init_distributed(cpu=cpu if cpu else None)
         self.device = self.env.device

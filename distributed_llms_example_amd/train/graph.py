@@ -376,6 +376,50 @@ class StepRunner:
         self._eager_sigs: set = set()  # signatures the probe sent back to eager steps
         if self.enabled:
             engine.enable_step_seeds()
+        # multi-rank runs: a step that does not finish within DLLM_STEP_TIMEOUT ends the rank with a report of where it
+        # stood (utils/watchdog.py); single-process runs have no partner to wait for
+        self.watchdog = None
+        self.steps = 0
+        if engine.reducer is not None and engine.reducer.dp:
+            from ..utils.watchdog import StepWatchdog
+            wd = StepWatchdog(engine.env.rank, describe=self._where)
+            self.watchdog = wd if wd.enabled else None
+
+    def _where(self) -> dict:
+        red = self.eng.reducer
+        out = {"graph": self.graph is not None, "replays": self.replays, "eager_steps": self.eager_steps}
+        if red is not None:
+            out.update(n_buckets=len(red.buckets), buckets_launched=red._launched_count(),
+                       bucket_bounds=[list(b) for b in red.buckets[:4]] + (["..."] if len(red.buckets) > 4 else []))
+        return out
+
+    def comm_report(self) -> dict:
+        """The communication design this runner's steps use (entry points: first JSON line): the reducer's bucket
+        choice and layout (GradReducer.describe) plus the graph policy and the data-parallel graph schedule."""
+        red = self.eng.reducer
+        rep = red.describe() if red is not None else {"world_size": self.eng.env.world_size, "reducer": None}
+        if red is not None and red.dp:
+            # every rank's bucket layout (RCCL pairs collectives by order and size): they must be identical
+            import hashlib
+            import json as _json
+            import torch.distributed as dist
+            sha = hashlib.sha1(_json.dumps(red.layout_signature()).encode()).hexdigest()[:16]
+            shas = [None] * dist.get_world_size(red.group)
+            dist.all_gather_object(shas, sha, group=red.group)
+            if len(set(shas)) != 1:
+                raise RuntimeError(f"gradient bucket layouts differ across ranks: {shas}")
+            rep.update(bucket_layout_sha=sha, bucket_layouts_agree=True)
+        sched = None
+        if red is not None and self.policy != "off":
+            default = "overlap" if (red.overlap and red.dp) else "split"
+            sched = self.comm or os.environ.get("DLLM_GRAPH_COMM", default)
+            if sched == "overlap" and not (red.overlap and red.dp):
+                sched = "split"
+        rep.update(graph_policy=self.policy, graph_schedule=sched,
+                   eager_schedule=("hook-overlap" if red is not None and red.overlap else "post-backward")
+                   if red is not None else None,
+                   step_timeout_s=self.watchdog.timeout_s if self.watchdog is not None else 0)
+        return rep
 
     def invalidate(self):
         """Something a captured graph baked in changed (e.g. the clip norm): drop the graph; the next steps of the
@@ -388,6 +432,17 @@ class StepRunner:
 
     def __call__(self, passes: list[dict], num_items: torch.Tensor | None = None, lr: float | None = None):
         """Run one step; returns (per-pass mean losses, pre-clip grad norm or None) as device tensors."""
+        wd = self.watchdog
+        if wd is None:
+            return self._step(passes, num_items, lr)
+        self.steps += 1
+        wd.begin(self.steps)
+        try:
+            return self._step(passes, num_items, lr)
+        finally:
+            wd.end(self.eng.env.device)
+
+    def _step(self, passes, num_items, lr):
         eng = self.eng
         if lr is not None:
             eng.optimizer.param_groups[0]["lr"] = lr
@@ -406,7 +461,7 @@ class StepRunner:
                 if probing and len(self._replay_t) >= self.PROBE:
                     self._decide()
                     if self.graph is None:
-                        return self(passes, num_items=num_items)
+                        return self._step(passes, num_items, None)
                     probing = False
                 ev = self._events() if probing else None
                 g.replay(passes, num_items=num_items)
@@ -441,7 +496,7 @@ class StepRunner:
                         get_logger(__name__).warning(f"HIP graph capture failed, eager steps: {self.graph_error}")
                         torch.cuda.synchronize()
                     else:
-                        return self(passes, num_items=num_items)
+                        return self._step(passes, num_items, None)
             # the eager steps of the signature that will be captured are the probe's baseline (not the first one: it
             # carries the lazy initialisation)
             if self.policy == "auto" and self.decision is None and sig == self._sig and self._seen >= 2:

@@ -29,7 +29,6 @@ from ..ops.rng import manual_seed
 from ..parallel import collectives
 from ..parallel.context import shard_sequence
 from ..parallel.env import init_distributed
-from ..parallel.reducer import DEFAULT_BUCKET_MB
 from ..parallel.sampler import ShardedBatchSampler
 from ..utils.logging import get_logger
 from .callbacks import CallbackHandler, DefaultFlowCallback, TrainerControl, TrainerState
@@ -72,7 +71,7 @@ class TrainingArguments:
     dataloader_num_workers: int = 0
     dataloader_drop_last: bool = False
     ddp_find_unused_parameters: bool | None = None
-    ddp_bucket_cap_mb: float | str | None = None  # MiB, or "auto" (parallel/reducer.py choose_bucket_mb)
+    ddp_bucket_cap_mb: float | str | None = "auto"  # MiB, or "auto"/None (parallel/reducer.py choose_bucket_mb)
     ddp_timeout: int = 1800
     overlap_comm: bool = True
     grad_reduce_dtype: str = "fp32"  # "bf16": compress each gradient bucket for the wire (fp32 accumulation kept)
@@ -130,7 +129,7 @@ class Trainer:
         self.engine = TrainEngine(model, self.env, lr=args.learning_rate, weight_decay=args.weight_decay,
                                   betas=(args.adam_beta1, args.adam_beta2), eps=args.adam_epsilon,
                                   max_grad_norm=args.max_grad_norm, dtype=self.dtype,
-                                  bucket_mb=args.ddp_bucket_cap_mb or DEFAULT_BUCKET_MB, overlap=args.overlap_comm,
+                                  bucket_mb=args.ddp_bucket_cap_mb or "auto", overlap=args.overlap_comm,
                                   grad_reduce_dtype=args.grad_reduce_dtype,
                                   no_decay=default_no_decay, label_smoothing=args.label_smoothing_factor)
         self.model = self.engine.model
@@ -280,6 +279,8 @@ class Trainer:
         if runner.enabled and step_seed_start is not None:
             eng.enable_step_seeds(step_seed_start)
         self.step_runner = runner
+        # first JSON line: the communication design of this run (bucket size and how it was chosen, schedules)
+        self.log({"comm": runner.comm_report()})
         self._batch_shape = None
         if cap == -1:
             torch.cuda.synchronize()

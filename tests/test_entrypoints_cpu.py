@@ -144,3 +144,58 @@ def test_train_torchrun_context_parallel_two_ranks(tmp_path):
     final = [x for x in logs if "train_samples_per_second" in x]
     assert final and final[-1]["train_loss"] > 0
     assert (tmp_path / "outputs" / "cp" / "model.safetensors").exists()
+
+
+def _comm_line(stdout):
+    comm = [x["comm"] for x in _json_lines(stdout) if "comm" in x]
+    assert comm, stdout[-2000:]
+    return comm[0]
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("wire", ["fp32", "bf16"])
+def test_train_torchrun_four_ranks_match_one_rank(tmp_path, wire):
+    """train-torchrun on 4 gloo ranks with the default probed bucket size (--bucket-mb auto) equals one rank running the
+    same global batches as gradient-accumulation micro-batches (Trainer batches are dealt round-robin to ranks, the loss
+    is normalised by the global token count): same parameters after 3 steps (dropout off).  The first JSON line reports
+    the probed bucket choice and a bucket layout every rank agrees on."""
+    from safetensors.torch import load_file
+    base = [os.path.join(ROOT, "train-torchrun.py"), "--model-ckpt", "t5-tiny", "--max-steps", "3",
+            "--evaluation-steps", "1000", "--warmup-steps", "1", "--model-overrides", "dropout_rate=0.0,attention_dropout=0.0",
+            "--coalesce-grad-accum", "0", "--grad-reduce-dtype", wire, "--max-eval-samples", "4", *COMMON]
+    env = _env(tmp_path)
+    r1 = subprocess.run([sys.executable] + base + ["--output-dir", "one", "--batch-size", "2", "--grad-accum", "4"],
+                        env=env, capture_output=True, text=True, timeout=300)
+    assert r1.returncode == 0, r1.stderr[-3000:]
+    assert _comm_line(r1.stdout)["world_size"] == 1
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4", "--master-addr",
+           "127.0.0.1", "--master-port", str(_port())] + base + ["--output-dir", "four", "--batch-size", "2",
+                                                                 "--grad-accum", "1"]
+    r4 = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    assert r4.returncode == 0, r4.stderr[-3000:]
+    comm = _comm_line(r4.stdout)
+    assert comm["world_size"] == 4 and comm["bucket_layouts_agree"] is True, comm
+    assert isinstance(comm["bucket_choice"], dict) and comm["bucket_choice"]["iters"] >= 10, comm
+    assert comm["wire_dtype"] == ("bf16" if wire == "bf16" else "float32"), comm
+    a = load_file(str(tmp_path / "outputs" / "one" / "model.safetensors"))
+    b = load_file(str(tmp_path / "outputs" / "four" / "model.safetensors"))
+    assert a.keys() == b.keys()
+    tol = 1e-6 if wire == "fp32" else 2e-5
+    for k in a:
+        torch.testing.assert_close(a[k], b[k], rtol=1e-4, atol=tol, msg=k)
+
+
+@pytest.mark.slow
+def test_train_task_four_local_ranks_probe_and_bf16_wire(tmp_path):
+    """train-task --local-procs 4 (spawned ranks, gloo) with the default probed buckets and the bf16 wire: it trains,
+    evaluates and saves, and its first JSON line reports the probe and an agreed bucket layout."""
+    cmd = [sys.executable, os.path.join(ROOT, "train-task.py"), "--model-ckpt", "t5-tiny", "--output-dir", "task4",
+           "--batch-size", "2", "--local-procs", "4", "--master-port", str(_port()), "--grad-reduce-dtype", "bf16",
+           "--max-eval-samples", "8", *COMMON]
+    r = subprocess.run(cmd, env=_env(tmp_path), capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    comm = _comm_line(r.stdout)
+    assert comm["world_size"] == 4 and comm["bucket_layouts_agree"] is True and comm["wire_dtype"] == "bf16", comm
+    assert isinstance(comm["bucket_choice"], dict) and comm["bucket_choice"]["bucket_mb"] > 0, comm
+    assert any("rouge1" in x for x in _json_lines(r.stdout))
+    assert (tmp_path / "outputs" / "task4" / "model.safetensors").exists()

@@ -40,7 +40,7 @@ class ModelTrainer:
     def __init__(self, args):
         self.args = args
         mp = None if args.precision is None else ("bf16" if args.precision == "bf16" else "no")
-        self.accelerator = Accelerator(mixed_precision=mp, bucket_mb=args.bucket_mb or 128.0,
+        self.accelerator = Accelerator(mixed_precision=mp, bucket_mb=args.bucket_mb or "auto",
                                        overlap_comm=not args.no_overlap, seed=args.seed,
                                        grad_reduce_dtype=args.grad_reduce_dtype)
         self.device = self.accelerator.device
@@ -81,6 +81,7 @@ class ModelTrainer:
         lr_scheduler = get_scheduler("linear", optimizer, num_warmup_steps=1, num_training_steps=max_train_steps)
         metric = rouge.load("rouge")
         train_step = acc.make_train_step(model, optimizer)
+        self.dump({"comm": train_step.runner.comm_report()})  # bucket choice and step schedules of this run
         self.logger.info(f"***** Running training ***** examples={len(train_ds)} epochs={a.num_epochs}")
         completed = 0
         shape = None

@@ -82,7 +82,7 @@ def run(env, args):
     dtype = torch.bfloat16 if (args.precision or ("bf16" if env.device.type == "cuda" else "fp32")) == "bf16" \
         else torch.float32
     eng = TrainEngine(model, env, lr=args.learning_rate, weight_decay=0.0, max_grad_norm=None, dtype=dtype,
-                      bucket_mb=args.bucket_mb or 128.0, overlap=not args.no_overlap, no_decay=None,
+                      bucket_mb=args.bucket_mb or "auto", overlap=not args.no_overlap, no_decay=None,
                       grad_reduce_dtype=args.grad_reduce_dtype)
     collator = DataCollatorForSeq2Seq.for_model(cfg, pad_to_multiple_of=8)
     # partition_dataset (ref/train-task.py:176-191)
@@ -102,6 +102,7 @@ def run(env, args):
     # forward + backward + gradient all-reduce + AdamW, replayed from HIP graphs once the batch shape repeats
     # (train/graph.py StepRunner; eager on CPU, DLLM_GRAPH=0, or for a ragged last batch)
     runner = StepRunner(eng)
+    dump_metrics({"comm": runner.comm_report()}, env.is_main_process)  # bucket choice and step schedules of this run
     completed = 0
     for epoch in range(args.num_epochs):
         eng.train()
