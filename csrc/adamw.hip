@@ -75,7 +75,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(TP* __restrict__ param, floa
 // Bandwidth version (n % 8 == 0, the flat buffers are 64-element aligned): 8 elements per thread and iteration, every
 // load of both halves issued before any math (two 16-B loads in flight per stream).  It moves 31 B per parameter with
 // fp32 gradients and master weights (17 read, 14 written) at ~4.9 TB/s, i.e. HBM-bound; nontemporal access
-// (DLLM_ADAMW_NT=1) measured 1.8x slower (tools/adamw_bench.py, profiles/r2_adamw_bench.jsonl).
+// (non-temporal loads / stores) measured 1.8x slower (tools/adamw_bench.py, profiles/r2_adamw_bench.jsonl).
 template <bool NT, typename T>
 DLLM_DEVICE f32x4 ld4_nt(T* p) {
   if constexpr (!NT) {
@@ -183,20 +183,12 @@ extern "C" int dllm_adamw(void* param, float* master, const void* grad, float* m
   const int G = grid_for(n4, 4096);
   const float step_size = lr / bc1;
   const float inv_sqrt_bc2 = 1.f / sqrtf(bc2);
-  if (n % 8 == 0 && getenv("DLLM_ADAMW_V1") == nullptr) {
+  if (n % 8 == 0) {
     const long n8 = n / 8;
-    const char* ge = getenv("DLLM_ADAMW_GRID");
-    const int G8 = grid_for(n8, ge ? atoi(ge) : 1024);  // tools/adamw_bench.py: ~4.9 TB/s moved (nt: 2.8, slower)
-    const bool nt = getenv("DLLM_ADAMW_NT") != nullptr && getenv("DLLM_ADAMW_NT")[0] == '1';
+    const int G8 = grid_for(n8, 1024);  // tools/adamw_bench.py: ~4.9 TB/s moved (non-temporal stores: 2.8, slower)
 #define A8(TP, TG, MS)                                                                                                  \
-  do {                                                                                                                  \
-    if (nt)                                                                                                             \
-      hipLaunchKernelGGL((adamw8_kernel<TP, TG, MS, true>), dim3(G8), dim3(256), 0, st, (TP*)param, master,             \
-                         (const TG*)grad, m, v, wd_mask, coef, n8, lr, b1, b2, eps, wd, step_size, inv_sqrt_bc2, hyper);       \
-    else                                                                                                                \
-      hipLaunchKernelGGL((adamw8_kernel<TP, TG, MS, false>), dim3(G8), dim3(256), 0, st, (TP*)param, master,            \
-                         (const TG*)grad, m, v, wd_mask, coef, n8, lr, b1, b2, eps, wd, step_size, inv_sqrt_bc2, hyper);       \
-  } while (0)
+  hipLaunchKernelGGL((adamw8_kernel<TP, TG, MS, false>), dim3(G8), dim3(256), 0, st, (TP*)param, master,               \
+                     (const TG*)grad, m, v, wd_mask, coef, n8, lr, b1, b2, eps, wd, step_size, inv_sqrt_bc2, hyper)
     if (is_bf16 && grad_f32) { if (master) A8(uint16_t, float, true); else A8(uint16_t, float, false); }
     else if (is_bf16) { if (master) A8(uint16_t, uint16_t, true); else A8(uint16_t, uint16_t, false); }
     else { if (master) A8(float, float, true); else A8(float, float, false); }

@@ -33,6 +33,7 @@
 // reading the LUT, and dK/dV credits its whole dS sum to the range's end entry instead of shearing diagonals (the
 // LUT gradient is consumed per bucket).  dK/dV -12..20 %, forward -2 % (interleaved A/B, r1_attn_bench_v8_ab).
 #include "common.h"
+#include "route.h"
 #include "attn_params.h"
 #include "attn_tile.h"
 #include <stdlib.h>
@@ -713,252 +714,6 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dq_kernel(AttnParams P) {
   }
 #endif
 }
-
-// ================================================================================== backward: dK, dV
-template <bool HAS_BIAS, bool HAS_KPM, bool CAUSAL, bool DROP>
-__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnParams P) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  uint16_t* QD = reinterpret_cast<uint16_t*>(smem);             // [2 buffers][Q tile | dO tile] (32 rows)
-  float* rowv = reinterpret_cast<float*>(QD + 4 * TILE32);       // [2][3][32]: lse2, delta, rowhash
-  float* kmask = rowv + 2 * 3 * BWD_BQ;                          // [128]
-  uint32_t* mwd = reinterpret_cast<uint32_t*>(kmask + BWD_BK);   // [2][4][32] dropout bit words (see fwd)
-  float* lut_r = reinterpret_cast<float*>(mwd + 2 * 4 * BWD_BQ); // [Sq + 128 + 32] reversed, log2-scaled
-  float* dlut_s = lut_r + (HAS_BIAS ? P.Sq + BWD_BK + BWD_BQ : 0);  // [Sq + 128]
-
-  // w through readfirstlane: wave-uniform to the compiler, so per-wave tile decisions are scalar branches
-  const int tid = threadIdx.x, w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, r = lane & 31,
-            hh = lane >> 5;
-  const int logical = xcd_remap(blockIdx.x, gridDim.x);
-  const int kblk = logical % P.n_tiles;
-  const int bh = logical / P.n_tiles;
-  const int h = bh % P.H, b = bh / P.H;
-  const int k0 = kblk * BWD_BK;
-  const int kw0 = k0 + w * 32;
-  const int key = kw0 + r;
-  const bool kvalid = key < P.Sk;
-  const int L = P.Sq + P.Sk - 1;
-  const int win = P.Sq + BWD_BK;
-  const float sl2 = P.scale * LOG2E;
-
-  if (HAS_BIAS) {
-    // lut_r[t] = LUT[k0 + win - 1 - t] (0 outside): a score's LUT index li = key - q + Sq - 1 - k0 (>= -32 for
-    // the padded rows of a partial last q-tile) lives at t = win - 1 - li = lane base + (row offset in tile)
-    const float* lrow = P.lut + (long)h * L;
-    for (int t = tid; t < win + BWD_BQ; t += 256) {
-      const int i = win - 1 - t, gi = k0 + i;
-      lut_r[t] = (i >= 0 && gi < L) ? lrow[gi] * LOG2E : 0.f;
-    }
-    for (int i = tid; i < win; i += 256) dlut_s[i] = 0.f;
-  }
-  const float c_lo = HAS_BIAS ? P.lut[(long)h * L] * LOG2E : 0.f;  // saturated-range biases (log2-scaled)
-  const float c_hi = HAS_BIAS ? P.lut[(long)h * L + L - 1] * LOG2E : 0.f;
-  float sat_acc_lo = 0.f, sat_acc_hi = 0.f;                          // dS sums of saturated tiles
-  bool key_ok = false;
-  if (tid < BWD_BK) {
-    const int kk = k0 + tid;
-    key_ok = kk < P.Sk;
-    if (HAS_KPM && key_ok) key_ok = P.kpm[(long)b * P.Sk + kk] != 0;
-    kmask[tid] = key_ok ? 0.f : -INFINITY;
-  }
-  // a key block that is entirely padding gets dK = dV = 0 without visiting any query tile
-  const bool block_live = !HAS_KPM || __syncthreads_or(key_ok ? 1 : 0);
-  bf16x8v kf[4], vf[4];
-  {
-    const uint16_t* kp = P.k + b * P.k_sb + (long)key * P.k_ss + h * P.k_sh;
-    const uint16_t* vp = P.v + b * P.v_sb + (long)key * P.v_ss + h * P.v_sh;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      u16x8 a = {0, 0, 0, 0, 0, 0, 0, 0}, c = a;
-      if (kvalid) {
-        a = *reinterpret_cast<const u16x8*>(kp + 16 * s + 8 * hh);
-        c = *reinterpret_cast<const u16x8*>(vp + 16 * s + 8 * hh);
-      }
-      kf[s] = as_frag(a);
-      vf[s] = as_frag(c);
-    }
-  }
-  // this lane's dropout bit: the forward's lane (hh_f) and register (bit) that held (q, key)
-  const int kl = key - k0, kc = kl & 31;
-  const int mcol = (kl >> 6) * 2 + ((kc >> 2) & 1);
-  const int mbit = keep_bit((kl >> 5) & 1, (kc & 3) + 4 * (kc >> 3));
-  const float dscale = DROP ? 1.f / (1.f - P.p_drop) : 1.f;
-  const uint32_t dsbits = __float_as_uint(dscale);
-  int qt_begin = 0;
-  if (CAUSAL) {
-    const int qmin = k0 - P.causal_off;  // first query that can see key k0
-    qt_begin = qmin > 0 ? qmin / BWD_BQ : 0;
-  }
-  const int nqt = block_live ? (P.Sq + BWD_BQ - 1) / BWD_BQ : qt_begin;
-  const long bh_rows = (long)(b * P.H + h) * P.Sq;
-  const float* lse_row = P.lse + bh_rows;
-  const float* del_row = P.delta + bh_rows;
-
-  const int srow = tid >> 3, sch = tid & 7;  // 32 rows x 8 chunks
-  u16x8 qr, dr;
-  float lr = 0.f, dl = 0.f;
-  uint32_t mwr = 0;
-  auto load_tile = [&](int qt) {
-    const int qg = qt * BWD_BQ + srow;
-    u16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
-    qr = z;
-    dr = z;
-    if (qg < P.Sq) {
-      qr = *reinterpret_cast<const u16x8*>(P.q + b * P.q_sb + (long)qg * P.q_ss + h * P.q_sh + sch * 8);
-      dr = *reinterpret_cast<const u16x8*>(P.dout + b * P.do_sb + (long)qg * P.do_ss + h * P.do_sh + sch * 8);
-    }
-    if (tid < BWD_BQ) {
-      const int q2 = qt * BWD_BQ + tid;
-      lr = q2 < P.Sq ? lse_row[q2] : INFINITY;
-      dl = q2 < P.Sq ? del_row[q2] : 0.f;
-    }
-    if (DROP && tid < 4 * BWD_BQ) {  // words of the 2 forward key tiles x 2 lane halves this key block spans
-      const int col = tid >> 5, q2 = qt * BWD_BQ + (tid & 31);
-      const int ktf = (k0 >> 6) + (col >> 1);
-      mwr = (q2 < P.Sq && ktf < P.n_ktiles)
-                ? P.dmask[(((long)bh * P.n_ktiles + ktf) * 2 + (col & 1)) * P.sq_pad + q2] : 0u;
-    }
-  };
-  auto store_tile = [&](int buf) {
-    uint16_t* Qb = QD + buf * 2 * TILE32;
-    st_row(Qb, srow, sch, qr);
-    st_row(Qb + TILE32, srow, sch, dr);
-    if (tid < BWD_BQ) {
-      float* rv = rowv + buf * 3 * BWD_BQ;
-      rv[tid] = lr;
-      rv[BWD_BQ + tid] = dl;
-    }
-    if (DROP && tid < 4 * BWD_BQ) mwd[buf * 4 * BWD_BQ + tid] = mwr;
-  };
-
-  f32x16 dv0 = {}, dv1 = {}, dk0 = {}, dk1 = {};
-  if (qt_begin < nqt) {
-    load_tile(qt_begin);
-    store_tile(0);
-  }
-  __syncthreads();
-  const float km = kmask[w * 32 + r];  // 0 or -inf for this lane's key column
-  for (int qt = qt_begin; qt < nqt; ++qt) {
-    const int cur = (qt - qt_begin) & 1;
-    const int q0 = qt * BWD_BQ;
-    if (qt + 1 < nqt) load_tile(qt + 1);
-    const uint16_t* Qb = QD + cur * 2 * TILE32;
-    const uint16_t* dOb = Qb + TILE32;
-    const float* rv = rowv + cur * 3 * BWD_BQ;
-
-    f32x16 sacc = {}, dpacc = {};
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      sacc = mfma32(as_frag(ld_row(Qb, r, 2 * s + hh)), kf[s], sacc);
-      dpacc = mfma32(as_frag(ld_row(dOb, r, 2 * s + hh)), vf[s], dpacc);
-    }
-    const bool tile_causal = CAUSAL && (kw0 + 31 > q0 + P.causal_off);
-    // row i of the tile sits at t = lbase + crow(i, 0): immediate ds_read offsets, no per-score index math
-    const float* lrow_t = lut_r + (win - 1 - (key - q0 - 4 * hh + P.Sq - 1 - k0));
-    uint32_t mw[16];
-    if (DROP) {
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const u32x4 v = *reinterpret_cast<const u32x4*>(mwd + cur * 4 * BWD_BQ + mcol * BWD_BQ + 8 * g + 4 * hh);
-        mw[4 * g] = v.x;
-        mw[4 * g + 1] = v.y;
-        mw[4 * g + 2] = v.z;
-        mw[4 * g + 3] = v.w;
-      }
-    }
-    // saturated tile (LUT indices kw0 - q0 - 31 + Sq - 1 .. kw0 + 31 - q0 + Sq - 1 in one constant range): scalar
-    // bias, and the dS sum is credited to the range's end entry instead of the per-diagonal shear
-    const int sat = !HAS_BIAS ? 0
-                    : (kw0 + 31 - q0 + P.Sq - 1 <= P.sat_lo ? 1 : (kw0 - q0 - 31 + P.Sq - 1 >= P.sat_hi ? 2 : 0));
-    f32x16 pd, ds;
-    auto probs = [&](auto use_lut, float cbias) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int ql = crow(i, hh);
-        const int qg = q0 + ql;
-        float sv = sacc[i] * sl2 + km;
-        if constexpr (decltype(use_lut)::value) sv += lrow_t[crow(i, 0)];
-        else if (HAS_BIAS) sv += cbias;
-        if (tile_causal && key > qg + P.causal_off) sv = -INFINITY;
-        const float pr = fast_exp2(sv - rv[ql]);  // lse = +inf for q >= Sq -> 0
-        float keepf = 1.f;
-        if (DROP) keepf = __uint_as_float((uint32_t)__builtin_amdgcn_sbfe((int)mw[i], mbit, 1) & dsbits);
-        pd[i] = pr * keepf;
-        ds[i] = pr * (dpacc[i] * keepf - rv[BWD_BQ + ql]);
-      }
-    };
-    if (HAS_BIAS && sat == 0) probs(std::true_type{}, 0.f);
-    else probs(std::false_type{}, sat == 1 ? c_lo : c_hi);
-    if (HAS_BIAS && sat != 0) {
-      float t = 0.f;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) t += ds[i];
-      if (sat == 1) sat_acc_lo += t;
-      else sat_acc_hi += t;
-    } else if (HAS_BIAS) {
-      // diagonal sums of the wave's 32x32 dS tile: rotate register i (row rho = crow(i, hh)) left by rho
-      // lanes so lane r receives element (rho, (r + rho) & 31) whose diagonal (col - row) is r or r - 32
-      float pos = 0.f, neg = 0.f;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int rho = crow(i, hh);
-        const float v = __shfl(ds[i], ((r + rho) & 31) + 32 * hh, 64);
-        if (r + rho < 32) pos += v; else neg += v;
-      }
-      pos += __shfl_xor(pos, 32, 64);
-      neg += __shfl_xor(neg, 32, 64);
-      if (hh == 0) {
-        const int li = w * 32 + r - q0 + P.Sq - 1;
-        atomicAdd(&dlut_s[li], pos);
-        if (li >= 32) atomicAdd(&dlut_s[li - 32], neg);
-      }
-    }
-    const bf16x8v pf0 = pack8(pd, 0), pf1 = pack8(pd, 8), sf0 = pack8(ds, 0), sf1 = pack8(ds, 8);
-#pragma unroll
-    for (int sp = 0; sp < 2; ++sp) {
-      const int c0 = 16 * sp + 4 * hh;
-      const bf16x8v pfv = sp == 0 ? pf0 : pf1, sfv = sp == 0 ? sf0 : sf1;
-      dv0 = mfma32(ld_tr_operand(dOb, c0, 0, r), pfv, dv0);
-      dv1 = mfma32(ld_tr_operand(dOb, c0, 1, r), pfv, dv1);
-      dk0 = mfma32(ld_tr_operand(Qb, c0, 0, r), sfv, dk0);
-      dk1 = mfma32(ld_tr_operand(Qb, c0, 1, r), sfv, dk1);
-    }
-    if (qt + 1 < nqt) store_tile(cur ^ 1);
-    __syncthreads();
-  }
-
-  if (kvalid) {
-    uint16_t* dkp = P.dk + b * P.dk_sb + (long)key * P.dk_ss + h * P.dk_sh;
-    uint16_t* dvp = P.dv + b * P.dv_sb + (long)key * P.dv_ss + h * P.dv_sh;
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const f32x16& ak = t == 0 ? dk0 : dk1;
-      const f32x16& av = t == 0 ? dv0 : dv1;
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        u16x4 pk = {f2bf(ak[4 * g] * P.scale), f2bf(ak[4 * g + 1] * P.scale), f2bf(ak[4 * g + 2] * P.scale),
-                    f2bf(ak[4 * g + 3] * P.scale)};
-        u16x4 pv = {f2bf(av[4 * g]), f2bf(av[4 * g + 1]), f2bf(av[4 * g + 2]), f2bf(av[4 * g + 3])};
-        *reinterpret_cast<u16x4*>(dkp + 32 * t + 8 * g + 4 * hh) = pk;
-        *reinterpret_cast<u16x4*>(dvp + 32 * t + 8 * g + 4 * hh) = pv;
-      }
-    }
-  }
-  if (HAS_BIAS) {
-    __syncthreads();
-    float* grow = P.dlut + (long)h * L;
-    for (int i = tid; i < win; i += 256) {
-      const int gi = k0 + i;
-      const float v = dlut_s[i];
-      if (gi < L && v != 0.f) atomicAdd(grow + gi, v);
-    }
-    const float a_lo = wave_sum(sat_acc_lo), a_hi = wave_sum(sat_acc_hi);
-    if (lane == 0) {
-      if (a_lo != 0.f) atomicAdd(grow, a_lo);
-      if (a_hi != 0.f) atomicAdd(grow + L - 1, a_hi);
-    }
-  }
-}
-
 
 // ================================================================================== backward: dK, dV (v2)
 // Key blocks of 128 (4 waves x 32 keys, key on the lane as in v1), query tiles of 64 rows per pipeline stage: the
@@ -1646,11 +1401,8 @@ template <bool HB, bool HK, bool CA, bool DR>
 void launch_fwd_t(const AttnParams& p, int nblk, size_t lds, hipStream_t st) {
   // lds was sized for the 3-deep ring; the 2-deep one drops one K/V buffer pair and one keep-bit slot
   const size_t lds2 = lds - (size_t)2 * TILE64 * 2 - 256 * 4;
-  static const int occ = [] {
-    const char* e = getenv("DLLM_ATTN_FWD_OCC");
-    return e != nullptr ? atoi(e) : 3;  // 3: t5-base encoder forward -10 % (profiles/r2_attn_fwd_occ3.txt)
-  }();
-  if (occ == 3 && 3 * lds2 <= 160 * 1024) {
+  // 3 workgroups per CU on the 2-deep ring: t5-base encoder forward -10 % (profiles/r2_attn_fwd_occ3.txt)
+  if (3 * lds2 <= 160 * 1024) {
     if (DR && p.dmask_ready)
       hipLaunchKernelGGL((attn_fwd_kernel<HB, HK, CA, DR, true, 2>), dim3(nblk), dim3(256), lds2, st, p);
     else
@@ -1664,42 +1416,23 @@ void launch_fwd_t(const AttnParams& p, int nblk, size_t lds, hipStream_t st) {
 }
 template <bool HB, bool HK, bool CA, bool DR>
 void launch_bwd_dq_t(const AttnParams& p, int nblk, size_t lds, hipStream_t st) {
-  static const int occ = [] {
-    const char* e = getenv("DLLM_ATTN_DQ_OCC");
-    return e != nullptr ? atoi(e) : 2;  // 3 measured equal (profiles/r2_ab_attn_dq_halves.txt)
-  }();
+  // 2 workgroups per CU (3 measured equal, profiles/r2_ab_attn_dq_halves.txt and r5_dq_occ_rounds_ab.txt)
   if constexpr (!HB) {
     if (p.csq != nullptr) {  // column sums for the q-projection bias (BART)
       hipLaunchKernelGGL((attn_bwd_dq_kernel<HB, HK, CA, DR, 2, true>), dim3(nblk), dim3(256), lds, st, p);
       return;
     }
   }
-  if (occ == 3 && !CA && 3 * lds <= 160 * 1024)  // the causal variant spills at 168 VGPRs
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<HB, HK, CA, DR, 3>), dim3(nblk), dim3(256), lds, st, p);
-  else
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<HB, HK, CA, DR, 2>), dim3(nblk), dim3(256), lds, st, p);
-}
-template <bool HB, bool HK, bool CA, bool DR>
-void launch_bwd_dkdv_t(const AttnParams& p, int nblk, size_t lds, hipStream_t st) {
-  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<HB, HK, CA, DR>), dim3(nblk), dim3(256), lds, st, p);
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<HB, HK, CA, DR, 2>), dim3(nblk), dim3(256), lds, st, p);
 }
 template <bool HB, bool HK, bool CA, bool DR>
 void launch_bwd_dkdv2_t(const AttnParams& p, int nblk, size_t lds, hipStream_t st) {
-  static const int occ = [] {
-    const char* e = getenv("DLLM_ATTN_DKDV_OCC");
-    return e != nullptr ? atoi(e) : 3;
-  }();
   const size_t lds2 = lds - K2_STAGE;  // lds was sized for the 3-deep ring
-  static const int occ_dr = [] {
-    const char* e = getenv("DLLM_ATTN_DKDV_OCC_DR");
-    return e != nullptr ? atoi(e) : 1;
-  }();
   // bias- and dropout-free variants: they fit 168 VGPRs without spills (BART-large shapes: bwd -4..6 %, bench
   // +0.8 %, profiles/r2_attn_dkdv_occ3.txt).  The dropout variant spills (7 VGPRs bias-free) and measured 2 % slower on
   // self-attention, but short-query (Sq <= 256) bias-free calls — T5 cross-attention, two 64-row stages per key block,
   // prologue-latency bound — gain from the third workgroup: step -0.5 % (profiles/r3_cross_dkdv_occ3_ab.txt);
-  // DLLM_ATTN_DKDV_OCC_DR=0 turns that off
-  if (occ == 3 && !HB && (!DR || (occ_dr == 1 && p.Sq <= 256)) && 3 * lds2 <= 160 * 1024) {
+  if (!HB && (!DR || p.Sq <= 256) && 3 * lds2 <= 160 * 1024) {
     if constexpr (!HB) {
       if (p.csk != nullptr) {  // column sums for the k / v projection biases (BART)
         hipLaunchKernelGGL((attn_bwd_dkdv2_kernel<HB, HK, CA, DR, 2, true>), dim3(nblk), dim3(256), lds2, st, p);
@@ -1804,23 +1537,19 @@ extern "C" int dllm_attn_bwd(AttnParams* pp, hipStream_t st) {
   p.n_tiles = (p.Sk + BWD_BK - 1) / BWD_BK;
   nblk = (long)p.n_tiles * p.H * p.B;
   // short-query cross-attention (Sq <= 128, no bias, not causal): one workgroup walks MB key blocks with the query
-  // side resident (attn_bwd_dkdv_sq_kernel) — the largest MB in {8, 4, 2} (capped by DLLM_ATTN_DKDV_SQ_MB, default 4;
-  // 0 / 1 = off) that still launches 6 workgroups per CU (3 rounds at 2 per CU); smaller launches keep one workgroup
-  // per key block (dkdv2).  Batch sweep at the T5 cross shape: dkdv2 wins at batch 8 / 16, MB 2 at 32, MB 4 from 64.
-  // In the t5-base b=512 step: 15.34 -> 13.50 ms/step (MB 8: 14.10), profiles/r4_dkdv_sq_ab.txt
-  static const int sq_cap = [] {
-    const char* e = getenv("DLLM_ATTN_DKDV_SQ_MB");
-    return e != nullptr ? atoi(e) : 4;
-  }();
+  // side resident (attn_bwd_dkdv_sq_kernel) — the largest MB in {4, 2} that still launches 6 workgroups per CU (3
+  // rounds at 2 per CU); smaller launches keep one workgroup per key block (dkdv2).  Batch sweep at the T5 cross
+  // shape: dkdv2 wins at batch 8 / 16, MB 2 at 32, MB 4 from 64.  In the t5-base b=512 step: 15.34 -> 13.50 ms/step
+  // (MB 8: 14.10), profiles/r4_dkdv_sq_ab.txt
+  constexpr int sq_cap = 4;
   static const int cus = [] {
     int dev = 0, n = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
     return n > 0 ? n : 256;
   }();
-  // DLLM_ATTN_DKDV_SQ_FORCE=1 (read per call; tests): the largest allowed MB whatever the launch size
-  const char* force_e = getenv("DLLM_ATTN_DKDV_SQ_FORCE");
-  const bool force = force_e != nullptr && force_e[0] == '1';
+  // DLLM_ROUTE attn_dkdv_sq_force=1 (read per call; tests): the largest allowed MB whatever the launch size
+  const bool force = route_int("attn_dkdv_sq_force", 0) == 1;
   int mb = 0;
   for (int m = 8; m >= 2; m /= 2)
     if (m <= sq_cap && mb == 0 && (force || (long)((p.n_tiles + m - 1) / m) * p.H * p.B >= 6L * cus)) mb = m;
@@ -1837,20 +1566,14 @@ extern "C" int dllm_attn_bwd(AttnParams* pp, hipStream_t st) {
     DLLM_CHECK_LAUNCH();
     return 0;
   }
-  if (p.rowrec != nullptr) {  // v2: 64-row stages through an LDS-DMA ring (per-row terms from the dQ kernel)
-    lds = (size_t)K2_NBUF * K2_STAGE + BWD_BK * 4;
-    if (p.lut) lds += (size_t)(2 * (p.Sq + BWD_BK) + K2_QT) * 4;
-    if (nblk <= 0 || nblk > 0x7fffffff || lds > 160 * 1024) return -4;
-    DISPATCH4(launch_bwd_dkdv2_t, p.lut != nullptr, p.kpm != nullptr, p.causal != 0, p.p_drop > 0.f, p, (int)nblk,
-              lds, st);
-    DLLM_CHECK_LAUNCH();
-    return 0;
-  }
-  lds = (size_t)4 * TILE32 * 2 + (size_t)2 * 3 * BWD_BQ * 4 + BWD_BK * 4 + (size_t)2 * 4 * BWD_BQ * 4;
-  if (p.lut) lds += (size_t)(2 * (p.Sq + BWD_BK) + BWD_BQ) * 4;
+  // v2: 64-row stages through an LDS-DMA ring (per-row terms from the dQ kernel).  Round 6 deleted the v1 kernel
+  // (32-row register-staged stages), reachable only through an A/B switch since round 2.
+  if (p.rowrec == nullptr) return -5;
+  lds = (size_t)K2_NBUF * K2_STAGE + BWD_BK * 4;
+  if (p.lut) lds += (size_t)(2 * (p.Sq + BWD_BK) + K2_QT) * 4;
   if (nblk <= 0 || nblk > 0x7fffffff || lds > 160 * 1024) return -4;
-  DISPATCH4(launch_bwd_dkdv_t, p.lut != nullptr, p.kpm != nullptr, p.causal != 0, p.p_drop > 0.f, p, (int)nblk, lds,
-            st);
+  DISPATCH4(launch_bwd_dkdv2_t, p.lut != nullptr, p.kpm != nullptr, p.causal != 0, p.p_drop > 0.f, p, (int)nblk,
+            lds, st);
   DLLM_CHECK_LAUNCH();
   return 0;
 }

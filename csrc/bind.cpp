@@ -13,6 +13,7 @@
 #include "attn_f32_params.h"
 #include "attn_params.h"
 #include "gemm_params.h"
+#include "route.h"
 
 extern "C" {
 int dllm_norm_fwd(const void*, const void*, const void*, const void*, void*, void*, float*, float*, int, int, float,
@@ -41,7 +42,6 @@ int dllm_attn_dropout_mask(AttnParams*, hipStream_t);
 int dllm_attn_f32_fwd(AttnF32Params*, hipStream_t);
 int dllm_attn_f32_bwd(AttnF32Params*, hipStream_t);
 int dllm_set_seed_step_attn_f32(const uint32_t*);
-int dllm_gemm_wgrad(const GemmWgradParams*, int, hipStream_t);
 int dllm_wgrad_reduce(const GemmWgradParams*, hipStream_t);
 int dllm_gemm_fused(const GemmFusedParams*, int, int, hipStream_t);
 int dllm_gemm_w4(const GemmW4Params*, int, int, int, hipStream_t);
@@ -586,11 +586,9 @@ std::vector<Tensor> attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& 
   Tensor dk = pick(dk_out, P.Sk, "dk_out");
   Tensor dv = pick(dv_out, P.Sk, "dv_out");
   auto delta = at::empty({P.B, P.H, P.Sq}, f32);
-  // per-row terms the dQ kernel hands to the v2 dK/dV kernel ([B*H][sq_pad/64][4][64]); DLLM_ATTN_DKDV=1: v1 kernel
-  static const bool dkdv_v1 = [] { const char* e = std::getenv("DLLM_ATTN_DKDV"); return e && e[0] == '1'; }();
-  Tensor rowrec;
-  if (!dkdv_v1) rowrec = at::empty({(int64_t)P.B * P.H * ((P.Sq + 127) / 128 * 128) * 4}, f32);
-  P.rowrec = rowrec.defined() ? rowrec.data_ptr<float>() : nullptr;
+  // per-row terms the dQ kernel hands to the dK/dV kernel ([B*H][sq_pad/64][4][64])
+  Tensor rowrec = at::empty({(int64_t)P.B * P.H * ((P.Sq + 127) / 128 * 128) * 4}, f32);
+  P.rowrec = rowrec.data_ptr<float>();
   Tensor dlut;
   if (P.lut != nullptr) dlut = at::zeros({P.H, P.Sq + P.Sk - 1}, f32);
   P.o = reinterpret_cast<const uint16_t*>(o.data_ptr());
@@ -656,8 +654,6 @@ int wgrad_splits(int T, int K) {
     const int n = at::cuda::getCurrentDeviceProperties()->multiProcessorCount;
     return n > 0 ? n : 256;
   }();
-  static const bool legacy = std::getenv("DLLM_WGRAD_SPLIT_LEGACY") != nullptr;  // A/B: fill the CUs once
-  if (legacy) return std::max(1, cus / T);
   const int smax = std::max(1, std::min(K / 256, 64));
   int best = 1;
   double bestc = 1e30;
@@ -672,13 +668,14 @@ int wgrad_splits(int T, int K) {
   return best;
 }
 
-constexpr int64_t kWgradW4 = 12;  // gemm_wgrad variant: csrc/gemm_w4.hip's weight-gradient mode
+constexpr int64_t kWgradW4 = 12;  // the only gemm_wgrad variant: csrc/gemm_w4.hip's weight-gradient mode
 
 int64_t gemm_wgrad(const Tensor& a, const Tensor& b, Tensor& c, bool beta, int64_t variant, int64_t splits_req) {
   TORCH_CHECK(gemm_wgrad_supported(a, b, c),
               "gemm_wgrad: need bf16 GPU [K,M] x [K,N] -> bf16/fp32 [M,N], unit inner stride, 16-B aligned rows, K % 64 == 0, "
               "M % 8 == 0, N a multiple of 256");
   TORCH_CHECK(a.device() == b.device() && a.device() == c.device(), "gemm_wgrad: device mismatch");
+  TORCH_CHECK(variant < 0 || variant == kWgradW4, "gemm_wgrad: variant must be -1 (the w4 weight-gradient mode)");
   const int K = a.size(0), M = a.size(1), N = b.size(1);
   GemmWgradParams P{};
   P.A = reinterpret_cast<const uint16_t*>(a.data_ptr());
@@ -697,19 +694,14 @@ int64_t gemm_wgrad(const Tensor& a, const Tensor& b, Tensor& c, bool beta, int64
   int splits = splits_req > 0 ? (int)splits_req : wgrad_splits(P.ntiles, K);
   splits = std::max(1, std::min(splits, K / 256));
   int kchunk = ((K + splits - 1) / splits + 63) / 64 * 64;
-  // default (variant < 0): the w4 weight-gradient mode — +1.2 % t5-base b=512, +1.5 % bart-large b=256 steps, equal at
-  // b=8 (profiles/r5_wgrad_w4_ab.txt); kernel-level 2-8 % faster than variant 9 on every T5 / BART shape
-  if (variant < 0) variant = kWgradW4;
-  if (variant == kWgradW4) {
-    // the w4 kernel addresses a split's k-rows through one 32-bit buffer-descriptor range: more splits when a wide
-    // operand (e.g. the decoder's stacked cross-attention K/V gradient, 24576 columns) would overflow it
-    const long ld = std::max(P.lda, P.ldb), wd = std::max(M, N);
-    while (kchunk > 64 && ((long)(kchunk - 1) * ld + wd) * 2 >= 0xFFFFFFFFL) {
-      ++splits;
-      kchunk = ((K + splits - 1) / splits + 63) / 64 * 64;
-    }
-    if (((long)(kchunk - 1) * ld + wd) * 2 >= 0xFFFFFFFFL) variant = 9;  // even 64-row splits overflow: csrc/gemm.hip
+  // the w4 kernel addresses a split's k-rows through one 32-bit buffer-descriptor range: more splits when a wide
+  // operand (e.g. the decoder's stacked cross-attention K/V gradient, 24576 columns) would overflow it
+  const long ld = std::max(P.lda, P.ldb), wd = std::max(M, N);
+  while (kchunk > 64 && ((long)(kchunk - 1) * ld + wd) * 2 >= 0xFFFFFFFFL) {
+    ++splits;
+    kchunk = ((K + splits - 1) / splits + 63) / 64 * 64;
   }
+  TORCH_CHECK(((long)(kchunk - 1) * ld + wd) * 2 < 0xFFFFFFFFL, "gemm_wgrad: operand rows too long for 64-row splits");
   splits = (K + kchunk - 1) / kchunk;
   P.kchunk = kchunk;
   P.splits = splits;
@@ -718,7 +710,7 @@ int64_t gemm_wgrad(const Tensor& a, const Tensor& b, Tensor& c, bool beta, int64
     ws = at::empty({(int64_t)splits * M * N}, a.options().dtype(at::kFloat));
     P.ws = ws.data_ptr<float>();
   }
-  if (variant == kWgradW4) {
+  {
     // csrc/gemm_w4.hip weight-gradient mode: one wave per SIMD, both operands k-major, fp32 split slabs
     GemmW4Params Q{};
     Q.A = P.A;
@@ -740,9 +732,7 @@ int64_t gemm_wgrad(const Tensor& a, const Tensor& b, Tensor& c, bool beta, int64
     Q.beta = P.beta;
     check_rc(dllm_gemm_w4(&Q, 1, 0, 10, stream()), "gemm_wgrad (w4)");
     if (splits > 1) check_rc(dllm_wgrad_reduce(&P, stream()), "gemm_wgrad (w4) split-K reduce");
-    return splits;
   }
-  check_rc(dllm_gemm_wgrad(&P, (int)variant, stream()), "gemm_wgrad");
   return splits;
 }
 
@@ -896,11 +886,10 @@ Tensor gemm_fused(const Tensor& a, const Tensor& b, bool b_kmajor, int64_t epi, 
     P.thr = t >= 65535.0 ? 0xFFFFu : (uint32_t)t;
   }
   {  // tile-order group size of the ping-pong kernel (read per call so microbenchmarks can A/B it in one process)
-    const char* e = std::getenv("DLLM_GEMM_GRP");
-    P.grp = e ? std::max(0, std::atoi(e)) : 4;  // 4: +1-3 % over row-major (profiles/r1_gemm_experiments.md)
+    P.grp = std::max(0, dllm::route_int("gemm_grp", 4));  // 4: +1-3 % over row-major (profiles/r1_gemm_experiments.md)
   }
   const int v = variant >= 0 ? (int)variant : (int)gemm_fused_variant(K);
-  TORCH_CHECK(v >= 0 && v <= 9, "gemm_fused: bad variant ", v);
+  TORCH_CHECK(v == 1 || v == 8 || v == 9, "gemm_fused: variant must be 1, 8 or 9, got ", v);
   // ReLU derivative bit mask (ping-pong kernel only): epi 1 writes it when given, epi 7 (d-relu) reads it instead of aux
   const bool has_mask = mask.has_value() && mask->defined();
   TORCH_CHECK(epi != 7 || has_mask, "gemm_fused: epilogue 7 needs the ReLU mask");
@@ -1181,8 +1170,7 @@ static GemmFusedParams geglu_params(const Tensor& a, const Tensor& b, bool b_kma
   P.tn = (int)(N / 256);
   P.epi = epi;
   P.scale = 1.f;
-  const char* e = std::getenv("DLLM_GEMM_GRP");
-  P.grp = e ? std::max(0, std::atoi(e)) : 4;
+  P.grp = std::max(0, dllm::route_int("gemm_grp", 4));
   return P;
 }
 

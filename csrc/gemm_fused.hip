@@ -1025,20 +1025,10 @@ int launch_pp(const GemmFusedParams& p, bool persist, hipStream_t st) {
   const size_t lds = (size_t)2 * 2 * 64 * 256 * 2 + (EPI == EPI_DRELU_M ? 2 * 8192 : 0) + (staged ? 8 * 4096 : 0);
   const int T = p.tm * p.tn, cus = num_cus() / 8 * 8;
   // the gated forward is store-only too; its backward (two aux loads per accumulator block) measured 6-10 % faster
-  // persistent as well (profiles/r2_geglu_bench.jsonl); DLLM_GEGLU_BWD_PERSIST=0 keeps one tile per workgroup
-  static const bool dgeglu_persist = [] {
-    const char* e = std::getenv("DLLM_GEGLU_BWD_PERSIST");
-    return !(e && e[0] == '0');
-  }();
-  // the GELU forward (two stores, no loads) is persistent too: +0.9 % on the bart-large b=256 step in round 4
-  // (profiles/r4_gelu_persist_ab.txt); DLLM_PP_PERSIST_GELU=0 turns it off
-  static const bool gelu_persist = [] {
-    const char* e = std::getenv("DLLM_PP_PERSIST_GELU");
-    return !(e && e[0] == '0');
-  }();
+  // persistent as well (profiles/r2_geglu_bench.jsonl); the GELU forward (two stores, no loads) is persistent too:
+  // +0.9 % on the bart-large b=256 step in round 4 (profiles/r4_gelu_persist_ab.txt)
   const bool light = EPI == EPI_NONE || EPI == EPI_RELU || EPI == EPI_DRELU_M || EPI == EPI_GEGLU ||
-                     (EPI == EPI_DGEGLU && dgeglu_persist) ||
-                     ((EPI == EPI_GELU || EPI == EPI_GELU_TANH) && gelu_persist);
+                     EPI == EPI_DGEGLU || EPI == EPI_GELU || EPI == EPI_GELU_TANH;
   if (light && persist && cus >= 8 && T >= 2 * cus && p.K >= 128) {
     static bool attr = false;
     if (!attr) {
@@ -1078,15 +1068,9 @@ template <bool BKM, int EPI>
 int launch_v(const GemmFusedParams& p, int variant, hipStream_t st) {
   switch (variant) {
     case 1: return launch<32, 4, BKM, EPI, 32>(p, st);
-    case 2: return launch<32, 3, BKM, EPI, 32>(p, st);
-    case 3: return launch<64, 2, BKM, EPI, 16>(p, st);
-    case 4: return launch<64, 2, BKM, EPI, 16, true>(p, st);
-    case 5: return launch<32, 3, BKM, EPI, 16>(p, st);
-    case 6: return launch<32, 4, BKM, EPI, 16>(p, st);
-    case 7: return launch<32, 5, BKM, EPI, 16>(p, st);
     case 8: return launch_pp<EPI, BKM>(p, false, st);
     case 9: return launch_pp<EPI, BKM>(p, true, st);
-    default: return launch<64, 2, BKM, EPI, 32>(p, st);
+    default: return -6;
   }
 }
 
@@ -1112,13 +1096,13 @@ int dispatch_epi(const GemmFusedParams& p, int variant, hipStream_t st) {
 
 }  // namespace
 
-// variant: 0 = BK64 x 2 stages, 1 = BK32 x 4 stages, 2 = BK32 x 3 stages (all 128 / 96 KB LDS, 32x32x16 MFMA),
-// 3 = BK64 x 2 stages with 16x16x32 MFMA, 4 = variant 3 with both k-steps' fragments read up front,
-// 5 / 6 / 7 = BK32 x 3 / 4 / 5 stages with 16x16x32 MFMA (96 / 128 / 160 KB: 1-3 stages in flight behind the one
-// being read), 8 = ping-pong kernel gemm_pp_kernel, 9 = its persistent form
+// variant: 1 = the staged kernel, BK32 x 4 stages, 32x32x16 MFMA (reduction lengths K % 64 != 0), 8 = ping-pong kernel
+// gemm_pp_kernel, 9 = its persistent form (the default for K % 64 == 0).  Variants 0 and 2-7 (other BK / stage / MFMA
+// shapes of the staged kernel, all slower than the ping-pong kernel on every T5 / BART shape,
+// profiles/r1_gemm_experiments.md) were deleted in round 6.
 extern "C" int dllm_gemm_fused(const GemmFusedParams* pp, int b_kmajor, int variant, hipStream_t st) {
   const GemmFusedParams& p = *pp;
-  const int bk = (variant == 0 || variant == 3 || variant == 4 || variant >= 8) ? 64 : 32;
+  const int bk = variant >= 8 ? 64 : 32;
   if (p.M % BM || p.N % BN || p.K <= 0 || p.K % bk || p.tm * BM != p.M || p.tn * BN != p.N) return -4;
   return b_kmajor ? dispatch_epi<true>(p, variant, st) : dispatch_epi<false>(p, variant, st);
 }

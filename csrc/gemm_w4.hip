@@ -101,6 +101,13 @@ DLLM_DEVICE i32x4 srd_advance(const i32x4& s, uint32_t bytes) {
   return r;
 }
 
+// which of a chunk's n DMAs rides on its MFMA j (DMA k on MFMA 1 + 7 k / n), or -1
+constexpr int dma_slot(int j, int n) {
+  for (int k = 0; k < n; ++k)
+    if (1 + 7 * k / n == j) return k;
+  return -1;
+}
+
 template <int B, int E, typename F>
 DLLM_DEVICE void sfor(F&& f) {
   if constexpr (B < E) {
@@ -147,12 +154,29 @@ DLLM_DEVICE void mfma(f32x4& c, const bf16x8v& b, const bf16x8v& a) {
 DLLM_DEVICE void mfma0(f32x4& c, const bf16x8v& b, const bf16x8v& a) {
   asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(c) : "v"(b), "v"(a));
 }
+// c += b . a^T with an LDS-DMA riding on it: M0 is formed BEFORE the MFMA, which covers the M0 -> LDS-DMA wait state
+// (no s_nop), and the DMA issues right behind it.  One wave per SIMD pays each DMA's issue in MFMA-pipe cycles
+// (tools/mfma_dma_probe.hip, profiles/r6_mfma_dma_probe3.txt: ~28 cycles per 1-KB DMA beside 16x16x32 MFMAs, -6 with
+// M0 formed early, more when DMAs issue back to back), so the kernel spreads its DMAs one per few MFMAs this way.
+template <uint32_t IMM>
+DLLM_DEVICE void mfma_dma(f32x4& c, const bf16x8v& b, const bf16x8v& a, const i32x4& srd, uint32_t voff, uint32_t soff,
+                          uint32_t ldsb) {
+  asm volatile("s_add_u32 m0, %5, %6\n\tv_mfma_f32_16x16x32_bf16 %0, %1, %2, %0\n\tbuffer_load_dwordx4 %3, %4, %7 offen lds"
+               : "+a"(c)
+               : "v"(b), "v"(a), "v"(voff), "s"(srd), "s"(ldsb), "i"(IMM), "s"(soff)
+               : "memory", "m0", "scc");
+}
+DLLM_DEVICE void mfma_v(f32x4& c, const bf16x8v& b, const bf16x8v& a) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(b), "v"(a));
+}
 
 // RS bit 0 = fragment read schedule: 0 spreads the 16 next-sub-step reads over the 8 chunks (2 per chunk), 1 issues
 // them 4 per chunk in the first 4 chunks after they become legal (more MFMA cover for their latency).
 // RS bit 1 = direct epilogue stores from the accumulator layout instead of the LDS-staged whole-row stores (A/B).
 // RS bits 4..7 = ABLATIONS for timing studies only (results are garbage): 16 no k-loop DMAs, 32 no k-loop fragment
 // reads, 64 no k-loop wait + barrier, 128 no epilogue stores (tools/gemm_w4_bench.py --ablate)
+// RS bit 8 = k-loop DMAs fused into MFMAs (mfma_dma: M0 formed early, one DMA every few MFMAs) instead of 2-3 DMA
+// statements back to back after each chunk
 template <bool BKM, bool BIAS, bool ACC, int RS, int EPI = W4_EPI_NONE>
 __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -265,6 +289,12 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
     constexpr int d = decltype(D)::value;
     if constexpr (d < 8) dma16<(uint32_t)d * 1024u>(q.sa, va[d], q.soa, q.ldsb);
     else dma16<TB + (uint32_t)(d - 8) * 1024u>(q.sb, vb[d - 8], q.sob, q.ldsb);
+  };
+  // MFMA (i, j) of a chunk carrying DMA d of k-tile plan q
+  auto mfma_dma_d = [&](f32x4& c, const bf16x8v& b, const bf16x8v& a, const Dma& q, auto D) {
+    constexpr int d = decltype(D)::value;
+    if constexpr (d < 8) mfma_dma<(uint32_t)d * 1024u>(c, b, a, q.sa, va[d], q.soa, q.ldsb);
+    else mfma_dma<TB + (uint32_t)(d - 8) * 1024u>(c, b, a, q.sb, vb[d - 8], q.sob, q.ldsb);
   };
 
   // ---- fragment reads.  Row image: a[i] = rows wm*128 + 16 i + (l & 15), k chunk kk/8 + (l >> 4), swizzled by
@@ -405,9 +435,21 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
       const Dma q = plan_next(ti, kt, b);
       sfor<1, 8>([&](auto I) {
         constexpr int i = decltype(I)::value;
-        chunk(fa1, fb1, i);
         // DMA: instructions 0..7 of A then of B, spread over chunks 1..7 (2, 2, 2, 3, 2, 2, 3)
-        if constexpr ((RS & 16) == 0) sfor<(i - 1) * 16 / 7, i * 16 / 7>([&](auto D) { dma(q, D); });
+        constexpr int d0 = (i - 1) * 16 / 7, d1 = i * 16 / 7;
+        if constexpr ((RS & 256) != 0 && (RS & 16) == 0) {
+          // DMA k of the chunk's n rides on MFMA 1 + 7 k / n (1, 4 or 1, 3, 5)
+          sfor<0, 8>([&](auto J) {
+            constexpr int j = decltype(J)::value;
+            constexpr int n = d1 - d0;
+            constexpr int k = dma_slot(j, n);
+            if constexpr (k >= 0) mfma_dma_d(acc[i][j], fb1[j], fa1[i], q, std::integral_constant<int, d0 + k>{});
+            else mfma_v(acc[i][j], fb1[j], fa1[i]);
+          });
+        } else {
+          chunk(fa1, fb1, i);
+          if constexpr ((RS & 16) == 0) sfor<d0, d1>([&](auto D) { dma(q, D); });
+        }
         // fragments of k-tile g+1 (buffer b ^ 1), first half: B in chunks 1..4, A in chunks 5..7
         if constexpr ((RS & 32) != 0) {
         } else if constexpr ((RS & 1) == 0) {
@@ -855,6 +897,7 @@ int launch(const GemmW4Params& p, bool persist, hipStream_t st) {
       default: break;
     }
   }
+  if (rs & 256) return launch_rs<BKM, BIAS, ACC, 257>(p, persist, st);
   switch (rs & 3) {  // bit 1: direct (unstaged) epilogue stores, for A/B
     case 0: return launch_rs<BKM, BIAS, ACC, 0>(p, persist, st);
     case 2: return launch_rs<BKM, BIAS, ACC, 2>(p, persist, st);
@@ -874,17 +917,23 @@ int dispatch(const GemmW4Params& p, bool persist, hipStream_t st) {
 // epi: W4_EPI_NONE, W4_EPI_RELU (NT, optional bias, no accumulate), W4_EPI_DRELU_M (NN, no bias, no accumulate)
 extern "C" int dllm_gemm_w4(const GemmW4Params* pp, int b_kmajor, int persist, int epi, hipStream_t st) {
   const GemmW4Params& p = *pp;
+  const char* rs_env = getenv("DLLM_W4_RS");
+  const bool il = rs_env != nullptr && (atoi(rs_env) & 256) != 0;
   // N % 8: 16-B C stores (CEF stores no C: any N)
   if (p.M <= 0 || p.N <= 0 || p.K <= 0 || p.K % BK || (p.N % 8 && epi != W4_EPI_CEF) || p.tm * 256 < p.M ||
       p.tn * 256 < p.N)
     return -4;
   if (epi == W4_EPI_RELU) {
     if (b_kmajor || p.accumulate || p.mask == nullptr) return -5;
+    if (il)
+      return p.bias ? launch_rs<false, true, false, 257, W4_EPI_RELU>(p, persist != 0, st)
+                    : launch_rs<false, false, false, 257, W4_EPI_RELU>(p, persist != 0, st);
     return p.bias ? launch_rs<false, true, false, 1, W4_EPI_RELU>(p, persist != 0, st)
                   : launch_rs<false, false, false, 1, W4_EPI_RELU>(p, persist != 0, st);
   }
   if (epi == W4_EPI_DRELU_M) {
     if (!b_kmajor || p.accumulate || p.bias || p.mask == nullptr) return -5;
+    if (il) return launch_rs<true, false, false, 257, W4_EPI_DRELU_M>(p, persist != 0, st);
     return launch_rs<true, false, false, 1, W4_EPI_DRELU_M>(p, persist != 0, st);
   }
   if (epi == W4_EPI_GELU) {  // NT, bias, two outputs; persistent (store-only epilogue)
@@ -925,6 +974,7 @@ extern "C" int dllm_gemm_w4(const GemmW4Params* pp, int b_kmajor, int persist, i
     // every split's k-major descriptors (k-rows x leading dimension) must fit their 32-bit byte range
     const long span = ((long)(p.kchunk - 1) * std::max(p.lda, p.ldb) + std::max(p.M, p.N)) * 2;
     if (span >= 0xFFFFFFFFL) return -6;
+    if (il) return launch_rs<true, false, false, 257, W4_EPI_WG>(p, false, st);
     return launch_rs<true, false, false, 1, W4_EPI_WG>(p, false, st);
   }
   if (epi != W4_EPI_NONE) return -5;

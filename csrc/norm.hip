@@ -320,16 +320,9 @@ extern "C" int dllm_norm_fwd(const void* x, const void* resid, const void* w, co
               : launch_fwd<float, 0>(x, resid, w, b, out, s_out, mean, rstd, N, d, eps, p, seed, st);
 }
 
-// Number of partial rows the caller must allocate for dw_part/db_part.
-// DLLM_NORM_BWD_G: cap on the workgroups (default 512 = 2 per CU; each wave then walks N / 2048 rows, two at a time)
-static int norm_bwd_cap() {
-  static const int cap = [] {
-    const char* e = getenv("DLLM_NORM_BWD_G");
-    const int v = e != nullptr ? atoi(e) : 0;
-    return v > 0 ? v : 512;
-  }();
-  return cap;
-}
+// Number of partial rows the caller must allocate for dw_part/db_part: the workgroup cap, 512 = 2 per CU (each wave
+// then walks N / 2048 rows, two at a time; other caps measured no better, profiles/r4_norm_bandwidth.txt)
+static int norm_bwd_cap() { return 512; }
 
 // out[col] (+)= sum of the G rows of part [G][d] (fp32 partial column sums handed to a bias gradient, ops/gemm.py)
 extern "C" int dllm_colsum_partials_acc(const float* part, void* out, int out_is_bf16, int G, int d, hipStream_t st) {

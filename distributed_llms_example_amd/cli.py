@@ -13,6 +13,7 @@ import os
 from .data.dataset import convert_examples_to_features, load_samsum, synthetic_samsum_records
 from .data.tokenization import load_tokenizer
 from .models.config import resolve_config
+from .ops import routing
 from .platform import valohai
 
 
@@ -75,14 +76,15 @@ def base_parser(description: str, defaults: dict | None = None) -> argparse.Argu
 # all 818 at once; tools/eval_bench.py, profiles/r2_eval_batch.txt), and a 288 GB GPU holds the caches of hundreds of
 # sequences, so GPU runs evaluate in batches of at least this many samples (the reference evaluates with its training
 # batch size, or 1 in train-accelerator).  Results are the same per sample.
-GPU_EVAL_BATCH = int(os.environ.get("DLLM_EVAL_BATCH", "256"))
+def gpu_eval_batch() -> int:
+    return int(routing.get("eval_batch"))
 
 
 def eval_batch_size(args, device) -> int:
     if getattr(args, "eval_batch_size", None):
         return args.eval_batch_size
     bs = args.batch_size or 1
-    return max(bs, GPU_EVAL_BATCH) if getattr(device, "type", str(device)) == "cuda" else bs
+    return max(bs, gpu_eval_batch()) if getattr(device, "type", str(device)) == "cuda" else bs
 
 
 def apply_overrides(cfg, spec: str | None):

@@ -19,7 +19,6 @@ input starts from the label's last non-pad token (the language id).
 """
 from __future__ import annotations
 
-import os
 
 import math
 
@@ -38,7 +37,7 @@ from .config import Seq2SeqConfig
 from .output import Seq2SeqLMOutput
 
 
-_NORM_BIAS_COLSUM = os.environ.get("DLLM_NORM_BIAS_COLSUM", "1") != "0"  # 0: separate column-sum pass (A/B)
+_NORM_BIAS_COLSUM = True  # False: a separate column-sum pass for the out_proj / fc2 bias gradients (tests flip it)
 
 class BartAttention(nn.Module):
     def __init__(self, cfg: Seq2SeqConfig, cross: bool):

@@ -16,10 +16,10 @@ projected once per generate call, and every decode step runs the same fused kern
 """
 from __future__ import annotations
 
-import os
 
 import torch
 
+from ..ops import routing
 from ..ops.attention import relative_bias_lut  # noqa: F401  (documented dependency)
 
 
@@ -117,7 +117,7 @@ def _apply_processors_device(logp, seqs, cur_len, min_length, no_repeat_ngram_si
 
 def _fused_beam_ok(logits, nb: int) -> bool:
     from .. import _ext
-    return (os.environ.get("DLLM_GEN_FUSED_BEAM", "1") != "0" and nb <= 8 and 2 * nb <= 16 and logits.dim() == 2
+    return (bool(routing.get("gen_fused_beam")) and nb <= 8 and 2 * nb <= 16 and logits.dim() == 2
             and logits.dtype in (torch.bfloat16, torch.float32) and _ext.use_native(logits))
 
 
@@ -275,7 +275,7 @@ def generate(model, input_ids, attention_mask=None, max_length: int | None = Non
         # cross-attention K/V projected once per batch entry and shared by its nb hypotheses: the decoder's
         # cross-attention runs the beams as nb query rows of one (entry, head) — K/V read once per step, not nb times
         cross = model.project_cross_kv(enc)
-        if nb > 1 and os.environ.get("DLLM_GEN_SHARED_CROSS", "1") == "0":  # A/B: per-hypothesis copies
+        if nb > 1 and not routing.get("gen_shared_cross"):  # A/B: per-hypothesis copies
             enc = enc.repeat_interleave(nb, 0)
             attention_mask = attention_mask.repeat_interleave(nb, 0) if attention_mask is not None else None
             cross = model.project_cross_kv(enc)
@@ -287,7 +287,7 @@ def generate(model, input_ids, attention_mask=None, max_length: int | None = Non
         seqs = torch.full((N, max_length), pad, dtype=torch.long, device=dev)
         seqs[:, 0] = start
         cur = 1
-        check_every = max(1, int(os.environ.get("DLLM_GEN_CHECK_EVERY", "8")))
+        check_every = max(1, int(routing.get("gen_check_every")))
 
         def process(logp, sq, c):
             return _apply_processors_device(logp, sq, c, min_length, no_repeat_ngram_size, forced_bos, forced_eos,
@@ -313,12 +313,12 @@ def generate(model, input_ids, attention_mask=None, max_length: int | None = Non
             flags = torch.stack(all_done_at).tolist() if all_done_at else []
             end = next((i + 2 for i, f in enumerate(flags) if f), cur)
             return seqs[:, :end]
-        if os.environ.get("DLLM_GEN_HOST", "0") != "1":
+        if not routing.get("gen_host"):
             proc = (min_length, no_repeat_ngram_size, forced_bos, forced_eos, max_length, eos)
             return _beam_search_device(model, seqs, enc, attention_mask, caches, cross, B, nb, max_length, proc,
                                        eos, pad, length_penalty, early_stopping, check_every)
         # ---------------------------------------------------------------- beam search, host bookkeeping
-        # (DLLM_GEN_HOST=1: the original per-step host loop, kept as the A/B oracle of the device version)
+        # (routing gen_host=1: the original per-step host loop, kept as the A/B oracle of the device version)
         beam_scores = torch.zeros(B, nb, device=dev)
         beam_scores[:, 1:] = -1e9
         beam_scores = beam_scores.view(-1)

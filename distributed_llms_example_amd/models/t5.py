@@ -95,13 +95,12 @@ class T5Attention(nn.Module):
             else:
                 o = ring_attention(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], group=lut.group, **kw2)
         else:
-            pre = attn_ops.prefetch_dropout_mask(x, B, H, S, S, p, seed) if cache is None else None
             qkv = self.qkv(x).view(B, S, 3, H, D)
             if cache is not None:
                 k, v = cache.append(qkv[:, :, 1], qkv[:, :, 2])
                 o = attn_ops.attention(qkv[:, :, 0], k, v, **kw)
             else:
-                o = attn_ops.attention_qkv(qkv, pre=pre, **kw)
+                o = attn_ops.attention_qkv(qkv, **kw)
         return self.o(o.reshape(B, S, H * D))
 
 

@@ -24,11 +24,11 @@ from __future__ import annotations
 
 import math
 
-import os
 
 import torch
 
 from .. import _ext
+from . import routing
 from . import streams
 from .gemm import colsum_record
 from .rng import attention_keep_mask
@@ -153,9 +153,9 @@ class _AttnFn(torch.autograd.Function):
             dmask_in.record_stream(cur)
         sat = getattr(lut, "_dllm_sat", None) if lut is not None else None
         sat_lo, sat_hi = sat if sat is not None else (-1, -1)
-        fsat = os.environ.get("DLLM_ATTN_FWD_SAT", "1") == "1"  # forward scalar-bias tiles (A/B knob, -2 %)
+        # saturated bias tiles add a scalar instead of reading the LUT (forward -2 %)
         o, lse, dmask = C.attn_fwd(q, k, v, kpm, lut, float(scale), bool(causal), float(p), int(seed), dmask_in,
-                                   sat_lo if fsat else -1, sat_hi if fsat else -1)
+                                   sat_lo, sat_hi)
         ctx.save_for_backward(a, b, c, o, lse, lut, kpm, dmask)
         ctx.cfg = (mode, scale, causal, p, seed, lut is not None and lut.requires_grad, sat_lo, sat_hi)
         # packed inputs straight from a biased projection (ops/linear.py marks its output): the backward kernels also
@@ -220,8 +220,8 @@ class _AttnFn(torch.autograd.Function):
         return None, da, db, dc, (dlut if need_dlut else None), None, None, None, None, None, None
 
 
-# 0: the projections' bias gradients from a separate column reduction of dQKV (A/B; tests flip the module attribute)
-BIAS_COLSUM = os.environ.get("DLLM_ATTN_BIAS_COLSUM", "1") != "0"
+# False: the projections' bias gradients from a separate column reduction of dQKV (tests flip the module attribute)
+BIAS_COLSUM = True
 
 
 def _bias_out(t) -> bool:
@@ -245,13 +245,13 @@ def _native(t) -> bool:
     """bf16 -> csrc/attn.hip; fp32 — the reference's own precision (ref/train-torchrun.py:115-128 sets neither bf16
     nor fp16; Accelerate's default mixed_precision is 'no') — -> csrc/attn_f32.hip (f32-input MFMA, exact f32
     products).  Head dim 64 (every model this framework builds).  Anything else (CPU, other head dims) takes the
-    composite ``_reference`` below, the exact-math oracle the kernels are tested against.  ``DLLM_ATTN_F32=0`` sends
-    fp32 to the composite (A/B)."""
+    composite ``_reference`` below, the exact-math oracle the kernels are tested against.  ops/routing.py ``attn_f32``
+    = 0 sends fp32 to the composite (A/B)."""
     if not _ext.use_native(t) or t.shape[-1] != 64:
         return False
     if t.dtype == torch.bfloat16:
         return True
-    return t.dtype == torch.float32 and os.environ.get("DLLM_ATTN_F32", "1") != "0"
+    return t.dtype == torch.float32 and bool(routing.get("attn_f32"))
 
 
 def attention(q, k, v, *, scale: float = 1.0, causal: bool = False, key_padding_mask=None, bias_lut=None,
@@ -276,11 +276,11 @@ _SIDE: dict = {}
 
 
 def prefetch_dropout_mask(like: torch.Tensor, B: int, H: int, Sq: int, Sk: int, p: float, seed: int):
-    """``DLLM_ATTN_MASK_STREAM=1``: generate the attention-dropout keep bits for an upcoming call on a side HIP
-    stream, so the VALU-only mask kernel overlaps the (MFMA-bound) projection GEMM issued meanwhile on the
-    compute stream.  Returns a handle for ``attention_qkv(pre=...)`` or None (mask hashed inside the forward)."""
-    if (p <= 0.0 or os.environ.get("DLLM_ATTN_MASK_STREAM", "0") != "1" or not _native(like)
-            or like.dtype != torch.bfloat16):
+    """Generate the attention-dropout keep bits for an upcoming call on a side HIP stream (the VALU-only mask kernel
+    overlapping a projection GEMM issued meanwhile on the compute stream).  Returns a handle for
+    ``attention_qkv(pre=...)`` or None.  Not used by the models: the forward hashing the bits itself measured faster
+    (profiles/r3_attn_dropout_packed_ab.txt); kept as an API, tested equal to the in-kernel bits."""
+    if p <= 0.0 or not _native(like) or like.dtype != torch.bfloat16:
         return None
     dev = like.device
     side = _SIDE.get(dev)

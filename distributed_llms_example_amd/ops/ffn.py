@@ -26,46 +26,27 @@ Taken only when both linears carry FlatParams-managed gradients (``_dllm_fused_w
 bf16 on the GPU and the shapes suit the kernel (tokens and d_ff multiples of 256, d_model of 64); anything
 else (CPU, odd token counts) runs the unfused modules with identical semantics.  Gated FLAN-T5 FFNs take
 ``gated_ffn`` (one GEMM pairs gate and up columns in registers, epilogues 8 / 9).
-``DLLM_FUSED_FFN=0`` forces the unfused path (A/B runs); ``DLLM_GEMM_FUSED_VARIANT=n`` forces a kernel
-variant (csrc/gemm_fused.hip); ``DLLM_RELU_MASK=0`` makes the ReLU backward read ``H`` instead of the bits.
+Which kernel runs which FFN (row thresholds, GELU kernel, gated bounds) is ops/routing.py's table (``ffn*`` and
+``gated_*`` keys; ``DLLM_ROUTE=ffn=unfused`` forces the unfused path for A/B runs).
 """
 from __future__ import annotations
-
-import os
 
 import torch
 import torch.nn.functional as F
 
 from .. import _ext
 from .activations import act_dropout
-from . import gemm, streams
+from . import gemm, routing, streams
 from .gemm import bias_grad_accumulate, linear_dgrad, linear_fwd, wgrad_accumulate
-from .linear import _RES_GEMM, _fire, _fusable, _gbuf, _use
+from . import linear as _linear
+from .linear import _fire, _fusable, _gbuf, _use
 
 # activation -> (forward epilogue, backward epilogue) of csrc/gemm_fused.hip
 EPILOGUES = {"relu": (1, 3), "gelu": (2, 4), "gelu_new": (5, 6), "gelu_fast": (5, 6)}
-_VARIANT = int(os.environ.get("DLLM_GEMM_FUSED_VARIANT", "-1"))  # -1: picked by K in csrc/bind.cpp
-_RELU_MASK = os.environ.get("DLLM_RELU_MASK", "1") != "0"  # 0: the backward re-reads H (A/B runs)
-_COLSUM = os.environ.get("DLLM_FFN_BIAS_COLSUM", "1") != "0"  # 0: wi bias gradient by a separate column-sum pass
-# ReLU FFN (T5) on csrc/gemm_w4.hip (default since round 5): forward with the ReLU + dropout + bit-mask epilogue, backward
-# input gradient through that mask, instead of the 8-wave ping-pong kernel of csrc/gemm_fused.hip (DLLM_W4_FFN=0).  In
-# round 3 it measured 0.5 % slower (profiles/r3_w4_ffn_ab.txt): its epilogue spilled 53 VGPRs because all 8 mask words
-# of a tile stayed live through it.  Stored per row group (round 5) the bias-free variant is spill-free: forward 2.74 vs
-# 2.90 ms at the t5-base encoder shape, step +0.24 % / +0.50 % on two boxes (profiles/r5_w4_relu_ffn_ab.txt).
-_W4_FFN = os.environ.get("DLLM_W4_FFN", "1") != "0"
-# ... from this many token rows up; below it the ping-pong forward (its bit mask feeds the same w4 backward) measured
-# +0.35 % / +0.26 % at t5-base b=8 / b=1 x GA16 (8K / 1K encoder rows: too few 256 x 256 tiles for w4's one workgroup
-# per CU, profiles/r5_ffn_small_rows_ab.txt)
-_W4_FFN_MIN_ROWS = int(os.environ.get("DLLM_W4_FFN_MIN_ROWS", "65536"))
-# The ReLU backward (dU = dY Wo through the forward's bit mask) on csrc/gemm_w4.hip, reading the ping-pong forward's
-# mask layout (mask_pp): 17 % faster than the ping-pong backward kernel (profiles/r3_ffn_kernel_profile.txt; whole step -0.9 %, profiles/r3_w4_ffn_bwd_ab.txt)
-_W4_FFN_BWD = os.environ.get("DLLM_W4_FFN_BWD", "1") != "0"
-# GELU (erf) FFN (BART) on csrc/gemm_w4.hip's GELU epilogues (forward: h and the dropout-scaled derivative; backward:
-# dU = dH * derivative with the wi bias column partials) instead of the ping-pong kernel's epilogues 2 / 4 (DLLM_W4_GELU=1).
-# Off by default: at the BART fc1 shape both kernels are bound by the forward's two [tokens, d_ff] bf16 outputs
-# (w4 GELU forward 2660 us vs 1835 us without the epilogue; ping-pong 2552 us; backward equal), and the bart-large step
-# ran 0.25-0.43 % slower with it (profiles/r5_w4_gelu_ab.txt)
-_W4_GELU = os.environ.get("DLLM_W4_GELU", "0") == "1"
+# kernel choices, with their evidence: ops/routing.py.  The ReLU FFN runs on csrc/gemm_w4.hip (ReLU + dropout + bit-mask
+# epilogue forward, input gradient through that mask) from ``ffn_w4_min_rows`` token rows and on the ping-pong kernel
+# below (its bit mask feeds the same w4 backward); the GELU FFN on the ping-pong kernel (``ffn_gelu`` = pp) or the w4
+# GELU epilogues (= w4); FFNs under ``ffn_min_rows`` rows run unfused (hipBLASLt + the activation kernel)
 w4_ffn_calls = 0
 w4_gelu_calls = 0
 fused_calls = 0  # number of FFN forwards that took the fused path (tests assert the kernel really ran)
@@ -73,18 +54,11 @@ fused_calls = 0  # number of FFN forwards that took the fused path (tests assert
 
 def _pingpong(C, K: int) -> bool:
     """The kernel chosen for reduction length K is the ping-pong one (the only one with the ReLU bit mask)."""
-    return (_VARIANT if _VARIANT >= 0 else C.gemm_fused_variant(K)) in (8, 9)
+    return C.gemm_fused_variant(K) in (8, 9)
 
 
 def _enabled() -> bool:
-    return os.environ.get("DLLM_FUSED_FFN", "1") != "0"
-
-
-# FFNs with fewer token rows than this run unfused (library GEMMs + the activation / dropout kernel): at 1024 rows and
-# below (t5-base b=1 x GA16 encoder and decoder, b=8 decoder) the fused kernels' 256 x 256 tiles leave most CUs idle and
-# hipBLASLt's tuned small-shape kernels win: +1.9 % (b=8 x GA16), +2.2 % (b=1 x GA16) over fusing them
-# (profiles/r5_ffn_small_rows_ab.txt; unfusing the 8K-row encoder FFNs of b=8 as well lost 1.6 %)
-_FUSED_MIN_ROWS = int(os.environ.get("DLLM_FUSED_FFN_MIN_ROWS", "1025"))
+    return routing.get("ffn") == "fused"
 
 
 class _FusedFFNFn(torch.autograd.Function):
@@ -95,7 +69,7 @@ class _FusedFFNFn(torch.autograd.Function):
         x2 = x.reshape(-1, shape[-1])
         efwd, _ = EPILOGUES[act]
         u = mask = None
-        if efwd == 1 and _W4_FFN and x2.shape[0] >= _W4_FFN_MIN_ROWS and C.gemm_w4_supported(x2, wi, False) and \
+        if efwd == 1 and x2.shape[0] >= routing.get("ffn_w4_min_rows") and C.gemm_w4_supported(x2, wi, False) and \
                 (bi is None or (bi.dtype == torch.bfloat16 and bi.is_contiguous())):
             global w4_ffn_calls
             w4_ffn_calls += 1
@@ -113,7 +87,7 @@ class _FusedFFNFn(torch.autograd.Function):
         ctx.w4 = False
         if efwd != 1:  # GELU: the backward multiplies by the stored derivative
             u = torch.empty(x2.shape[0], wi.shape[0], device=x.device, dtype=x.dtype)
-        if efwd == 2 and _W4_GELU and C.gemm_w4_supported(x2, wi, False) and \
+        if efwd == 2 and routing.get("ffn_gelu") == "w4" and C.gemm_w4_supported(x2, wi, False) and \
                 (bi is None or (bi.dtype == torch.bfloat16 and bi.is_contiguous())):
             global w4_gelu_calls
             w4_gelu_calls += 1
@@ -126,9 +100,9 @@ class _FusedFFNFn(torch.autograd.Function):
                 _use(q)
             ctx.cfg = (act, float(p), int(seed), shape)
             return y.view(*shape[:-1], wo.shape[0]), x.view_as(x)
-        if efwd == 1 and _RELU_MASK and _pingpong(C, x2.shape[1]) and _pingpong(C, wo.shape[0]):  # ReLU: mask bits
+        if efwd == 1 and _pingpong(C, x2.shape[1]) and _pingpong(C, wo.shape[0]):  # ReLU: mask bits
             mask = torch.empty(x2.shape[0] * wi.shape[0] // 32, device=x.device, dtype=torch.int32)
-        h = C.gemm_fused(x2, wi, False, efwd, bi, None, u, float(p), int(seed), _VARIANT, mask)
+        h = C.gemm_fused(x2, wi, False, efwd, bi, None, u, float(p), int(seed), -1, mask)
         y = linear_fwd(h, wo, bo)
         ctx.set_materialize_grads(False)  # the residual alias's gradient is None when the caller does not use it
         ctx.save_for_backward(x2, h, u, mask)
@@ -151,8 +125,9 @@ class _FusedFFNFn(torch.autograd.Function):
             dy2 = dy2.contiguous()
         # GELU: the wi bias gradient comes out of the same GEMM's epilogue as per-128-row column sums of dU
         bsum = None
-        w4g = ebwd == 4 and _W4_GELU and dy2.shape[0] % 128 == 0 and C.gemm_w4_supported(dy2, wo, True)
-        if Bi is not None and ebwd in (4, 6) and _COLSUM and (w4g or _pingpong(C, wo.shape[0])):
+        w4g = (ebwd == 4 and routing.get("ffn_gelu") == "w4" and dy2.shape[0] % 128 == 0
+               and C.gemm_w4_supported(dy2, wo, True))
+        if Bi is not None and ebwd in (4, 6) and (w4g or _pingpong(C, wo.shape[0])):
             bsum = torch.empty(dy2.shape[0] // 128, wo.shape[1], device=dy2.device, dtype=torch.float32)
         if w4g:  # dU = dH * (stored derivative) + per-128-row column partials, on the w4 kernel
             cs = bsum if bsum is not None else torch.empty(dy2.shape[0] // 128, wo.shape[1], device=dy2.device,
@@ -162,12 +137,12 @@ class _FusedFFNFn(torch.autograd.Function):
             if not C.gemm_w4_supported(dy2, wo, True):
                 dy2 = dy2.contiguous()
             du = C.gemm_w4(dy2, wo, True, None, None, False, -1, True, 7, p, seed, mask)
-        elif mask is not None and _W4_FFN_BWD and C.gemm_w4_supported(dy2, wo, True):  # d-relu, ping-pong mask
+        elif mask is not None and C.gemm_w4_supported(dy2, wo, True):  # d-relu, ping-pong mask
             du = C.gemm_w4(dy2, wo, True, None, None, False, -1, True, 7, p, seed, mask, True)
         elif mask is not None:  # d-relu from the bit mask
-            du = C.gemm_fused(dy2, wo, True, 7, None, None, None, p, seed, _VARIANT, mask)
+            du = C.gemm_fused(dy2, wo, True, 7, None, None, None, p, seed, -1, mask)
         else:
-            du = C.gemm_fused(dy2, wo, True, ebwd, None, h if ebwd == 3 else u, None, p, seed, _VARIANT, None, bsum)
+            du = C.gemm_fused(dy2, wo, True, ebwd, None, h if ebwd == 3 else u, None, p, seed, -1, None, bsum)
         with torch.no_grad():
             wgrad_accumulate(_gbuf(Wo), dy2, h, async_ok=streams.site_ok(Wo))
             if Bo is not None:
@@ -249,21 +224,18 @@ class _FusedGatedFFNFn(torch.autograd.Function):
 
 
 gated_calls = 0  # number of gated FFN forwards that took the fused path
-# Where the fused gated GEMMs win (tools/geglu_bench.py, profiles/r2_geglu_bench.jsonl, flan-t5 A/Bs in
-# profiles/r2_geglu_ab.txt): they need >= 2 output tiles per CU to run persistent (epilogue stores / loads under the
-# next tile's MFMAs), so tokens x d_ff >= _GATED_MIN_MF; and with the longest reduction (d_model 2048) hipBLASLt's
-# GEMM outruns the ping-pong kernel by as much as the two activation passes cost, so d_model <= _GATED_MAX_D.  Round 2
-# had flan-t5-large 3 % slower fused; since the gated backward's epilogue loads and stores whole rows through LDS
-# (round 4, profiles/r4_gemm_pp_stage_ab.txt) flan-t5-large b=32 is 2.1 % faster fused and flan-t5-xl equal, so the
-# bound moved from 768 to 1024.  flan-t5-base at b=128: 875 samples/s.
-_GATED_MIN_MF = int(os.environ.get("DLLM_GATED_MIN_MF", str(2 * 256 * 256 * 256)))
-_GATED_MAX_D = int(os.environ.get("DLLM_GATED_MAX_D", "1024"))
+# Where the fused gated GEMMs win (ops/routing.py gated_min_mf / gated_max_d; tools/geglu_bench.py,
+# profiles/r2_geglu_bench.jsonl, flan-t5 A/Bs in profiles/r2_geglu_ab.txt): they need >= 2 output tiles per CU to run
+# persistent (epilogue stores / loads under the next tile's MFMAs), and with the longest reduction (d_model 2048)
+# hipBLASLt's GEMM outruns the ping-pong kernel by as much as the two activation passes cost.  Since the gated
+# backward's epilogue loads and stores whole rows through LDS (round 4, profiles/r4_gemm_pp_stage_ab.txt)
+# flan-t5-large b=32 is 2.1 % faster fused and flan-t5-xl equal, so the bound moved from 768 to 1024.
 
 
 def gated_ffn(x: torch.Tensor, lin_in, lin_out, act: str, p: float = 0.0, seed: int = 0) -> torch.Tensor:
     """``lin_out(dropout(act(x wi_0ᵀ) * (x wi_1ᵀ)))`` with ``lin_in.weight = [wi_0; wi_1]``, fused where possible
-    (tanh GELU, bias-free, tokens and d_ff multiples of 256, tokens x d_ff >= ``_GATED_MIN_MF``,
-    d_model <= ``_GATED_MAX_D``)."""
+    (tanh GELU, bias-free, tokens and d_ff multiples of 256, tokens x d_ff >= ``gated_min_mf``,
+    d_model <= ``gated_max_d``, ops/routing.py)."""
     global gated_calls
     wi, wo = lin_in.weight, lin_out.weight
     if (act in ("gelu_new", "gelu_fast") and _enabled() and x.dtype == torch.bfloat16 and _ext.use_native(x)
@@ -273,8 +245,8 @@ def gated_ffn(x: torch.Tensor, lin_in, lin_out, act: str, p: float = 0.0, seed: 
         x2 = x.reshape(-1, x.shape[-1])
         Fd = wo.shape[1]
         if (tuple(wi.shape) == (2 * Fd, x2.shape[1]) and tuple(wo.shape) == (x2.shape[1], Fd) and Fd % 256 == 0
-                and x2.shape[0] % 256 == 0 and 2 * x2.shape[0] * Fd < 2**32 and x2.shape[0] * Fd >= _GATED_MIN_MF
-                and x2.shape[1] <= _GATED_MAX_D
+                and x2.shape[0] % 256 == 0 and 2 * x2.shape[0] * Fd < 2**32
+                and x2.shape[0] * Fd >= routing.get("gated_min_mf") and x2.shape[1] <= routing.get("gated_max_d")
                 and C.gemm_fused_supported(x2, wi, False) and C.gemm_fused_supported(x2, wo, True)):
             gated_calls += 1
             return _FusedGatedFFNFn.apply(x, wi.detach(), wo.detach(), p, seed, (wi, wo))
@@ -294,12 +266,12 @@ def ffn_res(x: torch.Tensor, lin_in, lin_out, act: str, p: float = 0.0, seed: in
             and torch.is_grad_enabled()
             and all(_fusable(t) for t in (lin_in.weight, lin_in.bias, lin_out.weight, lin_out.bias))):
         x2 = x.reshape(-1, x.shape[-1])
-        if x2.shape[0] >= _FUSED_MIN_ROWS and _fusable_shapes(x2, lin_in.weight, lin_out.weight):
+        if x2.shape[0] >= routing.get("ffn_min_rows") and _fusable_shapes(x2, lin_in.weight, lin_out.weight):
             fused_calls += 1
             bi, bo = lin_in.bias, lin_out.bias
             y, res = _FusedFFNFn.apply(x, lin_in.weight.detach(), None if bi is None else bi.detach(),
                                        lin_out.weight.detach(), None if bo is None else bo.detach(), act, p, seed,
                                        (lin_in.weight, bi, lin_out.weight, bo))
-            return (y, res) if residual and _RES_GEMM else (y, x) if residual else y
+            return (y, res) if residual and _linear._RES_GEMM else (y, x) if residual else y
     y = lin_out(act_dropout(lin_in(x), act, p, seed))
     return (y, x) if residual else y

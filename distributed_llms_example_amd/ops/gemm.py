@@ -9,11 +9,10 @@ Who runs what (t5-base / bart-large training step, default settings):
   (ops/ffn.py): csrc/gemm_fused.hip and csrc/gemm_w4.hip;
 * the PLAIN projections — forward ``Y = X Wᵀ (+ b)`` of the attention q/k/v/o and FFN output layers, and the LM
   head — go to the library (hipBLASLt through torch, with the TunableOp table in configs/tunableop/): csrc/gemm_w4.hip
-  ties it on these shapes in isolation and lost 0.8 % of the step in situ (``_W4_MODE`` below,
-  profiles/r3_w4_routing_ab.txt).  Their input gradients ``dX (+)= dY W`` run on csrc/gemm_w4.hip where that measured
-  faster in the step (layers at most 768 features wide, >= 64K token rows: t5-base at large batch), on hipBLASLt
-  otherwise.  ``DLLM_W4_GEMM=1`` routes every supported shape to csrc/gemm_w4.hip, ``auto`` the shapes it wins in
-  isolation, ``0`` none.
+  ties it on these shapes in isolation and lost 0.8 % of the step in situ (profiles/r3_w4_routing_ab.txt).  Their input
+  gradients ``dX (+)= dY W`` run on csrc/gemm_w4.hip where that measured faster in the step (layers at most 768
+  features wide, >= 64K token rows: t5-base at large batch), on hipBLASLt otherwise.  The choice is ops/routing.py's
+  table (``proj_fwd`` / ``proj_dgrad``).
 
 Weight-gradient GEMM notes:
 
@@ -21,62 +20,40 @@ Both operands are token-major ([tokens, features]), the reduction runs over toke
 result is accumulated straight into the flat gradient buffer (bf16, or fp32 for fp32 gradient
 accumulation).  Shapes the kernel does not cover (N not a multiple of 256, M not of 8, token counts not
 multiples of 64, CPU tensors) go to
-``torch.addmm`` (hipBLASLt / CPU BLAS).  ``DLLM_NATIVE_WGRAD=0`` forces the library path (A/B runs).
+``torch.addmm`` (hipBLASLt / CPU BLAS).
 """
 from __future__ import annotations
 
 import contextlib
-import os
 
 import torch
 import torch.nn.functional as F
 
 from .. import _ext
-from . import streams
+from . import routing, streams
 
-# Routing of the projection GEMMs (profiles/r3_gemm_w4_vs_hipblaslt.jsonl, t5-base / bart-large shapes):
-#   "auto": csrc/gemm_w4.hip for input gradients whose reduction depth (the layer's output features) is
-#          <= 1024, <= 2304 with >= 128K token rows, or <= 3072 with >= 1024 output columns — there it beats
-#          hipBLASLt's NN kernels by 1-12 % (o / wo / fc2, encoder-QKV and BART-QKV dgrads, the residual-accumulating
-#          ones included) and the short-K wide forwards (QKV, +1-3 %); the other forwards and the deeper dgrads stay on
-#          hipBLASLt, which is 1-17 % faster there (profiles/r3_gemm_w4_grp_sweep.txt);
-#   "dgrad": the input-gradient shapes of "auto" only; "1": every supported shape on gemm_w4 (A/B and tests);
-#   "dgrad768" (default): the "dgrad" shapes whose output (the layer's input features) is at most 768 wide, >= 64K rows;
-#   "0": none (hipBLASLt for every plain projection).
-# In-situ whole-step A/B (profiles/r3_w4_routing_ab.txt) overrules the microbenchmark: with every shape above routed
-# to w4 the t5-base / bart-large steps ran 0.8-1 % SLOWER than hipBLASLt-only, although each routed shape is faster in
-# isolation (operands there sit in the caches; in the step they come from HBM, and w4's one-k-tile prefetch depth is
-# the shallower).  The forwards therefore stay on hipBLASLt.  The input gradients measured in situ split by width:
-# d_model 768 (t5-base's o / q / qkv input gradients) +0.33 % and +0.23 % on two leases, 4 of 4 interleaved pairs ahead
-# on the second (profiles/r5_w4route_dgrad_ab.txt, r5_w4_dgrad768_ab.txt); d_model 1024 (t5-large, bart-large) -0.45 to
-# -0.86 %: "dgrad768" routes the first and leaves the second on hipBLASLt, and only with >= 64K token rows: at the
-# micro-batch shapes (t5-base b=8 / b=1 x GA16, 8K / 1K rows) w4 cost 2.9 / 6.3 % of the step (r5_w4_dgrad768_ab.txt).
-# csrc/gemm_w4.hip also runs the T5 FFN ReLU forward and input gradient (ops/ffn.py).
-_W4_MODE = os.environ.get("DLLM_W4_GEMM", "dgrad768")
-_W4 = _W4_MODE != "0"
-_W4_DGRAD_MAX_K = 1024
-_W4_NARROW_MAX_OUT = 768
-# fewer token rows (micro-batches of 8 / 1): hipBLASLt, 2.9 / 6.3 % faster in the step
-_W4_NARROW_MIN_ROWS = int(os.environ.get("DLLM_W4_DGRAD_MIN_ROWS", "65536"))
+# Routing of the projection GEMMs: ops/routing.py ("proj_fwd", "proj_dgrad" and thresholds; the evidence is cited
+# there).  Input gradients on w4 additionally need a reduction depth (the layer's output features) the kernel wins at:
+# <= 1024, <= 2304 with >= 128K token rows, or <= 3072 with >= 1024 output columns (profiles/r3_gemm_w4_grp_sweep.txt).
 w4_calls = 0  # projections that ran on csrc/gemm_w4.hip (tests assert the kernel really ran)
 colsum_handoffs = 0  # bias gradients taken from a norm backward's column sums (bias_grad_accumulate)
 
 
 def _w4_ok(a: torch.Tensor, b: torch.Tensor, kmajor: bool) -> bool:
-    if not _W4 or a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16 or not _ext.use_native(a):
+    if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16 or not _ext.use_native(a):
         return False
-    if _W4_MODE in ("auto", "dgrad", "dgrad768"):
-        K = a.shape[-1]
-        if _W4_MODE != "auto" and not kmajor:  # "dgrad", "dgrad768": the input-gradient half of "auto" only
+    if kmajor:  # input gradients
+        mode = routing.get("proj_dgrad")
+        if mode == "lib":
             return False
-        if _W4_MODE == "dgrad768" and (b.shape[-1] > _W4_NARROW_MAX_OUT or a.shape[0] < _W4_NARROW_MIN_ROWS):
-            return False
-        if kmajor:  # input gradients
-            ok = K <= _W4_DGRAD_MAX_K or (K <= 2304 and a.shape[0] >= 131072) or (K <= 3072 and b.shape[-1] >= 1024)
-        else:  # forwards: short-K, wide outputs (the QKV projections)
-            ok = K <= 1024 and 2048 <= b.shape[0] <= 4096 and a.shape[0] >= 131072
-        if not ok:
-            return False
+        if mode == "narrow":
+            K = a.shape[-1]
+            if b.shape[-1] > routing.get("proj_dgrad_max_n") or a.shape[0] < routing.get("proj_dgrad_min_rows"):
+                return False
+            if not (K <= 1024 or (K <= 2304 and a.shape[0] >= 131072) or (K <= 3072 and b.shape[-1] >= 1024)):
+                return False
+    elif routing.get("proj_fwd") != "w4":  # forwards
+        return False
     return bool(_ext.native().gemm_w4_supported(a, b, kmajor))
 
 
@@ -106,12 +83,8 @@ def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = N
         return out
     return torch.matmul(dy, w)
 
-# -1: csrc/gemm_w4.hip's weight-gradient mode (csrc/bind.cpp kWgradW4 = 12); 0..11: the csrc/gemm.hip variants (A/B)
-_VARIANT = int(os.environ.get("DLLM_WGRAD_VARIANT", "-1"))
-
-
 def _native_ok(dy2: torch.Tensor, x2: torch.Tensor, out: torch.Tensor) -> bool:
-    if os.environ.get("DLLM_NATIVE_WGRAD", "1") == "0" or not _ext.use_native(dy2):
+    if not _ext.use_native(dy2):
         return False
     return bool(_ext.native().gemm_wgrad_supported(dy2, x2, out))
 
@@ -153,7 +126,7 @@ class WgradDefer:
                 raise RuntimeError("deferred weight-gradient operand modified in place (a writer must check holds())")
         dys, xs = [p[0] for p in parts], [p[1] for p in parts]
         d0, x0 = dys[0], xs[0]
-        if (_VARIANT in (-1, 12) and _native_ok(d0, x0, out)
+        if (_native_ok(d0, x0, out)
                 and all(d.shape == d0.shape and d.stride() == d0.stride() for d in dys)
                 and all(x.shape == x0.shape and x.stride() == x0.stride() for x in xs)):
             C = _ext.native()
@@ -254,7 +227,7 @@ def wgrad_accumulate(out: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, bet
 
 def _wgrad(out, dy2, x2, beta):
     if _native_ok(dy2, x2, out):
-        _ext.native().gemm_wgrad(dy2, x2, out, beta, _VARIANT, 0)
+        _ext.native().gemm_wgrad(dy2, x2, out, beta, -1, 0)
         return out
     if out.dtype != dy2.dtype:  # fp32 gradient buffer, bf16 operands: the product itself in fp32, then one fp32 add
         if dy2.is_cuda:

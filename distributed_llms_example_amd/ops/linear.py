@@ -14,7 +14,6 @@ ordinary autograd with identical results.
 """
 from __future__ import annotations
 
-import os
 
 import torch
 import torch.nn as nn
@@ -137,7 +136,7 @@ class _LinearResFn(torch.autograd.Function):
         return dx, None, None, None
 
 
-_RES_GEMM = os.environ.get("DLLM_RESID_GEMM", "1") != "0"  # 0: residual gradient summed by autograd (A/B)
+_RES_GEMM = True  # False: the residual gradient summed by autograd (tests flip the module attribute)
 
 
 def linear_res(x: torch.Tensor, mod) -> tuple[torch.Tensor, torch.Tensor]:

@@ -8,7 +8,7 @@ b=128; 3.3 GB for BART-large b=32 at 1024 target tokens), written by the GEMM, r
 written by its backward, read twice more by the input- and weight-gradient GEMMs.
 
 Here the vocabulary is processed in chunks of ``Vc`` columns sized so a chunk of logits (``N·Vc·2`` bytes,
-≤ ``DLLM_LMHEAD_CHUNK_MB``, default 128 MiB) stays resident in the MI355X's 256 MiB Infinity Cache:
+≤ ops/routing.py ``lmhead_chunk_mb``, default 128 MiB) stays resident in the MI355X's 256 MiB Infinity Cache:
 
 * forward: per chunk one GEMM ``h·W_cᵀ`` into a reused buffer, then csrc/ce.hip ``ce_chunk_fwd`` merges the
   chunk into a per-row online state {max, Σexp, Σx, x_label}; the last chunk writes loss_row and lse;
@@ -18,11 +18,11 @@ Here the vocabulary is processed in chunks of ``Vc`` columns sized so a chunk of
 
 The price is one extra logits GEMM per step (the recompute); the gain is memory (no ``[N, V]`` tensor, no
 ``[N, V]`` gradient) and cache-resident CE passes.  Used when the full logits would exceed
-``DLLM_LMHEAD_FULL_MB`` (default 16384 MiB — sized for the 288 GB HBM: the t5-base bench at 512 samples per GPU keeps
+``lmhead_full_mb`` (default 16384 MiB — sized for the 288 GB HBM: the t5-base bench at 512 samples per GPU keeps
 its 4 GiB of logits and runs 1.7 % faster than chunked, ``profiles/r3_lmhead_b512_ab.txt``; ``0`` = always chunked,
 ``-1`` = never), or explicitly by callers.
 
-GEMM-fused variant (``_LMHeadCEFusedFn``, the no-materialised-logits path unless ``DLLM_LMHEAD_FUSED=0``; see
+GEMM-fused variant (``_LMHeadCEFusedFn``, the no-materialised-logits path unless ``lmhead`` = logits; see
 ``use_fused``): the cross-entropy runs INSIDE the logits GEMM's epilogue (csrc/gemm_w4.hip W4_EPI_CEF / W4_EPI_CEB):
 
 * forward: ONE GEMM over the whole vocabulary whose epilogue reduces every row's 128-column half tile to an
@@ -33,19 +33,19 @@ GEMM-fused variant (``_LMHeadCEFusedFn``, the no-materialised-logits path unless
 """
 from __future__ import annotations
 
-import os
 
 import torch
 import torch.nn.functional as F
 
 from .. import _ext
 from . import gemm as _gemm
+from . import routing
 from .gemm import wgrad_accumulate
 from .linear import _fire, _fusable, _gbuf, _use
 
 
 def _chunk_cols(N: int, V: int) -> int:
-    mb = float(os.environ.get("DLLM_LMHEAD_CHUNK_MB", "128"))
+    mb = float(routing.get("lmhead_chunk_mb"))
     c = int(mb * 2**20 / (2 * max(N, 1))) // 256 * 256
     c = max(256, min(c, (V + 255) // 256 * 256))
     if V % 8 and c >= V:  # a ragged vocabulary needs >= 2 chunks (the tail chunk re-covers aligned columns)
@@ -69,7 +69,7 @@ def _chunks(V: int, vc: int):
 
 
 def use_chunked(N: int, V: int) -> bool:
-    lim = float(os.environ.get("DLLM_LMHEAD_FULL_MB", "16384"))
+    lim = float(routing.get("lmhead_full_mb"))
     if lim < 0:
         return False
     return N * V * 2 > lim * 2**20
@@ -77,10 +77,10 @@ def use_chunked(N: int, V: int) -> bool:
 
 def wants_lm_head_loss(hidden: torch.Tensor, N: int, V: int) -> bool:
     """Whether a model's training loss goes through :func:`lm_head_loss` (no materialised logits): when the full
-    logits would exceed ``DLLM_LMHEAD_FULL_MB`` (use_chunked), or always with ``DLLM_LMHEAD_FUSED=1`` (bf16 GPU)."""
+    logits would exceed ``lmhead_full_mb`` (use_chunked), or always with ``lmhead`` = fused (bf16 GPU)."""
     if use_chunked(N, V):
         return True
-    return (os.environ.get("DLLM_LMHEAD_FUSED", "auto") == "1" and hidden.dtype == torch.bfloat16
+    return (routing.get("lmhead") == "fused" and hidden.dtype == torch.bfloat16
             and hidden.shape[-1] % 64 == 0 and _ext.use_native(hidden))
 
 
@@ -212,12 +212,12 @@ class _LMHeadCEFusedFn(torch.autograd.Function):
 
 
 def use_fused() -> bool:
-    """The GEMM-epilogue CE (``_LMHeadCEFusedFn``) in place of the vocabulary-chunked path.  ``DLLM_LMHEAD_FUSED``:
+    """The GEMM-epilogue CE (``_LMHeadCEFusedFn``) in place of the vocabulary-chunked path.  ops/routing.py ``lmhead``:
     ``auto`` (default) = whenever logits are not materialised (it beats the chunked path: no logits round trip, no CE
-    passes); ``1`` = also below the full-logits budget; ``0`` = never.  Below the budget the materialised-logits path
+    passes); ``fused`` = also below the full-logits budget; ``logits`` = never.  Below the budget the materialised-logits path
     stays the default: it skips the backward's logits recompute and was 1.0 % faster per t5-base b=512 step
     (profiles/r4_lmhead_fused_ab.txt)."""
-    return os.environ.get("DLLM_LMHEAD_FUSED", "auto") != "0"
+    return routing.get("lmhead") != "logits"
 
 
 def fused_ok(h: torch.Tensor, w: torch.Tensor) -> bool:

@@ -18,7 +18,7 @@ Ordering and memory, without ``record_stream``:
 
 All three are stream waits, so a HIP-graph capture records them as graph edges (train/graph.py).
 
-Paired mode (``DLLM_WGRAD_STREAM_SITES=qkv,wi,...``, the layer roles of the parameters: the name of the module that
+Paired mode (``DLLM_ROUTE=wgrad_stream_sites=qkv+wi+...``, the layer roles of the parameters: the name of the module that
 owns the weight, e.g. T5 ``qkv`` / ``o`` / ``wi`` / ``wo``, BART ``qkv_proj`` / ``out_proj`` / ``fc1`` / ``fc2``): only
 those layers' weight gradients go to the side stream, at any micro-batch size, and instead of the lagged joins the
 compute stream joins at the end of the NEXT memory- or VALU-bound backward op (``pair_join``: the norm backward,
@@ -33,14 +33,15 @@ from __future__ import annotations
 
 import collections
 import contextlib
-import os
 import re
 
 import torch
 
-LAG = max(1, int(os.environ.get("DLLM_WGRAD_STREAM_LAG", "2")))
-_SITES_ENV = os.environ.get("DLLM_WGRAD_STREAM_SITES")
-SITES = frozenset(s for s in re.split(r"[,+]", _SITES_ENV or "") if s) if _SITES_ENV is not None else None
+from . import routing
+
+LAG = max(1, int(routing.get("wgrad_stream_lag")))
+_SITES_RAW = str(routing.get("wgrad_stream_sites"))
+SITES = frozenset(s for s in re.split(r"[,+]", _SITES_RAW) if s) if _SITES_RAW else None
 _on = [False]
 _side: dict = {}
 _used: set = set()  # devices whose side stream has work since the last join
@@ -49,18 +50,18 @@ launches = 0  # side-stream launches since import (tests assert the path really 
 
 
 def default_enabled(tokens: int | None = None) -> bool:
-    """``DLLM_WGRAD_STREAM``: ``auto`` (default) = on for micro-batches of at most ``DLLM_WGRAD_STREAM_MAX_TOKENS``
-    input tokens (default 32768), where single kernels leave the chip partly idle; off above, where two full-chip
-    GEMMs side by side only compete (t5-base, one MI355X, interleaved: batch 1 +9.8 %, batch 8 x GA 16 +4.2 %,
-    batch 512 -3.6 %, profiles/r4_wgrad_stream_ab.txt); ``1`` always; ``0`` never."""
-    mode = os.environ.get("DLLM_WGRAD_STREAM", "auto")
+    """ops/routing.py ``wgrad_stream``: ``auto`` (default) = on for micro-batches of at most
+    ``wgrad_stream_max_tokens`` input tokens (default 32768), where single kernels leave the chip partly idle; off
+    above, where two full-chip GEMMs side by side only compete (t5-base, one MI355X, interleaved: batch 1 +9.8 %,
+    batch 8 x GA 16 +4.2 %, batch 512 -3.6 %, profiles/r4_wgrad_stream_ab.txt); ``1`` always; ``0`` never."""
+    mode = str(routing.get("wgrad_stream"))
     if mode == "0":
         return False
     if SITES is not None:
         return bool(SITES)
     if mode == "1" or tokens is None:
         return True
-    return tokens <= int(os.environ.get("DLLM_WGRAD_STREAM_MAX_TOKENS", "32768"))
+    return tokens <= int(routing.get("wgrad_stream_max_tokens"))
 
 
 def _side_stream(dev: torch.device) -> torch.cuda.Stream:

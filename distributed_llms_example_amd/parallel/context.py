@@ -450,14 +450,14 @@ def chunked_attention(q, k, v, *, chunk: int, scale: float = 1.0, key_padding_ma
 
 def long_sequence_chunk(n: int, cross: bool = False, rows: int = 0) -> int | None:
     """Chunk size for an encoder of ``n`` tokens, or None when the single kernel handles it
-    (``DLLM_ATTN_CHUNK`` = block length, default 4096, used above ``DLLM_ATTN_CHUNK_MIN`` = 8192 tokens;
-    0 disables).  ``rows`` = batch x heads: with fewer than 32 rows a 4K block launches under 1024 query-tile
+    (ops/routing.py ``attn_chunk`` = block length, default 4096, used above ``attn_chunk_min`` = 8192 tokens;
+    -1 disables).  ``rows`` = batch x heads: with fewer than 32 rows a 4K block launches under 1024 query-tile
     workgroups (4 per CU), so the default block grows to 8K.  Cross-attention (a short query: few workgroups per block) keeps the single kernel up to
     its 16K-key limit and then uses 16K-key blocks."""
-    import os
-    c = int(os.environ.get("DLLM_ATTN_CHUNK", "8192" if 0 < rows < 32 else "4096"))
-    lo = int(os.environ.get("DLLM_ATTN_CHUNK_MIN", "8192"))
-    if cross and c > 0 and lo >= 8192:  # (test overrides with a small DLLM_ATTN_CHUNK_MIN chunk cross too)
+    from ..ops import routing
+    c = int(routing.get("attn_chunk")) or (8192 if 0 < rows < 32 else 4096)
+    lo = int(routing.get("attn_chunk_min"))
+    if cross and c > 0 and lo >= 8192:  # (test overrides with a small attn_chunk_min chunk cross too)
         c, lo = max(c, 16384), max(lo, 16384)
     if c <= 0 or n <= max(lo, c):
         return None

@@ -21,7 +21,6 @@ loads in csrc/adamw.hip.  Tied parameters (T5 ``shared`` == ``lm_head``) appear 
 from __future__ import annotations
 
 import builtins
-import os
 from dataclasses import dataclass
 
 import torch
@@ -90,10 +89,6 @@ class FlatParams:
         # autograd insists p.grad has p's dtype: with fp32 gradients for bf16 weights the flat slices are handed
         # to the fused ops as p._dllm_gbuf instead, and p.grad stays None
         self.views_as_grad = self.grad_dtype == self.dtype
-        fused = os.environ.get("DLLM_FUSED_WGRAD", "1") != "0"
-        if not self.views_as_grad and not fused:
-            raise ValueError("fp32 gradients for low-precision parameters need the fused gradient paths "
-                             "(DLLM_FUSED_WGRAD=1)")
         self._hooks = []
         with torch.no_grad():
             for i, (seg, p) in enumerate(zip(self.segments, self.params)):
@@ -101,7 +96,7 @@ class FlatParams:
                 view.copy_(p.data)
                 p.data = view
                 # ops/linear.py may accumulate this parameter's weight gradient inside the GEMM
-                p._dllm_fused_wgrad = fused
+                p._dllm_fused_wgrad = True
                 p._dllm_gbuf = self.grad_view(i)
                 p._dllm_pending = 0
                 p._dllm_fused_seen = False

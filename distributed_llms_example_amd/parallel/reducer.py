@@ -27,19 +27,19 @@ Two engines implement the same bucket/launch policy: the native one (csrc/reduce
 ``NativeReducer``: bucket state machine and c10d ``ProcessGroup::allreduce`` launches in C++ — the
 counterpart of DDP's C++ Reducer; readiness is signalled per parameter by FlatParams' post-accumulate
 hooks and by the fused ops, ops/linear.py ``_fire``) is used whenever the
-extension is built (``DLLM_NATIVE_REDUCER=0`` selects the Python engine below, kept as the readable
+extension is built (ops/routing.py ``reducer`` = python selects the Python engine below, kept as the readable
 reference and for A/B tests).  Bucket layout is computed here once and handed to either engine.
 """
 from __future__ import annotations
 
 import contextlib
-import os
 import time
 
 import torch
 import torch.distributed as dist
 
 from .. import _ext
+from ..ops import routing
 from ..utils import profiling
 from .flat import FlatParams
 
@@ -129,12 +129,12 @@ class GradReducer:
                 bucket_mb = self.bucket_choice["bucket_mb"]
         self.bucket_mb, self.first_bucket_mb = float(bucket_mb), first_bucket_mb
         if native is None:
-            native = os.environ.get("DLLM_NATIVE_REDUCER", "1") != "0" and _ext.native() is not None
+            native = routing.get("reducer") != "python" and _ext.native() is not None
         self.use_native = bool(native)
         # DDP's _rebuild_buckets: after the first synchronised backward the flat layout (and with it the buckets)
         # is re-laid in the order gradients actually became ready, broadcast from rank 0 so every rank agrees
         if rebuild is None:
-            rebuild = os.environ.get("DLLM_REBUILD_BUCKETS", "1") != "0"
+            rebuild = bool(routing.get("rebuild_buckets"))
         self._rebuild_pending = bool(rebuild) and overlap and self.dp
         # per synchronised backward (diagnostics / tests): segment indices in readiness order, and (bucket, number of
         # segments ready at its launch) in launch order; the previous backward's logs are kept in *_last

@@ -21,7 +21,6 @@ fp32 on CPU.
 from __future__ import annotations
 
 import contextlib
-import os
 
 import torch
 
@@ -115,7 +114,7 @@ class Accelerator:
         self.env = init_distributed(cpu=cpu if cpu else None)
         self.device = self.env.device
         if mixed_precision is None:
-            mixed_precision = os.environ.get("DLLM_MIXED_PRECISION", "bf16" if self.device.type == "cuda" else "no")
+            mixed_precision = "bf16" if self.device.type == "cuda" else "no"
         self.mixed_precision = mixed_precision
         self.dtype = torch.bfloat16 if mixed_precision == "bf16" else torch.float32
         self.gradient_accumulation_steps = gradient_accumulation_steps

@@ -6,7 +6,7 @@ GPU, sets the step time.  ``GraphedStep`` captures forward + backward (+ the gra
 global-norm clip + AdamW + zero_grad with ``torch.cuda.graph`` and then replays it: one or two host calls per step.
 
 Data parallel (an engine with a gradient reducer, parallel/reducer.py) is graphed in one of three schedules
-(``comm``; default ``DLLM_GRAPH_COMM``, else "overlap" when the reducer overlaps, "split" with ``--no-overlap``):
+(``comm``; default ops/routing.py ``graph_comm``, else "overlap" when the reducer overlaps, "split" with ``--no-overlap``):
 
 * ``"overlap"`` (default): the forward + backward is captured as a CHAIN of graph segments cut at the reducer's bucket
   boundaries.  During the capture of the synchronised pass the reducer counts gradient readiness exactly as in an
@@ -57,6 +57,7 @@ import os
 import torch
 
 from ..ops import rng as rng_mod
+from ..ops import routing
 
 COMM_MODES = ("overlap", "split", "capture")
 
@@ -74,7 +75,7 @@ class GraphedStep:
         self.eng = engine
         self.red = engine.reducer
         default = "overlap" if (self.red is not None and self.red.overlap and self.red.dp) else "split"
-        self.comm = (comm or os.environ.get("DLLM_GRAPH_COMM", default)) if self.red is not None else None
+        self.comm = (comm or routing.get("graph_comm") or default) if self.red is not None else None
         if self.comm == "overlap" and not (self.red.overlap and self.red.dp):
             self.comm = "split"  # no readiness hooks (--no-overlap) or nothing to reduce: post-backward buckets
         if self.comm is not None and self.comm not in COMM_MODES:
@@ -412,7 +413,7 @@ class StepRunner:
         sched = None
         if red is not None and self.policy != "off":
             default = "overlap" if (red.overlap and red.dp) else "split"
-            sched = self.comm or os.environ.get("DLLM_GRAPH_COMM", default)
+            sched = self.comm or routing.get("graph_comm") or default
             if sched == "overlap" and not (red.overlap and red.dp):
                 sched = "split"
         rep.update(graph_policy=self.policy, graph_schedule=sched,

@@ -83,7 +83,7 @@ class TrainingArguments:
     # of 8 because its GPUs lack memory; a 288 GB MI355X holds the whole group, and one pass of 128 runs ~2x the
     # samples/s of 16 launch-bound passes of 8 (profiles/r2_entry_points.md).  "auto": as many micro-batches per pass
     # as the first step's measured activation memory allows within coalesce_memory_fraction of the device (GPU only);
-    # an int caps the samples per pass (0 / 1: off).  env DLLM_COALESCE_GA overrides.
+    # an int caps the samples per pass (0 / 1: off).
     coalesce_grad_accum: str | int = "auto"
     coalesce_memory_fraction: float = 0.6
     report_to: list = field(default_factory=list)
@@ -156,7 +156,7 @@ class Trainer:
         """Max padded tokens (samples x padded sequence lengths, _padded_tokens) per forward/backward pass when coalescing
         micro-batches; None = off, -1 = decide after step 1.  An explicit integer setting counts micro-batches of the
         configured batch size at the first group's padded lengths."""
-        v = os.environ.get("DLLM_COALESCE_GA", self.args.coalesce_grad_accum)
+        v = self.args.coalesce_grad_accum
         if self.cp_group is not None or self.args.gradient_accumulation_steps <= 1:
             return None
         if str(v) == "auto":

@@ -5,8 +5,8 @@ default heuristic picks are 5-30 % off the best solution for this model family's
 (K = 768 / 1024 with 10^4-10^5 rows), so the best solution per (op, M, N, K) measured on MI355X is
 recorded in ``configs/tunableop/<arch>.csv`` and replayed (tuning off) at start-up.  The CSV carries
 validator lines (torch / HIP / hipBLASLt / rocBLAS versions, gfx arch); TunableOp ignores the table if
-they do not match the running stack.  ``DLLM_TUNABLEOP=0`` disables; ``DLLM_TUNABLEOP=tune`` re-tunes
-unseen shapes and writes them to the per-process file (merge with tools/merge_tunableop.py).
+they do not match the running stack.  ``DLLM_TUNABLEOP=0`` disables; ``DLLM_TUNABLEOP=tune[:<dir>]`` re-tunes
+unseen shapes and writes them to the per-process file (in <dir>; merge with tools/merge_tunableop.py).
 """
 from __future__ import annotations
 
@@ -17,14 +17,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 
 
 def enable(device_index: int = 0, arch: str = "gfx950") -> str | None:
-    mode = os.environ.get("DLLM_TUNABLEOP", "1")
+    mode, _, tune_dir = os.environ.get("DLLM_TUNABLEOP", "1").partition(":")  # "tune:<dir>": results written there
     if mode == "0" or "PYTORCH_TUNABLEOP_ENABLED" in os.environ:
         return None
     # DLLM_TUNABLEOP_TABLE: another table (A/B of a re-tuned table against the shipped one)
     src = os.environ.get("DLLM_TUNABLEOP_TABLE") or os.path.join(ROOT, "configs", "tunableop", f"{arch}.csv")
     if not os.path.exists(src):
         return None
-    d = os.environ.get("DLLM_TUNABLEOP_DIR") or tempfile.mkdtemp(prefix="dllm_tunableop_")
+    d = tune_dir or tempfile.mkdtemp(prefix="dllm_tunableop_")
     os.makedirs(d, exist_ok=True)
     # every rank gets its own copy of the shared table (TunableOp may append to it)
     dst = os.path.join(d, f"tunableop_results{device_index}.csv")

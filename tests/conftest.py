@@ -9,9 +9,9 @@ if ROOT not in sys.path:
 os.environ.setdefault("TRANSFORMERS_NO_ADVISORY_WARNINGS", "true")
 os.environ.setdefault("HF_HUB_OFFLINE", "1")
 os.environ.setdefault("TRANSFORMERS_OFFLINE", "1")
-# the tests' small shapes run the fused FFN kernels (in production FFNs of <= 1024 token rows go unfused, ops/ffn.py
-# _FUSED_MIN_ROWS; tests/test_model_gpu.py::test_small_ffn_runs_unfused_by_default covers that routing)
-os.environ.setdefault("DLLM_FUSED_FFN_MIN_ROWS", "0")
+# the tests' small shapes run the fused FFN kernels (in production FFNs of <= 1024 token rows go unfused, ops/routing.py
+# ffn_min_rows; tests/test_model_gpu.py::test_small_ffn_runs_unfused_by_default covers that routing)
+os.environ.setdefault("DLLM_ROUTE", "ffn_min_rows=0")
 
 
 def pytest_configure(config):

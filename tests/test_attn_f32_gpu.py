@@ -75,7 +75,7 @@ def test_attn_f32_matches_fp64(B, Sq, Sk, H, scale, causal, use_kpm, bias, p):
 
 
 def test_attn_f32_kernel_runs_not_composite(monkeypatch):
-    """fp32 attention on the GPU goes to csrc/attn_f32.hip (the O(S^2) composite only with DLLM_ATTN_F32=0)."""
+    """fp32 attention on the GPU goes to csrc/attn_f32.hip (the O(S^2) composite only with routing attn_f32=0)."""
     from distributed_llms_example_amd import _ext
     from distributed_llms_example_amd.ops import attention as A
     calls = []

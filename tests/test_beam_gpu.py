@@ -64,7 +64,7 @@ def test_generation_fused_beam_step_matches_composite(monkeypatch):
     am = torch.ones_like(ids)
     outs = []
     for flag in ("0", "1"):
-        monkeypatch.setenv("DLLM_GEN_FUSED_BEAM", flag)
+        monkeypatch.setenv("DLLM_ROUTE", f"gen_fused_beam={flag}")
         outs.append(m.generate(ids, attention_mask=am, max_length=24, num_beams=2, no_repeat_ngram_size=3,
                                min_length=5))
     assert _ext.native() is not None

@@ -153,7 +153,7 @@ def test_chunked_attention_matches_full():
 
 @pytest.mark.parametrize("name", ["t5-tiny", "umt5-tiny"])
 def test_t5_long_sequence_chunked_encoder(monkeypatch, name):
-    """Above DLLM_ATTN_CHUNK_MIN tokens the T5 encoder runs chunked attention: same loss and gradients."""
+    """Above ops/routing.py attn_chunk_min tokens the T5 encoder runs chunked attention: same loss and gradients."""
     from distributed_llms_example_amd.models import build_model
     torch.manual_seed(0)
     model = build_model(name).eval()
@@ -166,8 +166,7 @@ def test_t5_long_sequence_chunked_encoder(monkeypatch, name):
     ref.loss.backward()
     g_ref = [p.grad.clone() for p in model.parameters()]
     model.zero_grad(set_to_none=True)
-    monkeypatch.setenv("DLLM_ATTN_CHUNK", "8")
-    monkeypatch.setenv("DLLM_ATTN_CHUNK_MIN", "16")
+    monkeypatch.setenv("DLLM_ROUTE", "attn_chunk=8,attn_chunk_min=16")
     out = model(input_ids=ids, attention_mask=mask, labels=lab)
     out.loss.backward()
     assert float(out.loss) == pytest.approx(float(ref.loss), rel=1e-5)
@@ -190,8 +189,7 @@ def test_chunked_attention_ragged_length():
 
 def test_long_sequence_chunk_prime_lengths(monkeypatch):
     from distributed_llms_example_amd.parallel.context import long_sequence_chunk
-    monkeypatch.delenv("DLLM_ATTN_CHUNK", raising=False)
-    monkeypatch.delenv("DLLM_ATTN_CHUNK_MIN", raising=False)
+    monkeypatch.delenv("DLLM_ROUTE", raising=False)
     for n in (9001, 10007, 8200, 16384, 32768, 65521):
         c = long_sequence_chunk(n, rows=64)
         blocks = -(-n // c)

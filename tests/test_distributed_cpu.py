@@ -70,7 +70,7 @@ def _grad_case(rank, world, overlap=True, ga=1, bucket_mb=0.05, native=None):
             for p in model.parameters():
                 p.add_(1.0)
     if native is not None:
-        os.environ["DLLM_NATIVE_REDUCER"] = "1" if native else "0"
+        os.environ["DLLM_ROUTE"] = "reducer=native" if native else "reducer=python"
     eng = TrainEngine(model, env, lr=1e-3, dtype=torch.float32, bucket_mb=bucket_mb, overlap=overlap)
     if native:
         assert eng.reducer.native is not None
@@ -139,7 +139,7 @@ def _rebuild_case(rank, world, native):
     from distributed_llms_example_amd.models import build_model
     from distributed_llms_example_amd.parallel.env import DistEnv
     from distributed_llms_example_amd.train.engine import TrainEngine
-    os.environ["DLLM_NATIVE_REDUCER"] = "1" if native else "0"
+    os.environ["DLLM_ROUTE"] = "reducer=native" if native else "reducer=python"
     torch.manual_seed(0)
     model = build_model("t5-tiny")
     env = DistEnv(rank=rank, world_size=world, backend="gloo", device=torch.device("cpu"))
@@ -246,7 +246,7 @@ def _debug_steps(rank, world, native):
     from distributed_llms_example_amd.parallel.env import DistEnv
     from distributed_llms_example_amd.train.engine import TrainEngine, token_count
     assert dist.get_debug_level() == dist.DebugLevel.DETAIL
-    os.environ["DLLM_NATIVE_REDUCER"] = "1" if native else "0"
+    os.environ["DLLM_ROUTE"] = "reducer=native" if native else "reducer=python"
     torch.manual_seed(0)
     model = build_model("t5-tiny")
     env = DistEnv(rank=rank, world_size=world, backend="gloo", device=torch.device("cpu"))
@@ -352,7 +352,7 @@ def _split_schedule_case(rank, world, native=True, ga=2, steps=3, comm="split", 
     from distributed_llms_example_amd.parallel.env import DistEnv
     from distributed_llms_example_amd.train.engine import TrainEngine
     from distributed_llms_example_amd.train.graph import GraphedStep
-    os.environ["DLLM_NATIVE_REDUCER"] = "1" if native else "0"
+    os.environ["DLLM_ROUTE"] = "reducer=native" if native else "reducer=python"
     env = DistEnv(rank=rank, world_size=world, backend="gloo", device=torch.device("cpu"))
     g = torch.Generator().manual_seed(7 + rank)
     data = [{"input_ids": torch.randint(3, 500, (2, 12), generator=g), "attention_mask": torch.ones(2, 12, dtype=torch.long),
@@ -421,7 +421,7 @@ def _wire_case(rank, world, native, wire):
     from distributed_llms_example_amd.models import build_model
     from distributed_llms_example_amd.parallel.env import DistEnv
     from distributed_llms_example_amd.train.engine import TrainEngine
-    os.environ["DLLM_NATIVE_REDUCER"] = "1" if native else "0"
+    os.environ["DLLM_ROUTE"] = "reducer=native" if native else "reducer=python"
     torch.manual_seed(0)
     env = DistEnv(rank=rank, world_size=world, backend="gloo", device=torch.device("cpu"))
     eng = TrainEngine(build_model("t5-tiny"), env, lr=1e-3, dtype=torch.float32, bucket_mb=0.05, grad_reduce_dtype=wire)
@@ -564,7 +564,7 @@ def _defer_last_big_case(rank, world, native=True, defer=True):
     from distributed_llms_example_amd.models import build_model
     from distributed_llms_example_amd.parallel.env import DistEnv
     from distributed_llms_example_amd.train.engine import TrainEngine
-    os.environ["DLLM_NATIVE_REDUCER"] = "1" if native else "0"
+    os.environ["DLLM_ROUTE"] = "reducer=native" if native else "reducer=python"
     env = DistEnv(rank=rank, world_size=world, backend="gloo", device=torch.device("cpu"))
     torch.manual_seed(0)
     eng = TrainEngine(build_model("t5-tiny"), env, lr=1e-3, dtype=torch.float32, bucket_mb=0.05, overlap=True)

@@ -195,13 +195,13 @@ def test_gemm_w4_gelu_backward_colsum(M, d, F_):
                                                  (768, 768, 8192, False), (1024, 1024, 65536, False),
                                                  (3072, 1024, 131072, False)])
 def test_default_dgrad_routing(N_out, K_in, M, routed):
-    """Default DLLM_W4_GEMM=dgrad768 (ops/gemm.py): a projection's input gradient dX = dY W runs on gemm_w4 when the
+    """Default route (ops/routing.py proj_dgrad = narrow): a projection's input gradient dX = dY W runs on gemm_w4 when the
     layer is at most 768 features wide and has >= 64K token rows (t5-base's o / qkv at large batch; 2304-deep only with
     >= 128K rows), on hipBLASLt for wider layers (t5-large / bart-large) and micro-batches, and the forward always on
     hipBLASLt; either way it matches fp32."""
-    from distributed_llms_example_amd.ops import gemm
-    if gemm._W4_MODE != "dgrad768":
-        pytest.skip(f"DLLM_W4_GEMM={gemm._W4_MODE} set in the environment")
+    from distributed_llms_example_amd.ops import gemm, routing
+    if any(k.startswith("proj_") for k in routing.overrides()):
+        pytest.skip(f"DLLM_ROUTE={routing.overrides()} set in the environment")
     torch.manual_seed(N_out + K_in)
     dy = torch.randn(M, N_out, device=DEV).to(torch.bfloat16)
     w = (torch.randn(N_out, K_in, device=DEV) * N_out ** -0.5).to(torch.bfloat16)

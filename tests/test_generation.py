@@ -52,7 +52,7 @@ def test_no_repeat_ngram_and_min_length():
 @pytest.mark.parametrize("beams,early,lp,ngram,minlen", [
     (2, False, 1.0, 0, 0), (3, True, 2.0, 3, 4), (4, "never", 0.5, 2, 0), (2, False, 1.0, 0, 6)])
 def test_device_beam_search_matches_host_loop(name, beams, early, lp, ngram, minlen, monkeypatch):
-    """Device-side beam bookkeeping == the per-step host loop (DLLM_GEN_HOST=1) on an eos-heavy model, so finished
+    """Device-side beam bookkeeping == the per-step host loop (routing gen_host=1) on an eos-heavy model, so finished
     hypotheses, the stopping rule and the finalize path are all exercised."""
     torch.manual_seed(0)
     m = build_model(name).eval()
@@ -69,9 +69,9 @@ def test_device_beam_search_matches_host_loop(name, beams, early, lp, ngram, min
     ids = torch.randint(4, m.config.vocab_size, (4, 15), generator=g)
     kw = dict(max_length=16, num_beams=beams, min_length=minlen, no_repeat_ngram_size=ngram, length_penalty=lp,
               early_stopping=early)
-    monkeypatch.setenv("DLLM_GEN_CHECK_EVERY", "3")
+    monkeypatch.setenv("DLLM_ROUTE", "gen_check_every=3")
     a = m.generate(ids, **kw)
-    monkeypatch.setenv("DLLM_GEN_HOST", "1")
+    monkeypatch.setenv("DLLM_ROUTE", "gen_check_every=3,gen_host=1")
     b = m.generate(ids, **kw)
     assert torch.equal(a, b), (a, b)
     assert int((a == eos).sum()) >= 2
@@ -81,8 +81,8 @@ def test_greedy_trims_steps_after_all_done(monkeypatch):
     torch.manual_seed(0)
     m = build_model("bart-tiny").eval()
     ids = torch.randint(4, 500, (2, 9), generator=torch.Generator().manual_seed(3))
-    monkeypatch.setenv("DLLM_GEN_CHECK_EVERY", "1")
+    monkeypatch.setenv("DLLM_ROUTE", "gen_check_every=1")
     a = m.generate(ids, max_length=20, num_beams=1)
-    monkeypatch.setenv("DLLM_GEN_CHECK_EVERY", "7")
+    monkeypatch.setenv("DLLM_ROUTE", "gen_check_every=7")
     b = m.generate(ids, max_length=20, num_beams=1)
     assert torch.equal(a, b)

@@ -252,8 +252,8 @@ def test_lm_head_chunked_ce_matches_fp32(bias, smooth, V, fused, monkeypatch):
     from distributed_llms_example_amd.ops import lm_head as LH
     from distributed_llms_example_amd.ops.lm_head import lm_head_loss
     from distributed_llms_example_amd.parallel.flat import FlatParams
-    monkeypatch.setenv("DLLM_LMHEAD_CHUNK_MB", "8")  # several chunks, ragged last one
-    monkeypatch.setenv("DLLM_LMHEAD_FUSED", fused)
+    # several chunks, ragged last one; fused "1": the GEMM-epilogue CE, "0": vocabulary chunks
+    monkeypatch.setenv("DLLM_ROUTE", "lmhead_chunk_mb=8,lmhead=" + ("fused" if fused == "1" else "logits"))
     torch.manual_seed(0)
     N, d = 1000, 768
     emb = torch.nn.Embedding(V, d).cuda().to(torch.bfloat16)
@@ -316,9 +316,8 @@ def test_t5_chunked_lm_head_matches_full(monkeypatch):
     sd = build_model(cfg).state_dict()
     b = _micro_batches(cfg, n=1, B=4)[0]
     res = []
-    monkeypatch.setenv("DLLM_LMHEAD_FUSED", "0")  # this test pins the vocab-chunked path against full logits
-    for full_mb in ("-1", "0"):
-        monkeypatch.setenv("DLLM_LMHEAD_FULL_MB", full_mb)
+    for full_mb in ("-1", "0"):  # this test pins the vocab-chunked path against full logits
+        monkeypatch.setenv("DLLM_ROUTE", f"lmhead=logits,lmhead_full_mb={full_mb}")
         eng = _engine(cfg, sd, torch.float32)
         loss = eng.forward_backward(b)
         res.append((float(loss), eng.flat.grad_buf.clone()))
@@ -333,10 +332,9 @@ def test_t5_fused_lm_head_matches_materialised_logits(monkeypatch):
     torch.manual_seed(0)
     sd = build_model(cfg).state_dict()
     b = _micro_batches(cfg, n=1, B=4)[0]
-    monkeypatch.setenv("DLLM_LMHEAD_FULL_MB", "-1")  # never chunked: "1" forces the fused path, "0" full logits
     res = []
-    for fused in ("1", "0"):
-        monkeypatch.setenv("DLLM_LMHEAD_FUSED", fused)
+    for fused in ("1", "0"):  # never chunked: "1" forces the fused path, "0" full logits
+        monkeypatch.setenv("DLLM_ROUTE", "lmhead_full_mb=-1,lmhead=" + ("fused" if fused == "1" else "logits"))
         eng = _engine(cfg, sd, torch.float32)
         eng.train(False)
         loss = eng.forward_backward(b)
@@ -360,7 +358,7 @@ def test_side_stream_wgrad_matches_single_stream(graphed, sites, monkeypatch):
     mbs = _micro_batches(cfg, n=2, B=2)
     res = []
     for on in ("1", "0"):  # "1": forced on (the default "auto" enables it for small micro-batches only)
-        monkeypatch.setenv("DLLM_WGRAD_STREAM", on)
+        monkeypatch.setenv("DLLM_ROUTE", f"wgrad_stream={on}")
         eng = _engine(cfg, sd, torch.float32)
         eng.train(False)
         n0 = streams.launches
@@ -392,7 +390,7 @@ def test_bart_attention_bias_colsum_matches_column_reduction(sq_force, monkeypat
     from distributed_llms_example_amd.ops import attention as A
     from distributed_llms_example_amd.ops import gemm as G
     from distributed_llms_example_amd.ops.linear import _gbuf
-    monkeypatch.setenv("DLLM_ATTN_DKDV_SQ_FORCE", sq_force)
+    monkeypatch.setenv("DLLM_ROUTE", f"attn_dkdv_sq_force={sq_force}")
     cfg = resolve_config("bart-large").replace(num_layers=2, num_decoder_layers=2, vocab_size=4096, d_model=512,
                                                num_heads=8, d_ff=1024, dropout_rate=0.0, attention_dropout=0.0)
     torch.manual_seed(0)
@@ -454,7 +452,7 @@ def test_deferred_weight_gradients_gpu(model, monkeypatch):
     res = []
     for mode in ("1", "0"):
         monkeypatch.setenv("DLLM_DEFER_WGRAD", mode)
-        monkeypatch.setenv("DLLM_WGRAD_STREAM", "1")
+        monkeypatch.setenv("DLLM_ROUTE", "wgrad_stream=1")
         eng = _engine(cfg, sd, torch.float32)
         eng.train(False)
         for i, b in enumerate(mbs):

@@ -186,7 +186,7 @@ ATTN_CASES = [
 def test_attention(B, H, Sq, Sk, bias, kpm, causal, p, scale, monkeypatch):
     # short-query cross-attention: the dK/dV kernel that walks several key blocks per workgroup, which the launcher
     # otherwise keeps for launches that still fill the chip (csrc/attn.hip attn_bwd_dkdv_sq_kernel)
-    monkeypatch.setenv("DLLM_ATTN_DKDV_SQ_FORCE", "1")
+    monkeypatch.setenv("DLLM_ROUTE", "attn_dkdv_sq_force=1")
     torch.manual_seed(Sq * 7 + Sk)
     D = 64
     q = torch.randn(B, Sq, H, D, device=DEV).to(torch.bfloat16)
@@ -349,9 +349,8 @@ def test_attention_prefetched_dropout_planes_match(monkeypatch):
     g = torch.randn(B, S, H, D, device=DEV).to(torch.bfloat16)
     outs = []
     for use_pre in (False, True):
-        monkeypatch.setenv("DLLM_ATTN_MASK_STREAM", "1" if use_pre else "0")
         x = qkv.clone().requires_grad_(True)
-        pre = A.prefetch_dropout_mask(x, B, H, S, S, p, seed)
+        pre = A.prefetch_dropout_mask(x, B, H, S, S, p, seed) if use_pre else None
         assert (pre is not None) == use_pre
         o = A.attention_qkv(x, pre=pre, scale=0.125, dropout_p=p, seed=seed)
         o.backward(g)
@@ -440,8 +439,8 @@ def test_gemm_fused_short_k(variant, K):
 
 @pytest.mark.parametrize("grp", [1, 2, 3, 4, 8])
 def test_gemm_pp_tile_order_groups(grp, monkeypatch):
-    """Grouped tile order of the ping-pong kernel (DLLM_GEMM_GRP), including a last group shorter than grp."""
-    monkeypatch.setenv("DLLM_GEMM_GRP", str(grp))
+    """Grouped tile order of the ping-pong kernel (routing gemm_grp), including a last group shorter than grp."""
+    monkeypatch.setenv("DLLM_ROUTE", f"gemm_grp={grp}")
     torch.manual_seed(3)
     M, K, N = 1280, 256, 768
     C = _ext.native()

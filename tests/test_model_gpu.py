@@ -167,20 +167,19 @@ def test_engine_steps_reduce_loss_on_gpu():
 @pytest.mark.parametrize("name", ["t5-base", "t5-base:w4", "bart-base", "flan-t5-base"])
 def test_fused_ffn_matches_unfused_in_engine(name, monkeypatch):
     """TrainEngine (FlatParams: the FFN runs as GEMMs with activation/dropout epilogues, ops/ffn.py) vs the same
-    step with DLLM_FUSED_FFN=0 (library GEMMs + activation kernels): same loss, same dropout masks, and the fused
+    step with the routing table's ffn=unfused (library GEMMs + activation kernels): same loss, same dropout masks, and the fused
     gradient no further from the fp32 torch reference step (same bf16-representable weights) than the unfused one —
     two bf16 paths differ by bf16 noise, so their mutual cosine alone is not a sharp test."""
-    from distributed_llms_example_amd.ops import ffn as ffn_mod
+    from distributed_llms_example_amd.ops import ffn as ffn_mod, routing
     from distributed_llms_example_amd.ops.rng import manual_seed
     from distributed_llms_example_amd.parallel.env import init_distributed
     from distributed_llms_example_amd.train.engine import TrainEngine
     env = init_distributed()
     w4 = name.endswith(":w4")  # the T5 ReLU FFN forward on csrc/gemm_w4.hip (default only from 64K token rows up)
     name = name.split(":")[0]
-    monkeypatch.setattr(ffn_mod, "_W4_FFN_MIN_ROWS", 0 if w4 else 1 << 62)
+    # small shapes: force the fused gated path as well
+    base = routing.merged(ffn_w4_min_rows=0 if w4 else 1 << 62, gated_min_mf=0, gated_max_d=1 << 30)
     cfg = _cfg(name)
-    monkeypatch.setattr(ffn_mod, "_GATED_MIN_MF", 0)  # small shapes: force the fused gated path as well
-    monkeypatch.setattr(ffn_mod, "_GATED_MAX_D", 1 << 30)
     torch.manual_seed(0)
     sd = {k: v.to(torch.bfloat16).float() for k, v in build_model(cfg).state_dict().items()}
     w4_before = ffn_mod.w4_ffn_calls
@@ -196,7 +195,7 @@ def test_fused_ffn_matches_unfused_in_engine(name, monkeypatch):
     monkeypatch.delenv("DLLM_REFERENCE_OPS")
     res = []
     for flag in ("0", "1"):
-        monkeypatch.setenv("DLLM_FUSED_FFN", flag)
+        monkeypatch.setenv("DLLM_ROUTE", base + ",ffn=" + ("fused" if flag == "1" else "unfused"))
         m = build_model(cfg)
         m.load_state_dict(sd)
         eng = TrainEngine(m, env, lr=1e-4, dtype=torch.bfloat16)
@@ -219,13 +218,13 @@ def test_fused_ffn_matches_unfused_in_engine(name, monkeypatch):
 
 
 def test_small_ffn_runs_unfused_by_default(monkeypatch):
-    """Production default (ops/ffn.py _FUSED_MIN_ROWS = 1025): in the engine, FFNs of <= 1024 token rows run unfused
+    """Production default (ops/routing.py ffn_min_rows = 1025): in the engine, FFNs of <= 1024 token rows run unfused
     (library GEMMs + activation kernel) and larger ones on the fused kernels.  Encoder 4 x 512 = 2048 rows, decoder
     4 x 64 = 256 rows: one fused FFN per encoder layer, none in the decoder; the step stays finite."""
     from distributed_llms_example_amd.ops import ffn as ffn_mod
     from distributed_llms_example_amd.parallel.env import init_distributed
     from distributed_llms_example_amd.train.engine import TrainEngine
-    monkeypatch.setattr(ffn_mod, "_FUSED_MIN_ROWS", 1025)
+    monkeypatch.setenv("DLLM_ROUTE", "ffn_min_rows=1025")
     env = init_distributed()
     cfg = _cfg("t5-base")
     torch.manual_seed(0)
@@ -252,7 +251,6 @@ def test_bart_residual_grad_in_dgrad_gemm(monkeypatch):
     res = []
     for flag in (False, True):
         monkeypatch.setattr(lin_mod, "_RES_GEMM", flag)
-        monkeypatch.setattr(ffn_mod, "_RES_GEMM", flag)
         m = build_model(cfg)
         m.load_state_dict(sd)
         eng = TrainEngine(m, env, lr=1e-4, dtype=torch.bfloat16)

@@ -62,7 +62,7 @@ def run(B, H, Sq, Sk, bias, kpm, causal, p, iters=20, sat=True):
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true")
-    ap.add_argument("--ab", action="store_true", help="repeat the bias cases 3x, forward saturated tiles off/on")
+    ap.add_argument("--ab", action="store_true", help="repeat every case 3x")
     a = ap.parse_args()
     cases = [(32, 12, 1024, 1024, True, True, False, 0.1), (32, 12, 1024, 1024, True, True, False, 0.0),
              (32, 12, 1024, 1024, False, False, False, 0.0), (32, 12, 128, 128, True, False, True, 0.1),
@@ -71,13 +71,5 @@ if __name__ == "__main__":
         cases = cases[:1]
     ap2 = a
     for c in cases:
-        if c[4]:  # bias cases: forward scalar-bias tiles off / on, interleaved 3x (A/B in one process)
-            for rep in range(3 if ap2.ab else 1):
-                for fsat in ("0", "1"):
-                    os.environ["DLLM_ATTN_FWD_SAT"] = fsat
-                    r = run(*c)
-                    r["fwd_sat"] = fsat == "1"
-                    print(json.dumps(r), flush=True)
-            os.environ["DLLM_ATTN_FWD_SAT"] = "0"
-        else:
+        for rep in range(3 if ap2.ab else 1):
             print(json.dumps(run(*c)), flush=True)

@@ -1,7 +1,7 @@
 """Eval-generation throughput: ``generate(num_beams=2, max_length=128)`` over 818 SAMSum-test-shaped samples
 (ref/train-accelerator.py:239-249).  Modes: ``fused`` = device-side beam bookkeeping with the one-kernel beam step
-(csrc/beam.hip), ``device`` = the same with the torch composite step (DLLM_GEN_FUSED_BEAM=0), ``host`` = the per-step
-host loop (DLLM_GEN_HOST=1).
+(csrc/beam.hip), ``device`` = the same with the torch composite step (DLLM_ROUTE gen_fused_beam=0), ``host`` = the
+per-step host loop (gen_host=1).
 
     python tools/eval_bench.py [--model t5-base] [--batch 64] [--src-len 512] [--n 818] [--modes fused,device,host]
 Synthetic prompts (random ids, ragged attention masks) and random-init weights; prints one JSON line per mode.
@@ -36,8 +36,8 @@ def main():
     lens = torch.randint(a.src_len // 4, a.src_len + 1, (a.n,), generator=g)
     am = (torch.arange(a.src_len)[None, :] < lens[:, None]).long()
     for mode in a.modes.split(","):
-        os.environ["DLLM_GEN_HOST"] = "1" if mode == "host" else "0"
-        os.environ["DLLM_GEN_FUSED_BEAM"] = "1" if mode == "fused" else "0"
+        os.environ["DLLM_ROUTE"] = (f"gen_host={1 if mode == 'host' else 0},"
+                                    f"gen_fused_beam={1 if mode == 'fused' else 0}")
         m.generate(ids[:a.batch].cuda(), attention_mask=am[:a.batch].cuda(), max_length=8, num_beams=a.beams)
         torch.cuda.synchronize()
         t0 = time.perf_counter()

@@ -36,7 +36,7 @@ def main():
     a = ap.parse_args()
     tunableop.enable(0)
     C = _ext.native()
-    # a variant "8g4" runs variant 8 with DLLM_GEMM_GRP=4 (tile-order group size, read per call by the binding)
+    # a variant "8g4" runs variant 8 with DLLM_ROUTE gemm_grp=4 (tile-order group size, read per call by the binding)
     variants = a.variants.split(",")
     # (name, tokens M, in K, out N): t5-base at b=64 (enc 65536 tokens, dec 8192), bart-large at b=32
     shapes = [("t5b enc qkv", 65536, 768, 2304), ("t5b enc o", 65536, 768, 768), ("t5b enc wi", 65536, 768, 3072),
@@ -67,7 +67,7 @@ def main():
                 for vi, v in enumerate(variants):
                     tag = f"v{v}" + ("b" * variants[:vi].count(v))  # a repeated variant (A/B/A order) gets its own key
                     vv, _, grp = v.partition("g")
-                    os.environ["DLLM_GEMM_GRP"] = grp or "0"
+                    os.environ["DLLM_ROUTE"] = f"gemm_grp={grp or 0}"
                     fn = mk(int(vv))
                     out = fn().float()
                     rec[f"{tag}_relerr"] = float(f"{((out - ref).norm() / ref.norm()).item():.2e}")

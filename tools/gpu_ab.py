@@ -5,7 +5,7 @@ Replaces the per-experiment lease scripts of rounds 1-4.  Run on the GPU box (th
 
     python tools/gpu_ab.py --tag r5a --tests "tests/test_kernels_gpu.py -k attn" \
         --bench "--steps 12 --warmup 3" --arms base=ab/base.so,new=distributed_llms_example_amd/_C*.so --reps 3 \
-        --env-arms "w4off=DLLM_W4_GEMM=0,w4on=DLLM_W4_GEMM=1" --prof "--steps 2 --warmup 1 --graph off"
+        --env-arms "lib=DLLM_ROUTE=proj_dgrad=lib,w4=DLLM_ROUTE=proj_dgrad=w4" --prof "--steps 2 --warmup 1 --graph off"
 
 Steps, each under its own time limit; the session stops at the first failure (a GPU fault, a time limit, an abort):
 

@@ -1,7 +1,6 @@
 """Fused residual + dropout + RMSNorm kernels (csrc/norm.hip) at the t5-base b=512 shapes: time and HBM rate.
 
-    python tools/norm_bench.py            # one process per DLLM_NORM_BWD_G value (the cap is read once per process)
-    python tools/norm_bench.py --one      # this process's setting only
+    python tools/norm_bench.py            # the t5-base b=512 shapes
     python tools/norm_bench.py --rows 4096,1024 --partials   # micro-batch shapes of a deferred GA window
 
 Bytes counted: forward reads x + resid, writes out + s; backward reads dout + ds_extra + s, writes dx + dstream.
@@ -9,7 +8,6 @@ Bytes counted: forward reads x + resid, writes out + s; backward reads dout + ds
 import argparse
 import json
 import os
-import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -32,7 +30,7 @@ def one(rows_list, d, reps, partials=False):
         o, s, mean, rstd = fwd()
         bwd = lambda: C.norm_bwd(dout, dse, s, w, None, mean, rstd, 0.1, 7, 0, True, None, None,
                                  partials_only=partials)
-        res = {"N": N, "d": d, "G": int(os.environ.get("DLLM_NORM_BWD_G", "512")), "partials_only": partials}
+        res = {"N": N, "d": d, "G": 512, "partials_only": partials}
         for name, fn, nbytes in (("fwd", fwd, 4 * N * d * 2), ("bwd", bwd, 5 * N * d * 2)):
             for _ in range(3):
                 fn()
@@ -53,23 +51,13 @@ def one(rows_list, d, reps, partials=False):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--one", action="store_true")
     ap.add_argument("--rows", default="524288,65536")
     ap.add_argument("--d", type=int, default=768)
     ap.add_argument("--reps", type=int, default=20)
-    ap.add_argument("--grids", default="256,512,1024,2048")
     ap.add_argument("--partials", action="store_true", help="backward keeps the per-block dw partials (deferred GA)")
     a = ap.parse_args()
     rows = [int(v) for v in a.rows.split(",")]
-    if a.one:
-        one(rows, a.d, a.reps, a.partials)
-        return
-    for gv in a.grids.split(","):
-        env = dict(os.environ, DLLM_NORM_BWD_G=gv)
-        r = subprocess.run([sys.executable, __file__, "--one", "--rows", a.rows, "--d", str(a.d), "--reps",
-                            str(a.reps)] + (["--partials"] if a.partials else []), env=env)
-        if r.returncode != 0:
-            sys.exit(r.returncode)
+    one(rows, a.d, a.reps, a.partials)
 
 
 if __name__ == "__main__":

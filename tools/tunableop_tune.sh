@@ -10,7 +10,7 @@ mkdir -p $O
 HB=$!
 trap "kill $HB" EXIT
 echo "[tune] tuning run"
-DLLM_TUNABLEOP=tune DLLM_TUNABLEOP_DIR=$O PYTORCH_TUNABLEOP_MAX_TUNING_DURATION_MS=${TUNE_MS:-40} PYTORCH_TUNABLEOP_VERBOSE=0 \
+DLLM_TUNABLEOP=tune:$O PYTORCH_TUNABLEOP_MAX_TUNING_DURATION_MS=${TUNE_MS:-40} PYTORCH_TUNABLEOP_VERBOSE=0 \
   timeout -k 10 ${TUNE_TIMEOUT:-1000} python -u bench.py --steps 1 --warmup 1 --graph off "$@" > $O/tune.log 2>&1 || { tail -20 $O/tune.log; exit 1; }
 tail -2 $O/tune.log | cut -c1-200
 python tools/merge_tunableop.py configs/tunableop/gfx950.csv $O/tunableop_results0.csv -o $O/merged.csv
