@@ -886,7 +886,7 @@ int launch_rs(const GemmW4Params& p, bool persist, hipStream_t st) {
 template <bool BKM, bool BIAS, bool ACC>
 int launch(const GemmW4Params& p, bool persist, hipStream_t st) {
   const char* e = getenv("DLLM_W4_RS");
-  const int rs = e ? atoi(e) : 1;  // default: early fragment reads (1-8 % faster on the routed dgrads)
+  const int rs = e ? atoi(e) : 257;  // default: early fragment reads, DMAs riding on MFMAs
   if constexpr (!BKM && !BIAS && !ACC) {
     switch (rs) {
       case 16: return launch_rs<BKM, BIAS, ACC, 16>(p, persist, st);
@@ -918,7 +918,7 @@ int dispatch(const GemmW4Params& p, bool persist, hipStream_t st) {
 extern "C" int dllm_gemm_w4(const GemmW4Params* pp, int b_kmajor, int persist, int epi, hipStream_t st) {
   const GemmW4Params& p = *pp;
   const char* rs_env = getenv("DLLM_W4_RS");
-  const bool il = rs_env != nullptr && (atoi(rs_env) & 256) != 0;
+  const bool il = rs_env == nullptr || (atoi(rs_env) & 256) != 0;
   // N % 8: 16-B C stores (CEF stores no C: any N)
   if (p.M <= 0 || p.N <= 0 || p.K <= 0 || p.K % BK || (p.N % 8 && epi != W4_EPI_CEF) || p.tm * 256 < p.M ||
       p.tn * 256 < p.N)

@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--batch", type=int, default=128)
     a = ap.parse_args()
     C = _ext.native()
+    assert C is not None, f"native extension not loaded: {_ext.load_error()}"
     T = 1024 * a.batch
     r = lambda *s: torch.randn(*s, device="cuda").to(torch.bfloat16)  # noqa: E731
     x768, w2304, w768, wi, wo = r(T, 768), r(2304, 768) * 0.03, r(768, 768) * 0.03, r(3072, 768) * 0.03, r(768, 3072) * 0.02
