@@ -35,6 +35,7 @@
 
 #include "gelu.h"
 #include "gemm_params.h"
+#include "route.h"
 
 using namespace dllm;
 
@@ -881,12 +882,12 @@ int launch_rs(const GemmW4Params& p, bool persist, hipStream_t st) {
   return 0;
 }
 
-// DLLM_W4_RS: fragment read schedule (kernel template RS), read per call so microbenchmarks can A/B it in one process;
+// DLLM_ROUTE w4_sched (kernel template RS; ops/routing.py), read per call so microbenchmarks can A/B it in one process;
 // the ablation values (bits 4..7) exist for the plain forward only
 template <bool BKM, bool BIAS, bool ACC>
 int launch(const GemmW4Params& p, bool persist, hipStream_t st) {
-  const char* e = getenv("DLLM_W4_RS");
-  const int rs = e ? atoi(e) : 257;  // default: early fragment reads, DMAs riding on MFMAs
+  // default 257: early fragment reads, DMAs riding on MFMAs (profiles/r6_w4_dma_interleave_ab.txt)
+  const int rs = route_int("w4_sched", 257);
   if constexpr (!BKM && !BIAS && !ACC) {
     switch (rs) {
       case 16: return launch_rs<BKM, BIAS, ACC, 16>(p, persist, st);
@@ -917,8 +918,7 @@ int dispatch(const GemmW4Params& p, bool persist, hipStream_t st) {
 // epi: W4_EPI_NONE, W4_EPI_RELU (NT, optional bias, no accumulate), W4_EPI_DRELU_M (NN, no bias, no accumulate)
 extern "C" int dllm_gemm_w4(const GemmW4Params* pp, int b_kmajor, int persist, int epi, hipStream_t st) {
   const GemmW4Params& p = *pp;
-  const char* rs_env = getenv("DLLM_W4_RS");
-  const bool il = rs_env == nullptr || (atoi(rs_env) & 256) != 0;
+  const bool il = (route_int("w4_sched", 257) & 256) != 0;
   // N % 8: 16-B C stores (CEF stores no C: any N)
   if (p.M <= 0 || p.N <= 0 || p.K <= 0 || p.K % BK || (p.N % 8 && epi != W4_EPI_CEF) || p.tm * 256 < p.M ||
       p.tn * 256 < p.N)

@@ -82,7 +82,7 @@ def main():
                 if k != "lib":
                     rec[f"{k}_relerr"] = float(f"{((fn().float() - ref).norm() / ref.norm()).item():.2e}")
             rsv = {"w4rs1": "1", "w4direct": "3"}
-            arms["w4rs1"] = arms["w4"]  # same call, DLLM_W4_RS=1 (early fragment reads), set per arm below
+            arms["w4rs1"] = arms["w4"]  # same call, w4_sched=1 (early fragment reads), set per arm below
             arms["w4direct"] = arms["w4"]  # RS=3: early reads, unstaged epilogue stores
             if a.ablate and phase == "fwd":
                 for tag, v in (("nodma", "16"), ("noread", "32"), ("nobar", "64"), ("nostore", "128"),
@@ -92,9 +92,9 @@ def main():
             times = {k: [] for k in arms}
             for _ in range(a.rounds):
                 for k, fn in arms.items():
-                    os.environ["DLLM_W4_RS"] = rsv.get(k, "0")
+                    os.environ["DLLM_ROUTE"] = "w4_sched=" + rsv.get(k, "0")
                     times[k].append(timeit(fn, a.iters))
-            os.environ["DLLM_W4_RS"] = "0"
+            os.environ.pop("DLLM_ROUTE", None)
             for k, ts in times.items():
                 t = statistics.median(ts)
                 rec[f"{k}_us"] = round(t * 1e6, 1)

@@ -1,4 +1,4 @@
-"""A/B of two csrc/gemm_w4.hip k-loop schedules (DLLM_W4_RS, read per launch) on every mode the t5-base b=512 step
+"""A/B of two csrc/gemm_w4.hip k-loop schedules (DLLM_ROUTE w4_sched, read per launch) on every mode the t5-base b=512 step
 runs: NT forward, NN input gradient, weight gradient (split-K), ReLU FFN forward (bit mask) and its backward.
 Interleaved rounds in one process, median, random operands (cdna_hip_programming.md §5.4 rules 24-25).
 
@@ -60,9 +60,9 @@ def main():
     for name, (_, fn) in cases.items():
         if name.startswith("wgrad"):
             continue
-        os.environ["DLLM_W4_RS"] = a.rs_a
+        os.environ["DLLM_ROUTE"] = "w4_sched=" + a.rs_a
         ra = fn().clone()
-        os.environ["DLLM_W4_RS"] = a.rs_b
+        os.environ["DLLM_ROUTE"] = "w4_sched=" + a.rs_b
         rb = fn().clone()
         assert torch.equal(ra, rb), f"{name}: schedules disagree"
     print(f"# w4 schedules RS={a.rs_a} (A) vs RS={a.rs_b} (B), tokens {T}, median of {a.rounds} interleaved rounds; "
@@ -72,7 +72,7 @@ def main():
         ts = {"A": [], "B": []}
         for _ in range(a.rounds):
             for arm, rs in (("A", a.rs_a), ("B", a.rs_b)):
-                os.environ["DLLM_W4_RS"] = rs
+                os.environ["DLLM_ROUTE"] = "w4_sched=" + rs
                 ts[arm].append(timeit(fn, a.iters))
         ma, mb = statistics.median(ts["A"]), statistics.median(ts["B"])
         tot["A"] += ma
