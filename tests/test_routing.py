@@ -82,7 +82,7 @@ def test_step_launches_what_the_plan_says(monkeypatch):
     # rows); decoder rows (8K) too few for the 64K-row floor
     assert gemm_mod.w4_calls - w4_0 >= cfg.num_layers, gemm_mod.w4_calls - w4_0
     assert ffn_mod.w4_ffn_calls - ffn_0 == cfg.num_layers  # encoder ReLU FFNs on w4; decoder (8K rows) ping-pong
-    names = " ".join(e.name for e in prof.key_averages())
+    names = " ".join(e.key for e in prof.key_averages())
     for fam in ("gemm_w4_kernel", "gemm_pp_kernel", "attn_fwd_kernel", "attn_bwd_dq_kernel", "attn_bwd_dkdv2_kernel",
                 "norm_fwd_kernel", "norm_bwd_kernel", "adamw8_kernel", "splitk_reduce_kernel"):
         assert fam in names, (fam, names[:2000])
