@@ -149,9 +149,15 @@ def _torch_profile(step, path: str, top: int = 60) -> None:
     """One extra (untimed) eager step under torch.profiler: device time per (kernel, Python call site), so the small
     ATen kernels in a rocprofv3 summary can be traced to the op that launched them.  Env DLLM_TORCH_PROFILE=<file>."""
     from torch.profiler import ProfilerActivity, profile
-    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True, record_shapes=True) as prof:
         step(0)
         torch.cuda.synchronize()
+    # library GEMMs by operand shapes (which projections still run on hipBLASLt, and at what rate)
+    gemms = []
+    for e in prof.key_averages(group_by_input_shape=True):
+        if e.key in ("aten::mm", "aten::addmm", "aten::addmm_", "aten::bmm") and e.self_device_time_total > 0:
+            gemms.append((e.self_device_time_total, e.count, e.key, str(e.input_shapes)[:120]))
+    gemms.sort(reverse=True)
     rows = prof.key_averages(group_by_stack_n=6).table(sort_by="self_cuda_time_total", row_limit=top,
                                                        max_name_column_width=70)
     # ATen ops with their Python call sites (the rows above group by stack but do not print it)
@@ -166,6 +172,9 @@ def _torch_profile(step, path: str, top: int = 60) -> None:
         f.write("\n# ATen ops by call site: self device us, calls, op, stack\n")
         for us, n, k, st in sites[:top]:
             f.write(f"{us:10.1f} {n:6d} {k:28s} {st}\n")
+        f.write("\n# library GEMMs by input shapes: self device us, calls, op, shapes\n")
+        for us, n, k, sh in gemms[:top]:
+            f.write(f"{us:10.1f} {n:6d} {k:16s} {sh}\n")
 
 
 def check_rank_consistency(env, eng, model_name: str, batch: int):
