@@ -78,21 +78,25 @@ def main():
                     arms["pp9"] = lambda: C.gemm_fused(dy, w, True, 0, None, None, None, 0.0, 0, 9)
             ref = arms["lib"]().float()
             rec = {"shape": name, "phase": phase, "M": M, "K": K if phase == "fwd" else N, "N": N if phase == "fwd" else K}
-            for k, fn in arms.items():
-                if k != "lib":
-                    rec[f"{k}_relerr"] = float(f"{((fn().float() - ref).norm() / ref.norm()).item():.2e}")
-            rsv = {"w4rs1": "1", "w4direct": "3"}
-            arms["w4rs1"] = arms["w4"]  # same call, w4_sched=1 (early fragment reads), set per arm below
-            arms["w4direct"] = arms["w4"]  # RS=3: early reads, unstaged epilogue stores
+            # the same call under other w4_sched values (csrc/gemm_w4.hip RS), set per arm below: "w4" / "w4np" run the
+            # default (257); rs1 = the round-5 schedule
+            rsv = {"w4": "257", "w4np": "257", "w4rs1": "1"}
+            for k in ("w4rs1",):
+                arms[k] = arms["w4"]
+            arms.pop("pp9", None)
             if a.ablate and phase == "fwd":
                 for tag, v in (("nodma", "16"), ("noread", "32"), ("nobar", "64"), ("nostore", "128"),
                                ("mfmaonly", "112")):
                     arms["abl_" + tag] = arms["w4"]
                     rsv["abl_" + tag] = v
+            for k, fn in arms.items():
+                if k != "lib" and not k.startswith("abl_"):
+                    os.environ["DLLM_ROUTE"] = "w4_sched=" + rsv.get(k, "257")
+                    rec[f"{k}_relerr"] = float(f"{((fn().float() - ref).norm() / ref.norm()).item():.2e}")
             times = {k: [] for k in arms}
             for _ in range(a.rounds):
                 for k, fn in arms.items():
-                    os.environ["DLLM_ROUTE"] = "w4_sched=" + rsv.get(k, "0")
+                    os.environ["DLLM_ROUTE"] = "w4_sched=" + rsv.get(k, "257")
                     times[k].append(timeit(fn, a.iters))
             os.environ.pop("DLLM_ROUTE", None)
             for k, ts in times.items():
