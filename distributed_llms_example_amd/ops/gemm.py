@@ -4,7 +4,9 @@ Who runs what (t5-base / bart-large training step, default settings):
 
 * weight gradients ``dW (+)= dYᵀ X`` (wgrad_accumulate): csrc/gemm_w4.hip's weight-gradient mode (both operands
   token-major, K split over workgroups, fp32 split slabs summed into the flat gradient buffer by csrc/gemm.hip's
-  split-K pass; round 5, 2-8 % faster than the csrc/gemm.hip kernel it replaced);
+  split-K pass; round 5, 2-8 % faster than the csrc/gemm.hip kernel it replaced) from routing ``wgrad_min_rows``
+  (4096) token rows; below that hipBLASLt (fp32 addmm): a 256x256-tile kernel has ~23 us of fixed cost there, 2-4x
+  the library's time at the reference's batch-1 shapes (profiles/r6_wgrad_small_rows.txt);
 * the FFN input GEMMs with their activation / dropout epilogues and the FFN backward through the activation
   (ops/ffn.py): csrc/gemm_fused.hip and csrc/gemm_w4.hip;
 * the PLAIN projections — forward ``Y = X Wᵀ (+ b)`` of the attention q/k/v/o and FFN output layers, and the LM
@@ -126,7 +128,7 @@ class WgradDefer:
                 raise RuntimeError("deferred weight-gradient operand modified in place (a writer must check holds())")
         dys, xs = [p[0] for p in parts], [p[1] for p in parts]
         d0, x0 = dys[0], xs[0]
-        if (_native_ok(d0, x0, out)
+        if (d0.shape[0] * len(dys) >= routing.get("wgrad_min_rows") and _native_ok(d0, x0, out)
                 and all(d.shape == d0.shape and d.stride() == d0.stride() for d in dys)
                 and all(x.shape == x0.shape and x.stride() == x0.stride() for x in xs)):
             C = _ext.native()
@@ -226,10 +228,12 @@ def wgrad_accumulate(out: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, bet
 
 
 def _wgrad(out, dy2, x2, beta):
-    if _native_ok(dy2, x2, out):
+    if dy2.shape[0] >= routing.get("wgrad_min_rows") and _native_ok(dy2, x2, out):
         _ext.native().gemm_wgrad(dy2, x2, out, beta, -1, 0)
         return out
     if out.dtype != dy2.dtype:  # fp32 gradient buffer, bf16 operands: the product itself in fp32, then one fp32 add
+        if dy2.is_cuda and beta:  # accumulated in the GEMM (fp32 C, bf16 operands)
+            return torch.addmm(out, dy2.t(), x2, out_dtype=out.dtype, out=out)
         if dy2.is_cuda:
             g = torch.mm(dy2.t(), x2, out_dtype=out.dtype)  # fp32 output from bf16 operands (no bf16 rounding)
         else:

@@ -8,8 +8,10 @@ step launches is decided in one place and can be read off the table below; ``pla
 op (key)                       default route                                                 evidence (profiles/)
 =============================  ===========================================================  =============================
 weight gradient dW = dYᵀX      csrc/gemm_w4.hip weight-gradient mode (K split over           r5_wgrad_w4_ab.txt
-                               workgroups, fp32 slabs + csrc/gemm.hip split-K pass);
-                               deferred over a GA window (ops/gemm.py WgradDefer)            r5_defer_wgrad_ab.txt
+                               workgroups, fp32 slabs + csrc/gemm.hip split-K pass) from
+                               ``wgrad_min_rows`` (4096) token rows; hipBLASLt below (a       r6_wgrad_small_rows.txt
+                               256x256-tile kernel has ~23 us of fixed cost); deferred over
+                               a GA window (ops/gemm.py WgradDefer)                          r5_defer_wgrad_ab.txt
 projection forward             hipBLASLt + TunableOp table (``proj_fwd`` = lib); w4 ties     r5_gemm_half_tile_ab.txt,
 Y = X Wᵀ (+ b)                 it in isolation and lost 0.8-1.1 % in the step                r5_w4route_colsum_ab.txt
 projection input gradient      w4 when the layer's input is <= ``proj_dgrad_max_n`` (768)    r5_w4_dgrad768_ab.txt
@@ -58,6 +60,8 @@ DEFAULTS: dict = {
     "proj_dgrad": "narrow",       # narrow | w4 | lib
     "proj_dgrad_max_n": 768,
     "proj_dgrad_min_rows": 65536,
+    # weight gradients (ops/gemm.py): w4 weight-gradient mode from this many token rows, hipBLASLt (fp32 addmm) below
+    "wgrad_min_rows": 4096,
     # feed-forward blocks (ops/ffn.py)
     "ffn": "fused",               # fused | unfused
     "ffn_min_rows": 1025,
@@ -140,9 +144,10 @@ def plan(model: str, tokens_enc: int, tokens_dec: int, d_model: int, d_ff: int, 
     """What the table routes for one training step of an encoder-decoder model with these shapes (per micro-batch
     token rows): a dict op -> kernel family, as the tests and docs/ARCHITECTURE.md read it."""
     rows = {"enc": tokens_enc, "dec": tokens_dec}
-    out = {"wgrad": "w4-wgrad"}
+    out = {}
     narrow = get("proj_dgrad")
     for side, r in rows.items():
+        out[f"{side}.wgrad"] = "w4-wgrad" if r >= get("wgrad_min_rows") else "hipblaslt"
         out[f"{side}.proj_fwd"] = "w4" if get("proj_fwd") == "w4" else "hipblaslt"
         if narrow == "w4":
             dg = "w4"

@@ -11,7 +11,7 @@ os.environ.setdefault("HF_HUB_OFFLINE", "1")
 os.environ.setdefault("TRANSFORMERS_OFFLINE", "1")
 # the tests' small shapes run the fused FFN kernels (in production FFNs of <= 1024 token rows go unfused, ops/routing.py
 # ffn_min_rows; tests/test_model_gpu.py::test_small_ffn_runs_unfused_by_default covers that routing)
-os.environ.setdefault("DLLM_ROUTE", "ffn_min_rows=0")
+os.environ.setdefault("DLLM_ROUTE", "ffn_min_rows=0,wgrad_min_rows=0")
 
 
 def pytest_configure(config):

@@ -805,3 +805,22 @@ def test_chunked_attention_8k_blocks_vs_fp32(p):
     (ref * g).sum().backward()
     for name, x, y in zip(("dq", "dk", "dv", "dtable"), a + [t1], [qf, kf, vf, tab]):
         assert _rel(x.grad, y.grad) < 5e-2, (name, _rel(x.grad, y.grad))
+
+
+@pytest.mark.parametrize("rows,native", [(1024, False), (4096, True)])
+def test_wgrad_small_rows_route(rows, native, monkeypatch):
+    """routing wgrad_min_rows (default 4096): below it the weight gradient is the library's fp32 addmm into the fp32
+    gradient (accumulated, beta); from it the w4 weight-gradient mode.  Both equal the fp64 product."""
+    from distributed_llms_example_amd.ops import gemm as gemm_mod
+    monkeypatch.setenv("DLLM_ROUTE", "wgrad_min_rows=4096")
+    torch.manual_seed(7)
+    dy = torch.randn(rows, 768, device=DEV, dtype=torch.bfloat16)
+    x = torch.randn(rows, 512, device=DEV, dtype=torch.bfloat16)
+    g0 = torch.randn(768, 512, device=DEV, dtype=torch.float32)
+    g = g0.clone()
+    calls = []
+    monkeypatch.setattr(gemm_mod, "_native_ok", lambda *a: calls.append(1) or True)
+    gemm_mod._wgrad(g, dy, x, True)
+    assert (len(calls) > 0) == native
+    ref = g0.double() + dy.double().t() @ x.double()
+    assert _rel(g, ref) < 1e-5, _rel(g, ref)

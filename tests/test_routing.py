@@ -27,9 +27,12 @@ def test_route_overrides_parse_and_fail_loudly(monkeypatch):
 PLANS = [
     (("t5-base b512", 512 * 1024, 512 * 128, 768, 3072, "relu", 32128),
      {"enc.proj_fwd": "hipblaslt", "enc.proj_dgrad": "w4", "dec.proj_dgrad": "w4", "enc.ffn": "w4-relu",
-      "dec.ffn": "w4-relu", "lm_head": "hipblaslt+ce", "wgrad": "w4-wgrad"}),
+      "dec.ffn": "w4-relu", "lm_head": "hipblaslt+ce", "enc.wgrad": "w4-wgrad", "dec.wgrad": "w4-wgrad"}),
     (("t5-base b8", 8 * 1024, 8 * 128, 768, 3072, "relu", 32128),
-     {"enc.proj_dgrad": "hipblaslt", "enc.ffn": "pingpong-relu+w4-drelu", "dec.ffn": "hipblaslt+act"}),
+     {"enc.proj_dgrad": "hipblaslt", "enc.ffn": "pingpong-relu+w4-drelu", "dec.ffn": "hipblaslt+act",
+      "enc.wgrad": "w4-wgrad", "dec.wgrad": "hipblaslt"}),
+    (("t5-base b1 (train-accelerator)", 1024, 128, 768, 3072, "relu", 32128),
+     {"enc.wgrad": "hipblaslt", "dec.wgrad": "hipblaslt", "enc.ffn": "hipblaslt+act"}),
     (("bart-large b256", 256 * 1024, 256 * 128, 1024, 4096, "gelu", 50265),
      {"enc.proj_dgrad": "hipblaslt", "enc.ffn": "pingpong-gelu", "dec.ffn": "pingpong-gelu"}),
     (("t5-large b32", 32 * 1024, 32 * 128, 1024, 4096, "relu", 32128),
@@ -41,6 +44,7 @@ PLANS = [
 
 @pytest.mark.parametrize("args,expect", PLANS, ids=[p[0][0] for p in PLANS])
 def test_route_plan_for_baseline_configs(args, expect, monkeypatch):
+    """Run with the table's defaults (the test session's conftest override is removed)."""
     monkeypatch.delenv("DLLM_ROUTE", raising=False)
     plan = routing.plan(*args)
     for k, v in expect.items():
