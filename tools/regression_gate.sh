@@ -20,7 +20,11 @@ exec_args=(
 )
 # GATE_SMALL=1: also the reference's small micro-batch / long-target shapes (train-torchrun: batch 1 x GA 16, BART
 # 1024 / 1024)
-if [ "${GATE_SMALL:-0}" = 1 ]; then
+# GATE_SMALL=only: the small shapes alone (the two halves fit one gpurun call each)
+if [ "${GATE_SMALL:-0}" = only ]; then
+  exec_args=(--tag "$TAG" --tree-arms "base=$BASE,cur=." --reps "$REPS" --bench-limit 480)
+fi
+if [ "${GATE_SMALL:-0}" != 0 ]; then
   exec_args+=(
     --bench "--model bart-large --src-len 1024 --tgt-len 1024 --batch-per-gpu 64 --steps 5 --warmup 2"
     --bench "--batch-per-gpu 8 --grad-accum 16 --steps 6 --warmup 2"
