@@ -167,6 +167,15 @@ DLLM_DEVICE void mfma_dma(f32x4& c, const bf16x8v& b, const bf16x8v& a, const i3
                : "v"(b), "v"(a), "v"(voff), "s"(srd), "s"(ldsb), "i"(IMM), "s"(soff)
                : "memory", "m0", "scc");
 }
+// the first k-step's form of mfma_dma (C input 0)
+template <uint32_t IMM>
+DLLM_DEVICE void mfma0_dma(f32x4& c, const bf16x8v& b, const bf16x8v& a, const i32x4& srd, uint32_t voff, uint32_t soff,
+                           uint32_t ldsb) {
+  asm volatile("s_add_u32 m0, %5, %6\n\tv_mfma_f32_16x16x32_bf16 %0, %1, %2, 0\n\tbuffer_load_dwordx4 %3, %4, %7 offen lds"
+               : "=a"(c)
+               : "v"(b), "v"(a), "v"(voff), "s"(srd), "s"(ldsb), "i"(IMM), "s"(soff)
+               : "memory", "m0", "scc");
+}
 DLLM_DEVICE void mfma_v(f32x4& c, const bf16x8v& b, const bf16x8v& a) {
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(b), "v"(a));
 }
@@ -176,6 +185,9 @@ DLLM_DEVICE void mfma_v(f32x4& c, const bf16x8v& b, const bf16x8v& a) {
 // RS bit 1 = direct epilogue stores from the accumulator layout instead of the LDS-staged whole-row stores (A/B).
 // RS bits 4..7 = ABLATIONS for timing studies only (results are garbage): 16 no k-loop DMAs, 32 no k-loop fragment
 // reads, 64 no k-loop wait + barrier, 128 no epilogue stores (tools/gemm_w4_bench.py --ablate)
+// RS bit 9 = buffer b released half-way through sub-step 0 (lgkmcnt(0) + a second barrier): the DMA of k-tile g+2 starts
+// there, 8 pieces on sub-step 0's last 32 MFMAs and 8 on sub-step 1's, and sub-step 1's wait keeps those 8 in flight
+// (vmcnt(8)) — the DMA issue spread over 88 MFMAs instead of 56 (-4.8 % summed kernel time, bit-identical outputs)
 // RS bit 8 = k-loop DMAs fused into MFMAs (mfma_dma: M0 formed early, one DMA every few MFMAs) instead of 2-3 DMA
 // statements back to back after each chunk
 template <bool BKM, bool BIAS, bool ACC, int RS, int EPI = W4_EPI_NONE>
@@ -298,6 +310,12 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
     else mfma_dma<TB + (uint32_t)(d - 8) * 1024u>(c, b, a, q.sb, vb[d - 8], q.sob, q.ldsb);
   };
 
+  auto mfma_dma0_d = [&](f32x4& c, const bf16x8v& b, const bf16x8v& a, const Dma& q, auto D) {
+    constexpr int d = decltype(D)::value;
+    if constexpr (d < 8) mfma0_dma<(uint32_t)d * 1024u>(c, b, a, q.sa, va[d], q.soa, q.ldsb);
+    else mfma0_dma<TB + (uint32_t)(d - 8) * 1024u>(c, b, a, q.sb, vb[d - 8], q.sob, q.ldsb);
+  };
+
   // ---- fragment reads.  Row image: a[i] = rows wm*128 + 16 i + (l & 15), k chunk kk/8 + (l >> 4), swizzled by
   // ((row / 2) & 7), which does not depend on i: one base offset per 32-deep half, +2 KB per i.
   const int rl = lane & 15, qd = lane >> 4;
@@ -393,12 +411,38 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
       asm volatile("s_nop 2" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
       const int b = g & 1;
+      // RS bit 9 (A/B): buffer b is released by a barrier half-way through sub-step 0 (every wave's reads of its k 32..63
+      // half returned), so the DMA of k-tile g+2 into it starts there: 8 of its 16 pieces ride on sub-step 0's last 32
+      // MFMAs, 8 on sub-step 1's (the DMA issue spread over 88 MFMAs instead of 56)
+      constexpr bool EARLY = (RS & 512) != 0;
+      Dma q;
       // sub-step 0 (k 0..31, fragments fa0 / fb0): read the k 32..63 fragments into fa1 / fb1, two per chunk, B first
       // (the next sub-step's first chunk needs all of B and a[0])
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        if (kt == 0) chunk0(fa0, fb0, i);
-        else chunk(fa0, fb0, i);
+      sfor<0, 8>([&](auto I) {
+        constexpr int i = decltype(I)::value;
+        if constexpr (EARLY && i >= 4) {
+          if constexpr (i == 4) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            __builtin_amdgcn_sched_barrier(0);
+            q = plan_next(ti, kt, b);
+          }
+          // DMAs 2 (i - 4), 2 (i - 4) + 1 on MFMAs 1 and 5 of the chunk
+          sfor<0, 8>([&](auto J) {
+            constexpr int j = decltype(J)::value;
+            constexpr int d = 2 * (i - 4) + (j == 5 ? 1 : 0);
+            if (kt == 0) {
+              if constexpr (j == 1 || j == 5) mfma_dma0_d(acc[i][j], fb0[j], fa0[i], q, std::integral_constant<int, d>{});
+              else mfma0(acc[i][j], fb0[j], fa0[i]);
+            } else {
+              if constexpr (j == 1 || j == 5) mfma_dma_d(acc[i][j], fb0[j], fa0[i], q, std::integral_constant<int, d>{});
+              else mfma_v(acc[i][j], fb0[j], fa0[i]);
+            }
+          });
+        } else {
+          if (kt == 0) chunk0(fa0, fb0, i);
+          else chunk(fa0, fb0, i);
+        }
         if constexpr ((RS & 32) != 0) {
         } else if constexpr ((RS & 1) == 0) {
           if (i < 4) {
@@ -418,13 +462,24 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
           }
         }
         __builtin_amdgcn_sched_barrier(0);
-      }
+      });
       // sub-step 1 (k 32..63, fa1 / fb1).  After its first chunk: k-tile g+1 landed (its DMA was the last issued; after
       // an epilogue its 32 stores are queued behind it) and every wave is past its reads of buffer b -> barrier; then
       // DMA k-tile g+2 into buffer b and read k-tile g+1's first half into fa0 / fb0, spread over the remaining 7 chunks
       chunk(fa1, fb1, 0);
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr ((RS & 64) == 0) {
+      if constexpr (EARLY) {
+        // k-tile g+1 landed: everything but the 8 pieces of g+2 issued in sub-step 0 retired (after an epilogue its 32
+        // C stores are queued between them; modes whose epilogues issue other counts drain everything there)
+        if (kt == 0 && g > 0) {
+          if constexpr (!ACC && EPI != W4_EPI_CEF && EPI != W4_EPI_WG && EPI != W4_EPI_GELU && EPI != W4_EPI_DGELU)
+            asm volatile("s_waitcnt vmcnt(40) lgkmcnt(0)" ::: "memory");
+          else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        } else {
+          asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_s_barrier();
+      } else if constexpr ((RS & 64) == 0) {
         // after an epilogue its 32 C stores are the youngest VMEM ops (CEF stores fewer: drain everything)
         if (kt == 0 && g > 0 && !ACC && EPI != W4_EPI_CEF && EPI != W4_EPI_WG && EPI != W4_EPI_GELU &&
             EPI != W4_EPI_DGELU)
@@ -433,11 +488,13 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
         __builtin_amdgcn_s_barrier();
       }
       __builtin_amdgcn_sched_barrier(0);
-      const Dma q = plan_next(ti, kt, b);
+      if constexpr (!EARLY) q = plan_next(ti, kt, b);
       sfor<1, 8>([&](auto I) {
         constexpr int i = decltype(I)::value;
-        // DMA: instructions 0..7 of A then of B, spread over chunks 1..7 (2, 2, 2, 3, 2, 2, 3)
-        constexpr int d0 = (i - 1) * 16 / 7, d1 = i * 16 / 7;
+        // DMA: instructions 0..7 of A then of B, spread over chunks 1..7 (2, 2, 2, 3, 2, 2, 3); EARLY: the remaining 8
+        // (8..15), one per chunk and two in chunk 5
+        constexpr int d0 = EARLY ? 8 + (i - 1) + (i > 5 ? 1 : 0) : (i - 1) * 16 / 7;
+        constexpr int d1 = EARLY ? 8 + i + (i >= 5 ? 1 : 0) : i * 16 / 7;
         if constexpr ((RS & 256) != 0 && (RS & 16) == 0) {
           // DMA k of the chunk's n rides on MFMA 1 + 7 k / n (1, 4 or 1, 3, 5)
           sfor<0, 8>([&](auto J) {
@@ -886,8 +943,9 @@ int launch_rs(const GemmW4Params& p, bool persist, hipStream_t st) {
 // the ablation values (bits 4..7) exist for the plain forward only
 template <bool BKM, bool BIAS, bool ACC>
 int launch(const GemmW4Params& p, bool persist, hipStream_t st) {
-  // default 257: early fragment reads, DMAs riding on MFMAs (profiles/r6_w4_dma_interleave_ab.txt)
-  const int rs = route_int("w4_sched", 257);
+  // default 769: early fragment reads, DMAs riding on MFMAs (profiles/r6_w4_dma_interleave_ab.txt), buffer released
+  // half-way through sub-step 0 (profiles/r6_w4_early_release_ab.txt)
+  const int rs = route_int("w4_sched", 769);
   if constexpr (!BKM && !BIAS && !ACC) {
     switch (rs) {
       case 16: return launch_rs<BKM, BIAS, ACC, 16>(p, persist, st);
@@ -898,7 +956,7 @@ int launch(const GemmW4Params& p, bool persist, hipStream_t st) {
       default: break;
     }
   }
-  if (rs & 256) return launch_rs<BKM, BIAS, ACC, 257>(p, persist, st);
+  if (rs & 256) return (rs & 512) ? launch_rs<BKM, BIAS, ACC, 769>(p, persist, st) : launch_rs<BKM, BIAS, ACC, 257>(p, persist, st);
   switch (rs & 3) {  // bit 1: direct (unstaged) epilogue stores, for A/B
     case 0: return launch_rs<BKM, BIAS, ACC, 0>(p, persist, st);
     case 2: return launch_rs<BKM, BIAS, ACC, 2>(p, persist, st);
@@ -918,13 +976,17 @@ int dispatch(const GemmW4Params& p, bool persist, hipStream_t st) {
 // epi: W4_EPI_NONE, W4_EPI_RELU (NT, optional bias, no accumulate), W4_EPI_DRELU_M (NN, no bias, no accumulate)
 extern "C" int dllm_gemm_w4(const GemmW4Params* pp, int b_kmajor, int persist, int epi, hipStream_t st) {
   const GemmW4Params& p = *pp;
-  const bool il = (route_int("w4_sched", 257) & 256) != 0;
+  const int rsb = route_int("w4_sched", 769);
+  const bool il = (rsb & 256) != 0, early = il && (rsb & 512) != 0;
   // N % 8: 16-B C stores (CEF stores no C: any N)
   if (p.M <= 0 || p.N <= 0 || p.K <= 0 || p.K % BK || (p.N % 8 && epi != W4_EPI_CEF) || p.tm * 256 < p.M ||
       p.tn * 256 < p.N)
     return -4;
   if (epi == W4_EPI_RELU) {
     if (b_kmajor || p.accumulate || p.mask == nullptr) return -5;
+    if (early)
+      return p.bias ? launch_rs<false, true, false, 769, W4_EPI_RELU>(p, persist != 0, st)
+                    : launch_rs<false, false, false, 769, W4_EPI_RELU>(p, persist != 0, st);
     if (il)
       return p.bias ? launch_rs<false, true, false, 257, W4_EPI_RELU>(p, persist != 0, st)
                     : launch_rs<false, false, false, 257, W4_EPI_RELU>(p, persist != 0, st);
@@ -933,6 +995,7 @@ extern "C" int dllm_gemm_w4(const GemmW4Params* pp, int b_kmajor, int persist, i
   }
   if (epi == W4_EPI_DRELU_M) {
     if (!b_kmajor || p.accumulate || p.bias || p.mask == nullptr) return -5;
+    if (early) return launch_rs<true, false, false, 769, W4_EPI_DRELU_M>(p, persist != 0, st);
     if (il) return launch_rs<true, false, false, 257, W4_EPI_DRELU_M>(p, persist != 0, st);
     return launch_rs<true, false, false, 1, W4_EPI_DRELU_M>(p, persist != 0, st);
   }
@@ -974,6 +1037,7 @@ extern "C" int dllm_gemm_w4(const GemmW4Params* pp, int b_kmajor, int persist, i
     // every split's k-major descriptors (k-rows x leading dimension) must fit their 32-bit byte range
     const long span = ((long)(p.kchunk - 1) * std::max(p.lda, p.ldb) + std::max(p.M, p.N)) * 2;
     if (span >= 0xFFFFFFFFL) return -6;
+    if (early) return launch_rs<true, false, false, 769, W4_EPI_WG>(p, false, st);
     if (il) return launch_rs<true, false, false, 257, W4_EPI_WG>(p, false, st);
     return launch_rs<true, false, false, 1, W4_EPI_WG>(p, false, st);
   }

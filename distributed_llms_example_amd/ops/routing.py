@@ -97,9 +97,10 @@ DEFAULTS: dict = {
     # dK/dV kernel on any launch size
     "gemm_grp": 4,
     "attn_dkdv_sq_force": 0,
-    # csrc/gemm_w4.hip k-loop schedule (template RS): 257 = early fragment reads + DMAs riding on MFMAs (default),
-    # 1 = the round-5 schedule; bits 16-128 = timing ablations (tools/gemm_w4_bench.py --ablate; results garbage)
-    "w4_sched": 257,
+    # csrc/gemm_w4.hip k-loop schedule (template RS): 769 = early fragment reads + DMAs riding on MFMAs + the LDS buffer
+    # released half-way through sub-step 0 so the next DMA spreads over 88 MFMAs (default); 257 = without the early
+    # release, 1 = the round-5 schedule; bits 16-128 = timing ablations (tools/gemm_w4_bench.py --ablate; garbage)
+    "w4_sched": 769,
 }
 
 _cache: tuple[str, dict] | None = None

@@ -79,9 +79,10 @@ def main():
             ref = arms["lib"]().float()
             rec = {"shape": name, "phase": phase, "M": M, "K": K if phase == "fwd" else N, "N": N if phase == "fwd" else K}
             # the same call under other w4_sched values (csrc/gemm_w4.hip RS), set per arm below: "w4" / "w4np" run the
-            # default (257); rs1 = the round-5 schedule
-            rsv = {"w4": "257", "w4np": "257", "w4rs1": "1"}
-            for k in ("w4rs1",):
+            # default; rs1 = the round-5 schedule
+            # (769: + the early buffer release; 257: without it)
+            rsv = {"w4": "769", "w4np": "769", "w4rs1": "1", "w4il": "257"}
+            for k in ("w4rs1", "w4il"):
                 arms[k] = arms["w4"]
             arms.pop("pp9", None)
             if a.ablate and phase == "fwd":
@@ -91,12 +92,12 @@ def main():
                     rsv["abl_" + tag] = v
             for k, fn in arms.items():
                 if k != "lib" and not k.startswith("abl_"):
-                    os.environ["DLLM_ROUTE"] = "w4_sched=" + rsv.get(k, "257")
+                    os.environ["DLLM_ROUTE"] = "w4_sched=" + rsv.get(k, "769")
                     rec[f"{k}_relerr"] = float(f"{((fn().float() - ref).norm() / ref.norm()).item():.2e}")
             times = {k: [] for k in arms}
             for _ in range(a.rounds):
                 for k, fn in arms.items():
-                    os.environ["DLLM_ROUTE"] = "w4_sched=" + rsv.get(k, "257")
+                    os.environ["DLLM_ROUTE"] = "w4_sched=" + rsv.get(k, "769")
                     times[k].append(timeit(fn, a.iters))
             os.environ.pop("DLLM_ROUTE", None)
             for k, ts in times.items():
