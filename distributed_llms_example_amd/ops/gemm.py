@@ -12,9 +12,9 @@ Who runs what (t5-base / bart-large training step, default settings):
 * the PLAIN projections — forward ``Y = X Wᵀ (+ b)`` of the attention q/k/v/o and FFN output layers, and the LM
   head — go to the library (hipBLASLt through torch, with the TunableOp table in configs/tunableop/): csrc/gemm_w4.hip
   ties it on these shapes in isolation and lost 0.8 % of the step in situ (profiles/r3_w4_routing_ab.txt).  Their input
-  gradients ``dX (+)= dY W`` run on csrc/gemm_w4.hip where that measured faster in the step (layers at most 768
-  features wide, >= 64K token rows: t5-base at large batch), on hipBLASLt otherwise.  The choice is ops/routing.py's
-  table (``proj_fwd`` / ``proj_dgrad``).
+  gradients ``dX (+)= dY W`` run on csrc/gemm_w4.hip from 64K token rows at any layer width (its early-release schedule
+  beats the library on every such shape, profiles/r6_w4_early_release_ab.txt), on hipBLASLt below.  The choice is
+  ops/routing.py's table (``proj_fwd`` / ``proj_dgrad``).
 
 Weight-gradient GEMM notes:
 
@@ -34,9 +34,8 @@ import torch.nn.functional as F
 from .. import _ext
 from . import routing, streams
 
-# Routing of the projection GEMMs: ops/routing.py ("proj_fwd", "proj_dgrad" and thresholds; the evidence is cited
-# there).  Input gradients on w4 additionally need a reduction depth (the layer's output features) the kernel wins at:
-# <= 1024, <= 2304 with >= 128K token rows, or <= 3072 with >= 1024 output columns (profiles/r3_gemm_w4_grp_sweep.txt).
+# Routing of the projection GEMMs: ops/routing.py ("proj_fwd", "proj_dgrad" and its row threshold; the evidence is cited
+# there).
 w4_calls = 0  # projections that ran on csrc/gemm_w4.hip (tests assert the kernel really ran)
 colsum_handoffs = 0  # bias gradients taken from a norm backward's column sums (bias_grad_accumulate)
 
@@ -48,12 +47,8 @@ def _w4_ok(a: torch.Tensor, b: torch.Tensor, kmajor: bool) -> bool:
         mode = routing.get("proj_dgrad")
         if mode == "lib":
             return False
-        if mode == "narrow":
-            K = a.shape[-1]
-            if b.shape[-1] > routing.get("proj_dgrad_max_n") or a.shape[0] < routing.get("proj_dgrad_min_rows"):
-                return False
-            if not (K <= 1024 or (K <= 2304 and a.shape[0] >= 131072) or (K <= 3072 and b.shape[-1] >= 1024)):
-                return False
+        if mode == "rows" and a.shape[0] < routing.get("proj_dgrad_min_rows"):
+            return False
     elif routing.get("proj_fwd") != "w4":  # forwards
         return False
     return bool(_ext.native().gemm_w4_supported(a, b, kmajor))

@@ -12,11 +12,13 @@ weight gradient dW = dYᵀX      csrc/gemm_w4.hip weight-gradient mode (K split 
                                ``wgrad_min_rows`` (4096) token rows; hipBLASLt below (a       r6_wgrad_small_rows.txt
                                256x256-tile kernel has ~23 us of fixed cost); deferred over
                                a GA window (ops/gemm.py WgradDefer)                          r5_defer_wgrad_ab.txt
-projection forward             hipBLASLt + TunableOp table (``proj_fwd`` = lib); w4 ties     r5_gemm_half_tile_ab.txt,
-Y = X Wᵀ (+ b)                 it in isolation and lost 0.8-1.1 % in the step                r5_w4route_colsum_ab.txt
-projection input gradient      w4 when the layer's input is <= ``proj_dgrad_max_n`` (768)    r5_w4_dgrad768_ab.txt
-dX (+)= dY W                   wide and the GEMM has >= ``proj_dgrad_min_rows`` (64K) token
-                               rows; hipBLASLt otherwise (``proj_dgrad`` = narrow)
+projection forward             hipBLASLt + TunableOp table (``proj_fwd`` = lib); w4 is       r6_w4_early_release_ab.txt,
+Y = X Wᵀ (+ b)                 within -1.5..+7 % of it per shape (sum of t5-base forwards:    r5_w4route_colsum_ab.txt
+                               library ahead)
+projection input gradient      w4 from ``proj_dgrad_min_rows`` (64K) token rows at any       r6_w4_early_release_ab.txt,
+dX (+)= dY W                   width / depth (early-release schedule: faster than the         r6_dgrad_rows_ab.txt
+                               library on every such shape); hipBLASLt below (``proj_dgrad``
+                               = rows)
 FFN, ReLU (T5)                 forward: w4 ReLU + dropout + bit-mask epilogue from            r5_w4_relu_ffn_ab.txt,
                                ``ffn_w4_min_rows`` (64K) rows, ping-pong (csrc/gemm_fused)   r5_ffn_small_rows_ab.txt
                                below; backward: w4 through the bit mask; < ``ffn_min_rows``
@@ -57,8 +59,7 @@ import os
 DEFAULTS: dict = {
     # projection GEMMs (ops/gemm.py)
     "proj_fwd": "lib",            # lib | w4
-    "proj_dgrad": "narrow",       # narrow | w4 | lib
-    "proj_dgrad_max_n": 768,
+    "proj_dgrad": "rows",         # rows | w4 | lib
     "proj_dgrad_min_rows": 65536,
     # weight gradients (ops/gemm.py): w4 weight-gradient mode from this many token rows, hipBLASLt (fp32 addmm) below
     "wgrad_min_rows": 4096,
@@ -146,16 +147,16 @@ def plan(model: str, tokens_enc: int, tokens_dec: int, d_model: int, d_ff: int, 
     token rows): a dict op -> kernel family, as the tests and docs/ARCHITECTURE.md read it."""
     rows = {"enc": tokens_enc, "dec": tokens_dec}
     out = {}
-    narrow = get("proj_dgrad")
+    dmode = get("proj_dgrad")
     for side, r in rows.items():
         out[f"{side}.wgrad"] = "w4-wgrad" if r >= get("wgrad_min_rows") else "hipblaslt"
         out[f"{side}.proj_fwd"] = "w4" if get("proj_fwd") == "w4" else "hipblaslt"
-        if narrow == "w4":
+        if dmode == "w4":
             dg = "w4"
-        elif narrow == "lib":
+        elif dmode == "lib":
             dg = "hipblaslt"
         else:
-            dg = "w4" if d_model <= get("proj_dgrad_max_n") and r >= get("proj_dgrad_min_rows") else "hipblaslt"
+            dg = "w4" if r >= get("proj_dgrad_min_rows") else "hipblaslt"
         out[f"{side}.proj_dgrad"] = dg
         if get("ffn") != "fused" or r < get("ffn_min_rows"):
             out[f"{side}.ffn"] = "hipblaslt+act"

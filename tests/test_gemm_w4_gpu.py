@@ -192,13 +192,13 @@ def test_gemm_w4_gelu_backward_colsum(M, d, F_):
 
 
 @pytest.mark.parametrize("N_out,K_in,M,routed", [(768, 768, 65536, True), (2304, 768, 131072, True),
-                                                 (768, 768, 8192, False), (1024, 1024, 65536, False),
-                                                 (3072, 1024, 131072, False)])
+                                                 (768, 768, 8192, False), (1024, 1024, 65536, True),
+                                                 (3072, 1024, 131072, True), (3072, 768, 65536, True)])
 def test_default_dgrad_routing(N_out, K_in, M, routed):
-    """Default route (ops/routing.py proj_dgrad = narrow): a projection's input gradient dX = dY W runs on gemm_w4 when the
-    layer is at most 768 features wide and has >= 64K token rows (t5-base's o / qkv at large batch; 2304-deep only with
-    >= 128K rows), on hipBLASLt for wider layers (t5-large / bart-large) and micro-batches, and the forward always on
-    hipBLASLt; either way it matches fp32."""
+    """Default route (ops/routing.py proj_dgrad = rows): a projection's input gradient dX = dY W runs on gemm_w4 from 64K
+    token rows at any width and depth (the early-release schedule beats hipBLASLt on every such shape,
+    profiles/r6_w4_early_release_ab.txt), on hipBLASLt for micro-batches, and the forward always on hipBLASLt; either way
+    it matches fp32."""
     from distributed_llms_example_amd.ops import gemm, routing
     if any(k.startswith("proj_") for k in routing.overrides()):
         pytest.skip(f"DLLM_ROUTE={routing.overrides()} set in the environment")

@@ -34,7 +34,7 @@ PLANS = [
     (("t5-base b1 (train-accelerator)", 1024, 128, 768, 3072, "relu", 32128),
      {"enc.wgrad": "hipblaslt", "dec.wgrad": "hipblaslt", "enc.ffn": "hipblaslt+act"}),
     (("bart-large b256", 256 * 1024, 256 * 128, 1024, 4096, "gelu", 50265),
-     {"enc.proj_dgrad": "hipblaslt", "enc.ffn": "pingpong-gelu", "dec.ffn": "pingpong-gelu"}),
+     {"enc.proj_dgrad": "w4", "dec.proj_dgrad": "hipblaslt", "enc.ffn": "pingpong-gelu", "dec.ffn": "pingpong-gelu"}),
     (("t5-large b32", 32 * 1024, 32 * 128, 1024, 4096, "relu", 32128),
      {"enc.proj_dgrad": "hipblaslt", "enc.ffn": "pingpong-relu+w4-drelu"}),
     (("flan-t5-xl b16", 16 * 1024, 16 * 128, 2048, 5120, "gated-gelu", 32128),
