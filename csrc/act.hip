@@ -35,6 +35,12 @@ DLLM_DEVICE float act_df(float x) {
   return s * (1.f + x * (1.f - s));
 }
 
+// dropout of the activation output: the row-Weyl decisions of (token row, output column) that the fused FFN GEMM
+// epilogues draw (common.h rw_*, csrc/gemm_w4.hip / gemm_fused.hip; ops/rng.py rowwise_keep_mask)
+DLLM_DEVICE void drop4(f32x4& v, uint32_t seed, uint32_t thr, long row, int col, float dscale) {
+  rw_dropout4(v, mix32(seed, (uint32_t)row), rw_t2(thr), (uint32_t)col, dscale);
+}
+
 // one thread = 4 consecutive output elements of one row; F % 4 == 0
 template <typename T, int ACT, bool GATED>
 __global__ __launch_bounds__(256) void act_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, long total4, int F,
@@ -57,7 +63,7 @@ __global__ __launch_bounds__(256) void act_fwd_kernel(const T* __restrict__ x, T
 #pragma unroll
       for (int k = 0; k < 4; ++k) r[k] = act_f<ACT>(a[k]);
     }
-    if (p > 0.f) dropout4(r, seed, thr, (uint32_t)oidx, dscale);
+    if (p > 0.f) drop4(r, seed, thr, row, col, dscale);
     Elem<T>::store4(y + oidx, r);
   }
 }
@@ -74,7 +80,7 @@ __global__ __launch_bounds__(256) void act_bwd_kernel(const T* __restrict__ dy, 
     const int col = (int)(i - row * F4) * 4;
     const long oidx = row * F + col;
     f32x4 g = Elem<T>::load4(dy + oidx);
-    if (p > 0.f) dropout4(g, seed, thr, (uint32_t)oidx, dscale);
+    if (p > 0.f) drop4(g, seed, thr, row, col, dscale);
     if (GATED) {
       f32x4 a = Elem<T>::load4(x + row * 2 * F + col);
       f32x4 b = Elem<T>::load4(x + row * 2 * F + F + col);

@@ -53,30 +53,19 @@ DLLM_SEED_STEP_TU(attn)
 
 namespace {
 
-// attention dropout (ops/rng.py attention_keep_mask): per query row rh = mix32(seed, row); per key pair kp = key >> 1:
-// g = (rh & 0xFFFFFF) * C24 + kp * HG (mod 2^32: a Weyl sequence along the row, so a kernel adds one constant per
-// pair to a per-tile base), h = ((g ^ (g >> 15)) & 0xFFFFFF) * C24B (full-rate v_mul_u32_u24), y = h ^ (h >> 16);
-// the even key keeps iff ((y & 0xFFFF) ^ 0x8000) >= thr16, the odd key iff ((y >> 16) ^ 0x8000) >= thr16.  The
-// xorshift + multiply round matters: g alone is linear in kp and leaves lag-2 drops anti-correlated; with it every
-// lag-1/2/3/16 joint drop rate and the row-count variance match independent Bernoulli draws
-// (tests/test_training_cpu.py test_attention_dropout_hash_statistics).  The top-bit flip makes the compare a signed
-// 16-bit one, which the kernels do on both keys of a pair at once (drop_mask2).
-constexpr uint32_t C24 = 0x9E3779u, C24B = 0x85EBCBu;
-DLLM_DEVICE uint32_t pair_y(uint32_t g) {
-  const uint32_t h = __umul24(g ^ (g >> 15), C24B);
-  return h ^ (h >> 16);
-}
+// attention dropout (ops/rng.py attention_keep_mask): the row-Weyl hash of common.h (rw_*) with one row per (b, h,
+// query): per query row rh = mix32(seed, row); per key pair kp = key >> 1, g = (rh & 0xFFFFFF) * C24 + kp * HG, the
+// xorshift + 24-bit multiply round (pair_y), and the two-key signed compare (drop_mask2).  The xorshift + multiply
+// round matters: g alone is linear in kp and leaves lag-2 drops anti-correlated; with it every lag-1/2/3/16 joint drop
+// rate and the row-count variance match independent Bernoulli draws (tests/test_training_cpu.py
+// test_attention_dropout_hash_statistics).
+static_assert(HG == RW_G, "attention Weyl step = the row-Weyl hash's");
+DLLM_DEVICE uint32_t pair_y(uint32_t g) { return rw_pair_y(g); }
 // per-lane, per-tile start of the Weyl sequence: g of pair kp0 + j is gbase + j * HG
-DLLM_DEVICE uint32_t pair_gbase(uint32_t rh, uint32_t kp0) { return __umul24(rh, C24) + kp0 * HG; }
+DLLM_DEVICE uint32_t pair_gbase(uint32_t rh, uint32_t kp0) { return rw_gbase(rh, kp0); }
 // t2 = (thr16 - 0x8000) in both 16-bit halves.  Returns the pair's DROP mask: 0xFFFF in the half of each dropped key
-// (low half = even key, high half = odd key): saturating signed difference, then its sign spread over the half.
-DLLM_DEVICE uint32_t drop_mask2(uint32_t y, uint32_t t2) {
-  uint32_t d, m;
-  asm("v_pk_sub_i16 %0, %1, %2 clamp" : "=v"(d) : "v"(y), "s"(t2));
-  asm("v_pk_ashrrev_i16 %0, %1, %2" : "=v"(m) : "s"(0x000F000Fu), "v"(d));  // shift count per half (an inline 15
-                                                                            // would shift the high half by 0)
-  return m;
-}
+// (low half = even key, high half = odd key).
+DLLM_DEVICE uint32_t drop_mask2(uint32_t y, uint32_t t2) { return rw_drop2(y, t2); }
 
 // Keep-word layout of one (row, 64-key tile, lane half) — shared by the forward and both backward kernels: the lane's
 // 16 key pairs are slots p = 0..15, pair slot p of accumulator register i of s0 (t = 0) or s1 (t = 1) being

@@ -99,6 +99,46 @@ DLLM_DEVICE void dropout4(f32x4& v, uint32_t seed, uint32_t thr16, uint32_t e4, 
   v.w = k3 ? v.w * scale : 0.f;
 }
 
+// ---- row-Weyl dropout hash (attention probabilities and the FFN activations; ops/rng.py rowwise_keep_mask) ---------
+// For tensors whose kernels walk rows: rh = mix32(seed, row) once per row; per column pair kp = col >> 1,
+// g = (rh & 0xFFFFFF) * C24 + kp * G (mod 2^32: a Weyl sequence along the row, one add per pair), h = ((g ^ (g >> 15)) &
+// 0xFFFFFF) * C24B (full-rate v_mul_u32_u24), y = h ^ (h >> 16); the even column keeps iff ((y & 0xFFFF) ^ 0x8000) >=
+// thr16, the odd one iff ((y >> 16) ^ 0x8000) >= thr16.  ~7 VALU per pair, against mix32's three quarter-rate
+// v_mul_lo_u32 per pair; statistics: tests/test_training_cpu.py test_attention_dropout_hash_statistics.
+constexpr uint32_t RW_C24 = 0x9E3779u, RW_C24B = 0x85EBCBu, RW_G = 0x9E3779B1u;
+DLLM_DEVICE uint32_t rw_pair_y(uint32_t g) {
+  const uint32_t h = __umul24(g ^ (g >> 15), RW_C24B);
+  return h ^ (h >> 16);
+}
+// g of column pair kp0 of the row with hash rh (pair kp0 + j: + j * RW_G)
+DLLM_DEVICE uint32_t rw_gbase(uint32_t rh, uint32_t kp0) { return __umul24(rh, RW_C24) + kp0 * RW_G; }
+// (thr16 - 0x8000) in both 16-bit halves: the threshold operand of rw_drop2
+DLLM_HOST_DEVICE uint32_t rw_t2(uint32_t thr16) { return ((thr16 - 0x8000u) & 0xFFFFu) * 0x10001u; }
+// DROP mask of a pair: 0xFFFF in the half of each dropped column (low half = even column): saturating signed difference,
+// then its sign spread over the half
+DLLM_DEVICE uint32_t rw_drop2(uint32_t y, uint32_t t2) {
+  uint32_t d, m;
+  asm("v_pk_sub_i16 %0, %1, %2 clamp" : "=v"(d) : "v"(y), "s"(t2));  // t2: wave-uniform (kernel arguments)
+  asm("v_pk_ashrrev_i16 %0, %1, %2" : "=v"(m) : "s"(0x000F000Fu), "v"(d));  // per-half count (an inline 15 would
+                                                                            // shift the high half by 0)
+  return m;
+}
+// per-element factors (scale if kept, else 0) of the 4 columns of the two pairs starting at Weyl value g
+DLLM_DEVICE f32x4 rw_scale4(uint32_t g, uint32_t t2, float scale) {
+  const uint32_t m0 = rw_drop2(rw_pair_y(g), t2), m1 = rw_drop2(rw_pair_y(g + RW_G), t2);
+  return f32x4{(m0 & 0xFFFFu) ? 0.f : scale, (m0 >> 16) ? 0.f : scale, (m1 & 0xFFFFu) ? 0.f : scale,
+               (m1 >> 16) ? 0.f : scale};
+}
+// fp32 form for 4 consecutive columns col .. col+3 (col even) of the row with hash rh: kept ones scaled, dropped zeroed
+DLLM_DEVICE void rw_dropout4(f32x4& v, uint32_t rh, uint32_t t2, uint32_t col, float scale) {
+  const uint32_t g = rw_gbase(rh, col >> 1);
+  const uint32_t m0 = rw_drop2(rw_pair_y(g), t2), m1 = rw_drop2(rw_pair_y(g + RW_G), t2);
+  v.x = (m0 & 0xFFFFu) ? 0.f : v.x * scale;
+  v.y = (m0 >> 16) ? 0.f : v.y * scale;
+  v.z = (m1 & 0xFFFFu) ? 0.f : v.z * scale;
+  v.w = (m1 >> 16) ? 0.f : v.w * scale;
+}
+
 // ---- graph-replayable dropout seeds ----------------------------------------------------------------------------
 // A captured HIP graph replays its kernel arguments verbatim, so a per-site seed passed by value would draw the SAME
 // mask every replayed step.  Every translation unit with dropout therefore keeps a device pointer to ONE 32-bit step

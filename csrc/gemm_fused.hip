@@ -135,11 +135,11 @@ DLLM_DEVICE f32x4 load4(const uint16_t* p) {
 template <int EPI>
 DLLM_DEVICE f32x4 epilogue4(const GemmFusedParams& P, uint32_t seed, int m, int n, f32x4 v) {
   const bool drop = P.p > 0.f;
-  const uint32_t e = (uint32_t)m * (uint32_t)P.N + (uint32_t)n;  // output element index (< 2^32, host-checked)
   if (EPI == EPI_RELU) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) v[k] = fmaxf(v[k], 0.f);
-    if (drop) dropout4(v, seed, P.thr, e, P.scale);
+    // FFN activation dropout: the row-Weyl hash of (row m, column n) (common.h rw_*; the w4 epilogues' decisions)
+    if (drop) rw_dropout4(v, mix32(seed, (uint32_t)m), rw_t2(P.thr), (uint32_t)n, P.scale);
   } else if (EPI == EPI_GELU || EPI == EPI_GELU_TANH) {
     f32x4 dg;
 #pragma unroll
@@ -150,13 +150,10 @@ DLLM_DEVICE f32x4 epilogue4(const GemmFusedParams& P, uint32_t seed, int m, int 
       v[k] = g;
       dg[k] = d;
     }
-    if (drop) {
-      bool k0, k1, k2, k3;
-      keep_two(seed, P.thr, e, k0, k1);
-      keep_two(seed, P.thr, e + 2u, k2, k3);
-      const float s0 = k0 ? P.scale : 0.f, s1 = k1 ? P.scale : 0.f, s2 = k2 ? P.scale : 0.f, s3 = k3 ? P.scale : 0.f;
-      v = v * f32x4{s0, s1, s2, s3};
-      dg = dg * f32x4{s0, s1, s2, s3};
+    if (drop) {  // row-Weyl decisions of (row m, columns n ..) as the ReLU branch
+      const f32x4 sc = rw_scale4(rw_gbase(mix32(seed, (uint32_t)m), (uint32_t)n >> 1), rw_t2(P.thr), P.scale);
+      v = v * sc;
+      dg = dg * sc;
     }
     store4(P.aux_out + (long)m * P.ldaux + n, dg);
   } else if (EPI == EPI_DRELU) {
@@ -183,11 +180,11 @@ DLLM_DEVICE f32x4 epilogue4(const GemmFusedParams& P, uint32_t seed, int m, int 
 template <int EPI>
 DLLM_DEVICE f32x4 act4(const GemmFusedParams& P, uint32_t seed, int m, int n, f32x4 v, f32x4& dg) {
   const bool drop = P.p > 0.f;
-  const uint32_t e = (uint32_t)m * (uint32_t)P.N + (uint32_t)n;
   if (EPI == EPI_RELU) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) v[k] = fmaxf(v[k], 0.f);
-    if (drop) dropout4(v, seed, P.thr, e, P.scale);
+    // FFN activation dropout: the row-Weyl hash of (row m, column n) (common.h rw_*; the w4 epilogues' decisions)
+    if (drop) rw_dropout4(v, mix32(seed, (uint32_t)m), rw_t2(P.thr), (uint32_t)n, P.scale);
   } else if (EPI == EPI_GELU || EPI == EPI_GELU_TANH) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -197,13 +194,10 @@ DLLM_DEVICE f32x4 act4(const GemmFusedParams& P, uint32_t seed, int m, int n, f3
       v[k] = g;
       dg[k] = d;
     }
-    if (drop) {
-      bool k0, k1, k2, k3;
-      keep_two(seed, P.thr, e, k0, k1);
-      keep_two(seed, P.thr, e + 2u, k2, k3);
-      const float s0 = k0 ? P.scale : 0.f, s1 = k1 ? P.scale : 0.f, s2 = k2 ? P.scale : 0.f, s3 = k3 ? P.scale : 0.f;
-      v = v * f32x4{s0, s1, s2, s3};
-      dg = dg * f32x4{s0, s1, s2, s3};
+    if (drop) {  // row-Weyl decisions of (row m, columns n ..) as the ReLU branch
+      const f32x4 sc = rw_scale4(rw_gbase(mix32(seed, (uint32_t)m), (uint32_t)n >> 1), rw_t2(P.thr), P.scale);
+      v = v * sc;
+      dg = dg * sc;
     }
   }
   return v;
@@ -763,12 +757,8 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(GemmFusedParams P) {
             g1[r] = d * up[r];
             g2[r] = a;
           }
-          if (P.p > 0.f) {  // keep decision on the OUTPUT element m * F + f, as csrc/act.hip's gated path
-            bool k0, k1, k2, k3;
-            const uint32_t e = (uint32_t)m * (uint32_t)F + (uint32_t)f;
-            keep_two(seed, P.thr, e, k0, k1);
-            keep_two(seed, P.thr, e + 2u, k2, k3);
-            const f32x4 s = {k0 ? P.scale : 0.f, k1 ? P.scale : 0.f, k2 ? P.scale : 0.f, k3 ? P.scale : 0.f};
+          if (P.p > 0.f) {  // row-Weyl decision of the OUTPUT element (row m, column f), as csrc/act.hip's gated path
+            const f32x4 s = rw_scale4(rw_gbase(mix32(seed, (uint32_t)m), (uint32_t)f >> 1), rw_t2(P.thr), P.scale);
             h = h * s;
             g1 = g1 * s;
             g2 = g2 * s;

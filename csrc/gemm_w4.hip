@@ -144,6 +144,43 @@ DLLM_DEVICE bf16x8v frag_km16(const unsigned char* smem, uint32_t img, int kk, i
 
 DLLM_DEVICE uint32_t pk2(float a, float b) { return pack_bf16x2(a, b); }
 
+// ReLU of two packed bf16 (a set sign bit -> +0): one v_pk_max_i16
+DLLM_DEVICE uint32_t relu2(uint32_t v) {
+  uint32_t r;
+  asm("v_pk_max_i16 %0, %1, 0" : "=v"(r) : "v"(v));
+  return r;
+}
+// 1 in each nonzero 16-bit half, else 0: one v_pk_min_u16
+DLLM_DEVICE uint32_t nz2(uint32_t v) {
+  uint32_t r;
+  asm("v_pk_min_u16 %0, %1, %2" : "=v"(r) : "v"(v), "s"(0x00010001u));
+  return r;
+}
+// ReLU bit-mask layout (W4_EPI_RELU writes, W4_EPI_DRELU_M reads): in the 32-bit word of one accumulator row, element r
+// of column group j (columns 16 j + 4 qd + r) is pair p = 2 j + (r >> 1) of the row, at bit p (even column) or 16 + p
+// (odd column) — what nz2 of the packed pair shifted by p gives
+DLLM_DEVICE constexpr int mbit(int j, int r) { return 2 * j + (r >> 1) + 16 * (r & 1); }
+// 0xFFFF in the low / high half where bit p / 16 + p of w is set (p < 16): both bits moved to the halves' sign
+// positions, then one v_pk_ashrrev_i16 by 15
+DLLM_DEVICE uint32_t bits2(uint32_t w, int p) {
+  uint32_t r;
+  asm("v_pk_ashrrev_i16 %0, %1, %2" : "=v"(r) : "s"(0x000F000Fu), "v"(w << (15 - p)));
+  return r;
+}
+// even bits of w to the low half (bit 2k -> k), odd bits to the high half (2k+1 -> 16+k) (Hacker's Delight 7-2
+// unshuffle): the ping-pong kernel's 4 j + r bit order -> mbit order
+DLLM_DEVICE uint32_t unshuffle32(uint32_t x) {
+  uint32_t t = (x ^ (x >> 1)) & 0x22222222u;
+  x ^= t ^ (t << 1);
+  t = (x ^ (x >> 2)) & 0x0C0C0C0Cu;
+  x ^= t ^ (t << 2);
+  t = (x ^ (x >> 4)) & 0x00F000F0u;
+  x ^= t ^ (t << 4);
+  t = (x ^ (x >> 8)) & 0x0000FF00u;
+  x ^= t ^ (t << 8);
+  return x;
+}
+
 // c += b . a^T (16x16x32, bf16): inline asm so the accumulator is pinned to AGPRs ("+a") and the fragments to VGPRs.
 // With the builtin, hipcc (ROCm 7.2) spreads the 256 accumulators and 128 fragment registers over both halves of the
 // register file and spills ~200 VGPRs.  The asm is opaque to hipcc's hazard recognizer, so the kernel pads the two
@@ -667,7 +704,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
           for (int i = 0; i < 8; ++i) {
             const uint32_t a = (i >> 1) == 0 ? lo.x : (i >> 1) == 1 ? lo.y : (i >> 1) == 2 ? lo.z : lo.w;
             const uint32_t b = (i >> 1) == 0 ? hi.x : (i >> 1) == 1 ? hi.y : (i >> 1) == 2 ? hi.z : hi.w;
-            mw[i] = (i & 1) ? ((a >> 16) | (b & 0xFFFF0000u)) : ((a & 0xFFFFu) | (b << 16));
+            mw[i] = unshuffle32((i & 1) ? ((a >> 16) | (b & 0xFFFF0000u)) : ((a & 0xFFFFu) | (b << 16)));
           }
         } else {
           mw[0] = lo.x; mw[1] = lo.y; mw[2] = lo.z; mw[3] = lo.w;
@@ -716,8 +753,19 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
           ce_y[q] = (yt >= 0 && yt < 256) ? (int)yt : -1;
         }
       }
+      const uint32_t t2 = rw_t2(P.thr);  // row-Weyl dropout threshold pair (ReLU forward)
 #pragma unroll
       for (int ii = 0; ii < 4; ++ii) {
+        // ReLU / GELU forward dropout: row-Weyl bases of this lane's rows 32 ii + rl (x) and + 16 (y) at column pair kp0
+        uint32_t rwx = 0u, rwy = 0u;
+        if constexpr (EPI == W4_EPI_RELU || EPI == W4_EPI_GELU) {
+          if (P.p > 0.f) {
+            const uint32_t rx = (uint32_t)(m0 + wm * 128 + 32 * ii + rl);
+            const uint32_t kp0 = (uint32_t)(n0 + wn * 128 + 4 * qd) >> 1;
+            rwx = rw_gbase(mix32(seed, rx), kp0);
+            rwy = rw_gbase(mix32(seed, rx + 16u), kp0);
+          }
+        }
         u32x2 ga[8][2];  // GELU backward: the saved derivative at this lane's accumulator positions (rows ii, ii + 16)
         if constexpr (EPI == W4_EPI_DGELU) {
 #pragma unroll
@@ -742,27 +790,16 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
             yv += b4;
           }
           if constexpr (EPI == W4_EPI_RELU) {
-            const uint32_t n4 = (uint32_t)(n0 + wn * 128 + 16 * j + 4 * qd);
-            const uint32_t ex = (uint32_t)(m0 + wm * 128 + 32 * ii + rl) * (uint32_t)P.N + n4;  // element of xv[0]
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              xv[r] = fmaxf(xv[r], 0.f);
-              yv[r] = fmaxf(yv[r], 0.f);
-            }
+            // scaled in fp32 (rounded once, as before); ReLU, dropout and the mask bits follow on the packed pairs
             if (P.p > 0.f) {
-              dropout4(xv, seed, P.thr, ex, P.scale);
-              dropout4(yv, seed, P.thr, ex + 16u * (uint32_t)P.N, P.scale);
-            }
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              mw[2 * ii] |= (xv[r] > 0.f ? 1u : 0u) << (4 * j + r);
-              mw[2 * ii + 1] |= (yv[r] > 0.f ? 1u : 0u) << (4 * j + r);
+              xv *= P.scale;
+              yv *= P.scale;
             }
           } else if constexpr (EPI == W4_EPI_DRELU_M) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              xv[r] = (mw[2 * ii] >> (4 * j + r)) & 1u ? xv[r] * P.scale : 0.f;
-              yv[r] = (mw[2 * ii + 1] >> (4 * j + r)) & 1u ? yv[r] * P.scale : 0.f;
+            // scaled in fp32 (rounded once); the mask zeroes the packed pairs below
+            if (P.p > 0.f) {
+              xv *= P.scale;
+              yv *= P.scale;
             }
           } else if constexpr (EPI == W4_EPI_GELU) {
             // h = s gelu(u), G = s gelu'(u), s = keep / (1 - p) with the keep bits of the [M][N] element index
@@ -777,17 +814,9 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
               yv[r] = g;
               gy[r] = d;
             }
-            if (P.p > 0.f) {
-              const uint32_t n4 = (uint32_t)(n0 + wn * 128 + 16 * j + 4 * qd);
-              const uint32_t ex = (uint32_t)(m0 + wm * 128 + 32 * ii + rl) * (uint32_t)P.N + n4;
-              const uint32_t ey = ex + 16u * (uint32_t)P.N;
-              bool k0, k1, k2, k3;
-              keep_two(seed, P.thr, ex, k0, k1);
-              keep_two(seed, P.thr, ex + 2u, k2, k3);
-              const f32x4 sx = {k0 ? P.scale : 0.f, k1 ? P.scale : 0.f, k2 ? P.scale : 0.f, k3 ? P.scale : 0.f};
-              keep_two(seed, P.thr, ey, k0, k1);
-              keep_two(seed, P.thr, ey + 2u, k2, k3);
-              const f32x4 sy = {k0 ? P.scale : 0.f, k1 ? P.scale : 0.f, k2 ? P.scale : 0.f, k3 ? P.scale : 0.f};
+            if (P.p > 0.f) {  // row-Weyl decisions of column pairs kp0 + 8 j, + 1 (as the ReLU forward)
+              const f32x4 sx = rw_scale4(rwx + (uint32_t)(8 * j) * RW_G, t2, P.scale);
+              const f32x4 sy = rw_scale4(rwy + (uint32_t)(8 * j) * RW_G, t2, P.scale);
               xv *= sx;
               gx *= sx;
               yv *= sy;
@@ -828,6 +857,29 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(GemmW4Params P) {
             }
           }
           uint32_t x0 = pk2(xv.x, xv.y), x1 = pk2(xv.z, xv.w), y0 = pk2(yv.x, yv.y), y1 = pk2(yv.z, yv.w);
+          if constexpr (EPI == W4_EPI_RELU) {
+            // ReLU on the bf16 pairs (sign bit set -> 0), then the row-Weyl dropout of column pairs kp0 + 8 j (x0 / y0)
+            // and kp0 + 8 j + 1 (x1 / y1), then the kept-and-positive bits: 9 VALU per pair in all (was ~13 per element
+            // with fp32 ReLU, a mix32 per pair and per-element bit inserts)
+            x0 = relu2(x0);
+            x1 = relu2(x1);
+            y0 = relu2(y0);
+            y1 = relu2(y1);
+            if (P.p > 0.f) {
+              x0 &= ~rw_drop2(rw_pair_y(rwx + (uint32_t)(8 * j) * RW_G), t2);
+              x1 &= ~rw_drop2(rw_pair_y(rwx + (uint32_t)(8 * j + 1) * RW_G), t2);
+              y0 &= ~rw_drop2(rw_pair_y(rwy + (uint32_t)(8 * j) * RW_G), t2);
+              y1 &= ~rw_drop2(rw_pair_y(rwy + (uint32_t)(8 * j + 1) * RW_G), t2);
+            }
+            mw[2 * ii] |= (nz2(x0) << (2 * j)) | (nz2(x1) << (2 * j + 1));
+            mw[2 * ii + 1] |= (nz2(y0) << (2 * j)) | (nz2(y1) << (2 * j + 1));
+          } else if constexpr (EPI == W4_EPI_DRELU_M) {
+            // the pair's two mask bits widened to 16-bit halves (3 VALU per pair, was 4 per element)
+            x0 &= bits2(mw[2 * ii], 2 * j);
+            x1 &= bits2(mw[2 * ii], 2 * j + 1);
+            y0 &= bits2(mw[2 * ii + 1], 2 * j);
+            y1 &= bits2(mw[2 * ii + 1], 2 * j + 1);
+          }
           {
             const auto r0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
             const auto r1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);

@@ -14,7 +14,7 @@ import math
 import torch
 
 from .. import _ext
-from .rng import keep_mask
+from .rng import keep_mask, rowwise_keep_mask
 
 ACTS = {"relu": 0, "gelu": 1, "gelu_new": 2, "gelu_fast": 2, "silu": 3}
 
@@ -39,8 +39,19 @@ def _reference(x, act, gated, p, seed):
     else:
         y = _act_ref(xf, act)
     if p > 0.0:
-        y = y * keep_mask(seed, p, y.shape, y.device).to(y.dtype) * (1.0 / (1.0 - p))
+        y = y * ffn_keep_mask(act, gated, seed, p, y.shape, y.device).to(y.dtype) * (1.0 / (1.0 - p))
     return y.to(x.dtype)
+
+
+def ffn_keep_mask(act: str, gated: bool, seed: int, p: float, shape, device) -> torch.Tensor:
+    """The FFN activation's dropout decisions, as the kernels draw them: the row-Weyl hash of (token row, output column)
+    (ops/rng.py rowwise_keep_mask; csrc/common.h rw_* in csrc/gemm_w4.hip, csrc/gemm_fused.hip, csrc/act.hip) for
+    every activation, gated or not (``act`` / ``gated`` kept for call sites that name the FFN)."""
+    cols = shape[-1]
+    rows = 1
+    for s in shape[:-1]:
+        rows *= s
+    return rowwise_keep_mask(seed, p, rows, cols, device).view(shape)
 
 
 class _ActFn(torch.autograd.Function):

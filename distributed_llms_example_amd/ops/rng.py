@@ -7,6 +7,12 @@ to 1/65536).  Because the decision is a pure function of
 (seed, index), backward kernels regenerate the mask instead of storing it (no mask tensors in HBM),
 and the reference implementation below reproduces the kernels' masks bit-for-bit so numerics tests
 can run with p > 0.  Mirrors csrc/common.h ``dllm_mix32``.
+
+Kernels that walk rows — attention probabilities and the FFN activations — draw their decisions from the row-Weyl
+hash instead (:func:`rowwise_keep_mask`, csrc/common.h ``rw_*``): one ``mix32`` per row, then ~7 full-rate VALU per
+column pair, where ``mix32`` per pair costs three quarter-rate 32-bit multiplies (the T5 ReLU FFN forward epilogue:
+dropout 290 -> 160 us at the t5-base b=512 shape, profiles/r6_ffn_rowweyl_dropout_ab.txt).  The flat-index hash
+stays for the residual dropout of the norm kernels and the standalone dropout kernel (memory-bound).
 """
 from __future__ import annotations
 
@@ -54,23 +60,31 @@ _C24 = 0x9E3779
 _C24B = 0x85EBCB
 
 
-def attention_keep_mask(seed: int, p: float, B: int, H: int, Sq: int, Sk: int, device) -> torch.Tensor:
-    """Attention-probability mask [B, H, Sq, Sk] (mirrors csrc/attn.hip ``pair_gbase`` / ``pair_y`` / ``drop_mask2``).
+def rowwise_keep_mask(seed: int, p: float, rows: int, cols: int, device, row0: int = 0) -> torch.Tensor:
+    """Keep mask [rows, cols] of the row-Weyl hash (mirrors csrc/common.h ``rw_gbase`` / ``rw_pair_y`` / ``rw_drop2``),
+    the decisions of the kernels that walk rows: attention probabilities (one row per (b, h, query)) and the T5 ReLU FFN
+    activation (one row per token).
 
-    Per query row ``r = (b*H + h)*Sq + i``: ``rh = mix32(seed, r)`` (computed once per row in the kernels); per key
+    Per row ``r`` (``row0`` + 0 .. rows-1): ``rh = mix32(seed, r)`` (computed once per row in the kernels); per column
     pair ``kp = j >> 1``: ``g = (rh & 0xFFFFFF) * C24 + kp * G`` (mod 2^32: a Weyl sequence along the row, one add per
     pair in the kernels), ``h = ((g ^ (g >> 15)) & 0xFFFFFF) * C24B`` (the xorshift + multiply round: ``g`` alone is
-    linear in ``kp`` and leaves lag-2 drops anti-correlated), ``y = h ^ (h >> 16)``; the even key keeps iff
-    ``(y & 0xFFFF) ^ 0x8000 >= threshold16(p)``, the odd key iff ``(y >> 16) ^ 0x8000 >= threshold16(p)`` (the
+    linear in ``kp`` and leaves lag-2 drops anti-correlated), ``y = h ^ (h >> 16)``; the even column keeps iff
+    ``(y & 0xFFFF) ^ 0x8000 >= threshold16(p)``, the odd column iff ``(y >> 16) ^ 0x8000 >= threshold16(p)`` (the
     kernels compare both halves at once as signed 16-bit values)."""
-    rows = torch.arange(B * H * Sq, device=device, dtype=torch.int64)
-    rh = mix32(effective_seed(seed), rows).view(B, H, Sq, 1)
-    j = torch.arange(Sk, device=device, dtype=torch.int64).view(1, 1, 1, Sk)
+    r = torch.arange(row0, row0 + rows, device=device, dtype=torch.int64)
+    rh = mix32(effective_seed(seed), r).view(rows, 1)
+    j = torch.arange(cols, device=device, dtype=torch.int64).view(1, cols)
     g = ((rh & 0xFFFFFF) * _C24 + (j >> 1) * _G) & _MASK
     h = (((g ^ (g >> 15)) & 0xFFFFFF) * _C24B) & _MASK
     y = h ^ (h >> 16)
     half = torch.where((j & 1) == 1, y >> 16, y & 0xFFFF)
     return (half ^ 0x8000) >= threshold16(p)
+
+
+def attention_keep_mask(seed: int, p: float, B: int, H: int, Sq: int, Sk: int, device) -> torch.Tensor:
+    """Attention-probability mask [B, H, Sq, Sk] (csrc/attn.hip): :func:`rowwise_keep_mask` with one row per
+    query of each (batch, head), ``r = (b*H + h)*Sq + i``."""
+    return rowwise_keep_mask(seed, p, B * H * Sq, Sk, device).view(B, H, Sq, Sk)
 
 
 def mix_host(seed: int, idx: int) -> int:

@@ -90,10 +90,10 @@ def test_gemm_w4_rejects_bad_shapes():
 @pytest.mark.parametrize("p", [0.0, 0.1])
 @pytest.mark.parametrize("bias", [False, True])
 def test_gemm_w4_relu_dropout_mask_roundtrip(M, K, N, p, bias):
-    """T5 FFN on w4 (ops/ffn.py): forward H = dropout(relu(X Wiᵀ + b)) with the counter-hash keep decision of element
-    m * N + n (ops/rng.py keep_from_index), writing the keep-and-positive bit mask; backward dU = (dY Wo) * mask / (1-p)
-    read from that mask.  Both vs fp32 torch."""
-    from distributed_llms_example_amd.ops.rng import keep_from_index
+    """T5 FFN on w4 (ops/ffn.py): forward H = dropout(relu(X Wiᵀ + b)) with the row-Weyl keep decision of (row m,
+    column n) (ops/rng.py rowwise_keep_mask), writing the keep-and-positive bit mask; backward dU = (dY Wo) * mask /
+    (1-p) read from that mask.  Both vs fp32 torch."""
+    from distributed_llms_example_amd.ops.rng import rowwise_keep_mask
     C = _ext.native()
     torch.manual_seed(M + K + N)
     x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
@@ -103,8 +103,7 @@ def test_gemm_w4_relu_dropout_mask_roundtrip(M, K, N, p, bias):
     mask = torch.zeros(C.gemm_w4_mask_words(M, N), device=DEV, dtype=torch.int32)
     h = C.gemm_w4(x, wi, False, bi, None, False, -1, True, 1, p, seed, mask)
     u = x.float() @ wi.float().t() + (bi.float() if bias else 0.0)
-    keep = keep_from_index(seed, p, torch.arange(M * N, device=DEV, dtype=torch.int64)).view(M, N) if p > 0 else \
-        torch.ones(M, N, dtype=torch.bool, device=DEV)
+    keep = rowwise_keep_mask(seed, p, M, N, DEV) if p > 0 else torch.ones(M, N, dtype=torch.bool, device=DEV)
     ref = torch.relu(u) * keep / (1 - p)
     assert _rel(h, ref) < 8e-3, _rel(h, ref)
     # backward: dU = (dY Wo) through the mask, Wo = [K2, N] k-major operand of the dgrad
@@ -152,9 +151,9 @@ def _gelu_pair_ref(u):
                                           (1000, 256, 520, 0.0, False), (300, 128, 264, 0.1, True)])
 def test_gemm_w4_gelu_forward(M, K, N, p, bias):
     """W4_EPI_GELU: h = s gelu(x wᵀ + b) and aux = s gelu'(.) (s = dropout keep / (1 - p)) vs the fp32 composite with
-    the same keep bits; persistent (528 tiles) and ragged shapes; equal to the ping-pong kernel's epilogue 2 where
-    that kernel runs (M % 256 == 0, N % 256 == 0)."""
-    from distributed_llms_example_amd.ops.rng import keep_mask
+    the same keep bits (the row-Weyl decisions, ops/rng.py rowwise_keep_mask); persistent (528 tiles) and ragged shapes;
+    equal to the ping-pong kernel's epilogue 2 where that kernel runs (M % 256 == 0, N % 256 == 0)."""
+    from distributed_llms_example_amd.ops.rng import rowwise_keep_mask
     C = _ext.native()
     torch.manual_seed(M + N)
     x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
@@ -165,7 +164,7 @@ def test_gemm_w4_gelu_forward(M, K, N, p, bias):
     u = x.float() @ w.float().t() + (b.float() if bias else 0.0)
     g, dg = _gelu_pair_ref(u)
     if p > 0:
-        keep = keep_mask(31, p, (M, N), x.device).float() / (1.0 - p)
+        keep = rowwise_keep_mask(31, p, M, N, x.device).float() / (1.0 - p)
         g, dg = g * keep, dg * keep
     assert _rel(h, g) < 1e-2, _rel(h, g)
     assert _rel(aux, dg) < 1e-2, _rel(aux, dg)

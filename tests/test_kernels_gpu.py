@@ -368,7 +368,6 @@ _EPI_BWD = {"relu": 3, "gelu": 4, "gelu_new": 6}
                                         ("gelu_new", 0.1, True)])
 def test_gemm_fused_forward(variant, act, p, bias):
     """H = dropout(act(X Wᵀ + b)) with the epilogue in the GEMM (nn.Linear weight layout) vs fp32 torch."""
-    from distributed_llms_example_amd.ops.rng import keep_mask
     torch.manual_seed(0)
     M, K, N = 512, 768, 1280
     C = _ext.native()
@@ -382,7 +381,7 @@ def test_gemm_fused_forward(variant, act, p, bias):
     u = x.float() @ w.float().t() + (b.float() if bias else 0.0)
     ref = u if act is None else activations._act_ref(u, act)
     if p > 0:
-        ref = ref * keep_mask(77, p, ref.shape, ref.device).float() / (1.0 - p)
+        ref = ref * activations.ffn_keep_mask(act, False, 77, p, ref.shape, ref.device).float() / (1.0 - p)
     assert _rel(h, ref) < 1e-2, _rel(h, ref)
     _close(h, ref, 2e-2, 2e-2, "fused fwd")
     if aux is not None:  # GELU: the derivative with the dropout mask and scale applied (the backward's multiplier)
@@ -391,12 +390,11 @@ def test_gemm_fused_forward(variant, act, p, bias):
 
 def _act_grad(u, act, seed, p):
     """act'(u) * dropout'(.) in fp32 (what the GELU forward epilogues write as their second output)."""
-    from distributed_llms_example_amd.ops.rng import keep_mask
     uf = u.float().requires_grad_(True)
     activations._act_ref(uf, act).sum().backward()
     g = uf.grad
     if p > 0:
-        g = g * keep_mask(seed, p, g.shape, g.device).float() / (1.0 - p)
+        g = g * activations.ffn_keep_mask(act, False, seed, p, g.shape, g.device).float() / (1.0 - p)
     return g
 
 
@@ -404,14 +402,14 @@ def _act_grad(u, act, seed, p):
 @pytest.mark.parametrize("act,p", [("relu", 0.1), ("relu", 0.0), ("gelu", 0.1), ("gelu_new", 0.0)])
 def test_gemm_fused_backward(variant, act, p):
     """dU = act'(U) * dropout'(dY Wo) with Wo k-major ([d, F]) vs fp32 autograd of the same composite."""
-    from distributed_llms_example_amd.ops.rng import keep_mask
     torch.manual_seed(1)
     M, d, F_ = 768, 512, 1024
     C = _ext.native()
     dy = torch.randn(M, d, device=DEV).to(torch.bfloat16)
     wo = (torch.randn(d, F_, device=DEV) * d ** -0.5).to(torch.bfloat16)
     u = torch.randn(M, F_, device=DEV).to(torch.bfloat16)
-    keep = (keep_mask(9, p, (M, F_), u.device).float() / (1.0 - p)) if p > 0 else torch.ones(M, F_, device=DEV)
+    keep = (activations.ffn_keep_mask(act, False, 9, p, (M, F_), u.device).float() / (1.0 - p)) if p > 0 else \
+        torch.ones(M, F_, device=DEV)
     h = (activations._act_ref(u.float(), act) * keep).to(torch.bfloat16)
     # ReLU derives its mask from the saved activation itself; GELU multiplies by the derivative its forward stored
     aux = h if act == "relu" else _act_grad(u, act, 9, p).to(torch.bfloat16)
@@ -463,7 +461,8 @@ def test_gemm_pp_persistent(K, kmajor):
     if not kmajor:
         w = (torch.randn(N, K, device=DEV) * K ** -0.5).to(torch.bfloat16)
         h = C.gemm_fused(x, w, False, 1, None, None, None, p, 5, 9)
-        ref = torch.relu(x.float() @ w.float().t()) * keep_mask(5, p, (M, N), x.device).float() / (1.0 - p)
+        ref = torch.relu(x.float() @ w.float().t()) * activations.ffn_keep_mask("relu", False, 5, p, (M, N),
+                                                                                x.device).float() / (1.0 - p)
         _close(h, ref, 2e-2, 2e-2, "pp persistent fwd")
     else:
         w = (torch.randn(K, N, device=DEV) * K ** -0.5).to(torch.bfloat16)
@@ -477,7 +476,6 @@ def test_gemm_pp_persistent(K, kmajor):
 def test_gemm_pp_persistent_gelu(act, p):
     """GELU forward (bias + dropout, two stores: H and the scaled derivative) on the persistent ping-pong kernel: 528
     tiles over the CUs, so every workgroup runs an epilogue inside the DMA stream of its next tile."""
-    from distributed_llms_example_amd.ops.rng import keep_mask
     torch.manual_seed(6)
     M, K, N = 8448, 1024, 4096
     C = _ext.native()
@@ -489,7 +487,7 @@ def test_gemm_pp_persistent_gelu(act, p):
     u = x.float() @ w.float().t() + b.float()
     ref = activations._act_ref(u, act)
     if p > 0:
-        ref = ref * keep_mask(31, p, ref.shape, ref.device).float() / (1.0 - p)
+        ref = ref * activations.ffn_keep_mask(act, False, 31, p, ref.shape, ref.device).float() / (1.0 - p)
     _close(h, ref, 2e-2, 2e-2, "pp persistent gelu fwd")
     assert _rel(aux, _act_grad(u, act, 31, p)) < 1e-2, _rel(aux, _act_grad(u, act, 31, p))
 
@@ -521,8 +519,8 @@ def test_gemm_relu_bit_mask(variant, M, d, F_):
 
 def _geglu_ref(gate, up, seed, p):
     """fp32 h = dropout(gelu_tanh(gate) * up) and the two factors the gated forward epilogue stores."""
-    from distributed_llms_example_amd.ops.rng import keep_mask
-    s = (keep_mask(seed, p, gate.shape, gate.device).float() / (1.0 - p)) if p > 0 else torch.ones_like(gate)
+    s = (activations.ffn_keep_mask("gelu_new", True, seed, p, gate.shape, gate.device).float() / (1.0 - p)) if p > 0 \
+        else torch.ones_like(gate)
     g = gate.detach().float().clone().requires_grad_(True)
     a = activations._act_ref(g, "gelu_new")
     (da,) = torch.autograd.grad(a.sum(), g)
@@ -547,8 +545,7 @@ def test_gemm_geglu_forward(M, d, F_, p):
         assert _rel(got, ref) < 1e-2, (name, _rel(got, ref))
         _close(got, ref, 2e-2, 2e-2, f"geglu {name}")
     if p > 0:  # the unfused path (hipBLASLt + csrc/act.hip gated kernel) drops exactly the same elements
-        from distributed_llms_example_amd.ops.rng import keep_mask
-        dropped = ~keep_mask(21, p, (M, F_), x.device)
+        dropped = ~activations.ffn_keep_mask("gelu_new", True, 21, p, (M, F_), x.device)
         h_unf = activations.act_dropout(x @ wi.t(), "gelu_new", p, 21, gated=True)
         assert bool((h[dropped] == 0).all()) and bool((h_unf[dropped] == 0).all())
         assert _rel(h_unf, h) < 1e-2
@@ -575,8 +572,7 @@ def test_gemm_geglu_backward(M, d, F_):
     _close(du, ref, 2e-2, 2e-2, "dgeglu")
     # end to end against autograd of dropout(gelu(gate) * up)
     gf, uf = gate.detach().clone().requires_grad_(True), up.detach().clone().requires_grad_(True)
-    from distributed_llms_example_amd.ops.rng import keep_mask
-    keep = keep_mask(33, p, (M, F_), gate.device).float() / (1.0 - p)
+    keep = activations.ffn_keep_mask("gelu_new", True, 33, p, (M, F_), gate.device).float() / (1.0 - p)
     (activations._act_ref(gf, "gelu_new") * uf * keep).backward(dh)
     assert _rel(du, torch.cat([gf.grad, uf.grad], dim=1)) < 2e-2
 
