@@ -44,8 +44,8 @@ from .linear import _fire, _fusable, _gbuf, _use
 # activation -> (forward epilogue, backward epilogue) of csrc/gemm_fused.hip
 EPILOGUES = {"relu": (1, 3), "gelu": (2, 4), "gelu_new": (5, 6), "gelu_fast": (5, 6)}
 # kernel choices, with their evidence: ops/routing.py.  The ReLU FFN runs on csrc/gemm_w4.hip (ReLU + dropout + bit-mask
-# epilogue forward, input gradient through that mask) from ``ffn_w4_min_rows`` token rows and on the ping-pong kernel
-# below (its bit mask feeds the same w4 backward); the GELU FFN on the ping-pong kernel (``ffn_gelu`` = pp) or the w4
+# epilogue forward, input gradient through that mask) from ``ffn_w4_min_rows`` token rows (default 0: every fused size)
+# and on the ping-pong kernel below (its bit mask feeds the same w4 backward); the GELU FFN on the ping-pong kernel (``ffn_gelu`` = pp) or the w4
 # GELU epilogues (= w4); FFNs under ``ffn_min_rows`` rows run unfused (hipBLASLt + the activation kernel)
 w4_ffn_calls = 0
 w4_gelu_calls = 0

@@ -19,10 +19,11 @@ projection input gradient      w4 from ``proj_dgrad_min_rows`` (64K) token rows 
 dX (+)= dY W                   width / depth (early-release schedule: faster than the         r6_dgrad_rows_ab.txt
                                library on every such shape); hipBLASLt below (``proj_dgrad``
                                = rows)
-FFN, ReLU (T5)                 forward: w4 ReLU + dropout + bit-mask epilogue from            r5_w4_relu_ffn_ab.txt,
-                               ``ffn_w4_min_rows`` (64K) rows, ping-pong (csrc/gemm_fused)   r5_ffn_small_rows_ab.txt
-                               below; backward: w4 through the bit mask; < ``ffn_min_rows``
-                               (1025) rows: hipBLASLt + csrc/act.hip (unfused)
+FFN, ReLU (T5)                 forward: w4 ReLU + row-Weyl dropout + bit-mask epilogue at     r6_ffn_rowweyl_dropout_ab.txt,
+                               every fused size (``ffn_w4_min_rows`` = 0; the ping-pong       r6_ffn_w4_rows_ab.txt
+                               forward below it is the A/B arm); backward: w4 through the
+                               bit mask; < ``ffn_min_rows`` (1025) rows: hipBLASLt +
+                               csrc/act.hip (unfused)                                        r5_ffn_small_rows_ab.txt
 FFN, GELU (BART)               ping-pong GEMM with GELU epilogues (``ffn_gelu`` = pp; w4      r5_w4_gelu_ab.txt
                                GELU epilogues measured 0.25-0.43 % slower)
 FFN, gated GELU (FLAN-T5)      one GEMM pairing gate / up columns when tokens x d_ff >=       r4_gemm_pp_stage_ab.txt
@@ -66,7 +67,7 @@ DEFAULTS: dict = {
     # feed-forward blocks (ops/ffn.py)
     "ffn": "fused",               # fused | unfused
     "ffn_min_rows": 1025,
-    "ffn_w4_min_rows": 65536,
+    "ffn_w4_min_rows": 0,
     "ffn_gelu": "pp",             # pp | w4
     "gated_min_mf": 2 * 256 * 256 * 256,
     "gated_max_d": 1024,
