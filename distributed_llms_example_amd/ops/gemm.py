@@ -49,8 +49,13 @@ def _w4_ok(a: torch.Tensor, b: torch.Tensor, kmajor: bool) -> bool:
             return False
         if mode == "rows" and a.shape[0] < routing.get("proj_dgrad_min_rows"):
             return False
-    elif routing.get("proj_fwd") != "w4":  # forwards
-        return False
+    else:  # forwards: all on w4, none, or (narrow) the K <= 1024, N <= 4096 projections of >= proj_fwd_min_rows tokens
+        mode = routing.get("proj_fwd")
+        if mode == "lib":
+            return False
+        if mode == "narrow" and (a.shape[0] < routing.get("proj_fwd_min_rows") or a.shape[1] > 1024
+                                 or b.shape[0] > 4096):
+            return False
     return bool(_ext.native().gemm_w4_supported(a, b, kmajor))
 
 

@@ -59,7 +59,8 @@ import os
 
 DEFAULTS: dict = {
     # projection GEMMs (ops/gemm.py)
-    "proj_fwd": "lib",            # lib | w4
+    "proj_fwd": "lib",            # lib | w4 | narrow (w4 for K <= 1024, N <= 4096 at >= proj_fwd_min_rows tokens)
+    "proj_fwd_min_rows": 131072,
     "proj_dgrad": "rows",         # rows | w4 | lib
     "proj_dgrad_min_rows": 65536,
     # weight gradients (ops/gemm.py): w4 weight-gradient mode from this many token rows, hipBLASLt (fp32 addmm) below
@@ -151,7 +152,9 @@ def plan(model: str, tokens_enc: int, tokens_dec: int, d_model: int, d_ff: int, 
     dmode = get("proj_dgrad")
     for side, r in rows.items():
         out[f"{side}.wgrad"] = "w4-wgrad" if r >= get("wgrad_min_rows") else "hipblaslt"
-        out[f"{side}.proj_fwd"] = "w4" if get("proj_fwd") == "w4" else "hipblaslt"
+        fm = get("proj_fwd")
+        out[f"{side}.proj_fwd"] = ("w4" if fm == "w4" else "w4-narrow" if fm == "narrow" and r >= get("proj_fwd_min_rows")
+                                   else "hipblaslt")
         if dmode == "w4":
             dg = "w4"
         elif dmode == "lib":
