@@ -110,6 +110,7 @@ class GraphedStep:
         self.t.fill_(float(opt.step_count))
         self._t_host = opt.step_count
         torch.cuda.empty_cache()  # eager blocks cached by the warmup are not usable by the graph's private pool
+        _retire_collectives(self.red)
         # thread-local capture mode: only the capturing thread is barred from capture-unsafe HIP calls.  With the
         # default ("global") an unrelated thread's call during capture invalidates it — ProcessGroupNCCL's watchdog
         # thread polls the events of the warmup's all-reduces and aborts the process on that error (seen on a 1-rank
@@ -322,6 +323,25 @@ def _ranks_agree(sig, eng) -> bool:
     t = torch.tensor([k, -k], dtype=torch.int64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return int(t[0].item()) == -int(t[1].item())
+
+
+def _retire_collectives(red) -> None:
+    """Before a capture on an RCCL group: let ProcessGroupNCCL's watchdog retire every collective issued so far.  The
+    watchdog thread polls the end events of the works it holds (every ~100 ms) until they complete; a poll landing
+    inside a capture aborted the process once in the round-6 GPU suite (1-rank RCCL group, overlap schedule: the
+    aborting thread had no Python frame, the autograd thread was mid-capture).  The device is synchronised, so the
+    works are complete; two watchdog periods remove them from its list, and nothing is polled while capturing."""
+    if red is None or not getattr(red, "dp", False):
+        return
+    import time
+    import torch.distributed as dist
+    try:
+        backend = dist.get_backend(red.group)
+    except Exception:  # noqa: BLE001 - no default group (single process): nothing to retire
+        return
+    if backend == "nccl":
+        torch.cuda.synchronize()
+        time.sleep(0.25)
 
 
 def _all_ranks(flag: bool, eng) -> bool:
