@@ -12,9 +12,10 @@ weight gradient dW = dYᵀX      csrc/gemm_w4.hip weight-gradient mode (K split 
                                ``wgrad_min_rows`` (4096) token rows; hipBLASLt below (a       r6_wgrad_small_rows.txt
                                256x256-tile kernel has ~23 us of fixed cost); deferred over
                                a GA window (ops/gemm.py WgradDefer)                          r5_defer_wgrad_ab.txt
-projection forward             hipBLASLt + TunableOp table (``proj_fwd`` = lib); w4 is       r6_w4_early_release_ab.txt,
-Y = X Wᵀ (+ b)                 within -1.5..+7 % of it per shape (sum of t5-base forwards:    r5_w4route_colsum_ab.txt
-                               library ahead)
+projection forward             hipBLASLt + TunableOp table (``proj_fwd`` = lib); arms:       r6_proj_fwd_arms_ab.txt,
+Y = X Wᵀ (+ b)                 ``narrow`` (w4 for K <= 1024, N <= 4096 at >=                 r6_w4_vs_lib_nt_pmc.txt
+                               ``proj_fwd_min_rows`` tokens: step-neutral), ``w4`` (every
+                               forward: -0.46 % t5-base, -0.67 % bart-large)
 projection input gradient      w4 from ``proj_dgrad_min_rows`` (64K) token rows at any       r6_w4_early_release_ab.txt,
 dX (+)= dY W                   width / depth (early-release schedule: faster than the         r6_dgrad_rows_ab.txt
                                library on every such shape); hipBLASLt below (``proj_dgrad``
