@@ -313,6 +313,22 @@ def test_attention_dropout_hash_statistics(p):
     assert (col - p).abs().max().item() < 0.06 and (row - p).abs().max().item() < 0.06
 
 
+def test_ffn_dropout_is_the_row_weyl_hash():
+    """The FFN activations draw the row-Weyl decisions (ops/activations.py ffn_keep_mask, csrc/common.h rw_*): one
+    row per token of the flattened [..., d_ff] activation, the same function as the attention mask with B = H = 1;
+    drop rate p and independent adjacent rows / column pairs at the FFN shapes."""
+    from distributed_llms_example_amd.ops import activations
+    for act, gated in (("relu", False), ("gelu", False), ("gelu_new", True)):
+        k = activations.ffn_keep_mask(act, gated, 91, 0.1, (4, 128, 768), "cpu")
+        assert k.shape == (4, 128, 768)
+        assert torch.equal(k.view(512, 768), rng.rowwise_keep_mask(91, 0.1, 512, 768, "cpu"))
+        assert torch.equal(k.view(512, 768), rng.attention_keep_mask(91, 0.1, 1, 1, 512, 768, "cpu")[0, 0])
+    d = 1 - rng.rowwise_keep_mask(5, 0.1, 2048, 3072, "cpu").double()
+    assert abs(d.mean().item() - 0.1) < 0.002
+    for v in ((d[0::2] * d[1::2]).mean().item(), (d[:, 0::2] * d[:, 1::2]).mean().item()):
+        assert abs(v - 0.01) < 0.001, v
+
+
 def test_relayout_keeps_stacked_groups_adjacent():
     """FlatParams.relayout with an order that splits a stacked group (the decoder's cross-attention K/V weights,
     consumed as ONE tensor by ops/linear.py stacked_linear): the group is re-joined at its first member's position,
