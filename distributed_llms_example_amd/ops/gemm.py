@@ -12,7 +12,7 @@ Who runs what (t5-base / bart-large training step, default settings):
 * the PLAIN projections — forward ``Y = X Wᵀ (+ b)`` of the attention q/k/v/o and FFN output layers, and the LM
   head — go to the library (hipBLASLt through torch, with the TunableOp table in configs/tunableop/): csrc/gemm_w4.hip
   ties it on these shapes in isolation and lost 0.8 % of the step in situ (profiles/r3_w4_routing_ab.txt).  Their input
-  gradients ``dX (+)= dY W`` run on csrc/gemm_w4.hip from 64K token rows at any layer width (its early-release schedule
+  gradients ``dX (+)= dY W`` run on csrc/gemm_w4.hip from 16K token rows at any layer width (its early-release schedule
   beats the library on every such shape, profiles/r6_w4_early_release_ab.txt), on hipBLASLt below.  The choice is
   ops/routing.py's table (``proj_fwd`` / ``proj_dgrad``).
 

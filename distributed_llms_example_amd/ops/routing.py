@@ -16,7 +16,7 @@ projection forward             hipBLASLt + TunableOp table (``proj_fwd`` = lib);
 Y = X Wᵀ (+ b)                 ``narrow`` (w4 for K <= 1024, N <= 4096 at >=                 r6_w4_vs_lib_nt_pmc.txt
                                ``proj_fwd_min_rows`` tokens: step-neutral), ``w4`` (every
                                forward: -0.46 % t5-base, -0.67 % bart-large)
-projection input gradient      w4 from ``proj_dgrad_min_rows`` (64K) token rows at any       r6_w4_early_release_ab.txt,
+projection input gradient      w4 from ``proj_dgrad_min_rows`` (16K) token rows at any       r6_dgrad_min_rows_ab.txt,
 dX (+)= dY W                   width / depth (early-release schedule: faster than the         r6_dgrad_rows_ab.txt
                                library on every such shape); hipBLASLt below (``proj_dgrad``
                                = rows)
@@ -63,7 +63,7 @@ DEFAULTS: dict = {
     "proj_fwd": "lib",            # lib | w4 | narrow (w4 for K <= 1024, N <= 4096 at >= proj_fwd_min_rows tokens)
     "proj_fwd_min_rows": 131072,
     "proj_dgrad": "rows",         # rows | w4 | lib
-    "proj_dgrad_min_rows": 65536,
+    "proj_dgrad_min_rows": 16384,
     # weight gradients (ops/gemm.py): w4 weight-gradient mode from this many token rows, hipBLASLt (fp32 addmm) below
     "wgrad_min_rows": 4096,
     # feed-forward blocks (ops/ffn.py)
