@@ -820,3 +820,24 @@ def test_wgrad_small_rows_route(rows, native, monkeypatch):
     assert (len(calls) > 0) == native
     ref = g0.double() + dy.double().t() @ x.double()
     assert _rel(g, ref) < 1e-5, _rel(g, ref)
+
+
+@pytest.mark.parametrize("G,d", [(512, 768), (2048, 1024), (8192, 768), (4100, 520)])
+@pytest.mark.parametrize("out_dtype", [torch.float32, torch.bfloat16])
+def test_colsum_partials_acc(G, d, out_dtype):
+    """out += part.sum(0) over fp32 partial rows (norm-weight / bias gradients; a deferred accumulation window hands
+    thousands of rows), fp32 or bf16 destination, deterministic, vs fp64."""
+    torch.manual_seed(G + d)
+    C = _ext.native()
+    part = torch.randn(G, d, device=DEV)
+    base = torch.randn(d, device=DEV).to(out_dtype)
+    out = base.clone()
+    C.colsum_partials_acc(part, out)
+    ref = base.double() + part.double().sum(0)
+    if out_dtype == torch.float32:  # fp32 summation error, bounded against the column's L1 mass
+        assert ((out.double() - ref).abs() / part.double().abs().sum(0)).max().item() < 2e-6
+    else:  # the bf16 store's rounding
+        assert ((out.double() - ref).abs() / ref.abs().clamp_min(1.0)).max().item() < 1e-2
+    out2 = base.clone()
+    C.colsum_partials_acc(part, out2)
+    assert torch.equal(out, out2)  # run-to-run identical
